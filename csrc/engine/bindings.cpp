@@ -1,0 +1,238 @@
+// pybind11 module `rocalphago_amd._rocgo`: Go engine, feature extraction, LZF codec, search.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <thread>
+
+#include "go_engine.hpp"
+
+namespace py = pybind11;
+using namespace rag;
+
+namespace rag {
+size_t lzf_decompress(const uint8_t* in, size_t n, uint8_t* out, size_t cap);
+size_t lzf_compress(const uint8_t* in, size_t n, uint8_t* out, size_t cap);
+void register_search(py::module_& m);
+void register_rollout(py::module_& m);
+}  // namespace rag
+
+namespace {
+
+std::shared_ptr<const Zobrist> make_zobrist(py::array_t<uint64_t, py::array::c_style> w,
+                                           py::array_t<uint64_t, py::array::c_style> b) {
+  auto z = std::make_shared<Zobrist>();
+  z->white.assign(w.data(), w.data() + w.size());
+  z->black.assign(b.data(), b.data() + b.size());
+  return z;
+}
+
+py::array_t<int8_t> board_array(const Board& b) {
+  const int S = b.size();
+  py::array_t<int8_t> a({S, S});
+  auto r = a.mutable_unchecked<2>();
+  for (int x = 0; x < S; ++x)
+    for (int y = 0; y < S; ++y) r(x, y) = (int8_t)b.color(x * S + y);
+  return a;
+}
+
+std::vector<int> to_fids(const std::vector<int>& f) { return f; }
+
+int total_planes(const std::vector<int>& fids) {
+  int t = 0;
+  for (int f : fids) t += feature_planes(f);
+  return t;
+}
+
+void parallel_for(int n, int nthreads, const std::function<void(int)>& fn) {
+  if (nthreads <= 1 || n <= 1) {
+    for (int i = 0; i < n; ++i) fn(i);
+    return;
+  }
+  nthreads = std::min(nthreads, n);
+  std::atomic<int> next{0};
+  std::vector<std::thread> ts;
+  for (int t = 0; t < nthreads; ++t)
+    ts.emplace_back([&]() {
+      for (int i = next++; i < n; i = next++) fn(i);
+    });
+  for (auto& t : ts) t.join();
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_rocgo, m) {
+  m.doc() = "RocAlphaGo-MI355X native engine (rules, features, LZF, search)";
+  static py::exception<IllegalMoveError> exc(m, "IllegalMove");
+  py::register_exception_translator([](std::exception_ptr p) {
+    try {
+      if (p) std::rethrow_exception(p);
+    } catch (const IllegalMoveError& e) {
+      exc(e.what());
+    }
+  });
+
+  py::class_<Zobrist, std::shared_ptr<Zobrist>>(m, "Zobrist");
+  m.def("make_zobrist", [](py::array_t<uint64_t, py::array::c_style> w,
+                           py::array_t<uint64_t, py::array::c_style> b) {
+    return std::const_pointer_cast<Zobrist>(make_zobrist(w, b));
+  });
+
+  py::class_<Board>(m, "Board")
+      .def(py::init([](int size, double komi, bool superko, std::shared_ptr<Zobrist> z) {
+        return Board(size, komi, superko, z);
+      }))
+      .def("copy", [](const Board& b) { return Board(b); })
+      .def("do_move", &Board::do_move, py::arg("a"), py::arg("color") = 0)
+      .def("play_unchecked", &Board::play_unchecked)
+      .def("is_legal", &Board::is_legal)
+      .def("is_suicide", &Board::is_suicide)
+      .def("is_positional_superko", &Board::is_positional_superko)
+      .def("is_eyeish", &Board::is_eyeish)
+      .def("is_eye",
+           [](const Board& b, int p, int owner, std::vector<int> stack) {
+             return b.is_eye_stack(p, owner, stack);
+           })
+      .def("is_ladder_capture", &Board::is_ladder_capture, py::arg("a"), py::arg("prey") = -1,
+           py::arg("remaining") = 80)
+      .def("is_ladder_escape", &Board::is_ladder_escape, py::arg("a"), py::arg("prey") = -1,
+           py::arg("remaining") = 80)
+      .def("legal_moves",
+           [](const Board& b) {
+             std::vector<int> ne, ey;
+             b.legal_moves(ne, ey);
+             return py::make_tuple(ne, ey);
+           })
+      .def("get_winner", &Board::get_winner)
+      .def("score",
+           [](const Board& b) {
+             double bl, wh;
+             b.score(bl, wh);
+             return py::make_tuple(wh, bl);
+           })
+      .def("place_handicaps", &Board::place_handicaps)
+      .def("board", &board_array)
+      .def("liberty_counts",
+           [](const Board& b) {
+             const int S = b.size();
+             py::array_t<int64_t> a({S, S});
+             auto r = a.mutable_unchecked<2>();
+             for (int x = 0; x < S; ++x)
+               for (int y = 0; y < S; ++y) r(x, y) = b.liberty_count(x * S + y);
+             return a;
+           })
+      .def("stone_ages",
+           [](const Board& b) {
+             const int S = b.size();
+             py::array_t<int64_t> a({S, S});
+             auto r = a.mutable_unchecked<2>();
+             for (int x = 0; x < S; ++x)
+               for (int y = 0; y < S; ++y) r(x, y) = b.stone_age(x * S + y);
+             return a;
+           })
+      .def("group_heads",
+           [](const Board& b) {
+             const int S = b.size();
+             py::array_t<int32_t> a({S * S});
+             auto r = a.mutable_unchecked<1>();
+             for (int p = 0; p < S * S; ++p) r(p) = b.group_head(p);
+             return a;
+           })
+      .def("group",
+           [](const Board& b, int p) {
+             std::vector<int> s;
+             b.group_stones(p, s);
+             return s;
+           })
+      .def("liberty_set",
+           [](const Board& b, int p) {
+             Bitset bs;
+             b.liberty_set(p, bs);
+             std::vector<int> v;
+             bs.for_each(b.geom().W, [&](int i) { v.push_back(i); });
+             return v;
+           })
+      .def("groups_around",
+           [](const Board& b, int p) {
+             int h[4];
+             int n = b.groups_around(p, h);
+             return std::vector<int>(h, h + n);
+           })
+      .def("color_at", &Board::color)
+      .def("liberty_count", &Board::liberty_count)
+      .def("features",
+           [](const Board& b, const std::vector<int>& fids) {
+             const int S = b.size();
+             py::array_t<uint8_t> a({total_planes(fids), S, S});
+             extract_features(b, fids.data(), (int)fids.size(), a.mutable_data());
+             return a;
+           })
+      .def_property_readonly("size", &Board::size)
+      .def_property("current_player", &Board::current_player, &Board::set_current_player)
+      .def_property("ko", &Board::ko, &Board::set_ko)
+      .def_property("komi", &Board::komi, &Board::set_komi)
+      .def_property("enforce_superko", &Board::enforce_superko, &Board::set_enforce_superko)
+      .def_property("end_of_game", &Board::end_of_game, &Board::set_end_of_game)
+      .def_property_readonly("black_prisoners", &Board::black_prisoners)
+      .def_property_readonly("white_prisoners", &Board::white_prisoners)
+      .def("set_prisoners", &Board::set_prisoners)
+      .def_property_readonly("passes_black", &Board::passes_black)
+      .def_property_readonly("passes_white", &Board::passes_white)
+      .def("set_passes", &Board::set_passes)
+      .def_property_readonly("hash", &Board::hash)
+      .def_property_readonly("history",
+                             [](const Board& b) {
+                               const auto& h = b.history();
+                               return std::vector<int>(h.begin(), h.end());
+                             })
+      .def_property_readonly("move_count", &Board::move_count)
+      .def_property_readonly("handicaps",
+                             [](const Board& b) {
+                               const auto& h = b.handicaps();
+                               return std::vector<int>(h.begin(), h.end());
+                             })
+      .def_property_readonly("previous_hashes", [](const Board& b) { return b.previous_hashes(); });
+
+  m.def(
+      "batch_features",
+      [](const std::vector<const Board*>& boards, const std::vector<int>& fids, int nthreads) {
+        if (boards.empty()) throw std::invalid_argument("empty batch");
+        const int S = boards[0]->size();
+        for (auto* b : boards)
+          if (b->size() != S) throw std::invalid_argument("all states must have the same size");
+        const int F = total_planes(fids);
+        const int B = (int)boards.size();
+        py::array_t<uint8_t> a({B, F, S, S});
+        uint8_t* base = a.mutable_data();
+        const size_t stride = (size_t)F * S * S;
+        {
+          py::gil_scoped_release nogil;
+          parallel_for(B, nthreads, [&](int i) {
+            extract_features(*boards[i], fids.data(), (int)fids.size(), base + i * stride);
+          });
+        }
+        return a;
+      },
+      py::arg("boards"), py::arg("fids"), py::arg("nthreads") = 8);
+
+  m.def("feature_planes", &feature_planes);
+
+  m.def("lzf_decompress", [](py::bytes data, size_t out_size) {
+    std::string in = data;
+    std::string out(out_size, '\0');
+    size_t n = lzf_decompress((const uint8_t*)in.data(), in.size(), (uint8_t*)out.data(), out_size);
+    if (n != out_size) throw std::runtime_error("lzf: corrupt stream or size mismatch");
+    return py::bytes(out);
+  });
+  m.def("lzf_compress", [](py::bytes data) -> py::object {
+    std::string in = data;
+    std::string out(in.size() + 64, '\0');
+    size_t n = lzf_compress((const uint8_t*)in.data(), in.size(), (uint8_t*)out.data(), in.size());
+    if (n == 0) return py::none();  // incompressible: caller stores the raw chunk
+    out.resize(n);
+    return py::bytes(out);
+  });
+
+  register_search(m);
+  register_rollout(m);
+}
