@@ -1,0 +1,61 @@
+// Shared definitions for the gfx950 (CDNA4 / MI355X) kernels of RocAlphaGo-MI355X.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define RAG_API extern "C" __attribute__((visibility("default")))
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16;
+
+#define LDS_PTR(T) __attribute__((address_space(3))) T*
+
+namespace rag {
+
+__device__ __forceinline__ float bf2f(bf16 v) { return (float)v; }
+__device__ __forceinline__ bf16 f2bf(float v) { return (bf16)v; }
+
+// 16-byte global -> LDS direct copy (global_load_lds_dwordx4). LDS destination is
+// wave-uniform `lds_base` + lane*16; the global source is per lane.
+__device__ __forceinline__ void glds16(const void* gsrc, void* lds_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
+                                   (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// Row swizzle for [row][32 x bf16] (64-byte) LDS tiles read as 16x16x32 MFMA fragments with
+// ds_read_b128 (lane reads row lane&15, 16-byte chunk lane>>4). Swapping chunk bit 1 on rows
+// with bit 3 set makes all four 16-lane ds_read_b128 groups conflict-free (derivation in
+// docs/KERNELS.md). Involution: applied to the global source on staging and on the read.
+__device__ __forceinline__ int swz64(int row) { return ((row >> 3) & 1) << 1; }
+
+__device__ __forceinline__ int wave_id() {
+  return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+}
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// Bijective XCD-aware remap of a 1-D block index (guide T1): consecutive tiles land on one XCD.
+__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
+  const int q = nblk / 8, r = nblk % 8;
+  const int xcd = bid % 8, idx = bid / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+__device__ __forceinline__ float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float warp_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+}  // namespace rag

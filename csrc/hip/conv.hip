@@ -1,0 +1,574 @@
+// Implicit-GEMM convolutions for 19x19 Go boards on gfx950 (MI355X) — kernels K01/K02/K05/K06/K08.
+//
+// Activation layout ("padded channels-last"): bf16 [B][S+2H][S+2H][C] with an all-zero halo of
+// width H (H=1 for 3x3 and 1x1 layers, H=2 for the 5x5 input layer) and C padded to a multiple
+// of 32. A 'same' convolution then needs no boundary test: output pixel (i,j) reads input rows
+// ((b*W + i + ky + shift) * W + j + kx + shift), shift = H - KS/2. The halo is written once
+// (buffers are zero-initialised) and never touched by any kernel.
+//
+// GEMM view:  Y[m, n] = sum_{tap, c} X[row(m, tap), c] * Wf[tap, n, c]
+//             m = b*S*S + i*S + j (B*361 rows), n = output channel, K = taps * C.
+// The same kernel computes dgrad with tap-flipped, transposed weights Wb[tap', c, n] and an
+// epilogue mask (input > 0) that applies the producing layer's ReLU derivative in place.
+//
+// Tiling (conv_igemm): 256 threads = 4 waves (2 along M x 2 along N); block tile 128 pixels x
+// 32*NT channels; wave tile 64 x 16*NT as 4 x NT MFMA 16x16x32 bf16 tiles. K step = one tap x 32
+// channels. Both operands are staged global->LDS with global_load_lds_dwordx4 (per-lane gathered
+// source rows, lane-linear LDS image, swizzle applied on the source address), double-buffered.
+// The MFMA is issued as C^T = W * X^T so each lane owns 4 consecutive output channels of one
+// pixel: the epilogue (bias, ReLU, ReLU-mask, bf16 pack) stores 8 bytes per lane.
+#include "common.h"
+
+using namespace rag;
+
+namespace {
+
+constexpr int kBM = 128;  // pixels per block
+constexpr int kBK = 32;   // K per step (one MFMA)
+
+template <int KS, int NT>
+__global__ void __launch_bounds__(256, 2)
+conv_igemm_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
+                  const float* __restrict__ bias, bf16* __restrict__ Y,
+                  const bf16* __restrict__ mask, int M, int S, int WI, int shift, int WO, int HO,
+                  int CIN, int WROWS, int YC, int relu) {
+  constexpr int BN = 32 * NT;
+  constexpr int WN = 16 * NT;
+  constexpr int STAGE = (kBM + BN) * kBK;  // bf16 elements per stage
+  __shared__ __attribute__((aligned(16))) bf16 lds[2 * STAGE];
+
+  const int lane = lane_id();
+  const int w = wave_id();
+  const int wm = w & 1, wn = w >> 1;
+  const int m0 = blockIdx.x * kBM;
+  const int n0 = blockIdx.y * BN;
+  const int S2 = S * S;
+
+  // per-lane gather rows for the A (pixel) tile: instructions w and w+4, 16 rows each
+  int abase[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int row = (w + 4 * k) * 16 + (lane >> 2);
+    int m = m0 + row;
+    m = m < M ? m : M - 1;
+    const int b = m / S2;
+    const int rem = m - b * S2;
+    const int i = rem / S;
+    const int j = rem - i * S;
+    abase[k] = ((b * WI + i + shift) * WI + j + shift) * CIN + (((lane & 3) ^ swz64(row)) * 8);
+  }
+  constexpr int BINST = BN / 16;  // wave-instructions per B tile
+  int bbase[(BINST + 3) / 4];
+#pragma unroll
+  for (int k = 0; k < (BINST + 3) / 4; ++k) {
+    const int row = (w + 4 * k) * 16 + (lane >> 2);
+    bbase[k] = (n0 + row) * CIN + (((lane & 3) ^ swz64(row)) * 8);
+  }
+
+  const int cchunks = CIN / kBK;
+  const int nsteps = KS * KS * cchunks;
+
+  auto stage = [&](int buf, int s) {
+    const int tap = s / cchunks;
+    const int c0 = (s - tap * cchunks) * kBK;
+    const int ky = tap / KS, kx = tap - (tap / KS) * KS;
+    const int aoff = (ky * WI + kx) * CIN + c0;
+    bf16* la = lds + buf * STAGE;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) glds16(X + abase[k] + aoff, la + (w + 4 * k) * 16 * kBK);
+    bf16* lb = la + kBM * kBK;
+    const int boff = tap * WROWS * CIN + c0;
+#pragma unroll
+    for (int k = 0; k < (BINST + 3) / 4; ++k) {
+      const int inst = w + 4 * k;
+      if (inst < BINST) glds16(Wt + bbase[k] + boff, lb + inst * 16 * kBK);
+    }
+  };
+
+  f32x4 acc[NT][4];
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int frow = lane & 15;
+  const int fq = lane >> 4;
+  for (int s = 0; s < nsteps; ++s) {
+    const int cur = s & 1;
+    if (s + 1 < nsteps) stage(cur ^ 1, s + 1);
+    const bf16* la = lds + cur * STAGE;
+    const bf16* lb = la + kBM * kBK;
+    bf16x8 xa[4], wb[NT];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = wm * 64 + i * 16 + frow;
+      xa[i] = *reinterpret_cast<const bf16x8*>(la + row * kBK + ((fq ^ swz64(row)) * 8));
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int row = wn * WN + j * 16 + frow;
+      wb[j] = *reinterpret_cast<const bf16x8*>(lb + row * kBK + ((fq ^ swz64(row)) * 8));
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[j][i] = mfma16(wb[j], xa[i], acc[j][i]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // epilogue: lane owns channels n..n+3 of pixel m for every (j, i) tile
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + wm * 64 + i * 16 + frow;
+    if (m >= M) continue;
+    const int b = m / S2;
+    const int rem = m - b * S2;
+    const int pi = rem / S;
+    const int pj = rem - pi * S;
+    const size_t orow = (size_t)((b * WO + pi + HO) * WO + pj + HO) * YC;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int n = n0 + wn * WN + j * 16 + fq * 4;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[j][i][r];
+      if (bias) {
+        const float4 bb = *reinterpret_cast<const float4*>(bias + n);
+        v[0] += bb.x;
+        v[1] += bb.y;
+        v[2] += bb.z;
+        v[3] += bb.w;
+      }
+      if (relu) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      }
+      if (mask) {
+        const bf16x4 mk = *reinterpret_cast<const bf16x4*>(mask + orow + n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = ((float)mk[r] > 0.f) ? v[r] : 0.f;
+      }
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (bf16)v[r];
+      *reinterpret_cast<bf16x4*>(Y + orow + n) = o;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------- wgrad
+// dW[tap][n][c] = sum_m G[m][n] * X[row(m,tap)][c]   (G = gradient w.r.t. pre-activation)
+// Block = (pixel chunk, (n,c) tile, tap). Per step: 32 pixels of G and of the tap-shifted X are
+// staged row-major ([pixel][channel], the natural layout) by global_load_lds; fragments along
+// the pixel (K) axis are read with ds_read_tr16_b64 (hardware transpose). fp32 partials go to a
+// per-chunk slab (plain stores), reduced by wgrad_reduce_kernel, which also emits OIHW layout.
+template <int KS, int NTN, int NTC>
+__global__ void __launch_bounds__(256, 1)
+conv_wgrad_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
+                  float* __restrict__ part, float* __restrict__ bpart, int M, int S, int WI,
+                  int shift, int WG, int GC, int CIN, int steps_per_chunk, int COUTP, int CINP,
+                  int ntile_c) {
+  constexpr int BNN = 32 * NTN, BNC = 32 * NTC;
+  constexpr int WNN = 16 * NTN, WNC = 16 * NTC;
+  constexpr int GROW = BNN, XROW = BNC;  // elements per LDS row
+  constexpr int STAGE = 32 * (GROW + XROW);
+  __shared__ __attribute__((aligned(16))) bf16 lds[2 * STAGE];
+
+  const int lane = lane_id();
+  const int w = wave_id();
+  const int wa = w & 1, wb = w >> 1;  // wa along n, wb along c
+  const int chunk = blockIdx.x;
+  const int tn = blockIdx.y / ntile_c, tc = blockIdx.y - (blockIdx.y / ntile_c) * ntile_c;
+  const int tap = blockIdx.z;
+  const int n0 = tn * BNN, c0 = tc * BNC;
+  const int ky = tap / KS, kx = tap - (tap / KS) * KS;
+  const int S2 = S * S;
+  const int mbeg = chunk * steps_per_chunk * 32;
+
+  constexpr int GCH = BNN / 8, XCH = BNC / 8;  // 16B chunks per row
+  constexpr int GINST = 32 * GCH / 64, XINST = 32 * XCH / 64;
+
+  auto stage = [&](int buf, int s) {
+    bf16* lg = lds + buf * STAGE;
+    bf16* lx = lg + 32 * GROW;
+    const int mb = mbeg + s * 32;
+    for (int k = w; k < GINST; k += 4) {
+      const int idx = k * 64 + lane;
+      const int row = idx / GCH, ch = idx - (idx / GCH) * GCH;
+      const int m = mb + row;
+      size_t src = 0;  // padded row 0 is halo (zero): contributes nothing
+      if (m < M) {
+        const int b = m / S2, rem = m - (m / S2) * S2;
+        const int pi = rem / S, pj = rem - (rem / S) * S;
+        src = (size_t)((b * WG + pi + 1) * WG + pj + 1) * GC + n0 + ch * 8;
+      }
+      glds16(G + src, lg + k * 512);
+    }
+    for (int k = w; k < XINST; k += 4) {
+      const int idx = k * 64 + lane;
+      const int row = idx / XCH, ch = idx - (idx / XCH) * XCH;
+      int m = mb + row;
+      m = m < M ? m : M - 1;  // G row is zero for m >= M
+      const int b = m / S2, rem = m - (m / S2) * S2;
+      const int pi = rem / S, pj = rem - (rem / S) * S;
+      const size_t src =
+          (size_t)((b * WI + pi + ky + shift) * WI + pj + kx + shift) * CIN + c0 + ch * 8;
+      glds16(X + src, lx + k * 512);
+    }
+  };
+
+  f32x4 acc[NTN][NTC];
+#pragma unroll
+  for (int a = 0; a < NTN; ++a)
+#pragma unroll
+    for (int c = 0; c < NTC; ++c) acc[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;
+  const bool do_bias = (bpart != nullptr) && tap == 0 && tc == 0;
+
+  const int mleft = M - mbeg;
+  int nsteps = (mleft + 31) / 32;
+  nsteps = nsteps < steps_per_chunk ? nsteps : steps_per_chunk;
+
+  if (nsteps > 0) {
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  for (int s = 0; s < nsteps; ++s) {
+    const int cur = s & 1;
+    if (s + 1 < nsteps) stage(cur ^ 1, s + 1);
+    const bf16* lg = lds + cur * STAGE;
+    const bf16* lx = lg + 32 * GROW;
+    bf16x8 fa[NTN], fb[NTC];
+#pragma unroll
+    for (int a = 0; a < NTN; ++a) {
+      const int col = wa * WNN + a * 16 + 4 * p;
+      const bf16* p0 = lg + (8 * g + q) * GROW + col;
+      const bf16* p1 = lg + (8 * g + 4 + q) * GROW + col;
+      bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_PTR(bf16x4))p0);
+      bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_PTR(bf16x4))p1);
+      fa[a] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+#pragma unroll
+    for (int c = 0; c < NTC; ++c) {
+      const int col = wb * WNC + c * 16 + 4 * p;
+      const bf16* p0 = lx + (8 * g + q) * XROW + col;
+      const bf16* p1 = lx + (8 * g + 4 + q) * XROW + col;
+      bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_PTR(bf16x4))p0);
+      bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_PTR(bf16x4))p1);
+      fb[c] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+#pragma unroll
+    for (int a = 0; a < NTN; ++a)
+#pragma unroll
+      for (int c = 0; c < NTC; ++c) acc[a][c] = mfma16(fa[a], fb[c], acc[a][c]);
+    if (do_bias && (int)threadIdx.x < BNN) {
+#pragma unroll 8
+      for (int r = 0; r < 32; ++r) bsum += (float)lg[r * GROW + threadIdx.x];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // write the partial slab part[chunk][tap][n][c] (fp32, plain stores)
+  const int taps = KS * KS;
+  float* dst = part + ((size_t)(chunk * taps + tap) * COUTP) * CINP;
+#pragma unroll
+  for (int a = 0; a < NTN; ++a)
+#pragma unroll
+    for (int c = 0; c < NTC; ++c) {
+      const int n = n0 + wa * WNN + a * 16 + g * 4;
+      const int cc = c0 + wb * WNC + c * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dst[(size_t)(n + r) * CINP + cc] = acc[a][c][r];
+    }
+  if (do_bias && (int)threadIdx.x < BNN) bpart[(size_t)chunk * COUTP + n0 + threadIdx.x] = bsum;
+}
+
+// sum partial slabs -> OIHW fp32 weight gradient (unpadded) and bias gradient
+__global__ void wgrad_reduce_kernel(const float* __restrict__ part, const float* __restrict__ bpart,
+                                    float* __restrict__ dW, float* __restrict__ db, int nchunks,
+                                    int taps, int COUT, int CIN, int COUTP, int CINP, int KS,
+                                    int accumulate) {
+  const int total = COUT * CIN * taps;
+  const size_t slab = (size_t)taps * COUTP * CINP;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total + COUT;
+       idx += gridDim.x * blockDim.x) {
+    if (idx < total) {
+      // OIHW: idx = (n*CIN + c)*taps + tap
+      const int tap = idx % taps;
+      const int nc = idx / taps;
+      const int c = nc % CIN, n = nc / CIN;
+      const size_t off = ((size_t)tap * COUTP + n) * CINP + c;
+      float s = 0.f;
+      for (int k = 0; k < nchunks; ++k) s += part[k * slab + off];
+      dW[idx] = accumulate ? dW[idx] + s : s;
+    } else if (db && bpart) {
+      const int n = idx - total;
+      float s = 0.f;
+      for (int k = 0; k < nchunks; ++k) s += bpart[(size_t)k * COUTP + n];
+      db[n] = accumulate ? db[n] + s : s;
+    }
+  }
+}
+
+// OIHW fp32 master weights -> bf16 forward [tap][COUTP][CINP] and dgrad [tap'][CINP][COUTP]
+__global__ void pack_weights_kernel(const float* __restrict__ W, bf16* __restrict__ Wf,
+                                    bf16* __restrict__ Wb, int COUT, int CIN, int KS, int COUTP,
+                                    int CINP) {
+  const int taps = KS * KS;
+  const int total = taps * COUTP * CINP;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += gridDim.x * blockDim.x) {
+    const int c = idx % CINP;
+    const int n = (idx / CINP) % COUTP;
+    const int tap = idx / (CINP * COUTP);
+    float v = 0.f;
+    if (n < COUT && c < CIN) v = W[((size_t)n * CIN + c) * taps + tap];
+    Wf[idx] = (bf16)v;
+    if (Wb) Wb[((size_t)(taps - 1 - tap) * CINP + c) * COUTP + n] = (bf16)v;
+  }
+}
+
+__device__ __forceinline__ void dihedral(int t, int n, int i, int j, int& si, int& sj) {
+  // source coordinate of output (i, j) under transform t (np.rot90 / flips, reference order
+  // noop, rot90, rot180, rot270, fliplr, flipud, diag1, diag2)
+  switch (t) {
+    case 1: si = j; sj = n - 1 - i; break;
+    case 2: si = n - 1 - i; sj = n - 1 - j; break;
+    case 3: si = n - 1 - j; sj = i; break;
+    case 4: si = i; sj = n - 1 - j; break;
+    case 5: si = n - 1 - i; sj = j; break;
+    case 6: si = j; sj = i; break;
+    case 7: si = n - 1 - j; sj = n - 1 - i; break;
+    default: si = i; sj = j; break;
+  }
+}
+
+// uint8 feature planes [B][F][S][S] (optionally gathered by index and dihedral-transformed)
+// -> padded channels-last bf16 [B][S+2H][S+2H][CP]   (K08 fused with layout conversion)
+template <typename T>
+__global__ void pack_input_kernel(const T* __restrict__ F, const int64_t* __restrict__ index,
+                                  const int* __restrict__ tf, bf16* __restrict__ X, int B, int NF,
+                                  int S, int H, int CP) {
+  const int S2 = S * S;
+  const int total = B * S2;
+  const int WP = S + 2 * H;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += gridDim.x * blockDim.x) {
+    const int b = idx / S2;
+    const int rem = idx - b * S2;
+    const int i = rem / S, j = rem - (rem / S) * S;
+    int si = i, sj = j;
+    if (tf) dihedral(tf[b], S, i, j, si, sj);
+    const int64_t sb = index ? index[b] : b;
+    const T* src = F + (size_t)sb * NF * S2 + si * S + sj;
+    bf16* dst = X + ((size_t)(b * WP + i + H) * WP + j + H) * CP;
+    for (int c8 = 0; c8 < CP; c8 += 8) {
+      bf16x8 v;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int c = c8 + k;
+        v[k] = (bf16)(c < NF ? (float)src[(size_t)c * S2] : 0.f);
+      }
+      *reinterpret_cast<bf16x8*>(dst + c8) = v;
+    }
+  }
+}
+
+// padded channels-last bf16 -> NCHW fp32 (tests / debugging / generic consumers)
+__global__ void unpack_kernel(const bf16* __restrict__ X, float* __restrict__ out, int B, int C,
+                              int S, int H, int CP) {
+  const int S2 = S * S;
+  const int WP = S + 2 * H;
+  const int total = B * C * S2;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += gridDim.x * blockDim.x) {
+    const int p = idx % S2;
+    const int c = (idx / S2) % C;
+    const int b = idx / (S2 * C);
+    const int i = p / S, j = p % S;
+    out[idx] = (float)X[((size_t)(b * WP + i + H) * WP + j + H) * CP + c];
+  }
+}
+
+// NCHW fp32 -> padded channels-last bf16 (gradient / activation import)
+__global__ void pack_nchw_kernel(const float* __restrict__ in, bf16* __restrict__ X, int B, int C,
+                                 int S, int H, int CP) {
+  const int S2 = S * S;
+  const int WP = S + 2 * H;
+  const int total = B * S2 * CP;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += gridDim.x * blockDim.x) {
+    const int c = idx % CP;
+    const int p = (idx / CP) % S2;
+    const int b = idx / (CP * S2);
+    const int i = p / S, j = p % S;
+    const float v = c < C ? in[((size_t)b * C + c) * S2 + p] : 0.f;
+    X[((size_t)(b * WP + i + H) * WP + j + H) * CP + c] = (bf16)v;
+  }
+}
+
+template <int KS>
+void launch_igemm_ks(int nt, dim3 grid, hipStream_t st, const bf16* X, const bf16* W,
+                     const float* bias, bf16* Y, const bf16* mask, int M, int S, int WI,
+                     int shift, int WO, int HO, int CIN, int WROWS, int YC, int relu) {
+  switch (nt) {
+#define RAG_NT(N)                                                                              \
+  case N:                                                                                      \
+    conv_igemm_kernel<KS, N><<<grid, 256, 0, st>>>(X, W, bias, Y, mask, M, S, WI, shift, WO, \
+                                                   HO, CIN, WROWS, YC, relu);                 \
+    break;
+    RAG_NT(1) RAG_NT(2) RAG_NT(3) RAG_NT(4) RAG_NT(6)
+#undef RAG_NT
+  }
+}
+
+int pick_nt(int coutp) {
+  if (coutp % 192 == 0) return 6;
+  if (coutp % 128 == 0) return 4;
+  if (coutp % 96 == 0) return 3;
+  if (coutp % 64 == 0) return 2;
+  return 1;
+}
+
+}  // namespace
+
+// ============================================================================= C ABI
+// Conv forward / dgrad.  X: padded input (halo HI, CIN channels, CIN % 32 == 0).  W: packed
+// bf16 weights [taps][WROWS][CIN].  Y: padded output (halo HO, YC channels, COUTP % 32 == 0,
+// COUTP <= YC).  bias: fp32 [COUTP] or null.  mask: same layout as Y or null.
+RAG_API int rag_conv_igemm(const void* X, const void* W, const float* bias, void* Y,
+                           const void* mask, int B, int S, int HI, int HO, int CIN, int COUTP,
+                           int YC, int KS, int relu, hipStream_t stream) {
+  if (CIN % 32 || COUTP % 32 || YC < COUTP || HI < KS / 2) return -1;
+  const int M = B * S * S;
+  const int nt = pick_nt(COUTP);
+  dim3 grid((M + kBM - 1) / kBM, COUTP / (32 * nt));
+  const int WI = S + 2 * HI, WO = S + 2 * HO, shift = HI - KS / 2;
+  const bf16* x = (const bf16*)X;
+  const bf16* w = (const bf16*)W;
+  bf16* y = (bf16*)Y;
+  const bf16* mk = (const bf16*)mask;
+  switch (KS) {
+    case 1: launch_igemm_ks<1>(nt, grid, stream, x, w, bias, y, mk, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu); break;
+    case 3: launch_igemm_ks<3>(nt, grid, stream, x, w, bias, y, mk, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu); break;
+    case 5: launch_igemm_ks<5>(nt, grid, stream, x, w, bias, y, mk, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu); break;
+    case 7: launch_igemm_ks<7>(nt, grid, stream, x, w, bias, y, mk, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu); break;
+    default: return -2;
+  }
+  return (int)hipGetLastError();
+}
+
+// Workspace (floats) needed by rag_conv_wgrad for the partial slabs.
+RAG_API size_t rag_conv_wgrad_workspace(int B, int S, int COUTP, int CINP, int KS, int* nchunks) {
+  const int M = B * S * S;
+  const int taps = KS * KS;
+  const int ntn = COUTP % 192 == 0 ? 6 : (COUTP % 128 == 0 ? 4 : (COUTP % 64 == 0 ? 2 : 1));
+  const int ntc = CINP % 96 == 0 ? 3 : (CINP % 64 == 0 ? 2 : 1);
+  const int tiles = taps * (COUTP / (32 * ntn)) * (CINP / (32 * ntc));
+  const int msteps = (M + 31) / 32;
+  int nc = (512 + tiles - 1) / tiles;
+  if (nc > msteps) nc = msteps;
+  if (nc < 1) nc = 1;
+  if (nchunks) *nchunks = nc;
+  return (size_t)nc * taps * COUTP * CINP + (size_t)nc * COUTP;
+}
+
+template <int KS>
+static void launch_wgrad_ks(int ntn, int ntc, dim3 grid, hipStream_t st, const bf16* G,
+                            const bf16* X, float* part, float* bpart, int M, int S, int WI,
+                            int shift, int WG, int GC, int CIN, int spc, int COUTP, int CINP,
+                            int ntile_c) {
+#define RAG_WG(A, C)                                                                          \
+  if (ntn == A && ntc == C) {                                                                 \
+    conv_wgrad_kernel<KS, A, C><<<grid, 256, 0, st>>>(G, X, part, bpart, M, S, WI, shift, WG, \
+                                                      GC, CIN, spc, COUTP, CINP, ntile_c);   \
+    return;                                                                                   \
+  }
+  RAG_WG(6, 3) RAG_WG(6, 2) RAG_WG(6, 1) RAG_WG(4, 3) RAG_WG(4, 2) RAG_WG(4, 1)
+  RAG_WG(2, 3) RAG_WG(2, 2) RAG_WG(2, 1) RAG_WG(1, 3) RAG_WG(1, 2) RAG_WG(1, 1)
+#undef RAG_WG
+}
+
+// Weight + bias gradient. G: dL/d(pre-activation) in padded layout (halo 1, GC channels).
+// X: the layer input (halo HI, CINP channels). dW: OIHW fp32 [COUT][CIN][KS][KS]. db: [COUT].
+RAG_API int rag_conv_wgrad(const void* G, const void* X, float* dW, float* db, float* work,
+                           int B, int S, int HI, int GC, int COUT, int COUTP, int CIN, int CINP,
+                           int KS, int accumulate, hipStream_t stream) {
+  if (COUTP % 32 || CINP % 32) return -1;
+  int nchunks = 1;
+  rag_conv_wgrad_workspace(B, S, COUTP, CINP, KS, &nchunks);
+  const int M = B * S * S;
+  const int taps = KS * KS;
+  const int ntn = COUTP % 192 == 0 ? 6 : (COUTP % 128 == 0 ? 4 : (COUTP % 64 == 0 ? 2 : 1));
+  const int ntc = CINP % 96 == 0 ? 3 : (CINP % 64 == 0 ? 2 : 1);
+  const int ntile_n = COUTP / (32 * ntn), ntile_c = CINP / (32 * ntc);
+  const int msteps = (M + 31) / 32;
+  const int spc = (msteps + nchunks - 1) / nchunks;
+  float* part = work;
+  float* bpart = db ? work + (size_t)nchunks * taps * COUTP * CINP : nullptr;
+  dim3 grid(nchunks, ntile_n * ntile_c, taps);
+  const int WI = S + 2 * HI, shift = HI - KS / 2, WG = S + 2;
+  const bf16* g = (const bf16*)G;
+  const bf16* x = (const bf16*)X;
+  switch (KS) {
+    case 1: launch_wgrad_ks<1>(ntn, ntc, grid, stream, g, x, part, bpart, M, S, WI, shift, WG, GC, CINP, spc, COUTP, CINP, ntile_c); break;
+    case 3: launch_wgrad_ks<3>(ntn, ntc, grid, stream, g, x, part, bpart, M, S, WI, shift, WG, GC, CINP, spc, COUTP, CINP, ntile_c); break;
+    case 5: launch_wgrad_ks<5>(ntn, ntc, grid, stream, g, x, part, bpart, M, S, WI, shift, WG, GC, CINP, spc, COUTP, CINP, ntile_c); break;
+    case 7: launch_wgrad_ks<7>(ntn, ntc, grid, stream, g, x, part, bpart, M, S, WI, shift, WG, GC, CINP, spc, COUTP, CINP, ntile_c); break;
+    default: return -2;
+  }
+  const int total = COUT * CIN * taps + COUT;
+  wgrad_reduce_kernel<<<(total + 255) / 256, 256, 0, stream>>>(part, bpart, dW, db, nchunks, taps,
+                                                              COUT, CIN, COUTP, CINP, KS,
+                                                              accumulate);
+  return (int)hipGetLastError();
+}
+
+RAG_API int rag_pack_weights(const float* W, void* Wf, void* Wb, int COUT, int CIN, int KS,
+                             int COUTP, int CINP, hipStream_t stream) {
+  const int total = KS * KS * COUTP * CINP;
+  const int blocks = (total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048;
+  pack_weights_kernel<<<blocks, 256, 0, stream>>>(W, (bf16*)Wf, (bf16*)Wb, COUT, CIN, KS, COUTP,
+                                                  CINP);
+  return (int)hipGetLastError();
+}
+
+RAG_API int rag_pack_input_u8(const uint8_t* F, const int64_t* index, const int* tf, void* X,
+                              int B, int NF, int S, int H, int CP, hipStream_t stream) {
+  const int total = B * S * S;
+  const int blocks = (total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096;
+  pack_input_kernel<uint8_t><<<blocks, 256, 0, stream>>>(F, index, tf, (bf16*)X, B, NF, S, H, CP);
+  return (int)hipGetLastError();
+}
+
+RAG_API int rag_pack_input_f32(const float* F, const int64_t* index, const int* tf, void* X,
+                               int B, int NF, int S, int H, int CP, hipStream_t stream) {
+  const int total = B * S * S;
+  const int blocks = (total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096;
+  pack_input_kernel<float><<<blocks, 256, 0, stream>>>(F, index, tf, (bf16*)X, B, NF, S, H, CP);
+  return (int)hipGetLastError();
+}
+
+RAG_API int rag_unpack(const void* X, float* out, int B, int C, int S, int H, int CP,
+                       hipStream_t stream) {
+  const int total = B * C * S * S;
+  const int blocks = (total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096;
+  unpack_kernel<<<blocks, 256, 0, stream>>>((const bf16*)X, out, B, C, S, H, CP);
+  return (int)hipGetLastError();
+}
+
+RAG_API int rag_pack_nchw(const float* in, void* X, int B, int C, int S, int H, int CP,
+                          hipStream_t stream) {
+  const int total = B * S * S * CP;
+  const int blocks = (total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096;
+  pack_nchw_kernel<<<blocks, 256, 0, stream>>>(in, (bf16*)X, B, C, S, H, CP);
+  return (int)hipGetLastError();
+}

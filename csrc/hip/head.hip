@@ -1,0 +1,212 @@
+// Network heads on gfx950 — kernels K03/K04 (policy head + fused softmax cross-entropy /
+// REINFORCE loss) and the 1x1-conv part of K11 (value head), forward and backward.
+//
+// Policy head (reference policy.py:124-136 + nn_util.py:118-133):
+//   z[b,p] = sum_k w[k] * h[b,p,k] + b0 + bias[p];  prob = softmax_p(z)
+// One workgroup per board: pixel dot products (16-byte channel loads), logits kept in LDS, block
+// max/sum reductions, then probabilities, per-sample loss, dL/dz and top-1 hit written in the same
+// pass. Loss modes: 0 = none (inference), 1 = categorical cross-entropy (Keras, mean over batch),
+// 2 = REINFORCE log_loss (Keras: -y log clip(p), averaged over the S*S classes and the batch;
+// reinforcement_policy_trainer.py:89-94), each sample scaled by an optional signed weight.
+#include "common.h"
+
+using namespace rag;
+
+namespace {
+
+constexpr int kHeadThreads = 256;
+
+__device__ __forceinline__ float block_reduce(float v, float* sh, bool is_max) {
+  v = is_max ? warp_max(v) : warp_sum(v);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) sh[w] = v;
+  __syncthreads();
+  float r = sh[0];
+  const int nw = blockDim.x >> 6;
+  for (int k = 1; k < nw; ++k) r = is_max ? fmaxf(r, sh[k]) : r + sh[k];
+  return r;
+}
+
+__global__ void __launch_bounds__(kHeadThreads)
+policy_head_fwd_kernel(const bf16* __restrict__ H, const float* __restrict__ w, const float* b0,
+                       const float* __restrict__ pbias, float* __restrict__ probs,
+                       const int64_t* __restrict__ labels, const float* __restrict__ sweight,
+                       float* __restrict__ loss, float* __restrict__ dz, float* __restrict__ hit,
+                       int S, int KP, int K, int mode, float gscale) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* z = smem;                    // S*S logits
+  float* ws = smem + ((S * S + 3) & ~3);  // KP weights
+  __shared__ float red[16];
+  const int b = blockIdx.x;
+  const int S2 = S * S, WP = S + 2;
+  for (int k = threadIdx.x; k < KP; k += blockDim.x) ws[k] = k < K ? w[k] : 0.f;
+  __syncthreads();
+  const float bias0 = b0 ? *b0 : 0.f;
+  for (int p = threadIdx.x; p < S2; p += blockDim.x) {
+    const int i = p / S, j = p - (p / S) * S;
+    const bf16* row = H + ((size_t)(b * WP + i + 1) * WP + j + 1) * KP;
+    float acc = 0.f;
+    for (int c = 0; c < KP; c += 8) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(row + c);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) acc += (float)v[t] * ws[c + t];
+    }
+    z[p] = acc + bias0 + (pbias ? pbias[p] : 0.f);
+  }
+  __syncthreads();
+  float mx = -INFINITY;
+  int amax = 0;
+  for (int p = threadIdx.x; p < S2; p += blockDim.x)
+    if (z[p] > mx) {
+      mx = z[p];
+      amax = p;
+    }
+  const float gmax = block_reduce(mx, red, true);
+  float se = 0.f;
+  for (int p = threadIdx.x; p < S2; p += blockDim.x) se += __expf(z[p] - gmax);
+  const float sum = block_reduce(se, red, false);
+  const float inv = 1.f / sum;
+  const int64_t lab = (mode && labels) ? labels[b] : -1;
+  const float sw = sweight ? sweight[b] : 1.f;
+  const float cls = (mode == 2) ? 1.f / (float)S2 : 1.f;
+  for (int p = threadIdx.x; p < S2; p += blockDim.x) {
+    const float pr = __expf(z[p] - gmax) * inv;
+    probs[(size_t)b * S2 + p] = pr;
+    if (mode && dz) {
+      const float y = (p == lab) ? 1.f : 0.f;
+      dz[(size_t)b * S2 + p] = (pr - y) * sw * cls * gscale;
+    }
+  }
+  if (mode && threadIdx.x == 0 && lab >= 0) {
+    float pl = __expf(z[lab] - gmax) * inv;
+    pl = fminf(fmaxf(pl, 1e-7f), 1.f - 1e-7f);
+    if (loss) loss[b] = -__logf(pl) * sw * cls;
+  }
+  // top-1 hit (ties -> lowest index, like argmax)
+  if (mode && hit) {
+    // reduce (value, index) pair: first the max value is known (gmax); find lowest index == gmax
+    int cand = (mx == gmax) ? amax : 0x7fffffff;
+    for (int o = 32; o > 0; o >>= 1) cand = min(cand, __shfl_xor(cand, o, 64));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = __int_as_float(cand);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int best = 0x7fffffff;
+      for (int k = 0; k < (int)(blockDim.x >> 6); ++k) best = min(best, __float_as_int(red[k]));
+      hit[b] = (best == lab) ? 1.f : 0.f;
+    }
+  }
+}
+
+// Backward of the 1x1 K->1 head conv (+ per-position bias): given dz [B][S2],
+//   dH[b,p,k] = dz[b,p] * w[k] * (H[b,p,k] > 0)   (fused ReLU derivative of the last trunk layer)
+//   dw[k] += sum dz*H, db0 += sum dz, dpbias[p] += sum_b dz
+__global__ void __launch_bounds__(kHeadThreads)
+head_bwd_kernel(const bf16* __restrict__ H, const float* __restrict__ w,
+                const float* __restrict__ dz, bf16* __restrict__ dH, float* __restrict__ dw,
+                float* __restrict__ db0, float* __restrict__ dpbias, int S, int KP, int K,
+                int relu_mask) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* ws = smem;       // KP
+  float* dwl = smem + KP;  // KP partial dw
+  __shared__ float red[16];
+  const int b = blockIdx.x;
+  const int S2 = S * S, WP = S + 2;
+  for (int k = threadIdx.x; k < KP; k += blockDim.x) {
+    ws[k] = k < K ? w[k] : 0.f;
+    dwl[k] = 0.f;
+  }
+  __syncthreads();
+  // one wave per pixel row group: lanes split the channel axis (8 channels per lane)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int lanes_per_row = KP / 8;  // <= 64 for KP <= 512
+  const int rows_per_wave = 64 / lanes_per_row;
+  const int sub = lane / lanes_per_row, cl = lane - sub * lanes_per_row;
+  float dwacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float dbacc = 0.f;
+  for (int p0 = wv * rows_per_wave; p0 < S2; p0 += nw * rows_per_wave) {
+    const int p = p0 + sub;
+    if (sub < rows_per_wave && p < S2) {
+      const int i = p / S, j = p - (p / S) * S;
+      const size_t off = ((size_t)(b * WP + i + 1) * WP + j + 1) * KP + cl * 8;
+      const float g = dz[(size_t)b * S2 + p];
+      const bf16x8 hv = *reinterpret_cast<const bf16x8*>(H + off);
+      bf16x8 o;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const float hf = (float)hv[t];
+        float d = g * ws[cl * 8 + t];
+        if (relu_mask && !(hf > 0.f)) d = 0.f;
+        o[t] = (bf16)d;
+        dwacc[t] += g * hf;
+      }
+      if (dH) *reinterpret_cast<bf16x8*>(dH + off) = o;
+      if (cl == 0) {
+        dbacc += g;
+        if (dpbias) atomicAdd(dpbias + p, g);
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 8; ++t) atomicAdd(&dwl[cl * 8 + t], dwacc[t]);  // LDS atomics
+  const float dbs = block_reduce(dbacc, red, false);
+  __syncthreads();
+  for (int k = threadIdx.x; k < K; k += blockDim.x) atomicAdd(dw + k, dwl[k]);
+  if (threadIdx.x == 0 && db0) atomicAdd(db0, dbs);
+}
+
+// z[b,p] = sum_k w[k]*h[b,p,k] + b0 (value-head 1x1 conv, no softmax)
+__global__ void __launch_bounds__(kHeadThreads)
+head_linear_kernel(const bf16* __restrict__ H, const float* __restrict__ w, const float* b0,
+                   float* __restrict__ z, int B, int S, int KP, int K) {
+  const int S2 = S * S, WP = S + 2;
+  const int total = B * S2;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += gridDim.x * blockDim.x) {
+    const int b = idx / S2, p = idx - (idx / S2) * S2;
+    const int i = p / S, j = p - (p / S) * S;
+    const bf16* row = H + ((size_t)(b * WP + i + 1) * WP + j + 1) * KP;
+    float acc = 0.f;
+    for (int c = 0; c < K; c += 8) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(row + c);
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+        if (c + t < K) acc += (float)v[t] * w[c + t];
+    }
+    z[idx] = acc + (b0 ? *b0 : 0.f);
+  }
+}
+
+}  // namespace
+
+RAG_API int rag_policy_head_fwd(const void* H, const float* w, const float* b0,
+                                const float* pbias, float* probs, const int64_t* labels,
+                                const float* sweight, float* loss, float* dz, float* hit, int B,
+                                int S, int KP, int K, int mode, float gscale,
+                                hipStream_t stream) {
+  const size_t sm = (size_t)(((S * S + 3) & ~3) + KP) * sizeof(float);
+  policy_head_fwd_kernel<<<B, kHeadThreads, sm, stream>>>((const bf16*)H, w, b0, pbias, probs,
+                                                          labels, sweight, loss, dz, hit, S, KP,
+                                                          K, mode, gscale);
+  return (int)hipGetLastError();
+}
+
+RAG_API int rag_head_bwd(const void* H, const float* w, const float* dz, void* dH, float* dw,
+                         float* db0, float* dpbias, int B, int S, int KP, int K, int relu_mask,
+                         hipStream_t stream) {
+  if (KP % 8 || KP / 8 > 64) return -1;
+  const size_t sm = (size_t)(2 * KP) * sizeof(float);
+  head_bwd_kernel<<<B, kHeadThreads, sm, stream>>>((const bf16*)H, w, dz, (bf16*)dH, dw, db0,
+                                                   dpbias, S, KP, K, relu_mask);
+  return (int)hipGetLastError();
+}
+
+RAG_API int rag_head_linear(const void* H, const float* w, const float* b0, float* z, int B,
+                            int S, int KP, int K, hipStream_t stream) {
+  const int total = B * S * S;
+  const int blocks = (total + kHeadThreads - 1) / kHeadThreads;
+  head_linear_kernel<<<blocks < 4096 ? blocks : 4096, kHeadThreads, 0, stream>>>(
+      (const bf16*)H, w, b0, z, B, S, KP, K);
+  return (int)hipGetLastError();
+}

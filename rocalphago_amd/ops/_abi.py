@@ -1,0 +1,37 @@
+"""ctypes signatures of the C ABI exported by rocalphago_amd/_hipkernels.so (csrc/hip/*.hip)."""
+import ctypes as C
+
+P = C.c_void_p
+I = C.c_int
+F = C.c_float
+I64 = C.c_int64
+SZ = C.c_size_t
+
+SIGNATURES = {
+    # conv.hip
+    "rag_conv_igemm": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
+    "rag_conv_wgrad_workspace": [I, I, I, I, I, P],
+    "rag_conv_wgrad": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P],
+    "rag_pack_weights": [P, P, P, I, I, I, I, I, P],
+    "rag_pack_input_u8": [P, P, P, P, I, I, I, I, I, P],
+    "rag_pack_input_f32": [P, P, P, P, I, I, I, I, I, P],
+    "rag_unpack": [P, P, I, I, I, I, I, P],
+    "rag_pack_nchw": [P, P, I, I, I, I, I, P],
+    # head.hip
+    "rag_policy_head_fwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, P],
+    "rag_head_bwd": [P, P, P, P, P, P, P, I, I, I, I, I, P],
+    "rag_head_linear": [P, P, P, P, I, I, I, I, P],
+    # optim.hip
+    "rag_sgd": [P, P, P, I64, F, F, F, I, P],
+}
+
+RESTYPES = {"rag_conv_wgrad_workspace": SZ}
+
+
+def declare(lib):
+    for name, args in SIGNATURES.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue  # optional kernels added in later milestones
+        fn.argtypes = args
+        fn.restype = RESTYPES.get(name, I)

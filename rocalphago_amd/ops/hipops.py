@@ -1,0 +1,145 @@
+"""Torch-facing wrappers over the gfx950 HIP kernels (C ABI via ctypes).
+
+All functions take/return torch CUDA tensors and launch on the current HIP stream, so they can be
+captured into HIP graphs (torch.cuda.graph). Activations use the padded channels-last bf16 layout
+described in csrc/hip/conv.hip: ``[B, S+2H, S+2H, CP]`` with a zero halo of width ``H`` and
+``CP = round_up(C, 32)`` channels.
+"""
+import ctypes
+
+import torch
+
+from .._native import hip as _hip_lib
+
+_PAD = 32
+
+
+def pad_channels(c):
+    return (c + _PAD - 1) // _PAD * _PAD
+
+
+def _lib():
+    return _hip_lib(required=True)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _check(rc, name):
+    if rc != 0:
+        raise RuntimeError("%s failed (rc=%d)" % (name, rc))
+
+
+def alloc_padded(B, S, H, CP, device, dtype=torch.bfloat16):
+    """Zero-initialised padded activation buffer (the halo is never written afterwards)."""
+    return torch.zeros((B, S + 2 * H, S + 2 * H, CP), dtype=dtype, device=device)
+
+
+def pack_weights(w, coutp, cinp, wf=None, wb=None):
+    """OIHW fp32 -> bf16 forward [taps, coutp, cinp] (+ dgrad [taps, cinp, coutp] if wb given)."""
+    cout, cin, ks, _ = w.shape
+    taps = ks * ks
+    if wf is None:
+        wf = torch.empty((taps, coutp, cinp), dtype=torch.bfloat16, device=w.device)
+    w = w.contiguous()
+    _check(_lib().rag_pack_weights(_ptr(w), _ptr(wf), _ptr(wb), cout, cin, ks, coutp, cinp,
+                                   _stream()), "pack_weights")
+    return wf, wb
+
+
+def conv_igemm(x, wpack, bias, y, B, S, hi, ho, cinp, coutp, ks, relu, mask=None):
+    """y[pad ho] = act(conv_ks(x[pad hi]) + bias) (or the dgrad form with a ReLU mask)."""
+    _check(_lib().rag_conv_igemm(_ptr(x), _ptr(wpack), _ptr(bias), _ptr(y), _ptr(mask), B, S, hi,
+                                 ho, cinp, coutp, y.shape[-1], ks, int(relu), _stream()),
+           "conv_igemm")
+    return y
+
+
+_ws_cache = {}
+
+
+def wgrad_workspace(B, S, coutp, cinp, ks, device):
+    n = _lib().rag_conv_wgrad_workspace(B, S, coutp, cinp, ks, None)
+    key = (device, )
+    buf = _ws_cache.get(key)
+    if buf is None or buf.numel() < n:
+        buf = torch.empty(int(n * 1.25) + 1024, dtype=torch.float32, device=device)
+        _ws_cache[key] = buf
+    return buf
+
+
+def conv_wgrad(g, x, dw, db, B, S, hi, cout, coutp, cin, cinp, ks, accumulate=False, work=None):
+    """dW (OIHW fp32) and db from dL/dpre g [pad 1] and the layer input x [pad hi]."""
+    if work is None:
+        work = wgrad_workspace(B, S, coutp, cinp, ks, g.device)
+    _check(_lib().rag_conv_wgrad(_ptr(g), _ptr(x), _ptr(dw), _ptr(db), _ptr(work), B, S, hi,
+                                 g.shape[-1], cout, coutp, cin, cinp, ks, int(accumulate),
+                                 _stream()), "conv_wgrad")
+
+
+def pack_input(features, out, H, index=None, transforms=None):
+    """[N, F, S, S] uint8/float32 planes (optionally gathered by ``index`` [B] and dihedral-
+    transformed by ``transforms`` [B] int32) -> padded bf16 ``out`` [B, S+2H, S+2H, CP]."""
+    B = out.shape[0]
+    S = features.shape[-1]
+    NF = features.shape[1]
+    CP = out.shape[-1]
+    fn = _lib().rag_pack_input_u8 if features.dtype == torch.uint8 else _lib().rag_pack_input_f32
+    if features.dtype not in (torch.uint8, torch.float32):
+        features = features.float()
+    _check(fn(_ptr(features), _ptr(index), _ptr(transforms), _ptr(out), B, NF, S, H, CP,
+              _stream()), "pack_input")
+    return out
+
+
+def unpack(x, C, H):
+    """padded channels-last bf16 -> NCHW fp32 (first C channels)."""
+    B, WP, _, CP = x.shape
+    S = WP - 2 * H
+    out = torch.empty((B, C, S, S), dtype=torch.float32, device=x.device)
+    _check(_lib().rag_unpack(_ptr(x), _ptr(out), B, C, S, H, CP, _stream()), "unpack")
+    return out
+
+
+def pack_nchw(t, H, CP, out=None):
+    B, C, S, _ = t.shape
+    if out is None:
+        out = alloc_padded(B, S, H, CP, t.device)
+    t = t.contiguous().float()
+    _check(_lib().rag_pack_nchw(_ptr(t), _ptr(out), B, C, S, H, CP, _stream()), "pack_nchw")
+    return out
+
+
+def policy_head_fwd(h, w, b0, pbias, probs, K, labels=None, sweight=None, loss=None, dz=None,
+                    hit=None, mode=0, gscale=1.0):
+    B, WP, _, KP = h.shape
+    S = WP - 2
+    _check(_lib().rag_policy_head_fwd(_ptr(h), _ptr(w), _ptr(b0), _ptr(pbias), _ptr(probs),
+                                      _ptr(labels), _ptr(sweight), _ptr(loss), _ptr(dz),
+                                      _ptr(hit), B, S, KP, K, mode, float(gscale), _stream()),
+           "policy_head_fwd")
+
+
+def head_bwd(h, w, dz, dh, dw, db0, dpbias, K, relu_mask=True):
+    B, WP, _, KP = h.shape
+    S = WP - 2
+    _check(_lib().rag_head_bwd(_ptr(h), _ptr(w), _ptr(dz), _ptr(dh), _ptr(dw), _ptr(db0),
+                               _ptr(dpbias), B, S, KP, K, int(relu_mask), _stream()), "head_bwd")
+
+
+def head_linear(h, w, b0, z, K):
+    B, WP, _, KP = h.shape
+    S = WP - 2
+    _check(_lib().rag_head_linear(_ptr(h), _ptr(w), _ptr(b0), _ptr(z), B, S, KP, K, _stream()),
+           "head_linear")
+
+
+def sgd_(p, g, lr, momentum=0.0, v=None, wd=0.0, nesterov=False):
+    """In-place Keras-style SGD on a flat fp32 buffer."""
+    _check(_lib().rag_sgd(_ptr(p), _ptr(g), _ptr(v), p.numel(), float(lr), float(momentum),
+                          float(wd), int(nesterov), _stream()), "sgd")

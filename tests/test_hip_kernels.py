@@ -1,0 +1,147 @@
+"""Numerics of the gfx950 HIP kernels against plain PyTorch fp32 references (GPU only)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+def rel_err(a, b):
+    return ((a - b).abs().max() / (b.abs().max() + 1e-6)).item()
+
+
+@pytest.fixture(scope="module")
+def ops():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from rocalphago_amd.ops import hipops
+    return hipops
+
+
+@pytest.mark.parametrize("B,cin,cout,ks,S", [(3, 192, 192, 3, 19), (5, 48, 192, 5, 19),
+                                             (2, 16, 16, 3, 19), (7, 128, 128, 3, 13),
+                                             (4, 192, 32, 1, 19), (1, 12, 16, 5, 9),
+                                             (2, 64, 96, 3, 7)])
+def test_conv_forward(ops, B, cin, cout, ks, S):
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    x = torch.randn(B, cin, S, S, device=dev)
+    w = torch.randn(cout, cin, ks, ks, device=dev) * 0.05
+    b = torch.randn(cout, device=dev) * 0.1
+    ref = F.relu(F.conv2d(bf(x), bf(w), b, padding=ks // 2))
+    cinp, coutp = ops.pad_channels(cin), ops.pad_channels(cout)
+    hi = ks // 2 if ks > 1 else 1
+    xp = ops.pack_nchw(x, hi, cinp)
+    wf, _ = ops.pack_weights(w, coutp, cinp)
+    bias = torch.zeros(coutp, device=dev)
+    bias[:cout] = b
+    y = ops.alloc_padded(B, S, 1, coutp, dev)
+    ops.conv_igemm(xp, wf, bias, y, B, S, hi, 1, cinp, coutp, ks, relu=True)
+    out = ops.unpack(y, cout, 1)
+    assert rel_err(out, ref) < 2e-2
+    # halo stays zero
+    assert y[:, 0].abs().max().item() == 0 and y[:, :, -1].abs().max().item() == 0
+
+
+@pytest.mark.parametrize("B,cin,cout,ks", [(3, 192, 192, 3), (2, 16, 16, 3), (4, 64, 128, 3),
+                                           (3, 32, 192, 5)])
+def test_conv_backward(ops, B, cin, cout, ks):
+    dev = torch.device("cuda")
+    torch.manual_seed(1)
+    S = 19
+    x = F.relu(torch.randn(B, cin, S, S, device=dev))
+    w = torch.randn(cout, cin, ks, ks, device=dev) * 0.05
+    g = torch.randn(B, cout, S, S, device=dev)
+    xr, wr = bf(x).requires_grad_(), bf(w).requires_grad_()
+    y = F.conv2d(xr, wr, padding=ks // 2)
+    (y * bf(g)).sum().backward()
+    cinp, coutp = ops.pad_channels(cin), ops.pad_channels(cout)
+    hi = ks // 2
+    xp = ops.pack_nchw(x, hi, cinp)
+    gp = ops.pack_nchw(g, 1, coutp)
+    wf, wb = ops.pack_weights(w, coutp, cinp,
+                              wb=torch.empty(ks * ks, cinp, coutp, dtype=torch.bfloat16,
+                                             device=dev))
+    if ks == 3:
+        # dgrad with fused ReLU mask of the layer input
+        xm = ops.pack_nchw(x, 1, cinp)
+        dx = ops.alloc_padded(B, S, 1, cinp, dev)
+        ops.conv_igemm(gp, wb, None, dx, B, S, 1, 1, coutp, cinp, ks, relu=False, mask=xm)
+        ref_dx = xr.grad * (x > 0)
+        assert rel_err(ops.unpack(dx, cin, 1), ref_dx) < 2e-2
+    dw = torch.zeros(cout, cin, ks, ks, device=dev)
+    db = torch.zeros(cout, device=dev)
+    ops.conv_wgrad(gp, xp, dw, db, B, S, hi, cout, coutp, cin, cinp, ks)
+    assert rel_err(dw, wr.grad) < 2e-2
+    assert rel_err(db, bf(g).sum((0, 2, 3))) < 2e-2
+
+
+def test_pack_input_transforms(ops):
+    dev = torch.device("cuda")
+    S, NF, B = 19, 48, 8
+    feats = (torch.rand(10, NF, S, S, device=dev) > 0.5).to(torch.uint8)
+    idx = torch.tensor([3, 1, 4, 1, 5, 9, 2, 6], device=dev, dtype=torch.int64)
+    tf = torch.arange(8, device=dev, dtype=torch.int32)
+    out = ops.alloc_padded(B, S, 2, 64, dev)
+    ops.pack_input(feats, out, 2, index=idx, transforms=tf)
+    got = ops.unpack(out, NF, 2).cpu().numpy()
+    fn = [lambda a: a, lambda a: np.rot90(a, 1), lambda a: np.rot90(a, 2), lambda a: np.rot90(a, 3),
+          np.fliplr, np.flipud, np.transpose, lambda a: np.fliplr(np.rot90(a, 1))]
+    src = feats.cpu().numpy()
+    for b in range(B):
+        for c in (0, 7, 47):
+            assert np.array_equal(got[b, c], fn[b](src[idx[b].item(), c]).astype(np.float32))
+
+
+def test_policy_head_and_backward(ops):
+    dev = torch.device("cuda")
+    torch.manual_seed(2)
+    B, K, S = 6, 192, 19
+    h = F.relu(torch.randn(B, K, S, S, device=dev))
+    w = torch.randn(K, device=dev) * 0.1
+    b0 = torch.tensor([0.3], device=dev)
+    pb = torch.randn(S * S, device=dev) * 0.1
+    lab = torch.randint(0, S * S, (B,), device=dev)
+    hp = ops.pack_nchw(h, 1, K)
+    probs = torch.empty(B, S * S, device=dev)
+    loss = torch.empty(B, device=dev)
+    dz = torch.empty(B, S * S, device=dev)
+    hit = torch.empty(B, device=dev)
+    ops.policy_head_fwd(hp, w, b0, pb, probs, K, labels=lab, loss=loss, dz=dz, hit=hit, mode=1,
+                        gscale=1.0 / B)
+    hr = bf(h).requires_grad_()
+    wr, br, pbr = w.clone().requires_grad_(), b0.clone().requires_grad_(), pb.clone().requires_grad_()
+    z = (hr * wr.view(1, K, 1, 1)).sum(1).flatten(1) + br + pbr
+    ref = F.softmax(z, dim=1)
+    assert rel_err(probs, ref) < 1e-2
+    l = F.cross_entropy(z, lab)
+    l.backward()
+    assert abs(loss.mean().item() - l.item()) < 1e-2 * max(1.0, l.item())
+    assert torch.equal(hit.bool(), z.argmax(1) == lab)
+    dh = ops.alloc_padded(B, S, 1, K, dev)
+    dw = torch.zeros(K, device=dev)
+    db0 = torch.zeros(1, device=dev)
+    dpb = torch.zeros(S * S, device=dev)
+    ops.head_bwd(hp, w, dz, dh, dw, db0, dpb, K, relu_mask=True)
+    assert rel_err(ops.unpack(dh, K, 1), hr.grad * (h > 0)) < 2e-2
+    assert rel_err(dw, wr.grad) < 2e-2
+    assert abs(db0.item() - br.grad.item()) < 1e-4  # both ~0: sum of (p - y)
+    assert rel_err(dpb, pbr.grad) < 2e-2
+
+
+def test_sgd(ops):
+    dev = torch.device("cuda")
+    p = torch.randn(1001, device=dev)
+    g = torch.randn(1001, device=dev)
+    ref = p - 0.1 * g
+    ops.sgd_(p, g, 0.1)
+    assert torch.allclose(p, ref, atol=1e-6)
+    v = torch.zeros(1001, device=dev)
+    p2 = p.clone()
+    ops.sgd_(p, g, 0.1, momentum=0.9, v=v)
+    assert torch.allclose(p, p2 - 0.1 * g, atol=1e-6)
