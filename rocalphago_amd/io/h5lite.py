@@ -1,0 +1,1046 @@
+"""h5lite — a self-contained HDF5 subset reader/writer (h5py is not available here).
+
+Scope = what the reference persists through h5py:
+  * Keras-1 weight files (nn_util.py:81,104): root attr ``layer_names``, per-layer groups with
+    attr ``weight_names`` and float32 datasets.
+  * The converter's feature dataset (game_converter.py:54-96): LZF-chunked, resizable uint8
+    ``states`` / ``actions``, group ``file_offsets``, scalar string ``features``.
+
+Format features implemented (HDF5 File Format Specification v2, "version 0" structures):
+  superblock v0/v1; object headers v1 (+ continuation blocks); symbol-table groups (v1 B-tree
+  type 0 + SNOD leaves + local heap) of any size; dataspace v1/v2; datatypes fixed-point,
+  IEEE float, fixed-length strings, variable-length strings (global heap, read only); layouts
+  compact / contiguous / chunked (v1 B-tree type 1, any depth); filters LZF (32000, native C++),
+  deflate (1) and shuffle (2) on read; attributes v1-v3.
+
+The writer streams chunked datasets to disk as their chunks fill (sequential appends, as the
+converter writes), buffers small datasets in memory, and lays out all metadata at close, then
+patches the superblock — so a crash leaves a file without a valid root, never a half-valid one.
+"""
+import os
+import struct
+import zlib
+
+import numpy as np
+
+from .._native import engine as _engine
+
+SIG = b"\x89HDF\r\n\x1a\n"
+UNDEF = 0xFFFFFFFFFFFFFFFF
+LZF_ID = 32000
+
+
+def _lzf_decompress(data, size):
+    return _engine().lzf_decompress(bytes(data), size)
+
+
+def _lzf_compress(data):
+    return _engine().lzf_compress(bytes(data))
+
+
+# ============================================================================ reading
+
+class _Dtype(object):
+    def __init__(self, np_dtype, vlen_str=False):
+        self.np = np_dtype
+        self.vlen_str = vlen_str
+
+
+def _parse_dtype(buf, off):
+    cv = buf[off]
+    cls, ver = cv & 0x0F, cv >> 4
+    b0, b1, b2 = buf[off + 1], buf[off + 2], buf[off + 3]
+    size = struct.unpack_from("<I", buf, off + 4)[0]
+    if cls == 0:  # fixed point
+        order = ">" if (b0 & 1) else "<"
+        signed = bool(b0 & 0x08)
+        return _Dtype(np.dtype("%s%s%d" % (order, "i" if signed else "u", size)))
+    if cls == 1:
+        order = ">" if (b0 & 1) else "<"
+        return _Dtype(np.dtype("%sf%d" % (order, size)))
+    if cls == 3:
+        return _Dtype(np.dtype("S%d" % size))
+    if cls == 9:  # variable length
+        vtype = b0 & 0x0F
+        if vtype == 1:  # string
+            return _Dtype(np.dtype(object), vlen_str=True)
+        raise NotImplementedError("variable-length sequences are not supported")
+    if cls == 8:  # enum (h5py bools) -> base type follows the properties
+        base = _parse_dtype(buf, off + 8)
+        return base
+    raise NotImplementedError("HDF5 datatype class %d not supported" % cls)
+
+
+class _Space(object):
+    def __init__(self, shape, maxshape):
+        self.shape = shape
+        self.maxshape = maxshape
+
+
+def _parse_space(buf, off, so=8, sl=8):
+    ver = buf[off]
+    rank = buf[off + 1]
+    flags = buf[off + 2]
+    if ver == 1:
+        p = off + 8
+    else:
+        stype = buf[off + 3]
+        p = off + 4
+        if stype == 0:
+            return _Space((), ())
+        if stype == 2:
+            return _Space(None, None)
+    dims = struct.unpack_from("<%dQ" % rank, buf, p)
+    p += 8 * rank
+    maxd = dims
+    if flags & 1:
+        maxd = tuple(None if v == UNDEF else v for v in struct.unpack_from("<%dQ" % rank, buf, p))
+    return _Space(tuple(dims), tuple(maxd))
+
+
+class Attributes(dict):
+    """dict of attribute name -> numpy value (read side) / value to write (write side)."""
+
+
+class _Reader(object):
+    def __init__(self, path):
+        with open(path, "rb") as f:
+            self.buf = f.read()
+        b = self.buf
+        base = b.find(SIG)
+        if base != 0:
+            raise IOError("not an HDF5 file (or user block unsupported): %s" % path)
+        ver = b[8]
+        if ver not in (0, 1):
+            raise NotImplementedError("superblock v%d not supported" % ver)
+        self.so, self.sl = b[13], b[14]
+        if self.so != 8 or self.sl != 8:
+            raise NotImplementedError("only 8-byte offsets/lengths supported")
+        p = 24 + (4 if ver == 1 else 0)
+        self.base, _, self.eof, _ = struct.unpack_from("<4Q", b, p)
+        p += 32
+        # root symbol table entry
+        self.root_ohdr = struct.unpack_from("<Q", b, p + 8)[0]
+        self._vlen_cache = {}
+
+    # --- object headers
+    def messages(self, addr):
+        b = self.buf
+        ver = b[addr]
+        if ver == 1:
+            nmsg = struct.unpack_from("<H", b, addr + 2)[0]
+            size = struct.unpack_from("<I", b, addr + 8)[0]
+            blocks = [(addr + 16, size)]
+            out = []
+            while blocks:
+                start, length = blocks.pop(0)
+                p = start
+                end = start + length
+                while p + 8 <= end:
+                    mtype, msize, mflags = struct.unpack_from("<HHB", b, p)
+                    data_off = p + 8
+                    if mtype == 0x10:
+                        caddr, clen = struct.unpack_from("<QQ", b, data_off)
+                        blocks.append((caddr, clen))
+                    elif mtype != 0:
+                        out.append((mtype, data_off, msize, mflags))
+                    p = data_off + msize
+            return out
+        if b[addr:addr + 4] == b"OHDR":
+            return self._messages_v2(addr)
+        raise NotImplementedError("object header version %d" % ver)
+
+    def _messages_v2(self, addr):
+        b = self.buf
+        flags = b[addr + 5]
+        p = addr + 6
+        if flags & 0x20:
+            p += 16
+        if flags & 0x10:
+            p += 4
+        szlen = 1 << (flags & 3)
+        size = int.from_bytes(b[p:p + szlen], "little")
+        p += szlen
+        blocks = [(p, size)]
+        out = []
+        track = bool(flags & 0x04)
+        while blocks:
+            start, length = blocks.pop(0)
+            q, end = start, start + length
+            while q + 4 <= end:
+                mtype = b[q]
+                msize = struct.unpack_from("<H", b, q + 1)[0]
+                mflags = b[q + 3]
+                q += 4 + (2 if track else 0)
+                if mtype == 0x10:
+                    caddr, clen = struct.unpack_from("<QQ", b, q)
+                    blocks.append((caddr + 4, clen - 8))  # skip OCHK sig, checksum
+                elif mtype != 0:
+                    out.append((mtype, q, msize, mflags))
+                q += msize
+        return out
+
+    # --- groups
+    def group_entries(self, ohdr):
+        """name -> object header address, for symbol-table and link-message groups."""
+        entries = {}
+        for mtype, off, size, _ in self.messages(ohdr):
+            if mtype == 0x11:
+                btree, heap = struct.unpack_from("<QQ", self.buf, off)
+                heap_data = self._local_heap(heap)
+                self._walk_group_btree(btree, heap_data, entries)
+            elif mtype == 0x06:
+                name, addr = self._parse_link(off)
+                if addr is not None:
+                    entries[name] = addr
+        return entries
+
+    def _parse_link(self, off):
+        b = self.buf
+        flags = b[off + 1]
+        p = off + 2
+        ltype = 0
+        if flags & 0x08:
+            ltype = b[p]
+            p += 1
+        if flags & 0x04:
+            p += 8
+        if flags & 0x10:
+            p += 1
+        lsz = 1 << (flags & 3)
+        nlen = int.from_bytes(b[p:p + lsz], "little")
+        p += lsz
+        name = b[p:p + nlen].decode("utf-8")
+        p += nlen
+        if ltype != 0:
+            return name, None
+        return name, struct.unpack_from("<Q", b, p)[0]
+
+    def _local_heap(self, addr):
+        b = self.buf
+        if b[addr:addr + 4] != b"HEAP":
+            raise IOError("bad local heap signature")
+        dsize, _, daddr = struct.unpack_from("<QQQ", b, addr + 8)
+        return b[daddr:daddr + dsize]
+
+    @staticmethod
+    def _cstr(heap, off):
+        end = heap.index(b"\x00", off)
+        return heap[off:end].decode("utf-8")
+
+    def _walk_group_btree(self, addr, heap, entries):
+        b = self.buf
+        if b[addr:addr + 4] != b"TREE":
+            raise IOError("bad group B-tree signature")
+        level = b[addr + 5]
+        used = struct.unpack_from("<H", b, addr + 6)[0]
+        p = addr + 24
+        for i in range(used):
+            child = struct.unpack_from("<Q", b, p + 8)[0]
+            p += 16
+            if level > 0:
+                self._walk_group_btree(child, heap, entries)
+            else:
+                self._read_snod(child, heap, entries)
+
+    def _read_snod(self, addr, heap, entries):
+        b = self.buf
+        if b[addr:addr + 4] != b"SNOD":
+            raise IOError("bad symbol node signature")
+        n = struct.unpack_from("<H", b, addr + 6)[0]
+        p = addr + 8
+        for _ in range(n):
+            name_off, ohdr = struct.unpack_from("<QQ", b, p)
+            entries[self._cstr(heap, name_off)] = ohdr
+            p += 40
+
+    # --- attributes
+    def attributes(self, ohdr):
+        out = Attributes()
+        b = self.buf
+        for mtype, off, size, _ in self.messages(ohdr):
+            if mtype != 0x0C:
+                continue
+            ver = b[off]
+            if ver == 1:
+                nlen, dlen, slen = struct.unpack_from("<HHH", b, off + 2)
+                p = off + 8
+                name = b[p:p + nlen].split(b"\x00")[0].decode("utf-8")
+                p += (nlen + 7) & ~7
+                dt = _parse_dtype(b, p)
+                p += (dlen + 7) & ~7
+                sp = _parse_space(b, p)
+                p += (slen + 7) & ~7
+            else:
+                nlen, dlen, slen = struct.unpack_from("<HHH", b, off + 2)
+                p = off + 8 + (1 if ver == 3 else 0)
+                name = b[p:p + nlen].split(b"\x00")[0].decode("utf-8")
+                p += nlen
+                dt = _parse_dtype(b, p)
+                p += dlen
+                sp = _parse_space(b, p)
+                p += slen
+            out[name] = self._decode_values(b, p, dt, sp.shape)
+        return out
+
+    def _decode_values(self, b, p, dt, shape):
+        n = int(np.prod(shape)) if shape else 1
+        if dt.vlen_str:
+            vals = []
+            for i in range(n):
+                length, gaddr, gidx = struct.unpack_from("<IQI", b, p + 16 * i)
+                vals.append(self._global_heap_obj(gaddr, gidx)[:length].decode("utf-8"))
+            arr = np.array(vals, dtype=object)
+        else:
+            arr = np.frombuffer(b, dtype=dt.np, count=n, offset=p).copy()
+        return arr.reshape(shape) if shape else arr[0]
+
+    def _global_heap_obj(self, addr, idx):
+        key = (addr, idx)
+        if key in self._vlen_cache:
+            return self._vlen_cache[key]
+        b = self.buf
+        if b[addr:addr + 4] != b"GCOL":
+            raise IOError("bad global heap signature")
+        csize = struct.unpack_from("<Q", b, addr + 8)[0]
+        p, end = addr + 16, addr + csize
+        while p + 16 <= end:
+            hidx, _, _, osize = struct.unpack_from("<HHIQ", b, p)
+            if hidx == 0:
+                break
+            data = b[p + 16:p + 16 + osize]
+            self._vlen_cache[(addr, hidx)] = data
+            p += 16 + ((osize + 7) & ~7)
+        return self._vlen_cache[key]
+
+
+class Dataset(object):
+    """Read-side dataset with numpy-style indexing along the first axis."""
+
+    def __init__(self, reader, ohdr, name):
+        self._r = reader
+        self.name = name
+        self._ohdr = ohdr
+        self.attrs = reader.attributes(ohdr)
+        b = reader.buf
+        self._filters = []
+        self._layout = None
+        for mtype, off, size, _ in reader.messages(ohdr):
+            if mtype == 0x01:
+                sp = _parse_space(b, off)
+                self.shape, self.maxshape = sp.shape, sp.maxshape
+            elif mtype == 0x03:
+                self._dt = _parse_dtype(b, off)
+            elif mtype == 0x08:
+                self._layout = self._parse_layout(b, off)
+            elif mtype == 0x0B:
+                self._filters = self._parse_filters(b, off)
+        self.dtype = self._dt.np
+        self._chunk_cache = {}
+        self._chunk_index = None
+
+    @staticmethod
+    def _parse_layout(b, off):
+        ver = b[off]
+        if ver == 3:
+            cls = b[off + 1]
+            if cls == 0:
+                size = struct.unpack_from("<H", b, off + 2)[0]
+                return ("compact", off + 4, size)
+            if cls == 1:
+                addr, size = struct.unpack_from("<QQ", b, off + 2)
+                return ("contiguous", addr, size)
+            if cls == 2:
+                nd = b[off + 2]
+                addr = struct.unpack_from("<Q", b, off + 3)[0]
+                dims = struct.unpack_from("<%dI" % nd, b, off + 11)
+                return ("chunked", addr, dims)
+        elif ver in (1, 2):
+            nd = b[off + 1]
+            cls = b[off + 2]
+            p = off + 8
+            addr = None
+            if cls != 0:
+                addr = struct.unpack_from("<Q", b, p)[0]
+                p += 8
+            dims = struct.unpack_from("<%dI" % nd, b, p)
+            p += 4 * nd
+            if cls == 1:
+                return ("contiguous", addr, None)
+            if cls == 2:
+                return ("chunked", addr, dims)
+            size = struct.unpack_from("<I", b, p)[0]
+            return ("compact", p + 4, size)
+        raise NotImplementedError("layout message version %d" % ver)
+
+    @staticmethod
+    def _parse_filters(b, off):
+        ver = b[off]
+        n = b[off + 1]
+        p = off + (8 if ver == 1 else 2)
+        out = []
+        for _ in range(n):
+            fid = struct.unpack_from("<H", b, p)[0]
+            if ver == 1 or fid >= 256:
+                nlen = struct.unpack_from("<H", b, p + 2)[0]
+                flags, ncd = struct.unpack_from("<HH", b, p + 4)
+                p += 8 + ((nlen + 7) & ~7 if ver == 1 else nlen)
+            else:
+                flags, ncd = struct.unpack_from("<HH", b, p + 2)
+                p += 6
+            cd = struct.unpack_from("<%dI" % ncd, b, p)
+            p += 4 * ncd
+            if ver == 1 and ncd % 2:
+                p += 4
+            out.append((fid, cd))
+        return out
+
+    def __len__(self):
+        return self.shape[0] if self.shape else 1
+
+    @property
+    def ndim(self):
+        return len(self.shape)
+
+    @property
+    def chunks(self):
+        if self._layout and self._layout[0] == "chunked":
+            return tuple(self._layout[2][:-1])
+        return None
+
+    # --- raw access
+    def _contiguous(self):
+        kind, a, s = self._layout
+        n = int(np.prod(self.shape)) if self.shape else 1
+        if kind == "compact":
+            return np.frombuffer(self._r.buf, dtype=self.dtype, count=n, offset=a)
+        if a == UNDEF:
+            return np.zeros(n, dtype=self.dtype)
+        return np.frombuffer(self._r.buf, dtype=self.dtype, count=n, offset=a)
+
+    def _index_chunks(self):
+        if self._chunk_index is not None:
+            return self._chunk_index
+        idx = {}
+        rank = len(self.shape)
+
+        def walk(addr):
+            b = self._r.buf
+            if b[addr:addr + 4] != b"TREE":
+                raise IOError("bad chunk B-tree signature")
+            level = b[addr + 5]
+            used = struct.unpack_from("<H", b, addr + 6)[0]
+            ksize = 8 + 8 * (rank + 1)
+            p = addr + 24
+            for _ in range(used):
+                csize, fmask = struct.unpack_from("<II", b, p)
+                offs = struct.unpack_from("<%dQ" % rank, b, p + 8)
+                child = struct.unpack_from("<Q", b, p + ksize)[0]
+                if level > 0:
+                    walk(child)
+                else:
+                    idx[offs] = (child, csize, fmask)
+                p += ksize + 8
+
+        if self._layout[1] != UNDEF:
+            walk(self._layout[1])
+        self._chunk_index = idx
+        return idx
+
+    def _read_chunk(self, offs):
+        hit = self._chunk_cache.get(offs)
+        if hit is not None:
+            return hit
+        cdims = self._layout[2][:-1]
+        n = int(np.prod(cdims))
+        ent = self._index_chunks().get(offs)
+        if ent is None:
+            arr = np.zeros(cdims, dtype=self.dtype)
+        else:
+            addr, csize, fmask = ent
+            data = self._r.buf[addr:addr + csize]
+            nbytes = n * self.dtype.itemsize
+            for k, (fid, cd) in reversed(list(enumerate(self._filters))):
+                if fmask & (1 << k):
+                    continue
+                if fid == LZF_ID:
+                    data = _lzf_decompress(data, nbytes)
+                elif fid == 1:
+                    data = zlib.decompress(data)
+                elif fid == 2:
+                    es = self.dtype.itemsize
+                    raw = np.frombuffer(data, dtype=np.uint8).reshape(es, -1)
+                    data = raw.T.copy().tobytes()
+                else:
+                    raise NotImplementedError("HDF5 filter %d not supported" % fid)
+            arr = np.frombuffer(data, dtype=self.dtype, count=n).reshape(cdims)
+        if len(self._chunk_cache) > 64:
+            self._chunk_cache.clear()
+        self._chunk_cache[offs] = arr
+        return arr
+
+    def _read_rows(self, start, stop):
+        """rows [start, stop) along axis 0 as an array."""
+        kind = self._layout[0]
+        shape = self.shape
+        if kind != "chunked":
+            full = self._contiguous().reshape(shape)
+            return np.array(full[start:stop])
+        cdims = self._layout[2][:-1]
+        out = np.empty((stop - start,) + tuple(shape[1:]), dtype=self.dtype)
+        c0 = cdims[0]
+        rest_chunks = [range(0, shape[d], cdims[d]) for d in range(1, len(shape))]
+        import itertools
+        for cs in range((start // c0) * c0, stop, c0):
+            lo, hi = max(start, cs), min(stop, cs + c0)
+            for rest in itertools.product(*rest_chunks):
+                offs = (cs,) + tuple(rest)
+                chunk = self._read_chunk(offs)
+                sl_out = [slice(lo - start, hi - start)]
+                sl_in = [slice(lo - cs, hi - cs)]
+                for d, r0 in enumerate(rest, start=1):
+                    e = min(shape[d], r0 + cdims[d])
+                    sl_out.append(slice(r0, e))
+                    sl_in.append(slice(0, e - r0))
+                out[tuple(sl_out)] = chunk[tuple(sl_in)]
+        return out
+
+    def __getitem__(self, key):
+        if key == () or key is Ellipsis:
+            if not self.shape:
+                v = self._scalar()
+                return v
+            return self._read_rows(0, self.shape[0])
+        if isinstance(key, (int, np.integer)):
+            k = int(key)
+            if k < 0:
+                k += self.shape[0]
+            if not 0 <= k < self.shape[0]:
+                raise IndexError(key)
+            return self._read_rows(k, k + 1)[0]
+        if isinstance(key, slice):
+            start, stop, step = key.indices(self.shape[0])
+            rows = self._read_rows(start, stop) if stop > start else \
+                np.empty((0,) + tuple(self.shape[1:]), self.dtype)
+            return rows[::step] if step != 1 else rows
+        if isinstance(key, tuple):
+            return self[key[0]][key[1:]] if len(key) > 1 else self[key[0]]
+        arr = np.asarray(key)
+        if arr.dtype == bool:
+            arr = np.nonzero(arr)[0]
+        return np.stack([self[int(i)] for i in arr]) if len(arr) else \
+            np.empty((0,) + tuple(self.shape[1:]), self.dtype)
+
+    def _scalar(self):
+        if self._dt.vlen_str:
+            kind, a, s = self._layout
+            b = self._r.buf
+            length, gaddr, gidx = struct.unpack_from("<IQI", b, a)
+            return self._r._global_heap_obj(gaddr, gidx)[:length].decode("utf-8")
+        v = self._contiguous()[0]
+        return v
+
+    def read_direct(self):
+        return self[()]
+
+
+class Group(object):
+    def __init__(self, reader, ohdr, name="/"):
+        self._r = reader
+        self._ohdr = ohdr
+        self.name = name
+        self._entries = reader.group_entries(ohdr)
+        self.attrs = reader.attributes(ohdr)
+
+    def keys(self):
+        return list(self._entries.keys())
+
+    def __iter__(self):
+        return iter(self._entries)
+
+    def __len__(self):
+        return len(self._entries)
+
+    def __contains__(self, name):
+        try:
+            self[name]
+            return True
+        except KeyError:
+            return False
+
+    def _is_group(self, ohdr):
+        return any(m[0] in (0x11, 0x06, 0x02) for m in self._r.messages(ohdr)) and not any(
+            m[0] == 0x08 for m in self._r.messages(ohdr))
+
+    def __getitem__(self, name):
+        parts = [p for p in name.split("/") if p]
+        node = self
+        for i, part in enumerate(parts):
+            if not isinstance(node, Group) or part not in node._entries:
+                raise KeyError(name)
+            addr = node._entries[part]
+            full = (node.name.rstrip("/") + "/" + part)
+            node = Group(self._r, addr, full) if node._is_group(addr) else \
+                Dataset(self._r, addr, full)
+        return node
+
+    def items(self):
+        return [(k, self[k]) for k in self.keys()]
+
+    def get(self, name, default=None):
+        try:
+            return self[name]
+        except KeyError:
+            return default
+
+
+class ReadFile(Group):
+    def __init__(self, path):
+        r = _Reader(path)
+        super(ReadFile, self).__init__(r, r.root_ohdr, "/")
+        self.filename = path
+
+    def close(self):
+        pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+# ============================================================================ writing
+
+def _align8(n):
+    return (n + 7) & ~7
+
+
+def _encode_dtype(dt):
+    dt = np.dtype(dt)
+    if dt.kind in "ui":
+        bits = 0x08 if dt.kind == "i" else 0x00
+        return (struct.pack("<B3BI", 0x10, bits, 0, 0, dt.itemsize) +
+                struct.pack("<HH", 0, dt.itemsize * 8))
+    if dt.kind == "f":
+        if dt.itemsize == 4:
+            sign, eloc, esz, msz, bias = 31, 23, 8, 23, 127
+        elif dt.itemsize == 8:
+            sign, eloc, esz, msz, bias = 63, 52, 11, 52, 1023
+        else:
+            sign, eloc, esz, msz, bias = 15, 10, 5, 10, 15
+        return (struct.pack("<B3BI", 0x11, 0x20, sign, 0, dt.itemsize) +
+                struct.pack("<HHBBBBI", 0, dt.itemsize * 8, eloc, esz, 0, msz, bias))
+    if dt.kind == "S":
+        return struct.pack("<B3BI", 0x13, 0x01, 0, 0, dt.itemsize)  # null-padded ASCII
+    if dt.kind == "b":
+        return _encode_dtype(np.uint8)
+    raise TypeError("cannot store dtype %s" % dt)
+
+
+def _encode_space(shape, maxshape=None):
+    rank = len(shape)
+    flags = 1 if maxshape is not None and rank else 0
+    out = struct.pack("<BBBB4x", 1, rank, flags, 0)
+    out += struct.pack("<%dQ" % rank, *shape)
+    if flags:
+        out += struct.pack("<%dQ" % rank, *[UNDEF if m is None else m for m in maxshape])
+    return out
+
+
+def _msg(mtype, data, flags=0):
+    data = data + b"\x00" * (_align8(len(data)) - len(data))
+    return struct.pack("<HHB3x", mtype, len(data), flags) + data
+
+
+def _to_storable(value):
+    if isinstance(value, str):
+        value = value.encode("utf-8")
+    if isinstance(value, bytes):
+        return np.array(value, dtype="S%d" % max(1, len(value)))
+    arr = np.asarray(value)
+    if arr.dtype.kind == "U":
+        arr = np.char.encode(arr, "utf-8")
+    if arr.dtype.kind == "O":
+        arr = np.array([str(v).encode("utf-8") for v in arr.ravel()]).reshape(arr.shape)
+    return arr
+
+
+class WDataset(object):
+    """Write-side dataset. Chunked datasets accept sequential row appends and stream to disk."""
+
+    def __init__(self, wfile, name, shape, dtype, maxshape=None, chunks=None, compression=None,
+                 data=None):
+        self._f = wfile
+        self.name = name
+        self.dtype = np.dtype(dtype)
+        self.shape = tuple(shape)
+        self.maxshape = tuple(maxshape) if maxshape is not None else None
+        self.chunks = tuple(chunks) if chunks else None
+        self.compression = compression
+        self.attrs = Attributes()
+        if compression not in (None, "lzf"):
+            raise NotImplementedError("only lzf compression is supported by h5lite")
+        if self.chunks is None:
+            self._data = np.zeros(self.shape, dtype=self.dtype) if data is None else \
+                np.array(data, dtype=self.dtype).reshape(self.shape)
+        else:
+            if any(c <= 0 for c in self.chunks):
+                raise ValueError("bad chunk shape")
+            if len(self.chunks) > 1 and tuple(self.chunks[1:]) != tuple(self.shape[1:]):
+                raise NotImplementedError("h5lite chunks must span all trailing dimensions")
+            self._row_shape = tuple(self.shape[1:])
+            self._pending = np.zeros((self.chunks[0],) + self._row_shape, dtype=self.dtype)
+            self._pending_start = 0      # first row index held in _pending
+            self._flushed = []           # (row_offset, addr, nbytes, filter_mask)
+            self._max_written = 0
+            if data is not None:
+                d = np.asarray(data, dtype=self.dtype)
+                for i in range(d.shape[0]):
+                    self[i] = d[i]
+
+    def __len__(self):
+        return self.shape[0]
+
+    def resize(self, shape):
+        shape = tuple(shape)
+        if self.chunks is None:
+            new = np.zeros(shape, dtype=self.dtype)
+            sl = tuple(slice(0, min(a, b)) for a, b in zip(shape, self.shape))
+            new[sl] = self._data[sl]
+            self._data = new
+        else:
+            if shape[1:] != self.shape[1:]:
+                raise NotImplementedError("only the first axis of a chunked dataset can grow")
+            if self.maxshape is not None and self.maxshape[0] is not None and \
+                    shape[0] > self.maxshape[0]:
+                raise ValueError("resize beyond maxshape")
+        self.shape = shape
+
+    def _flush_pending(self):
+        raw = self._pending.tobytes()
+        comp = _lzf_compress(raw) if self.compression == "lzf" else None
+        mask = 0
+        if self.compression == "lzf" and comp is None:
+            comp, mask = raw, 1  # incompressible: store raw with the filter skipped
+        data = comp if comp is not None else raw
+        addr = self._f._append_raw(data)
+        self._flushed.append((self._pending_start, addr, len(data), mask))
+        self._pending_start += self.chunks[0]
+        self._pending[...] = 0
+
+    def __setitem__(self, key, value):
+        if self.chunks is None:
+            self._data[key] = value
+            return
+        if isinstance(key, slice):
+            start, stop, _ = key.indices(self.shape[0])
+            value = np.asarray(value, dtype=self.dtype)
+            for i in range(start, stop):
+                self[i] = value[i - start]
+            return
+        i = int(key)
+        if i < self._pending_start:
+            raise NotImplementedError("h5lite chunked datasets are append-only (row %d)" % i)
+        while i >= self._pending_start + self.chunks[0]:
+            self._flush_pending()
+        self._pending[i - self._pending_start] = value
+        self._max_written = max(self._max_written, i + 1)
+
+    def __getitem__(self, key):
+        if self.chunks is None:
+            return self._data[key]
+        raise NotImplementedError("read chunked datasets after closing the file")
+
+    def _finish(self):
+        if self.chunks is not None:
+            nrows = self.shape[0]
+            if nrows > self._pending_start and self._max_written > self._pending_start:
+                self._flush_pending()
+
+
+class WGroup(object):
+    def __init__(self, wfile, name):
+        self._f = wfile
+        self.name = name
+        self._children = {}
+        self.attrs = Attributes()
+
+    def keys(self):
+        return list(self._children.keys())
+
+    def __contains__(self, name):
+        try:
+            self._lookup(name)
+            return True
+        except KeyError:
+            return False
+
+    def _lookup(self, name):
+        node = self
+        for part in [p for p in name.split("/") if p]:
+            if not isinstance(node, WGroup) or part not in node._children:
+                raise KeyError(name)
+            node = node._children[part]
+        return node
+
+    def __getitem__(self, name):
+        return self._lookup(name)
+
+    def _parent_of(self, name):
+        parts = [p for p in name.split("/") if p]
+        node = self
+        for part in parts[:-1]:
+            node = node.require_group(part)
+        return node, parts[-1]
+
+    def create_group(self, name):
+        parent, leaf = self._parent_of(name)
+        if leaf in parent._children:
+            raise ValueError("%s exists" % name)
+        g = WGroup(self._f, parent.name.rstrip("/") + "/" + leaf)
+        parent._children[leaf] = g
+        return g
+
+    def require_group(self, name):
+        try:
+            return self._lookup(name)
+        except KeyError:
+            return self.create_group(name)
+
+    def create_dataset(self, name, shape=None, dtype=None, data=None, maxshape=None, chunks=None,
+                       compression=None, **_):
+        if data is not None:
+            data = _to_storable(data)
+            shape = data.shape if shape is None else shape
+            dtype = data.dtype if dtype is None else dtype
+        parent, leaf = self._parent_of(name)
+        ds = WDataset(self._f, parent.name.rstrip("/") + "/" + leaf, shape, dtype, maxshape,
+                      chunks, compression, data)
+        parent._children[leaf] = ds
+        return ds
+
+    def require_dataset(self, name, shape, dtype, exact=False, **kw):
+        try:
+            return self._lookup(name)
+        except KeyError:
+            return self.create_dataset(name, shape=shape, dtype=dtype, **kw)
+
+    def __setitem__(self, name, value):
+        self.create_dataset(name, data=value)
+
+
+class WriteFile(WGroup):
+    """Streaming HDF5 writer. Use as a context manager or call close()."""
+
+    SUPERBLOCK = 96  # v0 superblock incl. root symbol table entry
+
+    def __init__(self, path):
+        super(WriteFile, self).__init__(self, "/")
+        self.filename = path
+        self._fh = open(path, "wb")
+        self._fh.write(b"\x00" * self.SUPERBLOCK)
+        self._pos = self.SUPERBLOCK
+        self._closed = False
+
+    def _append_raw(self, data):
+        addr = self._pos
+        self._fh.write(data)
+        self._pos += len(data)
+        pad = _align8(self._pos) - self._pos
+        if pad:
+            self._fh.write(b"\x00" * pad)
+            self._pos += pad
+        return addr
+
+    # --- metadata serialisation (allocation by appending)
+    def _attr_msgs(self, attrs):
+        out = []
+        for name, value in attrs.items():
+            arr = _to_storable(value)
+            nm = name.encode("utf-8") + b"\x00"
+            dt = _encode_dtype(arr.dtype)
+            sp = _encode_space(arr.shape)
+            body = struct.pack("<BBHHH", 1, 0, len(nm), len(dt), len(sp))
+            body += nm + b"\x00" * (_align8(len(nm)) - len(nm))
+            body += dt + b"\x00" * (_align8(len(dt)) - len(dt))
+            body += sp + b"\x00" * (_align8(len(sp)) - len(sp))
+            body += np.ascontiguousarray(arr).tobytes()
+            out.append(_msg(0x0C, body))
+        return out
+
+    def _object_header(self, msgs):
+        body = b"".join(msgs)
+        if not body:
+            body = _msg(0x00, b"")
+        hdr = struct.pack("<BBHII4x", 1, 0, len(msgs) if msgs else 1, 1, len(body))
+        return self._append_raw(hdr + body)
+
+    def _write_chunk_btree(self, ds):
+        rank = len(ds.shape)
+        K = 32  # indexed-storage internal node K (superblock v0 default)
+        cap = 2 * K
+        ksize = 8 + 8 * (rank + 1)
+        chunk0 = ds.chunks[0]
+        rest = tuple(ds.chunks[1:])
+        leaves = []
+        for (row, addr, nbytes, mask) in ds._flushed:
+            if row >= ds.shape[0]:
+                continue
+            leaves.append(((row,) + (0,) * (rank - 1), addr, nbytes, mask))
+        if not leaves:
+            return UNDEF
+
+        def key(offs, nbytes=0, mask=0):
+            return struct.pack("<II", nbytes, mask) + struct.pack("<%dQ" % (rank + 1),
+                                                                   *(tuple(offs) + (0,)))
+
+        def node(level, entries, right_key):
+            # entries: list of (left_key_bytes, child_addr)
+            body = struct.pack("<4sBBHQQ", b"TREE", 1, level, len(entries), UNDEF, UNDEF)
+            for k, child in entries:
+                body += k + struct.pack("<Q", child)
+            body += right_key
+            full = 24 + cap * (ksize + 8) + ksize
+            body += b"\x00" * (full - len(body))
+            return self._append_raw(body)
+
+        def right_of(offs):
+            return key((offs[0] + chunk0,) + tuple(o + r for o, r in zip(offs[1:], rest)))
+
+        level_nodes = []
+        for i in range(0, len(leaves), cap):
+            grp = leaves[i:i + cap]
+            ents = [(key(o, n, m), a) for (o, a, n, m) in grp]
+            addr = node(0, ents, right_of(grp[-1][0]))
+            level_nodes.append((grp[0][0], grp[-1][0], addr))
+        level = 0
+        while len(level_nodes) > 1:
+            level += 1
+            nxt = []
+            for i in range(0, len(level_nodes), cap):
+                grp = level_nodes[i:i + cap]
+                ents = [(key(first), addr) for (first, last, addr) in grp]
+                addr = node(level, ents, right_of(grp[-1][1]))
+                nxt.append((grp[0][0], grp[-1][1], addr))
+            level_nodes = nxt
+        return level_nodes[0][2]
+
+    def _write_dataset(self, ds):
+        ds._finish()
+        msgs = [_msg(0x01, _encode_space(ds.shape, ds.maxshape if ds.chunks else None)),
+                _msg(0x03, _encode_dtype(ds.dtype))]
+        # fill value (v2): alloc time late/incremental, write time if-set, undefined fill
+        msgs.append(_msg(0x05, struct.pack("<BBBB", 2, 3 if ds.chunks else 2, 2, 0)))
+        if ds.chunks is None:
+            raw = np.ascontiguousarray(ds._data).tobytes()
+            addr = self._append_raw(raw) if raw else UNDEF
+            msgs.append(_msg(0x08, struct.pack("<BBQQ", 3, 1, addr, len(raw))))
+        else:
+            bt = self._write_chunk_btree(ds)
+            dims = tuple(ds.chunks) + (ds.dtype.itemsize,)
+            msgs.append(_msg(0x08, struct.pack("<BBBQ", 3, 2, len(dims), bt) +
+                             struct.pack("<%dI" % len(dims), *dims)))
+            if ds.compression == "lzf":
+                nm = b"lzf\x00"
+                csz = int(np.prod(ds.chunks)) * ds.dtype.itemsize
+                cd = (4, 1, csz)
+                filt = struct.pack("<HHHH", LZF_ID, len(nm) + 4, 1, len(cd))  # optional filter
+                filt += nm + b"\x00" * 4 + struct.pack("<%dI" % len(cd), *cd) + b"\x00" * 4
+                msgs.append(_msg(0x0B, struct.pack("<BB6x", 1, 1) + filt))
+        msgs += self._attr_msgs(ds.attrs)
+        return self._object_header(msgs)
+
+    def _write_group(self, g):
+        child_addr = {}
+        for name, child in g._children.items():
+            child_addr[name] = self._write_group(child) if isinstance(child, WGroup) else \
+                self._write_dataset(child)
+        names = sorted(child_addr.keys(), key=lambda s: s.encode("utf-8"))
+        # local heap: "" at offset 0 then names
+        heap = b"\x00" * 8
+        offsets = {}
+        for n in names:
+            offsets[n] = len(heap)
+            e = n.encode("utf-8") + b"\x00"
+            heap += e + b"\x00" * (_align8(len(e)) - len(e))
+        heap_data = self._append_raw(heap)
+        heap_hdr = self._append_raw(struct.pack("<4sB3xQQQ", b"HEAP", 0, len(heap), UNDEF,
+                                                heap_data))
+        leafK, intK = 4, 16
+        snods = []
+        for i in range(0, max(1, len(names)), 2 * leafK):
+            chunk = names[i:i + 2 * leafK]
+            body = struct.pack("<4sBBH", b"SNOD", 1, 0, len(chunk))
+            for n in chunk:
+                body += struct.pack("<QQII16x", offsets[n], child_addr[n], 0, 0)
+            body += b"\x00" * (8 + 2 * leafK * 40 - len(body))
+            snods.append((chunk[-1] if chunk else None, self._append_raw(body)))
+        cap = 2 * intK
+
+        def node(level, children, first_key_off):
+            body = struct.pack("<4sBBHQQ", b"TREE", 0, level, len(children), UNDEF, UNDEF)
+            body += struct.pack("<Q", first_key_off)
+            for last_name, addr in children:
+                body += struct.pack("<QQ", addr, offsets.get(last_name, 0) if last_name else 0)
+            full = 24 + cap * 16 + 8
+            body += b"\x00" * (full - len(body))
+            return self._append_raw(body)
+
+        level_nodes = []
+        for i in range(0, len(snods), cap):
+            grp = snods[i:i + cap]
+            level_nodes.append((grp[-1][0], node(0, grp, 0)))
+        level = 0
+        while len(level_nodes) > 1:
+            level += 1
+            nxt = []
+            for i in range(0, len(level_nodes), cap):
+                grp = level_nodes[i:i + cap]
+                nxt.append((grp[-1][0], node(level, grp, 0)))
+            level_nodes = nxt
+        btree = level_nodes[0][1]
+        msgs = [_msg(0x11, struct.pack("<QQ", btree, heap_hdr))] + self._attr_msgs(g.attrs)
+        addr = self._object_header(msgs)
+        if g is self:
+            self._root_btree, self._root_heap = btree, heap_hdr
+        return addr
+
+    def close(self):
+        if self._closed:
+            return
+        root = self._write_group(self)
+        eof = self._pos
+        sb = SIG + struct.pack("<BBBBBBBBHHI", 0, 0, 0, 0, 0, 8, 8, 0, 4, 16, 0)
+        sb += struct.pack("<QQQQ", 0, UNDEF, eof, UNDEF)
+        sb += struct.pack("<QQII", 0, root, 1, 0) + struct.pack("<QQ", self._root_btree,
+                                                                self._root_heap)
+        assert len(sb) == self.SUPERBLOCK
+        self._fh.seek(0)
+        self._fh.write(sb)
+        self._fh.close()
+        self._closed = True
+
+    def flush(self):
+        pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, exc_type, *a):
+        if exc_type is None:
+            self.close()
+        else:
+            self._fh.close()
+            self._closed = True
+
+
+def File(path, mode="r"):
+    """h5py-style entry point: mode 'r' reads, 'w' writes (truncates)."""
+    if mode in ("r", None):
+        return ReadFile(path)
+    if mode == "w":
+        return WriteFile(path)
+    if mode in ("a", "r+") and not os.path.exists(path):
+        return WriteFile(path)
+    raise NotImplementedError("h5lite supports modes 'r' and 'w'")

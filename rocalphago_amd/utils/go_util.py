@@ -81,7 +81,15 @@ def sgf_iter_states(sgf_string, include_end=True):
                 move = _parse_sgf_move(props['B'][0])
                 player = go.BLACK
             else:
-                continue  # comment / setup-only node
+                # setup node (e.g. the ';AB[..]' handicap node our own writer emits, like the
+                # reference's save_gamestate_to_sgf): AB before any move = handicap stones
+                if 'AB' in props and len(gs.history) == 0 and 'AW' not in props:
+                    gs.place_handicaps(_expand_point_list(props['AB']))
+                else:
+                    for key, color in (('AB', go.BLACK), ('AW', go.WHITE)):
+                        for stone in _expand_point_list(props.get(key, [])):
+                            gs.do_move(stone, color)
+                continue
             yield (gs, move, player)
             gs.do_move(move, player)
     if include_end:
