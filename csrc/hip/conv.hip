@@ -171,8 +171,8 @@ template <int KS, int NTN, int NTC>
 __global__ void __launch_bounds__(256, 1)
 conv_wgrad_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
                   float* __restrict__ part, float* __restrict__ bpart, int M, int S, int WI,
-                  int shift, int WG, int GC, int CIN, int steps_per_chunk, int COUTP, int CINP,
-                  int ntile_c) {
+                  int shift, int WG, int HG, int GC, int CIN, int steps_per_chunk, int COUTP,
+                  int CINP, int ntile_c) {
   constexpr int BNN = 32 * NTN, BNC = 32 * NTC;
   constexpr int WNN = 16 * NTN, WNC = 16 * NTC;
   constexpr int GROW = BNN, XROW = BNC;  // elements per LDS row
@@ -205,7 +205,7 @@ conv_wgrad_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
       if (m < M) {
         const int b = m / S2, rem = m - (m / S2) * S2;
         const int pi = rem / S, pj = rem - (rem / S) * S;
-        src = (size_t)((b * WG + pi + 1) * WG + pj + 1) * GC + n0 + ch * 8;
+        src = (size_t)((b * WG + pi + HG) * WG + pj + HG) * GC + n0 + ch * 8;
       }
       glds16(G + src, lg + k * 512);
     }
@@ -484,12 +484,12 @@ RAG_API size_t rag_conv_wgrad_workspace(int B, int S, int COUTP, int CINP, int K
 template <int KS>
 static void launch_wgrad_ks(int ntn, int ntc, dim3 grid, hipStream_t st, const bf16* G,
                             const bf16* X, float* part, float* bpart, int M, int S, int WI,
-                            int shift, int WG, int GC, int CIN, int spc, int COUTP, int CINP,
-                            int ntile_c) {
+                            int shift, int WG, int HG, int GC, int CIN, int spc, int COUTP,
+                            int CINP, int ntile_c) {
 #define RAG_WG(A, C)                                                                          \
   if (ntn == A && ntc == C) {                                                                 \
     conv_wgrad_kernel<KS, A, C><<<grid, 256, 0, st>>>(G, X, part, bpart, M, S, WI, shift, WG, \
-                                                      GC, CIN, spc, COUTP, CINP, ntile_c);   \
+                                                      HG, GC, CIN, spc, COUTP, CINP, ntile_c);\
     return;                                                                                   \
   }
   RAG_WG(6, 3) RAG_WG(6, 2) RAG_WG(6, 1) RAG_WG(4, 3) RAG_WG(4, 2) RAG_WG(4, 1)
@@ -500,8 +500,8 @@ static void launch_wgrad_ks(int ntn, int ntc, dim3 grid, hipStream_t st, const b
 // Weight + bias gradient. G: dL/d(pre-activation) in padded layout (halo 1, GC channels).
 // X: the layer input (halo HI, CINP channels). dW: OIHW fp32 [COUT][CIN][KS][KS]. db: [COUT].
 RAG_API int rag_conv_wgrad(const void* G, const void* X, float* dW, float* db, float* work,
-                           int B, int S, int HI, int GC, int COUT, int COUTP, int CIN, int CINP,
-                           int KS, int accumulate, hipStream_t stream) {
+                           int B, int S, int HI, int HG, int GC, int COUT, int COUTP, int CIN,
+                           int CINP, int KS, int accumulate, hipStream_t stream) {
   if (COUTP % 32 || CINP % 32) return -1;
   int nchunks = 1;
   rag_conv_wgrad_workspace(B, S, COUTP, CINP, KS, &nchunks);
@@ -515,14 +515,14 @@ RAG_API int rag_conv_wgrad(const void* G, const void* X, float* dW, float* db, f
   float* part = work;
   float* bpart = db ? work + (size_t)nchunks * taps * COUTP * CINP : nullptr;
   dim3 grid(nchunks, ntile_n * ntile_c, taps);
-  const int WI = S + 2 * HI, shift = HI - KS / 2, WG = S + 2;
+  const int WI = S + 2 * HI, shift = HI - KS / 2, WG = S + 2 * HG;
   const bf16* g = (const bf16*)G;
   const bf16* x = (const bf16*)X;
   switch (KS) {
-    case 1: launch_wgrad_ks<1>(ntn, ntc, grid, stream, g, x, part, bpart, M, S, WI, shift, WG, GC, CINP, spc, COUTP, CINP, ntile_c); break;
-    case 3: launch_wgrad_ks<3>(ntn, ntc, grid, stream, g, x, part, bpart, M, S, WI, shift, WG, GC, CINP, spc, COUTP, CINP, ntile_c); break;
-    case 5: launch_wgrad_ks<5>(ntn, ntc, grid, stream, g, x, part, bpart, M, S, WI, shift, WG, GC, CINP, spc, COUTP, CINP, ntile_c); break;
-    case 7: launch_wgrad_ks<7>(ntn, ntc, grid, stream, g, x, part, bpart, M, S, WI, shift, WG, GC, CINP, spc, COUTP, CINP, ntile_c); break;
+    case 1: launch_wgrad_ks<1>(ntn, ntc, grid, stream, g, x, part, bpart, M, S, WI, shift, WG, HG, GC, CINP, spc, COUTP, CINP, ntile_c); break;
+    case 3: launch_wgrad_ks<3>(ntn, ntc, grid, stream, g, x, part, bpart, M, S, WI, shift, WG, HG, GC, CINP, spc, COUTP, CINP, ntile_c); break;
+    case 5: launch_wgrad_ks<5>(ntn, ntc, grid, stream, g, x, part, bpart, M, S, WI, shift, WG, HG, GC, CINP, spc, COUTP, CINP, ntile_c); break;
+    case 7: launch_wgrad_ks<7>(ntn, ntc, grid, stream, g, x, part, bpart, M, S, WI, shift, WG, HG, GC, CINP, spc, COUTP, CINP, ntile_c); break;
     default: return -2;
   }
   const int total = COUT * CIN * taps + COUT;

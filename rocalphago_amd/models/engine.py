@@ -1,0 +1,216 @@
+"""HIP network engine: the GPU execution path of the convolutional policy / value networks.
+
+A ``HipTrunk`` executes a sequential stack of 'same' convolutions (+bias, optional ReLU) on
+preallocated padded channels-last bf16 activations (layout: csrc/hip/conv.hip), with
+
+  * forward    : one implicit-GEMM MFMA launch per layer (bias + ReLU fused in the epilogue)
+  * backward   : per layer one wgrad launch (+ slab reduce) and one dgrad launch whose epilogue
+                 applies the ReLU derivative of the layer below (so no separate mask pass)
+  * weights    : fp32 OIHW master parameters (views of one flat buffer owned by the model) are
+                 repacked to the two bf16 GEMM layouts only when they change.
+
+Heads: ``PolicyHeadEngine`` (1x1 conv -> per-position Bias -> softmax, with the cross-entropy /
+REINFORCE loss fused into the same kernel) and ``ValueHeadEngine`` (1x1 conv on HIP, then the two
+dense layers as plain library GEMMs — hipBLASLt via torch.matmul — and tanh).
+
+No autograd graph is built on the hot path; ``models/kerasish.py`` exposes these engines through
+torch.autograd.Function wrappers for generic use and calls ``train_step`` directly for speed.
+"""
+import torch
+
+from ..ops import hipops as ops
+
+
+class ConvSpec(object):
+    __slots__ = ("ks", "cin", "cout", "relu", "cinp", "coutp", "halo_in", "bias")
+
+    def __init__(self, ks, cin, cout, relu, bias=True):
+        self.ks, self.cin, self.cout, self.relu, self.bias = ks, cin, cout, relu, bias
+        self.cinp, self.coutp = ops.pad_channels(cin), ops.pad_channels(cout)
+        self.halo_in = max(1, ks // 2)
+
+
+class HipTrunk(object):
+    def __init__(self, specs, board, device):
+        assert specs, "empty trunk"
+        self.specs = specs
+        self.S = board
+        self.device = device
+        self.L = len(specs)
+        for a, b in zip(specs[:-1], specs[1:]):
+            assert a.cout == b.cin, "channel mismatch in trunk"
+        self._B = 0
+        self.acts = []
+        self._gbufs = {}
+        self._wf = [None] * self.L
+        self._wb = [None] * self.L
+        self._bias = [torch.zeros(s.coutp, device=device) for s in specs]
+        self._packed_version = None
+        self._work = None
+
+    # ------------------------------------------------------------------ buffers
+    def _halos(self):
+        """halo[b] of activation boundary b (acts[b] and the gradient g_{b-1} share it, so the
+        dgrad epilogue can read its ReLU mask in the output layout)."""
+        sp = self.specs
+        h = [max(1, sp[0].ks // 2)]
+        for b in range(1, self.L):
+            h.append(max(1, sp[b].ks // 2, sp[b - 1].ks // 2 if b - 1 >= 1 else 0))
+        assert self.L == 1 or sp[-1].ks <= 3, "last trunk layer must be 1x1 or 3x3"
+        h.append(1)
+        return h
+
+    def ensure_batch(self, B):
+        if B <= self._B:
+            return
+        B = max(B, 1)
+        S = self.S
+        self.halo = self._halos()
+        acts = [ops.alloc_padded(B, S, self.halo[0], self.specs[0].cinp, self.device)]
+        for l, s in enumerate(self.specs):
+            acts.append(ops.alloc_padded(B, S, self.halo[l + 1], s.coutp, self.device))
+        self.acts = acts
+        self._gbufs = {}
+        for l, s in enumerate(self.specs):
+            key = (s.coutp, self.halo[l + 1])
+            if key not in self._gbufs:
+                self._gbufs[key] = [ops.alloc_padded(B, S, key[1], key[0], self.device)
+                                    for _ in range(2)]
+        self._B = B
+        need = 0
+        for s in self.specs:
+            need = max(need, ops._lib().rag_conv_wgrad_workspace(B, S, s.coutp, s.cinp, s.ks,
+                                                                 None))
+        self._work = torch.empty(need + 1024, dtype=torch.float32, device=self.device)
+
+    def input_buffer(self, B):
+        self.ensure_batch(B)
+        return self.acts[0][:B]
+
+    def output(self, B):
+        return self.acts[-1][:B]
+
+    def grad_buffer(self, l, which, B):
+        """g_l = dL/d(pre-activation of layer l), halo of boundary l+1."""
+        s = self.specs[l]
+        return self._gbufs[(s.coutp, self.halo[l + 1])][which][:B]
+
+    # ------------------------------------------------------------------ weights
+    def sync_weights(self, weights, biases, version):
+        """Repack bf16 GEMM layouts from fp32 OIHW masters when ``version`` changed."""
+        if version == self._packed_version:
+            return
+        for l, s in enumerate(self.specs):
+            taps = s.ks * s.ks
+            if self._wf[l] is None:
+                self._wf[l] = torch.empty((taps, s.coutp, s.cinp), dtype=torch.bfloat16,
+                                          device=self.device)
+                self._wb[l] = torch.empty((taps, s.cinp, s.coutp), dtype=torch.bfloat16,
+                                          device=self.device)
+            ops.pack_weights(weights[l], s.coutp, s.cinp, self._wf[l], self._wb[l])
+            if biases[l] is not None:
+                self._bias[l][:s.cout].copy_(biases[l])
+        self._packed_version = version
+
+    # ------------------------------------------------------------------ compute
+    def forward(self, B):
+        S = self.S
+        for l, s in enumerate(self.specs):
+            x, y = self.acts[l][:B], self.acts[l + 1][:B]
+            ops.conv_igemm(x, self._wf[l], self._bias[l], y, B, S, self.halo[l],
+                           self.halo[l + 1], s.cinp, s.coutp, s.ks, s.relu)
+        return self.acts[-1][:B]
+
+    def backward(self, B, dws, dbs, top_which=0, accumulate=False, on_layer_done=None):
+        """Backprop from grad_buffer(L-1, top_which) (= dL/d pre-activation of the last layer,
+        already ReLU-masked) down to the first layer; writes fp32 OIHW grads into dws/dbs.
+        ``on_layer_done(l)`` fires right after layer l's wgrad is queued (DP bucket overlap)."""
+        S = self.S
+        which = top_which
+        for l in range(self.L - 1, -1, -1):
+            s = self.specs[l]
+            g = self.grad_buffer(l, which, B)
+            x = self.acts[l][:B]
+            ops.conv_wgrad(g, x, dws[l], dbs[l], B, S, self.halo[l], s.cout, s.coutp, s.cin,
+                           s.cinp, s.ks, accumulate=accumulate, work=self._work,
+                           hg=self.halo[l + 1])
+            if on_layer_done is not None:
+                on_layer_done(l)
+            if l > 0:
+                below = self.specs[l - 1]
+                which ^= 1
+                gout = self.grad_buffer(l - 1, which, B)
+                ops.conv_igemm(g, self._wb[l], None, gout, B, S, self.halo[l + 1],
+                               self.halo[l], s.coutp, s.cinp, s.ks, False,
+                               mask=x if below.relu else None)
+
+
+class PolicyHeadEngine(object):
+    """1x1 conv (K->1, scalar bias) -> Flatten -> per-position Bias -> softmax."""
+
+    def __init__(self, trunk, K):
+        self.trunk = trunk
+        self.K = K
+        self.S = trunk.S
+        self._B = 0
+
+    def ensure(self, B):
+        if B <= self._B:
+            return
+        dev = self.trunk.device
+        S2 = self.S * self.S
+        self.probs = torch.empty((B, S2), device=dev)
+        self.dz = torch.empty((B, S2), device=dev)
+        self.loss = torch.empty((B,), device=dev)
+        self.hit = torch.empty((B,), device=dev)
+        self._B = B
+
+    def forward(self, B, w, b0, pbias, labels=None, sweight=None, mode=0, gscale=1.0):
+        self.ensure(B)
+        h = self.trunk.output(B)
+        ops.policy_head_fwd(h, w, b0, pbias, self.probs[:B], self.K, labels=labels,
+                            sweight=sweight, loss=self.loss[:B] if mode else None,
+                            dz=self.dz[:B] if mode else None, hit=self.hit[:B] if mode else None,
+                            mode=mode, gscale=gscale)
+        return self.probs[:B]
+
+    def backward(self, B, w, dz, dw, db0, dpbias):
+        """dz [B, S*S] -> head param grads + trunk top gradient (ReLU-masked) in grad buffer 0."""
+        h = self.trunk.output(B)
+        L = self.trunk.L
+        dh = self.trunk.grad_buffer(L - 1, 0, B)
+        dw.zero_()
+        db0.zero_()
+        dpbias.zero_()
+        ops.head_bwd(h, w, dz, dh, dw, db0, dpbias, self.K,
+                     relu_mask=self.trunk.specs[-1].relu)
+
+
+class ValueHeadEngine(object):
+    """1x1 conv (K->1) on HIP; Dense(S*S->H) + act; Dense(H->1) + tanh via torch GEMMs."""
+
+    def __init__(self, trunk, K):
+        self.trunk = trunk
+        self.K = K
+        self.S = trunk.S
+        self._B = 0
+
+    def ensure(self, B):
+        if B <= self._B:
+            return
+        self.z = torch.empty((B, self.S * self.S), device=self.trunk.device)
+        self._B = B
+
+    def conv_out(self, B, w, b0):
+        self.ensure(B)
+        ops.head_linear(self.trunk.output(B), w, b0, self.z[:B], self.K)
+        return self.z[:B]
+
+    def backward_conv(self, B, w, dz, dw, db0):
+        h = self.trunk.output(B)
+        L = self.trunk.L
+        dh = self.trunk.grad_buffer(L - 1, 0, B)
+        dw.zero_()
+        db0.zero_()
+        ops.head_bwd(h, w, dz.contiguous(), dh, dw, db0, None, self.K,
+                     relu_mask=self.trunk.specs[-1].relu)

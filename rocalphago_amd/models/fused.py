@@ -1,0 +1,220 @@
+"""Fused HIP execution plans for the two flagship architectures.
+
+``detect_plan`` pattern-matches a kerasish Sequential model:
+
+  PolicyPlan:  [Conv2D 'same' (+ReLU)]* -> Conv2D 1x1 (1 filter, linear) -> Flatten -> Bias ->
+               Activation(softmax)                      (CNNPolicy, reference policy.py:96-136)
+  ValuePlan:   [Conv2D 'same' (+ReLU)]* -> Conv2D 1x1 (1 filter) -> Flatten -> Dense(H) ->
+               Dense(1, tanh)                          (CNNValue / reference value.py:14-28)
+
+and executes them on the HIP engine (models/engine.py): one packed-input kernel (uint8 or fp32
+planes, optional gather + dihedral transform), one MFMA conv launch per layer, the fused head
+(softmax + loss + dL/dz in one kernel), per-layer wgrad/dgrad, with gradients written straight
+into the model's flat fp32 gradient buffer (ready for one all-reduce and the fused SGD kernel).
+"""
+import torch
+
+from ..ops import hipops as ops
+from .engine import ConvSpec, HipTrunk, PolicyHeadEngine, ValueHeadEngine
+
+
+def _conv_ok(ld):
+    c = ld.config
+    return (ld.class_name == "Convolution2D" and c.get("border_mode") == "same" and
+            c["nb_row"] == c["nb_col"] and c["nb_row"] % 2 == 1 and
+            tuple(c.get("subsample", (1, 1))) == (1, 1) and
+            c.get("activation", "linear") in ("relu", "linear"))
+
+
+def detect_plan(model):
+    if model.functional:
+        return None
+    L = model.layers
+    n = 0
+    while n < len(L) and L[n].class_name == "Convolution2D":
+        n += 1
+    if n < 2 or not all(_conv_ok(ld) for ld in L[:n]):
+        return None
+    head = L[n - 1]
+    if head.config["nb_filter"] != 1 or head.config["nb_row"] != 1 or \
+            head.config.get("activation", "linear") != "linear":
+        return None
+    if L[n - 2].config["nb_row"] > 3:
+        return None
+    rest = [ld.class_name for ld in L[n:]]
+    S = model.input_shape[-1]
+    if S > 25 or model.input_shape[-2] != S:
+        return None
+    if rest == ["Flatten", "Bias", "Activation"] and L[-1].config["activation"] == "softmax":
+        return PolicyPlan(model, L[:n - 1], head, L[n + 1])
+    if rest == ["Flatten", "Dense", "Dense"] and L[-1].config["output_dim"] == 1 and \
+            L[-1].config.get("activation") == "tanh" and \
+            L[n + 1].config.get("activation", "linear") in ("relu", "linear", "tanh"):
+        return ValuePlan(model, L[:n - 1], head, L[n + 1], L[n + 2])
+    return None
+
+
+class _TrunkPlan(object):
+    def __init__(self, model, convs, head_conv):
+        net = model.net
+        self.model = model
+        self.net = net
+        specs = []
+        for ld in convs:
+            W = net.params_of(ld.name)[0]
+            specs.append(ConvSpec(ld.config["nb_row"], W.shape[1], W.shape[0],
+                                  ld.config.get("activation", "linear") == "relu"))
+        self.S = model.input_shape[-1]
+        self.trunk = HipTrunk(specs, self.S, net.device)
+        self.conv_names = [ld.name for ld in convs]
+        self.head_name = head_conv.name
+        self.K = specs[-1].cout
+
+    def _params(self):
+        Ws, bs = [], []
+        for name in self.conv_names:
+            p = self.net.params_of(name)
+            Ws.append(p[0])
+            bs.append(p[1] if len(p) > 1 else None)
+        return Ws, bs
+
+    def _grads(self):
+        dWs, dbs = [], []
+        for name in self.conv_names:
+            g = self.net.grads_of(name)
+            dWs.append(g[0])
+            dbs.append(g[1] if len(g) > 1 else None)
+        return dWs, dbs
+
+    def prepare(self, x, index=None, transforms=None):
+        """Pack input planes [N, F, S, S] (uint8 or fp32, on device) into the trunk input."""
+        B = x.shape[0] if index is None else index.shape[0]
+        self.trunk.ensure_batch(B)
+        Ws, bs = self._params()
+        self.trunk.sync_weights(Ws, bs, self.net.weights_version())
+        if x.dtype not in (torch.uint8, torch.float32):
+            x = x.float()
+        ops.pack_input(x.contiguous(), self.trunk.input_buffer(B), self.trunk.halo[0],
+                       index=index, transforms=transforms)
+        return B
+
+    def head_params(self):
+        p = self.net.params_of(self.head_name)
+        w = p[0].reshape(-1)
+        b0 = p[1] if len(p) > 1 else None
+        return w, b0
+
+    def head_grads(self):
+        g = self.net.grads_of(self.head_name)
+        return g[0].reshape(-1), (g[1] if len(g) > 1 else torch.zeros(1, device=self.net.device))
+
+
+class PolicyPlan(_TrunkPlan):
+    def __init__(self, model, convs, head_conv, bias_layer):
+        super(PolicyPlan, self).__init__(model, convs, head_conv)
+        self.bias_name = bias_layer.name
+        self.head = PolicyHeadEngine(self.trunk, self.K)
+
+    def forward(self, x, index=None, transforms=None):
+        B = self.prepare(x, index, transforms)
+        self.trunk.forward(B)
+        w, b0 = self.head_params()
+        pb = self.net.params_of(self.bias_name)[0]
+        return self.head.forward(B, w, b0, pb).clone()
+
+    @staticmethod
+    def loss_mode(loss):
+        if loss == "categorical_crossentropy":
+            return 1
+        return getattr(loss, "_rag_head_mode", None)
+
+    def train_step(self, x, y, loss, sw=None, want_acc=False, labels=None, index=None,
+                   transforms=None):
+        mode = self.loss_mode(loss)
+        if mode is None:
+            return None
+        if labels is None:
+            # one-hot targets only (the reference's CE / REINFORCE targets); else generic path
+            if not bool(((y.sum(1) == 1) & (y.max(1).values == 1)).all()):
+                return None
+            labels = y.argmax(1)
+        B = self.prepare(x, index, transforms)
+        norm = 1.0
+        if sw is not None:
+            norm = float((sw != 0).float().mean().clamp_min(1e-12))
+        self.fwd_bwd(B, labels, sw, mode, 1.0 / (B * norm))
+        lossv = float(self.head.loss[:B].mean()) / norm
+        acc = float(self.head.hit[:B].mean()) if want_acc else None
+        return lossv, acc
+
+    def fwd_bwd(self, B, labels, sw, mode, gscale, on_layer_grads=None):
+        """Forward + fused loss + full backward into net.flat_grad (no host syncs)."""
+        self.trunk.forward(B)
+        w, b0 = self.head_params()
+        pb = self.net.params_of(self.bias_name)[0]
+        self.head.forward(B, w, b0, pb, labels=labels, sweight=sw, mode=mode, gscale=gscale)
+        dw, db0 = self.head_grads()
+        dpb = self.net.grads_of(self.bias_name)[0]
+        self.head.backward(B, w, self.head.dz[:B], dw, db0, dpb)
+        dWs, dbs = self._grads()
+        self.trunk.backward(B, dWs, dbs, on_layer_done=on_layer_grads)
+
+    def layer_offsets(self):
+        """Start offset (elements) of each trunk conv layer's params in net.flat."""
+        base = self.net.flat.data_ptr()
+        return [(self.net.params_of(n)[0].data_ptr() - base) // 4 for n in self.conv_names]
+
+
+class ValuePlan(_TrunkPlan):
+    def __init__(self, model, convs, head_conv, dense1, dense2):
+        super(ValuePlan, self).__init__(model, convs, head_conv)
+        self.d1, self.d2 = dense1.name, dense2.name
+        self.act1 = dense1.config.get("activation", "linear")
+        self.head = ValueHeadEngine(self.trunk, self.K)
+
+    def _mlp(self, z, params):
+        W1, b1, W2, b2 = params
+        h = z @ W1 + b1
+        if self.act1 == "relu":
+            h = torch.relu(h)
+        elif self.act1 == "tanh":
+            h = torch.tanh(h)
+        return torch.tanh(h @ W2 + b2)
+
+    def _dense_params(self):
+        return self.net.params_of(self.d1) + self.net.params_of(self.d2)
+
+    def forward(self, x, index=None, transforms=None):
+        B = self.prepare(x, index, transforms)
+        self.trunk.forward(B)
+        w, b0 = self.head_params()
+        z = self.head.conv_out(B, w, b0)
+        return self._mlp(z, self._dense_params())
+
+    def train_step(self, x, y, loss, sw=None, want_acc=False, index=None, transforms=None):
+        if loss not in ("mse", "mean_squared_error"):
+            return None
+        B = self.prepare(x, index, transforms)
+        lossv = self.fwd_bwd(B, y.reshape(B, -1), sw)
+        return float(lossv), None
+
+    def fwd_bwd(self, B, y, sw=None):
+        self.trunk.forward(B)
+        w, b0 = self.head_params()
+        z = self.head.conv_out(B, w, b0).detach().requires_grad_()
+        params = [p.detach().requires_grad_() for p in self._dense_params()]
+        v = self._mlp(z, params)
+        per = ((v - y) ** 2).mean(-1)
+        if sw is not None:
+            per = per * sw / (sw != 0).float().mean().clamp_min(1e-12)
+        lossv = per.mean()
+        grads = torch.autograd.grad(lossv, [z] + params)
+        dg = self.net.grads_of(self.d1) + self.net.grads_of(self.d2)
+        with torch.no_grad():
+            for gv, g in zip(dg, grads[1:]):
+                gv.copy_(g)
+        dw, db0 = self.head_grads()
+        self.head.backward_conv(B, w, grads[0], dw, db0)
+        dWs, dbs = self._grads()
+        self.trunk.backward(B, dWs, dbs)
+        return lossv.detach()

@@ -1,0 +1,93 @@
+"""NeuralNetBase, the @neuralnet registry and the Bias layer — reference AlphaGo/models/nn_util.py.
+
+``save_model`` writes the reference JSON spec ``{class, keras_model, feature_list[, weights_file]}``
+(nn_util.py:85-108) and ``load_model`` reads it back, rebuilding the network from the embedded
+Keras-1 JSON through our kerasish interpreter (nn_util.py:60-83).
+"""
+import json
+import os
+
+from ..features.preprocessing import Preprocess
+from . import kerasish
+
+
+class NeuralNetBase(object):
+    """Base class: feature preprocessing + a network built by the subclass' create_network."""
+
+    subclasses = {}
+
+    def __init__(self, feature_list, **kwargs):
+        self.preprocessor = Preprocess(feature_list)
+        kwargs["input_dim"] = self.preprocessor.output_dim
+        if kwargs.get('init_network', True):
+            self.model = self.__class__.create_network(**kwargs)
+            self.forward = self._model_forward()
+
+    def _model_forward(self):
+        """np/tensor batch (B, F, S, S) -> network output as numpy (learning phase = test)."""
+        model = self.model
+        return lambda inpt: model.predict(inpt)
+
+    @staticmethod
+    def load_model(json_file, device=None):
+        with open(json_file, 'r') as f:
+            object_specs = json.load(f)
+        class_name = object_specs.get('class', 'CNNPolicy')
+        try:
+            network_class = NeuralNetBase.subclasses[class_name]
+        except KeyError:
+            raise ValueError("Unknown neural network type in json file: {}\n"
+                             "(was it registered with the @neuralnet decorator?)"
+                             .format(class_name))
+        new_net = network_class(object_specs['feature_list'], init_network=False)
+        new_net.model = kerasish.model_from_json(object_specs['keras_model'],
+                                                 custom_objects={'Bias': Bias}, device=device)
+        if 'weights_file' in object_specs:
+            new_net.model.load_weights(_resolve(object_specs['weights_file'], json_file))
+        new_net.forward = new_net._model_forward()
+        return new_net
+
+    def save_model(self, json_file, weights_file=None):
+        object_specs = {
+            'class': self.__class__.__name__,
+            'keras_model': self.model.to_json(),
+            'feature_list': self.preprocessor.feature_list
+        }
+        if weights_file is not None:
+            self.model.save_weights(weights_file)
+            object_specs['weights_file'] = weights_file
+        with open(json_file, 'w') as f:
+            json.dump(object_specs, f)
+
+
+def _resolve(path, json_file):
+    """Weights paths in specs are relative to the working directory (reference behaviour); if
+    that fails, also try relative to the JSON file and its parent directories."""
+    if os.path.isabs(path) or os.path.exists(path):
+        return path
+    d = os.path.dirname(os.path.abspath(json_file))
+    while True:
+        cand = os.path.join(d, path)
+        if os.path.exists(cand):
+            return cand
+        parent = os.path.dirname(d)
+        if parent == d:
+            return path
+        d = parent
+
+
+def neuralnet(cls):
+    """Class decorator registering NeuralNetBase subclasses for load_model."""
+    NeuralNetBase.subclasses[cls.__name__] = cls
+    return cls
+
+
+class Bias(object):
+    """Per-position trainable bias added after Flatten (reference nn_util.py:118-133).
+
+    Calling ``Bias()`` yields the kerasish layer description; its single weight ``param_0`` has
+    the input's shape minus the batch axis and is initialised to zeros. On the HIP path it is
+    fused into the policy-head kernel."""
+
+    def __new__(cls, **kwargs):
+        return kerasish.BiasLayer(name=kwargs.get("name"))

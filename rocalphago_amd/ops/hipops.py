@@ -73,11 +73,14 @@ def wgrad_workspace(B, S, coutp, cinp, ks, device):
     return buf
 
 
-def conv_wgrad(g, x, dw, db, B, S, hi, cout, coutp, cin, cinp, ks, accumulate=False, work=None):
-    """dW (OIHW fp32) and db from dL/dpre g [pad 1] and the layer input x [pad hi]."""
+def conv_wgrad(g, x, dw, db, B, S, hi, cout, coutp, cin, cinp, ks, accumulate=False, work=None,
+               hg=None):
+    """dW (OIHW fp32) and db from dL/dpre g [pad hg] and the layer input x [pad hi]."""
     if work is None:
         work = wgrad_workspace(B, S, coutp, cinp, ks, g.device)
-    _check(_lib().rag_conv_wgrad(_ptr(g), _ptr(x), _ptr(dw), _ptr(db), _ptr(work), B, S, hi,
+    if hg is None:
+        hg = (g.shape[1] - S) // 2
+    _check(_lib().rag_conv_wgrad(_ptr(g), _ptr(x), _ptr(dw), _ptr(db), _ptr(work), B, S, hi, hg,
                                  g.shape[-1], cout, coutp, cin, cinp, ks, int(accumulate),
                                  _stream()), "conv_wgrad")
 

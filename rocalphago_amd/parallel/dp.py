@@ -1,0 +1,140 @@
+"""Data parallelism over RCCL (torch.distributed backend "nccl" == RCCL on ROCm) — SURVEY C48/R01.
+
+One process per GPU (torchrun / MASTER_ADDR env). Each rank computes the gradient of the mean
+loss over its local batch into the model's flat fp32 gradient buffer; gradients are summed with
+all-reduce and scaled by 1/world (equal local batches => the global-batch mean), then every rank
+applies the identical fused SGD update, so replicas stay bit-identical without re-broadcasts.
+
+Overlap: ``BucketedAllReduce`` splits the flat buffer into contiguous buckets at layer
+boundaries. Backward produces gradients last-layer-first, so a bucket's all-reduce is issued
+(async, on RCCL's stream, ordered after the kernels already queued on the compute stream) as soon
+as its lowest layer's wgrad has been launched, overlapping communication with the remaining
+backward kernels. Buckets are sized for xGMI ring throughput (a few MB each), not NVSwitch.
+
+CPU runs (tests) use the gloo backend with the same code path.
+"""
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def env_world():
+    return int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")), \
+        int(os.environ.get("LOCAL_RANK", "0"))
+
+
+class DPContext(object):
+    def __init__(self, device=None, backend=None, timeout_s=600):
+        world, rank, local = env_world()
+        self.world, self.rank, self.local_rank = world, rank, local
+        self.enabled = world > 1
+        if device is None:
+            device = torch.device("cuda", local % max(1, torch.cuda.device_count())) \
+                if torch.cuda.is_available() else torch.device("cpu")
+        self.device = torch.device(device)
+        if self.enabled and not dist.is_initialized():
+            if self.device.type == "cuda":
+                torch.cuda.set_device(self.device)
+            backend = backend or ("nccl" if self.device.type == "cuda" else "gloo")
+            kw = {}
+            if backend == "nccl" and self.device.type == "cuda":
+                kw["device_id"] = self.device
+            dist.init_process_group(backend=backend,
+                                    timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        self.is_root = self.rank == 0
+
+    def broadcast_(self, t, src=0):
+        if self.enabled:
+            dist.broadcast(t, src)
+        return t
+
+    def broadcast_model(self, model):
+        """Make every replica start from rank 0's weights."""
+        if self.enabled:
+            dist.broadcast(model.net.flat, 0)
+            model.net.bump()
+
+    def allreduce_mean_(self, t):
+        if self.enabled:
+            dist.all_reduce(t)
+            t.div_(self.world)
+        return t
+
+    def allreduce_sum_(self, t):
+        if self.enabled:
+            dist.all_reduce(t)
+        return t
+
+    def barrier(self):
+        if self.enabled:
+            if self.device.type == "cuda":
+                dist.barrier(device_ids=[self.device.index])
+            else:
+                dist.barrier()
+
+    def max_scalar(self, v):
+        if not self.enabled:
+            return v
+        t = torch.tensor([float(v)], device=self.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def shutdown(self):
+        if self.enabled and dist.is_initialized():
+            dist.destroy_process_group()
+
+
+class BucketedAllReduce(object):
+    """Async all-reduce of a flat gradient buffer in layer-aligned buckets (back to front)."""
+
+    def __init__(self, ctx, flat_grad, layer_offsets, bucket_bytes=4 << 20):
+        """layer_offsets: ascending start offsets (elements) of each trunk layer's params in
+        ``flat_grad``; the tail after the last offset (head params) joins the last bucket."""
+        self.ctx = ctx
+        self.flat = flat_grad
+        self.handles = []
+        n = flat_grad.numel()
+        # build buckets from the end: [start, end)
+        bounds = []
+        end = n
+        cur_start = n
+        for off in reversed(layer_offsets):
+            cur_start = off
+            if (end - cur_start) * 4 >= bucket_bytes:
+                bounds.append((cur_start, end))
+                end = cur_start
+        if end > 0:
+            bounds.append((0, end))
+        self.bounds = bounds  # in backward order
+        # layer index -> bucket to launch once that layer's grads exist
+        self.trigger = {}
+        for bi, (s, e) in enumerate(bounds):
+            for li, off in enumerate(layer_offsets):
+                if off == s:
+                    self.trigger[li] = bi
+        self._launched = set()
+
+    def reset(self):
+        self.handles = []
+        self._launched = set()
+
+    def layer_done(self, layer):
+        bi = self.trigger.get(layer)
+        if bi is None or bi in self._launched or not self.ctx.enabled:
+            return
+        s, e = self.bounds[bi]
+        self.handles.append(dist.all_reduce(self.flat[s:e], async_op=True))
+        self._launched.add(bi)
+
+    def finish(self):
+        if not self.ctx.enabled:
+            return
+        for bi, (s, e) in enumerate(self.bounds):
+            if bi not in self._launched:
+                self.handles.append(dist.all_reduce(self.flat[s:e], async_op=True))
+        for h in self.handles:
+            h.wait()
+        self.flat.div_(self.ctx.world)
+        self.reset()

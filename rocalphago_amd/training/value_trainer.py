@@ -1,0 +1,197 @@
+"""Value-network training — the reference's reinforcement_value_trainer.py is empty and
+value.py only has TODO stubs; this module provides both halves:
+
+* ``generate_value_dataset``: self-play with a policy (batched, lock-step games), ONE position
+  sampled uniformly per game (decorrelated, as in the AlphaGo paper), label z = +1 if the player
+  to move at that position eventually won, -1 if lost, 0 for a tie. Written as HDF5
+  (``states`` uint8 [N, F, S, S] with the value features incl. ``color``, ``values`` float32
+  [N, 1], ``features``).
+* ``ValueTrainer`` / ``run_training``: MSE regression of a CNNValue on such a dataset with the
+  same device-resident pipeline as supervised training (random symmetries — the value is
+  invariant), RCCL data parallelism and the same output directory contract (metadata.json,
+  weights.{epoch:05d}.hdf5).
+"""
+import json
+import os
+import time
+
+import numpy as np
+import torch
+
+from ..engine import gamestate as go
+from ..features.preprocessing import VALUE_FEATURES, Preprocess
+from ..io import h5lite
+from ..models import kerasish as K
+from ..models.value import CNNValue
+from ..parallel.dp import BucketedAllReduce, DPContext
+from .data import transform_ids
+from .supervised import MetadataWriterCallback
+
+
+def generate_value_dataset(player, n_games, out_file=None, board=19, features=VALUE_FEATURES,
+                           move_limit=500, rng=None, batch_games=64):
+    """Self-play ``n_games`` with ``player`` (needs get_moves); return (states, values)."""
+    rng = rng or np.random.RandomState(0)
+    pp = Preprocess(features)
+    all_states, all_values = [], []
+    done = 0
+    while done < n_games:
+        n = min(batch_games, n_games - done)
+        states = [go.GameState(size=board) for _ in range(n)]
+        target = [int(rng.randint(0, move_limit // 2)) for _ in range(n)]
+        snap = [None] * n
+        unfinished = list(range(n))
+        while unfinished:
+            sts = [states[i] for i in unfinished]
+            for i, st in zip(unfinished, sts):
+                if snap[i] is None and len(st.history) >= target[i]:
+                    snap[i] = st.copy()
+            moves = player.get_moves(sts)
+            nxt = []
+            for i, st, mv in zip(unfinished, sts, moves):
+                st.do_move(mv)
+                if not st.is_end_of_game and len(st.history) < move_limit:
+                    nxt.append(i)
+            unfinished = nxt
+        for i in range(n):
+            s = snap[i] if snap[i] is not None else states[i]
+            w = states[i].get_winner()
+            z = 0.0 if w == 0 else (1.0 if w == s.current_player else -1.0)
+            all_states.append(s)
+            all_values.append(z)
+        done += n
+    X = pp.states_to_tensor_u8(all_states)
+    y = np.asarray(all_values, np.float32).reshape(-1, 1)
+    if out_file:
+        with h5lite.File(out_file, "w") as f:
+            f.create_dataset("states", data=X, chunks=(64,) + X.shape[1:], compression="lzf",
+                             maxshape=(None,) + X.shape[1:])
+            f["values"] = y
+            f["features"] = np.bytes_(",".join(features))
+    return X, y
+
+
+class ValueTrainer(object):
+    """Device-resident value-net loop (MSE), shared by run_training and bench.py."""
+
+    def __init__(self, value_model, states, values, batch_size, symmetries=None, dp=None,
+                 seed=0):
+        self.model = value_model
+        self.dev = value_model.device
+        self.states = states if isinstance(states, torch.Tensor) else \
+            torch.from_numpy(np.ascontiguousarray(states, np.uint8)).to(self.dev)
+        self.values = values if isinstance(values, torch.Tensor) else \
+            torch.from_numpy(np.asarray(values, np.float32).reshape(-1, 1)).to(self.dev)
+        self.B = batch_size
+        self.dp = dp
+        self.sym = torch.tensor(transform_ids(symmetries or ["noop"]), dtype=torch.int32,
+                                device=self.dev)
+        self.gen = torch.Generator(device=self.dev)
+        self.gen.manual_seed(seed + (dp.rank if dp else 0))
+        self.plan = value_model._plan_for() if self.dev.type == "cuda" else None
+        self.bucketer = None
+        if self.plan is not None and dp is not None and dp.enabled:
+            self.bucketer = BucketedAllReduce(dp, value_model.net.flat_grad,
+                                              self.plan.layer_offsets())
+        self.loss_sum = torch.zeros((), device=self.dev)
+        self.count = 0
+
+    def step(self, index):
+        n = index.numel()
+        model = self.model
+        tf = self.sym[torch.randint(0, self.sym.numel(), (n,), generator=self.gen,
+                                    device=self.dev)]
+        y = self.values[index]
+        if self.plan is not None:
+            B = self.plan.prepare(self.states, index=index, transforms=tf)
+            loss = self.plan.fwd_bwd(B, y, None)
+            if self.bucketer:
+                self.bucketer.finish()
+            model.optimizer.apply(model.net)
+            self.loss_sum += loss * n
+        else:
+            from .data import apply_transform_np
+            st = self.states[index].cpu().numpy()
+            X = np.stack([apply_transform_np(s, int(t)) for s, t in zip(st, tf.cpu().numpy())])
+            saved = model.grad_allreduce
+            if self.dp is not None and self.dp.enabled:
+                model.grad_allreduce = self.dp.allreduce_mean_
+            loss = model.train_on_batch(X.astype(np.float32), y.cpu().numpy())
+            model.grad_allreduce = saved
+            self.loss_sum += float(loss) * n
+        self.count += n
+
+    def pop_loss(self):
+        t = torch.stack([self.loss_sum, torch.tensor(float(self.count), device=self.dev)])
+        if self.dp is not None and self.dp.enabled:
+            self.dp.allreduce_sum_(t)
+        t = t.cpu().numpy()
+        self.loss_sum.zero_()
+        self.count = 0
+        return float(t[0] / max(t[1], 1))
+
+
+def run_training(cmd_line_args=None):
+    import argparse
+    parser = argparse.ArgumentParser(description='Train a value network on self-play positions.')
+    parser.add_argument("model", help="Path to a CNNValue JSON model file")
+    parser.add_argument("train_data", help="HDF5 with 'states' and 'values' (see generate_value_dataset)")  # noqa: E501
+    parser.add_argument("out_directory", help="directory where metadata and weights will be saved")
+    parser.add_argument("--minibatch", "-B", type=int, default=32)
+    parser.add_argument("--epochs", "-E", type=int, default=10)
+    parser.add_argument("--learning-rate", "-r", type=float, default=0.003)
+    parser.add_argument("--decay", "-d", type=float, default=8.664339379294006e-08)
+    parser.add_argument("--train-val-test", nargs=3, type=float, default=[0.93, .05, .02])
+    parser.add_argument("--symmetries", default='noop,rot90,rot180,rot270,fliplr,flipud,diag1,diag2')  # noqa: E501
+    parser.add_argument("--weights", default=None, help="resume from weights in out_directory")
+    parser.add_argument("--verbose", "-v", default=False, action="store_true")
+    args = parser.parse_args(cmd_line_args)
+
+    dp = DPContext()
+    net = CNNValue.load_model(args.model, device=dp.device)
+    model = net.model
+    if args.weights:
+        model.load_weights(os.path.join(args.out_directory, args.weights))
+    dp.broadcast_model(model)
+    data = h5lite.File(args.train_data)
+    states, values = data["states"][()], data["values"][()]
+    if states.shape[1] != net.preprocessor.output_dim:
+        raise ValueError("dataset has %d planes, model expects %d" %
+                         (states.shape[1], net.preprocessor.output_dim))
+    n = len(states)
+    n_train = int(args.train_val_test[0] * n)
+    n_train -= n_train % args.minibatch
+    if dp.is_root and not os.path.exists(args.out_directory):
+        os.makedirs(args.out_directory)
+    dp.barrier()
+    meta = MetadataWriterCallback(os.path.join(args.out_directory, "metadata.json"))
+    meta.metadata["training_data"] = args.train_data
+    meta.metadata["model_file"] = args.model
+    meta.metadata["cmd_line_args"] = [vars(args)]
+    ckpt = K.ModelCheckpoint(os.path.join(args.out_directory, "weights.{epoch:05d}.hdf5"))
+    ckpt.set_model(model)
+    model.compile(loss="mean_squared_error", optimizer=K.SGD(lr=args.learning_rate,
+                                                             decay=args.decay))
+    perm = np.random.RandomState(0).permutation(n)
+    trainer = ValueTrainer(model, states, values, args.minibatch,
+                           args.symmetries.split(","), dp)
+    tr = torch.from_numpy(perm[:n_train].astype(np.int64)).to(dp.device)
+    va = perm[n_train:]
+    for epoch in range(args.epochs):
+        t0 = time.time()
+        for s in range(dp.rank * args.minibatch, n_train, args.minibatch * dp.world):
+            trainer.step(tr[s:s + args.minibatch])
+        logs = {"loss": trainer.pop_loss()}
+        if len(va):
+            pred = model.predict(states[va].astype(np.float32))
+            logs["val_loss"] = float(np.mean((pred - values[va]) ** 2))
+        meta.on_epoch_end(epoch, logs)
+        ckpt.on_epoch_end(epoch, logs)
+        if args.verbose and dp.is_root:
+            print("epoch %d: %s (%.1fs)" % (epoch, json.dumps(logs), time.time() - t0))
+    dp.barrier()
+    return meta.metadata
+
+
+if __name__ == '__main__':
+    run_training()
