@@ -1,0 +1,135 @@
+"""Flagship benchmark: SL policy-network training throughput on MI355X.
+
+Metric (BASELINE.json): positions/sec of SL-policy training on 19x19 — the north-star policy net
+(48 feature planes, 5x5 + 11 x 3x3 convs at 192 filters + 1x1 head + per-position bias + softmax,
+3,882,794 params), bf16 compute on the hand-written gfx950 kernels, synthetic device-resident
+positions with random dihedral augmentation, random-init weights, full SGD step (forward, fused
+softmax cross-entropy, backward, RCCL gradient all-reduce for N>1, fused SGD update) in the timed
+region. Weak scaling: fixed per-GPU batch.
+
+  python bench.py --gpus N --steps K --warmup W        (N>1: launched under torchrun)
+
+Rank 0 prints ONE JSON line; value = whole-job positions/s (max step time over ranks).
+"""
+import argparse
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PAPER_SL_POSITIONS_PER_S = 3000.0  # paper-derived SL throughput (50 GPUs)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256, help="positions per GPU per step")
+    ap.add_argument("--filters", type=int, default=192)
+    ap.add_argument("--layers", type=int, default=12)
+    ap.add_argument("--dataset", type=int, default=65536, help="synthetic positions per GPU")
+    ap.add_argument("--mcts", action="store_true", help="also measure APV-MCTS sims/s")
+    args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # launched by hand: spawn one rank per GPU (child process, no exec)
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               "--nproc-per-node", str(args.gpus), "--master-addr", "127.0.0.1",
+               "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
+
+    import torch
+
+    from rocalphago_amd.features.preprocessing import DEFAULT_FEATURES
+    from rocalphago_amd.models import kerasish as K
+    from rocalphago_amd.models.policy import CNNPolicy
+    from rocalphago_amd.parallel.dp import DPContext
+    from rocalphago_amd.training.data import TRANSFORM_NAMES, DeviceDataset
+    from rocalphago_amd.training.supervised import SupervisedTrainer
+
+    dp = DPContext()
+    dev = dp.device
+    if dev.type != "cuda":
+        raise SystemExit("bench.py needs a GPU")
+    torch.manual_seed(1234)
+    policy = CNNPolicy(DEFAULT_FEATURES, board=19, filters_per_layer=args.filters,
+                       layers=args.layers, device=dev, seed=1234)
+    model = policy.model
+    dp.broadcast_model(model)
+    model.compile(loss="categorical_crossentropy", optimizer=K.SGD(lr=0.003, decay=0.0001),
+                  metrics=["accuracy"])
+    nparams = sum(int(w.numel()) for w in model.net._views)
+    ds = DeviceDataset.synthetic(args.dataset, 48, 19, dev, seed=17 + dp.rank)
+    trainer = SupervisedTrainer(model, ds, args.batch, TRANSFORM_NAMES, dp, seed=5)
+    if trainer.plan is None:
+        raise SystemExit("HIP fused plan not active for the policy network")
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(99 + dp.rank)
+
+    def step():
+        idx = torch.randint(0, ds.N, (args.batch,), generator=gen, device=dev)
+        trainer.step(idx)
+
+    for _ in range(args.warmup):
+        step()
+    dp.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    dp.barrier()
+    dt = time.perf_counter() - t0
+    dt = dp.max_scalar(dt)
+    loss, acc = trainer.pop_metrics()
+    ms = dt / args.steps * 1e3
+    value = dp.world * args.batch * args.steps / dt
+    result = {
+        "metric": "positions/sec SL-policy train (19x19, 48 planes, 192 filters, 13 layers)",
+        "value": round(value, 1),
+        "unit": "positions/s",
+        "n_gpus": dp.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / PAPER_SL_POSITIONS_PER_S, 2),
+        "dtype": "bf16",
+        "data": "synthetic (random 48-plane 19x19 uint8 positions, device-resident, random "
+                "dihedral augmentation); random-init weights",
+        "config": {"model": "CNNPolicy 48x19x19, 12x conv(5x5,3x3...) @%d + 1x1 head, %d params"
+                            % (args.filters, nparams),
+                   "global_batch": args.batch * dp.world, "per_gpu_batch": args.batch,
+                   "seq_len": 361, "parallelism": "dp%d" % dp.world},
+        "train_loss": round(loss, 4),
+        "baseline_note": "vs_baseline = value / 3000 positions/s (paper-derived SL throughput, "
+                         "BASELINE.md; the reference publishes no numbers)",
+    }
+    if args.mcts and dp.is_root:
+        try:
+            from benchmarks.mcts_bench import measure_sims_per_s
+            result["mcts_sims_per_s"] = round(measure_sims_per_s(dev), 1)
+        except Exception as e:  # the SL metric stands on its own
+            result["mcts_error"] = str(e)[:200]
+    if dp.is_root:
+        print(json.dumps(result), flush=True)
+    dp.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,71 @@
+"""End-to-end HIP execution of the flagship networks vs the CPU/torch reference path (GPU)."""
+import numpy as np
+import pytest
+import torch
+
+from rocalphago_amd.engine import GameState
+from rocalphago_amd.features.preprocessing import DEFAULT_FEATURES
+from rocalphago_amd.models import kerasish as K
+from rocalphago_amd.models.policy import CNNPolicy, ResnetPolicy
+from rocalphago_amd.models.value import CNNValue
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(cls, feats, **kw):
+    gpu = cls(feats, device="cuda", seed=3, **kw)
+    cpu = cls(feats, device="cpu", seed=3, **kw)
+    cpu.model.set_weights(gpu.model.get_weights())
+    return gpu, cpu
+
+
+def test_policy_forward_matches_cpu(cuda):
+    g, c = _pair(CNNPolicy, DEFAULT_FEATURES, filters_per_layer=64, layers=4)
+    assert g.model._plan_for() is not None
+    states = [GameState() for _ in range(3)]
+    for i, s in enumerate(states):
+        for m in [(3, 3), (15, 15), (3, 15)][:i + 1]:
+            s.do_move(m)
+    x = g.preprocessor.states_to_tensor(states)
+    pg, pc = g.forward(x), c.forward(x)
+    assert np.abs(pg - pc).max() < 2e-3 * max(1.0, np.abs(pc).max() * 361)
+    assert np.allclose(pg.sum(1), 1, atol=1e-4)
+
+
+def test_policy_train_step_matches_cpu(cuda):
+    g, c = _pair(CNNPolicy, DEFAULT_FEATURES, filters_per_layer=32, layers=3)
+    for m in (g, c):
+        m.model.compile(loss="categorical_crossentropy", optimizer=K.SGD(lr=0.1))
+    rng = np.random.RandomState(0)
+    X = (rng.rand(8, 48, 19, 19) > 0.6).astype(np.float32)
+    Y = np.zeros((8, 361), np.float32)
+    Y[np.arange(8), rng.randint(0, 361, 8)] = 1
+    lg = g.model.train_on_batch(X, Y)
+    lc = c.model.train_on_batch(X, Y)
+    assert abs(lg - lc) < 1e-2 * abs(lc)
+    wg, wc = g.model.get_weights(), c.model.get_weights()
+    for a, b in zip(wg, wc):
+        assert np.abs(a - b).max() < 2e-2 * max(1e-3, np.abs(b).max())
+
+
+def test_value_net_gpu(cuda):
+    g, c = _pair(CNNValue, None or __import__("rocalphago_amd.features.preprocessing",
+                                              fromlist=["x"]).VALUE_FEATURES,
+                 filters_per_layer=32, layers=3)
+    assert g.model._plan_for() is not None
+    s = [GameState(), GameState()]
+    s[1].do_move((4, 4))
+    vg, vc = g.batch_eval_state(s), c.batch_eval_state(s)
+    assert np.abs(vg - vc).max() < 2e-2
+    g.model.compile(loss="mse", optimizer=K.SGD(lr=0.05))
+    X = g.preprocessor.states_to_tensor(s)
+    l0 = g.model.train_on_batch(X, np.array([[1.0], [-1.0]], np.float32))
+    for _ in range(10):
+        l1 = g.model.train_on_batch(X, np.array([[1.0], [-1.0]], np.float32))
+    assert l1 < l0
+
+
+def test_resnet_uses_hip_convs(cuda):
+    g, c = _pair(ResnetPolicy, ["board", "ones"], filters_per_layer=32, layers=3)
+    x = g.preprocessor.state_to_tensor(GameState())
+    assert np.abs(g.forward(x) - c.forward(x)).max() < 2e-3
