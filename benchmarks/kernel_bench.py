@@ -50,7 +50,7 @@ def main():
         y = ops.alloc_padded(B, S, 1, coutp, dev)
         t = timeit(lambda: ops.conv_igemm(xp, wf, bias, y, B, S, hi, 1, cinp, coutp, ks, True))
         res.append(("fwd", cin, cout, ks, t, flops / t / 1e6))
-        g = ops.pack_nchw(torch.randn(B, cout, S, S, device=dev), 1, coutp)
+        g = ops.pack_nchw(torch.randn(B, cout, S, S, device=dev), hi, coutp)
         if ks == 3:
             dx = ops.alloc_padded(B, S, 1, cinp, dev)
             t = timeit(lambda: ops.conv_igemm(g, wb, None, dx, B, S, 1, 1, coutp, cinp, ks, False,

@@ -35,6 +35,24 @@ __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const 
 // docs/KERNELS.md). Involution: applied to the global source on staging and on the read.
 __device__ __forceinline__ int swz64(int row) { return ((row >> 3) & 1) << 1; }
 
+// Row swizzle (16-byte chunk XOR) for [row][CH x 16B] LDS tiles read with ds_read_tr16_b64 as
+// 16x16x32 fragments: a 32-lane half reads rows {8g+q (+4)}, g,q in 0..3, 32 bytes each, so rows
+// r and r+8 (and, for some row lengths, r+2) alias onto the same banks. The XOR makes the eight
+// 32-byte windows of a half disjoint (conflict-free) for every row length used (derivation in
+// docs/KERNELS.md); it only permutes even chunk pairs, so 32-byte windows stay contiguous.
+template <int CH>
+__device__ __forceinline__ int swz_tr(int r) {
+  if constexpr (CH % 16 == 0) {
+    return 2 * (r & 3) + 8 * ((r >> 3) & 1);
+  } else if constexpr (CH % 8 == 0) {
+    return 2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1);
+  } else if constexpr (CH % 4 == 0) {
+    return 2 * ((r >> 3) & 1);
+  } else {
+    return 0;
+  }
+}
+
 __device__ __forceinline__ int wave_id() {
   return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 }

@@ -167,58 +167,100 @@ conv_igemm_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
 // staged row-major ([pixel][channel], the natural layout) by global_load_lds; fragments along
 // the pixel (K) axis are read with ds_read_tr16_b64 (hardware transpose). fp32 partials go to a
 // per-chunk slab (plain stores), reduced by wgrad_reduce_kernel, which also emits OIHW layout.
+// Software pipeline: 64-pixel stages (two MFMA k-steps), 3 LDS buffers, loads for stage s+2
+// issued right after the barrier of stage s; every wave issues the same number of
+// global_load_lds per stage, so a single counted `s_waitcnt vmcnt(PER_STAGE)` retires exactly
+// stage s while s+1 stays in flight, followed by a raw s_barrier (never __syncthreads, whose
+// implicit vmcnt(0) would drain the prefetch).
 template <int KS, int NTN, int NTC>
 __global__ void __launch_bounds__(256, 1)
 conv_wgrad_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
                   float* __restrict__ part, float* __restrict__ bpart, int M, int S, int WI,
                   int shift, int WG, int HG, int GC, int CIN, int steps_per_chunk, int COUTP,
                   int CINP, int ntile_c) {
+  constexpr int BKP = 64;  // pixels per stage
+  constexpr int NBUF = 3;
   constexpr int BNN = 32 * NTN, BNC = 32 * NTC;
   constexpr int WNN = 16 * NTN, WNC = 16 * NTC;
   constexpr int GROW = BNN, XROW = BNC;  // elements per LDS row
-  constexpr int STAGE = 32 * (GROW + XROW);
-  __shared__ __attribute__((aligned(16))) bf16 lds[2 * STAGE];
+  constexpr int STAGE = BKP * (GROW + XROW);
+  constexpr int GCH = BNN / 8, XCH = BNC / 8;  // 16B chunks per row
+  constexpr int GINST = BKP * GCH / 64, XINST = BKP * XCH / 64;
+  static_assert(GINST % 4 == 0 && XINST % 4 == 0, "uniform per-wave load count");
+  constexpr int GK = GINST / 4, XK = XINST / 4;
+  constexpr int PER_STAGE = GK + XK;  // glds per wave per stage
+  __shared__ __attribute__((aligned(16))) bf16 lds[NBUF * STAGE];
 
   const int lane = lane_id();
   const int w = wave_id();
   const int wa = w & 1, wb = w >> 1;  // wa along n, wb along c
-  const int chunk = blockIdx.x;
-  const int tn = blockIdx.y / ntile_c, tc = blockIdx.y - (blockIdx.y / ntile_c) * ntile_c;
-  const int tap = blockIdx.z;
+  // 1-D grid, XCD-aware: the taps x tiles blocks that share one pixel chunk get consecutive
+  // work ids on the same XCD, so its G/X rows come from HBM once and then hit that XCD's L2.
+  const int taps = KS * KS;
+  const int ntile_n = COUTP / BNN;
+  const int per_chunk = taps * ntile_n * ntile_c;
+  const int wid = xcd_remap(blockIdx.x, gridDim.x);
+  const int chunk = wid / per_chunk;
+  const int wrem = wid - chunk * per_chunk;
+  const int tile = wrem / taps;
+  const int tap = wrem - tile * taps;
+  const int tn = tile / ntile_c, tc = tile - (tile / ntile_c) * ntile_c;
   const int n0 = tn * BNN, c0 = tc * BNC;
   const int ky = tap / KS, kx = tap - (tap / KS) * KS;
-  const int S2 = S * S;
-  const int mbeg = chunk * steps_per_chunk * 32;
+  const int mbeg = chunk * steps_per_chunk * BKP;
 
-  constexpr int GCH = BNN / 8, XCH = BNC / 8;  // 16B chunks per row
-  constexpr int GINST = 32 * GCH / 64, XINST = 32 * XCH / 64;
+  // per-lane pixel coordinates of its staged rows, advanced by BKP pixels per stage
+  int gm[GK], gb[GK], gi[GK], gj[GK], goff[GK];
+  int xm[XK], xb[XK], xi[XK], xj[XK], xoff[XK];
+  auto init_pix = [&](int m, int& b, int& i, int& j) {
+    const int S2 = S * S;
+    const int mm = m < M ? m : M - 1;
+    b = mm / S2;
+    const int r = mm - b * S2;
+    i = r / S;
+    j = r - i * S;
+  };
+  auto adv = [&](int& b, int& i, int& j) {
+    j += BKP;
+    while (j >= S) { j -= S; ++i; }
+    while (i >= S) { i -= S; ++b; }
+  };
+#pragma unroll
+  for (int k = 0; k < GK; ++k) {
+    const int idx = (w + 4 * k) * 64 + lane;
+    const int row = idx / GCH;
+    goff[k] = n0 + ((idx - row * GCH) ^ swz_tr<GCH>(row)) * 8;
+    gm[k] = mbeg + row;
+    init_pix(gm[k], gb[k], gi[k], gj[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < XK; ++k) {
+    const int idx = (w + 4 * k) * 64 + lane;
+    const int row = idx / XCH;
+    xoff[k] = c0 + ((idx - row * XCH) ^ swz_tr<XCH>(row)) * 8;
+    xm[k] = mbeg + row;
+    init_pix(xm[k], xb[k], xi[k], xj[k]);
+  }
 
-  auto stage = [&](int buf, int s) {
+  auto stage = [&](int buf) {
     bf16* lg = lds + buf * STAGE;
-    bf16* lx = lg + 32 * GROW;
-    const int mb = mbeg + s * 32;
-    for (int k = w; k < GINST; k += 4) {
-      const int idx = k * 64 + lane;
-      const int row = idx / GCH, ch = idx - (idx / GCH) * GCH;
-      const int m = mb + row;
-      size_t src = 0;  // padded row 0 is halo (zero): contributes nothing
-      if (m < M) {
-        const int b = m / S2, rem = m - (m / S2) * S2;
-        const int pi = rem / S, pj = rem - (rem / S) * S;
-        src = (size_t)((b * WG + pi + HG) * WG + pj + HG) * GC + n0 + ch * 8;
-      }
-      glds16(G + src, lg + k * 512);
+    bf16* lx = lg + BKP * GROW;
+#pragma unroll
+    for (int k = 0; k < GK; ++k) {
+      // rows past M read padded row 0 (a halo pixel: zero) and contribute nothing
+      const size_t src = gm[k] < M
+          ? (size_t)((gb[k] * WG + gi[k] + HG) * WG + gj[k] + HG) * GC + goff[k] : 0;
+      glds16(G + src, lg + (w + 4 * k) * 512);
+      gm[k] += BKP;
+      if (gm[k] < M) adv(gb[k], gi[k], gj[k]);
     }
-    for (int k = w; k < XINST; k += 4) {
-      const int idx = k * 64 + lane;
-      const int row = idx / XCH, ch = idx - (idx / XCH) * XCH;
-      int m = mb + row;
-      m = m < M ? m : M - 1;  // G row is zero for m >= M
-      const int b = m / S2, rem = m - (m / S2) * S2;
-      const int pi = rem / S, pj = rem - (rem / S) * S;
-      const size_t src =
-          (size_t)((b * WI + pi + ky + shift) * WI + pj + kx + shift) * CIN + c0 + ch * 8;
-      glds16(X + src, lx + k * 512);
+#pragma unroll
+    for (int k = 0; k < XK; ++k) {
+      const size_t src = (size_t)((xb[k] * WI + xi[k] + ky + shift) * WI + xj[k] + kx +
+                                  shift) * CIN + xoff[k];
+      glds16(X + src, lx + (w + 4 * k) * 512);
+      xm[k] += BKP;
+      if (xm[k] < M) adv(xb[k], xi[k], xj[k]);
     }
   };
 
@@ -231,53 +273,62 @@ conv_wgrad_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
   const bool do_bias = (bpart != nullptr) && tap == 0 && tc == 0;
 
   const int mleft = M - mbeg;
-  int nsteps = (mleft + 31) / 32;
+  int nsteps = (mleft + BKP - 1) / BKP;
   nsteps = nsteps < steps_per_chunk ? nsteps : steps_per_chunk;
+  nsteps = nsteps > 0 ? nsteps : 0;
 
-  if (nsteps > 0) {
-    stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
+  if (nsteps > 0) stage(0);
+  if (nsteps > 1) stage(1);
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
   for (int s = 0; s < nsteps; ++s) {
-    const int cur = s & 1;
-    if (s + 1 < nsteps) stage(cur ^ 1, s + 1);
-    const bf16* lg = lds + cur * STAGE;
-    const bf16* lx = lg + 32 * GROW;
-    bf16x8 fa[NTN], fb[NTC];
+    // retire stage s (stage s+1 may stay in flight), then make it visible to all waves
+    if (s + 1 < nsteps)
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(PER_STAGE) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (s + 2 < nsteps) stage((s + 2) % NBUF);
+    const bf16* lg = lds + (s % NBUF) * STAGE;
+    const bf16* lx = lg + BKP * GROW;
 #pragma unroll
-    for (int a = 0; a < NTN; ++a) {
-      const int col = wa * WNN + a * 16 + 4 * p;
-      const bf16* p0 = lg + (8 * g + q) * GROW + col;
-      const bf16* p1 = lg + (8 * g + 4 + q) * GROW + col;
-      bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_PTR(bf16x4))p0);
-      bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_PTR(bf16x4))p1);
-      fa[a] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    for (int h = 0; h < 2; ++h) {  // two MFMA k-steps of 32 pixels
+      const int rb = h * 32;
+      bf16x8 fa[NTN], fb[NTC];
+#pragma unroll
+      for (int a = 0; a < NTN; ++a) {
+        const int col = wa * WNN + a * 16 + 4 * p;
+        const int r0 = rb + 8 * g + q, r1 = r0 + 4;
+        const bf16* p0 = lg + r0 * GROW + (((col >> 3) ^ swz_tr<GCH>(r0)) << 3) + (col & 7);
+        const bf16* p1 = lg + r1 * GROW + (((col >> 3) ^ swz_tr<GCH>(r1)) << 3) + (col & 7);
+        bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_PTR(bf16x4))p0);
+        bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_PTR(bf16x4))p1);
+        fa[a] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int c = 0; c < NTC; ++c) {
+        const int col = wb * WNC + c * 16 + 4 * p;
+        const int r0 = rb + 8 * g + q, r1 = r0 + 4;
+        const bf16* p0 = lx + r0 * XROW + (((col >> 3) ^ swz_tr<XCH>(r0)) << 3) + (col & 7);
+        const bf16* p1 = lx + r1 * XROW + (((col >> 3) ^ swz_tr<XCH>(r1)) << 3) + (col & 7);
+        bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_PTR(bf16x4))p0);
+        bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_PTR(bf16x4))p1);
+        fb[c] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int a = 0; a < NTN; ++a)
+#pragma unroll
+        for (int c = 0; c < NTC; ++c) acc[a][c] = mfma16(fa[a], fb[c], acc[a][c]);
     }
-#pragma unroll
-    for (int c = 0; c < NTC; ++c) {
-      const int col = wb * WNC + c * 16 + 4 * p;
-      const bf16* p0 = lx + (8 * g + q) * XROW + col;
-      const bf16* p1 = lx + (8 * g + 4 + q) * XROW + col;
-      bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_PTR(bf16x4))p0);
-      bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_PTR(bf16x4))p1);
-      fb[c] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    }
-#pragma unroll
-    for (int a = 0; a < NTN; ++a)
-#pragma unroll
-      for (int c = 0; c < NTC; ++c) acc[a][c] = mfma16(fa[a], fb[c], acc[a][c]);
     if (do_bias && (int)threadIdx.x < BNN) {
+      const int c = threadIdx.x;
 #pragma unroll 8
-      for (int r = 0; r < 32; ++r) bsum += (float)lg[r * GROW + threadIdx.x];
+      for (int r = 0; r < BKP; ++r)
+        bsum += (float)lg[r * GROW + (((c >> 3) ^ swz_tr<GCH>(r)) << 3) + (c & 7)];
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
   }
 
   // write the partial slab part[chunk][tap][n][c] (fp32, plain stores)
-  const int taps = KS * KS;
   float* dst = part + ((size_t)(chunk * taps + tap) * COUTP) * CINP;
 #pragma unroll
   for (int a = 0; a < NTN; ++a)
@@ -467,16 +518,58 @@ RAG_API int rag_conv_igemm(const void* X, const void* W, const float* bias, void
 }
 
 // Workspace (floats) needed by rag_conv_wgrad for the partial slabs.
-RAG_API size_t rag_conv_wgrad_workspace(int B, int S, int COUTP, int CINP, int KS, int* nchunks) {
+int rag_launch_wgrad_taps(const bf16* G, const bf16* X, float* part, float* bpart, int R, int WP,
+                          int GC, int CIN, int spc, int COUTP, int CINP, int KS, int RG,
+                          int nchunks, hipStream_t stream);  // wgrad.hip
+bool rag_wgrad_taps_fits(int WP, int KS, int RG);  // wgrad.hip
+int rag_wgrad_taps_target_blocks();  // wgrad.hip
+
+namespace {
+// all-taps variant applicability and plan (see wgrad.hip)
+struct TapsPlan {
+  bool ok;
+  int rg, nchunks, spc;
+};
+TapsPlan taps_plan(int B, int S, int H, int HG, int COUTP, int CINP, int KS) {
+  TapsPlan p{false, 1, 1, 1};
+  if (H != HG || H < KS / 2 || COUTP % 64 || CINP % 64) return p;
+  const int WP = S + 2 * H;
+  const int rg = (KS == 3) ? 3 : 1;
+  if (!rag_wgrad_taps_fits(WP, KS, rg)) return p;
+  const int R = B * WP * WP;
+  const int steps = (R + 63) / 64;
+  const int per_chunk = (KS / rg) * (COUTP / 64) * (CINP / 64);
+  int nc = rag_wgrad_taps_target_blocks() / per_chunk;  // one full wave of resident blocks
+  if (nc > steps) nc = steps;
+  if (nc < 1) nc = 1;
+  p.ok = true;
+  p.rg = rg;
+  p.spc = (steps + nc - 1) / nc;
+  p.nchunks = (steps + p.spc - 1) / p.spc;
+  return p;
+}
+int gather_nchunks(int B, int S, int COUTP, int CINP, int KS) {
   const int M = B * S * S;
   const int taps = KS * KS;
   const int ntn = COUTP % 192 == 0 ? 6 : (COUTP % 128 == 0 ? 4 : (COUTP % 64 == 0 ? 2 : 1));
   const int ntc = CINP % 96 == 0 ? 3 : (CINP % 64 == 0 ? 2 : 1);
   const int tiles = taps * (COUTP / (32 * ntn)) * (CINP / (32 * ntc));
-  const int msteps = (M + 31) / 32;
+  const int msteps = (M + 63) / 64;
   int nc = (512 + tiles - 1) / tiles;
   if (nc > msteps) nc = msteps;
   if (nc < 1) nc = 1;
+  return nc;
+}
+}  // namespace
+
+// Upper bound (floats) of the wgrad workspace over both kernel variants and halos <= 3.
+RAG_API size_t rag_conv_wgrad_workspace(int B, int S, int COUTP, int CINP, int KS, int* nchunks) {
+  const int taps = KS * KS;
+  int nc = gather_nchunks(B, S, COUTP, CINP, KS);
+  for (int H = 1; H <= 3; ++H) {
+    TapsPlan tp = taps_plan(B, S, H, H, COUTP, CINP, KS);
+    if (tp.ok && tp.nchunks > nc) nc = tp.nchunks;
+  }
   if (nchunks) *nchunks = nc;
   return (size_t)nc * taps * COUTP * CINP + (size_t)nc * COUTP;
 }
@@ -503,27 +596,38 @@ RAG_API int rag_conv_wgrad(const void* G, const void* X, float* dW, float* db, f
                            int B, int S, int HI, int HG, int GC, int COUT, int COUTP, int CIN,
                            int CINP, int KS, int accumulate, hipStream_t stream) {
   if (COUTP % 32 || CINP % 32) return -1;
-  int nchunks = 1;
-  rag_conv_wgrad_workspace(B, S, COUTP, CINP, KS, &nchunks);
-  const int M = B * S * S;
   const int taps = KS * KS;
-  const int ntn = COUTP % 192 == 0 ? 6 : (COUTP % 128 == 0 ? 4 : (COUTP % 64 == 0 ? 2 : 1));
-  const int ntc = CINP % 96 == 0 ? 3 : (CINP % 64 == 0 ? 2 : 1);
-  const int ntile_n = COUTP / (32 * ntn), ntile_c = CINP / (32 * ntc);
-  const int msteps = (M + 31) / 32;
-  const int spc = (msteps + nchunks - 1) / nchunks;
-  float* part = work;
-  float* bpart = db ? work + (size_t)nchunks * taps * COUTP * CINP : nullptr;
-  dim3 grid(nchunks, ntile_n * ntile_c, taps);
-  const int WI = S + 2 * HI, shift = HI - KS / 2, WG = S + 2 * HG;
   const bf16* g = (const bf16*)G;
   const bf16* x = (const bf16*)X;
-  switch (KS) {
-    case 1: launch_wgrad_ks<1>(ntn, ntc, grid, stream, g, x, part, bpart, M, S, WI, shift, WG, HG, GC, CINP, spc, COUTP, CINP, ntile_c); break;
-    case 3: launch_wgrad_ks<3>(ntn, ntc, grid, stream, g, x, part, bpart, M, S, WI, shift, WG, HG, GC, CINP, spc, COUTP, CINP, ntile_c); break;
-    case 5: launch_wgrad_ks<5>(ntn, ntc, grid, stream, g, x, part, bpart, M, S, WI, shift, WG, HG, GC, CINP, spc, COUTP, CINP, ntile_c); break;
-    case 7: launch_wgrad_ks<7>(ntn, ntc, grid, stream, g, x, part, bpart, M, S, WI, shift, WG, HG, GC, CINP, spc, COUTP, CINP, ntile_c); break;
-    default: return -2;
+  TapsPlan tp = taps_plan(B, S, HI, HG, COUTP, CINP, KS);
+  int nchunks;
+  float* part = work;
+  float* bpart;
+  if (tp.ok) {
+    nchunks = tp.nchunks;
+    bpart = db ? work + (size_t)nchunks * taps * COUTP * CINP : nullptr;
+    const int WP = S + 2 * HI;
+    const int rc = rag_launch_wgrad_taps(g, x, part, bpart, B * WP * WP, WP, GC, CINP, tp.spc,
+                                         COUTP, CINP, KS, tp.rg, nchunks, stream);
+    if (rc) return rc;
+  } else {
+    nchunks = gather_nchunks(B, S, COUTP, CINP, KS);
+    const int M = B * S * S;
+    const int ntn = COUTP % 192 == 0 ? 6 : (COUTP % 128 == 0 ? 4 : (COUTP % 64 == 0 ? 2 : 1));
+    const int ntc = CINP % 96 == 0 ? 3 : (CINP % 64 == 0 ? 2 : 1);
+    const int ntile_n = COUTP / (32 * ntn), ntile_c = CINP / (32 * ntc);
+    const int msteps = (M + 63) / 64;
+    const int spc = (msteps + nchunks - 1) / nchunks;
+    bpart = db ? work + (size_t)nchunks * taps * COUTP * CINP : nullptr;
+    dim3 grid(nchunks * ntile_n * ntile_c * taps);
+    const int WI = S + 2 * HI, shift = HI - KS / 2, WG = S + 2 * HG;
+    switch (KS) {
+      case 1: launch_wgrad_ks<1>(ntn, ntc, grid, stream, g, x, part, bpart, M, S, WI, shift, WG, HG, GC, CINP, spc, COUTP, CINP, ntile_c); break;
+      case 3: launch_wgrad_ks<3>(ntn, ntc, grid, stream, g, x, part, bpart, M, S, WI, shift, WG, HG, GC, CINP, spc, COUTP, CINP, ntile_c); break;
+      case 5: launch_wgrad_ks<5>(ntn, ntc, grid, stream, g, x, part, bpart, M, S, WI, shift, WG, HG, GC, CINP, spc, COUTP, CINP, ntile_c); break;
+      case 7: launch_wgrad_ks<7>(ntn, ntc, grid, stream, g, x, part, bpart, M, S, WI, shift, WG, HG, GC, CINP, spc, COUTP, CINP, ntile_c); break;
+      default: return -2;
+    }
   }
   const int total = COUT * CIN * taps + COUT;
   wgrad_reduce_kernel<<<(total + 255) / 256, 256, 0, stream>>>(part, bpart, dW, db, nchunks, taps,

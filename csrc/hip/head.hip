@@ -99,61 +99,87 @@ policy_head_fwd_kernel(const bf16* __restrict__ H, const float* __restrict__ w, 
   }
 }
 
-// Backward of the 1x1 K->1 head conv (+ per-position bias): given dz [B][S2],
-//   dH[b,p,k] = dz[b,p] * w[k] * (H[b,p,k] > 0)   (fused ReLU derivative of the last trunk layer)
-//   dw[k] += sum dz*H, db0 += sum dz, dpbias[p] += sum_b dz
+// Backward of the 1x1 K->1 head conv (+ per-position bias), two launches without contended
+// global atomics:
+//  (1) per board: dH[b,p,k] = dz[b,p] * w[k] * (H[b,p,k] > 0)  (fused ReLU derivative of the
+//      last trunk layer) and the board's partial dw: dwpart[b,k] = sum_p dz[b,p] * H[b,p,k]
+//  (2) column sums: dw[k] = sum_b dwpart[b,k], dpbias[p] = sum_b dz[b,p], db0 = sum_p dpbias[p]
+template <int CH>  // CH = KP / 8 sixteen-byte channel chunks per pixel row
 __global__ void __launch_bounds__(kHeadThreads)
 head_bwd_kernel(const bf16* __restrict__ H, const float* __restrict__ w,
-                const float* __restrict__ dz, bf16* __restrict__ dH, float* __restrict__ dw,
-                float* __restrict__ db0, float* __restrict__ dpbias, int S, int KP, int K,
+                const float* __restrict__ dz, bf16* __restrict__ dH, float* __restrict__ dwpart,
+                float* __restrict__ db0, int npix, int pix_per_block, int S, int K,
                 int relu_mask) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* ws = smem;       // KP
-  float* dwl = smem + KP;  // KP partial dw
-  __shared__ float red[16];
-  const int b = blockIdx.x;
-  const int S2 = S * S, WP = S + 2;
+  constexpr int KP = CH * 8;
+  constexpr int PPI = kHeadThreads / CH;  // pixels per block iteration
+  __shared__ float ws[KP];
+  __shared__ float dwl[KP];
   for (int k = threadIdx.x; k < KP; k += blockDim.x) {
     ws[k] = k < K ? w[k] : 0.f;
     dwl[k] = 0.f;
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && db0) *db0 = 0.f;
   __syncthreads();
-  // one wave per pixel row group: lanes split the channel axis (8 channels per lane)
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int lanes_per_row = KP / 8;  // <= 64 for KP <= 512
-  const int rows_per_wave = 64 / lanes_per_row;
-  const int sub = lane / lanes_per_row, cl = lane - sub * lanes_per_row;
-  float dwacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  float dbacc = 0.f;
-  for (int p0 = wv * rows_per_wave; p0 < S2; p0 += nw * rows_per_wave) {
-    const int p = p0 + sub;
-    if (sub < rows_per_wave && p < S2) {
+  const int S2 = S * S, WP = S + 2;
+  const int ch = threadIdx.x % CH, sub = threadIdx.x / CH;
+  float wl[8], dwacc[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    wl[t] = ws[ch * 8 + t];
+    dwacc[t] = 0.f;
+  }
+  const int pbeg = blockIdx.x * pix_per_block;
+  const int pend = min(npix, pbeg + pix_per_block);
+  if (sub < PPI) {
+#pragma unroll 4
+    for (int P = pbeg + sub; P < pend; P += PPI) {
+      const int b = P / S2, p = P - (P / S2) * S2;
       const int i = p / S, j = p - (p / S) * S;
-      const size_t off = ((size_t)(b * WP + i + 1) * WP + j + 1) * KP + cl * 8;
-      const float g = dz[(size_t)b * S2 + p];
+      const size_t off = ((size_t)(b * WP + i + 1) * WP + j + 1) * KP + ch * 8;
+      const float g = dz[P];
       const bf16x8 hv = *reinterpret_cast<const bf16x8*>(H + off);
       bf16x8 o;
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
         const float hf = (float)hv[t];
-        float d = g * ws[cl * 8 + t];
+        float d = g * wl[t];
         if (relu_mask && !(hf > 0.f)) d = 0.f;
         o[t] = (bf16)d;
         dwacc[t] += g * hf;
       }
       if (dH) *reinterpret_cast<bf16x8*>(dH + off) = o;
-      if (cl == 0) {
-        dbacc += g;
-        if (dpbias) atomicAdd(dpbias + p, g);
-      }
+    }
+#pragma unroll
+    for (int t = 0; t < 8; ++t) atomicAdd(&dwl[ch * 8 + t], dwacc[t]);  // LDS atomics only
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < KP; k += blockDim.x) dwpart[(size_t)blockIdx.x * KP + k] = dwl[k];
+}
+
+// blocks [0, K): dw[k] = sum over head_bwd blocks; blocks [K, K+S2): dpbias[p] = sum_b dz[b,p]
+// (and db0 += dpbias[p]). One workgroup per output, block-reduced.
+__global__ void __launch_bounds__(kHeadThreads)
+head_bwd_reduce_kernel(const float* __restrict__ dwpart, const float* __restrict__ dz,
+                       float* __restrict__ dw, float* __restrict__ db0,
+                       float* __restrict__ dpbias, int nblk, int B, int S2, int KP, int K) {
+  __shared__ float red[16];
+  const int o = blockIdx.x;
+  float s = 0.f;
+  if (o < K) {
+    for (int r = threadIdx.x; r < nblk; r += blockDim.x) s += dwpart[(size_t)r * KP + o];
+  } else {
+    const int p = o - K;
+    for (int b = threadIdx.x; b < B; b += blockDim.x) s += dz[(size_t)b * S2 + p];
+  }
+  s = block_reduce(s, red, false);
+  if (threadIdx.x == 0) {
+    if (o < K) {
+      dw[o] = s;
+    } else {
+      if (dpbias) dpbias[o - K] = s;
+      if (db0) atomicAdd(db0, s);
     }
   }
-#pragma unroll
-  for (int t = 0; t < 8; ++t) atomicAdd(&dwl[cl * 8 + t], dwacc[t]);  // LDS atomics
-  const float dbs = block_reduce(dbacc, red, false);
-  __syncthreads();
-  for (int k = threadIdx.x; k < K; k += blockDim.x) atomicAdd(dw + k, dwl[k]);
-  if (threadIdx.x == 0 && db0) atomicAdd(db0, dbs);
 }
 
 // z[b,p] = sum_k w[k]*h[b,p,k] + b0 (value-head 1x1 conv, no softmax)
@@ -193,13 +219,34 @@ RAG_API int rag_policy_head_fwd(const void* H, const float* w, const float* b0,
 }
 
 RAG_API int rag_head_bwd(const void* H, const float* w, const float* dz, void* dH, float* dw,
-                         float* db0, float* dpbias, int B, int S, int KP, int K, int relu_mask,
-                         hipStream_t stream) {
-  if (KP % 8 || KP / 8 > 64) return -1;
-  const size_t sm = (size_t)(2 * KP) * sizeof(float);
-  head_bwd_kernel<<<B, kHeadThreads, sm, stream>>>((const bf16*)H, w, dz, (bf16*)dH, dw, db0,
-                                                   dpbias, S, KP, K, relu_mask);
+                         float* db0, float* dpbias, float* work, int B, int S, int KP, int K,
+                         int relu_mask, hipStream_t stream) {
+  // work: >= rag_head_bwd_workspace(B, S, KP) floats
+  const int npix = B * S * S;
+  int nblk = (npix + 47) / 48;
+  if (nblk > 2048) nblk = 2048;
+  const int ppb = (npix + nblk - 1) / nblk;
+#define RAG_HB(C)                                                                             \
+  case C:                                                                                     \
+    head_bwd_kernel<C><<<nblk, kHeadThreads, 0, stream>>>((const bf16*)H, w, dz, (bf16*)dH,   \
+                                                          work, db0, npix, ppb, S, K,         \
+                                                          relu_mask);                         \
+    break;
+  switch (KP / 8) {
+    RAG_HB(4) RAG_HB(8) RAG_HB(12) RAG_HB(16) RAG_HB(24) RAG_HB(32) RAG_HB(48) RAG_HB(64)
+    default: return -1;
+  }
+#undef RAG_HB
+  head_bwd_reduce_kernel<<<K + S * S, kHeadThreads, 0, stream>>>(work, dz, dw, db0, dpbias, nblk,
+                                                                 B, S * S, KP, K);
   return (int)hipGetLastError();
+}
+
+RAG_API size_t rag_head_bwd_workspace(int B, int S, int KP) {
+  const int npix = B * S * S;
+  int nblk = (npix + 47) / 48;
+  if (nblk > 2048) nblk = 2048;
+  return (size_t)nblk * KP;
 }
 
 RAG_API int rag_head_linear(const void* H, const float* w, const float* b0, float* z, int B,

@@ -53,9 +53,12 @@ class HipTrunk(object):
         """halo[b] of activation boundary b (acts[b] and the gradient g_{b-1} share it, so the
         dgrad epilogue can read its ReLU mask in the output layout)."""
         sp = self.specs
+        # b >= 1 also takes the producing layer's ks//2 so that g_{b-1} (the wgrad G operand of
+        # layer b-1) has the same padded geometry as that layer's input: the all-taps wgrad
+        # kernel then shifts rows instead of gathering them.
         h = [max(1, sp[0].ks // 2)]
         for b in range(1, self.L):
-            h.append(max(1, sp[b].ks // 2, sp[b - 1].ks // 2 if b - 1 >= 1 else 0))
+            h.append(max(1, sp[b].ks // 2, sp[b - 1].ks // 2, h[b - 1] if b == 1 else 0))
         assert self.L == 1 or sp[-1].ks <= 3, "last trunk layer must be 1x1 or 3x3"
         h.append(1)
         return h
@@ -179,9 +182,6 @@ class PolicyHeadEngine(object):
         h = self.trunk.output(B)
         L = self.trunk.L
         dh = self.trunk.grad_buffer(L - 1, 0, B)
-        dw.zero_()
-        db0.zero_()
-        dpbias.zero_()
         ops.head_bwd(h, w, dz, dh, dw, db0, dpbias, self.K,
                      relu_mask=self.trunk.specs[-1].relu)
 
@@ -210,7 +210,5 @@ class ValueHeadEngine(object):
         h = self.trunk.output(B)
         L = self.trunk.L
         dh = self.trunk.grad_buffer(L - 1, 0, B)
-        dw.zero_()
-        db0.zero_()
         ops.head_bwd(h, w, dz.contiguous(), dh, dw, db0, None, self.K,
                      relu_mask=self.trunk.specs[-1].relu)

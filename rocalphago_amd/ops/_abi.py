@@ -19,13 +19,14 @@ SIGNATURES = {
     "rag_pack_nchw": [P, P, I, I, I, I, I, P],
     # head.hip
     "rag_policy_head_fwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, P],
-    "rag_head_bwd": [P, P, P, P, P, P, P, I, I, I, I, I, P],
+    "rag_head_bwd": [P, P, P, P, P, P, P, P, I, I, I, I, I, P],
+    "rag_head_bwd_workspace": [I, I, I],
     "rag_head_linear": [P, P, P, P, I, I, I, I, P],
     # optim.hip
     "rag_sgd": [P, P, P, I64, F, F, F, I, P],
 }
 
-RESTYPES = {"rag_conv_wgrad_workspace": SZ}
+RESTYPES = {"rag_conv_wgrad_workspace": SZ, "rag_head_bwd_workspace": SZ}
 
 
 def declare(lib):

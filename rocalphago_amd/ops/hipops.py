@@ -128,11 +128,22 @@ def policy_head_fwd(h, w, b0, pbias, probs, K, labels=None, sweight=None, loss=N
            "policy_head_fwd")
 
 
-def head_bwd(h, w, dz, dh, dw, db0, dpbias, K, relu_mask=True):
+_head_ws = {}
+
+
+def head_bwd(h, w, dz, dh, dw, db0, dpbias, K, relu_mask=True, work=None):
+    """dH (ReLU-masked) + dw / db0 / dpbias (all overwritten, not accumulated)."""
     B, WP, _, KP = h.shape
     S = WP - 2
+    if work is None:
+        need = _lib().rag_head_bwd_workspace(B, S, KP)
+        work = _head_ws.get(h.device)
+        if work is None or work.numel() < need:
+            work = torch.empty(need, dtype=torch.float32, device=h.device)
+            _head_ws[h.device] = work
     _check(_lib().rag_head_bwd(_ptr(h), _ptr(w), _ptr(dz), _ptr(dh), _ptr(dw), _ptr(db0),
-                               _ptr(dpbias), B, S, KP, K, int(relu_mask), _stream()), "head_bwd")
+                               _ptr(dpbias), _ptr(work), B, S, KP, K, int(relu_mask), _stream()),
+           "head_bwd")
 
 
 def head_linear(h, w, b0, z, K):

@@ -48,12 +48,14 @@ def test_conv_forward(ops, B, cin, cout, ks, S):
     assert y[:, 0].abs().max().item() == 0 and y[:, :, -1].abs().max().item() == 0
 
 
-@pytest.mark.parametrize("B,cin,cout,ks", [(3, 192, 192, 3), (2, 16, 16, 3), (4, 64, 128, 3),
-                                           (3, 32, 192, 5)])
-def test_conv_backward(ops, B, cin, cout, ks):
+# (hi, hg) = input / gradient halos; hi == hg selects the all-taps wgrad kernel (wgrad.hip)
+@pytest.mark.parametrize("B,cin,cout,ks,hi,hg,S", [
+    (3, 192, 192, 3, 1, 1, 19), (2, 16, 16, 3, 1, 1, 19), (4, 64, 128, 3, 1, 1, 19),
+    (3, 32, 192, 5, 2, 1, 19), (3, 64, 192, 5, 2, 2, 19), (2, 128, 64, 1, 1, 1, 19),
+    (37, 192, 192, 3, 1, 1, 19), (5, 64, 64, 3, 2, 2, 9), (6, 128, 192, 3, 1, 1, 13)])
+def test_conv_backward(ops, B, cin, cout, ks, hi, hg, S):
     dev = torch.device("cuda")
     torch.manual_seed(1)
-    S = 19
     x = F.relu(torch.randn(B, cin, S, S, device=dev))
     w = torch.randn(cout, cin, ks, ks, device=dev) * 0.05
     g = torch.randn(B, cout, S, S, device=dev)
@@ -61,13 +63,12 @@ def test_conv_backward(ops, B, cin, cout, ks):
     y = F.conv2d(xr, wr, padding=ks // 2)
     (y * bf(g)).sum().backward()
     cinp, coutp = ops.pad_channels(cin), ops.pad_channels(cout)
-    hi = ks // 2
     xp = ops.pack_nchw(x, hi, cinp)
-    gp = ops.pack_nchw(g, 1, coutp)
+    gp = ops.pack_nchw(g, hg, coutp)
     wf, wb = ops.pack_weights(w, coutp, cinp,
                               wb=torch.empty(ks * ks, cinp, coutp, dtype=torch.bfloat16,
                                              device=dev))
-    if ks == 3:
+    if ks == 3 and hg == 1:
         # dgrad with fused ReLU mask of the layer input
         xm = ops.pack_nchw(x, 1, cinp)
         dx = ops.alloc_padded(B, S, 1, cinp, dev)
@@ -76,7 +77,7 @@ def test_conv_backward(ops, B, cin, cout, ks):
         assert rel_err(ops.unpack(dx, cin, 1), ref_dx) < 2e-2
     dw = torch.zeros(cout, cin, ks, ks, device=dev)
     db = torch.zeros(cout, device=dev)
-    ops.conv_wgrad(gp, xp, dw, db, B, S, hi, cout, coutp, cin, cinp, ks)
+    ops.conv_wgrad(gp, xp, dw, db, B, S, hi, cout, coutp, cin, cinp, ks, hg=hg)
     assert rel_err(dw, wr.grad) < 2e-2
     assert rel_err(db, bf(g).sum((0, 2, 3))) < 2e-2
 
