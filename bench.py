@@ -99,7 +99,9 @@ def main():
     ms = dt / args.steps * 1e3
     value = dp.world * args.batch * args.steps / dt
     result = {
-        "metric": "positions/sec SL-policy train (19x19, 48 planes, 192 filters, 13 layers)",
+        # BASELINE.json's headline metric; value = the SL-policy training positions/s half
+        # (MCTS sims/s is reported alongside with --mcts)
+        "metric": "positions/sec SL-policy train + MCTS sims/sec (19x19) at 1/2/4/8 MI355X",
         "value": round(value, 1),
         "unit": "positions/s",
         "n_gpus": dp.world,
@@ -112,8 +114,9 @@ def main():
         "dtype": "bf16",
         "data": "synthetic (random 48-plane 19x19 uint8 positions, device-resident, random "
                 "dihedral augmentation); random-init weights",
-        "config": {"model": "CNNPolicy 48x19x19, 12x conv(5x5,3x3...) @%d + 1x1 head, %d params"
-                            % (args.filters, nparams),
+        "config": {"model": "19x19 SL policy net (13 layers, %d filters, 48 planes): 5x5 + "
+                            "%dx 3x3 conv + 1x1 head + position bias + softmax, %d params"
+                            % (args.filters, args.layers - 1, nparams),
                    "global_batch": args.batch * dp.world, "per_gpu_batch": args.batch,
                    "seq_len": 361, "parallelism": "dp%d" % dp.world},
         "train_loss": round(loss, 4),
