@@ -1,0 +1,122 @@
+"""Multi-process data parallelism on the CPU (gloo, world_size 2) — same code path as RCCL on GPU.
+
+* SL training with DPContext: replicas stay identical and match single-process training on the
+  concatenated global batch (mean of equal-sized local means == global mean).
+* BucketedAllReduce: layer-triggered async bucket all-reduce == plain mean all-reduce.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+FEATS = ["board", "ones", "turns_since"]  # 12 planes
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _setup(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+
+
+def _make_model(lr=0.05):
+    from rocalphago_amd.models import kerasish as K
+    from rocalphago_amd.models.policy import CNNPolicy
+    policy = CNNPolicy(FEATS, board=9, filters_per_layer=8, layers=3, device="cpu", seed=7)
+    policy.model.compile(loss="categorical_crossentropy", optimizer=K.SGD(lr=lr),
+                         metrics=["accuracy"])
+    return policy.model
+
+
+def _dataset():
+    from rocalphago_amd.training.data import DeviceDataset
+    return DeviceDataset.synthetic(64, 12, 9, torch.device("cpu"), seed=11)
+
+
+def _sl_worker(rank, world, port, outdir, steps, local_b):
+    _setup(rank, world, port)
+    from rocalphago_amd.parallel.dp import DPContext
+    from rocalphago_amd.training.supervised import SupervisedTrainer
+    dp = DPContext(device="cpu")
+    model = _make_model()
+    if rank == 1:  # diverge on purpose: broadcast_model must restore rank 0's weights
+        with torch.no_grad():
+            model.net.flat.add_(1.0)
+        model.net.bump()
+    dp.broadcast_model(model)
+    trainer = SupervisedTrainer(model, _dataset(), local_b, ["noop"], dp, seed=0)
+    gb = local_b * world
+    for s in range(steps):
+        trainer.step(torch.arange(s * gb + rank * local_b, s * gb + (rank + 1) * local_b))
+    loss, acc = trainer.pop_metrics()
+    np.save(os.path.join(outdir, "flat%d.npy" % rank), model.net.flat.detach().numpy())
+    np.save(os.path.join(outdir, "metrics%d.npy" % rank), np.array([loss, acc]))
+    dp.shutdown()
+
+
+def _bucket_worker(rank, world, port, outdir):
+    _setup(rank, world, port)
+    from rocalphago_amd.parallel.dp import BucketedAllReduce, DPContext
+    dp = DPContext(device="cpu")
+    n = 1000
+    offsets = [0, 100, 250, 600, 900]
+    g = torch.arange(n, dtype=torch.float32) * (rank + 1)
+    br = BucketedAllReduce(dp, g, offsets, bucket_bytes=200 * 4)
+    for layer in reversed(range(len(offsets))):
+        br.layer_done(layer)
+    br.finish()
+    np.save(os.path.join(outdir, "bucket%d.npy" % rank), g.numpy())
+    # second use of the same bucketer (reset state) with only finish()
+    g.copy_(torch.ones(n) * (rank + 1))
+    br.finish()
+    np.save(os.path.join(outdir, "bucket_b%d.npy" % rank), g.numpy())
+    dp.shutdown()
+
+
+def _spawn(fn, args, world=2):
+    mp.spawn(fn, args=(world, _port()) + args, nprocs=world, join=True)
+
+
+@pytest.mark.timeout(300)
+def test_dp_sl_training_matches_single_process(tmp_path):
+    steps, local_b, world = 3, 8, 2
+    _spawn(_sl_worker, (str(tmp_path), steps, local_b), world)
+    f0 = np.load(tmp_path / "flat0.npy")
+    f1 = np.load(tmp_path / "flat1.npy")
+    assert np.array_equal(f0, f1), "replicas diverged"
+    m0, m1 = np.load(tmp_path / "metrics0.npy"), np.load(tmp_path / "metrics1.npy")
+    assert np.allclose(m0, m1)
+
+    # single process on the global batch
+    from rocalphago_amd.training.supervised import SupervisedTrainer
+    torch.set_num_threads(1)
+    model = _make_model()
+    start = model.net.flat.detach().clone()
+    trainer = SupervisedTrainer(model, _dataset(), local_b * world, ["noop"], None, seed=0)
+    gb = local_b * world
+    for s in range(steps):
+        trainer.step(torch.arange(s * gb, (s + 1) * gb))
+    ref = model.net.flat.detach().numpy()
+    assert not np.allclose(ref, start.numpy()), "training did not move the weights"
+    np.testing.assert_allclose(f0, ref, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.timeout(300)
+def test_bucketed_allreduce_mean(tmp_path):
+    _spawn(_bucket_worker, (str(tmp_path),))
+    n = 1000
+    want = np.arange(n, dtype=np.float32) * 1.5  # mean of x1 and x2
+    for r in range(2):
+        np.testing.assert_allclose(np.load(tmp_path / ("bucket%d.npy" % r)), want, rtol=1e-6)
+        np.testing.assert_allclose(np.load(tmp_path / ("bucket_b%d.npy" % r)),
+                                   np.full(n, 1.5, np.float32))
