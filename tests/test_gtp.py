@@ -1,0 +1,154 @@
+"""GTP engine (reference tests/test_gtp_wrapper.py, extended to check every reply) and the
+match harness (interface/TestPlay.py)."""
+import io
+import multiprocessing as mp
+
+import pytest
+
+from rocalphago_amd.engine.gamestate import BLACK, WHITE, GameState
+from rocalphago_amd.gtp import engine as gtp
+from rocalphago_amd.gtp.match import PlayMatch
+
+
+class PassPlayer(object):
+    def get_move(self, state):
+        return None
+
+
+class FirstLegalPlayer(object):
+    def get_move(self, state):
+        moves = state.get_legal_moves(include_eyes=False)
+        return moves[0] if moves else None
+
+
+def _engine(player=None):
+    return gtp.ExtendedGtpEngine(gtp.GTPGameConnector(player or PassPlayer()), "T", "9.9")
+
+
+def test_vertex_roundtrip():
+    assert gtp.parse_vertex("A1") == (1, 1)
+    assert gtp.parse_vertex("j10") == (9, 10)  # no 'I' column
+    assert gtp.parse_vertex("T19") == (19, 19)
+    assert gtp.parse_vertex("pass") == gtp.PASS
+    assert gtp.parse_vertex("I5") is None and gtp.parse_vertex("Z") is None
+    for v in [(1, 1), (8, 3), (9, 9), (19, 19)]:
+        assert gtp.parse_vertex(gtp.format_vertex(v)) == v
+
+
+def test_base_protocol():
+    e = _engine()
+    assert e.send("1 name") == "=1 T\n\n"
+    assert e.send("version") == "= 9.9\n\n"
+    assert e.send("protocol_version") == "= 2\n\n"
+    assert e.send("2 known_command play") == "=2 true\n\n"
+    assert e.send("known_command fly") == "= false\n\n"
+    assert "genmove" in e.send("list_commands")
+    assert e.send("3 frobnicate").startswith("?3 unknown command")
+    assert e.send("# just a comment") == ""
+    assert e.send("boardsize 99").startswith("? ")
+    assert e.send("boardsize 9") == "=\n\n"
+    assert e.send("komi 6.5") == "=\n\n"
+    assert e._game._state.komi == 6.5
+
+
+def test_play_genmove_and_illegal():
+    e = _engine(FirstLegalPlayer())
+    e.send("boardsize 9")
+    e.send("clear_board")
+    assert e.send("play black E5") == "=\n\n"
+    assert e.send("play white E5").startswith("? illegal")
+    st = e._game._state
+    assert st.board[4][4] == BLACK
+    r = e.send("genmove white")
+    assert r.startswith("= ") and r.strip() != "= pass"
+    v = gtp.parse_vertex(r[2:].strip())
+    assert st.board[v[0] - 1][v[1] - 1] == WHITE
+    assert e.send("undo") == "=\n\n"
+    assert st is not e._game._state and e._game._state.board[v[0] - 1][v[1] - 1] == 0
+
+
+def test_handicap_and_score():
+    e = _engine()
+    assert e.send("place_free_handicap 4") == "= D4 Q16 D16 Q4\n\n"
+    st = e._game._state
+    assert st.board[3][3] == BLACK and st.board[15][15] == BLACK
+    assert e.send("place_free_handicap 12").startswith("?")
+    # 4 black stones, no territory counted, komi from the state
+    sw, sb = st.get_score()
+    r = e.send("final_score")
+    assert r.startswith("= ")
+    if gtp.shutil.which("gnugo") is None:
+        d = sb - sw
+        assert r.strip() == "= " + (("B+%g" % d) if d > 0 else ("W+%g" % -d))
+        assert "D4" in e.send("final_status_list alive")
+
+
+def test_sgf_commands(tmp_path):
+    e = _engine()
+    e.send("boardsize 9")
+    e.send("play b C3")
+    e.send("play w G7")
+    path = str(tmp_path / "g.sgf")
+    assert e.send("printsgf %s" % path) == "=\n\n"
+    e2 = _engine()
+    assert e2.send("loadsgf %s" % path) == "=\n\n"
+    st = e2._game._state
+    assert st.size == 9 and st.board[2][2] == BLACK and st.board[6][6] == WHITE
+    assert "X" in e2.send("showboard")
+
+
+def test_run_gtp_session():
+    lines = iter(["1 name", "2 boardsize 19", "3 clear_board", "4 genmove black",
+                  "5 genmove white", "99 quit", "6 name"])
+    out = io.StringIO()
+    eng = gtp.run_gtp(PassPlayer(), lambda: next(lines), name="P", out=out)
+    assert eng.disconnect
+    assert out.getvalue() == "=1 P\n\n=2\n\n=3\n\n=4 pass\n\n=5 pass\n\n=99\n\n"
+
+
+def _proc_target(q):
+    # reference test shape: a separate process fed a multi-command string
+    def stdin_simulator():
+        return "\n".join(["1 name", "2 boardsize 19", "3 clear_board", "4 genmove black",
+                          "5 genmove white", "99 quit"])
+    out = io.StringIO()
+    gtp.run_gtp(PassPlayer(), stdin_simulator, out=out)
+    q.put(out.getvalue())
+
+
+def test_gtp_process():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_proc_target, args=(q,))
+    p.start()
+    text = q.get(timeout=120)
+    p.join(timeout=30)
+    assert p.exitcode == 0
+    assert text.endswith("=99\n\n")
+
+
+def test_compat_interface_imports():
+    from interface.gtp_wrapper import ExtendedGtpEngine, run_gtp  # noqa: F401
+    from interface.TestPlay import play_match
+    assert play_match is PlayMatch
+
+
+def test_play_match_to_end():
+    m = PlayMatch(FirstLegalPlayer(), FirstLegalPlayer(), size=5)
+    assert m.playover(turn=200, showboard=False)
+    st = m.state
+    assert st.history[-1] is None and st.history[-2] is None
+    sw, sb = m.calculate_score()
+    assert (sw, sb) == tuple(float(v) for v in st.get_score())
+    s = m.board_string()
+    assert "Winner" in s or "Draw" in s
+    m.clear(showboard=False)
+    assert len(m.state.history) == 0 and not m.playout
+
+
+@pytest.mark.parametrize("n", [2, 9])
+def test_recommended_handicaps_are_legal(n):
+    st = GameState()
+    vs = [gtp.parse_vertex(v) for v in gtp.ExtendedGtpEngine.recommended_handicaps[n].split()]
+    st.place_handicaps([(x - 1, y - 1) for x, y in vs])
+    assert len(st.handicaps) == n
