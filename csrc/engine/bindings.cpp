@@ -186,6 +186,7 @@ PYBIND11_MODULE(_rocgo, m) {
                                return std::vector<int>(h.begin(), h.end());
                              })
       .def_property_readonly("move_count", &Board::move_count)
+      .def_property_readonly("last_moves", [](const Board& b) { return py::make_tuple(b.last1(), b.last2()); })
       .def_property_readonly("handicaps",
                              [](const Board& b) {
                                const auto& h = b.handicaps();

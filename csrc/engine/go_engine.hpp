@@ -148,6 +148,10 @@ class Board {
   const std::vector<uint64_t>& previous_hashes() const { return *prev_hashes_; }
   int move_count() const { return (int)history_->size(); }
   int last_move() const { return history_->empty() ? -2 : history_->back(); }
+  // last two moves, also valid in light mode (-2 = none)
+  int last1() const { return last1_; }
+  int last2() const { return last2_; }
+  int nmoves() const { return nmoves_; }
   const Zobrist& zobrist() const { return *zob_; }
   std::shared_ptr<const Zobrist> zobrist_ptr() const { return zob_; }
   const Geometry& geom() const { return *g_; }

@@ -1,0 +1,200 @@
+"""APV-MCTS: asynchronous policy-and-value Monte Carlo tree search.
+
+The reference declares ``ParallelMCTS`` as an empty stub (AlphaGo/mcts.py:219-220); this is the
+full search, built for a GPU evaluator:
+
+  * the tree, PUCT selection with virtual loss, expansion, negamax backup and tree reuse are
+    native C++ (csrc/mcts/search.cpp, ``_rocgo.Search``);
+  * every *wave* selects ``batch`` leaves (virtual loss spreads them), extracts their input
+    planes natively on a thread pool, and evaluates the policy and value networks for all of
+    them in one batched pass on the GPU (hand-written HIP kernels via the fused plans);
+  * while the GPU runs, the fast-rollout playouts of the same leaves run either on the native
+    thread pool or — ``rollout_device="gpu"`` — as the gfx950 rollout kernel
+    (csrc/hip/rollout.hip, one wavefront per game, ``rollouts_per_leaf`` games per leaf);
+  * leaf value V = (1 - lmbda) * v_theta + lmbda * z (the AlphaGo mixing).
+
+``ParallelMCTS(policy, value=None, ...)`` mirrors the reference MCTS interface
+(``get_move(state)``, ``update_with_move(move)``); ``ParallelMCTSPlayer`` mirrors MCTSPlayer.
+"""
+import numpy as np
+import torch
+
+from .._native import engine as _engine
+from ..engine.gamestate import PASS_MOVE
+
+_rg = _engine()
+
+
+class NetworkEvaluator(object):
+    """Batched leaf evaluation: native boards -> (move priors [n, S*S], values [n])."""
+
+    def __init__(self, policy=None, value=None, nthreads=8):
+        self.policy = policy
+        self.value = value
+        self.nthreads = nthreads
+        self.pfids = policy.preprocessor.feature_ids if policy is not None else None
+        self.vfids = value.preprocessor.feature_ids if value is not None else None
+
+    def _run(self, net, fids, boards):
+        x = _rg.batch_features(boards, fids, self.nthreads)
+        return net.model.predict(x)
+
+    def __call__(self, boards):
+        n = len(boards)
+        priors = values = None
+        if n == 0:
+            return priors, values
+        if self.policy is not None:
+            priors = np.ascontiguousarray(self._run(self.policy, self.pfids, boards),
+                                          dtype=np.float32)
+        if self.value is not None:
+            values = np.ascontiguousarray(self._run(self.value, self.vfids, boards),
+                                          dtype=np.float32).reshape(-1)
+        return priors, values
+
+
+class ParallelMCTS(object):
+    """Wave-batched APV-MCTS over the native tree.
+
+    policy: a CNNPolicy (priors); value: a CNNValue or None (then lmbda is forced to 1, i.e.
+    rollouts only); rollout: a ``_rocgo.RolloutPolicy`` (default weights if None).
+    """
+
+    def __init__(self, policy=None, value=None, rollout=None, lmbda=0.5, c_puct=5.0,
+                 n_playout=1600, batch=256, virtual_loss=3, rollout_limit=500,
+                 playout_depth=722, nthreads=8, rollout_device="cpu", rollouts_per_leaf=1,
+                 seed=1, evaluator=None):
+        if value is None and lmbda < 1:
+            lmbda = 1.0
+        self.evaluator = evaluator or NetworkEvaluator(policy, value, nthreads)
+        self.rollout = rollout or _rg.RolloutPolicy()
+        self.lmbda = float(lmbda)
+        self.c_puct = float(c_puct)
+        self.n_playout = int(n_playout)
+        self.batch = int(batch)
+        self.virtual_loss = int(virtual_loss)
+        self.rollout_limit = int(rollout_limit)
+        self.playout_depth = int(playout_depth)
+        self.nthreads = int(nthreads)
+        self.rollout_device = rollout_device
+        self.rollouts_per_leaf = int(rollouts_per_leaf)
+        self.seed = int(seed)
+        self._search = None
+        self._history = None
+        self._gpu_rollout = None
+        self.stats = {"waves": 0, "sims": 0}
+
+    # ------------------------------------------------------------------ tree management
+    def _configure(self, s):
+        s.c_puct = self.c_puct
+        s.lmbda = self.lmbda
+        s.n_vl = self.virtual_loss
+        s.rollout_limit = self.rollout_limit
+        s.max_depth = self.playout_depth
+        s.nthreads = self.nthreads
+        s.seed = self.seed
+        s.set_rollout_policy(self.rollout)
+
+    def _sync_root(self, state):
+        """Point the tree at ``state``: reuse the subtree when state extends the tree's root
+        by at most a few moves, otherwise start a fresh tree."""
+        hist = list(state.history)
+        s = self._search
+        if s is not None and self._history is not None and \
+                hist[:len(self._history)] == self._history and \
+                len(hist) - len(self._history) <= 4:
+            ok = True
+            for mv in hist[len(self._history):]:
+                flat = -1 if mv is PASS_MOVE else mv[0] * state.size + mv[1]
+                try:
+                    s.advance(flat)
+                except Exception:
+                    ok = False
+                    break
+            if ok and s.root_board.hash == state.native.hash and \
+                    s.root_board.current_player == state.current_player:
+                self._history = hist
+                return s
+        s = _rg.Search(state.native)
+        self._configure(s)
+        self._search = s
+        self._history = hist
+        return s
+
+    # ------------------------------------------------------------------ search
+    def _wave(self, s, want):
+        n = s.select(want)
+        if n == 0:
+            return 0
+        boards = s.leaf_boards()
+        gpu_z = None
+        if self.lmbda > 0:
+            if self.rollout_device == "gpu":
+                gpu_z = self._gpu_rollouts(s, boards)
+            else:
+                s.start_rollouts()  # native threads, overlapped with the network pass
+        priors, values = self.evaluator(boards)
+        if gpu_z is not None:
+            s.set_rollout_results(gpu_z.result())
+        s.backup(priors, values)
+        self.stats["waves"] += 1
+        self.stats["sims"] += n
+        return n
+
+    def _gpu_rollouts(self, s, boards):
+        if self._gpu_rollout is None:
+            from .gpu_rollout import GpuRollouts
+            self._gpu_rollout = GpuRollouts(self.rollout, torch.device("cuda"))
+        return self._gpu_rollout.launch(s, self.rollouts_per_leaf, self.rollout_limit,
+                                        seed=self.seed + self.stats["waves"])
+
+    def search(self, state, n_playout=None):
+        s = self._sync_root(state)
+        target = s.root_visits + (n_playout or self.n_playout)
+        stall = 0
+        while s.root_visits < target:
+            want = min(self.batch, target - s.root_visits)
+            before = s.root_visits
+            self._wave(s, want)
+            stall = stall + 1 if s.root_visits == before else 0
+            if stall > 3:
+                break
+        return s
+
+    def get_move(self, state):
+        s = self.search(state)
+        a = s.best_move()
+        return PASS_MOVE if a < 0 else divmod(int(a), state.size)
+
+    def root_statistics(self):
+        """(moves, visits, Q, prior) of the root children."""
+        return self._search.root_stats()
+
+    def update_with_move(self, last_move):
+        s = self._search
+        if s is None:
+            return
+        flat = -1 if last_move is PASS_MOVE else last_move[0] * s.root_board.size + last_move[1]
+        try:
+            s.advance(flat)
+            self._history = (self._history or []) + [last_move]
+        except Exception:
+            self._search = None
+            self._history = None
+
+
+class ParallelMCTSPlayer(object):
+    """Player wrapper (reference ai.py:136-149 MCTSPlayer shape) around ParallelMCTS."""
+
+    def __init__(self, policy=None, value=None, rollout=None, lmbda=0.5, c_puct=5,
+                 rollout_limit=500, playout_depth=722, n_playout=1600, **kw):
+        self.mcts = ParallelMCTS(policy, value, rollout, lmbda, c_puct, n_playout,
+                                 rollout_limit=rollout_limit, playout_depth=playout_depth, **kw)
+
+    def get_move(self, state):
+        sensible = state.get_legal_moves(include_eyes=False)
+        if len(sensible) == 0:
+            return PASS_MOVE
+        move = self.mcts.get_move(state)
+        self.mcts.update_with_move(move)
+        return move
