@@ -1,0 +1,87 @@
+"""APV-MCTS throughput (BASELINE config #5): simulations/s of the full search on 19x19 —
+north-star policy (48 planes, 192 filters, 12+1 layers) + value net (49 planes, same trunk, FC256,
+tanh) evaluated on the GPU for every wave of leaves, fast rollouts on the GPU (rollout kernel,
+``--rollouts-per-leaf`` games per leaf), lambda = 0.5, random-init weights, from the empty board.
+
+  python benchmarks/mcts_bench.py [--playouts 8192] [--batch 256] [--rollout-device gpu|cpu]
+
+One JSON line: sims/s, leaf evals/s, rollouts/s and the per-phase time split.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def build_search(device, filters=192, layers=12, batch=256, rollout_device="gpu",
+                 rollouts_per_leaf=4, lmbda=0.5, nthreads=16, seed=1):
+    from rocalphago_amd.features.preprocessing import DEFAULT_FEATURES
+    from rocalphago_amd.models.policy import CNNPolicy
+    from rocalphago_amd.models.value import CNNValue
+    from rocalphago_amd.search.apv import ParallelMCTS
+    pol = CNNPolicy(DEFAULT_FEATURES, board=19, filters_per_layer=filters, layers=layers,
+                    device=device, seed=seed)
+    val = CNNValue(DEFAULT_FEATURES + ["color"], board=19, filters_per_layer=filters,
+                   layers=layers, device=device, seed=seed + 1)
+    return ParallelMCTS(pol, val, lmbda=lmbda, batch=batch, rollout_device=rollout_device,
+                        rollouts_per_leaf=rollouts_per_leaf, nthreads=nthreads, seed=seed)
+
+
+def measure(device, playouts=8192, warmup=512, moves=1, **kw):
+    import torch
+    from rocalphago_amd.engine.gamestate import GameState
+    mc = build_search(device, **kw)
+    mc.n_playout = playouts
+    st = GameState()
+    mc.search(st, warmup)  # compiles / allocates; discarded tree
+    mc._search = None
+    mc.stats = {"waves": 0, "sims": 0}
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(moves):
+        mv = mc.get_move(st)
+        st.do_move(mv)
+        mc.update_with_move(mv)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    s = mc.stats
+    out = {"sims_per_s": s["sims"] / dt, "sims": s["sims"], "seconds": dt,
+           "waves": s["waves"], "batch": mc.batch, "rollouts_per_leaf": mc.rollouts_per_leaf,
+           "rollout_device": mc.rollout_device}
+    if mc.lmbda > 0:
+        out["rollouts_per_s"] = s["sims"] * (mc.rollouts_per_leaf if mc.rollout_device == "gpu"
+                                             else 1) / dt
+    for k in ("t_select", "t_eval", "t_rollout_wait", "t_backup"):
+        out[k + "_frac"] = round(s.get(k, 0.0) / dt, 3)
+    return out
+
+
+def measure_sims_per_s(device, **kw):
+    return measure(device, **kw)["sims_per_s"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--playouts", type=int, default=8192)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--rollout-device", default="gpu", choices=["gpu", "cpu"])
+    ap.add_argument("--rollouts-per-leaf", type=int, default=4)
+    ap.add_argument("--lmbda", type=float, default=0.5)
+    ap.add_argument("--filters", type=int, default=192)
+    ap.add_argument("--threads", type=int, default=16)
+    args = ap.parse_args()
+    import torch
+    dev = torch.device("cuda")
+    r = measure(dev, playouts=args.playouts, batch=args.batch,
+                rollout_device=args.rollout_device, rollouts_per_leaf=args.rollouts_per_leaf,
+                lmbda=args.lmbda, filters=args.filters, nthreads=args.threads)
+    r.update({"metric": "MCTS simulations/s (19x19 APV-MCTS, policy+value on GPU)",
+              "model": "policy 48x192x13 + value 49x192x13+FC256", "lmbda": args.lmbda})
+    print(json.dumps({k: (round(v, 2) if isinstance(v, float) else v) for k, v in r.items()}))
+
+
+if __name__ == "__main__":
+    main()

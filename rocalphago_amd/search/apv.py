@@ -16,6 +16,8 @@ full search, built for a GPU evaluator:
 ``ParallelMCTS(policy, value=None, ...)`` mirrors the reference MCTS interface
 (``get_move(state)``, ``update_with_move(move)``); ``ParallelMCTSPlayer`` mirrors MCTSPlayer.
 """
+import time
+
 import numpy as np
 import torch
 
@@ -123,10 +125,12 @@ class ParallelMCTS(object):
 
     # ------------------------------------------------------------------ search
     def _wave(self, s, want):
+        t0 = time.perf_counter()
         n = s.select(want)
         if n == 0:
             return 0
         boards = s.leaf_boards()
+        t1 = time.perf_counter()
         gpu_z = None
         if self.lmbda > 0:
             if self.rollout_device == "gpu":
@@ -134,11 +138,19 @@ class ParallelMCTS(object):
             else:
                 s.start_rollouts()  # native threads, overlapped with the network pass
         priors, values = self.evaluator(boards)
+        t2 = time.perf_counter()
         if gpu_z is not None:
             s.set_rollout_results(gpu_z.result())
+        t3 = time.perf_counter()
         s.backup(priors, values)
-        self.stats["waves"] += 1
-        self.stats["sims"] += n
+        t4 = time.perf_counter()
+        st = self.stats
+        st["waves"] += 1
+        st["sims"] += n
+        st["t_select"] = st.get("t_select", 0.0) + (t1 - t0)
+        st["t_eval"] = st.get("t_eval", 0.0) + (t2 - t1)
+        st["t_rollout_wait"] = st.get("t_rollout_wait", 0.0) + (t3 - t2)
+        st["t_backup"] = st.get("t_backup", 0.0) + (t4 - t3)
         return n
 
     def _gpu_rollouts(self, s, boards):

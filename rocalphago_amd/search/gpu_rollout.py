@@ -1,0 +1,100 @@
+"""GPU fast rollouts (csrc/hip/rollout.hip): thousands of playouts per launch, one wavefront per
+game, on a side HIP stream so they overlap the policy/value network pass of the same wave."""
+import ctypes
+
+import numpy as np
+import torch
+
+from ..ops.hipops import _check, _lib, _ptr
+
+
+class _Pending(object):
+    def __init__(self, event, winners, n, R):
+        self.event = event
+        self.winners = winners
+        self.n = n
+        self.R = R
+
+    def result(self):
+        """Mean result per leaf from BLACK's point of view, numpy float32 [n]."""
+        self.event.synchronize()
+        w = self.winners.view(self.n, self.R).float().mean(1)
+        return w.cpu().numpy()
+
+
+class GpuRollouts(object):
+    def __init__(self, policy, device=None):
+        self.device = torch.device(device or "cuda")
+        self.stream = torch.cuda.Stream(self.device)
+        self.set_policy(policy)
+
+    def set_policy(self, policy):
+        self.w = torch.tensor(np.asarray(policy.weights, np.float32), device=self.device)
+        self.pattern = torch.tensor(np.asarray(policy.pattern, np.float32), device=self.device)
+
+    def _launch(self, colors, meta, S, komi, R, limit, seed, length=False, dbg=False):
+        n = colors.shape[0]
+        games = n * R
+        winners = torch.empty(games, dtype=torch.int8, device=self.device)
+        lengths = torch.empty(games, dtype=torch.int16, device=self.device) if length else None
+        logits = torch.empty(games, S * S, dtype=torch.float32, device=self.device) \
+            if dbg else None
+        cur = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            c = torch.from_numpy(np.ascontiguousarray(colors, np.int8)).pin_memory() \
+                .to(self.device, non_blocking=True)
+            m = torch.from_numpy(np.ascontiguousarray(meta, np.int32)).pin_memory() \
+                .to(self.device, non_blocking=True)
+            _check(_lib().rag_rollouts(_ptr(c), _ptr(m), n, R, S, float(komi), int(limit),
+                                       _ptr(self.w), _ptr(self.pattern),
+                                       ctypes.c_uint(seed & 0xFFFFFFFF), _ptr(winners),
+                                       _ptr(lengths), _ptr(logits),
+                                       ctypes.c_void_p(self.stream.cuda_stream)),
+                   "rollouts")
+            # keep the staged inputs alive until the kernel has consumed them
+            c.record_stream(self.stream)
+            m.record_stream(self.stream)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        return ev, winners, lengths, logits
+
+    def launch(self, search, R, limit, seed=1):
+        """Start R playouts for every pending leaf of a native Search (non-blocking)."""
+        colors, meta = search.rollout_inputs()
+        b = search.root_board
+        ev, winners, _, _ = self._launch(colors, meta, b.size, b.komi, R, limit, seed)
+        return _Pending(ev, winners, colors.shape[0], R)
+
+    # ---------------------------------------------------------------- direct use / tests
+    @staticmethod
+    def encode(states):
+        """GameStates -> (colors [n, S*S] int8, meta [n, 8] int32)."""
+        S = states[0].size
+        colors = np.zeros((len(states), S * S), np.int8)
+        meta = np.zeros((len(states), 8), np.int32)
+        for i, st in enumerate(states):
+            b = st.native
+            colors[i] = np.asarray(b.board(), np.int8).reshape(-1)
+            l1, l2 = b.last_moves
+            meta[i] = [b.current_player, b.ko, l1, l2, b.passes_black, b.passes_white,
+                       b.move_count, int(b.end_of_game)]
+        return colors, meta
+
+    def run(self, states, R=1, limit=500, seed=1):
+        """(winners [n, R] int8, lengths [n, R] int16) as numpy."""
+        colors, meta = self.encode(states)
+        ev, w, ln, _ = self._launch(colors, meta, states[0].size, states[0].komi, R, limit,
+                                    seed, length=True)
+        ev.synchronize()
+        n = len(states)
+        return w.view(n, R).cpu().numpy(), ln.view(n, R).cpu().numpy()
+
+    def initial_logits(self, states):
+        """Debug: candidate logits at each state's position ([n, S*S], -inf = not a legal
+        candidate), for parity with RolloutPolicy.candidates."""
+        colors, meta = self.encode(states)
+        ev, _, _, lg = self._launch(colors, meta, states[0].size, states[0].komi, 1, 0, 1,
+                                    dbg=True)
+        ev.synchronize()
+        return lg.cpu().numpy()
