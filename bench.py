@@ -23,6 +23,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PAPER_SL_POSITIONS_PER_S = 3000.0  # paper-derived SL throughput (50 GPUs)
+PAPER_VALUE_POSITIONS_PER_S = 2600.0  # paper-derived value-net throughput
 
 
 def _free_port():
@@ -42,7 +43,11 @@ def main():
     ap.add_argument("--filters", type=int, default=192)
     ap.add_argument("--layers", type=int, default=12)
     ap.add_argument("--dataset", type=int, default=65536, help="synthetic positions per GPU")
-    ap.add_argument("--mcts", action="store_true", help="also measure APV-MCTS sims/s")
+    ap.add_argument("--model", default="policy", choices=["policy", "value"],
+                    help="policy: SL policy net (headline); value: value net (BASELINE config 4)")
+    ap.add_argument("--no-mcts", action="store_true",
+                    help="skip the APV-MCTS sims/s measurement (run after the timed SL steps)")
+    ap.add_argument("--mcts-playouts", type=int, default=4096)
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -66,22 +71,39 @@ def main():
     if dev.type != "cuda":
         raise SystemExit("bench.py needs a GPU")
     torch.manual_seed(1234)
-    policy = CNNPolicy(DEFAULT_FEATURES, board=19, filters_per_layer=args.filters,
-                       layers=args.layers, device=dev, seed=1234)
-    model = policy.model
-    dp.broadcast_model(model)
-    model.compile(loss="categorical_crossentropy", optimizer=K.SGD(lr=0.003, decay=0.0001),
-                  metrics=["accuracy"])
-    nparams = sum(int(w.numel()) for w in model.net._views)
-    ds = DeviceDataset.synthetic(args.dataset, 48, 19, dev, seed=17 + dp.rank)
-    trainer = SupervisedTrainer(model, ds, args.batch, TRANSFORM_NAMES, dp, seed=5)
-    if trainer.plan is None:
-        raise SystemExit("HIP fused plan not active for the policy network")
     gen = torch.Generator(device=dev)
     gen.manual_seed(99 + dp.rank)
+    if args.model == "policy":
+        policy = CNNPolicy(DEFAULT_FEATURES, board=19, filters_per_layer=args.filters,
+                           layers=args.layers, device=dev, seed=1234)
+        model = policy.model
+        dp.broadcast_model(model)
+        model.compile(loss="categorical_crossentropy", optimizer=K.SGD(lr=0.003, decay=0.0001),
+                      metrics=["accuracy"])
+        ds = DeviceDataset.synthetic(args.dataset, 48, 19, dev, seed=17 + dp.rank)
+        trainer = SupervisedTrainer(model, ds, args.batch, TRANSFORM_NAMES, dp, seed=5)
+        N = ds.N
+    else:
+        from rocalphago_amd.features.preprocessing import VALUE_FEATURES
+        from rocalphago_amd.models.value import CNNValue
+        from rocalphago_amd.training.value_trainer import ValueTrainer
+        value = CNNValue(VALUE_FEATURES, board=19, filters_per_layer=args.filters,
+                         layers=args.layers, device=dev, seed=1234)
+        model = value.model
+        dp.broadcast_model(model)
+        model.compile(loss="mse", optimizer=K.SGD(lr=0.003, decay=8.664339379294006e-08))
+        g = torch.Generator(device=dev)
+        g.manual_seed(17 + dp.rank)
+        N = args.dataset
+        states = (torch.rand((N, 49, 19, 19), generator=g, device=dev) < 0.3).to(torch.uint8)
+        values = (torch.randint(0, 2, (N, 1), generator=g, device=dev) * 2 - 1).float()
+        trainer = ValueTrainer(model, states, values, args.batch, TRANSFORM_NAMES, dp, seed=5)
+    nparams = sum(int(w.numel()) for w in model.net._views)
+    if trainer.plan is None:
+        raise SystemExit("HIP fused plan not active for the %s network" % args.model)
 
     def step():
-        idx = torch.randint(0, ds.N, (args.batch,), generator=gen, device=dev)
+        idx = torch.randint(0, N, (args.batch,), generator=gen, device=dev)
         trainer.step(idx)
 
     for _ in range(args.warmup):
@@ -95,12 +117,15 @@ def main():
     dp.barrier()
     dt = time.perf_counter() - t0
     dt = dp.max_scalar(dt)
-    loss, acc = trainer.pop_metrics()
+    if args.model == "policy":
+        loss, acc = trainer.pop_metrics()
+    else:
+        loss = trainer.pop_loss()
     ms = dt / args.steps * 1e3
     value = dp.world * args.batch * args.steps / dt
     result = {
         # BASELINE.json's headline metric; value = the SL-policy training positions/s half
-        # (MCTS sims/s is reported alongside with --mcts)
+        # (MCTS sims/s is reported alongside, measured after the timed SL region)
         "metric": "positions/sec SL-policy train + MCTS sims/sec (19x19) at 1/2/4/8 MI355X",
         "value": round(value, 1),
         "unit": "positions/s",
@@ -123,10 +148,28 @@ def main():
         "baseline_note": "vs_baseline = value / 3000 positions/s (paper-derived SL throughput, "
                          "BASELINE.md; the reference publishes no numbers)",
     }
-    if args.mcts and dp.is_root:
+    if args.model == "value":
+        result["metric"] = "positions/sec value-net train (19x19) at 1/2/4/8 MI355X"
+        result["vs_baseline"] = round(value / PAPER_VALUE_POSITIONS_PER_S, 2)
+        result["data"] = "synthetic (random 49-plane 19x19 uint8 positions, +-1 outcomes, " \
+                         "device-resident, random dihedral augmentation); random-init weights"
+        result["config"]["model"] = "19x19 value net (49 planes, %d filters, 13 conv layers, " \
+                                    "FC256 + tanh, MSE), %d params" % (args.filters, nparams)
+        result["baseline_note"] = "vs_baseline = value / 2600 positions/s (paper-derived value " \
+                                  "training throughput, BASELINE.md)"
+    if not args.no_mcts and args.model == "policy":
+        # one independent search per GPU (root parallelism); whole-job sims/s = sum over ranks
         try:
-            from benchmarks.mcts_bench import measure_sims_per_s
-            result["mcts_sims_per_s"] = round(measure_sims_per_s(dev), 1)
+            from benchmarks.mcts_bench import measure
+            r = measure(dev, playouts=args.mcts_playouts)
+            tot = torch.tensor([r["sims_per_s"], r.get("rollouts_per_s", 0.0)], device=dev)
+            dp.allreduce_sum_(tot)
+            result["mcts_sims_per_s"] = round(float(tot[0]), 1)
+            result["mcts_rollouts_per_s"] = round(float(tot[1]), 1)
+            result["mcts_config"] = "APV-MCTS 19x19, policy 48x192x13 + value 49x192x13+FC256 " \
+                                    "on GPU, lambda 0.5, %d GPU rollouts/leaf, wave %d, %d " \
+                                    "playouts/move" % (r["rollouts_per_leaf"], r["batch"],
+                                                       args.mcts_playouts)
         except Exception as e:  # the SL metric stands on its own
             result["mcts_error"] = str(e)[:200]
     if dp.is_root:

@@ -37,20 +37,32 @@ class NetworkEvaluator(object):
         self.pfids = policy.preprocessor.feature_ids if policy is not None else None
         self.vfids = value.preprocessor.feature_ids if value is not None else None
 
-    def _run(self, net, fids, boards):
-        x = _rg.batch_features(boards, fids, self.nthreads)
-        return net.model.predict(x)
+        # the value planes usually extend the policy planes (DEFAULT_FEATURES + color): then
+        # one native extraction feeds both networks
+        self.shared = (self.pfids is not None and self.vfids is not None and
+                       list(self.vfids[:len(self.pfids)]) == list(self.pfids))
+        if self.shared:
+            self.npol = sum(_rg.feature_planes(f) for f in self.pfids)
 
     def __call__(self, boards):
         n = len(boards)
         priors = values = None
         if n == 0:
             return priors, values
+        if self.shared:
+            x = _rg.batch_features(boards, self.vfids, self.nthreads)
+            xp = x[:, :self.npol]
+            xv = x
+        else:
+            xp = _rg.batch_features(boards, self.pfids, self.nthreads) \
+                if self.policy is not None else None
+            xv = _rg.batch_features(boards, self.vfids, self.nthreads) \
+                if self.value is not None else None
         if self.policy is not None:
-            priors = np.ascontiguousarray(self._run(self.policy, self.pfids, boards),
+            priors = np.ascontiguousarray(self.policy.model.predict(np.ascontiguousarray(xp)),
                                           dtype=np.float32)
         if self.value is not None:
-            values = np.ascontiguousarray(self._run(self.value, self.vfids, boards),
+            values = np.ascontiguousarray(self.value.model.predict(xv),
                                           dtype=np.float32).reshape(-1)
         return priors, values
 
