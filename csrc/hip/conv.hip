@@ -27,11 +27,11 @@ constexpr int kBM = 128;  // pixels per block
 constexpr int kBK = 32;   // K per step (one MFMA)
 
 template <int KS, int NT>
-__global__ void __launch_bounds__(256, 2)
+__global__ void __launch_bounds__(256, 3)
 conv_igemm_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                   const float* __restrict__ bias, bf16* __restrict__ Y,
                   const bf16* __restrict__ mask, int M, int S, int WI, int shift, int WO, int HO,
-                  int CIN, int WROWS, int YC, int relu) {
+                  int CIN, int WROWS, int YC, int relu, int HM) {
   constexpr int BN = 32 * NT;
   constexpr int WN = 16 * NT;
   constexpr int STAGE = (kBM + BN) * kBK;  // bf16 elements per stage
@@ -131,6 +131,8 @@ conv_igemm_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
     const int pi = rem / S;
     const int pj = rem - pi * S;
     const size_t orow = (size_t)((b * WO + pi + HO) * WO + pj + HO) * YC;
+    const int WM = S + 2 * HM;  // the mask (layer input) may use its own halo
+    const size_t mrow = (size_t)((b * WM + pi + HM) * WM + pj + HM) * YC;
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       const int n = n0 + wn * WN + j * 16 + fq * 4;
@@ -149,7 +151,7 @@ conv_igemm_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
         for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
       }
       if (mask) {
-        const bf16x4 mk = *reinterpret_cast<const bf16x4*>(mask + orow + n);
+        const bf16x4 mk = *reinterpret_cast<const bf16x4*>(mask + mrow + n);
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = ((float)mk[r] > 0.f) ? v[r] : 0.f;
       }
@@ -347,21 +349,41 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ part, const float*
                                     float* __restrict__ dW, float* __restrict__ db, int nchunks,
                                     int taps, int COUT, int CIN, int COUTP, int CINP, int KS,
                                     int accumulate) {
-  const int total = COUT * CIN * taps;
+  // Threads walk the slab in its own [tap][n][c] order, 4 channels (16 B) per thread, so every
+  // chunk read is a coalesced float4 stream; the (4x smaller) OIHW writes are the scattered side.
   const size_t slab = (size_t)taps * COUTP * CINP;
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total + COUT;
-       idx += gridDim.x * blockDim.x) {
-    if (idx < total) {
-      // OIHW: idx = (n*CIN + c)*taps + tap
-      const int tap = idx % taps;
-      const int nc = idx / taps;
-      const int c = nc % CIN, n = nc / CIN;
-      const size_t off = ((size_t)tap * COUTP + n) * CINP + c;
-      float s = 0.f;
-      for (int k = 0; k < nchunks; ++k) s += part[k * slab + off];
-      dW[idx] = accumulate ? dW[idx] + s : s;
+  const int quads = (int)(slab / 4);
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < quads + COUTP;
+       q += gridDim.x * blockDim.x) {
+    if (q < quads) {
+      const size_t off = (size_t)q * 4;
+      const int c = (int)(off % CINP);
+      const int tn = (int)(off / CINP);
+      const int n = tn % COUTP, tap = tn / COUTP;
+      if (n >= COUT || c >= CIN) continue;
+      const float4* p = reinterpret_cast<const float4*>(part + off);
+      const size_t st = slab / 4;
+      float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
+      int k = 0;
+      for (; k + 1 < nchunks; k += 2) {
+        const float4 a = p[k * st], b = p[(k + 1) * st];
+        s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
+        s1.x += b.x; s1.y += b.y; s1.z += b.z; s1.w += b.w;
+      }
+      if (k < nchunks) {
+        const float4 a = p[k * st];
+        s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
+      }
+      const float v[4] = {s0.x + s1.x, s0.y + s1.y, s0.z + s1.z, s0.w + s1.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (c + j >= CIN) break;
+        const size_t o = ((size_t)n * CIN + c + j) * taps + tap;  // OIHW
+        dW[o] = accumulate ? dW[o] + v[j] : v[j];
+      }
     } else if (db && bpart) {
-      const int n = idx - total;
+      const int n = q - quads;
+      if (n >= COUT) continue;
       float s = 0.f;
       for (int k = 0; k < nchunks; ++k) s += bpart[(size_t)k * COUTP + n];
       db[n] = accumulate ? db[n] + s : s;
@@ -469,12 +491,12 @@ __global__ void pack_nchw_kernel(const float* __restrict__ in, bf16* __restrict_
 template <int KS>
 void launch_igemm_ks(int nt, dim3 grid, hipStream_t st, const bf16* X, const bf16* W,
                      const float* bias, bf16* Y, const bf16* mask, int M, int S, int WI,
-                     int shift, int WO, int HO, int CIN, int WROWS, int YC, int relu) {
+                     int shift, int WO, int HO, int CIN, int WROWS, int YC, int relu, int HM) {
   switch (nt) {
 #define RAG_NT(N)                                                                              \
   case N:                                                                                      \
     conv_igemm_kernel<KS, N><<<grid, 256, 0, st>>>(X, W, bias, Y, mask, M, S, WI, shift, WO, \
-                                                   HO, CIN, WROWS, YC, relu);                 \
+                                                   HO, CIN, WROWS, YC, relu, HM);             \
     break;
     RAG_NT(1) RAG_NT(2) RAG_NT(3) RAG_NT(4) RAG_NT(6)
 #undef RAG_NT
@@ -492,12 +514,18 @@ int pick_nt(int coutp) {
 }  // namespace
 
 // ============================================================================= C ABI
+bool rag_conv_pipe_launch(const bf16* x, const bf16* w, const float* bias, bf16* y,
+                          const bf16* mk, int M, int S, int WI, int shift, int WO, int HO,
+                          int CIN, int COUTP, int YC, int KS, int relu, int HM,
+                          hipStream_t stream);  // conv_fwd.hip
+
 // Conv forward / dgrad.  X: padded input (halo HI, CIN channels, CIN % 32 == 0).  W: packed
 // bf16 weights [taps][WROWS][CIN].  Y: padded output (halo HO, YC channels, COUTP % 32 == 0,
-// COUTP <= YC).  bias: fp32 [COUTP] or null.  mask: same layout as Y or null.
+// COUTP <= YC).  bias: fp32 [COUTP] or null.  mask: the dgrad ReLU mask (layer input), null or
+// laid out like Y but with its own halo HM.
 RAG_API int rag_conv_igemm(const void* X, const void* W, const float* bias, void* Y,
                            const void* mask, int B, int S, int HI, int HO, int CIN, int COUTP,
-                           int YC, int KS, int relu, hipStream_t stream) {
+                           int YC, int KS, int relu, int HM, hipStream_t stream) {
   if (CIN % 32 || COUTP % 32 || YC < COUTP || HI < KS / 2) return -1;
   const int M = B * S * S;
   const int nt = pick_nt(COUTP);
@@ -507,11 +535,18 @@ RAG_API int rag_conv_igemm(const void* X, const void* W, const float* bias, void
   const bf16* w = (const bf16*)W;
   bf16* y = (bf16*)Y;
   const bf16* mk = (const bf16*)mask;
+  static const bool use_pipe = [] {
+    const char* e = getenv("RAG_CONV_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  if (use_pipe && rag_conv_pipe_launch(x, w, bias, y, mk, M, S, WI, shift, WO, HO, CIN, COUTP,
+                                       YC, KS, relu, HM, stream))
+    return (int)hipGetLastError();
   switch (KS) {
-    case 1: launch_igemm_ks<1>(nt, grid, stream, x, w, bias, y, mk, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu); break;
-    case 3: launch_igemm_ks<3>(nt, grid, stream, x, w, bias, y, mk, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu); break;
-    case 5: launch_igemm_ks<5>(nt, grid, stream, x, w, bias, y, mk, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu); break;
-    case 7: launch_igemm_ks<7>(nt, grid, stream, x, w, bias, y, mk, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu); break;
+    case 1: launch_igemm_ks<1>(nt, grid, stream, x, w, bias, y, mk, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM); break;
+    case 3: launch_igemm_ks<3>(nt, grid, stream, x, w, bias, y, mk, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM); break;
+    case 5: launch_igemm_ks<5>(nt, grid, stream, x, w, bias, y, mk, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM); break;
+    case 7: launch_igemm_ks<7>(nt, grid, stream, x, w, bias, y, mk, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM); break;
     default: return -2;
   }
   return (int)hipGetLastError();
@@ -629,7 +664,7 @@ RAG_API int rag_conv_wgrad(const void* G, const void* X, float* dW, float* db, f
       default: return -2;
     }
   }
-  const int total = COUT * CIN * taps + COUT;
+  const int total = taps * COUTP * CINP / 4 + COUTP;
   wgrad_reduce_kernel<<<(total + 255) / 256, 256, 0, stream>>>(part, bpart, dW, db, nchunks, taps,
                                                               COUT, CIN, COUTP, CINP, KS,
                                                               accumulate);

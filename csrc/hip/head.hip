@@ -131,23 +131,34 @@ head_bwd_kernel(const bf16* __restrict__ H, const float* __restrict__ w,
   const int pbeg = blockIdx.x * pix_per_block;
   const int pend = min(npix, pbeg + pix_per_block);
   if (sub < PPI) {
-#pragma unroll 4
-    for (int P = pbeg + sub; P < pend; P += PPI) {
-      const int b = P / S2, p = P - (P / S2) * S2;
-      const int i = p / S, j = p - (p / S) * S;
-      const size_t off = ((size_t)(b * WP + i + 1) * WP + j + 1) * KP + ch * 8;
-      const float g = dz[P];
-      const bf16x8 hv = *reinterpret_cast<const bf16x8*>(H + off);
-      bf16x8 o;
+    // 4 pixels per batch: all loads issued before any use (memory-level parallelism)
+    constexpr int U = 4;
+    for (int P0 = pbeg + sub; P0 < pend; P0 += U * PPI) {
+      size_t off[U];
+      float g[U];
+      bf16x8 hv[U];
 #pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        const float hf = (float)hv[t];
-        float d = g * wl[t];
-        if (relu_mask && !(hf > 0.f)) d = 0.f;
-        o[t] = (bf16)d;
-        dwacc[t] += g * hf;
+      for (int u = 0; u < U; ++u) {
+        const int P = min(P0 + u * PPI, pend - 1);
+        const int b = P / S2, p = P - (P / S2) * S2;
+        const int i = p / S, j = p - (p / S) * S;
+        off[u] = ((size_t)(b * WP + i + 1) * WP + j + 1) * KP + ch * 8;
+        g[u] = (P0 + u * PPI < pend) ? dz[P] : 0.f;
+        hv[u] = *reinterpret_cast<const bf16x8*>(H + off[u]);
       }
-      if (dH) *reinterpret_cast<bf16x8*>(dH + off) = o;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        bf16x8 o;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const float hf = (float)hv[u][t];
+          float d = g[u] * wl[t];
+          if (relu_mask && !(hf > 0.f)) d = 0.f;
+          o[t] = (bf16)d;
+          dwacc[t] += g[u] * hf;
+        }
+        if (dH && P0 + u * PPI < pend) *reinterpret_cast<bf16x8*>(dH + off[u]) = o;
+      }
     }
 #pragma unroll
     for (int t = 0; t < 8; ++t) atomicAdd(&dwl[ch * 8 + t], dwacc[t]);  // LDS atomics only

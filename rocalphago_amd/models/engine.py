@@ -50,16 +50,16 @@ class HipTrunk(object):
 
     # ------------------------------------------------------------------ buffers
     def _halos(self):
-        """halo[b] of activation boundary b (acts[b] and the gradient g_{b-1} share it, so the
-        dgrad epilogue can read its ReLU mask in the output layout)."""
+        """halo[b] of activation boundary b: the smallest halo layer b's kernel needs (1 for
+        1x1/3x3, 2 for the 5x5 input layer); the trunk output (read by the heads) has halo 1.
+
+        The gradient g_l (w.r.t. layer l's pre-activation) is stored with the halo of layer l's
+        INPUT, halo[l], not of its output: then G and X of layer l's wgrad share one padded
+        geometry and the all-taps wgrad kernel (wgrad.hip) applies to every layer. The dgrad
+        that produces g_{l-1} reads its ReLU mask (acts[l]) with that tensor's own halo."""
         sp = self.specs
-        # b >= 1 also takes the producing layer's ks//2 so that g_{b-1} (the wgrad G operand of
-        # layer b-1) has the same padded geometry as that layer's input: the all-taps wgrad
-        # kernel then shifts rows instead of gathering them.
-        h = [max(1, sp[0].ks // 2)]
-        for b in range(1, self.L):
-            h.append(max(1, sp[b].ks // 2, sp[b - 1].ks // 2, h[b - 1] if b == 1 else 0))
-        assert self.L == 1 or sp[-1].ks <= 3, "last trunk layer must be 1x1 or 3x3"
+        h = [max(1, s.ks // 2) for s in sp]
+        assert sp[-1].ks <= 3, "last trunk layer must be 1x1 or 3x3 (heads read halo 1)"
         h.append(1)
         return h
 
@@ -75,7 +75,7 @@ class HipTrunk(object):
         self.acts = acts
         self._gbufs = {}
         for l, s in enumerate(self.specs):
-            key = (s.coutp, self.halo[l + 1])
+            key = (s.coutp, self.halo[l])
             if key not in self._gbufs:
                 self._gbufs[key] = [ops.alloc_padded(B, S, key[1], key[0], self.device)
                                     for _ in range(2)]
@@ -94,9 +94,9 @@ class HipTrunk(object):
         return self.acts[-1][:B]
 
     def grad_buffer(self, l, which, B):
-        """g_l = dL/d(pre-activation of layer l), halo of boundary l+1."""
+        """g_l = dL/d(pre-activation of layer l), stored with the halo of layer l's input."""
         s = self.specs[l]
-        return self._gbufs[(s.coutp, self.halo[l + 1])][which][:B]
+        return self._gbufs[(s.coutp, self.halo[l])][which][:B]
 
     # ------------------------------------------------------------------ weights
     def sync_weights(self, weights, biases, version):
@@ -136,16 +136,16 @@ class HipTrunk(object):
             x = self.acts[l][:B]
             ops.conv_wgrad(g, x, dws[l], dbs[l], B, S, self.halo[l], s.cout, s.coutp, s.cin,
                            s.cinp, s.ks, accumulate=accumulate, work=self._work,
-                           hg=self.halo[l + 1])
+                           hg=self.halo[l])
             if on_layer_done is not None:
                 on_layer_done(l)
             if l > 0:
                 below = self.specs[l - 1]
                 which ^= 1
                 gout = self.grad_buffer(l - 1, which, B)
-                ops.conv_igemm(g, self._wb[l], None, gout, B, S, self.halo[l + 1],
-                               self.halo[l], s.coutp, s.cinp, s.ks, False,
-                               mask=x if below.relu else None)
+                ops.conv_igemm(g, self._wb[l], None, gout, B, S, self.halo[l],
+                               self.halo[l - 1], s.coutp, s.cinp, s.ks, False,
+                               mask=x if below.relu else None, mask_halo=self.halo[l])
 
 
 class PolicyHeadEngine(object):

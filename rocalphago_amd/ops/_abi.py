@@ -9,7 +9,7 @@ SZ = C.c_size_t
 
 SIGNATURES = {
     # conv.hip
-    "rag_conv_igemm": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
+    "rag_conv_igemm": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P],
     "rag_conv_wgrad_workspace": [I, I, I, I, I, P],
     "rag_conv_wgrad": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P],
     "rag_pack_weights": [P, P, P, I, I, I, I, I, P],

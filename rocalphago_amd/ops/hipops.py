@@ -52,10 +52,15 @@ def pack_weights(w, coutp, cinp, wf=None, wb=None):
     return wf, wb
 
 
-def conv_igemm(x, wpack, bias, y, B, S, hi, ho, cinp, coutp, ks, relu, mask=None):
-    """y[pad ho] = act(conv_ks(x[pad hi]) + bias) (or the dgrad form with a ReLU mask)."""
+def conv_igemm(x, wpack, bias, y, B, S, hi, ho, cinp, coutp, ks, relu, mask=None,
+               mask_halo=None):
+    """y[pad ho] = act(conv_ks(x[pad hi]) + bias), or the dgrad form with a ReLU mask (the layer
+    input: y's channel count, its own halo ``mask_halo``, default ho)."""
+    hm = ho if mask_halo is None else mask_halo
+    if mask is not None and (mask.shape[1] != S + 2 * hm or mask.shape[-1] != y.shape[-1]):
+        raise ValueError("mask layout does not match (halo %d, %d channels)" % (hm, y.shape[-1]))
     _check(_lib().rag_conv_igemm(_ptr(x), _ptr(wpack), _ptr(bias), _ptr(y), _ptr(mask), B, S, hi,
-                                 ho, cinp, coutp, y.shape[-1], ks, int(relu), _stream()),
+                                 ho, cinp, coutp, y.shape[-1], ks, int(relu), hm, _stream()),
            "conv_igemm")
     return y
 

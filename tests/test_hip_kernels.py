@@ -146,3 +146,24 @@ def test_sgd(ops):
     p2 = p.clone()
     ops.sgd_(p, g, 0.1, momentum=0.9, v=v)
     assert torch.allclose(p, p2 - 0.1 * g, atol=1e-6)
+
+
+def test_dgrad_mixed_halos(ops):
+    """dgrad writing g_{l-1} with the halo of layer l-1's input (2, a 5x5 layer below) while the
+    ReLU mask (layer l's input) keeps halo 1 — the layout the engine uses below the 5x5 layer."""
+    dev = torch.device("cuda")
+    torch.manual_seed(3)
+    B, S, cin, cout, ks = 3, 19, 192, 192, 3
+    x = F.relu(torch.randn(B, cin, S, S, device=dev))
+    w = torch.randn(cout, cin, ks, ks, device=dev) * 0.05
+    g = torch.randn(B, cout, S, S, device=dev)
+    xr, wr = bf(x).requires_grad_(), bf(w)
+    (F.conv2d(xr, wr, padding=1) * bf(g)).sum().backward()
+    _, wb = ops.pack_weights(w, cout, cin, wb=torch.empty(9, cin, cout, dtype=torch.bfloat16,
+                                                          device=dev))
+    gp = ops.pack_nchw(g, 1, cout)
+    xm = ops.pack_nchw(x, 1, cin)
+    dx = ops.alloc_padded(B, S, 2, cin, dev)
+    ops.conv_igemm(gp, wb, None, dx, B, S, 1, 2, cout, cin, ks, False, mask=xm, mask_halo=1)
+    assert rel_err(ops.unpack(dx, cin, 2), xr.grad * (x > 0)) < 2e-2
+    assert dx[:, :2].abs().max().item() == 0 and dx[:, :, -2:].abs().max().item() == 0
