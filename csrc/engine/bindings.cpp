@@ -216,6 +216,63 @@ PYBIND11_MODULE(_rocgo, m) {
       },
       py::arg("boards"), py::arg("fids"), py::arg("nthreads") = 8);
 
+  // Inputs of the GPU feature kernel (csrc/hip/features.hip): colours, stone ages, meta
+  // (player, ko), positional-superko-illegal points (only for boards that enforce superko) and,
+  // when asked, the two ladder planes (native search, threaded) for legal points.
+  m.def(
+      "gpu_feature_inputs",
+      [](const std::vector<const Board*>& boards, bool ladders, int nthreads) {
+        if (boards.empty()) throw std::invalid_argument("empty batch");
+        const int S = boards[0]->size(), P = S * S, B = (int)boards.size();
+        for (auto* b : boards)
+          if (b->size() != S) throw std::invalid_argument("all states must have the same size");
+        py::array_t<int8_t> colors({B, P});
+        py::array_t<int16_t> ages({B, P});
+        py::array_t<int32_t> meta({B, 4});
+        py::array_t<uint8_t> illegal({B, P});
+        py::array_t<uint8_t> lad({ladders ? B : 0, 2, P});
+        int8_t* c = colors.mutable_data();
+        int16_t* a = ages.mutable_data();
+        int32_t* mt = meta.mutable_data();
+        uint8_t* il = illegal.mutable_data();
+        uint8_t* ld = lad.mutable_data();
+        bool any_superko = false;
+        for (auto* b : boards) any_superko |= b->enforce_superko();
+        {
+          py::gil_scoped_release nogil;
+          parallel_for(B, nthreads, [&](int i) {
+            const Board& b = *boards[i];
+            for (int p = 0; p < P; ++p) {
+              c[(size_t)i * P + p] = (int8_t)b.color(p);
+              a[(size_t)i * P + p] = (int16_t)std::min(b.stone_age(p), 32767);
+              il[(size_t)i * P + p] = 0;
+            }
+            mt[i * 4 + 0] = b.current_player();
+            mt[i * 4 + 1] = b.ko();
+            mt[i * 4 + 2] = b.enforce_superko() ? 1 : 0;
+            mt[i * 4 + 3] = 0;
+            if (b.enforce_superko())
+              for (int p = 0; p < P; ++p)
+                if (b.color(p) == EMPTY && p != b.ko() && !b.is_suicide(p) &&
+                    b.is_positional_superko(p))
+                  il[(size_t)i * P + p] = 1;
+            if (ladders) {
+              uint8_t* l0 = ld + (size_t)i * 2 * P;
+              for (int p = 0; p < P; ++p) {
+                l0[p] = 0;
+                l0[P + p] = 0;
+                if (b.color(p) != EMPTY) continue;
+                l0[p] = b.is_ladder_capture(p, -1, 80) ? 1 : 0;
+                l0[P + p] = b.is_ladder_escape(p, -1, 80) ? 1 : 0;
+              }
+            }
+          });
+        }
+        return py::make_tuple(colors, ages, meta, any_superko ? py::object(illegal) : py::none(),
+                              ladders ? py::object(lad) : py::none());
+      },
+      py::arg("boards"), py::arg("ladders") = true, py::arg("nthreads") = 8);
+
   m.def("feature_planes", &feature_planes);
 
   m.def("lzf_decompress", [](py::bytes data, size_t out_size) {

@@ -1,0 +1,421 @@
+// Input feature planes on the GPU: one wavefront builds every plane of one
+// position, bit-exact with the native extractor (csrc/engine/features.cpp, itself pinned to the
+// reference preprocessing.py:14-205 by tests/test_features.py).
+//
+// Per position (LDS, S <= 19):
+//   * colours, stone ages; group labels by min-label propagation over same-coloured neighbours;
+//   * per label: stone count, liberty count, and the group's stone set and liberty set as 361-bit
+//     bitsets (built with LDS 64-bit atomic ORs), so "liberties after playing p" is an exact set
+//     union + popcount per candidate instead of a flood fill;
+//   * each lane then evaluates its points: board / ones / zeros / color / turns_since /
+//     liberties / legal (suicide, ko; superko via a host-provided mask) / capture_size /
+//     self_atari_size / liberties_after (captured stones adjacent to the merged group become
+//     liberties: bitset dilation, only on capturing moves) / sensibleness (the recursive true-eye
+//     rule, as an explicit per-lane DFS with the ancestor stack) / ladder planes (host-provided:
+//     ladder reading is a deep sequential search and stays in the native engine).
+// Output: uint8 [n][F][S*S] in the order of `fids`, the layout batch_features produces.
+#include "common.h"
+
+using namespace rag;
+
+namespace {
+
+constexpr int kFW = 2;    // positions per 128-thread block
+constexpr int kNW = 6;    // 64-bit words of a 361-point set
+constexpr int kPMAX = 384;
+constexpr int kNPL = 6;   // points per lane
+
+// feature ids (csrc/engine/go_engine.hpp FeatureId)
+enum { F_BOARD = 0, F_ONES, F_TURNS_SINCE, F_LIBERTIES, F_CAPTURE_SIZE, F_SELF_ATARI_SIZE,
+       F_LIBERTIES_AFTER, F_LADDER_CAPTURE, F_LADDER_ESCAPE, F_SENSIBLENESS, F_ZEROS, F_LEGAL,
+       F_COLOR };
+
+struct FShared {
+  unsigned long long libbits[kFW][kPMAX][kNW];
+  unsigned long long stonebits[kFW][kPMAX][kNW];
+  int lib[kFW][kPMAX];
+  int gsz[kFW][kPMAX];
+  int16_t lab[kFW][kPMAX];
+  int8_t col[kFW][kPMAX];
+};
+
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+struct Pos {
+  int S, P;
+  const int8_t* col;
+  const int16_t* lab;
+  const int* lib;
+  const int* gsz;
+  const unsigned long long (*libbits)[kNW];
+  const unsigned long long (*stonebits)[kNW];
+
+  __device__ int nb(int p, int k) const {
+    const int x = p / S, y = p - (p / S) * S;
+    switch (k) {
+      case 0: return x > 0 ? p - S : -1;
+      case 1: return x < S - 1 ? p + S : -1;
+      case 2: return y > 0 ? p - 1 : -1;
+      default: return y < S - 1 ? p + 1 : -1;
+    }
+  }
+  // reference diagonal order: (x-1,y-1),(x+1,y+1),(x+1,y-1),(x-1,y+1)
+  __device__ int dg(int p, int k) const {
+    const int x = p / S, y = p - (p / S) * S;
+    const int dx = (k == 0 || k == 3) ? -1 : 1;
+    const int dy = (k == 0 || k == 2) ? -1 : 1;
+    const int ax = x + dx, ay = y + dy;
+    return (ax < 0 || ay < 0 || ax >= S || ay >= S) ? -1 : ax * S + ay;
+  }
+  __device__ int nnb(int p) const {
+    const int x = p / S, y = p - (p / S) * S;
+    return (x > 0) + (x < S - 1) + (y > 0) + (y < S - 1);
+  }
+  __device__ bool eyeish(int p, int owner) const {
+    if (col[p] != 0) return false;
+    for (int k = 0; k < 4; ++k) {
+      const int q = nb(p, k);
+      if (q >= 0 && col[q] != owner) return false;
+    }
+    return true;
+  }
+  // recursive true-eye rule (go.py:298-327) as an explicit DFS; ancestors = frames below top
+  __device__ bool is_eye(int p, int owner) const {
+    if (!eyeish(p, owner)) return false;
+    constexpr int MAXD = 24;
+    int fp[MAXD], fi[MAXD], fb[MAXD];
+    int sp = 0;
+    fp[0] = p;
+    fi[0] = 0;
+    fb[0] = 0;
+    bool ret = true;
+    bool have_ret = false;
+    while (true) {
+      const int cur = fp[sp];
+      const int allow = nnb(cur) == 4 ? 1 : 0;
+      bool done = false;
+      if (have_ret) {
+        have_ret = false;
+        if (!ret) {
+          fb[sp]++;
+          if (fb[sp] > allow) {
+            ret = false;
+            done = true;
+          }
+        }
+      }
+      if (!done) {
+        bool pushed = false;
+        while (fi[sp] < 4) {
+          const int d = dg(cur, fi[sp]++);
+          if (d < 0) continue;
+          if (col[d] == -owner) {
+            if (++fb[sp] > allow) break;
+          } else if (col[d] == 0) {
+            bool anc = false;
+            for (int k = 0; k < sp; ++k) anc |= fp[k] == d;
+            if (anc) continue;
+            if (!eyeish(d, owner)) {
+              if (++fb[sp] > allow) break;
+              continue;
+            }
+            if (sp + 1 >= MAXD) continue;  // deeper than any real board position
+            ++sp;
+            fp[sp] = d;
+            fi[sp] = 0;
+            fb[sp] = 0;
+            pushed = true;
+            break;
+          }
+        }
+        if (pushed) continue;
+        ret = fb[sp] <= allow;
+      }
+      if (sp == 0) return ret;
+      --sp;
+      have_ret = true;
+    }
+  }
+};
+
+// set helpers over kNW words
+__device__ __forceinline__ int popc6(const unsigned long long* s) {
+  int c = 0;
+#pragma unroll
+  for (int k = 0; k < kNW; ++k) c += __popcll(s[k]);
+  return c;
+}
+
+__global__ void __launch_bounds__(64 * kFW)
+features_kernel(const int8_t* __restrict__ colors, const int16_t* __restrict__ ages,
+                const int32_t* __restrict__ meta, const uint8_t* __restrict__ extra_illegal,
+                const uint8_t* __restrict__ ladders, int n_pos, int S, const int* __restrict__ fids,
+                int nf, int F, uint8_t* __restrict__ out) {
+  __shared__ FShared sh;
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int pos = blockIdx.x * kFW + wv;
+  if (pos >= n_pos) return;
+  const int P = S * S;
+  int8_t* col = sh.col[wv];
+  int16_t* lab = sh.lab[wv];
+  int* lib = sh.lib[wv];
+  int* gsz = sh.gsz[wv];
+  Pos g{S, P, col, lab, lib, gsz, sh.libbits[wv], sh.stonebits[wv]};
+  const int me = meta[pos * 4 + 0];
+  const int ko = meta[pos * 4 + 1];
+
+#pragma unroll
+  for (int k = 0; k < kNPL; ++k) {
+    const int p = lane + 64 * k;
+    if (p < P) col[p] = colors[(size_t)pos * P + p];
+  }
+  wsync();
+  // labels: min stone index of the group
+#pragma unroll
+  for (int k = 0; k < kNPL; ++k) {
+    const int p = lane + 64 * k;
+    if (p < P) lab[p] = col[p] ? (int16_t)p : (int16_t)-1;
+  }
+  wsync();
+  for (int it = 0; it < 2 * kPMAX; ++it) {
+    int changed = 0;
+#pragma unroll
+    for (int k = 0; k < kNPL; ++k) {
+      const int p = lane + 64 * k;
+      if (p >= P || col[p] == 0) continue;
+      int m = lab[lab[p]];
+      for (int i = 0; i < 4; ++i) {
+        const int q = g.nb(p, i);
+        if (q >= 0 && col[q] == col[p]) m = min(m, (int)lab[q]);
+      }
+      if (m < lab[p]) {
+        lab[p] = (int16_t)m;
+        changed = 1;
+      }
+    }
+    wsync();
+    if (!__any(changed)) break;
+  }
+  // per-label tables
+#pragma unroll
+  for (int k = 0; k < kNPL; ++k) {
+    const int p = lane + 64 * k;
+    if (p >= P) continue;
+    lib[p] = 0;
+    gsz[p] = 0;
+#pragma unroll
+    for (int w = 0; w < kNW; ++w) {
+      sh.libbits[wv][p][w] = 0ull;
+      sh.stonebits[wv][p][w] = 0ull;
+    }
+  }
+  wsync();
+#pragma unroll
+  for (int k = 0; k < kNPL; ++k) {
+    const int p = lane + 64 * k;
+    if (p >= P) continue;
+    const unsigned long long bit = 1ull << (p & 63);
+    if (col[p] != 0) {
+      const int l = lab[p];
+      atomicAdd(&gsz[l], 1);
+      atomicOr(&sh.stonebits[wv][l][p >> 6], bit);
+    } else {
+      int seen[4], ns = 0;
+      for (int i = 0; i < 4; ++i) {
+        const int q = g.nb(p, i);
+        if (q < 0 || col[q] == 0) continue;
+        const int l = lab[q];
+        bool dup = false;
+        for (int j = 0; j < ns; ++j) dup |= seen[j] == l;
+        if (dup) continue;
+        seen[ns++] = l;
+        atomicAdd(&lib[l], 1);
+        atomicOr(&sh.libbits[wv][l][p >> 6], bit);
+      }
+    }
+  }
+  wsync();
+
+  // plane offsets of the requested features
+  uint8_t* o = out + (size_t)pos * F * P;
+#pragma unroll 1
+  for (int k = 0; k < kNPL; ++k) {
+    const int p = lane + 64 * k;
+    if (p >= P) continue;
+    const int c = col[p];
+    // ---- legality, captures and the simulated move
+    int own_l[4], cap_l[4], nown = 0, ncap = 0, empty_nb = 0;
+    bool own_multi = false;
+    for (int i = 0; i < 4; ++i) {
+      const int q = g.nb(p, i);
+      if (q < 0) continue;
+      const int cq = col[q];
+      if (cq == 0) {
+        ++empty_nb;
+        continue;
+      }
+      const int l = lab[q];
+      if (cq == me) {
+        if (lib[l] > 1) own_multi = true;
+        bool dup = false;
+        for (int j = 0; j < nown; ++j) dup |= own_l[j] == l;
+        if (!dup) own_l[nown++] = l;
+      } else if (lib[l] == 1) {
+        bool dup = false;
+        for (int j = 0; j < ncap; ++j) dup |= cap_l[j] == l;
+        if (!dup) cap_l[ncap++] = l;
+      }
+    }
+    const bool suicide = empty_nb == 0 && !own_multi && ncap == 0;
+    const bool legal = c == 0 && p != ko && !suicide &&
+                       !(extra_illegal && extra_illegal[(size_t)pos * P + p]);
+    int cap_size = 0;
+    for (int j = 0; j < ncap; ++j) cap_size += gsz[cap_l[j]];
+    int libs_after = 0, size_after = 1;
+    bool need_after = false;
+    for (int fi = 0; fi < nf; ++fi)
+      need_after |= fids[fi] == F_SELF_ATARI_SIZE || fids[fi] == F_LIBERTIES_AFTER;
+    if (legal && need_after) {
+      unsigned long long ls[kNW];
+#pragma unroll
+      for (int w = 0; w < kNW; ++w) ls[w] = 0ull;
+      for (int i = 0; i < 4; ++i) {
+        const int q = g.nb(p, i);
+        if (q >= 0 && col[q] == 0) ls[q >> 6] |= 1ull << (q & 63);
+      }
+      for (int j = 0; j < nown; ++j) {
+        size_after += gsz[own_l[j]];
+#pragma unroll
+        for (int w = 0; w < kNW; ++w) ls[w] |= sh.libbits[wv][own_l[j]][w];
+      }
+      if (ncap > 0) {
+        unsigned long long grp[kNW], cap[kNW];
+#pragma unroll
+        for (int w = 0; w < kNW; ++w) {
+          grp[w] = 0ull;
+          cap[w] = 0ull;
+        }
+        grp[p >> 6] |= 1ull << (p & 63);
+        for (int j = 0; j < nown; ++j)
+#pragma unroll
+          for (int w = 0; w < kNW; ++w) grp[w] |= sh.stonebits[wv][own_l[j]][w];
+        for (int j = 0; j < ncap; ++j)
+#pragma unroll
+          for (int w = 0; w < kNW; ++w) cap[w] |= sh.stonebits[wv][cap_l[j]][w];
+        // captured stones orthogonally adjacent to the merged group become liberties
+#pragma unroll
+        for (int w = 0; w < kNW; ++w) {
+          unsigned long long m = cap[w];
+          while (m) {
+            const int s = w * 64 + __builtin_ctzll(m);
+            m &= m - 1;
+            bool adj = false;
+            for (int i = 0; i < 4; ++i) {
+              const int q = g.nb(s, i);
+              adj |= q >= 0 && ((grp[q >> 6] >> (q & 63)) & 1ull);
+            }
+            if (adj) ls[w] |= 1ull << (s & 63);
+          }
+        }
+      }
+      ls[p >> 6] &= ~(1ull << (p & 63));
+      libs_after = popc6(ls);
+    }
+    // ---- write the planes
+    int base = 0;
+    for (int fi = 0; fi < nf; ++fi) {
+      const int f = fids[fi];
+      uint8_t* op = o + (size_t)base * P + p;
+      switch (f) {
+        case F_BOARD:
+          op[0] = c == me;
+          op[P] = c == -me;
+          op[2 * P] = c == 0;
+          base += 3;
+          break;
+        case F_ONES:
+          op[0] = 1;
+          base += 1;
+          break;
+        case F_ZEROS:
+          op[0] = 0;
+          base += 1;
+          break;
+        case F_COLOR:
+          op[0] = me == 1;
+          base += 1;
+          break;
+        case F_TURNS_SINCE: {
+          const int a = ages[(size_t)pos * P + p];
+          for (int t = 0; t < 8; ++t) op[t * P] = (a >= 0 && min(a, 7) == t);
+          base += 8;
+          break;
+        }
+        case F_LIBERTIES: {
+          const int l = c ? lib[lab[p]] : -1;
+          for (int t = 0; t < 8; ++t) op[t * P] = (l >= 1 && (l - 1 == t || (t == 7 && l >= 8)));
+          base += 8;
+          break;
+        }
+        case F_CAPTURE_SIZE: {
+          const int idx = min(cap_size, 7);
+          for (int t = 0; t < 8; ++t) op[t * P] = legal && idx == t;
+          base += 8;
+          break;
+        }
+        case F_SELF_ATARI_SIZE: {
+          const int idx = min(size_after - 1, 7);
+          for (int t = 0; t < 8; ++t) op[t * P] = legal && libs_after == 1 && idx == t;
+          base += 8;
+          break;
+        }
+        case F_LIBERTIES_AFTER: {
+          int idx = min(7, libs_after - 1);
+          if (idx < 0) idx += 8;  // python negative index semantics (features.cpp)
+          for (int t = 0; t < 8; ++t) op[t * P] = legal && idx == t;
+          base += 8;
+          break;
+        }
+        case F_LADDER_CAPTURE:
+          op[0] = legal && ladders && ladders[((size_t)pos * 2 + 0) * P + p];
+          base += 1;
+          break;
+        case F_LADDER_ESCAPE:
+          op[0] = legal && ladders && ladders[((size_t)pos * 2 + 1) * P + p];
+          base += 1;
+          break;
+        case F_SENSIBLENESS:
+          op[0] = legal && !g.is_eye(p, me);
+          base += 1;
+          break;
+        case F_LEGAL:
+          op[0] = legal;
+          base += 1;
+          break;
+        default:
+          break;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+// colors [n][S*S] int8, ages [n][S*S] int16 (-1 = empty), meta [n][4] int32 (player to move,
+// ko point, 0, 0), extra_illegal [n][S*S] uint8 or null (positional-superko points),
+// ladders [n][2][S*S] uint8 or null (capture, escape), fids [nf] int32 on the device,
+// out [n][F][S*S] uint8. S <= 19.
+RAG_API int rag_features(const void* colors, const void* ages, const int32_t* meta,
+                         const uint8_t* extra_illegal, const uint8_t* ladders, int n_pos, int S,
+                         const int* fids, int nf, int F, uint8_t* out, hipStream_t stream) {
+  if (S < 2 || S * S > kPMAX || n_pos <= 0) return -1;
+  dim3 grid((n_pos + kFW - 1) / kFW);
+  features_kernel<<<grid, 64 * kFW, 0, stream>>>((const int8_t*)colors, (const int16_t*)ages,
+                                                 meta, extra_illegal, ladders, n_pos, S, fids,
+                                                 nf, F, out);
+  return (int)hipGetLastError();
+}

@@ -26,6 +26,8 @@ SIGNATURES = {
     "rag_sgd": [P, P, P, I64, F, F, F, I, P],
     # rollout.hip
     "rag_rollouts": [P, P, I, I, I, F, I, P, P, C.c_uint, P, P, P, P],
+    # features.hip
+    "rag_features": [P, P, P, P, P, I, I, P, I, I, P, P],
 }
 
 RESTYPES = {"rag_conv_wgrad_workspace": SZ, "rag_head_bwd_workspace": SZ}

@@ -43,6 +43,26 @@ class NetworkEvaluator(object):
                        list(self.vfids[:len(self.pfids)]) == list(self.pfids))
         if self.shared:
             self.npol = sum(_rg.feature_planes(f) for f in self.pfids)
+        # on a GPU the planes are built by the HIP feature kernel (ops/features.py) and never
+        # leave the device
+        net = policy if policy is not None else value
+        self.gpu = None
+        if net is not None and net.model.net.device.type == "cuda":
+            from ..ops.features import GpuFeatures
+            dev = net.model.net.device
+            if self.shared or value is None:
+                self.gpu = {"p": GpuFeatures(value.preprocessor.feature_list if self.shared else
+                                             policy.preprocessor.feature_list, dev, nthreads)}
+            else:
+                self.gpu = {"p": GpuFeatures(policy.preprocessor.feature_list, dev, nthreads)
+                            if policy is not None else None,
+                            "v": GpuFeatures(value.preprocessor.feature_list, dev, nthreads)}
+
+    def _extract(self, fids, key, boards):
+        if self.gpu is not None and self.gpu.get(key) is not None and \
+                self.gpu[key].supports(boards[0].size):
+            return self.gpu[key](boards)
+        return _rg.batch_features(boards, fids, self.nthreads)
 
     def __call__(self, boards):
         n = len(boards)
@@ -50,17 +70,18 @@ class NetworkEvaluator(object):
         if n == 0:
             return priors, values
         if self.shared:
-            x = _rg.batch_features(boards, self.vfids, self.nthreads)
+            x = self._extract(self.vfids, "p", boards)
             xp = x[:, :self.npol]
             xv = x
         else:
-            xp = _rg.batch_features(boards, self.pfids, self.nthreads) \
-                if self.policy is not None else None
-            xv = _rg.batch_features(boards, self.vfids, self.nthreads) \
-                if self.value is not None else None
+            xp = self._extract(self.pfids, "p", boards) if self.policy is not None else None
+            xv = self._extract(self.vfids, "v", boards) if self.value is not None else None
         if self.policy is not None:
-            priors = np.ascontiguousarray(self.policy.model.predict(np.ascontiguousarray(xp)),
-                                          dtype=np.float32)
+            if isinstance(xp, np.ndarray):
+                xp = np.ascontiguousarray(xp)
+            else:
+                xp = xp.contiguous()
+            priors = np.ascontiguousarray(self.policy.model.predict(xp), dtype=np.float32)
         if self.value is not None:
             values = np.ascontiguousarray(self.value.model.predict(xv),
                                           dtype=np.float32).reshape(-1)
