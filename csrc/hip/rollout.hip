@@ -211,7 +211,7 @@ __device__ __forceinline__ float cand_logit(const Game<NPL>& g, int p, int c, in
     }
     pidx |= code << (2 * k);
   }
-  return s + pattern[pidx];
+  return pattern ? s + pattern[pidx] : s;
 }
 
 // meta: [cur, ko, last1, last2, passes_b, passes_w, nmoves, end]

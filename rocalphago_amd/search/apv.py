@@ -23,6 +23,7 @@ import torch
 
 from .._native import engine as _engine
 from ..engine.gamestate import PASS_MOVE
+from ..features.preprocessing import _FID
 
 _rg = _engine()
 
@@ -76,6 +77,19 @@ class NetworkEvaluator(object):
         else:
             xp = self._extract(self.pfids, "p", boards) if self.policy is not None else None
             xv = self._extract(self.vfids, "v", boards) if self.value is not None else None
+        # the sensibleness plane doubles as the expansion move list (saves native move
+        # generation in backup_value)
+        sens = None
+        planes = x if self.shared else (xp if xp is not None else xv)
+        fl = (self.value if self.shared or self.policy is None else self.policy) \
+            .preprocessor.feature_list
+        if "sensibleness" in fl:
+            off = 0
+            for f in fl[:fl.index("sensibleness")]:
+                off += _rg.feature_planes(_FID[f])
+            sens = planes[:, off]
+            sens = sens.reshape(n, -1).cpu().numpy() if not isinstance(sens, np.ndarray) \
+                else np.ascontiguousarray(sens.reshape(n, -1))
         if self.policy is not None:
             if isinstance(xp, np.ndarray):
                 xp = np.ascontiguousarray(xp)
@@ -85,7 +99,7 @@ class NetworkEvaluator(object):
         if self.value is not None:
             values = np.ascontiguousarray(self.value.model.predict(xv),
                                           dtype=np.float32).reshape(-1)
-        return priors, values
+        return priors, values, sens
 
 
 class ParallelMCTS(object):
@@ -98,7 +112,7 @@ class ParallelMCTS(object):
     def __init__(self, policy=None, value=None, rollout=None, lmbda=0.5, c_puct=5.0,
                  n_playout=1600, batch=256, virtual_loss=3, rollout_limit=500,
                  playout_depth=722, nthreads=8, rollout_device="cpu", rollouts_per_leaf=1,
-                 seed=1, evaluator=None):
+                 seed=1, evaluator=None, max_inflight=3):
         if value is None and lmbda < 1:
             lmbda = 1.0
         self.evaluator = evaluator or NetworkEvaluator(policy, value, nthreads)
@@ -117,6 +131,8 @@ class ParallelMCTS(object):
         self._search = None
         self._history = None
         self._gpu_rollout = None
+        self._inflight = []
+        self.max_inflight = max_inflight
         self.stats = {"waves": 0, "sims": 0}
 
     # ------------------------------------------------------------------ tree management
@@ -126,7 +142,6 @@ class ParallelMCTS(object):
         s.n_vl = self.virtual_loss
         s.rollout_limit = self.rollout_limit
         s.max_depth = self.playout_depth
-        s.nthreads = self.nthreads
         s.seed = self.seed
         s.set_rollout_policy(self.rollout)
 
@@ -150,48 +165,68 @@ class ParallelMCTS(object):
                     s.root_board.current_player == state.current_player:
                 self._history = hist
                 return s
-        s = _rg.Search(state.native)
+        s = _rg.Search(state.native, self.nthreads)
         self._configure(s)
         self._search = s
         self._history = hist
         return s
 
     # ------------------------------------------------------------------ search
+    def _acc(self, key, dt):
+        self.stats[key] = self.stats.get(key, 0.0) + dt
+
     def _wave(self, s, want):
+        """One wave: select, (launch rollouts), evaluate, value backup. GPU rollouts stay in
+        flight (up to ``max_inflight`` waves) and are backed up as they finish."""
         t0 = time.perf_counter()
-        n = s.select(want)
+        wid, n = s.select(want)
         if n == 0:
             return 0
-        boards = s.leaf_boards()
+        boards = s.leaf_boards(wid)
         t1 = time.perf_counter()
-        gpu_z = None
+        pending = None
         if self.lmbda > 0:
             if self.rollout_device == "gpu":
-                gpu_z = self._gpu_rollouts(s, boards)
+                pending = self._gpu_rollouts(s, wid)
             else:
-                s.start_rollouts()  # native threads, overlapped with the network pass
-        priors, values = self.evaluator(boards)
+                s.start_rollouts(wid)  # native pool, overlapped with the network pass
+        res = self.evaluator(boards)
+        priors, values = res[0], res[1]
+        sens = res[2] if len(res) > 2 else None
         t2 = time.perf_counter()
-        if gpu_z is not None:
-            s.set_rollout_results(gpu_z.result())
+        s.backup_value(wid, priors, values, sens)
         t3 = time.perf_counter()
-        s.backup(priors, values)
+        if self.lmbda > 0:
+            if pending is None:
+                s.finish_rollouts(wid)
+            else:
+                self._inflight.append((wid, pending))
+                self._harvest(s, self.max_inflight)
         t4 = time.perf_counter()
-        st = self.stats
-        st["waves"] += 1
-        st["sims"] += n
-        st["t_select"] = st.get("t_select", 0.0) + (t1 - t0)
-        st["t_eval"] = st.get("t_eval", 0.0) + (t2 - t1)
-        st["t_rollout_wait"] = st.get("t_rollout_wait", 0.0) + (t3 - t2)
-        st["t_backup"] = st.get("t_backup", 0.0) + (t4 - t3)
+        self.stats["waves"] += 1
+        self.stats["sims"] += n
+        self._acc("t_select", t1 - t0)
+        self._acc("t_eval", t2 - t1)
+        self._acc("t_backup", t3 - t2)
+        self._acc("t_rollout_wait", t4 - t3)
         return n
 
-    def _gpu_rollouts(self, s, boards):
+    def _harvest(self, s, keep):
+        """Back up finished GPU rollout waves; block on the oldest while more than ``keep``
+        are in flight."""
+        while self._inflight:
+            wid, pend = self._inflight[0]
+            if len(self._inflight) <= keep and not pend.done():
+                break
+            s.backup_rollout(wid, pend.result())
+            self._inflight.pop(0)
+
+    def _gpu_rollouts(self, s, wid):
         if self._gpu_rollout is None:
             from .gpu_rollout import GpuRollouts
             self._gpu_rollout = GpuRollouts(self.rollout, torch.device("cuda"))
-        return self._gpu_rollout.launch(s, self.rollouts_per_leaf, self.rollout_limit,
-                                        seed=self.seed + self.stats["waves"])
+        return self._gpu_rollout.launch(s, wid, self.rollouts_per_leaf, self.rollout_limit,
+                                        seed=self.seed * 7919 + self.stats["waves"])
 
     def search(self, state, n_playout=None):
         s = self._sync_root(state)
@@ -204,6 +239,9 @@ class ParallelMCTS(object):
             stall = stall + 1 if s.root_visits == before else 0
             if stall > 3:
                 break
+        t = time.perf_counter()
+        self._harvest(s, 0)  # every rollout of this move backed up before choosing
+        self._acc("t_rollout_wait", time.perf_counter() - t)
         return s
 
     def get_move(self, state):

@@ -15,6 +15,9 @@ class _Pending(object):
         self.n = n
         self.R = R
 
+    def done(self):
+        return self.event.query()
+
     def result(self):
         """Mean result per leaf from BLACK's point of view, numpy float32 [n]."""
         self.event.synchronize()
@@ -59,9 +62,9 @@ class GpuRollouts(object):
             ev.record(self.stream)
         return ev, winners, lengths, logits
 
-    def launch(self, search, R, limit, seed=1):
-        """Start R playouts for every pending leaf of a native Search (non-blocking)."""
-        colors, meta = search.rollout_inputs()
+    def launch(self, search, wave, R, limit, seed=1):
+        """Start R playouts for every leaf of a native Search wave (non-blocking)."""
+        colors, meta = search.rollout_inputs(wave)
         b = search.root_board
         ev, winners, _, _ = self._launch(colors, meta, b.size, b.komi, R, limit, seed)
         return _Pending(ev, winners, colors.shape[0], R)

@@ -102,18 +102,49 @@ def test_rollout_weights_roundtrip():
 # ---------------------------------------------------------------------------- native tree
 def test_virtual_loss_spreads_a_wave():
     st = GameState(size=7)
-    s = rg.Search(st.native)
+    s = rg.Search(st.native, 2)
     s.lmbda = 0.0
-    assert s.select(1) == 1
-    s.backup(np.full((1, 49), 1 / 49.0, np.float32), np.zeros(1, np.float32))
-    n = s.select(16)
+    wid, n = s.select(1)
+    assert n == 1
+    s.backup_value(wid, np.full((1, 49), 1 / 49.0, np.float32), np.zeros(1, np.float32))
+    wid, n = s.select(16)
     assert n == 16
     firsts = set()
-    for b in s.leaf_boards():
+    for b in s.leaf_boards(wid):
         firsts.add(b.last_moves[0])
     assert len(firsts) == 16, "virtual loss must send the 16 descents to different children"
-    s.backup(np.full((n, 49), 1 / 49.0, np.float32), np.zeros(n, np.float32))
+    s.backup_value(wid, np.full((n, 49), 1 / 49.0, np.float32), np.zeros(n, np.float32))
     assert s.root_visits == 17
+    assert s.pending_waves == 0
+
+
+def test_async_rollout_waves_keep_virtual_loss():
+    """With lambda > 0 a wave holds its virtual losses until its rollouts are backed up, and
+    later waves can be selected and value-backed-up meanwhile (the APV pipeline)."""
+    st = GameState(size=7)
+    s = rg.Search(st.native, 2)
+    s.lmbda = 0.5
+    pri = np.full((64, 49), 1 / 49.0, np.float32)
+    w0, n0 = s.select(1)
+    s.backup_value(w0, pri, np.zeros(n0, np.float32))
+    s.backup_rollout(w0, np.zeros(n0, np.float32))
+    w1, n1 = s.select(8)
+    s.backup_value(w1, pri, np.zeros(n1, np.float32))
+    w2, n2 = s.select(8)  # w1's rollouts still in flight
+    firsts = {b.last_moves[0] for b in s.leaf_boards(w1)} | \
+        {b.last_moves[0] for b in s.leaf_boards(w2)}
+    assert len(firsts) == 16, "in-flight waves must repel new descents"
+    assert s.pending_waves == 2
+    with pytest.raises(RuntimeError):
+        s.backup_rollout(w2, np.zeros(n2, np.float32))  # value backup must come first
+    s.backup_value(w2, pri, np.zeros(n2, np.float32))
+    s.backup_rollout(w2, np.ones(n2, np.float32))  # black wins every rollout
+    s.backup_rollout(w1, np.ones(n1, np.float32))
+    assert s.pending_waves == 0
+    mv, vis, q, _ = s.root_stats()
+    # black (to move at the root) wins the rollouts: mixed Q of explored children > 0
+    assert (q[vis > 0] > 0).all()
+    assert s.rollouts == 17
 
 
 def test_negamax_sign_prefers_good_moves_for_the_mover():
