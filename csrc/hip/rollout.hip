@@ -7,11 +7,22 @@
 // i.e. the same distribution the CPU rejection sampler draws from), so a move costs one wave-wide
 // max reduction.
 //
-// Board state lives in LDS, one slice per wave: colour per point, a group label per stone (the
-// index of a representative stone) and a liberty count per label. Each lane owns the points
-// p = lane + 64*k. A move: place the stone, remove captured groups (opponent neighbours whose
-// count was 1), relabel the merged own groups to the new stone, then recount every liberty from
-// scratch (each empty point adds 1 to each distinct neighbouring label with LDS atomics).
+// Latency design (a playout is ~430 strictly sequential moves, so per-move latency is the cost):
+//   * board state per wave in LDS: one byte per point ("cell": colour in bits 0-1, the liberty
+//     count of its group clamped to 3 in bits 2-3 — every feature only distinguishes 1 / 2 / 3+),
+//     a group label per stone and a liberty counter per label;
+//   * everything in a candidate's logit except the last-move terms is a function of its 3x3
+//     neighbourhood of cells, so it is cached per point for both players to move ("base") and
+//     recomputed only where a cell of that neighbourhood changed in the last move (the placed
+//     stone, captured stones, groups whose clamped liberty count moved) — a handful of points per
+//     move instead of all 361; the 256 KB pattern table is only read for those;
+//   * per move every lane then just reads its points' cached bases, adds the last-move features
+//     and Gumbel noise, and one wave-wide argmax picks the move;
+//   * neighbour indices come from a block-shared LDS table; the board edge is a template
+//     constant for 19x19 / 13x13 / 9x9.
+// A move: place, remove captured groups (opponent neighbours whose count was 1), relabel the
+// merged own groups to the new stone, recount liberties (each empty point adds 1 to each distinct
+// neighbouring label, LDS atomics), refresh the cells and mark changed neighbourhoods dirty.
 // Rules match the native engine in light mode: simple ko (reference rule Q15), no superko, end
 // of game after two passes with WHITE to move (Q3), area score with single-point eyeish
 // empties and komi, minus passes (Q12).
@@ -22,11 +33,22 @@ using namespace rag;
 namespace {
 
 constexpr int kWaves = 4;  // games per 256-thread block
+constexpr uint8_t kOff = 3;  // colour code of an off-board neighbour
 
-struct Shared {
-  int8_t col[kWaves][640];
-  int16_t lab[kWaves][640];
-  int lib[kWaves][640];
+template <int PM>
+struct GameLds {
+  float base[2][PM];  // cached logit w/o last-move terms; [0] black to move, [1] white
+  int lib[PM];
+  int16_t lab[PM];
+  uint8_t cell[PM];
+  uint8_t chg[PM];
+  uint8_t dirty[PM];
+};
+
+template <int PM>
+struct BlockLds {
+  int16_t ring[PM][8];  // clockwise from north ((x, y+1) first), -1 off board
+  GameLds<PM> g[kWaves];
 };
 
 __device__ __forceinline__ uint32_t hash32(uint32_t x) {
@@ -52,7 +74,6 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// wave-wide argmax of (key, idx); ties -> smaller idx
 __device__ __forceinline__ void wave_argmax(float& key, int& idx) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -71,73 +92,41 @@ __device__ __forceinline__ int wave_sum_i(int v) {
   return v;
 }
 
-template <int NPL>
+template <int SC, int NPL, int PM>
 struct Game {
-  int S, P;
-  int8_t* col;
-  int16_t* lab;
-  int* lib;
+  int S_rt;
+  GameLds<PM>* L;
+  const int16_t (*ring)[8];
   int lane;
 
-  __device__ int nb(int p, int k) const {  // orthogonal neighbour k (engine order) or -1
-    const int x = p / S, y = p - (p / S) * S;
-    switch (k) {
-      case 0: return x > 0 ? p - S : -1;
-      case 1: return x < S - 1 ? p + S : -1;
-      case 2: return y > 0 ? p - 1 : -1;
-      default: return y < S - 1 ? p + 1 : -1;
-    }
-  }
-
-  __device__ void recount_libs() {
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) {
-      const int p = lane + 64 * k;
-      if (p < P) lib[p] = 0;
-    }
-    wave_sync();
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) {
-      const int p = lane + 64 * k;
-      if (p >= P || col[p] != 0) continue;
-      int seen[4];
-      int ns = 0;
-      for (int i = 0; i < 4; ++i) {
-        const int q = nb(p, i);
-        if (q < 0 || col[q] == 0) continue;
-        const int l = lab[q];
-        bool dup = false;
-        for (int j = 0; j < ns; ++j) dup |= seen[j] == l;
-        if (!dup) {
-          seen[ns++] = l;
-          atomicAdd(&lib[l], 1);
-        }
-      }
-    }
-    wave_sync();
-  }
+  __device__ __forceinline__ int S() const { return SC > 0 ? SC : S_rt; }
+  __device__ __forceinline__ int P() const { return S() * S(); }
+  // orthogonal neighbours are ring slots 0 (N), 2 (E), 4 (S), 6 (W); diagonals 1, 3, 5, 7
+  __device__ __forceinline__ int orth(int p, int i) const { return ring[p][2 * i]; }
 
   __device__ void init_labels() {
+    const int P_ = P();
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
       const int p = lane + 64 * k;
-      if (p < P) lab[p] = col[p] ? (int16_t)p : (int16_t)-1;
+      if (p < P_) L->lab[p] = (L->cell[p] & 3) ? (int16_t)p : (int16_t)-1;
     }
     wave_sync();
-    // min-label propagation with pointer jumping until stable
-    for (int it = 0; it < 4 * 640; ++it) {
+    for (int it = 0; it < 4 * PM; ++it) {
       int changed = 0;
 #pragma unroll
       for (int k = 0; k < NPL; ++k) {
         const int p = lane + 64 * k;
-        if (p >= P || col[p] == 0) continue;
-        int m = lab[lab[p]];
+        if (p >= P_) continue;
+        const int c = L->cell[p] & 3;
+        if (!c) continue;
+        int m = L->lab[L->lab[p]];
         for (int i = 0; i < 4; ++i) {
-          const int q = nb(p, i);
-          if (q >= 0 && col[q] == col[p]) m = min(m, (int)lab[q]);
+          const int q = orth(p, i);
+          if (q >= 0 && (L->cell[q] & 3) == c) m = min(m, (int)L->lab[q]);
         }
-        if (m < lab[p]) {
-          lab[p] = (int16_t)m;
+        if (m < L->lab[p]) {
+          L->lab[p] = (int16_t)m;
           changed = 1;
         }
       }
@@ -145,151 +134,269 @@ struct Game {
       if (!__any(changed)) break;
     }
   }
+
+  // liberty counters per label, then the clamped count into every stone's cell (flagging the
+  // cells that changed)
+  __device__ void recount_libs() {
+    const int P_ = P();
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      const int p = lane + 64 * k;
+      if (p < P_) L->lib[p] = 0;
+    }
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      const int p = lane + 64 * k;
+      if (p >= P_ || (L->cell[p] & 3)) continue;
+      int seen[4];
+      int ns = 0;
+      for (int i = 0; i < 4; ++i) {
+        const int q = orth(p, i);
+        if (q < 0 || !(L->cell[q] & 3)) continue;
+        const int l = L->lab[q];
+        bool dup = false;
+        for (int j = 0; j < ns; ++j) dup |= seen[j] == l;
+        if (!dup) {
+          seen[ns++] = l;
+          atomicAdd(&L->lib[l], 1);
+        }
+      }
+    }
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      const int p = lane + 64 * k;
+      if (p >= P_) continue;
+      const uint8_t old = L->cell[p];
+      const uint8_t c = old & 3;
+      if (!c) continue;
+      const uint8_t nc = (uint8_t)(c | (min(L->lib[L->lab[p]], 3) << 2));
+      if (nc != old) {
+        L->cell[p] = nc;
+        L->chg[p] = 1;
+      }
+    }
+    wave_sync();
+  }
+
+  // base logit of p for both players (everything but the last-move terms)
+  __device__ void compute_base(int p, const float* __restrict__ w,
+                               const float* __restrict__ pattern) {
+    const int s = S();
+    const int x = p / s, y = p - (p / s) * s;
+    if (L->cell[p] & 3) {
+      L->base[0][p] = -INFINITY;
+      L->base[1][p] = -INFINITY;
+      return;
+    }
+    uint8_t r[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int q = ring[p][k];
+      r[k] = q < 0 ? kOff : L->cell[q];
+    }
+    int pb = 0, pw = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = r[k] & 3;
+      pb |= c << (2 * k);
+      pw |= ((c == 1 || c == 2) ? 3 - c : c) << (2 * k);
+    }
+    const bool edge = x == 0 || y == 0 || x == s - 1 || y == s - 1;
+#pragma unroll
+    for (int own = 1; own <= 2; ++own) {
+      const int opp = 3 - own;
+      int nnb = 0, own_nb = 0, empty_nb = 0, own_libs = 0;
+      bool capture = false, own_atari = false, own_multi = false;
+#pragma unroll
+      for (int k = 0; k < 8; k += 2) {
+        const int c = r[k] & 3;
+        if (c == kOff) continue;
+        ++nnb;
+        const int lc = r[k] >> 2;
+        if (c == 0) {
+          ++empty_nb;
+        } else if (c == own) {
+          ++own_nb;
+          if (lc == 1) own_atari = true;
+          else own_multi = true;
+          own_libs += lc - 1;
+        } else if (lc == 1) {
+          capture = true;
+        }
+      }
+      float v;
+      bool cand = true;
+      if (own_nb == nnb) {  // own single-point eye
+        int bad = 0;
+#pragma unroll
+        for (int k = 1; k < 8; k += 2) bad += (r[k] & 3) == opp;
+        if (nnb < 4 ? bad == 0 : bad <= 1) cand = false;
+      }
+      if (empty_nb == 0 && !own_multi && !capture) cand = false;  // suicide
+      if (cand) {
+        v = pattern ? pattern[own == 1 ? pb : pw] : 0.f;
+        if (edge) v += w[6];
+        if (capture) v += w[2];
+        if (own_atari && (empty_nb >= 2 || capture)) v += w[1];
+        if (!capture && empty_nb + own_libs <= 1) v += w[3];
+      } else {
+        v = -INFINITY;
+      }
+      L->base[own - 1][p] = v;
+    }
+  }
+
+  // mark the 3x3 neighbourhoods of changed cells dirty, recompute their bases, clear the flags
+  __device__ void refresh(const float* __restrict__ w, const float* __restrict__ pattern) {
+    const int P_ = P();
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      const int p = lane + 64 * k;
+      if (p >= P_ || !L->chg[p]) continue;
+      L->dirty[p] = 1;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int q = ring[p][j];
+        if (q >= 0) L->dirty[q] = 1;
+      }
+    }
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      const int p = lane + 64 * k;
+      if (p >= P_) continue;
+      if (L->dirty[p]) compute_base(p, w, pattern);
+      L->dirty[p] = 0;
+      L->chg[p] = 0;
+    }
+    wave_sync();
+  }
 };
 
-// logits of all candidates for player c (-inf for non-candidates); returns per-lane keys
-template <int NPL>
-__device__ __forceinline__ float cand_logit(const Game<NPL>& g, int p, int c, int ko, int l1,
-                                            int l2, const float* __restrict__ w,
-                                            const float* __restrict__ pattern) {
-  const int S = g.S;
-  if (g.col[p] != 0 || p == ko) return -INFINITY;
-  const int x = p / S, y = p - (p / S) * S;
-  int nnb = 0, own_nb = 0;
-  int empty_nb = 0, own_libs = 0;
-  bool capture = false, own_atari = false, own_multi = false;
-  for (int i = 0; i < 4; ++i) {
-    const int q = g.nb(p, i);
-    if (q < 0) continue;
-    ++nnb;
-    const int cq = g.col[q];
-    if (cq == 0) {
-      ++empty_nb;
-    } else if (cq == c) {
-      ++own_nb;
-      const int lc = g.lib[g.lab[q]];
-      if (lc == 1) own_atari = true;
-      else own_multi = true;
-      own_libs += lc - 1;
-    } else if (g.lib[g.lab[q]] == 1) {
-      capture = true;
-    }
-  }
-  // own single-point eye (all orthogonal neighbours own; <=1 opponent diagonal in the centre,
-  // none on the edge)
-  if (own_nb == nnb) {
-    int bad = 0;
-    const int dx[4] = {-1, 1, 1, -1}, dy[4] = {-1, 1, -1, 1};
-    for (int i = 0; i < 4; ++i) {
-      const int ax = x + dx[i], ay = y + dy[i];
-      if (ax < 0 || ay < 0 || ax >= S || ay >= S) continue;
-      bad += g.col[ax * S + ay] == -c;
-    }
-    if (nnb < 4 ? bad == 0 : bad <= 1) return -INFINITY;
-  }
-  // suicide
-  if (empty_nb == 0 && !own_multi && !capture) return -INFINITY;
-  float s = 0.f;
-  if (l1 >= 0) {
-    const int d1x = abs(x - l1 / S), d1y = abs(y - l1 % S);
-    if (d1x <= 1 && d1y <= 1) s += w[0];
-    else if (d1x + d1y <= 2) s += w[4];
-  }
-  if (l2 >= 0 && abs(x - l2 / S) <= 1 && abs(y - l2 % S) <= 1) s += w[5];
-  if (x == 0 || y == 0 || x == S - 1 || y == S - 1) s += w[6];
-  if (capture) s += w[2];
-  if (own_atari && (empty_nb >= 2 || capture)) s += w[1];
-  if (!capture && empty_nb + own_libs <= 1) s += w[3];
-  const int rdx[8] = {0, 1, 1, 1, 0, -1, -1, -1}, rdy[8] = {1, 1, 0, -1, -1, -1, 0, 1};
-  int pidx = 0;
-  for (int k = 0; k < 8; ++k) {
-    const int ax = x + rdx[k], ay = y + rdy[k];
-    int code = 3;
-    if (ax >= 0 && ay >= 0 && ax < S && ay < S) {
-      const int cq = g.col[ax * S + ay];
-      code = cq == 0 ? 0 : (cq == c ? 1 : 2);
-    }
-    pidx |= code << (2 * k);
-  }
-  return pattern ? s + pattern[pidx] : s;
-}
-
 // meta: [cur, ko, last1, last2, passes_b, passes_w, nmoves, end]
-template <int NPL>
+template <int SC, int NPL, int PM>
 __global__ void __launch_bounds__(256)
 rollout_kernel(const int8_t* __restrict__ colors, const int32_t* __restrict__ meta, int n_pos,
-               int R, int S, float komi, int limit, const float* __restrict__ w,
+               int R, int S_rt, float komi, int limit, const float* __restrict__ w,
                const float* __restrict__ pattern, uint32_t seed, int8_t* __restrict__ winner,
                int16_t* __restrict__ length, float* __restrict__ dbg_logits) {
-  __shared__ Shared sh;
+  __shared__ BlockLds<PM> sh;
+  const int S = SC > 0 ? SC : S_rt;
+  const int P = S * S;
+  // block-shared neighbour table (before any wave may leave)
+  for (int p = threadIdx.x; p < P; p += blockDim.x) {
+    const int x = p / S, y = p - (p / S) * S;
+    const int dx[8] = {0, 1, 1, 1, 0, -1, -1, -1}, dy[8] = {1, 1, 0, -1, -1, -1, 0, 1};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int ax = x + dx[k], ay = y + dy[k];
+      sh.ring[p][k] = (ax < 0 || ay < 0 || ax >= S || ay >= S) ? (int16_t)-1
+                                                                : (int16_t)(ax * S + ay);
+    }
+  }
+  __syncthreads();
   const int wv = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const int game = blockIdx.x * kWaves + wv;
   if (game >= n_pos * R) return;  // whole wave exits together
   const int pos = game / R;
-  Game<NPL> g;
-  g.S = S;
-  g.P = S * S;
-  g.col = sh.col[wv];
-  g.lab = sh.lab[wv];
-  g.lib = sh.lib[wv];
-  g.lane = lane;
-  const int P = g.P;
+  GameLds<PM>& L = sh.g[wv];
+  Game<SC, NPL, PM> g{S_rt, &L, sh.ring, lane};
+  float wl[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) wl[i] = w[i];
+  int px[NPL], py[NPL];
 #pragma unroll
   for (int k = 0; k < NPL; ++k) {
     const int p = lane + 64 * k;
-    if (p < P) g.col[p] = colors[(size_t)pos * P + p];
+    px[k] = p / S;
+    py[k] = p - px[k] * S;
+    if (p < P) {
+      const int c = colors[(size_t)pos * P + p];
+      L.cell[p] = (uint8_t)(c > 0 ? 1 : (c < 0 ? 2 : 0));
+      L.chg[p] = 0;
+      L.dirty[p] = 0;
+    }
   }
   wave_sync();
   g.init_labels();
   g.recount_libs();
+#pragma unroll
+  for (int k = 0; k < NPL; ++k) {
+    const int p = lane + 64 * k;
+    if (p < P) {
+      g.compute_base(p, wl, pattern);
+      L.chg[p] = 0;
+    }
+  }
+  wave_sync();
   const int32_t* m = meta + pos * 8;
   int cur = m[0], ko = m[1], l1 = m[2], l2 = m[3], pb = m[4], pw = m[5], nm = m[6];
   bool end = m[7] != 0;
   LaneRng rng{hash32(seed ^ hash32(game * 0x9E3779B9u + lane * 0x85EBCA6Bu + 1u))};
 
+  // logit of lane point k = cached base + last-move terms
+  auto full_logit = [&](int k, int own_idx, int l1x, int l1y, int l2x, int l2y) -> float {
+    const int p = lane + 64 * k;
+    if (p >= P || p == ko) return -INFINITY;
+    float v = L.base[own_idx][p];
+    if (v == -INFINITY) return v;
+    const int d1x = abs(px[k] - l1x), d1y = abs(py[k] - l1y);
+    if (d1x <= 1 && d1y <= 1) v += wl[0];
+    else if (d1x + d1y <= 2) v += wl[4];
+    if (abs(px[k] - l2x) <= 1 && abs(py[k] - l2y) <= 1) v += wl[5];
+    return v;
+  };
+
   if (dbg_logits) {  // debug: logits of the initial position only
+    const int l1x = l1 >= 0 ? l1 / S : -100, l1y = l1 >= 0 ? l1 % S : -100;
+    const int l2x = l2 >= 0 ? l2 / S : -100, l2y = l2 >= 0 ? l2 % S : -100;
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
       const int p = lane + 64 * k;
-      if (p < P) dbg_logits[(size_t)game * P + p] = cand_logit(g, p, cur, ko, l1, l2, w, pattern);
+      if (p < P)
+        dbg_logits[(size_t)game * P + p] = full_logit(k, cur > 0 ? 0 : 1, l1x, l1y, l2x, l2y);
     }
     return;
   }
 
   int moves = 0;
   while (!end && moves < limit) {
+    const int own = cur > 0 ? 1 : 2;
+    const int l1x = l1 >= 0 ? l1 / S : -100, l1y = l1 >= 0 ? l1 - (l1 / S) * S : -100;
+    const int l2x = l2 >= 0 ? l2 / S : -100, l2y = l2 >= 0 ? l2 - (l2 / S) * S : -100;
     float key = -INFINITY;
     int idx = 0x7fffffff;
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
-      const int p = lane + 64 * k;
-      if (p >= P) continue;
-      const float lg = cand_logit(g, p, cur, ko, l1, l2, w, pattern);
+      const float lg = full_logit(k, own - 1, l1x, l1y, l2x, l2y);
       if (lg == -INFINITY) continue;
-      const float u = rng.uniform();
-      const float kk = lg - __logf(-__logf(u));
+      const float kk = lg - __logf(-__logf(rng.uniform()));
       if (kk > key) {
         key = kk;
-        idx = p;
+        idx = lane + 64 * k;
       }
     }
     wave_argmax(key, idx);
     const int mv = key == -INFINITY ? -1 : idx;  // -1 = pass
     ko = -1;
     if (mv >= 0) {
-      // wave-uniform bookkeeping from LDS (all lanes read the same words)
+      // wave-uniform bookkeeping (every lane reads the same LDS words)
       int cap_l[4], own_l[4];
       int ncap = 0, nown = 0, cap_pt = -1;
       for (int i = 0; i < 4; ++i) {
-        const int q = g.nb(mv, i);
-        if (q < 0 || g.col[q] == 0) continue;
-        const int l = g.lab[q];
-        if (g.col[q] == cur) {
+        const int q = g.orth(mv, i);
+        if (q < 0) continue;
+        const uint8_t cq = L.cell[q];
+        if (!(cq & 3)) continue;
+        const int l = L.lab[q];
+        if ((cq & 3) == own) {
           bool dup = false;
           for (int j = 0; j < nown; ++j) dup |= own_l[j] == l;
           if (!dup) own_l[nown++] = l;
-        } else if (g.lib[l] == 1) {
+        } else if ((cq >> 2) == 1) {
           bool dup = false;
           for (int j = 0; j < ncap; ++j) dup |= cap_l[j] == l;
           if (!dup) {
@@ -304,32 +411,35 @@ rollout_kernel(const int8_t* __restrict__ colors, const int32_t* __restrict__ me
       for (int k = 0; k < NPL; ++k) {
         const int p = lane + 64 * k;
         if (p >= P) continue;
-        const int8_t cp = g.col[p];
-        if (cp == 0) continue;
-        const int l = g.lab[p];
-        if (cp == -cur) {
+        const int c = L.cell[p] & 3;
+        if (!c) continue;
+        const int l = L.lab[p];
+        if (c != own) {
           bool hit = false;
           for (int j = 0; j < ncap; ++j) hit |= cap_l[j] == l;
           if (hit) {
-            g.col[p] = 0;
-            g.lab[p] = -1;
+            L.cell[p] = 0;
+            L.lab[p] = -1;
+            L.chg[p] = 1;
             ++removed;
           }
         } else {
           bool hit = false;
           for (int j = 0; j < nown; ++j) hit |= own_l[j] == l;
-          if (hit) g.lab[p] = (int16_t)mv;
+          if (hit) L.lab[p] = (int16_t)mv;
         }
       }
       if (lane == 0) {
-        g.col[mv] = (int8_t)cur;
-        g.lab[mv] = (int16_t)mv;
+        L.cell[mv] = (uint8_t)own;
+        L.lab[mv] = (int16_t)mv;
+        L.chg[mv] = 1;
       }
       wave_sync();
       g.recount_libs();
       removed = wave_sum_i(removed);
       // ko: one stone captured by a lone stone that is left with a single liberty
-      if (removed == 1 && nown == 0 && g.lib[mv] == 1) ko = cap_pt;
+      if (removed == 1 && nown == 0 && L.lib[mv] == 1) ko = cap_pt;
+      g.refresh(wl, pattern);
     } else {
       if (cur == 1) ++pb;
       else ++pw;
@@ -347,18 +457,19 @@ rollout_kernel(const int8_t* __restrict__ colors, const int32_t* __restrict__ me
   for (int k = 0; k < NPL; ++k) {
     const int p = lane + 64 * k;
     if (p >= P) continue;
-    const int cp = g.col[p];
-    if (cp == 1) {
+    const int c = L.cell[p] & 3;
+    if (c == 1) {
       ++sb;
-    } else if (cp == -1) {
+    } else if (c == 2) {
       ++sw;
     } else {
       bool allb = true, allw = true;
       for (int i = 0; i < 4; ++i) {
-        const int q = g.nb(p, i);
+        const int q = g.orth(p, i);
         if (q < 0) continue;
-        allb &= g.col[q] == 1;
-        allw &= g.col[q] == -1;
+        const int cq = L.cell[q] & 3;
+        allb &= cq == 1;
+        allw &= cq == 2;
       }
       if (allb) ++sb;
       else if (allw) ++sw;
@@ -373,9 +484,17 @@ rollout_kernel(const int8_t* __restrict__ colors, const int32_t* __restrict__ me
   }
 }
 
+template <int SC, int NPL, int PM>
+void launch(dim3 grid, hipStream_t st, const int8_t* c, const int32_t* meta, int n_pos, int R,
+            int S, float komi, int limit, const float* w, const float* pattern, unsigned seed,
+            void* winner, void* length, float* dbg) {
+  rollout_kernel<SC, NPL, PM><<<grid, 256, 0, st>>>(c, meta, n_pos, R, S, komi, limit, w, pattern,
+                                                    seed, (int8_t*)winner, (int16_t*)length, dbg);
+}
+
 }  // namespace
 
-// colors [n_pos][S*S] int8, meta [n_pos][8] int32, weights [7], pattern [65536];
+// colors [n_pos][S*S] int8, meta [n_pos][8] int32, weights [7], pattern [65536] (or null);
 // winner [n_pos*R] int8 (+1 black, -1 white, 0 draw), length [n_pos*R] int16 (optional).
 // dbg_logits (optional, [n_pos*R][S*S]) switches to "initial logits only" mode.
 RAG_API int rag_rollouts(const void* colors, const int32_t* meta, int n_pos, int R, int S,
@@ -386,13 +505,14 @@ RAG_API int rag_rollouts(const void* colors, const int32_t* meta, int n_pos, int
   const int games = n_pos * R;
   dim3 grid((games + kWaves - 1) / kWaves);
   const int8_t* c = (const int8_t*)colors;
-  if (S * S <= 384)
-    rollout_kernel<6><<<grid, 256, 0, stream>>>(c, meta, n_pos, R, S, komi, limit, w, pattern,
-                                                seed, (int8_t*)winner, (int16_t*)length,
-                                                dbg_logits);
-  else
-    rollout_kernel<10><<<grid, 256, 0, stream>>>(c, meta, n_pos, R, S, komi, limit, w, pattern,
-                                                 seed, (int8_t*)winner, (int16_t*)length,
-                                                 dbg_logits);
+#define RAG_RO(SC, NPL, PM)                                                                    \
+  launch<SC, NPL, PM>(grid, stream, c, meta, n_pos, R, S, komi, limit, w, pattern, seed, winner, \
+                      length, dbg_logits)
+  if (S == 19) RAG_RO(19, 6, 384);
+  else if (S == 13) RAG_RO(13, 3, 192);
+  else if (S == 9) RAG_RO(9, 2, 128);
+  else if (S * S <= 384) RAG_RO(0, 6, 384);
+  else RAG_RO(0, 10, 640);
+#undef RAG_RO
   return (int)hipGetLastError();
 }
