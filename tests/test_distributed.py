@@ -120,3 +120,38 @@ def test_bucketed_allreduce_mean(tmp_path):
         np.testing.assert_allclose(np.load(tmp_path / ("bucket%d.npy" % r)), want, rtol=1e-6)
         np.testing.assert_allclose(np.load(tmp_path / ("bucket_b%d.npy" % r)),
                                    np.full(n, 1.5, np.float32))
+
+
+def _rl_worker(rank, world, port, outdir):
+    _setup(rank, world, port)
+    import numpy as np_
+    from rocalphago_amd.models import kerasish as K
+    from rocalphago_amd.models.policy import CNNPolicy
+    from rocalphago_amd.parallel.dp import DPContext
+    from rocalphago_amd.players.ai import ProbabilisticPolicyPlayer
+    from rocalphago_amd.training import reinforcement as rl
+    dp = DPContext(device="cpu")
+    np_.random.seed(100 + rank)  # different self-play games per rank
+    learner = CNNPolicy(FEATS, board=7, filters_per_layer=8, layers=2, device="cpu", seed=3)
+    opponent = CNNPolicy(FEATS, board=7, filters_per_layer=8, layers=2, device="cpu", seed=4)
+    dp.broadcast_model(learner.model)
+    opt = K.SGD(lr=0.01)
+    learner.model.compile(loss=rl.log_loss, optimizer=opt)
+    ratio = rl.run_n_games(opt, ProbabilisticPolicyPlayer(learner, move_limit=40),
+                           ProbabilisticPolicyPlayer(opponent, move_limit=40), 4,
+                           mode="batched", dp=dp)
+    np_.save(os.path.join(outdir, "rl%d.npy" % rank), learner.model.net.flat.detach().numpy())
+    np_.save(os.path.join(outdir, "ratio%d.npy" % rank), np_.array([ratio]))
+    dp.shutdown()
+
+
+@pytest.mark.timeout(300)
+def test_dp_rl_selfplay_sharded(tmp_path):
+    """RL self-play sharded over 2 ranks: different games, one all-reduced REINFORCE update,
+    identical replicas afterwards."""
+    _spawn(_rl_worker, (str(tmp_path),))
+    a, b = np.load(tmp_path / "rl0.npy"), np.load(tmp_path / "rl1.npy")
+    assert np.array_equal(a, b)
+    from rocalphago_amd.models.policy import CNNPolicy
+    fresh = CNNPolicy(FEATS, board=7, filters_per_layer=8, layers=2, device="cpu", seed=3)
+    assert not np.allclose(a, fresh.model.net.flat.detach().numpy()), "no update happened"
