@@ -1,7 +1,4 @@
 """AlphaGo.ai — players. See rocalphago_amd/players/ai.py and rocalphago_amd/search/apv.py."""
 from rocalphago_amd.players.ai import (GreedyPolicyPlayer, MCTSPlayer,  # noqa: F401
                                        ProbabilisticPolicyPlayer)
-try:
-    from rocalphago_amd.search.apv import ParallelMCTSPlayer  # noqa: F401
-except ImportError:  # pragma: no cover
-    pass
+from rocalphago_amd.search.apv import ParallelMCTSPlayer  # noqa: F401
