@@ -680,6 +680,51 @@ RAG_API int rag_pack_weights(const float* W, void* Wf, void* Wb, int COUT, int C
   return (int)hipGetLastError();
 }
 
+// One launch that repacks every layer of a trunk after an optimizer step: for each layer the
+// bf16 forward / dgrad GEMM layouts of its OIHW fp32 weights and the padded fp32 bias. `table`
+// holds kPackFields int64 per layer: W, b (or 0), COUT, CIN, KS, COUTP, CINP, Wf, Wb (or 0),
+// bias_out (or 0), first element index; elements of a layer = taps*COUTP*CINP + COUTP.
+namespace {
+constexpr int kPackFields = 11;
+__global__ void pack_trunk_kernel(const int64_t* __restrict__ table, int nlayers, int64_t total) {
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    int l = 0;
+    while (l + 1 < nlayers && table[(l + 1) * kPackFields + 10] <= idx) ++l;
+    const int64_t* t = table + l * kPackFields;
+    const float* W = (const float*)t[0];
+    const float* b = (const float*)t[1];
+    const int COUT = (int)t[2], CIN = (int)t[3], KS = (int)t[4], COUTP = (int)t[5],
+              CINP = (int)t[6];
+    bf16* Wf = (bf16*)t[7];
+    bf16* Wb = (bf16*)t[8];
+    float* bo = (float*)t[9];
+    const int taps = KS * KS;
+    const int64_t local = idx - t[10];
+    const int64_t wtotal = (int64_t)taps * COUTP * CINP;
+    if (local < wtotal) {
+      const int c = (int)(local % CINP);
+      const int n = (int)((local / CINP) % COUTP);
+      const int tap = (int)(local / ((int64_t)CINP * COUTP));
+      float v = 0.f;
+      if (n < COUT && c < CIN) v = W[((size_t)n * CIN + c) * taps + tap];
+      Wf[local] = (bf16)v;
+      if (Wb) Wb[((size_t)(taps - 1 - tap) * CINP + c) * COUTP + n] = (bf16)v;
+    } else if (bo) {
+      const int n = (int)(local - wtotal);
+      bo[n] = (b && n < COUT) ? b[n] : 0.f;
+    }
+  }
+}
+}  // namespace
+
+RAG_API int rag_pack_trunk(const int64_t* table, int nlayers, int64_t total, hipStream_t stream) {
+  const int64_t blocks64 = (total + 255) / 256;
+  const int blocks = blocks64 < 8192 ? (int)blocks64 : 8192;
+  pack_trunk_kernel<<<blocks, 256, 0, stream>>>(table, nlayers, total);
+  return (int)hipGetLastError();
+}
+
 RAG_API int rag_pack_input_u8(const uint8_t* F, const int64_t* index, const int* tf, void* X,
                               int B, int NF, int S, int H, int CP, hipStream_t stream) {
   const int total = B * S * S;

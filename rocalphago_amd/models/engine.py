@@ -110,9 +110,24 @@ class HipTrunk(object):
                                           device=self.device)
                 self._wb[l] = torch.empty((taps, s.cinp, s.coutp), dtype=torch.bfloat16,
                                           device=self.device)
-            ops.pack_weights(weights[l], s.coutp, s.cinp, self._wf[l], self._wb[l])
-            if biases[l] is not None:
-                self._bias[l][:s.cout].copy_(biases[l])
+        # one launch repacks all layers (GEMM layouts + padded biases); the pointer table is
+        # rebuilt only when a parameter tensor moved
+        ws = [w.contiguous() for w in weights]
+        key = tuple(w.data_ptr() for w in ws) + \
+            tuple(0 if b is None else b.data_ptr() for b in biases)
+        if getattr(self, "_pack_key", None) != key:
+            rows, start = [], 0
+            for l, s in enumerate(self.specs):
+                b = biases[l]
+                rows.append([ws[l].data_ptr(), 0 if b is None else b.data_ptr(), s.cout, s.cin,
+                             s.ks, s.coutp, s.cinp, self._wf[l].data_ptr(),
+                             self._wb[l].data_ptr(), self._bias[l].data_ptr(), start])
+                start += s.ks * s.ks * s.coutp * s.cinp + s.coutp
+            self._pack_table = torch.tensor(rows, dtype=torch.int64).to(self.device)
+            self._pack_total = start
+            self._pack_key = key
+            self._pack_keep = ws  # keep contiguous copies alive while the table points at them
+        ops.pack_trunk(self._pack_table, self.L, self._pack_total)
         self._packed_version = version
 
     # ------------------------------------------------------------------ compute

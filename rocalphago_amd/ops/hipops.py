@@ -52,6 +52,12 @@ def pack_weights(w, coutp, cinp, wf=None, wb=None):
     return wf, wb
 
 
+def pack_trunk(table, nlayers, total):
+    """Repack every layer of a trunk in one launch (table: device int64 [nlayers, 11], see
+    rag_pack_trunk in csrc/hip/conv.hip)."""
+    _check(_lib().rag_pack_trunk(_ptr(table), nlayers, int(total), _stream()), "pack_trunk")
+
+
 def conv_igemm(x, wpack, bias, y, B, S, hi, ho, cinp, coutp, ks, relu, mask=None,
                mask_halo=None):
     """y[pad ho] = act(conv_ks(x[pad hi]) + bias), or the dgrad form with a ReLU mask (the layer
