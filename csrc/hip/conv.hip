@@ -629,7 +629,8 @@ static void launch_wgrad_ks(int ntn, int ntc, dim3 grid, hipStream_t st, const b
 // X: the layer input (halo HI, CINP channels). dW: OIHW fp32 [COUT][CIN][KS][KS]. db: [COUT].
 RAG_API int rag_conv_wgrad(const void* G, const void* X, float* dW, float* db, float* work,
                            int B, int S, int HI, int HG, int GC, int COUT, int COUTP, int CIN,
-                           int CINP, int KS, int accumulate, hipStream_t stream) {
+                           int CINP, int KS, int accumulate, hipStream_t stream,
+                           hipStream_t reduce_stream) {
   if (COUTP % 32 || CINP % 32) return -1;
   const int taps = KS * KS;
   const bf16* g = (const bf16*)G;
@@ -664,10 +665,22 @@ RAG_API int rag_conv_wgrad(const void* G, const void* X, float* dW, float* db, f
       default: return -2;
     }
   }
+  // The slab reduce is bandwidth-bound while the next kernels (dgrad) are MFMA-bound: with a
+  // separate reduce stream it runs concurrently with them, ordered after this wgrad by an event.
+  hipStream_t rs = stream;
+  if (reduce_stream && reduce_stream != stream) {
+    static hipEvent_t ring[16];
+    static int next = 0;
+    hipEvent_t& ev = ring[next];
+    next = (next + 1) & 15;
+    if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return -3;
+    if (hipEventRecord(ev, stream) != hipSuccess) return -3;
+    if (hipStreamWaitEvent(reduce_stream, ev, 0) != hipSuccess) return -3;
+    rs = reduce_stream;
+  }
   const int total = taps * COUTP * CINP / 4 + COUTP;
-  wgrad_reduce_kernel<<<(total + 255) / 256, 256, 0, stream>>>(part, bpart, dW, db, nchunks, taps,
-                                                              COUT, CIN, COUTP, CINP, KS,
-                                                              accumulate);
+  wgrad_reduce_kernel<<<(total + 255) / 256, 256, 0, rs>>>(part, bpart, dW, db, nchunks, taps,
+                                                          COUT, CIN, COUTP, CINP, KS, accumulate);
   return (int)hipGetLastError();
 }
 

@@ -16,6 +16,8 @@ dense layers as plain library GEMMs — hipBLASLt via torch.matmul — and tanh)
 No autograd graph is built on the hot path; ``models/kerasish.py`` exposes these engines through
 torch.autograd.Function wrappers for generic use and calls ``train_step`` directly for speed.
 """
+import os
+
 import torch
 
 from ..ops import hipops as ops
@@ -47,6 +49,7 @@ class HipTrunk(object):
         self._bias = [torch.zeros(s.coutp, device=device) for s in specs]
         self._packed_version = None
         self._work = None
+        self._rstream = None
 
     # ------------------------------------------------------------------ buffers
     def _halos(self):
@@ -84,7 +87,16 @@ class HipTrunk(object):
         for s in self.specs:
             need = max(need, ops._lib().rag_conv_wgrad_workspace(B, S, s.coutp, s.cinp, s.ks,
                                                                  None))
-        self._work = torch.empty(need + 1024, dtype=torch.float32, device=self.device)
+        # two slab workspaces: layer l's reduction (on the reduce stream) may still read one
+        # while layer l-1's wgrad writes the other
+        self._work = [torch.empty(need + 1024, dtype=torch.float32, device=self.device)
+                      for _ in range(2)]
+        self._wevt = [None, None]
+        # Overlapping the reductions with dgrad on a second stream measured slower on MI355X
+        # (78.1k vs 80.8k positions/s: the two contend for CUs and L2); opt-in only.
+        if self._rstream is None and self.device.type == "cuda" and \
+                os.environ.get("RAG_WGRAD_OVERLAP") == "1":
+            self._rstream = torch.cuda.Stream(self.device)
 
     def input_buffer(self, B):
         self.ensure_batch(B)
@@ -145,15 +157,28 @@ class HipTrunk(object):
         ``on_layer_done(l)`` fires right after layer l's wgrad is queued (DP bucket overlap)."""
         S = self.S
         which = top_which
-        for l in range(self.L - 1, -1, -1):
+        main = torch.cuda.current_stream(self.device)
+        rs = self._rstream
+        for i, l in enumerate(range(self.L - 1, -1, -1)):
             s = self.specs[l]
             g = self.grad_buffer(l, which, B)
             x = self.acts[l][:B]
+            slot = i & 1 if rs is not None else 0
+            if rs is not None and self._wevt[slot] is not None:
+                main.wait_event(self._wevt[slot])  # the reduction that last read this slab
             ops.conv_wgrad(g, x, dws[l], dbs[l], B, S, self.halo[l], s.cout, s.coutp, s.cin,
-                           s.cinp, s.ks, accumulate=accumulate, work=self._work,
-                           hg=self.halo[l])
+                           s.cinp, s.ks, accumulate=accumulate, work=self._work[slot],
+                           hg=self.halo[l], reduce_stream=rs)
+            if rs is not None:
+                ev = torch.cuda.Event()
+                ev.record(rs)
+                self._wevt[slot] = ev
             if on_layer_done is not None:
-                on_layer_done(l)
+                if rs is not None:
+                    with torch.cuda.stream(rs):  # the bucket all-reduce follows the reduction
+                        on_layer_done(l)
+                else:
+                    on_layer_done(l)
             if l > 0:
                 below = self.specs[l - 1]
                 which ^= 1
@@ -161,6 +186,9 @@ class HipTrunk(object):
                 ops.conv_igemm(g, self._wb[l], None, gout, B, S, self.halo[l],
                                self.halo[l - 1], s.coutp, s.cinp, s.ks, False,
                                mask=x if below.relu else None, mask_halo=self.halo[l])
+        # weight / bias gradients complete before anything on the main stream reads them
+        if rs is not None:
+            main.wait_stream(rs)
 
 
 class PolicyHeadEngine(object):
