@@ -74,18 +74,27 @@ conv_pipe_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
   const int cchunks = CIN / kBK;
   const int nsteps = KS * KS * cchunks;
 
-  auto stage = [&](int buf, int s) {
-    const int tap = s / cchunks;
-    const int c0 = (s - tap * cchunks) * kBK;
-    const int ky = tap / KS, kx = tap - (tap / KS) * KS;
-    const int aoff = (ky * WI + kx) * CIN + c0;
+  // stages are issued strictly in order: a scalar (tap, channel-chunk) iterator replaces the
+  // per-stage divisions
+  int it_c0 = 0, it_tap = 0, it_kx = 0, it_ky = 0;
+  auto stage = [&](int buf, int /*s*/) {
+    const int aoff = (it_ky * WI + it_kx) * CIN + it_c0;
+    const int boff = it_tap * WROWS * CIN + it_c0;
     bf16* la = lds + buf * STAGE;
 #pragma unroll
     for (int k = 0; k < AK; ++k) glds16(X + abase[k] + aoff, la + (w + 4 * k) * 16 * kBK);
     bf16* lb = la + kBM * kBK;
-    const int boff = tap * WROWS * CIN + c0;
 #pragma unroll
     for (int k = 0; k < BK4; ++k) glds16(Wt + bbase[k] + boff, lb + (w + 4 * k) * 16 * kBK);
+    it_c0 += kBK;
+    if (it_c0 == CIN) {
+      it_c0 = 0;
+      ++it_tap;
+      if (++it_kx == KS) {
+        it_kx = 0;
+        ++it_ky;
+      }
+    }
   };
 
   f32x4 acc[NT][MT];
@@ -131,10 +140,12 @@ conv_pipe_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
     for (int i = 0; i < MT; ++i) xa[i] = *reinterpret_cast<const bf16x8*>(lb + aoffs[i]);
 #pragma unroll
     for (int j = 0; j < NT; ++j) wb[j] = *reinterpret_cast<const bf16x8*>(lb + boffs[j]);
+    __builtin_amdgcn_s_setprio(1);  // the MFMA burst goes first on the shared pipe
 #pragma unroll
     for (int j = 0; j < NT; ++j)
 #pragma unroll
       for (int i = 0; i < MT; ++i) acc[j][i] = mfma16(wb[j], xa[i], acc[j][i]);
+    __builtin_amdgcn_s_setprio(0);
     buf = buf + 1 == kNBUF ? 0 : buf + 1;
   }
 
