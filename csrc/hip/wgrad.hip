@@ -82,22 +82,43 @@ wgrad_taps_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
     srow[k] = row;
     scol[k] = ch * 8;
   }
+  // Running per-lane source offsets (elements), advanced by one stage per issue; stages are
+  // issued strictly in order. Only stages that touch the ends of the row range take the
+  // clamped path.
+  int soff[kPerWave];
+#pragma unroll
+  for (int k = 0; k < kPerWave; ++k) {
+    const int i = w + 4 * k;
+    soff[k] = i < kGInst ? (sbeg * kBK + srow[k]) * GC + n0 + scol[k]
+                         : (sbeg * kBK + xshift0 + srow[k]) * CIN + c0 + scol[k];
+  }
   auto stage = [&](int s, int buf) {
     const int r0 = (sbeg + s) * kBK;
     bf16* lb = lds + buf * kStageElems;
+    const bool inside = r0 + xshift0 >= 0 && r0 + xshift0 + kXRowsLoaded <= R && r0 + kBK <= R;
+    if (inside) {
 #pragma unroll
-    for (int k = 0; k < kPerWave; ++k) {
-      const int i = w + 4 * k;  // wave-uniform
-      if (i < kGInst) {
-        int r = r0 + srow[k];
-        r = r < R ? r : R - 1;  // past the end: the last padded row is halo (zero)
-        glds16(G + (size_t)r * GC + n0 + scol[k], lb + i * 512);
-      } else {
-        int r = r0 + xshift0 + srow[k];
-        r = r < 0 ? 0 : (r < R ? r : R - 1);  // only ever paired with zero G rows
-        glds16(X + (size_t)r * CIN + c0 + scol[k], lb + i * 512);
+      for (int k = 0; k < kPerWave; ++k) {
+        const int i = w + 4 * k;  // wave-uniform
+        glds16((i < kGInst ? G : X) + soff[k], lb + i * 512);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kPerWave; ++k) {
+        const int i = w + 4 * k;  // wave-uniform
+        if (i < kGInst) {
+          int r = r0 + srow[k];
+          r = r < R ? r : R - 1;  // past the end: the last padded row is halo (zero)
+          glds16(G + (size_t)r * GC + n0 + scol[k], lb + i * 512);
+        } else {
+          int r = r0 + xshift0 + srow[k];
+          r = r < 0 ? 0 : (r < R ? r : R - 1);  // only ever paired with zero G rows
+          glds16(X + (size_t)r * CIN + c0 + scol[k], lb + i * 512);
+        }
       }
     }
+#pragma unroll
+    for (int k = 0; k < kPerWave; ++k) soff[k] += w + 4 * k < kGInst ? kBK * GC : kBK * CIN;
   };
 
   f32x4 acc[NT][2][2];
