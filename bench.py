@@ -158,20 +158,28 @@ def main():
         result["baseline_note"] = "vs_baseline = value / 2600 positions/s (paper-derived value " \
                                   "training throughput, BASELINE.md)"
     if not args.no_mcts and args.model == "policy":
-        # one independent search per GPU (root parallelism); whole-job sims/s = sum over ranks
+        # one independent search per GPU (root parallelism); whole-job sims/s = sum over ranks.
+        # Every rank reaches the all-reduce whether or not its measurement worked (no hang).
+        r, err = None, None
         try:
             from benchmarks.mcts_bench import measure
             r = measure(dev, playouts=args.mcts_playouts)
-            tot = torch.tensor([r["sims_per_s"], r.get("rollouts_per_s", 0.0)], device=dev)
-            dp.allreduce_sum_(tot)
+        except Exception as e:  # the SL metric stands on its own
+            err = str(e)[:200]
+        tot = torch.tensor([r["sims_per_s"] if r else 0.0,
+                            r.get("rollouts_per_s", 0.0) if r else 0.0,
+                            1.0 if r else 0.0], device=dev)
+        dp.allreduce_sum_(tot)
+        if int(tot[2]) == dp.world:
             result["mcts_sims_per_s"] = round(float(tot[0]), 1)
             result["mcts_rollouts_per_s"] = round(float(tot[1]), 1)
             result["mcts_config"] = "APV-MCTS 19x19, policy 48x192x13 + value 49x192x13+FC256 " \
                                     "on GPU, lambda 0.5, %d GPU rollouts/leaf, wave %d, %d " \
-                                    "playouts/move" % (r["rollouts_per_leaf"], r["batch"],
-                                                       args.mcts_playouts)
-        except Exception as e:  # the SL metric stands on its own
-            result["mcts_error"] = str(e)[:200]
+                                    "playouts/move, one search per GPU" % (
+                                        r["rollouts_per_leaf"], r["batch"], args.mcts_playouts)
+        else:
+            result["mcts_error"] = err or "MCTS measurement failed on %d rank(s)" % (
+                dp.world - int(tot[2]))
     if dp.is_root:
         print(json.dumps(result), flush=True)
     dp.shutdown()
