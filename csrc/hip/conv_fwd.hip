@@ -23,6 +23,9 @@ namespace {
 
 constexpr int kBK = 32;
 constexpr int kNBUF = 3;
+// fragment double-buffering (see the K loop): needs ~48 more VGPRs and spills at 2 blocks/CU
+// with the 192x192 tile, so it is off
+constexpr bool kFragPrefetch = false;
 
 template <int KS, int NT, int MT>
 __global__ void __launch_bounds__(256, 2)
@@ -105,6 +108,7 @@ conv_pipe_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
 
   stage(0, 0);
   if (nsteps > 1) stage(1, 1);
+  if (kFragPrefetch && nsteps > 2) stage(2, 2);
 
   const int frow = lane & 15;
   const int fq = lane >> 4;
@@ -121,6 +125,58 @@ conv_pipe_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
     boffs[j] = kBM * kBK + row * kBK + ((fq ^ swz64(row)) * 8);
   }
 
+  if constexpr (kFragPrefetch) {
+    // Fragment double-buffering: the ds_reads of step s+1 are issued before the MFMAs of step
+    // s, so LDS latency hides behind the MFMA burst. Ring of 3 LDS stages: at step s the
+    // stage s+1 is read, s+2 is landing and s+3 is issued into the buffer of stage s (whose
+    // fragments every wave already holds in registers when it passes the barrier).
+    bf16x8 xa0[MT], wb0[NT], xa1[MT], wb1[NT];
+    auto read_frags = [&](int b, bf16x8 (&xa)[MT], bf16x8 (&wb)[NT]) {
+      const bf16* lb = lds + b * STAGE;
+#pragma unroll
+      for (int i = 0; i < MT; ++i) xa[i] = *reinterpret_cast<const bf16x8*>(lb + aoffs[i]);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) wb[j] = *reinterpret_cast<const bf16x8*>(lb + boffs[j]);
+    };
+    auto mfmas = [&](bf16x8 (&xa)[MT], bf16x8 (&wb)[NT]) {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int i = 0; i < MT; ++i) acc[j][i] = mfma16(wb[j], xa[i], acc[j][i]);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    int bcur = 0;  // LDS buffer of stage s
+    auto step = [&](int s, bf16x8 (&xc)[MT], bf16x8 (&wc)[NT], bf16x8 (&xn)[MT],
+                    bf16x8 (&wn2)[NT]) {
+      const int bnext = bcur + 1 == kNBUF ? 0 : bcur + 1;
+      if (s + 1 < nsteps) {
+        if (s + 2 < nsteps)
+          asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PER_STAGE) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (s + 3 < nsteps) stage(bcur, s + 3);
+        read_frags(bnext, xn, wn2);
+      }
+      mfmas(xc, wc);
+      bcur = bnext;
+    };
+    if (nsteps > 2)
+      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * PER_STAGE) : "memory");
+    else if (nsteps == 2)
+      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PER_STAGE) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    read_frags(0, xa0, wb0);
+    for (int s = 0; s < nsteps; s += 2) {
+      step(s, xa0, wb0, xa1, wb1);
+      if (s + 1 < nsteps) step(s + 1, xa1, wb1, xa0, wb0);
+    }
+  } else {
   int buf = 0;
   for (int s = 0; s < nsteps; ++s) {
     if (s + 1 < nsteps)
@@ -147,6 +203,7 @@ conv_pipe_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
       for (int i = 0; i < MT; ++i) acc[j][i] = mfma16(wb[j], xa[i], acc[j][i]);
     __builtin_amdgcn_s_setprio(0);
     buf = buf + 1 == kNBUF ? 0 : buf + 1;
+  }
   }
 
   // epilogue: lane owns channels n..n+3 of pixel m for every (j, i) tile
