@@ -1,0 +1,533 @@
+// Native APV-MCTS core (the reference's ParallelMCTS is an empty stub,
+// AlphaGo/mcts.py:219-220, and its sequential MCTS is AlphaGo/mcts.py:79-216).
+//
+// Asynchronous policy-and-value MCTS in the AlphaGo style, restructured for a GPU evaluator:
+// the search advances in *waves*. select(B) descends the tree B times with virtual loss, so the
+// descents spread over different leaves, and returns a wave id. For every wave
+//   * the policy / value networks evaluate all its leaves in one batched GPU pass, and
+//     backup_value() expands the leaves with the network priors and backs up the value-net
+//     statistics (N_v, W_v) at once;
+//   * the fast-rollout playouts of the same leaves run asynchronously — on the GPU rollout kernel
+//     (several waves in flight) or on a native thread pool — and backup_rollout() later adds the
+//     rollout statistics (N_r, W_r) and removes the wave's virtual losses.
+// As in AlphaGo, the two estimates are kept apart and mixed at selection time:
+//   Q(s,a) = (1 - lambda) W_v/N_v + lambda W_r/N_r
+//   a      = argmax  Q(s,a) + c_puct P(s,a) sqrt(N(s)) / (1 + N(s,a))
+// with n_vl virtual losses per in-flight descent (counted as rollout losses when rollouts are
+// used, value losses otherwise). Values are from the perspective of the player to move at the
+// leaf; a node stores them for the player who played its move (negamax signs on backup).
+//
+// Children are created for the leaf's sensible moves (legal, not an own true eye — the set the
+// players use) with priors renormalised over them; PASS is the only child when no sensible move
+// exists. Terminal leaves (end of game) are scored exactly and backed up at once.
+#pragma once
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <condition_variable>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <thread>
+#include <tuple>
+#include <vector>
+
+#include "../engine/go_engine.hpp"
+#include "rollout.hpp"
+
+namespace rag {
+
+namespace mcts_detail {
+
+enum : uint8_t { N_NEW = 0, N_PENDING = 1, N_EXPANDED = 2 };
+
+struct Node {
+  int32_t parent;
+  int32_t first;   // first child (children are contiguous)
+  int16_t nchild;
+  int16_t move;    // flat index, PASS = -1
+  float prior;
+  int32_t n;       // value-net visits (every completed evaluation)
+  int32_t nr;      // rollouts
+  int32_t vl;      // in-flight descents through this node
+  float w;         // value-net sum, for the player who played `move`
+  float wr;        // rollout sum, same perspective
+  uint8_t state;
+};
+
+struct Leaf {
+  Board board;
+  std::vector<int32_t> path;  // root .. leaf
+  float z = 0.f;
+};
+
+struct Wave {
+  std::vector<Leaf> leaves;
+  bool value_done = false;
+  std::thread worker;  // CPU rollouts
+  bool rolling = false;
+};
+
+// Persistent worker pool (thread start-up is not paid per call).
+class Pool {
+ public:
+  explicit Pool(int n) {
+    for (int i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+      ++gen_;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  int size() const { return (int)th_.size(); }
+  void run(int n, const std::function<void(int)>& fn) {
+    if (n <= 0) return;
+    std::lock_guard<std::mutex> serial(run_mu_);  // one job at a time per pool
+    if (th_.empty() || n == 1) {
+      for (int i = 0; i < n; ++i) fn(i);
+      return;
+    }
+    std::unique_lock<std::mutex> lk(mu_);
+    fn_ = &fn;
+    n_ = n;
+    next_ = 0;
+    active_ = (int)th_.size();
+    ++gen_;
+    cv_.notify_all();
+    done_.wait(lk, [this] { return active_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void loop() {
+    uint64_t seen = 0;
+    while (true) {
+      const std::function<void(int)>* fn;
+      int n;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (stop_) return;
+        fn = fn_;
+        n = n_;
+      }
+      for (int i = next_++; i < n; i = next_++) (*fn)(i);
+      std::lock_guard<std::mutex> g(mu_);
+      if (--active_ == 0) done_.notify_one();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex mu_, run_mu_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int)>* fn_ = nullptr;
+  int n_ = 0, active_ = 0;
+  std::atomic<int> next_{0};
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+}  // namespace mcts_detail
+
+using mcts_detail::Leaf;
+using mcts_detail::Node;
+using mcts_detail::Pool;
+using mcts_detail::Wave;
+using mcts_detail::N_EXPANDED;
+using mcts_detail::N_NEW;
+using mcts_detail::N_PENDING;
+
+class Search {
+ public:
+  float c_puct = 5.f, lambda = 0.5f;
+  int n_vl = 3, rollout_limit = 500, max_depth = 722;
+  uint64_t seed = 1;
+  std::shared_ptr<RolloutPolicy> rollout_policy;
+
+  explicit Search(const Board& root, int nthreads = 8)
+      : rollout_policy(std::make_shared<RolloutPolicy>()), pool_(std::max(nthreads, 1)) {
+    reset(root);
+  }
+  ~Search() { drop_waves(); }
+  Search(const Search&) = delete;
+  Search& operator=(const Search&) = delete;
+
+  void reset(const Board& root) {
+    drop_waves();
+    root_board_ = root;
+    nodes_.clear();
+    nodes_.reserve(1 << 20);
+    nodes_.push_back(Node{-1, -1, 0, (int16_t)PASS, 1.f, 0, 0, 0, 0.f, 0.f, N_NEW});
+    root_ = 0;
+  }
+
+  const Board& root_board() const { return root_board_; }
+  int nthreads() const { return pool_.size(); }
+
+  // ------------------------------------------------------------------ selection
+  float child_score(const Node& c, float sq) const {
+    const float vl = (float)(c.vl * n_vl);
+    const bool use_r = lambda > 0.f;
+    const bool use_v = lambda < 1.f;
+    float q = 0.f;
+    if (use_r && use_v) {
+      const float qv = c.n > 0 ? c.w / c.n : 0.f;
+      const float den = c.nr + vl;
+      const float qr = den > 0.f ? (c.wr - vl) / den : qv;
+      q = (1.f - lambda) * qv + lambda * qr;
+    } else if (use_r) {
+      const float den = c.nr + vl;
+      q = den > 0.f ? (c.wr - vl) / den : 0.f;
+    } else {
+      const float den = c.n + vl;
+      q = den > 0.f ? (c.w - vl) / den : 0.f;
+    }
+    return q + c_puct * c.prior * sq / (1.f + (float)c.n + vl);
+  }
+
+  int select_child(int p) const {
+    const Node& pn = nodes_[p];
+    const float np = (float)(pn.n + pn.vl * n_vl);
+    const float sq = std::sqrt(std::max(np, 1.f));
+    int best = pn.first;
+    float bv = -1e30f;
+    for (int k = 0; k < pn.nchild; ++k) {
+      const float v = child_score(nodes_[pn.first + k], sq);
+      if (v > bv) {
+        bv = v;
+        best = pn.first + k;
+      }
+    }
+    return best;
+  }
+
+  // Returns (wave id, number of leaves); id -1 when nothing was selected.
+  std::pair<int, int> select(int B) {
+    auto wave = std::make_unique<Wave>();
+    collisions_ = 0;
+    int attempts = 0;
+    while ((int)wave->leaves.size() < B && attempts < 4 * B) {
+      ++attempts;
+      Leaf L;
+      L.board = root_board_;
+      L.board.set_light(!root_board_.enforce_superko());
+      int node = root_;
+      L.path.push_back(node);
+      int depth = 0;
+      while (nodes_[node].state == N_EXPANDED && nodes_[node].nchild > 0 &&
+             !L.board.end_of_game() && depth < max_depth) {
+        node = select_child(node);
+        L.board.play_unchecked(nodes_[node].move);
+        L.path.push_back(node);
+        ++depth;
+      }
+      if (L.board.end_of_game() || depth >= max_depth ||
+          (nodes_[node].state == N_EXPANDED && nodes_[node].nchild == 0)) {
+        const int win = L.board.get_winner();
+        const int ptm = L.board.current_player();
+        const float v = win == 0 ? 0.f : (win == ptm ? 1.f : -1.f);
+        backup_value_path(L.path, v, false);
+        if (lambda > 0.f) backup_rollout_path(L.path, v, false);
+        ++terminal_;
+        continue;
+      }
+      if (nodes_[node].state == N_PENDING) {  // already waiting for its evaluation
+        ++collisions_;
+        continue;
+      }
+      nodes_[node].state = N_PENDING;
+      for (int id : L.path) nodes_[id].vl += 1;
+      wave->leaves.push_back(std::move(L));
+    }
+    const int n = (int)wave->leaves.size();
+    if (n == 0) return {-1, 0};
+    const int id = next_wave_++;
+    waves_[id] = std::move(wave);
+    return {id, n};
+  }
+
+  Wave& wave(int id) {
+    auto it = waves_.find(id);
+    if (it == waves_.end()) throw std::invalid_argument("unknown or finished wave");
+    return *it->second;
+  }
+  int num_leaves(int id) { return (int)wave(id).leaves.size(); }
+  std::vector<const Board*> leaf_boards(int id) {
+    std::vector<const Board*> v;
+    for (auto& L : wave(id).leaves) v.push_back(&L.board);
+    return v;
+  }
+
+  // ------------------------------------------------------------------ value backup
+  // priors: [n][stride] network move probabilities (nullptr => uniform); values: [n] (nullptr
+  // => value statistics untouched: rollouts only).
+  // sensible: optional [n][P] mask of the leaves' sensible moves (legal, not an own true eye),
+  // e.g. the sensibleness plane the GPU feature kernel already produced; otherwise the moves
+  // are generated natively on the pool.
+  void backup_value(int id, const float* priors, int stride, const float* values,
+                    const uint8_t* sensible = nullptr) {
+    Wave& wv = wave(id);
+    if (wv.value_done) throw std::runtime_error("value backup twice");
+    const int n = (int)wv.leaves.size();
+    const int P = root_board_.npoints();
+    std::vector<std::vector<int>> moves(n);
+    pool_.run(n, [&](int i) {
+      const Leaf& L = wv.leaves[i];
+      if (nodes_[L.path.back()].state == N_EXPANDED) return;
+      if (sensible) {
+        const uint8_t* m = sensible + (size_t)i * P;
+        for (int p = 0; p < P; ++p)
+          if (m[p]) moves[i].push_back(p);
+        return;
+      }
+      std::vector<int> eyes;
+      L.board.legal_moves(moves[i], eyes);
+    });
+    for (int i = 0; i < n; ++i) {
+      Leaf& L = wv.leaves[i];
+      expand(L.path.back(), moves[i], priors ? priors + (size_t)i * stride : nullptr);
+      backup_value_path(L.path, values ? values[i] : 0.f, lambda <= 0.f);
+    }
+    wv.value_done = true;
+    sims_ += n;
+    if (lambda <= 0.f) finish(id);
+  }
+
+  // ------------------------------------------------------------------ rollout backup
+  // Inputs of the GPU rollout kernel: colours [n][P] int8 and per-leaf meta
+  // (player to move, ko, last move, second-to-last move, black passes, white passes,
+  // moves played, end-of-game flag).
+  void rollout_inputs(int id, int8_t* colors, int32_t* meta) {
+    Wave& wv = wave(id);
+    const int P = root_board_.npoints();
+    for (size_t i = 0; i < wv.leaves.size(); ++i) {
+      const Board& b = wv.leaves[i].board;
+      for (int p = 0; p < P; ++p) colors[i * P + p] = (int8_t)b.color(p);
+      int32_t* m = meta + i * 8;
+      m[0] = b.current_player();
+      m[1] = b.ko();
+      m[2] = b.last1();
+      m[3] = b.last2();
+      m[4] = b.passes_black();
+      m[5] = b.passes_white();
+      m[6] = b.nmoves();
+      m[7] = b.end_of_game() ? 1 : 0;
+    }
+  }
+
+  // black_z: mean rollout result per leaf from BLACK's point of view
+  void backup_rollout(int id, const float* black_z) {
+    Wave& wv = wave(id);
+    if (!wv.value_done) throw std::runtime_error("rollout backup before the value backup");
+    if (wv.rolling) {
+      wv.worker.join();
+      wv.rolling = false;
+    }
+    for (size_t i = 0; i < wv.leaves.size(); ++i) {
+      Leaf& L = wv.leaves[i];
+      float z = L.z;
+      if (black_z) z = L.board.current_player() == BLACK ? black_z[i] : -black_z[i];
+      backup_rollout_path(L.path, z, true);
+    }
+    rollouts_ += (long)wv.leaves.size();
+    waves_.erase(id);
+  }
+
+  // CPU rollouts of a wave on a background thread (the pool runs them)
+  void start_rollouts(int id) {
+    Wave& wv = wave(id);
+    if (wv.rolling) return;
+    wv.rolling = true;
+    const uint64_t base = seed * 0x100000001B3ull + (uint64_t)id * 0x9E3779B9ull;
+    Wave* w = &wv;
+    if (!rpool_) rpool_ = std::make_unique<Pool>(pool_.size());
+    wv.worker = std::thread([this, w, base]() {
+      rpool_->run((int)w->leaves.size(), [&](int i) {
+        Leaf& L = w->leaves[i];
+        Board b = L.board;
+        b.set_enforce_superko(false);
+        b.set_light(true);
+        Rng rng(base + (uint64_t)i * 7919ull);
+        const int ptm = L.board.current_player();
+        const int win = rollout_policy->rollout(b, rng, rollout_limit);
+        L.z = win == 0 ? 0.f : (win == ptm ? 1.f : -1.f);
+      });
+    });
+  }
+
+  void finish_rollouts(int id) { backup_rollout(id, nullptr); }
+
+  int pending_waves() const { return (int)waves_.size(); }
+
+  // ------------------------------------------------------------------ results / tree reuse
+  float node_q(const Node& c) const {
+    const bool use_r = lambda > 0.f && c.nr > 0, use_v = lambda < 1.f && c.n > 0;
+    if (use_r && use_v) return (1.f - lambda) * c.w / c.n + lambda * c.wr / c.nr;
+    if (use_r) return c.wr / c.nr;
+    if (use_v) return c.w / c.n;
+    return 0.f;
+  }
+
+  int best_move() const {
+    const Node& r = nodes_[root_];
+    if (r.state != N_EXPANDED || r.nchild == 0) return PASS;
+    int best = r.first;
+    for (int k = 1; k < r.nchild; ++k)
+      if (nodes_[r.first + k].n > nodes_[best].n) best = r.first + k;
+    return nodes_[best].move;
+  }
+
+  // (moves, visits, Q, prior) of the root's children
+  void root_stats(std::vector<int32_t>& mv, std::vector<int32_t>& vis, std::vector<float>& q,
+                  std::vector<float>& pr) const {
+    const Node& r = nodes_[root_];
+    const int nc = r.state == N_EXPANDED ? r.nchild : 0;
+    mv.resize(nc);
+    vis.resize(nc);
+    q.resize(nc);
+    pr.resize(nc);
+    for (int k = 0; k < nc; ++k) {
+      const Node& c = nodes_[r.first + k];
+      mv[k] = c.move;
+      vis[k] = c.n;
+      q[k] = node_q(c);
+      pr[k] = c.prior;
+    }
+  }
+
+  // Re-root at the child reached by `move` (played on the root board). All waves must have
+  // been finished. Returns true when the subtree was kept.
+  bool advance(int move) {
+    if (!waves_.empty()) throw std::runtime_error("advance() with waves in flight");
+    root_board_.do_move(move, 0);
+    const Node& r = nodes_[root_];
+    int child = -1;
+    if (r.state == N_EXPANDED)
+      for (int k = 0; k < r.nchild; ++k)
+        if (nodes_[r.first + k].move == move) child = r.first + k;
+    if (child < 0) {
+      Board b = root_board_;
+      reset(b);
+      return false;
+    }
+    compact(child);
+    return true;
+  }
+
+  long sims() const { return sims_; }
+  long rollouts() const { return rollouts_; }
+  long terminal() const { return terminal_; }
+  int collisions() const { return collisions_; }
+  size_t num_nodes() const { return nodes_.size(); }
+  int root_visits() const { return nodes_[root_].n; }
+
+ private:
+  void finish(int id) {
+    Wave& wv = wave(id);
+    if (wv.rolling) {
+      wv.worker.join();
+      wv.rolling = false;
+    }
+    waves_.erase(id);
+  }
+
+  void drop_waves() {
+    for (auto& kv : waves_)
+      if (kv.second->rolling) kv.second->worker.join();
+    waves_.clear();
+  }
+
+  void expand(int node, const std::vector<int>& non_eye, const float* pri) {
+    if (nodes_[node].state == N_EXPANDED) return;
+    const int first = (int)nodes_.size();
+    const int nc = non_eye.empty() ? 1 : (int)non_eye.size();
+    float tot = 0.f;
+    for (int k = 0; k < nc; ++k) {
+      const int mv = non_eye.empty() ? PASS : non_eye[k];
+      float p = 1.f;
+      if (pri && mv != PASS) p = std::max(pri[mv], 0.f);
+      tot += p;
+      nodes_.push_back(Node{node, -1, 0, (int16_t)mv, p, 0, 0, 0, 0.f, 0.f, N_NEW});
+    }
+    for (int k = 0; k < nc; ++k) {
+      Node& c = nodes_[first + k];
+      c.prior = tot > 0.f ? c.prior / tot : 1.f / nc;
+    }
+    Node& nd = nodes_[node];  // nodes_ may have reallocated
+    nd.first = first;
+    nd.nchild = (int16_t)nc;
+    nd.state = N_EXPANDED;
+  }
+
+  // v: value for the player to move at the leaf; a node at depth d stores it for its mover,
+  // who is the leaf's player to move iff D-d is odd.
+  void backup_value_path(const std::vector<int32_t>& path, float v, bool drop_vl) {
+    const int D = (int)path.size() - 1;
+    for (int d = D; d >= 0; --d) {
+      Node& nd = nodes_[path[d]];
+      nd.n += 1;
+      if (drop_vl) nd.vl -= 1;
+      nd.w += ((D - d) & 1) ? v : -v;
+    }
+  }
+  void backup_rollout_path(const std::vector<int32_t>& path, float z, bool drop_vl) {
+    const int D = (int)path.size() - 1;
+    for (int d = D; d >= 0; --d) {
+      Node& nd = nodes_[path[d]];
+      nd.nr += 1;
+      if (drop_vl) nd.vl -= 1;
+      nd.wr += ((D - d) & 1) ? z : -z;
+    }
+  }
+
+  // copy the subtree under `keep` into a fresh pool (BFS keeps children contiguous)
+  void compact(int keep) {
+    std::vector<Node> out;
+    out.reserve(std::max<size_t>(nodes_.size() / 4, 1 << 16));
+    std::vector<int32_t> q{keep};
+    Node r = nodes_[keep];
+    r.parent = -1;
+    r.vl = 0;
+    if (r.state == N_PENDING) r.state = N_NEW;
+    out.push_back(r);
+    std::vector<int32_t> newid{0};
+    for (size_t h = 0; h < q.size(); ++h) {
+      const Node& old = nodes_[q[h]];
+      const int nid = newid[h];
+      if (old.state != N_EXPANDED || old.nchild == 0) continue;
+      const int first = (int)out.size();
+      for (int k = 0; k < old.nchild; ++k) {
+        Node c = nodes_[old.first + k];
+        c.parent = nid;
+        c.vl = 0;
+        if (c.state == N_PENDING) c.state = N_NEW;
+        out.push_back(c);
+        q.push_back(old.first + k);
+        newid.push_back(first + k);
+      }
+      out[nid].first = first;
+    }
+    nodes_.swap(out);
+    root_ = 0;
+  }
+
+  Board root_board_;
+  std::vector<Node> nodes_;
+  int root_ = 0;
+  std::map<int, std::unique_ptr<Wave>> waves_;
+  int next_wave_ = 0;
+  Pool pool_;                    // expansions
+  std::unique_ptr<Pool> rpool_;  // CPU rollouts (run from a wave's worker thread)
+  long sims_ = 0, rollouts_ = 0, terminal_ = 0;
+  int collisions_ = 0;
+};
+
+
+}  // namespace rag
