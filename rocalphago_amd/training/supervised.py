@@ -293,6 +293,14 @@ def run_training(cmd_line_args=None):
 
     sgd = K.SGD(lr=args.learning_rate, decay=args.decay)
     model.compile(loss='categorical_crossentropy', optimizer=sgd, metrics=["accuracy"])
+    # exact resume: the optimizer step count (Keras decay schedule) and the data cursor live in
+    # a sidecar next to each weights file (the reference does not save them)
+    cursor = 0
+    opt_state = _opt_sidecar(os.path.join(args.out_directory, args.weights)) if resume else None
+    if opt_state:
+        sgd.iterations = int(opt_state["iterations"])
+        cursor = int(opt_state.get("cursor", 0))
+    epoch_base = len(meta_writer.metadata.get("epochs", []))
 
     ds = DeviceDataset.from_hdf5(dataset, dp.device)
     trainer = SupervisedTrainer(model, ds, args.minibatch, symmetries, dp,
@@ -305,29 +313,63 @@ def run_training(cmd_line_args=None):
         print("STARTING TRAINING")
     # each rank consumes its own contiguous slice of every global batch, cycling through the
     # fixed shuffled order (the reference generator never reshuffles between epochs)
-    cursor = 0
     gb = args.minibatch * dp.world
     n_train = dev_train.numel()
+    fault = _fault_step(dp.rank)
+    metrics_file = os.path.join(args.out_directory, "metrics.jsonl")
     for epoch in range(args.epochs):
         t0 = time.time()
         seen = 0
         while seen < samples_per_epoch and n_train > 0:
+            if fault is not None and sgd.iterations >= fault:
+                raise RuntimeError("injected fault at step %d (RAG_FAULT_AT_STEP)" % fault)
             pos = (cursor + dp.rank * args.minibatch + torch.arange(args.minibatch,
                                                                   device=dp.device)) % n_train
             trainer.step(dev_train[pos])
             cursor = (cursor + gb) % n_train
             seen += args.minibatch
         loss, acc = trainer.pop_metrics()
+        dt = time.time() - t0
         logs = {"loss": loss, "acc": acc}
         if n_val_data > 0:
             vl, va = trainer.evaluate(dev_val)
             logs["val_loss"], logs["val_acc"] = vl, va
-        meta_writer.on_epoch_end(epoch, logs)
-        checkpointer.on_epoch_end(epoch, logs)
+        gepoch = epoch_base + epoch
+        meta_writer.on_epoch_end(gepoch, logs)
+        checkpointer.on_epoch_end(gepoch, logs)
+        if dp.is_root:
+            ckpt = checkpointer.filepath.format(epoch=gepoch, **logs)
+            with open(os.path.splitext(ckpt)[0] + ".opt.json", "w") as f:
+                json.dump({"iterations": int(sgd.iterations), "cursor": int(cursor),
+                           "epoch": gepoch, "lr": args.learning_rate, "decay": args.decay}, f)
+            with open(metrics_file, "a") as f:
+                f.write(json.dumps(dict(logs, epoch=gepoch, seconds=round(dt, 3),
+                                        positions_per_s=round(seen * dp.world / max(dt, 1e-9), 1),
+                                        world=dp.world, step=int(sgd.iterations))) + "\n")
         if args.verbose and dp.is_root:
-            print("epoch %d: %s (%.1fs)" % (epoch, json.dumps(logs), time.time() - t0))
+            print("epoch %d: %s (%.1fs)" % (gepoch, json.dumps(logs), dt))
     dp.barrier()
     return meta_writer.metadata
+
+
+def _opt_sidecar(weights_path):
+    p = os.path.splitext(weights_path)[0] + ".opt.json"
+    if os.path.exists(p):
+        with open(p) as f:
+            return json.load(f)
+    return None
+
+
+def _fault_step(rank):
+    """RAG_FAULT_AT_STEP=n (or "r:n" for rank r only): raise at optimizer step n — fault
+    injection for the checkpoint/resume tests."""
+    spec = os.environ.get("RAG_FAULT_AT_STEP")
+    if not spec:
+        return None
+    if ":" in spec:
+        r, n = spec.split(":", 1)
+        return int(n) if int(r) == rank else None
+    return int(spec)
 
 
 if __name__ == '__main__':
