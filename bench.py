@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--no-mcts", action="store_true",
                     help="skip the APV-MCTS sims/s measurement (run after the timed SL steps)")
     ap.add_argument("--mcts-playouts", type=int, default=4096)
+    ap.add_argument("--trace", default=None,
+                    help="also write a Chrome trace (torch.profiler) of 5 untimed steps here")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -117,6 +119,15 @@ def main():
     dp.barrier()
     dt = time.perf_counter() - t0
     dt = dp.max_scalar(dt)
+    if args.trace:
+        # host + device timeline of a few extra (untimed) steps, Chrome-trace JSON
+        from torch.profiler import ProfilerActivity, profile
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+            for _ in range(5):
+                step()
+            torch.cuda.synchronize()
+        path = args.trace if dp.world == 1 else "%s.rank%d.json" % (args.trace, dp.rank)
+        prof.export_chrome_trace(path)
     if args.model == "policy":
         loss, acc = trainer.pop_metrics()
     else:
