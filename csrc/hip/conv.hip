@@ -455,6 +455,38 @@ __global__ void pack_input_kernel(const T* __restrict__ F, const int64_t* __rest
   }
 }
 
+// Bit-packed positions (one 64-bit word per point, bit f = plane f; 2.9 KB per 19x19 position
+// instead of 17 KB of uint8 planes, so a GPU-resident buffer holds ~6x more positions) ->
+// padded bf16 trunk input, with the same index gather and dihedral transform.
+__global__ void pack_input_bits_kernel(const uint64_t* __restrict__ Fb,
+                                       const int64_t* __restrict__ index,
+                                       const int* __restrict__ tf, bf16* __restrict__ X, int B,
+                                       int NF, int S, int H, int CP) {
+  const int S2 = S * S;
+  const int total = B * S2;
+  const int WP = S + 2 * H;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += gridDim.x * blockDim.x) {
+    const int b = idx / S2;
+    const int rem = idx - b * S2;
+    const int i = rem / S, j = rem - (rem / S) * S;
+    int si = i, sj = j;
+    if (tf) dihedral(tf[b], S, i, j, si, sj);
+    const int64_t sb = index ? index[b] : b;
+    const uint64_t word = Fb[(size_t)sb * S2 + si * S + sj];
+    bf16* dst = X + ((size_t)(b * WP + i + H) * WP + j + H) * CP;
+    for (int c8 = 0; c8 < CP; c8 += 8) {
+      bf16x8 v;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int c = c8 + k;
+        v[k] = (bf16)((c < NF && ((word >> c) & 1ull)) ? 1.f : 0.f);
+      }
+      *reinterpret_cast<bf16x8*>(dst + c8) = v;
+    }
+  }
+}
+
 // padded channels-last bf16 -> NCHW fp32 (tests / debugging / generic consumers)
 __global__ void unpack_kernel(const bf16* __restrict__ X, float* __restrict__ out, int B, int C,
                               int S, int H, int CP) {
@@ -743,6 +775,15 @@ RAG_API int rag_pack_input_u8(const uint8_t* F, const int64_t* index, const int*
   const int total = B * S * S;
   const int blocks = (total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096;
   pack_input_kernel<uint8_t><<<blocks, 256, 0, stream>>>(F, index, tf, (bf16*)X, B, NF, S, H, CP);
+  return (int)hipGetLastError();
+}
+
+RAG_API int rag_pack_input_bits(const uint64_t* Fb, const int64_t* index, const int* tf, void* X,
+                                int B, int NF, int S, int H, int CP, hipStream_t stream) {
+  if (NF > 64) return -1;
+  const int total = B * S * S;
+  const int blocks = (total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096;
+  pack_input_bits_kernel<<<blocks, 256, 0, stream>>>(Fb, index, tf, (bf16*)X, B, NF, S, H, CP);
   return (int)hipGetLastError();
 }
 

@@ -87,15 +87,16 @@ class _TrunkPlan(object):
         return dWs, dbs
 
     def prepare(self, x, index=None, transforms=None):
-        """Pack input planes [N, F, S, S] (uint8 or fp32, on device) into the trunk input."""
+        """Pack input planes [N, F, S, S] (uint8 or fp32, on device), or bit-packed positions
+        [N, S, S] int64 (training/replay.py), into the trunk input."""
         B = x.shape[0] if index is None else index.shape[0]
         self.trunk.ensure_batch(B)
         Ws, bs = self._params()
         self.trunk.sync_weights(Ws, bs, self.net.weights_version())
-        if x.dtype not in (torch.uint8, torch.float32):
+        if x.dtype not in (torch.uint8, torch.float32, torch.int64):
             x = x.float()
         ops.pack_input(x.contiguous(), self.trunk.input_buffer(B), self.trunk.halo[0],
-                       index=index, transforms=transforms)
+                       index=index, transforms=transforms, nplanes=self.trunk.specs[0].cin)
         return B
 
     def head_params(self):

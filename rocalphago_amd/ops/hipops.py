@@ -100,13 +100,21 @@ def conv_wgrad(g, x, dw, db, B, S, hi, cout, coutp, cin, cinp, ks, accumulate=Fa
                                  _stream(), rs), "conv_wgrad")
 
 
-def pack_input(features, out, H, index=None, transforms=None):
-    """[N, F, S, S] uint8/float32 planes (optionally gathered by ``index`` [B] and dihedral-
-    transformed by ``transforms`` [B] int32) -> padded bf16 ``out`` [B, S+2H, S+2H, CP]."""
+def pack_input(features, out, H, index=None, transforms=None, nplanes=None):
+    """[N, F, S, S] uint8/float32 planes, or bit-packed int64 words [N, S, S] with ``nplanes``
+    (training/replay.py), optionally gathered by ``index`` [B] and dihedral-transformed by
+    ``transforms`` [B] int32 -> padded bf16 ``out`` [B, S+2H, S+2H, CP]."""
     B = out.shape[0]
     S = features.shape[-1]
-    NF = features.shape[1]
     CP = out.shape[-1]
+    if features.dtype == torch.int64:
+        if nplanes is None:
+            raise ValueError("bit-packed input needs nplanes")
+        _check(_lib().rag_pack_input_bits(_ptr(features), _ptr(index), _ptr(transforms),
+                                          _ptr(out), B, int(nplanes), S, H, CP, _stream()),
+               "pack_input_bits")
+        return out
+    NF = features.shape[1]
     fn = _lib().rag_pack_input_u8 if features.dtype == torch.uint8 else _lib().rag_pack_input_f32
     if features.dtype not in (torch.uint8, torch.float32):
         features = features.float()

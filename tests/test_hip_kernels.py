@@ -167,3 +167,40 @@ def test_dgrad_mixed_halos(ops):
     ops.conv_igemm(gp, wb, None, dx, B, S, 1, 2, cout, cin, ks, False, mask=xm, mask_halo=1)
     assert rel_err(ops.unpack(dx, cin, 2), xr.grad * (x > 0)) < 2e-2
     assert dx[:, :2].abs().max().item() == 0 and dx[:, :, -2:].abs().max().item() == 0
+
+
+def test_pack_input_bits_matches_uint8(ops):
+    from rocalphago_amd.training.replay import pack_bits
+    dev = torch.device("cuda")
+    S, NF, B = 19, 49, 16
+    feats = (torch.rand(40, NF, S, S, device=dev) > 0.5).to(torch.uint8)
+    bits = pack_bits(feats)
+    idx = torch.randint(0, 40, (B,), device=dev)
+    tf = torch.randint(0, 8, (B,), device=dev, dtype=torch.int32)
+    a = ops.alloc_padded(B, S, 2, 64, dev)
+    b = ops.alloc_padded(B, S, 2, 64, dev)
+    ops.pack_input(feats, a, 2, index=idx, transforms=tf)
+    ops.pack_input(bits, b, 2, index=idx, transforms=tf, nplanes=NF)
+    assert torch.equal(a, b)
+
+
+def test_packed_dataset_training_matches_plain(ops):
+    from rocalphago_amd.models import kerasish as K
+    from rocalphago_amd.models.policy import CNNPolicy
+    from rocalphago_amd.training.data import DeviceDataset
+    from rocalphago_amd.training.replay import PackedDataset
+    from rocalphago_amd.training.supervised import SupervisedTrainer
+    from rocalphago_amd.features.preprocessing import DEFAULT_FEATURES
+    rs = np.random.RandomState(4)
+    st = (rs.rand(64, 48, 19, 19) > 0.6).astype(np.uint8)
+    acts = rs.randint(0, 361, 64)
+    losses = []
+    for cls in (DeviceDataset, PackedDataset):
+        pol = CNNPolicy(DEFAULT_FEATURES, filters_per_layer=64, layers=3, device="cuda", seed=9)
+        pol.model.compile(loss="categorical_crossentropy", optimizer=K.SGD(lr=0.05))
+        tr = SupervisedTrainer(pol.model, cls(st, acts, "cuda"), 32, ["noop", "rot90"], None,
+                               seed=1)
+        for s in range(3):
+            tr.step(torch.arange(s * 16, s * 16 + 32, device="cuda") % 64)
+        losses.append(tr.pop_metrics()[0])
+    assert abs(losses[0] - losses[1]) < 1e-5
