@@ -84,6 +84,7 @@ class ValueTrainer(object):
             torch.from_numpy(np.asarray(values, np.float32).reshape(-1, 1)).to(self.dev)
         self.B = batch_size
         self.dp = dp
+        self.planes = value_model.input_shape[-3]  # (None,) F, S, S
         self.sym = torch.tensor(transform_ids(symmetries or ["noop"]), dtype=torch.int32,
                                 device=self.dev)
         self.gen = torch.Generator(device=self.dev)
@@ -111,7 +112,11 @@ class ValueTrainer(object):
             self.loss_sum += loss * n
         else:
             from .data import apply_transform_np
-            st = self.states[index].cpu().numpy()
+            st = self.states[index]
+            if st.dtype == torch.int64:  # bit-packed (training/replay.py)
+                from .replay import unpack_bits
+                st = unpack_bits(st, self.planes)
+            st = st.cpu().numpy()
             X = np.stack([apply_transform_np(s, int(t)) for s, t in zip(st, tf.cpu().numpy())])
             saved = model.grad_allreduce
             if self.dp is not None and self.dp.enabled:
@@ -120,6 +125,13 @@ class ValueTrainer(object):
             model.grad_allreduce = saved
             self.loss_sum += float(loss) * n
         self.count += n
+
+    @classmethod
+    def from_replay(cls, value_model, buffer, batch_size, symmetries=None, dp=None, seed=0):
+        """Train directly on a ReplayBuffer (bit-packed positions, float outcomes); sample
+        indices with ``buffer.sample``."""
+        return cls(value_model, buffer.states[:len(buffer)],
+                   buffer.targets[:len(buffer)].reshape(-1, 1), batch_size, symmetries, dp, seed)
 
     def pop_loss(self):
         t = torch.stack([self.loss_sum, torch.tensor(float(self.count), device=self.dev)])

@@ -62,3 +62,17 @@ def test_supervised_trainer_on_packed_cpu():
     tr.step(torch.arange(8))
     loss, _ = tr.pop_metrics()
     assert np.isfinite(loss)
+
+
+def test_value_trainer_from_replay_cpu():
+    from rocalphago_amd.features.preprocessing import VALUE_FEATURES
+    from rocalphago_amd.models import kerasish as K
+    from rocalphago_amd.models.value import CNNValue
+    from rocalphago_amd.training.value_trainer import ValueTrainer
+    val = CNNValue(VALUE_FEATURES, board=7, filters_per_layer=8, layers=2, device="cpu")
+    val.model.compile(loss="mse", optimizer=K.SGD(lr=0.01))
+    rb = ReplayBuffer(64, 49, 7, "cpu")
+    rb.add((torch.rand(40, 49, 7, 7) > 0.5).to(torch.uint8), torch.randint(0, 2, (40,)) * 2 - 1)
+    tr = ValueTrainer.from_replay(val.model, rb, 8, ["noop", "fliplr"])
+    tr.step(rb.sample(8, torch.Generator().manual_seed(1)))
+    assert np.isfinite(tr.pop_loss())
