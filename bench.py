@@ -40,17 +40,23 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256, help="positions per GPU per step")
-    ap.add_argument("--filters", type=int, default=192)
-    ap.add_argument("--layers", type=int, default=12)
+    ap.add_argument("--filters", type=int, default=None,
+                    help="default 192 (policy/value), 128 (resnet, ResnetPolicy's default)")
+    ap.add_argument("--layers", type=int, default=None, help="default 12 (policy/value), 20 (resnet)")
     ap.add_argument("--dataset", type=int, default=65536, help="synthetic positions per GPU")
-    ap.add_argument("--model", default="policy", choices=["policy", "value"],
-                    help="policy: SL policy net (headline); value: value net (BASELINE config 4)")
+    ap.add_argument("--model", default="policy", choices=["policy", "value", "resnet"],
+                    help="policy: SL policy net (headline); value: value net (BASELINE config 4); "
+                         "resnet: ResnetPolicy SL training (batch-statistics BN)")
     ap.add_argument("--no-mcts", action="store_true",
                     help="skip the APV-MCTS sims/s measurement (run after the timed SL steps)")
     ap.add_argument("--mcts-playouts", type=int, default=4096)
     ap.add_argument("--trace", default=None,
                     help="also write a Chrome trace (torch.profiler) of 5 untimed steps here")
     args = ap.parse_args()
+    if args.filters is None:
+        args.filters = 128 if args.model == "resnet" else 192
+    if args.layers is None:
+        args.layers = 20 if args.model == "resnet" else 12
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # launched by hand: spawn one rank per GPU (child process, no exec)
@@ -75,9 +81,14 @@ def main():
     torch.manual_seed(1234)
     gen = torch.Generator(device=dev)
     gen.manual_seed(99 + dp.rank)
-    if args.model == "policy":
-        policy = CNNPolicy(DEFAULT_FEATURES, board=19, filters_per_layer=args.filters,
-                           layers=args.layers, device=dev, seed=1234)
+    if args.model in ("policy", "resnet"):
+        if args.model == "resnet":
+            from rocalphago_amd.models.policy import ResnetPolicy
+            policy = ResnetPolicy(DEFAULT_FEATURES, board=19, filters_per_layer=args.filters,
+                                  layers=args.layers, device=dev, seed=1234)
+        else:
+            policy = CNNPolicy(DEFAULT_FEATURES, board=19, filters_per_layer=args.filters,
+                               layers=args.layers, device=dev, seed=1234)
         model = policy.model
         dp.broadcast_model(model)
         model.compile(loss="categorical_crossentropy", optimizer=K.SGD(lr=0.003, decay=0.0001),
@@ -128,7 +139,7 @@ def main():
             torch.cuda.synchronize()
         path = args.trace if dp.world == 1 else "%s.rank%d.json" % (args.trace, dp.rank)
         prof.export_chrome_trace(path)
-    if args.model == "policy":
+    if args.model in ("policy", "resnet"):
         loss, acc = trainer.pop_metrics()
     else:
         loss = trainer.pop_loss()
@@ -168,6 +179,13 @@ def main():
                                     "FC256 + tanh, MSE), %d params" % (args.filters, nparams)
         result["baseline_note"] = "vs_baseline = value / 2600 positions/s (paper-derived value " \
                                   "training throughput, BASELINE.md)"
+    if args.model == "resnet":
+        result["metric"] = "positions/sec ResnetPolicy SL train (19x19) at 1/2/4/8 MI355X"
+        result["vs_baseline"] = None
+        result["config"]["model"] = "19x19 ResnetPolicy (48 planes, %d filters, %d layers, " \
+                                    "column BN + ReLU + residual units), %d params" % (
+                                        args.filters, args.layers, nparams)
+        result["baseline_note"] = "no published baseline for the residual policy"
     if not args.no_mcts and args.model == "policy":
         # one independent search per GPU (root parallelism); whole-job sims/s = sum over ranks.
         # Every rank reaches the all-reduce whether or not its measurement worked (no hang).

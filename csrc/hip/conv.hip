@@ -30,7 +30,7 @@ template <int KS, int NT>
 __global__ void __launch_bounds__(256, 3)
 conv_igemm_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                   const float* __restrict__ bias, bf16* __restrict__ Y,
-                  const bf16* __restrict__ mask, int M, int S, int WI, int shift, int WO, int HO,
+                  const bf16* __restrict__ mask, const bf16* __restrict__ res, int M, int S, int WI, int shift, int WO, int HO,
                   int CIN, int WROWS, int YC, int relu, int HM) {
   constexpr int BN = 32 * NT;
   constexpr int WN = 16 * NT;
@@ -145,6 +145,11 @@ conv_igemm_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
         v[1] += bb.y;
         v[2] += bb.z;
         v[3] += bb.w;
+      }
+      if (res) {  // residual (ResNet sum-merge), laid out like Y
+        const bf16x4 rv = *reinterpret_cast<const bf16x4*>(res + orow + n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += (float)rv[r];
       }
       if (relu) {
 #pragma unroll
@@ -344,50 +349,66 @@ conv_wgrad_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
   if (do_bias && (int)threadIdx.x < BNN) bpart[(size_t)chunk * COUTP + n0 + threadIdx.x] = bsum;
 }
 
-// sum partial slabs -> OIHW fp32 weight gradient (unpadded) and bias gradient
-__global__ void wgrad_reduce_kernel(const float* __restrict__ part, const float* __restrict__ bpart,
-                                    float* __restrict__ dW, float* __restrict__ db, int nchunks,
-                                    int taps, int COUT, int CIN, int COUTP, int CINP, int KS,
-                                    int accumulate) {
-  // Threads walk the slab in its own [tap][n][c] order, 4 channels (16 B) per thread, so every
-  // chunk read is a coalesced float4 stream; the (4x smaller) OIHW writes are the scattered side.
+// sum partial slabs -> OIHW fp32 weight gradient (unpadded) and bias gradient.
+// Block = 64 consecutive float4 quads of the slab ([tap][n][c] order: every wave load is one
+// coalesced 1 KB row) x 4 waves that split the chunks (k = wave mod 4, 4 loads in flight per
+// lane), combined through LDS. Enough blocks to fill the chip even for K=128 (576 blocks) and
+// 16 outstanding 16-byte loads per quad: the slab walk runs at HBM/MALL speed instead of being
+// latency-bound on one serial chunk loop per thread. The last block row sums the bias slabs.
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(
+    const float* __restrict__ part, const float* __restrict__ bpart, float* __restrict__ dW,
+    float* __restrict__ db, int nchunks, int taps, int COUT, int CIN, int COUTP, int CINP, int KS,
+    int accumulate) {
+  __shared__ float4 red[3][64];
   const size_t slab = (size_t)taps * COUTP * CINP;
   const int quads = (int)(slab / 4);
-  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < quads + COUTP;
-       q += gridDim.x * blockDim.x) {
-    if (q < quads) {
-      const size_t off = (size_t)q * 4;
-      const int c = (int)(off % CINP);
-      const int tn = (int)(off / CINP);
-      const int n = tn % COUTP, tap = tn / COUTP;
-      if (n >= COUT || c >= CIN) continue;
-      const float4* p = reinterpret_cast<const float4*>(part + off);
-      const size_t st = slab / 4;
-      float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
-      int k = 0;
-      for (; k + 1 < nchunks; k += 2) {
-        const float4 a = p[k * st], b = p[(k + 1) * st];
-        s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
-        s1.x += b.x; s1.y += b.y; s1.z += b.z; s1.w += b.w;
-      }
-      if (k < nchunks) {
-        const float4 a = p[k * st];
-        s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
-      }
-      const float v[4] = {s0.x + s1.x, s0.y + s1.y, s0.z + s1.z, s0.w + s1.w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (c + j >= CIN) break;
-        const size_t o = ((size_t)n * CIN + c + j) * taps + tap;  // OIHW
-        dW[o] = accumulate ? dW[o] + v[j] : v[j];
-      }
-    } else if (db && bpart) {
-      const int n = q - quads;
-      if (n >= COUT) continue;
-      float s = 0.f;
-      for (int k = 0; k < nchunks; ++k) s += bpart[(size_t)k * COUTP + n];
-      db[n] = accumulate ? db[n] + s : s;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int qblocks = (quads + 63) / 64;
+  if ((int)blockIdx.x >= qblocks) {  // bias: COUTP values, 64 per block
+    const int n = ((int)blockIdx.x - qblocks) * 64 + lane;
+    if (w != 0 || !db || !bpart || n >= COUT) return;
+    float s = 0.f;
+    for (int k = 0; k < nchunks; ++k) s += bpart[(size_t)k * COUTP + n];
+    db[n] = accumulate ? db[n] + s : s;
+    return;
+  }
+  const int q = blockIdx.x * 64 + lane;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (q < quads) {
+    const float4* p = reinterpret_cast<const float4*>(part) + q;
+    const size_t st = slab / 4;
+    int k = w;
+    for (; k + 12 < nchunks; k += 16) {
+      const float4 a = p[k * st], b = p[(k + 4) * st], c = p[(k + 8) * st], d = p[(k + 12) * st];
+      acc.x += (a.x + b.x) + (c.x + d.x);
+      acc.y += (a.y + b.y) + (c.y + d.y);
+      acc.z += (a.z + b.z) + (c.z + d.z);
+      acc.w += (a.w + b.w) + (c.w + d.w);
     }
+    for (; k < nchunks; k += 4) {
+      const float4 a = p[k * st];
+      acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
+    }
+  }
+  if (w) red[w - 1][lane] = acc;
+  __syncthreads();
+  if (w || q >= quads) return;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float4 o = red[i][lane];
+    acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
+  }
+  const size_t off = (size_t)q * 4;
+  const int c = (int)(off % CINP);
+  const int tn = (int)(off / CINP);
+  const int n = tn % COUTP, tap = tn / COUTP;
+  if (n >= COUT || c >= CIN) return;
+  const float v[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (c + j >= CIN) break;
+    const size_t o = ((size_t)n * CIN + c + j) * taps + tap;  // OIHW
+    dW[o] = accumulate ? dW[o] + v[j] : v[j];
   }
 }
 
@@ -522,12 +543,12 @@ __global__ void pack_nchw_kernel(const float* __restrict__ in, bf16* __restrict_
 
 template <int KS>
 void launch_igemm_ks(int nt, dim3 grid, hipStream_t st, const bf16* X, const bf16* W,
-                     const float* bias, bf16* Y, const bf16* mask, int M, int S, int WI,
+                     const float* bias, bf16* Y, const bf16* mask, const bf16* res, int M, int S, int WI,
                      int shift, int WO, int HO, int CIN, int WROWS, int YC, int relu, int HM) {
   switch (nt) {
 #define RAG_NT(N)                                                                              \
   case N:                                                                                      \
-    conv_igemm_kernel<KS, N><<<grid, 256, 0, st>>>(X, W, bias, Y, mask, M, S, WI, shift, WO, \
+    conv_igemm_kernel<KS, N><<<grid, 256, 0, st>>>(X, W, bias, Y, mask, res, M, S, WI, shift, WO, \
                                                    HO, CIN, WROWS, YC, relu, HM);             \
     break;
     RAG_NT(1) RAG_NT(2) RAG_NT(3) RAG_NT(4) RAG_NT(6)
@@ -547,17 +568,19 @@ int pick_nt(int coutp) {
 
 // ============================================================================= C ABI
 bool rag_conv_pipe_launch(const bf16* x, const bf16* w, const float* bias, bf16* y,
-                          const bf16* mk, int M, int S, int WI, int shift, int WO, int HO,
-                          int CIN, int COUTP, int YC, int KS, int relu, int HM,
+                          const bf16* mk, const bf16* res, int M, int S, int WI, int shift,
+                          int WO, int HO, int CIN, int COUTP, int YC, int KS, int relu, int HM,
                           hipStream_t stream);  // conv_fwd.hip
 
 // Conv forward / dgrad.  X: padded input (halo HI, CIN channels, CIN % 32 == 0).  W: packed
 // bf16 weights [taps][WROWS][CIN].  Y: padded output (halo HO, YC channels, COUTP % 32 == 0,
 // COUTP <= YC).  bias: fp32 [COUTP] or null.  mask: the dgrad ReLU mask (layer input), null or
-// laid out like Y but with its own halo HM.
+// laid out like Y but with its own halo HM.  res: null or a residual added before the activation
+// (ResNet sum-merge), laid out like Y (may alias Y: each element is read then written by one lane).
 RAG_API int rag_conv_igemm(const void* X, const void* W, const float* bias, void* Y,
-                           const void* mask, int B, int S, int HI, int HO, int CIN, int COUTP,
-                           int YC, int KS, int relu, int HM, hipStream_t stream) {
+                           const void* mask, const void* resid, int B, int S, int HI, int HO,
+                           int CIN, int COUTP, int YC, int KS, int relu, int HM,
+                           hipStream_t stream) {
   if (CIN % 32 || COUTP % 32 || YC < COUTP || HI < KS / 2) return -1;
   const int M = B * S * S;
   const int nt = pick_nt(COUTP);
@@ -567,18 +590,19 @@ RAG_API int rag_conv_igemm(const void* X, const void* W, const float* bias, void
   const bf16* w = (const bf16*)W;
   bf16* y = (bf16*)Y;
   const bf16* mk = (const bf16*)mask;
+  const bf16* res = (const bf16*)resid;
   static const bool use_pipe = [] {
     const char* e = getenv("RAG_CONV_PIPE");
     return !(e && e[0] == '0');
   }();
-  if (use_pipe && rag_conv_pipe_launch(x, w, bias, y, mk, M, S, WI, shift, WO, HO, CIN, COUTP,
-                                       YC, KS, relu, HM, stream))
+  if (use_pipe && rag_conv_pipe_launch(x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN,
+                                       COUTP, YC, KS, relu, HM, stream))
     return (int)hipGetLastError();
   switch (KS) {
-    case 1: launch_igemm_ks<1>(nt, grid, stream, x, w, bias, y, mk, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM); break;
-    case 3: launch_igemm_ks<3>(nt, grid, stream, x, w, bias, y, mk, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM); break;
-    case 5: launch_igemm_ks<5>(nt, grid, stream, x, w, bias, y, mk, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM); break;
-    case 7: launch_igemm_ks<7>(nt, grid, stream, x, w, bias, y, mk, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM); break;
+    case 1: launch_igemm_ks<1>(nt, grid, stream, x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM); break;
+    case 3: launch_igemm_ks<3>(nt, grid, stream, x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM); break;
+    case 5: launch_igemm_ks<5>(nt, grid, stream, x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM); break;
+    case 7: launch_igemm_ks<7>(nt, grid, stream, x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM); break;
     default: return -2;
   }
   return (int)hipGetLastError();
@@ -710,8 +734,8 @@ RAG_API int rag_conv_wgrad(const void* G, const void* X, float* dW, float* db, f
     if (hipStreamWaitEvent(reduce_stream, ev, 0) != hipSuccess) return -3;
     rs = reduce_stream;
   }
-  const int total = taps * COUTP * CINP / 4 + COUTP;
-  wgrad_reduce_kernel<<<(total + 255) / 256, 256, 0, rs>>>(part, bpart, dW, db, nchunks, taps,
+  const int nblk = (taps * COUTP * CINP / 4 + 63) / 64 + (COUTP + 63) / 64;
+  wgrad_reduce_kernel<<<nblk, 256, 0, rs>>>(part, bpart, dW, db, nchunks, taps,
                                                           COUT, CIN, COUTP, CINP, KS, accumulate);
   return (int)hipGetLastError();
 }

@@ -31,7 +31,7 @@ template <int KS, int NT, int MT>
 __global__ void __launch_bounds__(256, 2)
 conv_pipe_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                  const float* __restrict__ bias, bf16* __restrict__ Y,
-                 const bf16* __restrict__ mask, int M, int S, int WI, int shift, int WO, int HO,
+                 const bf16* __restrict__ mask, const bf16* __restrict__ res, int M, int S, int WI, int shift, int WO, int HO,
                  int CIN, int WROWS, int YC, int relu, int HM) {
   constexpr int kBM = 32 * MT;  // 2 waves along M, MT 16-row fragments each
   constexpr int WM = 16 * MT;
@@ -231,6 +231,11 @@ conv_pipe_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
         v[2] += bb.z;
         v[3] += bb.w;
       }
+      if (res) {  // residual (ResNet sum-merge), laid out like Y
+        const bf16x4 rv = *reinterpret_cast<const bf16x4*>(res + orow + n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += (float)rv[r];
+      }
       if (relu) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
@@ -249,20 +254,40 @@ conv_pipe_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
 }
 
 template <int KS>
-bool launch_ks(int nt, dim3 grid, hipStream_t st, const bf16* X, const bf16* W,
-               const float* bias, bf16* Y, const bf16* mask, int M, int S, int WI, int shift,
-               int WO, int HO, int CIN, int WROWS, int YC, int relu, int HM) {
-  switch (nt) {
-#define RAG_PIPE(N)                                                                           \
-  case N:                                                                                     \
-    conv_pipe_kernel<KS, N, (N == 6 ? 6 : 4)><<<grid, 256, 0, st>>>(X, W, bias, Y, mask, M, S, WI, shift, WO,  \
-                                                  HO, CIN, WROWS, YC, relu, HM);             \
-    return true;
-    RAG_PIPE(2) RAG_PIPE(4) RAG_PIPE(6)
-#undef RAG_PIPE
-    default:
-      return false;
+bool launch_ks(int nt, int mt, dim3 grid, hipStream_t st, const bf16* X, const bf16* W,
+               const float* bias, bf16* Y, const bf16* mask, const bf16* res, int M, int S,
+               int WI, int shift, int WO, int HO, int CIN, int WROWS, int YC, int relu, int HM) {
+#define RAG_PIPE(N, T)                                                                        \
+  if (nt == N && mt == T) {                                                                   \
+    conv_pipe_kernel<KS, N, T><<<grid, 256, 0, st>>>(X, W, bias, Y, mask, res, M, S, WI, shift, \
+                                                     WO, HO, CIN, WROWS, YC, relu, HM);       \
+    return true;                                                                              \
   }
+  RAG_PIPE(2, 4) RAG_PIPE(2, 6) RAG_PIPE(2, 8) RAG_PIPE(4, 4) RAG_PIPE(4, 6) RAG_PIPE(4, 8)
+  RAG_PIPE(6, 4) RAG_PIPE(6, 6)
+#undef RAG_PIPE
+  return false;
+}
+
+// Pixel-tile height (MT 16-row fragments per wave, BM = 32*MT): the candidate that fills the
+// 512 resident-block slots (2 per CU) best — e.g. K=128 at B=256 (M=92416): MT=4 gives 722
+// blocks (two rounds, the second 41% full), MT=6 gives 482 blocks (one round, 94% full).
+int pick_mt(int M, int nt, int ntiles_n) {
+  const int cands[3] = {4, 6, 8};
+  const int ncand = nt == 6 ? 2 : 3;
+  int best = 4;
+  double best_eff = -1.0;
+  for (int i = 0; i < ncand; ++i) {
+    const int mt = cands[i];
+    const long nblk = (long)((M + 32 * mt - 1) / (32 * mt)) * ntiles_n;
+    const long rounds = (nblk + 511) / 512;
+    const double eff = (double)nblk / (double)(rounds * 512);
+    if (eff > best_eff + 0.02) {
+      best_eff = eff;
+      best = mt;
+    }
+  }
+  return best;
 }
 
 }  // namespace
@@ -270,18 +295,24 @@ bool launch_ks(int nt, dim3 grid, hipStream_t st, const bf16* X, const bf16* W,
 // Returns true if the pipelined kernel handled the launch (COUTP multiple of 64; any KS in
 // {1,3,5,7}); false leaves it to the generic kernel in conv.hip.
 bool rag_conv_pipe_launch(const bf16* x, const bf16* w, const float* bias, bf16* y,
-                          const bf16* mk, int M, int S, int WI, int shift, int WO, int HO,
-                          int CIN, int COUTP, int YC, int KS, int relu, int HM, hipStream_t stream) {
+                          const bf16* mk, const bf16* res, int M, int S, int WI, int shift,
+                          int WO, int HO, int CIN, int COUTP, int YC, int KS, int relu, int HM, hipStream_t stream) {
   const int nt = COUTP % 192 == 0 ? 6 : (COUTP % 128 == 0 ? 4 : (COUTP % 64 == 0 ? 2 : 0));
   if (!nt) return false;
-  const int bm = nt == 6 ? 192 : 128;
+  const int ntn = COUTP / (32 * nt);
+  static const int force_mt = [] {
+    const char* e = getenv("RAG_CONV_MT");
+    return e ? atoi(e) : 0;
+  }();
+  const int mt = force_mt ? force_mt : pick_mt(M, nt, ntn);
+  const int bm = 32 * mt;
   const int nblk_m = (M + bm - 1) / bm;
-  dim3 grid(nblk_m * (COUTP / (32 * nt)));
+  dim3 grid(nblk_m * ntn);
   switch (KS) {
-    case 1: return launch_ks<1>(nt, grid, stream, x, w, bias, y, mk, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM);
-    case 3: return launch_ks<3>(nt, grid, stream, x, w, bias, y, mk, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM);
-    case 5: return launch_ks<5>(nt, grid, stream, x, w, bias, y, mk, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM);
-    case 7: return launch_ks<7>(nt, grid, stream, x, w, bias, y, mk, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM);
+    case 1: return launch_ks<1>(nt, mt, grid, stream, x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM);
+    case 3: return launch_ks<3>(nt, mt, grid, stream, x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM);
+    case 5: return launch_ks<5>(nt, mt, grid, stream, x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM);
+    case 7: return launch_ks<7>(nt, mt, grid, stream, x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM);
     default: return false;
   }
 }

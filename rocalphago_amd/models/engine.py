@@ -32,7 +32,49 @@ class ConvSpec(object):
         self.halo_in = max(1, ks // 2)
 
 
-class HipTrunk(object):
+class _PackedConvs(object):
+    """bf16 GEMM layouts (+ padded fp32 biases) of a list of convolutions, repacked from the fp32
+    OIHW masters in one launch whenever the model's weight version changes."""
+
+    def _init_packing(self, specs, device):
+        self._wf = [None] * len(specs)
+        self._wb = [None] * len(specs)
+        self._bias = [torch.zeros(s.coutp, device=device) for s in specs]
+        self._packed_version = None
+
+    def sync_weights(self, weights, biases, version):
+        """Repack bf16 GEMM layouts from fp32 OIHW masters when ``version`` changed."""
+        if version == self._packed_version:
+            return
+        for l, s in enumerate(self.specs):
+            taps = s.ks * s.ks
+            if self._wf[l] is None:
+                self._wf[l] = torch.empty((taps, s.coutp, s.cinp), dtype=torch.bfloat16,
+                                          device=self.device)
+                self._wb[l] = torch.empty((taps, s.cinp, s.coutp), dtype=torch.bfloat16,
+                                          device=self.device)
+        # one launch repacks all layers (GEMM layouts + padded biases); the pointer table is
+        # rebuilt only when a parameter tensor moved
+        ws = [w.contiguous() for w in weights]
+        key = tuple(w.data_ptr() for w in ws) + \
+            tuple(0 if b is None else b.data_ptr() for b in biases)
+        if getattr(self, "_pack_key", None) != key:
+            rows, start = [], 0
+            for l, s in enumerate(self.specs):
+                b = biases[l]
+                rows.append([ws[l].data_ptr(), 0 if b is None else b.data_ptr(), s.cout, s.cin,
+                             s.ks, s.coutp, s.cinp, self._wf[l].data_ptr(),
+                             self._wb[l].data_ptr(), self._bias[l].data_ptr(), start])
+                start += s.ks * s.ks * s.coutp * s.cinp + s.coutp
+            self._pack_table = torch.tensor(rows, dtype=torch.int64).to(self.device)
+            self._pack_total = start
+            self._pack_key = key
+            self._pack_keep = ws  # keep contiguous copies alive while the table points at them
+        ops.pack_trunk(self._pack_table, len(self.specs), self._pack_total)
+        self._packed_version = version
+
+
+class HipTrunk(_PackedConvs):
     def __init__(self, specs, board, device):
         assert specs, "empty trunk"
         self.specs = specs
@@ -44,10 +86,7 @@ class HipTrunk(object):
         self._B = 0
         self.acts = []
         self._gbufs = {}
-        self._wf = [None] * self.L
-        self._wb = [None] * self.L
-        self._bias = [torch.zeros(s.coutp, device=device) for s in specs]
-        self._packed_version = None
+        self._init_packing(specs, device)
         self._work = None
         self._rstream = None
 
@@ -110,40 +149,16 @@ class HipTrunk(object):
         s = self.specs[l]
         return self._gbufs[(s.coutp, self.halo[l])][which][:B]
 
-    # ------------------------------------------------------------------ weights
-    def sync_weights(self, weights, biases, version):
-        """Repack bf16 GEMM layouts from fp32 OIHW masters when ``version`` changed."""
-        if version == self._packed_version:
-            return
-        for l, s in enumerate(self.specs):
-            taps = s.ks * s.ks
-            if self._wf[l] is None:
-                self._wf[l] = torch.empty((taps, s.coutp, s.cinp), dtype=torch.bfloat16,
-                                          device=self.device)
-                self._wb[l] = torch.empty((taps, s.cinp, s.coutp), dtype=torch.bfloat16,
-                                          device=self.device)
-        # one launch repacks all layers (GEMM layouts + padded biases); the pointer table is
-        # rebuilt only when a parameter tensor moved
-        ws = [w.contiguous() for w in weights]
-        key = tuple(w.data_ptr() for w in ws) + \
-            tuple(0 if b is None else b.data_ptr() for b in biases)
-        if getattr(self, "_pack_key", None) != key:
-            rows, start = [], 0
-            for l, s in enumerate(self.specs):
-                b = biases[l]
-                rows.append([ws[l].data_ptr(), 0 if b is None else b.data_ptr(), s.cout, s.cin,
-                             s.ks, s.coutp, s.cinp, self._wf[l].data_ptr(),
-                             self._wb[l].data_ptr(), self._bias[l].data_ptr(), start])
-                start += s.ks * s.ks * s.coutp * s.cinp + s.coutp
-            self._pack_table = torch.tensor(rows, dtype=torch.int64).to(self.device)
-            self._pack_total = start
-            self._pack_key = key
-            self._pack_keep = ws  # keep contiguous copies alive while the table points at them
-        ops.pack_trunk(self._pack_table, self.L, self._pack_total)
-        self._packed_version = version
-
     # ------------------------------------------------------------------ compute
-    def forward(self, B):
+    @property
+    def top_relu(self):
+        return self.specs[-1].relu
+
+    def top_grad(self, B):
+        """Where the head writes dL/d(trunk output) (ReLU-masked if top_relu)."""
+        return self.grad_buffer(self.L - 1, 0, B)
+
+    def forward(self, B, training=False):
         S = self.S
         for l, s in enumerate(self.specs):
             x, y = self.acts[l][:B], self.acts[l + 1][:B]
@@ -191,6 +206,176 @@ class HipTrunk(object):
             main.wait_stream(rs)
 
 
+class BNSpec(object):
+    """One column BatchNormalization (Keras-1 axis=-1 on (B, C, H, W) tensors: S statistics)."""
+    __slots__ = ("eps", "momentum", "gamma", "beta", "rmean", "rvar", "dgamma", "dbeta")
+
+    def __init__(self, eps, momentum, params, grads):
+        self.eps, self.momentum = eps, momentum
+        self.gamma, self.beta, self.rmean, self.rvar = params
+        self.dgamma, self.dbeta = grads[0], grads[1]
+
+
+class ResTrunk(_PackedConvs):
+    """Residual trunk of ResnetPolicy (reference policy.py:196-244) on the HIP engine:
+
+        A_0 = conv0(x)                                       (linear, 5x5 by default)
+        unit u: X = A_u; n_skip x [U = ReLU(BN(X)); X = conv(U)]; A_{u+1} = A_u + X
+        H = ReLU(A_U)                                        (read by the policy head)
+
+    Forward: the column BN statistics (bn.hip) + one fused BN+ReLU pass per BN, the MFMA conv
+    with the residual sum in its epilogue (conv.hip ``res``). Backward, per conv: all-taps wgrad,
+    dgrad with the ReLU mask of its input U in the epilogue, then the BN backward (reduction +
+    one elementwise pass that also adds the skip gradient, in place when the halos agree).
+
+    Halos: A_u / X / H use halo 1. U_j (conv l = j+1's input) and every gradient consumed by
+    conv l use halo hin[l] = max(1, ks_l // 2), so wgrad always runs the all-taps kernel and the
+    dgrad input is wide enough (the reference's filter_width_1 also sets the FIRST unit's conv,
+    5x5 by default). Memory: (units + BNs + ~4) activations of B x (S+2)^2 x K bf16 (29 MB each
+    at B=256, K=128) — trivial against 288 GB of HBM."""
+
+    def __init__(self, specs, units, bns, board, device):
+        assert specs and len(specs) == 1 + sum(units) == 1 + len(bns)
+        self.specs, self.units, self.bns = specs, list(units), bns
+        self.S = board
+        self.device = device
+        self.L = len(specs)
+        K = specs[0].cout
+        for s in specs[1:]:
+            assert s.cin == K and s.cout == K, "residual trunk needs constant width"
+        self.K, self.KP = K, specs[0].coutp
+        self._B = 0
+        self._init_packing(specs, device)
+        self.hin = [max(1, s.ks // 2) for s in specs]
+        self.halo = [self.hin[0]]
+        # last conv of each unit, and the gradient halo each unit's output gradient needs
+        ends, j = [], 0
+        for n in self.units:
+            j += n
+            ends.append(j)
+        self._unit_last = ends
+        self._work = None
+
+    # ------------------------------------------------------------------ buffers
+    def ensure_batch(self, B):
+        if B <= self._B:
+            return
+        B = max(B, 1)
+        S, KP, dev = self.S, self.KP, self.device
+        alloc = ops.alloc_padded
+        self.xin = alloc(B, S, self.hin[0], self.specs[0].cinp, dev)
+        self.A = [alloc(B, S, 1, KP, dev) for _ in range(len(self.units) + 1)]
+        nb = len(self.bns)
+        self.U = [alloc(B, S, self.hin[j + 1], KP, dev) for j in range(nb)]
+        # inner conv outputs of units with n_skip > 1 (BN j's input when it is not A_u)
+        self.Xin = [None] * nb
+        inner_h = set()
+        j = 0
+        for n in self.units:
+            for i in range(1, n):
+                self.Xin[j + i] = alloc(B, S, 1, KP, dev)
+                inner_h.add(self.hin[j + i])
+            j += n
+        self.H = alloc(B, S, 1, KP, dev)
+        self.G = {h: alloc(B, S, h, KP, dev) for h in set(self.hin) | {1}}
+        self.gI = {h: alloc(B, S, h, KP, dev) for h in inner_h}
+        self.dU = alloc(B, S, 1, KP, dev)
+        self.stats = torch.zeros((nb, 2, S), dtype=torch.float32, device=dev)
+        self.coef = torch.zeros((nb, 3, S), dtype=torch.float32, device=dev)
+        self.bcoef = torch.zeros((3, S), dtype=torch.float32, device=dev)
+        need = max(ops._lib().rag_conv_wgrad_workspace(B, S, s.coutp, s.cinp, s.ks, None)
+                   for s in self.specs)
+        self._work = torch.empty(need + 1024, dtype=torch.float32, device=dev)
+        self._B = B
+
+    def input_buffer(self, B):
+        self.ensure_batch(B)
+        return self.xin[:B]
+
+    def output(self, B):
+        return self.H[:B]
+
+    top_relu = True
+
+    def top_grad(self, B):
+        return self.G[1][:B]
+
+    def _bn_input(self, j, u, B):
+        return self.A[u][:B] if self.Xin[j] is None else self.Xin[j][:B]
+
+    # ------------------------------------------------------------------ compute
+    def forward(self, B, training=False):
+        S, K = self.S, self.K
+        s0 = self.specs[0]
+        ops.conv_igemm(self.xin[:B], self._wf[0], self._bias[0], self.A[0][:B], B, S,
+                       self.hin[0], 1, s0.cinp, s0.coutp, s0.ks, False)
+        j = 0
+        for u, n in enumerate(self.units):
+            for i in range(n):
+                bn, x, U = self.bns[j], self._bn_input(j, u, B), self.U[j][:B]
+                if training:
+                    ops.bn_train_fwd(x, B, S, K, bn.gamma, bn.beta, bn.rmean, bn.rvar, bn.eps,
+                                     bn.momentum, self.stats[j], self.coef[j])
+                else:
+                    ops.bn_infer_coef(bn.gamma, bn.beta, bn.rmean, bn.rvar, bn.eps, S,
+                                      self.coef[j])
+                ops.bn_apply(x, U, B, S, K, coef=self.coef[j], relu=True)
+                l, sp = j + 1, self.specs[j + 1]
+                last = i == n - 1
+                y = self.A[u + 1][:B] if last else self.Xin[j + 1][:B]
+                ops.conv_igemm(U, self._wf[l], self._bias[l], y, B, S, self.hin[l], 1, sp.cinp,
+                               sp.coutp, sp.ks, False,
+                               residual=self.A[u][:B] if last else None)
+                j += 1
+        ops.bn_apply(self.A[-1][:B], self.H[:B], B, S, K, coef=None, relu=True)
+        return self.H[:B]
+
+    def backward(self, B, dws, dbs, top_which=0, accumulate=False, on_layer_done=None):
+        """Backprop from top_grad (dL/dA_U, already ReLU-masked by the head) to conv0; writes
+        conv grads into dws/dbs and BN grads into each BNSpec's dgamma/dbeta (batch-statistics
+        BN, i.e. the training learning phase). ``on_layer_done(l)`` fires after conv l's wgrad
+        (BN j's grads, which sit between conv j and conv j+1 in the flat buffer, are complete
+        by then)."""
+        S, K = self.S, self.K
+        cur, hcur = self.G[1][:B], 1  # dL/dA_{u+1}
+        for u in range(len(self.units) - 1, -1, -1):
+            n, jend = self.units[u], self._unit_last[u]
+            need = self.hin[jend]
+            if hcur != need:  # only the top unit (the head writes halo 1): re-pad once
+                ops.bn_apply(cur, self.G[need][:B], B, S, K, coef=None, relu=False)
+                cur, hcur = self.G[need][:B], need
+            gx = cur
+            for i in range(n - 1, -1, -1):
+                j = jend - n + i
+                l, sp, bn = j + 1, self.specs[j + 1], self.bns[j]
+                U, x = self.U[j][:B], self._bn_input(j, u, B)
+                ops.conv_wgrad(gx, U, dws[l], dbs[l], B, S, self.hin[l], sp.cout, sp.coutp,
+                               sp.cin, sp.cinp, sp.ks, accumulate=accumulate, work=self._work,
+                               hg=self.hin[l])
+                if on_layer_done is not None:
+                    on_layer_done(l)
+                dU = self.dU[:B]
+                ops.conv_igemm(gx, self._wb[l], None, dU, B, S, self.hin[l], 1, sp.coutp,
+                               sp.cinp, sp.ks, False, mask=U, mask_halo=self.hin[l])
+                ops.bn_bwd_coef(x, dU, B, S, K, bn.gamma, self.stats[j], bn.dgamma, bn.dbeta,
+                                self.bcoef)
+                if i > 0:  # gradient of the inner conv output Xin[j] = conv j's gx
+                    gx = self.gI[self.hin[j]][:B]
+                    ops.bn_apply(x, gx, B, S, K, coef=self.bcoef, relu=False, dy=dU)
+                else:      # dL/dA_u = BN'(dU) + skip gradient (in place when halos agree)
+                    hn = self.hin[self._unit_last[u - 1]] if u > 0 else self.hin[0]
+                    out = self.G[hn][:B]
+                    ops.bn_apply(x, out, B, S, K, coef=self.bcoef, relu=False, dy=dU,
+                                 residual=cur)
+                    cur, hcur = out, hn
+        s0 = self.specs[0]
+        ops.conv_wgrad(cur, self.xin[:B], dws[0], dbs[0], B, S, self.hin[0], s0.cout,
+                       s0.coutp, s0.cin, s0.cinp, s0.ks, accumulate=accumulate, work=self._work,
+                       hg=self.hin[0])
+        if on_layer_done is not None:
+            on_layer_done(0)
+
+
 class PolicyHeadEngine(object):
     """1x1 conv (K->1, scalar bias) -> Flatten -> per-position Bias -> softmax."""
 
@@ -223,10 +408,8 @@ class PolicyHeadEngine(object):
     def backward(self, B, w, dz, dw, db0, dpbias):
         """dz [B, S*S] -> head param grads + trunk top gradient (ReLU-masked) in grad buffer 0."""
         h = self.trunk.output(B)
-        L = self.trunk.L
-        dh = self.trunk.grad_buffer(L - 1, 0, B)
-        ops.head_bwd(h, w, dz, dh, dw, db0, dpbias, self.K,
-                     relu_mask=self.trunk.specs[-1].relu)
+        ops.head_bwd(h, w, dz, self.trunk.top_grad(B), dw, db0, dpbias, self.K,
+                     relu_mask=self.trunk.top_relu)
 
 
 class ValueHeadEngine(object):
@@ -251,7 +434,5 @@ class ValueHeadEngine(object):
 
     def backward_conv(self, B, w, dz, dw, db0):
         h = self.trunk.output(B)
-        L = self.trunk.L
-        dh = self.trunk.grad_buffer(L - 1, 0, B)
-        ops.head_bwd(h, w, dz.contiguous(), dh, dw, db0, None, self.K,
-                     relu_mask=self.trunk.specs[-1].relu)
+        ops.head_bwd(h, w, dz.contiguous(), self.trunk.top_grad(B), dw, db0, None, self.K,
+                     relu_mask=self.trunk.top_relu)

@@ -6,6 +6,9 @@
                Activation(softmax)                      (CNNPolicy, reference policy.py:96-136)
   ValuePlan:   [Conv2D 'same' (+ReLU)]* -> Conv2D 1x1 (1 filter) -> Flatten -> Dense(H) ->
                Dense(1, tanh)                          (CNNValue / reference value.py:14-28)
+  ResnetPlan:  (functional) Conv2D linear -> [n_skip x (BN -> ReLU -> Conv2D linear) + sum-merge]*
+               -> ReLU -> Conv2D 1x1 -> Flatten -> Bias -> softmax
+                                                       (ResnetPolicy, reference policy.py:196-244)
 
 and executes them on the HIP engine (models/engine.py): one packed-input kernel (uint8 or fp32
 planes, optional gather + dihedral transform), one MFMA conv launch per layer, the fused head
@@ -15,7 +18,7 @@ into the model's flat fp32 gradient buffer (ready for one all-reduce and the fus
 import torch
 
 from ..ops import hipops as ops
-from .engine import ConvSpec, HipTrunk, PolicyHeadEngine, ValueHeadEngine
+from .engine import BNSpec, ConvSpec, HipTrunk, PolicyHeadEngine, ResTrunk, ValueHeadEngine
 
 
 def _conv_ok(ld):
@@ -28,7 +31,7 @@ def _conv_ok(ld):
 
 def detect_plan(model):
     if model.functional:
-        return None
+        return _detect_resnet(model)
     L = model.layers
     n = 0
     while n < len(L) and L[n].class_name == "Convolution2D":
@@ -150,7 +153,7 @@ class PolicyPlan(_TrunkPlan):
 
     def fwd_bwd(self, B, labels, sw, mode, gscale, on_layer_grads=None):
         """Forward + fused loss + full backward into net.flat_grad (no host syncs)."""
-        self.trunk.forward(B)
+        self.trunk.forward(B, training=True)
         w, b0 = self.head_params()
         pb = self.net.params_of(self.bias_name)[0]
         self.head.forward(B, w, b0, pb, labels=labels, sweight=sw, mode=mode, gscale=gscale)
@@ -200,7 +203,7 @@ class ValuePlan(_TrunkPlan):
         return float(lossv), None
 
     def fwd_bwd(self, B, y, sw=None):
-        self.trunk.forward(B)
+        self.trunk.forward(B, training=True)
         w, b0 = self.head_params()
         z = self.head.conv_out(B, w, b0).detach().requires_grad_()
         params = [p.detach().requires_grad_() for p in self._dense_params()]
@@ -219,3 +222,79 @@ class ValuePlan(_TrunkPlan):
         dWs, dbs = self._grads()
         self.trunk.backward(B, dWs, dbs)
         return lossv.detach()
+
+
+def _detect_resnet(model):
+    """Match ResnetPolicy's functional graph (topologically ordered layer list)."""
+    L = model.layers
+    S = model.input_shape[-1] if model.input_shape else None
+    if not S or S > 25 or len(L) < 8 or L[0].class_name != "InputLayer":
+        return None
+
+    def conv(ld, src, ks=None):
+        return (_conv_ok(ld) and ld.inbound == [src] and
+                ld.config.get("activation", "linear") == "linear" and
+                (ks is None or ld.config["nb_row"] == ks))
+
+    def bn_ok(ld, src):
+        c = ld.config
+        return (ld.class_name == "BatchNormalization" and ld.inbound == [src] and
+                c.get("mode", 0) == 0 and c.get("axis", -1) in (-1, 3))
+
+    def act(ld, src, name):
+        return (ld.class_name == "Activation" and ld.inbound == [src] and
+                ld.config["activation"] == name)
+
+    if not conv(L[1], L[0].name):
+        return None
+    convs, bns, units = [L[1]], [], []
+    cur, i = L[1].name, 2
+    while i < len(L) and L[i].class_name == "BatchNormalization":
+        path, n = cur, 0
+        while i + 2 < len(L) and bn_ok(L[i], path) and act(L[i + 1], L[i].name, "relu") and \
+                conv(L[i + 2], L[i + 1].name) and L[i + 2].config["nb_row"] <= 7:
+            bns.append(L[i])
+            convs.append(L[i + 2])
+            path = L[i + 2].name
+            n += 1
+            i += 3
+        m = L[i] if i < len(L) else None
+        if n == 0 or m is None or m.class_name != "Merge" or \
+                m.config.get("mode", "sum") != "sum" or sorted(m.inbound) != sorted([cur, path]):
+            return None
+        units.append(n)
+        cur, i = m.name, i + 1
+    rest = L[i:]
+    if not units or len(rest) != 5 or not act(rest[0], cur, "relu") or \
+            not conv(rest[1], rest[0].name, 1) or rest[1].config["nb_filter"] != 1 or \
+            rest[2].class_name != "Flatten" or rest[3].class_name != "Bias" or \
+            not act(rest[4], rest[3].name, "softmax"):
+        return None
+    K = L[1].config["nb_filter"]
+    if any(c.config["nb_filter"] != K for c in convs):
+        return None
+    return ResnetPlan(model, convs, bns, units, rest[1], rest[3])
+
+
+class ResnetPlan(PolicyPlan):
+    """ResnetPolicy on the HIP engine: ResTrunk (column BN + ReLU kernels, residual conv
+    epilogue) + the same fused policy head / loss as PolicyPlan. Training steps use batch
+    statistics (and update the running averages); forward / evaluation use the running ones,
+    like Keras' learning phase."""
+
+    def __init__(self, model, convs, bns, units, head_conv, bias_layer):
+        net = model.net
+        self.model, self.net = model, net
+        specs = []
+        for ld in convs:
+            W = net.params_of(ld.name)[0]
+            specs.append(ConvSpec(ld.config["nb_row"], W.shape[1], W.shape[0], False))
+        bspecs = [BNSpec(ld.config.get("epsilon", 1e-3), ld.config.get("momentum", 0.99),
+                         net.params_of(ld.name), net.grads_of(ld.name)) for ld in bns]
+        self.S = model.input_shape[-1]
+        self.trunk = ResTrunk(specs, units, bspecs, self.S, net.device)
+        self.conv_names = [ld.name for ld in convs]
+        self.head_name = head_conv.name
+        self.K = specs[-1].cout
+        self.bias_name = bias_layer.name
+        self.head = PolicyHeadEngine(self.trunk, self.K)

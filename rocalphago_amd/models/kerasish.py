@@ -761,11 +761,16 @@ class Model(object):
 
     def _generic_train_step(self, x, y, sw):
         net = self.net
-        params = [v.detach().requires_grad_() for v in net._views]
+        # clones: BN running averages are updated in place during the forward, which must not
+        # bump the version counter of tensors autograd saved (they would share the flat storage)
+        params = [v.detach().clone().requires_grad_() for v in net._views]
         out = net.forward(x.float(), training=True, params=params)
         loss = _objective(self._loss_fn(), y, out, sw)
         grads = torch.autograd.grad(loss, params, allow_unused=True)
         with torch.no_grad():
+            for (_, wname, _), v, p in zip(net.weight_names, net._views, params):
+                if "_running_" in wname:
+                    v.copy_(p)
             for gv, g in zip(net._gviews, grads):
                 if g is None:
                     gv.zero_()

@@ -28,6 +28,17 @@ class NeuralNetBase(object):
         model = self.model
         return lambda inpt: model.predict(inpt)
 
+    def forward_device(self, x):
+        """Device-resident batch -> device-resident output (no host round trip; used by the GPU
+        players and self-play). Learning phase = test, as ``forward``."""
+        import torch
+        model = self.model
+        plan = model._plan_for()
+        with torch.no_grad():
+            if plan is not None:
+                return plan.forward(x)
+            return model.net.forward(x.float(), training=False)
+
     @staticmethod
     def load_model(json_file, device=None):
         with open(json_file, 'r') as f:

@@ -9,7 +9,7 @@ SZ = C.c_size_t
 
 SIGNATURES = {
     # conv.hip
-    "rag_conv_igemm": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P],
+    "rag_conv_igemm": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P],
     "rag_conv_wgrad_workspace": [I, I, I, I, I, P],
     "rag_conv_wgrad": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, P],
     "rag_pack_weights": [P, P, P, I, I, I, I, I, P],
@@ -28,6 +28,14 @@ SIGNATURES = {
     "rag_sgd": [P, P, P, I64, F, F, F, I, P],
     # rollout.hip
     "rag_rollouts": [P, P, I, I, I, F, I, P, P, C.c_uint, P, P, P, P],
+    # bn.hip
+    "rag_bn_workspace": [I, I],
+    "rag_bn_train_fwd": [P, I, I, I, I, I, P, P, P, P, F, F, P, P, P, P],
+    "rag_bn_infer_coef": [P, P, P, P, F, I, P, P],
+    "rag_bn_bwd_coef": [P, I, P, I, I, I, I, I, P, P, P, P, P, P, P],
+    "rag_bn_apply": [P, I, P, I, P, I, P, I, P, I, I, I, I, I, P],
+    # sample.hip
+    "rag_sample_moves": [P, P, I, P, I, I, F, C.c_uint64, P, P],
     # features.hip
     "rag_features": [P, P, P, P, P, I, I, P, I, I, P, P],
 }

@@ -28,6 +28,7 @@ class GpuFeatures(object):
         self.fids_dev = torch.tensor(self.fids, dtype=torch.int32, device=self.device)
         self.ladders = any(f in _LADDERS for f in self.fids)
         self.nthreads = nthreads
+        self._sens_fid = None
 
     @staticmethod
     def supports(size):
@@ -39,7 +40,9 @@ class GpuFeatures(object):
         return torch.from_numpy(np.ascontiguousarray(a)).pin_memory().to(self.device,
                                                                           non_blocking=True)
 
-    def __call__(self, boards, out=None):
+    def __call__(self, boards, out=None, sens_out=None):
+        """Planes [n, F, S, S] on the device; with ``sens_out`` (uint8 [n, S*S] or [n, 1, S, S])
+        also the sensibleness mask (legal, not an own true eye) from the same native inputs."""
         n = len(boards)
         S = boards[0].size
         colors, ages, meta, illegal, lad = _rg.gpu_feature_inputs(boards, self.ladders,
@@ -50,4 +53,13 @@ class GpuFeatures(object):
         _check(_lib().rag_features(_ptr(c), _ptr(a), _ptr(m), _ptr(il), _ptr(ld), n, S,
                                    _ptr(self.fids_dev), len(self.fids), self.F, _ptr(out),
                                    _stream()), "features")
+        if sens_out is not None:
+            if sens_out.numel() != n * S * S or sens_out.dtype != torch.uint8:
+                raise ValueError("sens_out must be uint8 with n*S*S elements")
+            if self._sens_fid is None:
+                self._sens_fid = torch.tensor([_FID["sensibleness"]], dtype=torch.int32,
+                                              device=self.device)
+            _check(_lib().rag_features(_ptr(c), _ptr(a), _ptr(m), _ptr(il), None, n, S,
+                                       _ptr(self._sens_fid), 1, 1, _ptr(sens_out), _stream()),
+                   "features(sensibleness)")
         return out

@@ -59,16 +59,70 @@ def pack_trunk(table, nlayers, total):
 
 
 def conv_igemm(x, wpack, bias, y, B, S, hi, ho, cinp, coutp, ks, relu, mask=None,
-               mask_halo=None):
-    """y[pad ho] = act(conv_ks(x[pad hi]) + bias), or the dgrad form with a ReLU mask (the layer
-    input: y's channel count, its own halo ``mask_halo``, default ho)."""
+               mask_halo=None, residual=None):
+    """y[pad ho] = act(conv_ks(x[pad hi]) + bias [+ residual]), or the dgrad form with a ReLU
+    mask (the layer input: y's channel count, its own halo ``mask_halo``, default ho).
+    ``residual`` (ResNet sum-merge) has y's layout and may be y itself."""
     hm = ho if mask_halo is None else mask_halo
     if mask is not None and (mask.shape[1] != S + 2 * hm or mask.shape[-1] != y.shape[-1]):
         raise ValueError("mask layout does not match (halo %d, %d channels)" % (hm, y.shape[-1]))
-    _check(_lib().rag_conv_igemm(_ptr(x), _ptr(wpack), _ptr(bias), _ptr(y), _ptr(mask), B, S, hi,
-                                 ho, cinp, coutp, y.shape[-1], ks, int(relu), hm, _stream()),
-           "conv_igemm")
+    if residual is not None and residual.shape[1:] != y.shape[1:]:
+        raise ValueError("residual layout does not match the output")
+    _check(_lib().rag_conv_igemm(_ptr(x), _ptr(wpack), _ptr(bias), _ptr(y), _ptr(mask),
+                                 _ptr(residual), B, S, hi, ho, cinp, coutp, y.shape[-1], ks,
+                                 int(relu), hm, _stream()), "conv_igemm")
     return y
+
+
+# ---- column BatchNorm (bn.hip; ResnetPolicy). Activations use the padded layout above; every
+# per-column vector (gamma, beta, running mean / var, stats [2, S], coef [3, S]) is fp32.
+
+def _halo(t, S):
+    return (t.shape[1] - S) // 2
+
+
+def bn_workspace(B, S, device):
+    n = _lib().rag_bn_workspace(B, S)
+    key = ("bn", device)
+    buf = _ws_cache.get(key)
+    if buf is None or buf.numel() < n:
+        buf = torch.empty(n + 256, dtype=torch.float32, device=device)
+        _ws_cache[key] = buf
+    return buf
+
+
+def bn_train_fwd(x, B, S, C, gamma, beta, rmean, rvar, eps, momentum, stats, coef):
+    """Batch statistics of x [pad] per column -> stats (mean, rstd), coef (affine), running
+    averages updated in place (skipped when rmean is None)."""
+    _check(_lib().rag_bn_train_fwd(_ptr(x), _halo(x, S), B, S, C, x.shape[-1], _ptr(gamma),
+                                   _ptr(beta), _ptr(rmean), _ptr(rvar), float(eps),
+                                   float(momentum), _ptr(stats), _ptr(coef),
+                                   _ptr(bn_workspace(B, S, x.device)), _stream()), "bn_train_fwd")
+
+
+def bn_infer_coef(gamma, beta, rmean, rvar, eps, S, coef):
+    _check(_lib().rag_bn_infer_coef(_ptr(gamma), _ptr(beta), _ptr(rmean), _ptr(rvar),
+                                    float(eps), S, _ptr(coef), _stream()), "bn_infer_coef")
+
+
+def bn_bwd_coef(x, dy, B, S, C, gamma, stats, dgamma, dbeta, coef):
+    _check(_lib().rag_bn_bwd_coef(_ptr(x), _halo(x, S), _ptr(dy), _halo(dy, S), B, S, C,
+                                  x.shape[-1], _ptr(gamma), _ptr(stats), _ptr(dgamma),
+                                  _ptr(dbeta), _ptr(coef), _ptr(bn_workspace(B, S, x.device)),
+                                  _stream()), "bn_bwd_coef")
+
+
+def bn_apply(x, out, B, S, C, coef=None, relu=True, dy=None, residual=None):
+    """out = act(coef[0]*x + coef[1]*dy + coef[2] + residual) (interior; padded channels 0)."""
+    CP = x.shape[-1]
+    for t in (out, dy, residual):
+        if t is not None and t.shape[-1] != CP:
+            raise ValueError("bn_apply channel mismatch")
+    _check(_lib().rag_bn_apply(_ptr(x), _halo(x, S), _ptr(dy), 0 if dy is None else _halo(dy, S),
+                               _ptr(residual), 0 if residual is None else _halo(residual, S),
+                               _ptr(out), _halo(out, S), _ptr(coef), int(relu), B, S, C, CP,
+                               _stream()), "bn_apply")
+    return out
 
 
 _ws_cache = {}
@@ -174,6 +228,24 @@ def head_linear(h, w, b0, z, K):
     S = WP - 2
     _check(_lib().rag_head_linear(_ptr(h), _ptr(w), _ptr(b0), _ptr(z), B, S, KP, K, _stream()),
            "head_linear")
+
+
+def sample_moves(probs, mask, beta=1.0, greedy=None, seed=0, out=None):
+    """Per row: a move drawn from probs^beta restricted to ``mask`` (uint8 [B, >=P]), or the
+    masked argmax where ``greedy`` (uint8 [B]) is set; -1 for rows without candidates
+    (sample.hip, Gumbel-max). Returns int32 [B] on the device."""
+    B, P = probs.shape
+    probs = probs.contiguous().float()
+    mask = mask.reshape(B, -1)
+    if mask.dtype != torch.uint8:
+        mask = mask.to(torch.uint8)
+    mask = mask.contiguous()
+    if out is None:
+        out = torch.empty(B, dtype=torch.int32, device=probs.device)
+    _check(_lib().rag_sample_moves(_ptr(probs), _ptr(mask), mask.shape[1], _ptr(greedy), B, P,
+                                   float(beta), int(seed) & ((1 << 64) - 1), _ptr(out),
+                                   _stream()), "sample_moves")
+    return out
 
 
 def sgd_(p, g, lr, momentum=0.0, v=None, wd=0.0, nesterov=False):

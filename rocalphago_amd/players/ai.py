@@ -5,6 +5,12 @@ pass when none remain, when the move limit is exceeded, or when a pass is offere
 temperature applied in log space with beta = 1/T). ``get_moves`` evaluates all states in one
 batched network call (features by native threads, forward on the HIP engine).
 
+On a GPU, ``get_moves`` keeps the whole selection on the device (K12): feature planes and the
+sensibleness mask from the feature kernel (features.hip), the forward on the fused HIP plan, and
+one Gumbel-max sampling kernel over the masked, temperature-adjusted distribution (sample.hip) —
+only the chosen points come back to the host. Same distribution as the host path (p^beta over the
+sensible moves); the random stream differs, seeded from the player's ``rng``.
+
 Fixed quirk Q6: ``move_limit=None`` means "no limit" in the batched path too.
 """
 from operator import itemgetter
@@ -19,8 +25,40 @@ def _over_limit(state, move_limit):
     return move_limit is not None and len(state.history) > move_limit
 
 
+def _device_moves(policy, states, beta, greedy_rows, rng):
+    """Batched move choice on the GPU, or None when the policy is not a HIP model (CPU model,
+    duck-typed test policy, unsupported board size)."""
+    model = getattr(policy, "model", None)
+    if model is None or not hasattr(policy, "forward_device") or \
+            getattr(model, "device", None) is None or model.device.type != "cuda":
+        return None
+    import torch
+    from ..ops import hipops as ops
+    from ..ops.features import GpuFeatures
+    S = states[0].size
+    if any(st.size != S for st in states) or not GpuFeatures.supports(S):
+        return None
+    gf = getattr(policy, "_rag_gpu_features", None)
+    if gf is None or gf.device != model.device:
+        gf = GpuFeatures(policy.preprocessor.feature_list, model.device)
+        policy._rag_gpu_features = gf
+    n = len(states)
+    sens = torch.empty((n, S * S), dtype=torch.uint8, device=model.device)
+    x = gf([st.native for st in states], sens_out=sens)
+    probs = policy.forward_device(x)
+    greedy = None
+    if any(greedy_rows):
+        greedy = torch.tensor([1 if g else 0 for g in greedy_rows],
+                              dtype=torch.uint8).to(model.device)
+    seed = (int(rng.randint(0, 2 ** 31 - 1)) << 31) | int(rng.randint(0, 2 ** 31 - 1))
+    mv = ops.sample_moves(probs, sens, beta, greedy, seed).cpu().numpy()
+    return [go.PASS_MOVE if m < 0 else (int(m) // S, int(m) % S) for m in mv]
+
+
 class GreedyPolicyPlayer(object):
     """Plays the highest-probability sensible move."""
+
+    device_select = True  # get_moves on the GPU when the policy is a HIP model
 
     def __init__(self, policy_function, pass_when_offered=False, move_limit=None):
         self.policy = policy_function
@@ -40,6 +78,13 @@ class GreedyPolicyPlayer(object):
         return go.PASS_MOVE
 
     def get_moves(self, states):
+        if len(states) == 0:
+            return []
+        dev = _device_moves(self.policy, states, 1.0, [True] * len(states), np.random) \
+            if self.device_select else None
+        if dev is not None:
+            return [go.PASS_MOVE if _over_limit(st, self.move_limit) else m
+                    for st, m in zip(states, dev)]
         sensible = [st.get_legal_moves(include_eyes=False) for st in states]
         dists = self.policy.batch_eval_state(states, sensible)
         out = []
@@ -53,6 +98,8 @@ class GreedyPolicyPlayer(object):
 
 class ProbabilisticPolicyPlayer(object):
     """Samples a sensible move from the (temperature-adjusted) policy distribution."""
+
+    device_select = True
 
     def __init__(self, policy_function, temperature=1.0, pass_when_offered=False,
                  move_limit=None, greedy_start=None, rng=None):
@@ -93,6 +140,15 @@ class ProbabilisticPolicyPlayer(object):
 
     def get_moves(self, states):
         """Batched get_move: one network evaluation for all states."""
+        if len(states) == 0:
+            return []
+        greedy = [self.greedy_start is not None and len(st.history) >= self.greedy_start
+                  for st in states]
+        dev = _device_moves(self.policy, states, self.beta, greedy, self.rng) \
+            if self.device_select else None
+        if dev is not None:
+            return [go.PASS_MOVE if _over_limit(st, self.move_limit) else m
+                    for st, m in zip(states, dev)]
         sensible_move_lists = [st.get_legal_moves(include_eyes=False) for st in states]
         all_moves_distributions = self.policy.batch_eval_state(states, sensible_move_lists)
         move_list = [None] * len(states)

@@ -157,3 +157,23 @@ def test_resnet_batchnorm_learning_phase():
     assert r.model.uses_learning_phase
     out1 = r.forward(r.preprocessor.state_to_tensor(GameState()))
     assert np.isfinite(out1).all() and abs(out1.sum() - 1) < 1e-4
+
+
+def test_resnet_generic_training_updates_running_stats():
+    """Training-phase BN (batch statistics) through the generic executor: the running averages
+    move with momentum and the loss decreases (regression: in-place running-stat updates used
+    to invalidate tensors autograd saved)."""
+    r = small(ResnetPolicy, layers=3)
+    m = r.model
+    m.compile(loss="categorical_crossentropy", optimizer=K.SGD(lr=0.05))
+    S = m.input_shape[-1]
+    X = (np.random.RandomState(0).rand(8, m.input_shape[1], S, S) > 0.5).astype(np.uint8)
+    Y = np.eye(S * S, dtype=np.float32)[:8]
+    names = [w for (_, w, _) in m.net.weight_names]
+    i = names.index([n for n in names if n.endswith("_running_mean")][0])
+    before = m.get_weights()[i].copy()
+    l0 = m.train_on_batch(X, Y)
+    for _ in range(5):
+        l1 = m.train_on_batch(X, Y)
+    assert l1 < l0
+    assert np.abs(m.get_weights()[i] - before).max() > 0

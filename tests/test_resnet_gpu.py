@@ -1,0 +1,183 @@
+"""ResnetPolicy on the HIP engine (bn.hip column BatchNorm, residual conv epilogue, ResnetPlan)
+against plain PyTorch fp32 references: the kernels one by one, then the whole fused plan against
+the generic executor (reference policy.py:141-271; Keras-1 BN axis=-1 on 'th' tensors)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ops():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from rocalphago_amd.ops import hipops
+    return hipops
+
+
+def col_bn_ref(x, gamma, beta, eps):
+    """Keras-1 BN over axis=-1 of (B, C, H, W): one statistic per column w."""
+    mean = x.mean(dim=(0, 1, 2))
+    var = x.var(dim=(0, 1, 2), unbiased=False)
+    return (x - mean) / torch.sqrt(var + eps) * gamma + beta, mean, var
+
+
+def bfr(t):
+    return t.to(torch.bfloat16).float()
+
+
+@pytest.mark.parametrize("B,C,S", [(5, 40, 9), (3, 128, 19), (2, 192, 13)])
+def test_bn_forward_backward(ops, B, C, S):
+    dev = "cuda"
+    torch.manual_seed(0)
+    CP = ops.pad_channels(C)
+    x = bfr(torch.randn(B, C, S, S, device=dev) * 2 + 0.5)
+    gamma = torch.rand(S, device=dev) + 0.5
+    beta = torch.randn(S, device=dev) * 0.2
+    rmean, rvar = torch.zeros(S, device=dev), torch.ones(S, device=dev)
+    eps, mom = 1e-3, 0.99
+    xp = ops.pack_nchw(x, 1, CP)
+    stats = torch.zeros(2, S, device=dev)
+    coef = torch.zeros(3, S, device=dev)
+    ops.bn_train_fwd(xp, B, S, C, gamma, beta, rmean, rvar, eps, mom, stats, coef)
+    U = ops.alloc_padded(B, S, 1, CP, dev)
+    ops.bn_apply(xp, U, B, S, C, coef=coef, relu=True)
+    y_ref, mean, var = col_bn_ref(x, gamma, beta, eps)
+    got = ops.unpack(U, C, 1)
+    assert torch.allclose(got, F.relu(y_ref), atol=3e-2, rtol=1e-2)
+    assert torch.allclose(stats[0], mean, atol=1e-4)
+    assert torch.allclose(rmean, (1 - mom) * mean, atol=1e-5)
+    assert torch.allclose(rvar, mom + (1 - mom) * var, atol=1e-4)
+    # padded channels stay zero
+    if C < CP:
+        assert U[..., C:].abs().max().item() == 0
+    # backward: dx = BN'(dy) + residual
+    xr = x.clone().requires_grad_()
+    yr, _, _ = col_bn_ref(xr, gamma, beta, eps)
+    dy = bfr(torch.randn_like(x))
+    res = bfr(torch.randn_like(x))
+    yr.backward(dy)
+    dgamma, dbeta = torch.zeros(S, device=dev), torch.zeros(S, device=dev)
+    bcoef = torch.zeros(3, S, device=dev)
+    dyp = ops.pack_nchw(dy, 1, CP)
+    ops.bn_bwd_coef(xp, dyp, B, S, C, gamma, stats, dgamma, dbeta, bcoef)
+    out = ops.alloc_padded(B, S, 2, CP, dev)  # other output halo (the conv0 gradient case)
+    ops.bn_apply(xp, out, B, S, C, coef=bcoef, relu=False, dy=dyp,
+                 residual=ops.pack_nchw(res, 1, CP))
+    g_ref = xr.grad + res
+    got = ops.unpack(out, C, 2)
+    scale = g_ref.abs().max().item()
+    assert (got - g_ref).abs().max().item() < 2e-2 * scale
+    xn = (x - mean) / torch.sqrt(var + eps)
+    assert torch.allclose(dbeta, dy.sum(dim=(0, 1, 2)), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(dgamma, (dy * xn).sum(dim=(0, 1, 2)), rtol=1e-3, atol=1e-2)
+    # inference coefficients from running statistics
+    ops.bn_infer_coef(gamma, beta, rmean, rvar, eps, S, coef)
+    ops.bn_apply(xp, U, B, S, C, coef=coef, relu=True)
+    inf_ref = F.relu((x - rmean) / torch.sqrt(rvar + eps) * gamma + beta)
+    assert torch.allclose(ops.unpack(U, C, 1), inf_ref, atol=3e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("C,ks", [(64, 3), (192, 3), (32, 3), (128, 1)])
+def test_conv_residual_epilogue(ops, C, ks):
+    dev = "cuda"
+    torch.manual_seed(1)
+    B, S = 4, 19
+    CP = ops.pad_channels(C)
+    x = bfr(torch.randn(B, C, S, S, device=dev))
+    w = torch.randn(C, C, ks, ks, device=dev) * 0.05
+    b = torch.randn(C, device=dev) * 0.1
+    r = bfr(torch.randn(B, C, S, S, device=dev))
+    wf, _ = ops.pack_weights(w, CP, CP)
+    bias = torch.zeros(CP, device=dev)
+    bias[:C] = b
+    xp = ops.pack_nchw(x, 1, CP)
+    rp = ops.pack_nchw(r, 1, CP)
+    y = ops.alloc_padded(B, S, 1, CP, dev)
+    ops.conv_igemm(xp, wf, bias, y, B, S, 1, 1, CP, CP, ks, False, residual=rp)
+    ref = F.conv2d(x, bfr(w), b, padding=ks // 2) + r
+    got = ops.unpack(y, C, 1)
+    assert (got - ref).abs().max().item() < 3e-2 * ref.abs().max().item()
+    # in place: y = conv(x) + y
+    ops.conv_igemm(xp, wf, bias, rp, B, S, 1, 1, CP, CP, ks, False, residual=rp)
+    assert (ops.unpack(rp, C, 1) - ref).abs().max().item() < 3e-2 * ref.abs().max().item()
+
+
+def _pair(K, layers, board, n_skip, seed=3):
+    from rocalphago_amd.features.preprocessing import DEFAULT_FEATURES
+    from rocalphago_amd.models.policy import ResnetPolicy
+    kw = dict(board=board, filters_per_layer=K, layers=layers, seed=seed)
+    kw.update(n_skip)
+    cpu = ResnetPolicy(DEFAULT_FEATURES, device="cpu", **kw)
+    gpu = ResnetPolicy(DEFAULT_FEATURES, device="cuda", **kw)
+    rng = np.random.RandomState(seed)
+    ws = []
+    for (lname, wname, shape), v in zip(cpu.model.net.weight_names, cpu.model.get_weights()):
+        if "running_std" in wname:
+            v = (rng.rand(*shape) * 2 + 0.5).astype(np.float32)
+        elif "running_mean" in wname or "beta" in wname:
+            v = (rng.randn(*shape) * 0.1).astype(np.float32)
+        elif "gamma" in wname:
+            v = (rng.rand(*shape) + 0.5).astype(np.float32)
+        elif "param_0" in wname:
+            v = (rng.randn(*shape) * 0.1).astype(np.float32)
+        ws.append(v)
+    cpu.model.set_weights(ws)
+    gpu.model.set_weights(ws)
+    return cpu, gpu
+
+
+def _planes(n, board, seed=0):
+    rng = np.random.RandomState(seed)
+    return (rng.rand(n, 48, board, board) > 0.6).astype(np.uint8)
+
+
+@pytest.mark.parametrize("K,layers,board,n_skip", [(64, 5, 19, {}), (32, 4, 9, {"n_skip_1": 2}),
+                                                   (128, 7, 19, {"n_skip_3": 3})])
+def test_resnet_plan_forward_matches_generic(ops, K, layers, board, n_skip):
+    from rocalphago_amd.models.fused import ResnetPlan
+    cpu, gpu = _pair(K, layers, board, n_skip)
+    plan = gpu.model._plan_for()
+    assert isinstance(plan, ResnetPlan)
+    X = _planes(6, board)
+    ref = cpu.model.predict(X)
+    got = gpu.model.predict(X)
+    lr, lg = np.log(ref + 1e-12), np.log(got + 1e-12)
+    # bf16 activations through every layer: compare log-probabilities of the likely moves
+    sel = ref > 1e-3
+    assert np.abs(lr - lg)[sel].max() < 0.15
+    assert np.abs(ref - got).max() < 2e-2
+
+
+@pytest.mark.parametrize("K,layers,board,n_skip", [(64, 5, 19, {}), (32, 4, 9, {"n_skip_1": 2})])
+def test_resnet_plan_train_step_matches_generic(ops, K, layers, board, n_skip):
+    from rocalphago_amd.models import kerasish as KZ
+    cpu, gpu = _pair(K, layers, board, n_skip)
+    B = 16
+    X = _planes(B, board, 1)
+    lab = np.random.RandomState(2).randint(0, board * board, B)
+    Y = np.zeros((B, board * board), np.float32)
+    Y[np.arange(B), lab] = 1
+    for m in (cpu.model, gpu.model):
+        m.compile(loss="categorical_crossentropy", optimizer=KZ.SGD(lr=0.0))
+    r_cpu = cpu.model.train_on_batch(X, Y)
+    r_gpu = gpu.model.train_on_batch(X, Y)
+    assert abs(r_cpu - r_gpu) < 0.05 * abs(r_cpu)
+    net_c, net_g = cpu.model.net, gpu.model.net
+    for (lname, wname, shape), gc, gg, pc, pg in zip(net_c.weight_names, net_c._gviews,
+                                                     net_g._gviews, net_c._views, net_g._views):
+        gc, gg = gc.detach().reshape(-1), gg.detach().cpu().reshape(-1)
+        if "running" in wname:
+            # running statistics: updated from the batch statistics, no gradient
+            assert torch.allclose(pc.detach().cpu(), pg.detach().cpu(), rtol=1e-2, atol=2e-3), \
+                wname
+            continue
+        nc = gc.norm().item()
+        if nc < 1e-6:
+            assert gg.norm().item() < 1e-3, wname
+            continue
+        cos = torch.dot(gc, gg).item() / (nc * gg.norm().item() + 1e-12)
+        assert cos > 0.98, (wname, cos)
+        assert abs(gg.norm().item() / nc - 1) < 0.08, (wname, gg.norm().item(), nc)
