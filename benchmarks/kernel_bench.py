@@ -37,7 +37,7 @@ def main():
     dev = torch.device("cuda")
     B, S = args.batch, 19
     res = []
-    for (cin, cout, ks) in [(192, 192, 3), (48, 192, 5)]:
+    for (cin, cout, ks) in [(192, 192, 3), (48, 192, 5), (128, 128, 3)]:
         cinp, coutp = ops.pad_channels(cin), ops.pad_channels(cout)
         hi = ks // 2
         flops = 2.0 * B * S * S * cin * cout * ks * ks

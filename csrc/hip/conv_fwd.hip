@@ -25,9 +25,8 @@ constexpr int kBK = 32;
 constexpr int kNBUF = 3;
 // fragment double-buffering (see the K loop): needs ~48 more VGPRs and spills at 2 blocks/CU
 // with the 192x192 tile, so it is off
-constexpr bool kFragPrefetch = false;
 
-template <int KS, int NT, int MT>
+template <int KS, int NT, int MT, bool kFragPrefetch>
 __global__ void __launch_bounds__(256, 2)
 conv_pipe_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                  const float* __restrict__ bias, bf16* __restrict__ Y,
@@ -254,17 +253,19 @@ conv_pipe_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
 }
 
 template <int KS>
-bool launch_ks(int nt, int mt, dim3 grid, hipStream_t st, const bf16* X, const bf16* W,
+bool launch_ks(int nt, int mt, bool pf, dim3 grid, hipStream_t st, const bf16* X, const bf16* W,
                const float* bias, bf16* Y, const bf16* mask, const bf16* res, int M, int S,
                int WI, int shift, int WO, int HO, int CIN, int WROWS, int YC, int relu, int HM) {
-#define RAG_PIPE(N, T)                                                                        \
-  if (nt == N && mt == T) {                                                                   \
-    conv_pipe_kernel<KS, N, T><<<grid, 256, 0, st>>>(X, W, bias, Y, mask, res, M, S, WI, shift, \
-                                                     WO, HO, CIN, WROWS, YC, relu, HM);       \
+#define RAG_PIPE(N, T, PF)                                                                    \
+  if (nt == N && mt == T && pf == PF) {                                                       \
+    conv_pipe_kernel<KS, N, T, PF><<<grid, 256, 0, st>>>(X, W, bias, Y, mask, res, M, S, WI,    \
+                                                         shift, WO, HO, CIN, WROWS, YC, relu,  \
+                                                         HM);                                  \
     return true;                                                                              \
   }
-  RAG_PIPE(2, 4) RAG_PIPE(2, 6) RAG_PIPE(2, 8) RAG_PIPE(4, 4) RAG_PIPE(4, 6) RAG_PIPE(4, 8)
-  RAG_PIPE(6, 4) RAG_PIPE(6, 6)
+  RAG_PIPE(2, 4, false) RAG_PIPE(2, 6, false) RAG_PIPE(2, 8, false) RAG_PIPE(4, 4, false)
+  RAG_PIPE(4, 6, false) RAG_PIPE(4, 8, false) RAG_PIPE(6, 4, false) RAG_PIPE(6, 6, false)
+  RAG_PIPE(6, 4, true) RAG_PIPE(4, 4, true) RAG_PIPE(4, 6, true)
 #undef RAG_PIPE
   return false;
 }
@@ -305,14 +306,18 @@ bool rag_conv_pipe_launch(const bf16* x, const bf16* w, const float* bias, bf16*
     return e ? atoi(e) : 0;
   }();
   const int mt = force_mt ? force_mt : pick_mt(M, nt, ntn);
+  static const bool pf = [] {  // experimental: fragment double-buffering (RAG_CONV_PF=1)
+    const char* e = getenv("RAG_CONV_PF");
+    return e && e[0] == '1';
+  }();
   const int bm = 32 * mt;
   const int nblk_m = (M + bm - 1) / bm;
   dim3 grid(nblk_m * ntn);
   switch (KS) {
-    case 1: return launch_ks<1>(nt, mt, grid, stream, x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM);
-    case 3: return launch_ks<3>(nt, mt, grid, stream, x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM);
-    case 5: return launch_ks<5>(nt, mt, grid, stream, x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM);
-    case 7: return launch_ks<7>(nt, mt, grid, stream, x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM);
+    case 1: return launch_ks<1>(nt, mt, pf, grid, stream, x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM);
+    case 3: return launch_ks<3>(nt, mt, pf, grid, stream, x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM);
+    case 5: return launch_ks<5>(nt, mt, pf, grid, stream, x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM);
+    case 7: return launch_ks<7>(nt, mt, pf, grid, stream, x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM);
     default: return false;
   }
 }
