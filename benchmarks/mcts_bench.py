@@ -17,7 +17,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def build_search(device, filters=192, layers=12, batch=256, rollout_device="gpu",
-                 rollouts_per_leaf=4, lmbda=0.5, nthreads=16, seed=1):
+                 rollouts_per_leaf=1, lmbda=0.5, nthreads=16, seed=1, pipeline=2,
+                 max_inflight=4):
     from rocalphago_amd.features.preprocessing import DEFAULT_FEATURES
     from rocalphago_amd.models.policy import CNNPolicy
     from rocalphago_amd.models.value import CNNValue
@@ -27,7 +28,8 @@ def build_search(device, filters=192, layers=12, batch=256, rollout_device="gpu"
     val = CNNValue(DEFAULT_FEATURES + ["color"], board=19, filters_per_layer=filters,
                    layers=layers, device=device, seed=seed + 1)
     return ParallelMCTS(pol, val, lmbda=lmbda, batch=batch, rollout_device=rollout_device,
-                        rollouts_per_leaf=rollouts_per_leaf, nthreads=nthreads, seed=seed)
+                        rollouts_per_leaf=rollouts_per_leaf, nthreads=nthreads, seed=seed,
+                        pipeline=pipeline, max_inflight=max_inflight)
 
 
 def measure(device, playouts=8192, warmup=512, moves=1, **kw):
@@ -54,7 +56,7 @@ def measure(device, playouts=8192, warmup=512, moves=1, **kw):
     if mc.lmbda > 0:
         out["rollouts_per_s"] = s["sims"] * (mc.rollouts_per_leaf if mc.rollout_device == "gpu"
                                              else 1) / dt
-    for k in ("t_select", "t_eval", "t_rollout_wait", "t_backup"):
+    for k in ("t_select", "t_submit", "t_eval", "t_rollout_wait", "t_backup"):
         out[k + "_frac"] = round(s.get(k, 0.0) / dt, 3)
     return out
 
@@ -68,16 +70,22 @@ def main():
     ap.add_argument("--playouts", type=int, default=8192)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--rollout-device", default="gpu", choices=["gpu", "cpu"])
-    ap.add_argument("--rollouts-per-leaf", type=int, default=4)
+    ap.add_argument("--rollouts-per-leaf", type=int, default=1,
+                    help="playouts per leaf (1 = AlphaGo's APV-MCTS: one rollout per simulation)")
     ap.add_argument("--lmbda", type=float, default=0.5)
     ap.add_argument("--filters", type=int, default=192)
     ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--pipeline", type=int, default=2, help="waves in flight (1 = serial)")
+    ap.add_argument("--max-inflight", type=int, default=4, help="rollout waves in flight")
+    ap.add_argument("--moves", type=int, default=1)
     args = ap.parse_args()
     import torch
     dev = torch.device("cuda")
-    r = measure(dev, playouts=args.playouts, batch=args.batch,
+    r = measure(dev, playouts=args.playouts, batch=args.batch, moves=args.moves,
                 rollout_device=args.rollout_device, rollouts_per_leaf=args.rollouts_per_leaf,
-                lmbda=args.lmbda, filters=args.filters, nthreads=args.threads)
+                lmbda=args.lmbda, filters=args.filters, nthreads=args.threads,
+                pipeline=args.pipeline, max_inflight=args.max_inflight)
+    r["pipeline"] = args.pipeline
     r.update({"metric": "MCTS simulations/s (19x19 APV-MCTS, policy+value on GPU)",
               "model": "policy 48x192x13 + value 49x192x13+FC256", "lmbda": args.lmbda})
     print(json.dumps({k: (round(v, 2) if isinstance(v, float) else v) for k, v in r.items()}))

@@ -23,6 +23,7 @@
 #pragma once
 
 #include <algorithm>
+#include <cstring>
 #include <atomic>
 #include <cmath>
 #include <condition_variable>
@@ -34,6 +35,8 @@
 #include <thread>
 #include <tuple>
 #include <vector>
+
+#include <sys/mman.h>
 
 #include "../engine/go_engine.hpp"
 #include "rollout.hpp"
@@ -56,6 +59,56 @@ struct Node {
   float w;         // value-net sum, for the player who played `move`
   float wr;        // rollout sum, same perspective
   uint8_t state;
+};
+
+// Node storage: one anonymous mapping reserved up front (virtual until written, transparent
+// huge pages requested), so the tree never moves while it grows, and resize() leaves the new
+// slots uninitialised (backup_value fills them in parallel). A std::vector would zero-fill new
+// slots serially and copy the whole tree on every doubling.
+class NodeArena {
+ public:
+  NodeArena() = default;
+  ~NodeArena() { unmap(p_, cap_); }
+  NodeArena(const NodeArena&) = delete;
+  NodeArena& operator=(const NodeArena&) = delete;
+  void reserve(size_t cap) {
+    if (cap > cap_) grow(cap);
+  }
+  size_t size() const { return n_; }
+  size_t capacity() const { return cap_; }
+  Node& operator[](size_t i) { return p_[i]; }
+  const Node& operator[](size_t i) const { return p_[i]; }
+  void clear() { n_ = 0; }
+  void push_back(const Node& x) {
+    if (n_ == cap_) grow(cap_ ? 2 * cap_ : (size_t)1 << 16);
+    p_[n_++] = x;
+  }
+  void resize(size_t n) {
+    if (n > cap_) grow(std::max(n, 2 * cap_));
+    n_ = n;
+  }
+  void swap(NodeArena& o) {
+    std::swap(p_, o.p_);
+    std::swap(n_, o.n_);
+    std::swap(cap_, o.cap_);
+  }
+
+ private:
+  static void unmap(Node* p, size_t cap) {
+    if (p) munmap(p, cap * sizeof(Node));
+  }
+  void grow(size_t cap) {
+    void* m = mmap(nullptr, cap * sizeof(Node), PROT_READ | PROT_WRITE,
+                   MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    if (m == MAP_FAILED) throw std::bad_alloc();
+    madvise(m, cap * sizeof(Node), MADV_HUGEPAGE);
+    if (n_) std::memcpy(m, p_, n_ * sizeof(Node));
+    unmap(p_, cap_);
+    p_ = static_cast<Node*>(m);
+    cap_ = cap;
+  }
+  Node* p_ = nullptr;
+  size_t n_ = 0, cap_ = 0;
 };
 
 struct Leaf {
@@ -138,11 +191,16 @@ class Pool {
 
 using mcts_detail::Leaf;
 using mcts_detail::Node;
+using mcts_detail::NodeArena;
 using mcts_detail::Pool;
 using mcts_detail::Wave;
 using mcts_detail::N_EXPANDED;
 using mcts_detail::N_NEW;
 using mcts_detail::N_PENDING;
+
+// Node pool capacity reserved up front: growth by reallocation copies the whole tree (tens of
+// MB per doubling) inside backup_value; the reservation is virtual until nodes are written.
+constexpr size_t kNodeReserve = size_t(1) << 23;
 
 class Search {
  public:
@@ -163,7 +221,7 @@ class Search {
     drop_waves();
     root_board_ = root;
     nodes_.clear();
-    nodes_.reserve(1 << 20);
+    nodes_.reserve(kNodeReserve);
     nodes_.push_back(Node{-1, -1, 0, (int16_t)PASS, 1.f, 0, 0, 0, 0.f, 0.f, N_NEW});
     root_ = 0;
   }
@@ -209,45 +267,91 @@ class Search {
   }
 
   // Returns (wave id, number of leaves); id -1 when nothing was selected.
+  //
+  // Three phases: (1) serial tree walks with virtual loss that track only what the walk needs
+  // (player to move, the last two moves and the move count decide the end of the game, exactly
+  // as Board::play_unchecked does); (2) the leaf boards (root copy + the path's moves) are built
+  // in parallel on the pool; (3) descents that ended on a terminal position are scored on their
+  // board and backed up at once (their virtual loss, taken in phase 1 so that later walks of the
+  // same wave avoid them, is dropped again).
   std::pair<int, int> select(int B) {
-    auto wave = std::make_unique<Wave>();
     collisions_ = 0;
-    int attempts = 0;
-    while ((int)wave->leaves.size() < B && attempts < 4 * B) {
+    std::vector<std::vector<int32_t>> paths;
+    std::vector<uint8_t> term;
+    paths.reserve(B);
+    term.reserve(B);
+    int attempts = 0, nleaf = 0;
+    const Board& rb = root_board_;
+    while (nleaf < B && attempts < 4 * B) {
       ++attempts;
-      Leaf L;
-      L.board = root_board_;
-      L.board.set_light(!root_board_.enforce_superko());
+      std::vector<int32_t> path;
+      path.reserve(32);
       int node = root_;
-      L.path.push_back(node);
+      path.push_back(node);
       int depth = 0;
-      while (nodes_[node].state == N_EXPANDED && nodes_[node].nchild > 0 &&
-             !L.board.end_of_game() && depth < max_depth) {
+      int ptm = rb.current_player(), l1 = rb.last1(), l2 = rb.last2(), nm = rb.nmoves();
+      bool end = rb.end_of_game();
+      while (nodes_[node].state == N_EXPANDED && nodes_[node].nchild > 0 && !end &&
+             depth < max_depth) {
         node = select_child(node);
-        L.board.play_unchecked(nodes_[node].move);
-        L.path.push_back(node);
+        path.push_back(node);
         ++depth;
+        ++nm;
+        l2 = l1;
+        l1 = nodes_[node].move;
+        ptm = -ptm;
+        if (nm > 1 && l1 == PASS && l2 == PASS && ptm == WHITE) end = true;
       }
-      if (L.board.end_of_game() || depth >= max_depth ||
-          (nodes_[node].state == N_EXPANDED && nodes_[node].nchild == 0)) {
-        const int win = L.board.get_winner();
-        const int ptm = L.board.current_player();
-        const float v = win == 0 ? 0.f : (win == ptm ? 1.f : -1.f);
-        backup_value_path(L.path, v, false);
-        if (lambda > 0.f) backup_rollout_path(L.path, v, false);
-        ++terminal_;
-        continue;
+      const bool terminal = end || depth >= max_depth ||
+                            (nodes_[node].state == N_EXPANDED && nodes_[node].nchild == 0);
+      if (!terminal) {
+        if (nodes_[node].state == N_PENDING) {  // already waiting for its evaluation
+          ++collisions_;
+          continue;
+        }
+        nodes_[node].state = N_PENDING;
+        ++nleaf;
       }
-      if (nodes_[node].state == N_PENDING) {  // already waiting for its evaluation
-        ++collisions_;
-        continue;
+      for (int id : path) nodes_[id].vl += 1;
+      paths.push_back(std::move(path));
+      term.push_back(terminal ? 1 : 0);
+    }
+    const int nd = (int)paths.size();
+    // leaf boards go straight into a recycled wave (its Leaf storage is reused: no fresh pages);
+    // terminal descents get a scratch board
+    std::unique_ptr<Wave> wave = take_wave();
+    wave->leaves.resize(nleaf);
+    std::vector<int> slot(nd);
+    int nt = 0, nl = 0;
+    for (int i = 0; i < nd; ++i) slot[i] = term[i] ? nt++ : nl++;
+    std::vector<Board> tboards(nt);
+    const bool light = !rb.enforce_superko();
+    pool_.run(nd, [&](int i) {
+      Board& b = term[i] ? tboards[slot[i]] : wave->leaves[slot[i]].board;
+      b = rb;
+      b.set_light(light);
+      const std::vector<int32_t>& path = paths[i];
+      for (size_t d = 1; d < path.size(); ++d) b.play_unchecked(nodes_[path[d]].move);
+      if (!term[i]) {
+        Leaf& L = wave->leaves[slot[i]];
+        L.path.swap(paths[i]);
+        L.z = 0.f;
       }
-      nodes_[node].state = N_PENDING;
-      for (int id : L.path) nodes_[id].vl += 1;
-      wave->leaves.push_back(std::move(L));
+    });
+    for (int i = 0; i < nd; ++i) {
+      if (!term[i]) continue;
+      const Board& b = tboards[slot[i]];
+      const int win = b.get_winner();
+      const float v = win == 0 ? 0.f : (win == b.current_player() ? 1.f : -1.f);
+      backup_value_path(paths[i], v, true);
+      if (lambda > 0.f) backup_rollout_path(paths[i], v, false);
+      ++terminal_;
     }
     const int n = (int)wave->leaves.size();
-    if (n == 0) return {-1, 0};
+    if (n == 0) {
+      recycle(std::move(wave));
+      return {-1, 0};
+    }
     const int id = next_wave_++;
     waves_[id] = std::move(wave);
     return {id, n};
@@ -277,22 +381,58 @@ class Search {
     if (wv.value_done) throw std::runtime_error("value backup twice");
     const int n = (int)wv.leaves.size();
     const int P = root_board_.npoints();
-    std::vector<std::vector<int>> moves(n);
+    // pass 1 (parallel): children per leaf still to expand — the sensible-move mask's count, or
+    // natively generated moves; then one contiguous block for all of them (the leaves of one
+    // wave are distinct nodes: select() skips pending ones, so the blocks never overlap)
+    std::vector<int32_t> cnt(n, -1);
+    std::vector<std::vector<int>> moves(sensible ? 0 : n);
     pool_.run(n, [&](int i) {
       const Leaf& L = wv.leaves[i];
       if (nodes_[L.path.back()].state == N_EXPANDED) return;
+      int c = 0;
       if (sensible) {
         const uint8_t* m = sensible + (size_t)i * P;
-        for (int p = 0; p < P; ++p)
-          if (m[p]) moves[i].push_back(p);
-        return;
+        for (int p = 0; p < P; ++p) c += m[p] != 0;
+      } else {
+        std::vector<int> eyes;
+        L.board.legal_moves(moves[i], eyes);
+        c = (int)moves[i].size();
       }
-      std::vector<int> eyes;
-      L.board.legal_moves(moves[i], eyes);
+      cnt[i] = c;
+    });
+    std::vector<int32_t> first(n, -1);
+    size_t total = nodes_.size();
+    for (int i = 0; i < n; ++i) {
+      if (cnt[i] < 0) continue;
+      first[i] = (int32_t)total;
+      total += cnt[i] == 0 ? 1 : cnt[i];
+    }
+    nodes_.resize(total);
+    // pass 2 (parallel): write the children into their block
+    pool_.run(n, [&](int i) {
+      if (first[i] < 0) return;
+      const int node = wv.leaves[i].path.back();
+      const float* pri = priors ? priors + (size_t)i * stride : nullptr;
+      if (sensible) {
+        const uint8_t* m = sensible + (size_t)i * P;
+        int k = 0;
+        fill_children(node, first[i], cnt[i], pri, [&]() {
+          while (!m[k]) ++k;
+          return k++;
+        });
+      } else {
+        size_t k = 0;
+        fill_children(node, first[i], cnt[i], pri, [&]() { return moves[i][k++]; });
+      }
     });
     for (int i = 0; i < n; ++i) {
       Leaf& L = wv.leaves[i];
-      expand(L.path.back(), moves[i], priors ? priors + (size_t)i * stride : nullptr);
+      if (first[i] >= 0) {
+        Node& nd = nodes_[L.path.back()];
+        nd.first = first[i];
+        nd.nchild = (int16_t)(cnt[i] == 0 ? 1 : cnt[i]);
+        nd.state = N_EXPANDED;
+      }
       backup_value_path(L.path, values ? values[i] : 0.f, lambda <= 0.f);
     }
     wv.value_done = true;
@@ -337,7 +477,7 @@ class Search {
       backup_rollout_path(L.path, z, true);
     }
     rollouts_ += (long)wv.leaves.size();
-    waves_.erase(id);
+    release(id);
   }
 
   // CPU rollouts of a wave on a background thread (the pool runs them)
@@ -435,7 +575,28 @@ class Search {
       wv.worker.join();
       wv.rolling = false;
     }
-    waves_.erase(id);
+    release(id);
+  }
+
+  // finished waves are kept (up to a few) and handed out again by select(): their leaf boards
+  // and paths keep their storage, so a new wave touches no fresh memory
+  std::unique_ptr<Wave> take_wave() {
+    if (free_waves_.empty()) return std::make_unique<Wave>();
+    std::unique_ptr<Wave> w = std::move(free_waves_.back());
+    free_waves_.pop_back();
+    return w;
+  }
+  void recycle(std::unique_ptr<Wave> w) {
+    w->value_done = false;
+    w->rolling = false;
+    if (free_waves_.size() < 16) free_waves_.push_back(std::move(w));
+  }
+  void release(int id) {
+    auto it = waves_.find(id);
+    if (it == waves_.end()) return;
+    std::unique_ptr<Wave> w = std::move(it->second);
+    waves_.erase(it);
+    recycle(std::move(w));
   }
 
   void drop_waves() {
@@ -444,26 +605,24 @@ class Search {
     waves_.clear();
   }
 
-  void expand(int node, const std::vector<int>& non_eye, const float* pri) {
-    if (nodes_[node].state == N_EXPANDED) return;
-    const int first = (int)nodes_.size();
-    const int nc = non_eye.empty() ? 1 : (int)non_eye.size();
+  // children of `node` for its `count` sensible moves (PASS alone when there are none), moves in
+  // increasing point order from `next_move()`, priors renormalised over them, written into the
+  // preallocated slots [first, first + max(count, 1))
+  template <class F>
+  void fill_children(int node, int first, int count, const float* pri, F&& next_move) {
+    const int nc = count == 0 ? 1 : count;
     float tot = 0.f;
     for (int k = 0; k < nc; ++k) {
-      const int mv = non_eye.empty() ? PASS : non_eye[k];
+      const int mv = count == 0 ? PASS : next_move();
       float p = 1.f;
       if (pri && mv != PASS) p = std::max(pri[mv], 0.f);
       tot += p;
-      nodes_.push_back(Node{node, -1, 0, (int16_t)mv, p, 0, 0, 0, 0.f, 0.f, N_NEW});
+      nodes_[first + k] = Node{node, -1, 0, (int16_t)mv, p, 0, 0, 0, 0.f, 0.f, N_NEW};
     }
     for (int k = 0; k < nc; ++k) {
       Node& c = nodes_[first + k];
       c.prior = tot > 0.f ? c.prior / tot : 1.f / nc;
     }
-    Node& nd = nodes_[node];  // nodes_ may have reallocated
-    nd.first = first;
-    nd.nchild = (int16_t)nc;
-    nd.state = N_EXPANDED;
   }
 
   // v: value for the player to move at the leaf; a node at depth d stores it for its mover,
@@ -489,8 +648,8 @@ class Search {
 
   // copy the subtree under `keep` into a fresh pool (BFS keeps children contiguous)
   void compact(int keep) {
-    std::vector<Node> out;
-    out.reserve(std::max<size_t>(nodes_.size() / 4, 1 << 16));
+    NodeArena out;
+    out.reserve(std::max<size_t>(nodes_.capacity(), kNodeReserve));
     std::vector<int32_t> q{keep};
     Node r = nodes_[keep];
     r.parent = -1;
@@ -519,9 +678,10 @@ class Search {
   }
 
   Board root_board_;
-  std::vector<Node> nodes_;
+  NodeArena nodes_;
   int root_ = 0;
   std::map<int, std::unique_ptr<Wave>> waves_;
+  std::vector<std::unique_ptr<Wave>> free_waves_;
   int next_wave_ = 0;
   Pool pool_;                    // expansions
   std::unique_ptr<Pool> rpool_;  // CPU rollouts (run from a wave's worker thread)

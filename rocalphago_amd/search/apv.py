@@ -16,6 +16,7 @@ full search, built for a GPU evaluator:
 ``ParallelMCTS(policy, value=None, ...)`` mirrors the reference MCTS interface
 (``get_move(state)``, ``update_with_move(move)``); ``ParallelMCTSPlayer`` mirrors MCTSPlayer.
 """
+import collections
 import time
 
 import numpy as np
@@ -26,6 +27,29 @@ from ..engine.gamestate import PASS_MOVE
 from ..features.preprocessing import _FID
 
 _rg = _engine()
+
+
+class _Ready(object):
+    """An evaluation that finished synchronously."""
+
+    def __init__(self, res):
+        self.res = res
+
+    def result(self):
+        r = self.res
+        return (r[0], r[1], r[2] if len(r) > 2 else None)
+
+
+class _Pending(object):
+    """A queued GPU evaluation: pinned host copies that are valid once ``event`` completes."""
+
+    def __init__(self, event, priors, values, sens):
+        self.event = event
+        self.host = (priors, values, sens)
+
+    def result(self):
+        self.event.synchronize()
+        return tuple(None if h is None else h.numpy() for h in self.host)
 
 
 class NetworkEvaluator(object):
@@ -64,6 +88,58 @@ class NetworkEvaluator(object):
                 self.gpu[key].supports(boards[0].size):
             return self.gpu[key](boards)
         return _rg.batch_features(boards, fids, self.nthreads)
+
+    def submit(self, boards):
+        """Start the evaluation of a wave and return a handle whose ``result()`` gives
+        ``(priors, values, sensible)`` as numpy arrays. On the GPU path everything after the
+        native feature inputs is queued on the current stream and copied back into pinned host
+        buffers asynchronously, so the caller can select the next wave while this one runs."""
+        plans = self._plans()
+        gf = None if self.gpu is None else (self.gpu.get("p") or self.gpu.get("v"))
+        if plans is None or gf is None or not gf.supports(boards[0].size):
+            return _Ready(self(boards))
+        ppol, pval = plans
+        n = len(boards)
+        if self.shared or self.value is None:
+            x = self.gpu["p"](boards)
+            xp, xv = (x[:, :self.npol].contiguous() if self.shared else x), x
+            planes = x
+        else:
+            xp = self.gpu["p"](boards) if self.policy is not None else None
+            xv = self.gpu["v"](boards)
+            planes = xp if xp is not None else xv
+        with torch.no_grad():
+            sens = planes[:, self._sens_off].reshape(n, -1) if self._sens_off is not None \
+                else None
+            pr = ppol.forward(xp) if ppol is not None else None
+            v = pval.forward(xv).reshape(-1) if pval is not None else None
+        host = []
+        for t in (pr, v, sens):
+            if t is None:
+                host.append(None)
+                continue
+            h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+            h.copy_(t, non_blocking=True)
+            host.append(h)
+        ev = torch.cuda.Event()
+        ev.record()
+        return _Pending(ev, *host)
+
+    def _plans(self):
+        """(policy plan, value plan) when every network present runs a fused HIP plan, else
+        None (then submit() evaluates synchronously)."""
+        if not hasattr(self, "_plan_cache"):
+            pp = self.policy.model._plan_for() if self.policy is not None else None
+            pv = self.value.model._plan_for() if self.value is not None else None
+            ok = (self.policy is None or pp is not None) and (self.value is None or pv is not None)
+            self._plan_cache = (pp, pv) if ok else None
+            net = self.value if self.shared or self.policy is None else self.policy
+            fl = net.preprocessor.feature_list if net is not None else []
+            self._sens_off = None
+            if "sensibleness" in fl:
+                self._sens_off = sum(_rg.feature_planes(_FID[f])
+                                     for f in fl[:fl.index("sensibleness")])
+        return self._plan_cache
 
     def __call__(self, boards):
         n = len(boards)
@@ -112,7 +188,7 @@ class ParallelMCTS(object):
     def __init__(self, policy=None, value=None, rollout=None, lmbda=0.5, c_puct=5.0,
                  n_playout=1600, batch=256, virtual_loss=3, rollout_limit=500,
                  playout_depth=722, nthreads=8, rollout_device="cpu", rollouts_per_leaf=1,
-                 seed=1, evaluator=None, max_inflight=3):
+                 seed=1, evaluator=None, max_inflight=3, pipeline=2):
         if value is None and lmbda < 1:
             lmbda = 1.0
         self.evaluator = evaluator or NetworkEvaluator(policy, value, nthreads)
@@ -133,6 +209,7 @@ class ParallelMCTS(object):
         self._gpu_rollout = None
         self._inflight = []
         self.max_inflight = max_inflight
+        self.pipeline = int(pipeline)
         self.stats = {"waves": 0, "sims": 0}
 
     # ------------------------------------------------------------------ tree management
@@ -231,18 +308,77 @@ class ParallelMCTS(object):
     def search(self, state, n_playout=None):
         s = self._sync_root(state)
         target = s.root_visits + (n_playout or self.n_playout)
-        stall = 0
-        while s.root_visits < target:
-            want = min(self.batch, target - s.root_visits)
-            before = s.root_visits
-            self._wave(s, want)
-            stall = stall + 1 if s.root_visits == before else 0
-            if stall > 3:
-                break
+        submit = getattr(self.evaluator, "submit", None)
+        if self.pipeline > 1 and submit is not None:
+            self._search_pipelined(s, target, submit)
+        else:
+            stall = 0
+            while s.root_visits < target:
+                want = min(self.batch, target - s.root_visits)
+                before = s.root_visits
+                self._wave(s, want)
+                stall = stall + 1 if s.root_visits == before else 0
+                if stall > 3:
+                    break
         t = time.perf_counter()
         self._harvest(s, 0)  # every rollout of this move backed up before choosing
         self._acc("t_rollout_wait", time.perf_counter() - t)
         return s
+
+    def _search_pipelined(self, s, target, submit):
+        """Up to ``pipeline`` waves in flight: while the GPU evaluates wave k (features, policy
+        and value nets, copies back to pinned memory) the host selects wave k+1 — virtual loss
+        keeps the two apart — builds its feature inputs and launches its rollouts; then it
+        backs up wave k. Host tree work and GPU network work overlap instead of alternating."""
+        queue = collections.deque()
+        queued = 0
+        stall = 0
+        while True:
+            t0 = time.perf_counter()
+            if len(queue) < self.pipeline and s.root_visits + queued < target:
+                want = min(self.batch, target - s.root_visits - queued)
+                wid, n = s.select(want)
+                if n > 0:
+                    boards = s.leaf_boards(wid)
+                    pending = None
+                    if self.lmbda > 0:
+                        if self.rollout_device == "gpu":
+                            pending = self._gpu_rollouts(s, wid)
+                        else:
+                            s.start_rollouts(wid)
+                    t1 = time.perf_counter()
+                    queue.append((wid, n, submit(boards), pending))
+                    queued += n
+                    self._acc("t_select", t1 - t0)
+                    self._acc("t_submit", time.perf_counter() - t1)
+                    stall = 0
+                    continue
+                if not queue:
+                    stall += 1
+                    if stall > 3 or s.root_visits >= target:
+                        break
+                    continue
+            if not queue:
+                break
+            wid, n, handle, pending = queue.popleft()
+            queued -= n
+            t1 = time.perf_counter()
+            priors, values, sens = handle.result()
+            t2 = time.perf_counter()
+            s.backup_value(wid, priors, values, sens)
+            t3 = time.perf_counter()
+            if self.lmbda > 0:
+                if pending is None:
+                    s.finish_rollouts(wid)
+                else:
+                    self._inflight.append((wid, pending))
+                    self._harvest(s, self.max_inflight)
+            t4 = time.perf_counter()
+            self.stats["waves"] += 1
+            self.stats["sims"] += n
+            self._acc("t_eval", t2 - t1)
+            self._acc("t_backup", t3 - t2)
+            self._acc("t_rollout_wait", t4 - t3)
 
     def get_move(self, state):
         s = self.search(state)

@@ -1,5 +1,10 @@
 """GPU fast rollouts (csrc/hip/rollout.hip): thousands of playouts per launch, one wavefront per
-game, on a side HIP stream so they overlap the policy/value network pass of the same wave."""
+game, on side HIP streams so they overlap the policy/value network pass of the same wave.
+
+A playout is ~430 strictly sequential moves, so one launch lasts as long as its slowest game
+(milliseconds) however few games it holds. Launches of consecutive search waves therefore go to a
+small ring of streams (separate hardware queues) and run concurrently; on one stream they would
+serialise and cap the search at one wave of rollouts per playout latency."""
 import ctypes
 
 import numpy as np
@@ -26,25 +31,33 @@ class _Pending(object):
 
 
 class GpuRollouts(object):
-    def __init__(self, policy, device=None):
+    def __init__(self, policy, device=None, nstreams=4):
         self.device = torch.device(device or "cuda")
-        self.stream = torch.cuda.Stream(self.device)
+        self.streams = [torch.cuda.Stream(self.device) for _ in range(max(1, nstreams))]
+        self._next = 0
         self.set_policy(policy)
 
     def set_policy(self, policy):
         self.w = torch.tensor(np.asarray(policy.weights, np.float32), device=self.device)
         self.pattern = torch.tensor(np.asarray(policy.pattern, np.float32), device=self.device)
+        # the side streams must see the uploaded weights (later launches do not wait for the
+        # main stream)
+        for st in self.streams:
+            st.wait_stream(torch.cuda.current_stream(self.device))
 
     def _launch(self, colors, meta, S, komi, R, limit, seed, length=False, dbg=False):
         n = colors.shape[0]
         games = n * R
-        winners = torch.empty(games, dtype=torch.int8, device=self.device)
-        lengths = torch.empty(games, dtype=torch.int16, device=self.device) if length else None
-        logits = torch.empty(games, S * S, dtype=torch.float32, device=self.device) \
-            if dbg else None
-        cur = torch.cuda.current_stream(self.device)
-        self.stream.wait_stream(cur)
-        with torch.cuda.stream(self.stream):
+        # everything the kernel touches is allocated / staged on the side stream itself, so the
+        # launch does not wait for the network work queued on the main stream
+        stream = self.streams[self._next]
+        self._next = (self._next + 1) % len(self.streams)
+        with torch.cuda.stream(stream):
+            winners = torch.empty(games, dtype=torch.int8, device=self.device)
+            lengths = torch.empty(games, dtype=torch.int16, device=self.device) \
+                if length else None
+            logits = torch.empty(games, S * S, dtype=torch.float32, device=self.device) \
+                if dbg else None
             c = torch.from_numpy(np.ascontiguousarray(colors, np.int8)).pin_memory() \
                 .to(self.device, non_blocking=True)
             m = torch.from_numpy(np.ascontiguousarray(meta, np.int32)).pin_memory() \
@@ -53,13 +66,10 @@ class GpuRollouts(object):
                                        _ptr(self.w), _ptr(self.pattern),
                                        ctypes.c_uint(seed & 0xFFFFFFFF), _ptr(winners),
                                        _ptr(lengths), _ptr(logits),
-                                       ctypes.c_void_p(self.stream.cuda_stream)),
+                                       ctypes.c_void_p(stream.cuda_stream)),
                    "rollouts")
-            # keep the staged inputs alive until the kernel has consumed them
-            c.record_stream(self.stream)
-            m.record_stream(self.stream)
             ev = torch.cuda.Event()
-            ev.record(self.stream)
+            ev.record(stream)
         return ev, winners, lengths, logits
 
     def launch(self, search, wave, R, limit, seed=1):
