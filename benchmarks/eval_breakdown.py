@@ -49,7 +49,9 @@ def main():
             boards, True, nt))[0]))
     print("inputs no ladders: %.2f ms" % tm(lambda: rg.gpu_feature_inputs(boards, False, 16))[0])
     t, x = tm(lambda: gf(boards))
-    print("GpuFeatures total: %.2f ms" % t)
+    print("GpuFeatures total (host ladders, 16 threads): %.2f ms" % t)
+    gfg = GpuFeatures(feats, dev, 16, ladders="gpu")
+    print("GpuFeatures total (GPU ladder kernel): %.2f ms" % tm(lambda: gfg(boards))[0])
     print("native batch_features 16 thr: %.2f ms" % tm(lambda: rg.batch_features(
         boards, gf.fids, 16))[0])
     xp = x[:, :48].contiguous()

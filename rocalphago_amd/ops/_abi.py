@@ -38,9 +38,13 @@ SIGNATURES = {
     "rag_sample_moves": [P, P, I, P, I, I, F, C.c_uint64, P, P],
     # features.hip
     "rag_features": [P, P, P, P, P, I, I, P, I, I, P, P],
+    # ladder.hip
+    "rag_ladder_workspace": [I, I],
+    "rag_ladders": [P, P, I, I, P, P, P],
 }
 
-RESTYPES = {"rag_conv_wgrad_workspace": SZ, "rag_head_bwd_workspace": SZ}
+RESTYPES = {"rag_conv_wgrad_workspace": SZ, "rag_head_bwd_workspace": SZ,
+            "rag_ladder_workspace": SZ}
 
 
 def declare(lib):

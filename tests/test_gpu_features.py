@@ -34,12 +34,13 @@ def dev():
     return torch.device("cuda")
 
 
+@pytest.mark.parametrize("ladders", ["host", "gpu"])
 @pytest.mark.parametrize("size,seed", [(19, 1), (19, 2), (9, 3), (13, 4), (7, 5)])
-def test_gpu_features_match_native(dev, size, seed):
+def test_gpu_features_match_native(dev, size, seed, ladders):
     from rocalphago_amd.ops.features import GpuFeatures
     feats = DEFAULT_FEATURES + ["color", "legal"]
     states = _positions(48, size, seed)
-    gf = GpuFeatures(feats, dev)
+    gf = GpuFeatures(feats, dev, ladders=ladders)
     got = gf([s.native for s in states]).cpu().numpy()
     want = rg.batch_features([s.native for s in states], Preprocess(feats).feature_ids, 4)
     assert got.shape == want.shape
@@ -56,7 +57,7 @@ def test_gpu_features_superko_and_subsets(dev):
     states = _positions(24, 9, 7, superko=True)
     for feats in (["legal", "sensibleness"], ["liberties_after", "board", "zeros"],
                   ["ladder_escape", "capture_size", "ones"]):
-        gf = GpuFeatures(feats, dev)
+        gf = GpuFeatures(feats, dev, ladders="gpu")  # superko boards: native ladders anyway
         got = gf([s.native for s in states]).cpu().numpy()
         want = rg.batch_features([s.native for s in states], Preprocess(feats).feature_ids, 4)
         assert np.array_equal(got, want), feats
