@@ -557,6 +557,10 @@ bool rag_conv_pipe_launch(const bf16* x, const bf16* w, const float* bias, bf16*
                           const bf16* mk, const bf16* res, int M, int S, int WI, int shift,
                           int WO, int HO, int CIN, int COUTP, int YC, int KS, int relu, int HM,
                           hipStream_t stream);  // conv_fwd.hip
+bool rag_conv_slab_launch(const bf16* x, const bf16* w, const float* bias, bf16* y,
+                          const bf16* mk, const bf16* res, int B, int S, int HI, int WO, int HO,
+                          int CIN, int COUTP, int YC, int KS, int relu, int HM,
+                          hipStream_t stream);  // conv_slab.hip
 
 // Conv forward / dgrad.  X: padded input (halo HI, CIN channels, CIN % 32 == 0).  W: packed
 // bf16 weights [taps][WROWS][CIN].  Y: padded output (halo HO, YC channels, COUTP % 32 == 0,
@@ -581,6 +585,9 @@ RAG_API int rag_conv_igemm(const void* X, const void* W, const float* bias, void
     const char* e = getenv("RAG_CONV_PIPE");
     return !(e && e[0] == '0');
   }();
+  if (rag_conv_slab_launch(x, w, bias, y, mk, res, B, S, HI, WO, HO, CIN, COUTP, YC, KS, relu,
+                           HM, stream))
+    return (int)hipGetLastError();
   if (use_pipe && rag_conv_pipe_launch(x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN,
                                        COUTP, YC, KS, relu, HM, stream))
     return (int)hipGetLastError();
@@ -600,6 +607,10 @@ int rag_launch_wgrad_taps(const bf16* G, const bf16* X, float* part, float* bpar
                           int nchunks, hipStream_t stream);  // wgrad.hip
 bool rag_wgrad_taps_fits(int WP, int KS, int RG);  // wgrad.hip
 int rag_wgrad_taps_target_blocks();  // wgrad.hip
+bool rag_wgrad_slab_ok(int S, int H, int HG, int GC, int COUTP, int CINP, int KS);  // wgrad_slab.hip
+int rag_wgrad_slab_nchunks(int R, int CINP, int* spc);                            // wgrad_slab.hip
+int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpart, int R, int WP,
+                          int GC, int CIN, int spc, int CINP, int nchunks, hipStream_t stream);
 
 namespace {
 // all-taps variant applicability and plan (see wgrad.hip)
@@ -647,6 +658,10 @@ RAG_API size_t rag_conv_wgrad_workspace(int B, int S, int COUTP, int CINP, int K
     TapsPlan tp = taps_plan(B, S, H, H, COUTP, CINP, KS);
     if (tp.ok && tp.nchunks > nc) nc = tp.nchunks;
   }
+  if (rag_wgrad_slab_ok(S, 1, 1, COUTP, COUTP, CINP, KS)) {
+    const int sn = rag_wgrad_slab_nchunks(B * (S + 2) * (S + 2), CINP, nullptr);
+    if (sn > nc) nc = sn;
+  }
   if (nchunks) *nchunks = nc;
   return (size_t)nc * taps * COUTP * CINP + (size_t)nc * COUTP;
 }
@@ -681,7 +696,16 @@ RAG_API int rag_conv_wgrad(const void* G, const void* X, float* dW, float* db, f
   int nchunks;
   float* part = work;
   float* bpart;
-  if (tp.ok) {
+  if (rag_wgrad_slab_ok(S, HI, HG, GC, COUTP, CINP, KS)) {
+    const int WP = S + 2 * HI;
+    const int R = B * WP * WP;
+    int spc = 1;
+    nchunks = rag_wgrad_slab_nchunks(R, CINP, &spc);
+    bpart = db ? work + (size_t)nchunks * taps * COUTP * CINP : nullptr;
+    const int rc = rag_launch_wgrad_slab(g, x, part, bpart, R, WP, GC, CINP, spc, CINP, nchunks,
+                                         stream);
+    if (rc) return rc;
+  } else if (tp.ok) {
     nchunks = tp.nchunks;
     bpart = db ? work + (size_t)nchunks * taps * COUTP * CINP : nullptr;
     const int WP = S + 2 * HI;

@@ -1,0 +1,221 @@
+// Weight gradient of the 192-filter 3x3 trunk convolution, "all n, all taps" slab formulation.
+//
+// Same identity as wgrad.hip: with G and X sharing one padded geometry (halo 1, WP = S + 2),
+// every tap is a constant shift in the flattened padded row space,
+//
+//     dW[tap][n][c] = sum_r G[r][n] * X[r + (ky-1)*WP + (kx-1)][c],
+//
+// and G is zero on halo rows, so the sum runs over all padded rows with no masking.
+//
+// wgrad.hip's 64(n) x 64(c) tiles re-stage every G row for each of 3 c-tiles and every X row for
+// each of 3 n-tiles: ~39 B/clk/CU of L2 -> LDS traffic, above what an L2 gather sustains. Here a
+// 768-thread block owns ALL 192 n x 32 c x 9 taps (216 MFMA tiles, 18 per wave) for a chunk of
+// 64-row stages. Per stage it stages the 64 G rows (all 192 channels) and one 112-row X slab of
+// its 32 channels that covers every tap's shifted window: ~18 B/clk/CU at the MFMA rate.
+//
+// LDS layouts (no padding; 3-stage ring, 93 KB):
+//   * G [64][192]: fragments are transposed reads (ds_read_b64_tr_b16) of 8 rows x 32 B per
+//     32-lane half. Rows are 384 B (= 32 words mod 64 banks), so the 32-byte unit index is XORed
+//     with row bits 1..2: the 8 rows of a half then hit 8 distinct 8-word bank windows.
+//   * X [112][32]: rows are 64 B and a tap shifts the start row arbitrarily; XOR of the 16-byte
+//     chunk's bit 1 with row bit 2 makes any 8 consecutive rows hit 8 distinct windows (rows r and
+//     r+4 share r mod 4 and differ in bit 2).
+// The MFMA k index is permuted (krow) exactly as in wgrad.hip, identically for both operands.
+// fp32 partials go to part[chunk][tap][n][c] and are summed by wgrad_reduce_kernel (conv.hip).
+#include "common.h"
+
+using namespace rag;
+
+namespace {
+
+constexpr int kRows = 64;                       // padded rows per stage (two MFMA k-steps)
+constexpr int kN = 192;                         // output channels (all of them)
+constexpr int kC = 32;                          // input channels per block
+constexpr int kGChunks = kN / 8;                // 16-byte chunks per G row
+constexpr int kXRows = 112;                     // X slab rows (7 glds x 16 rows)
+constexpr int kXWaves = kXRows / 16;            // waves that stage X
+constexpr int kGElems = kRows * kN;
+constexpr int kStage = kGElems + kXRows * kC;
+constexpr int kNBUF = 3;
+constexpr int kWaves = 12;
+static_assert(kRows * kGChunks == kWaves * 2 * 64, "two G glds per wave");
+
+__device__ __forceinline__ int swz_x(int row) { return ((row >> 2) & 1) << 1; }
+__device__ __forceinline__ int swz_g(int row) { return ((row >> 1) & 3) << 1; }
+__device__ __forceinline__ int krow(int g, int q) { return (g & 1) * 4 + q + (g >> 1) * 8; }
+
+__device__ __forceinline__ bf16x8 tr_frag(const bf16* p0, const bf16* p1) {
+  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_PTR(bf16x4))p0);
+  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_PTR(bf16x4))p1);
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+__global__ void __launch_bounds__(768)
+wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
+                  float* __restrict__ part, float* __restrict__ bpart, int R, int WP, int GC,
+                  int CIN, int spc, int CINP) {
+  __shared__ __attribute__((aligned(16))) bf16 lds[kNBUF * kStage];
+  __shared__ float bred[kWaves * 64];
+
+  const int lane = lane_id();
+  const int w = wave_id();
+  const int tid = threadIdx.x;
+  const int ntc = CINP / kC;
+  const int wid = xcd_remap(blockIdx.x, gridDim.x);  // the c-tiles of a chunk share one XCD
+  const int chunk = wid / ntc;
+  const int ctile = wid - chunk * ntc;
+  const int c0 = ctile * kC;
+  const int steps = (R + kRows - 1) / kRows;
+  const int sbeg = chunk * spc;
+  int nsteps = steps - sbeg;
+  nsteps = nsteps < spc ? nsteps : spc;
+  nsteps = nsteps > 0 ? nsteps : 0;
+  const int xshift = -(WP + 1);  // X slab row 0 <-> stage row 0 shifted by tap (0, 0)
+
+  // staging: G instruction i = 2w + k covers chunk slots [64 i, 64 i + 64) of the [64][24] tile;
+  // X instruction w (< 7) covers slab rows [16 w, 16 w + 16)
+  int grow[2], gcol[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int slot = (2 * w + k) * 64 + lane;
+    const int row = slot / kGChunks;
+    const int pc = slot - row * kGChunks;
+    grow[k] = row;
+    gcol[k] = (pc ^ swz_g(row)) * 8;
+  }
+  const int xrow = w * 16 + (lane >> 2);
+  const int xcol = c0 + (((lane & 3) ^ swz_x(xrow)) * 8);
+  const bool xw = w < kXWaves;
+
+  auto stage = [&](int s, int buf) {
+    const int r0 = (sbeg + s) * kRows;
+    bf16* lg = lds + buf * kStage;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      int r = r0 + grow[k];
+      r = r < R ? r : R - 1;  // past the end: the last padded row is halo (zero)
+      glds16(G + (size_t)r * GC + gcol[k], lg + (2 * w + k) * 512);
+    }
+    if (xw) {
+      int r = r0 + xshift + xrow;
+      r = r < 0 ? 0 : (r < R ? r : R - 1);  // only ever paired with zero (halo) G rows
+      glds16(X + (size_t)r * CIN + xcol, lg + kGElems + w * 512);
+    }
+  };
+
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int kr = krow(g, q);
+  const int nf0 = (w % 6) * 2;  // this wave's two 16-channel n fragments
+  const int cf = w / 6;         // and its 16-channel c fragment
+  int goff[2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+    goff[a] = kr * kN + ((((nf0 + a) * 2 + (p >> 1)) ^ swz_g(kr)) * 8) + 4 * (p & 1);
+  int xoff[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int xr = kr + (t / 3) * WP + (t % 3);
+    xoff[t] = kGElems + xr * kC + (((cf * 2 + (p >> 1)) ^ swz_x(xr)) * 8) + 4 * (p & 1);
+  }
+
+  f32x4 acc[9][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool do_bias = bpart != nullptr;
+  const int bcol = ctile * 32 + (tid & 31);  // bias columns: this c-tile's 32 of the 192
+  const int brow = tid >> 5;                 // rows brow, brow + 24, brow + 48
+  float bsum = 0.f;
+
+  if (nsteps > 0) stage(0, 0);
+  if (nsteps > 1) stage(1, 1);
+  for (int s = 0; s < nsteps; ++s) {
+    // retire stage s; stage s+1 (2 or 3 glds of this wave) may stay in flight
+    if (s + 1 < nsteps) {
+      if (xw)
+        asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (s + 2 < nsteps) stage(s + 2, (s + 2) % kNBUF);
+    const bf16* lb = lds + (s % kNBUF) * kStage;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ro = kk * 32;  // rows; bits 1..2 unchanged, so the swizzles are unchanged
+      bf16x8 fa[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+        fa[a] = tr_frag(lb + goff[a] + ro * kN, lb + goff[a] + (ro + 16) * kN);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const bf16x8 fb = tr_frag(lb + xoff[t] + ro * kC, lb + xoff[t] + (ro + 16) * kC);
+        acc[t][0] = mfma16(fa[0], fb, acc[t][0]);
+        acc[t][1] = mfma16(fa[1], fb, acc[t][1]);
+      }
+      __builtin_amdgcn_s_setprio(0);
+    }
+    if (do_bias && bcol < kN) {
+      for (int r = brow; r < kRows; r += 24)
+        bsum += (float)lb[r * kN + (((bcol >> 3) ^ swz_g(r)) << 3) + (bcol & 7)];
+    }
+  }
+
+  // partial slab part[chunk][tap][n][c]; C layout: col = lane&15, row = 4*(lane>>4) + r
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    float* dst = part + ((size_t)(chunk * 9 + t) * kN) * CINP;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int n = (nf0 + a) * 16 + g * 4;
+      const int cc = c0 + cf * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dst[(size_t)(n + r) * CINP + cc] = acc[t][a][r];
+    }
+  }
+  if (do_bias) {
+    bred[tid] = bsum;
+    __syncthreads();
+    if (tid < 32 && bcol < kN) {
+      float v = 0.f;
+      for (int k = 0; k < 24; ++k) v += bred[k * 32 + tid];
+      bpart[(size_t)chunk * kN + bcol] = v;
+    }
+  }
+}
+
+}  // namespace
+
+// Applicability: 3x3, G and X both halo 1, 192 output channels, CINP == 192 (its six 32-channel
+// c-tiles also split the 192 bias columns), and the X slab covering every tap window of a stage
+// (64 + 2*WP + 2 <= 112). RAG_WGRAD_SLAB=0 disables it.
+bool rag_wgrad_slab_ok(int S, int H, int HG, int GC, int COUTP, int CINP, int KS) {
+  static const bool on = [] {
+    const char* e = getenv("RAG_WGRAD_SLAB");
+    return !(e && e[0] == '0');
+  }();
+  const int WP = S + 2 * H;
+  return on && KS == 3 && H == 1 && HG == 1 && COUTP == kN && CINP == kN && GC % 8 == 0 &&
+         GC >= kN && kRows + 2 * WP + 2 <= kXRows;
+}
+
+// Chunks of 64-row stages: one resident block per CU (256) over all c-tiles.
+int rag_wgrad_slab_nchunks(int R, int CINP, int* spc) {
+  const int steps = (R + kRows - 1) / kRows;
+  int nc = 256 / (CINP / kC);
+  nc = nc < steps ? nc : steps;
+  nc = nc > 0 ? nc : 1;
+  const int s = (steps + nc - 1) / nc;
+  if (spc) *spc = s;
+  return (steps + s - 1) / s;
+}
+
+int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpart, int R, int WP,
+                          int GC, int CIN, int spc, int CINP, int nchunks, hipStream_t stream) {
+  wgrad_slab_kernel<<<nchunks * (CINP / kC), 64 * kWaves, 0, stream>>>(G, X, part, bpart, R, WP,
+                                                                      GC, CIN, spc, CINP);
+  return (int)hipGetLastError();
+}

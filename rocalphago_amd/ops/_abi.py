@@ -41,6 +41,8 @@ SIGNATURES = {
     # ladder.hip
     "rag_ladder_workspace": [I, I],
     "rag_ladders": [P, P, I, I, P, P, P],
+    # conv_slab.hip
+    "rag_conv_slab_mode": [I],
 }
 
 RESTYPES = {"rag_conv_wgrad_workspace": SZ, "rag_head_bwd_workspace": SZ,

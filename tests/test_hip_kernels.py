@@ -26,7 +26,7 @@ def ops():
 @pytest.mark.parametrize("B,cin,cout,ks,S", [(3, 192, 192, 3, 19), (5, 48, 192, 5, 19),
                                              (2, 16, 16, 3, 19), (7, 128, 128, 3, 13),
                                              (4, 192, 32, 1, 19), (1, 12, 16, 5, 9),
-                                             (2, 64, 96, 3, 7)])
+                                             (2, 64, 96, 3, 7), (130, 192, 192, 3, 19)])
 def test_conv_forward(ops, B, cin, cout, ks, S):
     dev = torch.device("cuda")
     torch.manual_seed(0)
@@ -52,7 +52,8 @@ def test_conv_forward(ops, B, cin, cout, ks, S):
 @pytest.mark.parametrize("B,cin,cout,ks,hi,hg,S", [
     (3, 192, 192, 3, 1, 1, 19), (2, 16, 16, 3, 1, 1, 19), (4, 64, 128, 3, 1, 1, 19),
     (3, 32, 192, 5, 2, 1, 19), (3, 64, 192, 5, 2, 2, 19), (2, 128, 64, 1, 1, 1, 19),
-    (37, 192, 192, 3, 1, 1, 19), (5, 64, 64, 3, 2, 2, 9), (6, 128, 192, 3, 1, 1, 13)])
+    (37, 192, 192, 3, 1, 1, 19), (5, 64, 64, 3, 2, 2, 9), (6, 128, 192, 3, 1, 1, 13),
+    (128, 192, 192, 3, 1, 1, 19)])
 def test_conv_backward(ops, B, cin, cout, ks, hi, hg, S):
     dev = torch.device("cuda")
     torch.manual_seed(1)
@@ -80,6 +81,45 @@ def test_conv_backward(ops, B, cin, cout, ks, hi, hg, S):
     ops.conv_wgrad(gp, xp, dw, db, B, S, hi, cout, coutp, cin, cinp, ks, hg=hg)
     assert rel_err(dw, wr.grad) < 2e-2
     assert rel_err(db, bf(g).sum((0, 2, 3))) < 2e-2
+
+
+def test_conv_slab_residual(ops):
+    """The one-board-per-block slab kernel (conv_slab.hip, opt-in) vs fp32 PyTorch: residual
+    sum-merge epilogue, output halo 2 (stays zero), boards past B untouched, and dgrad."""
+    dev = torch.device("cuda")
+    torch.manual_seed(3)
+    B, C, S = 131, 192, 19
+    x = torch.randn(B, C, S, S, device=dev)
+    w = torch.randn(C, C, 3, 3, device=dev) * 0.05
+    b = torch.randn(C, device=dev) * 0.1
+    r = torch.randn(B, C, S, S, device=dev)
+    ref = F.relu(F.conv2d(bf(x), bf(w), b, padding=1) + bf(r))
+    xp = ops.pack_nchw(x, 1, C)
+    wf, _ = ops.pack_weights(w, C, C)
+    y = ops.alloc_padded(B + 1, S, 2, C, dev)
+    y[B:] = 7.0
+    rp = ops.alloc_padded(B, S, 2, C, dev)
+    rp[:, 2:-2, 2:-2] = ops.pack_nchw(r, 2, C)[:, 2:-2, 2:-2]
+    lib = ops._lib()
+    prev = lib.rag_conv_slab_mode(1)  # opt-in kernel (conv_slab.hip): force it for this test
+    try:
+        ops.conv_igemm(xp, wf, b, y[:B], B, S, 1, 2, C, C, 3, relu=True, residual=rp)
+        # dgrad form (ReLU mask of the layer input) through the slab kernel as well
+        wf2, wb2 = ops.pack_weights(w, C, C, wb=torch.empty(9, C, C, dtype=torch.bfloat16,
+                                                              device=dev))
+        g = torch.randn(B, C, S, S, device=dev)
+        xr = bf(F.relu(x)).requires_grad_()
+        F.conv2d(xr, bf(w), padding=1).mul(bf(g)).sum().backward()
+        xm = ops.pack_nchw(F.relu(x), 1, C)
+        dx = ops.alloc_padded(B, S, 1, C, dev)
+        ops.conv_igemm(ops.pack_nchw(g, 1, C), wb2, None, dx, B, S, 1, 1, C, C, 3, relu=False,
+                       mask=xm)
+    finally:
+        lib.rag_conv_slab_mode(prev)
+    assert rel_err(ops.unpack(dx, C, 1), xr.grad * (x > 0)) < 2e-2
+    assert rel_err(ops.unpack(y[:B], C, 2), ref) < 2e-2
+    assert y[:B, :2].abs().max().item() == 0 and y[:B, :, -2:].abs().max().item() == 0
+    assert (y[B:] == 7.0).all()
 
 
 def test_pack_input_transforms(ops):
