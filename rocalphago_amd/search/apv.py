@@ -188,7 +188,14 @@ class ParallelMCTS(object):
     def __init__(self, policy=None, value=None, rollout=None, lmbda=0.5, c_puct=5.0,
                  n_playout=1600, batch=256, virtual_loss=3, rollout_limit=500,
                  playout_depth=722, nthreads=8, rollout_device="cpu", rollouts_per_leaf=1,
-                 seed=1, evaluator=None, max_inflight=3, pipeline=2):
+                 seed=1, evaluator=None, max_inflight=3, pipeline=2, dp=None):
+        # dp (parallel/dp.DPContext, world > 1): root parallelism over ranks — every rank
+        # searches the same position with its own seed on its own GPU, and get_move() sums the
+        # root visit counts over ranks (one all-reduce of S*S+1 counts), so all
+        # ranks play the same move
+        self.dp = dp if dp is not None and dp.enabled else None
+        if self.dp is not None:
+            seed = int(seed) + 7919 * self.dp.rank
         if value is None and lmbda < 1:
             lmbda = 1.0
         self.evaluator = evaluator or NetworkEvaluator(policy, value, nthreads)
@@ -382,8 +389,24 @@ class ParallelMCTS(object):
 
     def get_move(self, state):
         s = self.search(state)
-        a = s.best_move()
+        a = s.best_move() if self.dp is None else self._merged_best(s, state.size)
         return PASS_MOVE if a < 0 else divmod(int(a), state.size)
+
+    def _merged_best(self, s, size):
+        """Most visited root move over all ranks (visit counts summed by all-reduce; ties go to
+        the lowest point, pass last, identically on every rank)."""
+        P = size * size
+        mvs, vis, _, _ = s.root_stats()
+        counts = np.zeros(P + 1, np.float64)  # slot P: pass
+        for m, v in zip(mvs, vis):
+            counts[P if m < 0 else m] += v
+        t = torch.from_numpy(counts).to(self.dp.device)
+        self.dp.allreduce_sum_(t)
+        self.merged_visits = t.cpu().numpy()
+        if self.merged_visits.max() <= 0:
+            return s.best_move()
+        best = int(np.argmax(self.merged_visits))
+        return -1 if best == P else best
 
     def root_statistics(self):
         """(moves, visits, Q, prior) of the root children."""

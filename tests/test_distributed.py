@@ -122,6 +122,57 @@ def test_bucketed_allreduce_mean(tmp_path):
                                    np.full(n, 1.5, np.float32))
 
 
+class _UniformEval(object):
+    """Evaluator stub for the search workers: uniform priors, no value."""
+
+    def __call__(self, boards):
+        n, P = len(boards), boards[0].size ** 2
+        return np.full((n, P), 1.0 / P, np.float32), None
+
+
+def _mcts_worker(rank, world, port, outdir):
+    _setup(rank, world, port)
+    from rocalphago_amd.engine.gamestate import GameState
+    from rocalphago_amd.parallel.dp import DPContext
+    from rocalphago_amd.search.apv import ParallelMCTS
+    dp = DPContext(device="cpu")
+    mc = ParallelMCTS(evaluator=_UniformEval(), lmbda=1.0, n_playout=96, batch=16,
+                      rollout_limit=60, nthreads=1, dp=dp)
+    st = GameState(size=7)
+    moves, local, merged = [], [], []
+    for _ in range(3):
+        mv = mc.get_move(st)
+        mvs, vis, _, _ = mc.root_statistics()
+        v = np.zeros(50)
+        for m, n in zip(mvs, vis):
+            v[49 if m < 0 else m] += n
+        local.append(v)
+        merged.append(mc.merged_visits.copy())
+        moves.append(-1 if mv is None else mv[0] * 7 + mv[1])
+        st.do_move(mv)
+        mc.update_with_move(mv)
+    np.save(os.path.join(outdir, "mv%d.npy" % rank), np.array(moves))
+    np.save(os.path.join(outdir, "loc%d.npy" % rank), np.array(local))
+    np.save(os.path.join(outdir, "mrg%d.npy" % rank), np.array(merged))
+    dp.shutdown()
+
+
+@pytest.mark.timeout(300)
+def test_root_parallel_mcts(tmp_path):
+    """Root parallelism: each rank searches its own tree (own rollout seeds), the root visit
+    counts are all-reduced and every rank plays the same most-visited move."""
+    _spawn(_mcts_worker, (str(tmp_path),))
+    m0, m1 = np.load(tmp_path / "mv0.npy"), np.load(tmp_path / "mv1.npy")
+    assert np.array_equal(m0, m1)
+    l0, l1 = np.load(tmp_path / "loc0.npy"), np.load(tmp_path / "loc1.npy")
+    g0, g1 = np.load(tmp_path / "mrg0.npy"), np.load(tmp_path / "mrg1.npy")
+    np.testing.assert_allclose(g0, l0 + l1)
+    np.testing.assert_allclose(g1, l0 + l1)
+    assert not np.array_equal(l0, l1), "ranks ran identical searches (seeds not per rank)"
+    for k in range(len(m0)):
+        assert m0[k] == int(np.argmax(g0[k])) or (m0[k] == -1 and np.argmax(g0[k]) == 49)
+
+
 def _rl_worker(rank, world, port, outdir):
     _setup(rank, world, port)
     import numpy as np_
