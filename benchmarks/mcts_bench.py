@@ -18,7 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def build_search(device, filters=192, layers=12, batch=256, rollout_device="gpu",
                  rollouts_per_leaf=1, lmbda=0.5, nthreads=16, seed=1, pipeline=2,
-                 max_inflight=4):
+                 max_inflight=8, rollout_group=3):
     from rocalphago_amd.features.preprocessing import DEFAULT_FEATURES
     from rocalphago_amd.models.policy import CNNPolicy
     from rocalphago_amd.models.value import CNNValue
@@ -29,7 +29,8 @@ def build_search(device, filters=192, layers=12, batch=256, rollout_device="gpu"
                    layers=layers, device=device, seed=seed + 1)
     return ParallelMCTS(pol, val, lmbda=lmbda, batch=batch, rollout_device=rollout_device,
                         rollouts_per_leaf=rollouts_per_leaf, nthreads=nthreads, seed=seed,
-                        pipeline=pipeline, max_inflight=max_inflight)
+                        pipeline=pipeline, max_inflight=max_inflight,
+                        rollout_group=rollout_group)
 
 
 def measure(device, playouts=8192, warmup=512, moves=1, **kw):
@@ -76,7 +77,8 @@ def main():
     ap.add_argument("--filters", type=int, default=192)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--pipeline", type=int, default=2, help="waves in flight (1 = serial)")
-    ap.add_argument("--max-inflight", type=int, default=4, help="rollout waves in flight")
+    ap.add_argument("--max-inflight", type=int, default=8, help="rollout waves in flight")
+    ap.add_argument("--rollout-group", type=int, default=3, help="waves per rollout launch")
     ap.add_argument("--moves", type=int, default=1)
     args = ap.parse_args()
     import torch
@@ -84,7 +86,8 @@ def main():
     r = measure(dev, playouts=args.playouts, batch=args.batch, moves=args.moves,
                 rollout_device=args.rollout_device, rollouts_per_leaf=args.rollouts_per_leaf,
                 lmbda=args.lmbda, filters=args.filters, nthreads=args.threads,
-                pipeline=args.pipeline, max_inflight=args.max_inflight)
+                pipeline=args.pipeline, max_inflight=args.max_inflight,
+                rollout_group=args.rollout_group)
     r["pipeline"] = args.pipeline
     r.update({"metric": "MCTS simulations/s (19x19 APV-MCTS, policy+value on GPU)",
               "model": "policy 48x192x13 + value 49x192x13+FC256", "lmbda": args.lmbda})

@@ -188,7 +188,8 @@ class ParallelMCTS(object):
     def __init__(self, policy=None, value=None, rollout=None, lmbda=0.5, c_puct=5.0,
                  n_playout=1600, batch=256, virtual_loss=3, rollout_limit=500,
                  playout_depth=722, nthreads=8, rollout_device="cpu", rollouts_per_leaf=1,
-                 seed=1, evaluator=None, max_inflight=3, pipeline=2, dp=None):
+                 seed=1, evaluator=None, max_inflight=8, pipeline=2, dp=None,
+                 rollout_group=3):
         # dp (parallel/dp.DPContext, world > 1): root parallelism over ranks — every rank
         # searches the same position with its own seed on its own GPU, and get_move() sums the
         # root visit counts over ranks (one all-reduce of S*S+1 counts), so all
@@ -216,6 +217,9 @@ class ParallelMCTS(object):
         self._gpu_rollout = None
         self._inflight = []
         self.max_inflight = max_inflight
+        # GPU rollouts of `rollout_group` consecutive waves go out as one launch
+        # (gpu_rollout.RolloutBatcher); up to `max_inflight` waves' rollouts are in flight
+        self.rollout_group = int(rollout_group)
         self.pipeline = int(pipeline)
         self.stats = {"waves": 0, "sims": 0}
 
@@ -307,10 +311,11 @@ class ParallelMCTS(object):
 
     def _gpu_rollouts(self, s, wid):
         if self._gpu_rollout is None:
-            from .gpu_rollout import GpuRollouts
-            self._gpu_rollout = GpuRollouts(self.rollout, torch.device("cuda"))
-        return self._gpu_rollout.launch(s, wid, self.rollouts_per_leaf, self.rollout_limit,
-                                        seed=self.seed * 7919 + self.stats["waves"])
+            from .gpu_rollout import GpuRollouts, RolloutBatcher
+            self._gpu_rollout = RolloutBatcher(GpuRollouts(self.rollout, torch.device("cuda")),
+                                               self.rollout_group)
+        return self._gpu_rollout.add(s, wid, self.rollouts_per_leaf, self.rollout_limit,
+                                     seed=self.seed * 7919 + self.stats["waves"])
 
     def search(self, state, n_playout=None):
         s = self._sync_root(state)
@@ -328,6 +333,8 @@ class ParallelMCTS(object):
                 if stall > 3:
                     break
         t = time.perf_counter()
+        if self._gpu_rollout is not None:
+            self._gpu_rollout.flush()
         self._harvest(s, 0)  # every rollout of this move backed up before choosing
         self._acc("t_rollout_wait", time.perf_counter() - t)
         return s

@@ -6,6 +6,7 @@ A playout is ~430 strictly sequential moves, so one launch lasts as long as its 
 small ring of streams (separate hardware queues) and run concurrently; on one stream they would
 serialise and cap the search at one wave of rollouts per playout latency."""
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -30,10 +31,86 @@ class _Pending(object):
         return w.cpu().numpy()
 
 
+class _Group(object):
+    """Rollouts of several search waves launched together (RolloutBatcher)."""
+
+    def __init__(self):
+        self.colors, self.meta = [], []
+        self.games = 0
+        self.pending = None
+        self._res = None
+
+    def result(self):
+        if self._res is None:
+            self._res = self.pending.result()
+        return self._res
+
+
+class _Slice(object):
+    """One wave's share of a group: the _Pending interface (done / result)."""
+
+    def __init__(self, batcher, group, off, n):
+        self.batcher, self.group, self.off, self.n = batcher, group, off, n
+
+    def done(self):
+        return self.group.pending is not None and self.group.pending.done()
+
+    def result(self):
+        if self.group.pending is None:
+            self.batcher.flush()
+        return self.group.result()[self.off:self.off + self.n]
+
+
+class RolloutBatcher(object):
+    """Launches the rollouts of ``group`` consecutive search waves as one kernel.
+
+    A launch lasts as long as its longest playout (~430 sequential moves) whether it holds 256 or
+    1024 games — a 256-leaf wave fills only 64 CUs — and launches of different waves overlap only
+    as far as the hardware queues allow. Grouping waves multiplies the rollouts per queue slot;
+    a wave's rollouts start at most one wave later, which the asynchronous rollout backup of
+    APV-MCTS absorbs."""
+
+    def __init__(self, rollouts, group=2):
+        self.gr = rollouts
+        self.k = max(1, int(group))
+        self.cur = None
+        self.args = None
+
+    def add(self, search, wave, R, limit, seed):
+        colors, meta = search.rollout_inputs(wave)
+        if self.cur is None:
+            self.cur = _Group()
+            b = search.root_board
+            self.args = (b.size, b.komi, R, limit, seed)
+        g = self.cur
+        sl = _Slice(self, g, g.games, colors.shape[0])
+        g.colors.append(colors)
+        g.meta.append(meta)
+        g.games += colors.shape[0]
+        if len(g.colors) >= self.k:
+            self.flush()
+        return sl
+
+    def flush(self):
+        g, self.cur = self.cur, None
+        if g is None:
+            return
+        S, komi, R, limit, seed = self.args
+        colors = np.concatenate(g.colors) if len(g.colors) > 1 else g.colors[0]
+        meta = np.concatenate(g.meta) if len(g.meta) > 1 else g.meta[0]
+        ev, winners, _, _ = self.gr._launch(colors, meta, S, komi, R, limit, seed)
+        g.pending = _Pending(ev, winners, colors.shape[0], R)
+
+
 class GpuRollouts(object):
-    def __init__(self, policy, device=None, nstreams=4):
+    def __init__(self, policy, device=None, nstreams=None, priority=None):
         self.device = torch.device(device or "cuda")
-        self.streams = [torch.cuda.Stream(self.device) for _ in range(max(1, nstreams))]
+        if nstreams is None:
+            nstreams = int(os.environ.get("RAG_ROLLOUT_STREAMS", "6"))
+        if priority is None:  # torch: larger number = lower priority; 0 = default
+            priority = int(os.environ.get("RAG_ROLLOUT_PRIORITY", "0"))
+        self.streams = [torch.cuda.Stream(self.device, priority=priority)
+                        for _ in range(max(1, nstreams))]
         self._next = 0
         self.set_policy(policy)
 
