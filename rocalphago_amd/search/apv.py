@@ -17,6 +17,8 @@ full search, built for a GPU evaluator:
 (``get_move(state)``, ``update_with_move(move)``); ``ParallelMCTSPlayer`` mirrors MCTSPlayer.
 """
 import collections
+import os
+import concurrent.futures
 import time
 
 import numpy as np
@@ -38,6 +40,16 @@ class _Ready(object):
     def result(self):
         r = self.res
         return (r[0], r[1], r[2] if len(r) > 2 else None)
+
+
+class _Async(object):
+    """Evaluation submitted from the worker thread: result() joins it, then its _Pending."""
+
+    def __init__(self, future):
+        self.future = future
+
+    def result(self):
+        return self.future.result().result()
 
 
 class _Pending(object):
@@ -220,6 +232,12 @@ class ParallelMCTS(object):
         # GPU rollouts of `rollout_group` consecutive waves go out as one launch
         # (gpu_rollout.RolloutBatcher); up to `max_inflight` waves' rollouts are in flight
         self.rollout_group = int(rollout_group)
+        # RAG_ASYNC_EVAL=1: feature extraction + network launch of a wave run on a worker thread
+        # (the native feature code releases the GIL) while the host selects the next wave.
+        # Measured slower (52-55k vs 59k sims/s): the host ladder reads are the bound and the
+        # concurrent select only competes with them for the CPU share, so it is off by default.
+        self.async_eval = os.environ.get("RAG_ASYNC_EVAL", "0") == "1"
+        self._pool = None
         self.pipeline = int(pipeline)
         self.stats = {"waves": 0, "sims": 0}
 
@@ -361,7 +379,13 @@ class ParallelMCTS(object):
                         else:
                             s.start_rollouts(wid)
                     t1 = time.perf_counter()
-                    queue.append((wid, n, submit(boards), pending))
+                    if self.async_eval:
+                        if self._pool is None:
+                            self._pool = concurrent.futures.ThreadPoolExecutor(1)
+                        handle = _Async(self._pool.submit(submit, boards))
+                    else:
+                        handle = submit(boards)
+                    queue.append((wid, n, handle, pending))
                     queued += n
                     self._acc("t_select", t1 - t0)
                     self._acc("t_submit", time.perf_counter() - t1)
