@@ -136,9 +136,36 @@ struct Game {
   }
 
   // liberty counters per label, then the clamped count into every stone's cell (flagging the
-  // cells that changed)
+  // cells that changed). Every LDS load of a phase is issued for all of the lane's points before
+  // the phase's first LDS write (uint8 cells alias everything, so the compiler cannot reorder
+  // loads across a store): a few LDS round trips per move instead of a dependent chain per
+  // neighbour.
   __device__ void recount_libs() {
     const int P_ = P();
+    int nb[NPL][4];
+    uint8_t cp[NPL];
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      const int p = lane + 64 * k;
+      const bool in = p < P_;
+      cp[k] = in ? L->cell[p] : (uint8_t)0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) nb[k][i] = in ? orth(p, i) : -1;
+    }
+    uint8_t cq[NPL][4];
+#pragma unroll
+    for (int k = 0; k < NPL; ++k)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) cq[k][i] = nb[k][i] >= 0 ? (uint8_t)(L->cell[nb[k][i]] & 3) : 0;
+    int lq[NPL][4], lp[NPL];
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      const int p = lane + 64 * k;
+      const bool empty = p < P_ && !(cp[k] & 3);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) lq[k][i] = (empty && cq[k][i]) ? (int)L->lab[nb[k][i]] : -1;
+      lp[k] = (p < P_ && (cp[k] & 3)) ? (int)L->lab[p] : -1;
+    }
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
       const int p = lane + 64 * k;
@@ -147,32 +174,25 @@ struct Game {
     wave_sync();
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
-      const int p = lane + 64 * k;
-      if (p >= P_ || (L->cell[p] & 3)) continue;
-      int seen[4];
-      int ns = 0;
+#pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int q = orth(p, i);
-        if (q < 0 || !(L->cell[q] & 3)) continue;
-        const int l = L->lab[q];
-        bool dup = false;
-        for (int j = 0; j < ns; ++j) dup |= seen[j] == l;
-        if (!dup) {
-          seen[ns++] = l;
-          atomicAdd(&L->lib[l], 1);
-        }
+        const int l = lq[k][i];
+        bool dup = l < 0;
+#pragma unroll
+        for (int j = 0; j < i; ++j) dup |= lq[k][j] == l;
+        if (!dup) atomicAdd(&L->lib[l], 1);
       }
     }
     wave_sync();
+    int lv[NPL];
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) lv[k] = lp[k] >= 0 ? L->lib[lp[k]] : 0;
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
+      if (lp[k] < 0) continue;
       const int p = lane + 64 * k;
-      if (p >= P_) continue;
-      const uint8_t old = L->cell[p];
-      const uint8_t c = old & 3;
-      if (!c) continue;
-      const uint8_t nc = (uint8_t)(c | (min(L->lib[L->lab[p]], 3) << 2));
-      if (nc != old) {
+      const uint8_t nc = (uint8_t)((cp[k] & 3) | (min(lv[k], 3) << 2));
+      if (nc != cp[k]) {
         L->cell[p] = nc;
         L->chg[p] = 1;
       }
@@ -180,29 +200,12 @@ struct Game {
     wave_sync();
   }
 
-  // base logit of p for both players (everything but the last-move terms)
-  __device__ void compute_base(int p, const float* __restrict__ w,
-                               const float* __restrict__ pattern) {
+  // base logit (everything but the last-move terms) for both players from the packed 3x3
+  // neighbourhood r (cells of ring slots 0..7, one byte each) and the two pattern weights
+  __device__ __forceinline__ void base_from(int p, uint64_t r8, float patb, float patw,
+                                            const float* __restrict__ w) {
     const int s = S();
     const int x = p / s, y = p - (p / s) * s;
-    if (L->cell[p] & 3) {
-      L->base[0][p] = -INFINITY;
-      L->base[1][p] = -INFINITY;
-      return;
-    }
-    uint8_t r[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int q = ring[p][k];
-      r[k] = q < 0 ? kOff : L->cell[q];
-    }
-    int pb = 0, pw = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int c = r[k] & 3;
-      pb |= c << (2 * k);
-      pw |= ((c == 1 || c == 2) ? 3 - c : c) << (2 * k);
-    }
     const bool edge = x == 0 || y == 0 || x == s - 1 || y == s - 1;
 #pragma unroll
     for (int own = 1; own <= 2; ++own) {
@@ -211,10 +214,11 @@ struct Game {
       bool capture = false, own_atari = false, own_multi = false;
 #pragma unroll
       for (int k = 0; k < 8; k += 2) {
-        const int c = r[k] & 3;
+        const int rk = (int)((r8 >> (8 * k)) & 0xff);
+        const int c = rk & 3;
         if (c == kOff) continue;
         ++nnb;
-        const int lc = r[k] >> 2;
+        const int lc = rk >> 2;
         if (c == 0) {
           ++empty_nb;
         } else if (c == own) {
@@ -231,12 +235,12 @@ struct Game {
       if (own_nb == nnb) {  // own single-point eye
         int bad = 0;
 #pragma unroll
-        for (int k = 1; k < 8; k += 2) bad += (r[k] & 3) == opp;
+        for (int k = 1; k < 8; k += 2) bad += (int)((r8 >> (8 * k)) & 3) == opp;
         if (nnb < 4 ? bad == 0 : bad <= 1) cand = false;
       }
       if (empty_nb == 0 && !own_multi && !capture) cand = false;  // suicide
       if (cand) {
-        v = pattern ? pattern[own == 1 ? pb : pw] : 0.f;
+        v = own == 1 ? patb : patw;
         if (edge) v += w[6];
         if (capture) v += w[2];
         if (own_atari && (empty_nb >= 2 || capture)) v += w[1];
@@ -248,28 +252,105 @@ struct Game {
     }
   }
 
-  // mark the 3x3 neighbourhoods of changed cells dirty, recompute their bases, clear the flags
+  // pattern indices (2 bits per ring slot) of a packed neighbourhood, black and white to move
+  __device__ __forceinline__ void pattern_idx(uint64_t r8, int& pb, int& pw) const {
+    pb = 0;
+    pw = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = (int)((r8 >> (8 * k)) & 3);
+      pb |= c << (2 * k);
+      pw |= ((c == 1 || c == 2) ? 3 - c : c) << (2 * k);
+    }
+  }
+
+  // gather the packed 3x3 neighbourhood of p (off-board slots = kOff)
+  __device__ __forceinline__ uint64_t gather(int p) const {
+    int q[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) q[k] = ring[p][k];
+    uint64_t r8 = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      r8 |= (uint64_t)(q[k] < 0 ? kOff : L->cell[q[k]]) << (8 * k);
+    return r8;
+  }
+
+  __device__ void compute_base(int p, const float* __restrict__ w,
+                               const float* __restrict__ pattern) {
+    if (L->cell[p] & 3) {
+      L->base[0][p] = -INFINITY;
+      L->base[1][p] = -INFINITY;
+      return;
+    }
+    const uint64_t r8 = gather(p);
+    int pb, pw;
+    pattern_idx(r8, pb, pw);
+    base_from(p, r8, pattern ? pattern[pb] : 0.f, pattern ? pattern[pw] : 0.f, w);
+  }
+
+  // mark the 3x3 neighbourhoods of changed cells dirty, recompute their bases, clear the flags.
+  // The recompute gathers every dirty point's neighbourhood first and then issues all pattern
+  // loads together (one global round trip per move, not one per point).
   __device__ void refresh(const float* __restrict__ w, const float* __restrict__ pattern) {
     const int P_ = P();
+    uint8_t ch[NPL];
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
       const int p = lane + 64 * k;
-      if (p >= P_ || !L->chg[p]) continue;
+      ch[k] = p < P_ ? L->chg[p] : (uint8_t)0;
+    }
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      if (!ch[k]) continue;
+      const int p = lane + 64 * k;
+      int q[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) q[j] = ring[p][j];
       L->dirty[p] = 1;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int q = ring[p][j];
-        if (q >= 0) L->dirty[q] = 1;
-      }
+      for (int j = 0; j < 8; ++j)
+        if (q[j] >= 0) L->dirty[q[j]] = 1;
     }
     wave_sync();
+    uint8_t d[NPL], cs[NPL];
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      const int p = lane + 64 * k;
+      d[k] = p < P_ ? L->dirty[p] : (uint8_t)0;
+      cs[k] = p < P_ ? L->cell[p] : (uint8_t)0;
+    }
+    uint64_t r8[NPL];
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      const int p = lane + 64 * k;
+      r8[k] = (d[k] && !(cs[k] & 3)) ? gather(p) : 0;
+    }
+    float pv[NPL][2];
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      pv[k][0] = pv[k][1] = 0.f;
+      if (d[k] && !(cs[k] & 3) && pattern) {
+        int pb, pw;
+        pattern_idx(r8[k], pb, pw);
+        pv[k][0] = pattern[pb];
+        pv[k][1] = pattern[pw];
+      }
+    }
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
       const int p = lane + 64 * k;
       if (p >= P_) continue;
-      if (L->dirty[p]) compute_base(p, w, pattern);
-      L->dirty[p] = 0;
-      L->chg[p] = 0;
+      if (d[k]) {
+        if (cs[k] & 3) {
+          L->base[0][p] = -INFINITY;
+          L->base[1][p] = -INFINITY;
+        } else {
+          base_from(p, r8[k], pv[k][0], pv[k][1], w);
+        }
+        L->dirty[p] = 0;
+      }
+      if (ch[k]) L->chg[p] = 0;
     }
     wave_sync();
   }
@@ -384,36 +465,50 @@ rollout_kernel(const int8_t* __restrict__ colors, const int32_t* __restrict__ me
     ko = -1;
     if (mv >= 0) {
       // wave-uniform bookkeeping (every lane reads the same LDS words)
+      int nq[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) nq[i] = g.orth(mv, i);
+      uint8_t cq4[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) cq4[i] = nq[i] >= 0 ? L.cell[nq[i]] : (uint8_t)0;
+      int lq4[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) lq4[i] = (cq4[i] & 3) ? (int)L.lab[nq[i]] : -1;
       int cap_l[4], own_l[4];
       int ncap = 0, nown = 0, cap_pt = -1;
+#pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int q = g.orth(mv, i);
-        if (q < 0) continue;
-        const uint8_t cq = L.cell[q];
-        if (!(cq & 3)) continue;
-        const int l = L.lab[q];
-        if ((cq & 3) == own) {
+        if (!(cq4[i] & 3)) continue;
+        const int l = lq4[i];
+        if ((cq4[i] & 3) == own) {
           bool dup = false;
           for (int j = 0; j < nown; ++j) dup |= own_l[j] == l;
           if (!dup) own_l[nown++] = l;
-        } else if ((cq >> 2) == 1) {
+        } else if ((cq4[i] >> 2) == 1) {
           bool dup = false;
           for (int j = 0; j < ncap; ++j) dup |= cap_l[j] == l;
           if (!dup) {
             cap_l[ncap++] = l;
-            cap_pt = q;
+            cap_pt = nq[i];
           }
         }
       }
       wave_sync();
       int removed = 0;
+      uint8_t cc[NPL];
+      int lc[NPL];
 #pragma unroll
       for (int k = 0; k < NPL; ++k) {
         const int p = lane + 64 * k;
-        if (p >= P) continue;
-        const int c = L.cell[p] & 3;
+        cc[k] = p < P ? (uint8_t)(L.cell[p] & 3) : (uint8_t)0;
+        lc[k] = cc[k] ? (int)L.lab[p] : -1;
+      }
+#pragma unroll
+      for (int k = 0; k < NPL; ++k) {
+        const int c = cc[k];
         if (!c) continue;
-        const int l = L.lab[p];
+        const int p = lane + 64 * k;
+        const int l = lc[k];
         if (c != own) {
           bool hit = false;
           for (int j = 0; j < ncap; ++j) hit |= cap_l[j] == l;
