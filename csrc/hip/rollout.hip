@@ -18,8 +18,9 @@
 //     move instead of all 361; the 256 KB pattern table is only read for those;
 //   * per move every lane then just reads its points' cached bases, adds the last-move features
 //     and Gumbel noise, and one wave-wide argmax picks the move;
-//   * neighbour indices come from a block-shared LDS table; the board edge is a template
-//     constant for 19x19 / 13x13 / 9x9.
+//   * neighbour indices are computed (p +- 1, p +- S with edge tests; the board size is a template
+//     constant for 19x19 / 13x13 / 9x9) instead of read from an LDS table: fewer LDS instructions
+//     per move and 6 KB less LDS per block (5 -> 6 blocks per CU).
 // A move: place, remove captured groups (opponent neighbours whose count was 1), relabel the
 // merged own groups to the new stone, recount liberties (each empty point adds 1 to each distinct
 // neighbouring label, LDS atomics), refresh the cells and mark changed neighbourhoods dirty.
@@ -47,9 +48,12 @@ struct GameLds {
 
 template <int PM>
 struct BlockLds {
-  int16_t ring[PM][8];  // clockwise from north ((x, y+1) first), -1 off board
   GameLds<PM> g[kWaves];
 };
+
+// ring slot k of the 3x3 neighbourhood, clockwise from north ((x, y+1) first)
+__device__ constexpr int kDx[8] = {0, 1, 1, 1, 0, -1, -1, -1};
+__device__ constexpr int kDy[8] = {1, 1, 0, -1, -1, -1, 0, 1};
 
 __device__ __forceinline__ uint32_t hash32(uint32_t x) {
   x ^= x >> 16;
@@ -96,13 +100,19 @@ template <int SC, int NPL, int PM>
 struct Game {
   int S_rt;
   GameLds<PM>* L;
-  const int16_t (*ring)[8];
   int lane;
 
   __device__ __forceinline__ int S() const { return SC > 0 ? SC : S_rt; }
   __device__ __forceinline__ int P() const { return S() * S(); }
-  // orthogonal neighbours are ring slots 0 (N), 2 (E), 4 (S), 6 (W); diagonals 1, 3, 5, 7
-  __device__ __forceinline__ int orth(int p, int i) const { return ring[p][2 * i]; }
+  // neighbour in ring slot k of p (-1 off board); orthogonal neighbours are ring slots 0 (N),
+  // 2 (E), 4 (S), 6 (W), diagonals 1, 3, 5, 7
+  __device__ __forceinline__ int ring(int p, int k) const {
+    const int s = S();
+    const int x = p / s, y = p - x * s;
+    const int ax = x + kDx[k], ay = y + kDy[k];
+    return (ax < 0 || ay < 0 || ax >= s || ay >= s) ? -1 : p + kDx[k] * s + kDy[k];
+  }
+  __device__ __forceinline__ int orth(int p, int i) const { return ring(p, 2 * i); }
 
   __device__ void init_labels() {
     const int P_ = P();
@@ -268,7 +278,7 @@ struct Game {
   __device__ __forceinline__ uint64_t gather(int p) const {
     int q[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) q[k] = ring[p][k];
+    for (int k = 0; k < 8; ++k) q[k] = ring(p, k);
     uint64_t r8 = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k)
@@ -306,7 +316,7 @@ struct Game {
       const int p = lane + 64 * k;
       int q[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) q[j] = ring[p][j];
+      for (int j = 0; j < 8; ++j) q[j] = ring(p, j);
       L->dirty[p] = 1;
 #pragma unroll
       for (int j = 0; j < 8; ++j)
@@ -358,33 +368,20 @@ struct Game {
 
 // meta: [cur, ko, last1, last2, passes_b, passes_w, nmoves, end]
 template <int SC, int NPL, int PM>
-__global__ void __launch_bounds__(256)
-rollout_kernel(const int8_t* __restrict__ colors, const int32_t* __restrict__ meta, int n_pos,
-               int R, int S_rt, float komi, int limit, const float* __restrict__ w,
-               const float* __restrict__ pattern, uint32_t seed, int8_t* __restrict__ winner,
-               int16_t* __restrict__ length, float* __restrict__ dbg_logits) {
-  __shared__ BlockLds<PM> sh;
+__device__ __forceinline__ void rollout_body(
+    BlockLds<PM>& sh, const int8_t* __restrict__ colors, const int32_t* __restrict__ meta,
+    int n_pos, int R, int S_rt, float komi, int limit, const float* __restrict__ w,
+    const float* __restrict__ pattern, uint32_t seed, int8_t* __restrict__ winner,
+    int16_t* __restrict__ length, float* __restrict__ dbg_logits) {
   const int S = SC > 0 ? SC : S_rt;
   const int P = S * S;
-  // block-shared neighbour table (before any wave may leave)
-  for (int p = threadIdx.x; p < P; p += blockDim.x) {
-    const int x = p / S, y = p - (p / S) * S;
-    const int dx[8] = {0, 1, 1, 1, 0, -1, -1, -1}, dy[8] = {1, 1, 0, -1, -1, -1, 0, 1};
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int ax = x + dx[k], ay = y + dy[k];
-      sh.ring[p][k] = (ax < 0 || ay < 0 || ax >= S || ay >= S) ? (int16_t)-1
-                                                                : (int16_t)(ax * S + ay);
-    }
-  }
-  __syncthreads();
   const int wv = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const int game = blockIdx.x * kWaves + wv;
   if (game >= n_pos * R) return;  // whole wave exits together
   const int pos = game / R;
   GameLds<PM>& L = sh.g[wv];
-  Game<SC, NPL, PM> g{S_rt, &L, sh.ring, lane};
+  Game<SC, NPL, PM> g{S_rt, &L, lane};
   float wl[7];
 #pragma unroll
   for (int i = 0; i < 7; ++i) wl[i] = w[i];
@@ -474,24 +471,19 @@ rollout_kernel(const int8_t* __restrict__ colors, const int32_t* __restrict__ me
       int lq4[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) lq4[i] = (cq4[i] & 3) ? (int)L.lab[nq[i]] : -1;
+      // one slot per neighbour (-1 = none): membership tests need no de-duplication, and fixed
+      // slots keep the arrays in registers (a running count index would put them in scratch)
       int cap_l[4], own_l[4];
-      int ncap = 0, nown = 0, cap_pt = -1;
+      int cap_pt = -1;
+      bool any_own = false;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        if (!(cq4[i] & 3)) continue;
-        const int l = lq4[i];
-        if ((cq4[i] & 3) == own) {
-          bool dup = false;
-          for (int j = 0; j < nown; ++j) dup |= own_l[j] == l;
-          if (!dup) own_l[nown++] = l;
-        } else if ((cq4[i] >> 2) == 1) {
-          bool dup = false;
-          for (int j = 0; j < ncap; ++j) dup |= cap_l[j] == l;
-          if (!dup) {
-            cap_l[ncap++] = l;
-            cap_pt = nq[i];
-          }
-        }
+        const int c = cq4[i] & 3;
+        own_l[i] = c == own ? lq4[i] : -1;
+        const bool cap = c && c != own && (cq4[i] >> 2) == 1;
+        cap_l[i] = cap ? lq4[i] : -1;
+        if (cap) cap_pt = nq[i];  // only used when exactly one stone is captured
+        any_own |= c == own;
       }
       wave_sync();
       int removed = 0;
@@ -511,7 +503,8 @@ rollout_kernel(const int8_t* __restrict__ colors, const int32_t* __restrict__ me
         const int l = lc[k];
         if (c != own) {
           bool hit = false;
-          for (int j = 0; j < ncap; ++j) hit |= cap_l[j] == l;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) hit |= cap_l[j] == l;
           if (hit) {
             L.cell[p] = 0;
             L.lab[p] = -1;
@@ -520,7 +513,8 @@ rollout_kernel(const int8_t* __restrict__ colors, const int32_t* __restrict__ me
           }
         } else {
           bool hit = false;
-          for (int j = 0; j < nown; ++j) hit |= own_l[j] == l;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) hit |= own_l[j] == l;
           if (hit) L.lab[p] = (int16_t)mv;
         }
       }
@@ -533,7 +527,7 @@ rollout_kernel(const int8_t* __restrict__ colors, const int32_t* __restrict__ me
       g.recount_libs();
       removed = wave_sum_i(removed);
       // ko: one stone captured by a lone stone that is left with a single liberty
-      if (removed == 1 && nown == 0 && L.lib[mv] == 1) ko = cap_pt;
+      if (removed == 1 && !any_own && L.lib[mv] == 1) ko = cap_pt;
       g.refresh(wl, pattern);
     } else {
       if (cur == 1) ++pb;
@@ -579,12 +573,49 @@ rollout_kernel(const int8_t* __restrict__ colors, const int32_t* __restrict__ me
   }
 }
 
+#define RAG_RO_ARGS                                                                              \
+  const int8_t *__restrict__ colors, const int32_t *__restrict__ meta, int n_pos, int R, int S_rt, \
+      float komi, int limit, const float *__restrict__ w, const float *__restrict__ pattern,       \
+      uint32_t seed, int8_t *__restrict__ winner, int16_t *__restrict__ length,                    \
+      float *__restrict__ dbg_logits
+#define RAG_RO_FWD colors, meta, n_pos, R, S_rt, komi, limit, w, pattern, seed, winner, length, dbg_logits
+
+// The same playout body at two register budgets: the compiler's choice (146 VGPRs for 19x19,
+// 3 waves per SIMD) and a cap at 128 VGPRs (4 waves per SIMD, a few spills outside the move
+// loop). RAG_ROLLOUT_WPE=3|4 picks one (default measured: see docs/KERNELS.md).
+template <int SC, int NPL, int PM>
+__global__ void __launch_bounds__(256) rollout_kernel(RAG_RO_ARGS) {
+  __shared__ BlockLds<PM> sh;
+  rollout_body<SC, NPL, PM>(sh, RAG_RO_FWD);
+}
+
+template <int SC, int NPL, int PM>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+rollout_kernel_w4(RAG_RO_ARGS) {
+  __shared__ BlockLds<PM> sh;
+  rollout_body<SC, NPL, PM>(sh, RAG_RO_FWD);
+}
+
+int rollout_wpe() {
+  static const int v = [] {
+    const char* e = getenv("RAG_ROLLOUT_WPE");
+    return e ? atoi(e) : 4;
+  }();
+  return v;
+}
+
 template <int SC, int NPL, int PM>
 void launch(dim3 grid, hipStream_t st, const int8_t* c, const int32_t* meta, int n_pos, int R,
             int S, float komi, int limit, const float* w, const float* pattern, unsigned seed,
             void* winner, void* length, float* dbg) {
-  rollout_kernel<SC, NPL, PM><<<grid, 256, 0, st>>>(c, meta, n_pos, R, S, komi, limit, w, pattern,
-                                                    seed, (int8_t*)winner, (int16_t*)length, dbg);
+  if (rollout_wpe() == 4)
+    rollout_kernel_w4<SC, NPL, PM><<<grid, 256, 0, st>>>(c, meta, n_pos, R, S, komi, limit, w,
+                                                         pattern, seed, (int8_t*)winner,
+                                                         (int16_t*)length, dbg);
+  else
+    rollout_kernel<SC, NPL, PM><<<grid, 256, 0, st>>>(c, meta, n_pos, R, S, komi, limit, w,
+                                                      pattern, seed, (int8_t*)winner,
+                                                      (int16_t*)length, dbg);
 }
 
 }  // namespace

@@ -72,6 +72,28 @@ def test_rollout_outcomes_match_native_statistics(gro):
     assert abs(lg.mean() - np.mean(lens)) < 0.1 * np.mean(lens)
 
 
+def test_rollouts_bit_exact_vs_recorded_run():
+    """Winners, lengths and initial logits of fixed positions + seed equal a run recorded on an
+    MI355X before the kernel's latency rewrites (scripts/dbg/rollout_ref.py; 384 positions x 4
+    playouts): the rewrites must not change a single game."""
+    import os
+    import sys
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "scripts", "dbg"))
+    from rollout_ref import states
+    from rocalphago_amd.search.gpu_rollout import GpuRollouts
+    sts, rp = states()
+    gr = GpuRollouts(rp, torch.device("cuda"))
+    w, ln = gr.run(sts, R=4, limit=500, seed=123)
+    lg = gr.initial_logits(sts[:64])
+    ref = np.load(os.path.join(root, "profiles", "rollout_ref.npz"))
+    assert np.array_equal(ref["w"], w)
+    assert np.array_equal(ref["ln"], ln)
+    assert np.array_equal(ref["lg"], lg)
+
+
 def test_gpu_rollouts_in_search_find_capture(gro):
     from rocalphago_amd.search.apv import ParallelMCTS
     import sys
