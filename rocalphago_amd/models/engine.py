@@ -413,7 +413,8 @@ class PolicyHeadEngine(object):
 
 
 class ValueHeadEngine(object):
-    """1x1 conv (K->1) on HIP; Dense(S*S->H) + act; Dense(H->1) + tanh via torch GEMMs."""
+    """1x1 conv (K->1) on HIP; Dense(S*S->H) + act; Dense(H->1) + tanh: inference through the
+    fused value_mlp_fwd HIP kernel (fused.ValuePlan.forward), training through torch GEMMs."""
 
     def __init__(self, trunk, K):
         self.trunk = trunk

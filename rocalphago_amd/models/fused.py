@@ -193,7 +193,11 @@ class ValuePlan(_TrunkPlan):
         self.trunk.forward(B)
         w, b0 = self.head_params()
         z = self.head.conv_out(B, w, b0)
-        return self._mlp(z, self._dense_params())
+        W1, b1, W2, b2 = self._dense_params()
+        if self.act1 in ops.MLP_ACTS:
+            # inference: one fused HIP kernel instead of two library GEMMs + elementwise ops
+            return ops.value_mlp_fwd(z, W1, b1, W2, b2, act=self.act1)
+        return self._mlp(z, (W1, b1, W2, b2))
 
     def train_step(self, x, y, loss, sw=None, want_acc=False, index=None, transforms=None):
         if loss not in ("mse", "mean_squared_error"):

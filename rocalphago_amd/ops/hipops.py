@@ -230,6 +230,36 @@ def head_linear(h, w, b0, z, K):
            "head_linear")
 
 
+MLP_ACTS = {"linear": 0, "relu": 1, "tanh": 2}
+_mlp_ws = {}
+
+
+def value_mlp_fwd(z, W1, b1, W2, b2, act="linear", out=None):
+    """tanh(act(z @ W1 + b1) @ W2 + b2) for fp32 z [B, P], W1 [P, H], W2 [H, 1] -> [B, 1]."""
+    B, P = z.shape
+    H = W1.shape[1]
+    if (W1.shape != (P, H) or b1.numel() != H or W2.numel() != H or b2.numel() != 1
+            or act not in MLP_ACTS):
+        raise ValueError("value_mlp_fwd: bad shapes/activation %s %s %s" %
+                         (tuple(z.shape), tuple(W1.shape), act))
+    for t in (z, W1, b1, W2, b2):
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError("value_mlp_fwd expects contiguous fp32 tensors")
+    if out is None:
+        out = torch.empty((B, 1), dtype=torch.float32, device=z.device)
+    need = _lib().rag_value_mlp_workspace(B, H)
+    stream = _stream()
+    key = (z.device, stream.value)  # per stream: pipelined evaluations may run concurrently
+    work = _mlp_ws.get(key)
+    if work is None or work.numel() < need:
+        work = torch.empty(need, dtype=torch.float32, device=z.device)
+        _mlp_ws[key] = work
+    _check(_lib().rag_value_mlp_fwd(_ptr(z), _ptr(W1), _ptr(b1), _ptr(W2), _ptr(b2), _ptr(out),
+                                    _ptr(work), B, P, H, MLP_ACTS[act], stream),
+           "value_mlp_fwd")
+    return out
+
+
 def sample_moves(probs, mask, beta=1.0, greedy=None, seed=0, out=None):
     """Per row: a move drawn from probs^beta restricted to ``mask`` (uint8 [B, >=P]), or the
     masked argmax where ``greedy`` (uint8 [B]) is set; -1 for rows without candidates

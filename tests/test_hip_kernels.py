@@ -244,3 +244,22 @@ def test_packed_dataset_training_matches_plain(ops):
             tr.step(torch.arange(s * 16, s * 16 + 32, device="cuda") % 64)
         losses.append(tr.pop_metrics()[0])
     assert abs(losses[0] - losses[1]) < 1e-5
+
+
+@pytest.mark.parametrize("B,P,H,act", [(256, 361, 256, "linear"), (5, 49, 64, "relu"),
+                                       (3, 81, 300, "tanh"), (1, 361, 256, "linear")])
+def test_value_mlp_fwd(ops, B, P, H, act):
+    dev = torch.device("cuda")
+    torch.manual_seed(3)
+    z = torch.randn(B, P, device=dev)
+    W1 = torch.randn(P, H, device=dev) * 0.05
+    b1 = torch.randn(H, device=dev) * 0.1
+    W2 = torch.randn(H, 1, device=dev) * 0.1
+    b2 = torch.randn(1, device=dev) * 0.1
+    h = z.double() @ W1.double() + b1.double()
+    h = {"linear": h, "relu": torch.relu(h), "tanh": torch.tanh(h)}[act]
+    ref = torch.tanh(h @ W2.double() + b2.double()).float()
+    out = ops.value_mlp_fwd(z, W1, b1, W2, b2, act=act)
+    torch.cuda.synchronize()
+    assert out.shape == (B, 1)
+    assert (out - ref).abs().max().item() < 1e-4
