@@ -232,7 +232,8 @@ constexpr int kMlpWaves = 8;
 __global__ void __launch_bounds__(64 * kMlpWaves)
 value_mlp_part_kernel(const float* __restrict__ z, const float* __restrict__ W1,
                       const float* __restrict__ b1, const float* __restrict__ W2,
-                      float* __restrict__ part, int B, int P, int H, int act) {
+                      float* __restrict__ part, float* __restrict__ hout, int B, int P, int H,
+                      int act) {
   extern __shared__ float zs[];  // [kMlpRows][P], then [kMlpWaves][kMlpRows][64] partials
   float* red = zs + kMlpRows * P;
   const int ntile = (H + kMlpCols - 1) / kMlpCols;
@@ -279,6 +280,7 @@ value_mlp_part_kernel(const float* __restrict__ z, const float* __restrict__ W1,
     float v = 0.f;
     if (j < H) {
       h += b1[j];
+      if (hout && r < nr) hout[(size_t)(b0 + r) * H + j] = h;  // pre-activation, for training
       if (act == 1) h = h > 0.f ? h : 0.f;
       else if (act == 2) h = tanhf(h);
       v = h * W2[j];
@@ -356,8 +358,8 @@ RAG_API size_t rag_value_mlp_workspace(int B, int H) {
 }
 
 RAG_API int rag_value_mlp_fwd(const float* z, const float* W1, const float* b1, const float* W2,
-                              const float* b2, float* out, float* work, int B, int P, int H,
-                              int act, hipStream_t stream) {
+                              const float* b2, float* out, float* work, float* hout, int B,
+                              int P, int H, int act, hipStream_t stream) {
   // work: >= rag_value_mlp_workspace(B, H) floats
   if (B <= 0) return 0;
   static_assert(kMlpRows <= kMlpWaves, "one wave per board in the epilogue");
@@ -365,7 +367,8 @@ RAG_API int rag_value_mlp_fwd(const float* z, const float* W1, const float* b1, 
   if (sm > 64 * 1024) return -1;
   const int ntile = (H + kMlpCols - 1) / kMlpCols;
   const int nblk = (B + kMlpRows - 1) / kMlpRows * ntile;
-  value_mlp_part_kernel<<<nblk, 64 * kMlpWaves, sm, stream>>>(z, W1, b1, W2, work, B, P, H, act);
+  value_mlp_part_kernel<<<nblk, 64 * kMlpWaves, sm, stream>>>(z, W1, b1, W2, work, hout, B, P, H,
+                                                              act);
   value_mlp_out_kernel<<<(B + 255) / 256, 256, 0, stream>>>(work, b2, out, B, ntile);
   return (int)hipGetLastError();
 }

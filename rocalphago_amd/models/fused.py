@@ -178,7 +178,9 @@ class ValuePlan(_TrunkPlan):
 
     def _mlp(self, z, params):
         W1, b1, W2, b2 = params
-        h = z @ W1 + b1
+        return self._mlp_tail(z @ W1 + b1, W2, b2)
+
+    def _mlp_tail(self, h, W2, b2):
         if self.act1 == "relu":
             h = torch.relu(h)
         elif self.act1 == "tanh":
@@ -209,20 +211,29 @@ class ValuePlan(_TrunkPlan):
     def fwd_bwd(self, B, y, sw=None):
         self.trunk.forward(B, training=True)
         w, b0 = self.head_params()
-        z = self.head.conv_out(B, w, b0).detach().requires_grad_()
-        params = [p.detach().requires_grad_() for p in self._dense_params()]
-        v = self._mlp(z, params)
+        z = self.head.conv_out(B, w, b0)
+        W1, b1, W2, b2 = self._dense_params()
+        # z @ W1 + b1 on the value-MLP HIP kernel (a library GEMM puts this 256 x 256 output on
+        # one workgroup); autograd from the pre-activation on; dW1 / db1 / dz by hand below.
+        h = torch.empty((B, W1.shape[1]), dtype=torch.float32, device=z.device)
+        ops.value_mlp_fwd(z, W1, b1, W2, b2, act=self.act1, hout=h)
+        h.requires_grad_()
+        W2p, b2p = W2.detach().requires_grad_(), b2.detach().requires_grad_()
+        v = self._mlp_tail(h, W2p, b2p)
         per = ((v - y) ** 2).mean(-1)
         if sw is not None:
             per = per * sw / (sw != 0).float().mean().clamp_min(1e-12)
         lossv = per.mean()
-        grads = torch.autograd.grad(lossv, [z] + params)
-        dg = self.net.grads_of(self.d1) + self.net.grads_of(self.d2)
+        dh, dW2, db2 = torch.autograd.grad(lossv, [h, W2p, b2p])
+        gW1, gb1, gW2, gb2 = self.net.grads_of(self.d1) + self.net.grads_of(self.d2)
         with torch.no_grad():
-            for gv, g in zip(dg, grads[1:]):
-                gv.copy_(g)
+            gW1.copy_(z.t() @ dh)
+            gb1.copy_(dh.sum(0))
+            gW2.copy_(dW2)
+            gb2.copy_(db2)
+            dz = dh @ W1.t()
         dw, db0 = self.head_grads()
-        self.head.backward_conv(B, w, grads[0], dw, db0)
+        self.head.backward_conv(B, w, dz, dw, db0)
         dWs, dbs = self._grads()
         self.trunk.backward(B, dWs, dbs)
         return lossv.detach()

@@ -24,7 +24,7 @@ SIGNATURES = {
     "rag_head_bwd": [P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "rag_head_bwd_workspace": [I, I, I],
     "rag_head_linear": [P, P, P, P, I, I, I, I, P],
-    "rag_value_mlp_fwd": [P, P, P, P, P, P, P, I, I, I, I, P],
+    "rag_value_mlp_fwd": [P, P, P, P, P, P, P, P, I, I, I, I, P],
     "rag_value_mlp_workspace": [I, I],
     # optim.hip
     "rag_sgd": [P, P, P, I64, F, F, F, I, P],

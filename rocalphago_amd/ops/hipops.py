@@ -234,8 +234,9 @@ MLP_ACTS = {"linear": 0, "relu": 1, "tanh": 2}
 _mlp_ws = {}
 
 
-def value_mlp_fwd(z, W1, b1, W2, b2, act="linear", out=None):
-    """tanh(act(z @ W1 + b1) @ W2 + b2) for fp32 z [B, P], W1 [P, H], W2 [H, 1] -> [B, 1]."""
+def value_mlp_fwd(z, W1, b1, W2, b2, act="linear", out=None, hout=None):
+    """tanh(act(z @ W1 + b1) @ W2 + b2) for fp32 z [B, P], W1 [P, H], W2 [H, 1] -> [B, 1].
+    ``hout`` (fp32 [B, H], optional) receives the pre-activation z @ W1 + b1 (training)."""
     B, P = z.shape
     H = W1.shape[1]
     if (W1.shape != (P, H) or b1.numel() != H or W2.numel() != H or b2.numel() != 1
@@ -245,6 +246,9 @@ def value_mlp_fwd(z, W1, b1, W2, b2, act="linear", out=None):
     for t in (z, W1, b1, W2, b2):
         if t.dtype != torch.float32 or not t.is_contiguous():
             raise ValueError("value_mlp_fwd expects contiguous fp32 tensors")
+    if hout is not None and (hout.shape != (B, H) or hout.dtype != torch.float32
+                             or not hout.is_contiguous()):
+        raise ValueError("value_mlp_fwd: hout must be contiguous fp32 [B, H]")
     if out is None:
         out = torch.empty((B, 1), dtype=torch.float32, device=z.device)
     need = _lib().rag_value_mlp_workspace(B, H)
@@ -255,7 +259,7 @@ def value_mlp_fwd(z, W1, b1, W2, b2, act="linear", out=None):
         work = torch.empty(need, dtype=torch.float32, device=z.device)
         _mlp_ws[key] = work
     _check(_lib().rag_value_mlp_fwd(_ptr(z), _ptr(W1), _ptr(b1), _ptr(W2), _ptr(b2), _ptr(out),
-                                    _ptr(work), B, P, H, MLP_ACTS[act], stream),
+                                    _ptr(work), _ptr(hout), B, P, H, MLP_ACTS[act], stream),
            "value_mlp_fwd")
     return out
 
