@@ -42,7 +42,8 @@ def main():
     ap.add_argument("--batch", type=int, default=256, help="positions per GPU per step")
     ap.add_argument("--filters", type=int, default=None,
                     help="default 192 (policy/value), 128 (resnet, ResnetPolicy's default)")
-    ap.add_argument("--layers", type=int, default=None, help="default 12 (policy/value), 20 (resnet)")
+    ap.add_argument("--layers", type=int, default=None,
+                    help="default 12 (policy/value), 20 (resnet)")
     ap.add_argument("--dataset", type=int, default=65536, help="synthetic positions per GPU")
     ap.add_argument("--model", default="policy", choices=["policy", "value", "resnet"],
                     help="policy: SL policy net (headline); value: value net (BASELINE config 4); "

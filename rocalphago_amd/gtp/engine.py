@@ -453,7 +453,8 @@ def run_gtp(player_obj, inpt_fn=None, name="Gtp Player", version="0.0", out=None
 def main(argv=None):
     """Serve a policy network (or MCTS over it) on stdin/stdout:
 
-    python -m rocalphago_amd.gtp.engine model.json [--weights W] [--player greedy|probabilistic|mcts]
+    python -m rocalphago_amd.gtp.engine model.json [--weights W] \
+        [--player greedy|probabilistic|mcts]
     """
     import argparse
     ap = argparse.ArgumentParser(description=main.__doc__)

@@ -112,6 +112,11 @@ class _TrunkPlan(object):
         g = self.net.grads_of(self.head_name)
         return g[0].reshape(-1), (g[1] if len(g) > 1 else torch.zeros(1, device=self.net.device))
 
+    def layer_offsets(self):
+        """Start offset (elements) of each trunk conv layer's params in net.flat."""
+        base = self.net.flat.data_ptr()
+        return [(self.net.params_of(n)[0].data_ptr() - base) // 4 for n in self.conv_names]
+
 
 class PolicyPlan(_TrunkPlan):
     def __init__(self, model, convs, head_conv, bias_layer):
@@ -163,11 +168,6 @@ class PolicyPlan(_TrunkPlan):
         dWs, dbs = self._grads()
         self.trunk.backward(B, dWs, dbs, on_layer_done=on_layer_grads)
 
-    def layer_offsets(self):
-        """Start offset (elements) of each trunk conv layer's params in net.flat."""
-        base = self.net.flat.data_ptr()
-        return [(self.net.params_of(n)[0].data_ptr() - base) // 4 for n in self.conv_names]
-
 
 class ValuePlan(_TrunkPlan):
     def __init__(self, model, convs, head_conv, dense1, dense2):
@@ -208,7 +208,7 @@ class ValuePlan(_TrunkPlan):
         lossv = self.fwd_bwd(B, y.reshape(B, -1), sw)
         return float(lossv), None
 
-    def fwd_bwd(self, B, y, sw=None):
+    def fwd_bwd(self, B, y, sw=None, on_layer_grads=None):
         self.trunk.forward(B, training=True)
         w, b0 = self.head_params()
         z = self.head.conv_out(B, w, b0)
@@ -235,7 +235,7 @@ class ValuePlan(_TrunkPlan):
         dw, db0 = self.head_grads()
         self.head.backward_conv(B, w, dz, dw, db0)
         dWs, dbs = self._grads()
-        self.trunk.backward(B, dWs, dbs)
+        self.trunk.backward(B, dWs, dbs, on_layer_done=on_layer_grads)
         return lossv.detach()
 
 

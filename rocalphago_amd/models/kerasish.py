@@ -1,8 +1,8 @@
 """A minimal, single-backend Keras-1 model surface (SURVEY §2.3 "Keras Model surface").
 
 The reference models are Keras 1.2 objects (policy.py, value.py, nn_util.py) and its trainers call
-into that API (``compile``, ``train_on_batch``, ``fit_generator``, ``save_weights`` ...). This module
-re-creates exactly that surface over our own execution engine:
+into that API (``compile``, ``train_on_batch``, ``fit_generator``, ``save_weights`` ...).
+This module re-creates exactly that surface over our own execution engine:
 
   * the Keras-1 JSON model spec is interpreted (Sequential and functional ``Model``; layers
     Convolution2D, Dense, Flatten, Activation, Bias, BatchNormalization, Merge, InputLayer,
@@ -312,6 +312,11 @@ class KerasNet(torch.nn.Module):
 
     def grads_of(self, lname):
         return [v for (ln, _, _), v in zip(self.weight_names, self._gviews) if ln == lname]
+
+    def buffer_views(self):
+        """Non-trainable state (BatchNorm running averages), as views into ``flat``."""
+        return [v for (_, wname, _), v in zip(self.weight_names, self._views)
+                if "_running_" in wname]
 
     def get_weights(self):
         return [v.detach().cpu().numpy().copy() for v in self._views]
@@ -727,14 +732,21 @@ class Model(object):
         return t.to(self.net.device, non_blocking=True)
 
     def predict(self, X, batch_size=None, verbose=0):
+        """Forward pass in chunks of ``batch_size`` rows (default 1024): the fused plan sizes
+        its activation buffers for one chunk, not for the whole input."""
         plan = self._plan_for()
-        x = self._to_tensor(X)
+        n = len(X)
+        bs = int(batch_size or 1024)
+        outs = []
         with torch.no_grad():
-            if plan is not None:
-                out = plan.forward(x)
-            else:
-                out = self.net.forward(x.float(), training=False)
-        return out.detach().cpu().numpy()
+            for s in range(0, max(n, 1), bs):
+                x = self._to_tensor(X[s:s + bs])
+                if plan is not None:
+                    out = plan.forward(x)
+                else:
+                    out = self.net.forward(x.float(), training=False)
+                outs.append(out.detach().cpu())
+        return torch.cat(outs).numpy() if len(outs) > 1 else outs[0].numpy()
 
     def predict_on_batch(self, X):
         return self.predict(X)

@@ -74,6 +74,29 @@ class DPContext(object):
             else:
                 dist.barrier()
 
+    def sync_buffers_(self, net):
+        """Average the non-trainable running statistics (BatchNorm ``*_running_mean`` /
+        ``*_running_std``) of ``net`` over the ranks. They get no gradient, so without this each
+        replica would keep its own local-batch averages. The running-mean update is linear in
+        the batch mean, so averaging after every step reproduces the global-batch running mean
+        exactly (equal local batches); the running variance becomes the mean of the local
+        variances."""
+        if not self.enabled:
+            return
+        views = net.buffer_views()
+        if not views:
+            return
+        buf = torch.cat([v.reshape(-1) for v in views])
+        dist.all_reduce(buf)
+        buf.div_(self.world)
+        off = 0
+        with torch.no_grad():
+            for v in views:
+                n = v.numel()
+                v.copy_(buf[off:off + n].view_as(v))
+                off += n
+        net.bump()
+
     def max_scalar(self, v):
         if not self.enabled:
             return v
@@ -89,11 +112,13 @@ class DPContext(object):
 class BucketedAllReduce(object):
     """Async all-reduce of a flat gradient buffer in layer-aligned buckets (back to front)."""
 
-    def __init__(self, ctx, flat_grad, layer_offsets, bucket_bytes=4 << 20):
+    def __init__(self, ctx, flat_grad, layer_offsets, bucket_bytes=4 << 20, timer=None):
         """layer_offsets: ascending start offsets (elements) of each trunk layer's params in
-        ``flat_grad``; the tail after the last offset (head params) joins the last bucket."""
+        ``flat_grad``; the tail after the last offset (head params) joins the last bucket.
+        ``timer`` (utils.metrics.CommTimer) brackets the exposed wait in ``finish``."""
         self.ctx = ctx
         self.flat = flat_grad
+        self.timer = timer
         self.handles = []
         n = flat_grad.numel()
         # build buckets from the end: [start, end)
@@ -131,10 +156,14 @@ class BucketedAllReduce(object):
     def finish(self):
         if not self.ctx.enabled:
             return
+        if self.timer is not None:
+            self.timer.start()
         for bi, (s, e) in enumerate(self.bounds):
             if bi not in self._launched:
                 self.handles.append(dist.all_reduce(self.flat[s:e], async_op=True))
         for h in self.handles:
             h.wait()
+        if self.timer is not None:
+            self.timer.stop()
         self.flat.div_(self.ctx.world)
         self.reset()

@@ -85,6 +85,11 @@ def run_n_games(optimizer, learner, opponent, num_games, mock_states=[], mode="p
                 dp=None):
     """Play ``num_games`` learner-vs-opponent games, learn from the learner's moves, return the
     learner's win ratio (reference reinforcement_policy_trainer.py:21-86)."""
+    if mode == "per_game" and dp is not None and dp.enabled:
+        # per-game updates would need one all-reduce per non-empty game, and ranks have
+        # different numbers of them: the collectives cannot pair up
+        raise ValueError("mode='per_game' cannot run data-parallel (WORLD_SIZE > 1); use "
+                         "mode='batched' (one all-reduced REINFORCE update per game batch)")
     board_size = learner.policy.model.input_shape[-1]
     states = [go.GameState(size=board_size) for _ in range(num_games)]
     if mock_states:
@@ -167,6 +172,9 @@ def run_training(cmd_line_args=None):
 
     dp = DPContext()
     mode = args.update or ("batched" if dp.enabled else "per_game")
+    if mode == "per_game" and dp.enabled:
+        raise SystemExit("--update per_game is single-process only (replicas would diverge "
+                         "without a gradient all-reduce); use --update batched with WORLD_SIZE > 1")
     ZEROTH_FILE = "weights.00000.hdf5"
 
     if args.resume:

@@ -25,6 +25,7 @@ from ..io import h5lite
 from ..models import kerasish as K
 from ..models.policy import CNNPolicy
 from ..parallel.dp import BucketedAllReduce, DPContext
+from ..utils.metrics import RankMetrics
 from .data import BOARD_TRANSFORMATIONS, DeviceDataset, transform_ids
 
 
@@ -81,8 +82,9 @@ class SupervisedTrainer(object):
     returns device scalars (loss_sum, hit_sum) without synchronising the host."""
 
     def __init__(self, policy_model, dataset, batch_size, symmetries=None, dp=None,
-                 loss="categorical_crossentropy", seed=0):
+                 loss="categorical_crossentropy", seed=0, metrics=None):
         self.model = policy_model
+        self.metrics = metrics  # utils.metrics.RankMetrics (optional)
         self.ds = dataset
         self.B = batch_size
         self.dp = dp
@@ -95,7 +97,10 @@ class SupervisedTrainer(object):
         self.bucketer = None
         if self.plan is not None and dp is not None and dp.enabled:
             self.bucketer = BucketedAllReduce(dp, policy_model.net.flat_grad,
-                                              self.plan.layer_offsets())
+                                              self.plan.layer_offsets(),
+                                              timer=metrics.comm if metrics else None)
+        # BatchNorm running statistics (ResnetPolicy) are averaged over ranks after each step
+        self.sync_bn = dp is not None and dp.enabled and bool(policy_model.net.buffer_views())
         self.loss_sum = torch.zeros((), device=dataset.device)
         self.hit_sum = torch.zeros((), device=dataset.device)
         self.count = 0
@@ -130,7 +135,11 @@ class SupervisedTrainer(object):
             loss, acc = (r if isinstance(r, list) else (r, 0.0))
             self.loss_sum += loss * n
             self.hit_sum += (acc or 0.0) * n
+        if self.sync_bn:
+            self.dp.sync_buffers_(model.net)
         self.count += n
+        if self.metrics is not None:
+            self.metrics.step_done()
 
     def pop_metrics(self):
         """(mean loss, accuracy) since the last call, averaged over all ranks."""
@@ -145,11 +154,15 @@ class SupervisedTrainer(object):
         return float(t[0] / max(t[2], 1)), float(t[1] / max(t[2], 1))
 
     def evaluate(self, indices, batch=None):
-        """Validation loss/accuracy over dataset rows (no augmentation), all ranks combined."""
+        """Validation loss/accuracy over dataset rows (no augmentation). Under DP each rank
+        evaluates its own strided shard and the sums are all-reduced, so the work is split N
+        ways and every row is counted once."""
         batch = batch or self.B
         model = self.model
         tot = torch.zeros(3, device=self.ds.device)
         noop = torch.zeros(0, dtype=torch.int32, device=self.ds.device)
+        if self.dp is not None and self.dp.enabled:
+            indices = indices[self.dp.rank::self.dp.world]
         for s in range(0, len(indices), batch):
             idx = indices[s:s + batch]
             if self.plan is not None:
@@ -180,7 +193,7 @@ def run_training(cmd_line_args=None):
     parser.add_argument("model", help="Path to a JSON model file (i.e. from CNNPolicy.save_model())")  # noqa: E501
     parser.add_argument("train_data", help="A .h5 file of training data")
     parser.add_argument("out_directory", help="directory where metadata and weights will be saved")
-    parser.add_argument("--minibatch", "-B", help="Size of training data minibatches (per rank). Default: 16", type=int, default=16)  # noqa: E501
+    parser.add_argument("--minibatch", "-B", "--per-gpu-batch", help="Size of training data minibatches (per rank / per GPU; the global batch is this x WORLD_SIZE). Default: 16", type=int, default=16)  # noqa: E501
     parser.add_argument("--epochs", "-E", help="Total number of iterations on the data. Default: 10", type=int, default=10)  # noqa: E501
     parser.add_argument("--epoch-length", "-l", help="Number of training examples considered 'one epoch'. Default: # training data", type=int, default=None)  # noqa: E501
     parser.add_argument("--learning-rate", "-r", help="Learning rate - how quickly the model learns at first. Default: .03", type=float, default=.03)  # noqa: E501
@@ -308,8 +321,9 @@ def run_training(cmd_line_args=None):
         ds = PackedDataset.from_hdf5(dataset, dp.device)
     else:
         ds = DeviceDataset.from_hdf5(dataset, dp.device)
+    rank_metrics = RankMetrics(args.out_directory, dp.rank, dp.world, dp.device)
     trainer = SupervisedTrainer(model, ds, args.minibatch, symmetries, dp,
-                                seed=args.seed or 0)
+                                seed=args.seed or 0, metrics=rank_metrics)
     samples_per_epoch = args.epoch_length or n_train_data
     dev_train = torch.from_numpy(np.asarray(train_indices, dtype=np.int64)).to(dp.device)
     dev_val = torch.from_numpy(np.asarray(val_indices, dtype=np.int64)).to(dp.device)
@@ -335,6 +349,7 @@ def run_training(cmd_line_args=None):
             seen += args.minibatch
         loss, acc = trainer.pop_metrics()
         dt = time.time() - t0
+        rank_metrics.log(epoch=epoch_base + epoch, step=int(sgd.iterations))
         logs = {"loss": loss, "acc": acc}
         if n_val_data > 0:
             vl, va = trainer.evaluate(dev_val)

@@ -25,7 +25,8 @@ from ..models import kerasish as K
 from ..models.value import CNNValue
 from ..parallel.dp import BucketedAllReduce, DPContext
 from .data import transform_ids
-from .supervised import MetadataWriterCallback
+from ..utils.metrics import RankMetrics
+from .supervised import MetadataWriterCallback, _fault_step, _opt_sidecar
 
 
 def generate_value_dataset(player, n_games, out_file=None, board=19, features=VALUE_FEATURES,
@@ -75,7 +76,7 @@ class ValueTrainer(object):
     """Device-resident value-net loop (MSE), shared by run_training and bench.py."""
 
     def __init__(self, value_model, states, values, batch_size, symmetries=None, dp=None,
-                 seed=0):
+                 seed=0, metrics=None):
         self.model = value_model
         self.dev = value_model.device
         self.states = states if isinstance(states, torch.Tensor) else \
@@ -84,6 +85,7 @@ class ValueTrainer(object):
             torch.from_numpy(np.asarray(values, np.float32).reshape(-1, 1)).to(self.dev)
         self.B = batch_size
         self.dp = dp
+        self.metrics = metrics
         self.planes = value_model.input_shape[-3]  # (None,) F, S, S
         self.sym = torch.tensor(transform_ids(symmetries or ["noop"]), dtype=torch.int32,
                                 device=self.dev)
@@ -92,8 +94,11 @@ class ValueTrainer(object):
         self.plan = value_model._plan_for() if self.dev.type == "cuda" else None
         self.bucketer = None
         if self.plan is not None and dp is not None and dp.enabled:
+            # layer-triggered buckets: the all-reduce of the top layers (+ the dense head) runs
+            # while the lower layers' wgrad/dgrad kernels are still queued
             self.bucketer = BucketedAllReduce(dp, value_model.net.flat_grad,
-                                              self.plan.layer_offsets())
+                                              self.plan.layer_offsets(),
+                                              timer=metrics.comm if metrics else None)
         self.loss_sum = torch.zeros((), device=self.dev)
         self.count = 0
 
@@ -105,26 +110,35 @@ class ValueTrainer(object):
         y = self.values[index]
         if self.plan is not None:
             B = self.plan.prepare(self.states, index=index, transforms=tf)
-            loss = self.plan.fwd_bwd(B, y, None)
+            hook = self.bucketer.layer_done if self.bucketer else None
+            loss = self.plan.fwd_bwd(B, y, None, on_layer_grads=hook)
             if self.bucketer:
                 self.bucketer.finish()
             model.optimizer.apply(model.net)
             self.loss_sum += loss * n
         else:
-            from .data import apply_transform_np
-            st = self.states[index]
-            if st.dtype == torch.int64:  # bit-packed (training/replay.py)
-                from .replay import unpack_bits
-                st = unpack_bits(st, self.planes)
-            st = st.cpu().numpy()
-            X = np.stack([apply_transform_np(s, int(t)) for s, t in zip(st, tf.cpu().numpy())])
+            X = self._host_states(index, tf)
             saved = model.grad_allreduce
             if self.dp is not None and self.dp.enabled:
                 model.grad_allreduce = self.dp.allreduce_mean_
-            loss = model.train_on_batch(X.astype(np.float32), y.cpu().numpy())
+            loss = model.train_on_batch(X, y.cpu().numpy())
             model.grad_allreduce = saved
             self.loss_sum += float(loss) * n
         self.count += n
+        if self.metrics is not None:
+            self.metrics.step_done()
+
+    def _host_states(self, index, tf=None):
+        from .data import apply_transform_np
+        st = self.states[index]
+        if st.dtype == torch.int64:  # bit-packed (training/replay.py)
+            from .replay import unpack_bits
+            st = unpack_bits(st, self.planes)
+        st = st.cpu().numpy()
+        if tf is None:
+            return st.astype(np.float32)
+        return np.stack([apply_transform_np(s, int(t))
+                         for s, t in zip(st, tf.cpu().numpy())]).astype(np.float32)
 
     @classmethod
     def from_replay(cls, value_model, buffer, batch_size, symmetries=None, dp=None, seed=0):
@@ -142,6 +156,32 @@ class ValueTrainer(object):
         self.count = 0
         return float(t[0] / max(t[1], 1))
 
+    def evaluate(self, indices, batch=None):
+        """Mean squared error over dataset rows ``indices`` (no augmentation), in minibatch
+        chunks straight from the device-resident uint8 states. Under DP every rank evaluates a
+        strided shard and the (sum, count) pair is all-reduced."""
+        batch = batch or max(self.B, 256)
+        if not isinstance(indices, torch.Tensor):
+            indices = torch.as_tensor(np.asarray(indices, np.int64), device=self.dev)
+        if self.dp is not None and self.dp.enabled:
+            indices = indices[self.dp.rank::self.dp.world]
+        tot = torch.zeros(2, dtype=torch.float64, device=self.dev)
+        with torch.no_grad():
+            for s in range(0, indices.numel(), batch):
+                idx = indices[s:s + batch]
+                y = self.values[idx].reshape(-1).double()
+                if self.plan is not None:
+                    pred = self.plan.forward(self.states, index=idx).reshape(-1).double()
+                else:
+                    pred = torch.as_tensor(self.model.predict(self._host_states(idx)),
+                                           device=self.dev).reshape(-1).double()
+                tot[0] += ((pred - y) ** 2).sum()
+                tot[1] += idx.numel()
+        if self.dp is not None and self.dp.enabled:
+            self.dp.allreduce_sum_(tot)
+        t = tot.cpu().numpy()
+        return float(t[0] / max(t[1], 1))
+
 
 def run_training(cmd_line_args=None):
     import argparse
@@ -149,20 +189,25 @@ def run_training(cmd_line_args=None):
     parser.add_argument("model", help="Path to a CNNValue JSON model file")
     parser.add_argument("train_data", help="HDF5 with 'states' and 'values' (see generate_value_dataset)")  # noqa: E501
     parser.add_argument("out_directory", help="directory where metadata and weights will be saved")
-    parser.add_argument("--minibatch", "-B", type=int, default=32)
+    parser.add_argument("--minibatch", "-B", "--per-gpu-batch", type=int, default=32,
+                        help="positions per rank per step (global batch = this x WORLD_SIZE)")
     parser.add_argument("--epochs", "-E", type=int, default=10)
+    parser.add_argument("--epoch-length", "-l", type=int, default=None,
+                        help="training positions per epoch (default: the training split)")
     parser.add_argument("--learning-rate", "-r", type=float, default=0.003)
     parser.add_argument("--decay", "-d", type=float, default=8.664339379294006e-08)
     parser.add_argument("--train-val-test", nargs=3, type=float, default=[0.93, .05, .02])
     parser.add_argument("--symmetries", default='noop,rot90,rot180,rot270,fliplr,flipud,diag1,diag2')  # noqa: E501
     parser.add_argument("--weights", default=None, help="resume from weights in out_directory")
+    parser.add_argument("--seed", type=int, default=0)
     parser.add_argument("--verbose", "-v", default=False, action="store_true")
     args = parser.parse_args(cmd_line_args)
 
     dp = DPContext()
+    resume = args.weights is not None
     net = CNNValue.load_model(args.model, device=dp.device)
     model = net.model
-    if args.weights:
+    if resume:
         model.load_weights(os.path.join(args.out_directory, args.weights))
     dp.broadcast_model(model)
     data = h5lite.File(args.train_data)
@@ -176,31 +221,64 @@ def run_training(cmd_line_args=None):
     if dp.is_root and not os.path.exists(args.out_directory):
         os.makedirs(args.out_directory)
     dp.barrier()
-    meta = MetadataWriterCallback(os.path.join(args.out_directory, "metadata.json"))
+    meta_file = os.path.join(args.out_directory, "metadata.json")
+    meta = MetadataWriterCallback(meta_file)
+    if resume and os.path.exists(meta_file):
+        with open(meta_file) as f:
+            meta.metadata = json.load(f)
     meta.metadata["training_data"] = args.train_data
     meta.metadata["model_file"] = args.model
-    meta.metadata["cmd_line_args"] = [vars(args)]
+    meta.metadata["cmd_line_args"] = meta.metadata.get("cmd_line_args", []) + [vars(args)]
     ckpt = K.ModelCheckpoint(os.path.join(args.out_directory, "weights.{epoch:05d}.hdf5"))
     ckpt.set_model(model)
-    model.compile(loss="mean_squared_error", optimizer=K.SGD(lr=args.learning_rate,
-                                                             decay=args.decay))
-    perm = np.random.RandomState(0).permutation(n)
-    trainer = ValueTrainer(model, states, values, args.minibatch,
-                           args.symmetries.split(","), dp)
+    sgd = K.SGD(lr=args.learning_rate, decay=args.decay)
+    model.compile(loss="mean_squared_error", optimizer=sgd)
+    cursor = 0
+    opt_state = _opt_sidecar(os.path.join(args.out_directory, args.weights)) if resume else None
+    if opt_state:
+        sgd.iterations = int(opt_state["iterations"])
+        cursor = int(opt_state.get("cursor", 0))
+    epoch_base = len(meta.metadata.get("epochs", []))
+    perm = np.random.RandomState(args.seed).permutation(n)
+    rank_metrics = RankMetrics(args.out_directory, dp.rank, dp.world, dp.device)
+    trainer = ValueTrainer(model, states, values, args.minibatch, args.symmetries.split(","), dp,
+                           seed=args.seed, metrics=rank_metrics)
     tr = torch.from_numpy(perm[:n_train].astype(np.int64)).to(dp.device)
-    va = perm[n_train:]
+    va = torch.from_numpy(perm[n_train:].astype(np.int64)).to(dp.device)
+    # every rank runs the SAME number of steps per epoch (ceil over the global batch), taking
+    # its slice of each global batch modulo n_train — so the gradient all-reduces pair up
+    # whatever n_train / (minibatch * world) is
+    gb = args.minibatch * dp.world
+    per_epoch = args.epoch_length or n_train
+    steps = -(-per_epoch // gb) if n_train else 0
+    fault = _fault_step(dp.rank)
+    arange = torch.arange(args.minibatch, device=dp.device)
     for epoch in range(args.epochs):
         t0 = time.time()
-        for s in range(dp.rank * args.minibatch, n_train, args.minibatch * dp.world):
-            trainer.step(tr[s:s + args.minibatch])
+        for _ in range(steps):
+            if fault is not None and sgd.iterations >= fault:
+                raise RuntimeError("injected fault at step %d (RAG_FAULT_AT_STEP)" % fault)
+            trainer.step(tr[(cursor + dp.rank * args.minibatch + arange) % n_train])
+            cursor = (cursor + gb) % n_train
         logs = {"loss": trainer.pop_loss()}
-        if len(va):
-            pred = model.predict(states[va].astype(np.float32))
-            logs["val_loss"] = float(np.mean((pred - values[va]) ** 2))
-        meta.on_epoch_end(epoch, logs)
-        ckpt.on_epoch_end(epoch, logs)
+        if va.numel():
+            logs["val_loss"] = trainer.evaluate(va)
+        dt = time.time() - t0
+        gepoch = epoch_base + epoch
+        rank_metrics.log(epoch=gepoch, step=int(sgd.iterations))
+        meta.on_epoch_end(gepoch, logs)
+        ckpt.on_epoch_end(gepoch, logs)
+        if dp.is_root:
+            path = ckpt.filepath.format(epoch=gepoch, **logs)
+            with open(os.path.splitext(path)[0] + ".opt.json", "w") as f:
+                json.dump({"iterations": int(sgd.iterations), "cursor": int(cursor),
+                           "epoch": gepoch, "lr": args.learning_rate, "decay": args.decay}, f)
+            with open(os.path.join(args.out_directory, "metrics.jsonl"), "a") as f:
+                f.write(json.dumps(dict(logs, epoch=gepoch, seconds=round(dt, 3),
+                                        positions_per_s=round(steps * gb / max(dt, 1e-9), 1),
+                                        world=dp.world, step=int(sgd.iterations))) + "\n")
         if args.verbose and dp.is_root:
-            print("epoch %d: %s (%.1fs)" % (epoch, json.dumps(logs), time.time() - t0))
+            print("epoch %d: %s (%.1fs)" % (gepoch, json.dumps(logs), dt))
     dp.barrier()
     return meta.metadata
 

@@ -206,3 +206,143 @@ def test_dp_rl_selfplay_sharded(tmp_path):
     from rocalphago_amd.models.policy import CNNPolicy
     fresh = CNNPolicy(FEATS, board=7, filters_per_layer=8, layers=2, device="cpu", seed=3)
     assert not np.allclose(a, fresh.model.net.flat.detach().numpy()), "no update happened"
+
+
+def _write_value_fixture(tmp):
+    """Tiny CNNValue (7x7, 3 planes of 'board' + color) and an HDF5 dataset of 40 positions."""
+    from rocalphago_amd.io import h5lite
+    from rocalphago_amd.models.value import CNNValue
+    feats = ["board", "color"]
+    net = CNNValue(feats, board=7, filters_per_layer=8, layers=2, dense=16, seed=5,
+                   device="cpu")
+    model_json = os.path.join(tmp, "value.json")
+    net.save_model(model_json)
+    rng = np.random.RandomState(0)
+    X = (rng.rand(40, 4, 7, 7) < 0.3).astype(np.uint8)
+    y = rng.choice([-1.0, 1.0], size=(40, 1)).astype(np.float32)
+    data = os.path.join(tmp, "vdata.h5")
+    with h5lite.File(data, "w") as f:
+        f["states"] = X
+        f["values"] = y
+        f["features"] = np.bytes_(",".join(feats))
+    return model_json, data
+
+
+def _value_worker(rank, world, port, outdir, model_json, data):
+    _setup(rank, world, port)
+    from rocalphago_amd.training import value_trainer as vt
+    captured = {}
+    orig = vt.CNNValue.load_model
+
+    def load(*a, **kw):
+        captured["net"] = orig(*a, **kw)
+        return captured["net"]
+
+    vt.CNNValue.load_model = staticmethod(load)
+    # 0.93 * 40 = 37 -> 36 training rows = 9 minibatches of 4: an odd number of batches, so
+    # ranks would run 5 vs 4 all-reduces without the shared step count
+    meta = vt.run_training([model_json, data, os.path.join(outdir, "out"), "-B", "4", "-E", "2",
+                            "--symmetries", "noop,rot90"])
+    np.save(os.path.join(outdir, "vflat%d.npy" % rank),
+            captured["net"].model.net.flat.detach().numpy())
+    np.save(os.path.join(outdir, "vloss%d.npy" % rank),
+            np.array([e["val_loss"] for e in meta["epochs"]]))
+
+
+@pytest.mark.timeout(300)
+def test_dp_value_training_uneven_batches(tmp_path):
+    """Value trainer under 2 gloo ranks with an odd number of minibatches per epoch: same step
+    count on every rank (no collective mismatch), identical replicas, sharded validation whose
+    all-reduced MSE every rank agrees on, per-rank metrics streams, resumable sidecar."""
+    import json
+    model_json, data = _write_value_fixture(str(tmp_path))
+    _spawn(_value_worker, (str(tmp_path), model_json, data))
+    a, b = np.load(tmp_path / "vflat0.npy"), np.load(tmp_path / "vflat1.npy")
+    assert np.array_equal(a, b), "value replicas diverged"
+    l0, l1 = np.load(tmp_path / "vloss0.npy"), np.load(tmp_path / "vloss1.npy")
+    np.testing.assert_allclose(l0, l1)
+    out = tmp_path / "out"
+    assert (out / "weights.00001.hdf5").exists()
+    side = json.load(open(out / "weights.00001.opt.json"))
+    assert side["iterations"] == 2 * 5  # ceil(36 / (4 * 2)) = 5 steps per epoch
+    for r in range(2):
+        recs = [json.loads(line) for line in open(out / ("metrics.rank%d.jsonl" % r))]
+        assert len(recs) == 2 and recs[-1]["rank"] == r and recs[-1]["steps"] == 5
+
+
+def _resnet_worker(rank, world, port, outdir):
+    _setup(rank, world, port)
+    from rocalphago_amd.models import kerasish as K
+    from rocalphago_amd.models.policy import ResnetPolicy
+    from rocalphago_amd.parallel.dp import DPContext
+    from rocalphago_amd.training.supervised import SupervisedTrainer
+    dp = DPContext(device="cpu")
+    pol = ResnetPolicy(FEATS, board=9, filters_per_layer=8, layers=3, device="cpu", seed=2)
+    model = pol.model
+    model.compile(loss="categorical_crossentropy", optimizer=K.SGD(lr=0.05), metrics=["accuracy"])
+    dp.broadcast_model(model)
+    trainer = SupervisedTrainer(model, _dataset(), 8, ["noop"], dp, seed=0)
+    for s in range(3):
+        trainer.step(torch.arange(s * 16 + rank * 8, s * 16 + (rank + 1) * 8))
+    vl, va = trainer.evaluate(torch.arange(48, 64))
+    np.save(os.path.join(outdir, "rflat%d.npy" % rank), model.net.flat.detach().numpy())
+    np.save(os.path.join(outdir, "rbuf%d.npy" % rank),
+            torch.cat([v.reshape(-1) for v in model.net.buffer_views()]).numpy())
+    np.save(os.path.join(outdir, "rval%d.npy" % rank), np.array([vl, va]))
+    dp.shutdown()
+
+
+@pytest.mark.timeout(300)
+def test_dp_resnet_bn_buffers_synced(tmp_path):
+    """ResnetPolicy under DP: the BatchNorm running averages are averaged over ranks each step,
+    so replicas (weights AND BN buffers) stay identical; validation is sharded by rank and the
+    all-reduced result equals a single-process evaluation of the same rows."""
+    _spawn(_resnet_worker, (str(tmp_path),))
+    b0, b1 = np.load(tmp_path / "rbuf0.npy"), np.load(tmp_path / "rbuf1.npy")
+    assert b0.size > 0
+    np.testing.assert_array_equal(b0, b1)
+    f0, f1 = np.load(tmp_path / "rflat0.npy"), np.load(tmp_path / "rflat1.npy")
+    np.testing.assert_array_equal(f0, f1)
+    v0, v1 = np.load(tmp_path / "rval0.npy"), np.load(tmp_path / "rval1.npy")
+    np.testing.assert_allclose(v0, v1)
+    # single-process evaluation of the trained replica on the same 16 rows
+    from rocalphago_amd.models import kerasish as K
+    from rocalphago_amd.models.policy import ResnetPolicy
+    from rocalphago_amd.training.supervised import SupervisedTrainer
+    torch.set_num_threads(1)
+    pol = ResnetPolicy(FEATS, board=9, filters_per_layer=8, layers=3, device="cpu", seed=2)
+    pol.model.compile(loss="categorical_crossentropy", optimizer=K.SGD(lr=0.05),
+                      metrics=["accuracy"])
+    with torch.no_grad():
+        pol.model.net.flat.copy_(torch.from_numpy(f0))
+    pol.model.net.bump()
+    tr = SupervisedTrainer(pol.model, _dataset(), 8, ["noop"], None, seed=0)
+    vl, va = tr.evaluate(torch.arange(48, 64))
+    np.testing.assert_allclose(v0, [vl, va], rtol=1e-5)
+
+
+def _rl_pergame_worker(rank, world, port, outdir):
+    _setup(rank, world, port)
+    from rocalphago_amd.models import kerasish as K
+    from rocalphago_amd.models.policy import CNNPolicy
+    from rocalphago_amd.parallel.dp import DPContext
+    from rocalphago_amd.players.ai import ProbabilisticPolicyPlayer
+    from rocalphago_amd.training import reinforcement as rl
+    dp = DPContext(device="cpu")
+    pol = CNNPolicy(FEATS, board=7, filters_per_layer=8, layers=2, device="cpu", seed=3)
+    opt = K.SGD(lr=0.01)
+    pol.model.compile(loss=rl.log_loss, optimizer=opt)
+    p = ProbabilisticPolicyPlayer(pol, move_limit=10)
+    try:
+        rl.run_n_games(opt, p, p, 2, mode="per_game", dp=dp)
+        ok = 0
+    except ValueError:
+        ok = 1
+    np.save(os.path.join(outdir, "pg%d.npy" % rank), np.array([ok]))
+    dp.shutdown()
+
+
+@pytest.mark.timeout(300)
+def test_dp_rl_per_game_rejected(tmp_path):
+    _spawn(_rl_pergame_worker, (str(tmp_path),))
+    assert np.load(tmp_path / "pg0.npy")[0] == 1 and np.load(tmp_path / "pg1.npy")[0] == 1

@@ -1,7 +1,6 @@
 """End-to-end HIP execution of the flagship networks vs the CPU/torch reference path (GPU)."""
 import numpy as np
 import pytest
-import torch
 
 from rocalphago_amd.engine import GameState
 from rocalphago_amd.features.preprocessing import DEFAULT_FEATURES

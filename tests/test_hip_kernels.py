@@ -156,7 +156,8 @@ def test_policy_head_and_backward(ops):
     ops.policy_head_fwd(hp, w, b0, pb, probs, K, labels=lab, loss=loss, dz=dz, hit=hit, mode=1,
                         gscale=1.0 / B)
     hr = bf(h).requires_grad_()
-    wr, br, pbr = w.clone().requires_grad_(), b0.clone().requires_grad_(), pb.clone().requires_grad_()
+    wr, br = w.clone().requires_grad_(), b0.clone().requires_grad_()
+    pbr = pb.clone().requires_grad_()
     z = (hr * wr.view(1, K, 1, 1)).sum(1).flatten(1) + br + pbr
     ref = F.softmax(z, dim=1)
     assert rel_err(probs, ref) < 1e-2
