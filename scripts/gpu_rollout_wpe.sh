@@ -1,7 +1,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 for w in 4 3; do
-  RAG_ROLLOUT_WPE=$w timeout -k 10 200 python scripts/dbg/rollout_ref.py check profiles/rollout_ref.npz > gpurun_out/rref_w$w.log 2>&1 || exit 1
+  RAG_ROLLOUT_WPE=$w timeout -k 10 200 python scripts/dbg/rollout_ref.py check tests/data/rollout_ref.npz > gpurun_out/rref_w$w.log 2>&1 || exit 1
   grep -q "winners equal True lengths equal True logits equal True" gpurun_out/rref_w$w.log || exit 1
 done
 for w in 4 3 4 3; do

@@ -88,7 +88,7 @@ def test_rollouts_bit_exact_vs_recorded_run():
     gr = GpuRollouts(rp, torch.device("cuda"))
     w, ln = gr.run(sts, R=4, limit=500, seed=123)
     lg = gr.initial_logits(sts[:64])
-    ref = np.load(os.path.join(root, "profiles", "rollout_ref.npz"))
+    ref = np.load(os.path.join(root, "tests", "data", "rollout_ref.npz"))
     assert np.array_equal(ref["w"], w)
     assert np.array_equal(ref["ln"], ln)
     assert np.array_equal(ref["lg"], lg)
