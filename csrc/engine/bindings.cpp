@@ -6,6 +6,7 @@
 #include <thread>
 
 #include "go_engine.hpp"
+#include "thread_pool.hpp"
 
 namespace py = pybind11;
 using namespace rag;
@@ -49,14 +50,7 @@ void parallel_for(int n, int nthreads, const std::function<void(int)>& fn) {
     for (int i = 0; i < n; ++i) fn(i);
     return;
   }
-  nthreads = std::min(nthreads, n);
-  std::atomic<int> next{0};
-  std::vector<std::thread> ts;
-  for (int t = 0; t < nthreads; ++t)
-    ts.emplace_back([&]() {
-      for (int i = next++; i < n; i = next++) fn(i);
-    });
-  for (auto& t : ts) t.join();
+  shared_pool(std::min(nthreads, 64)).run(n, fn);
 }
 
 }  // namespace
@@ -257,14 +251,9 @@ PYBIND11_MODULE(_rocgo, m) {
                     b.is_positional_superko(p))
                   il[(size_t)i * P + p] = 1;
             if (ladders) {
+              thread_local LadderReader reader;
               uint8_t* l0 = ld + (size_t)i * 2 * P;
-              for (int p = 0; p < P; ++p) {
-                l0[p] = 0;
-                l0[P + p] = 0;
-                if (b.color(p) != EMPTY) continue;
-                l0[p] = b.is_ladder_capture(p, -1, 80) ? 1 : 0;
-                l0[P + p] = b.is_ladder_escape(p, -1, 80) ? 1 : 0;
-              }
+              ladder_planes(b, l0, l0 + P, &reader);
             }
           });
         }
@@ -272,6 +261,29 @@ PYBIND11_MODULE(_rocgo, m) {
                               ladders ? py::object(lad) : py::none());
       },
       py::arg("boards"), py::arg("ladders") = true, py::arg("nthreads") = 8);
+
+  // Ladder planes [2, P] (capture, escape) of one board: the journaled single-copy reader
+  // (default, ladder.cpp) or, with copying=True, the reference-shaped recursive reader that copies
+  // the board at every ply (go_engine.cpp) — kept as the differential oracle.
+  m.def(
+      "ladder_planes",
+      [](const Board& b, bool copying) {
+        const int P = b.npoints();
+        py::array_t<uint8_t> out({2, P});
+        uint8_t* o = out.mutable_data();
+        if (copying) {
+          for (int p = 0; p < P; ++p) {
+            o[p] = o[P + p] = 0;
+            if (b.color(p) != EMPTY) continue;
+            o[p] = b.is_ladder_capture(p, -1, 80) ? 1 : 0;
+            o[P + p] = b.is_ladder_escape(p, -1, 80) ? 1 : 0;
+          }
+        } else {
+          ladder_planes(b, o, o + P);
+        }
+        return out;
+      },
+      py::arg("board"), py::arg("copying") = false);
 
   m.def("feature_planes", &feature_planes);
 

@@ -106,6 +106,7 @@ void extract_features(const Board& b, const int* fids, int nf, uint8_t* out) {
   const int me = b.current_player();
   bool have_after = false;
   std::vector<AfterMove> after;
+  std::vector<uint8_t> ladders;
 
   uint8_t* o = out;
   for (int i = 0; i < nf; ++i) {
@@ -173,10 +174,14 @@ void extract_features(const Board& b, const int* fids, int nf, uint8_t* out) {
         }
         break;
       case F_LADDER_CAPTURE:
-        for (int p : legal) o[p] = b.is_ladder_capture(p, -1, 80) ? 1 : 0;
-        break;
       case F_LADDER_ESCAPE:
-        for (int p : legal) o[p] = b.is_ladder_escape(p, -1, 80) ? 1 : 0;
+        // both planes come from one pass of the journaled reader (ladder.cpp); it answers
+        // illegal points with 0 like the per-point reference calls
+        if (ladders.empty()) {
+          ladders.resize(2 * (size_t)P);
+          ladder_planes(b, ladders.data(), ladders.data() + P);
+        }
+        std::memcpy(o, ladders.data() + (f == F_LADDER_CAPTURE ? 0 : P), P);
         break;
       case F_SENSIBLENESS:
         for (int p : non_eye) o[p] = 1;

@@ -159,6 +159,7 @@ class Board {
   void set_light(bool light) { light_ = light; }
 
  private:
+  friend class LadderReader;
   void place_stone(int p, int c);
   void remove_group(int h, int c);
   void recount_libs(int h);
@@ -190,6 +191,50 @@ class Board {
   int16_t libcnt_[MAXP];
   uint32_t placed_[MAXP];
 };
+
+// ------------------------------------------------------------------ ladders without copies
+// The reference's ladder reading (go.py:329-463) on one working copy of a board: moves are
+// played in place and taken back from a write journal (ladder.cpp). Results are identical to
+// Board::is_ladder_capture / is_ladder_escape for boards that do not enforce superko.
+class LadderReader {
+ public:
+  void reset(const Board& b);
+  bool capture(int a, int prey, int remaining);
+  bool escape(int a, int prey, int remaining);
+
+ private:
+  struct E8 {
+    int8_t* p;
+    int8_t old;
+  };
+  struct E16 {
+    int16_t* p;
+    int16_t old;
+  };
+  struct Frame {
+    uint32_t n8, n16;
+    int ko, player;
+  };
+  void set8(int8_t& r, int8_t v) {
+    j8_.push_back(E8{&r, r});
+    r = v;
+  }
+  void set16(int16_t& r, int16_t v) {
+    j16_.push_back(E16{&r, r});
+    r = v;
+  }
+  void play(int a);
+  void undo();
+  bool legal(int a) const;
+  Board b_;
+  std::vector<E8> j8_;
+  std::vector<E16> j16_;
+  std::vector<Frame> frames_;
+};
+
+// Both ladder planes (capture, escape; P bytes each) of one position; `reader` (optional) is a
+// reusable working board.
+void ladder_planes(const Board& b, uint8_t* cap, uint8_t* esc, LadderReader* reader = nullptr);
 
 // ------------------------------------------------------------------ features (preprocessing.py)
 // Feature ids; order matches the registry of the reference (preprocessing.py:209-258) plus

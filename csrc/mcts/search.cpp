@@ -26,7 +26,15 @@ void register_search(py::module_& m) {
       .def_property_readonly("nthreads", &Search::nthreads)
       .def("set_rollout_policy",
            [](Search& s, std::shared_ptr<RolloutPolicy> p) { s.rollout_policy = p; })
-      .def("select", &Search::select, py::arg("batch"))
+      .def("select", &Search::select, py::arg("batch"),
+           py::call_guard<py::gil_scoped_release>())
+      .def_readwrite("parallel_select_min", &Search::parallel_select_min)
+      .def("leaf_nodes",
+           [](Search& s, int id) {
+             std::vector<int32_t> v;
+             for (const Leaf& L : s.wave(id).leaves) v.push_back(L.path.back());
+             return v;
+           })
       .def("num_leaves", &Search::num_leaves)
       .def("leaf_boards", &Search::leaf_boards, py::return_value_policy::reference_internal)
       .def("backup_value",
@@ -161,8 +169,7 @@ void register_rollout(py::module_& m) {
              int8_t* o = out.mutable_data();
              {
                py::gil_scoped_release nogil;
-               Pool pool(std::max(1, nthreads));
-               pool.run(n, [&](int i) {
+               shared_pool(std::max(1, std::min(nthreads, 64))).run(n, [&](int i) {
                  Board c = *boards[i];
                  c.set_enforce_superko(false);
                  Rng rng(seed + (uint64_t)i * 7919ull);

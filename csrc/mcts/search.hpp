@@ -39,6 +39,7 @@
 #include <sys/mman.h>
 
 #include "../engine/go_engine.hpp"
+#include "../engine/thread_pool.hpp"
 #include "rollout.hpp"
 
 namespace rag {
@@ -124,75 +125,13 @@ struct Wave {
   bool rolling = false;
 };
 
-// Persistent worker pool (thread start-up is not paid per call).
-class Pool {
- public:
-  explicit Pool(int n) {
-    for (int i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
-  }
-  ~Pool() {
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      stop_ = true;
-      ++gen_;
-    }
-    cv_.notify_all();
-    for (auto& t : th_) t.join();
-  }
-  int size() const { return (int)th_.size(); }
-  void run(int n, const std::function<void(int)>& fn) {
-    if (n <= 0) return;
-    std::lock_guard<std::mutex> serial(run_mu_);  // one job at a time per pool
-    if (th_.empty() || n == 1) {
-      for (int i = 0; i < n; ++i) fn(i);
-      return;
-    }
-    std::unique_lock<std::mutex> lk(mu_);
-    fn_ = &fn;
-    n_ = n;
-    next_ = 0;
-    active_ = (int)th_.size();
-    ++gen_;
-    cv_.notify_all();
-    done_.wait(lk, [this] { return active_ == 0; });
-    fn_ = nullptr;
-  }
-
- private:
-  void loop() {
-    uint64_t seen = 0;
-    while (true) {
-      const std::function<void(int)>* fn;
-      int n;
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return gen_ != seen; });
-        seen = gen_;
-        if (stop_) return;
-        fn = fn_;
-        n = n_;
-      }
-      for (int i = next_++; i < n; i = next_++) (*fn)(i);
-      std::lock_guard<std::mutex> g(mu_);
-      if (--active_ == 0) done_.notify_one();
-    }
-  }
-  std::vector<std::thread> th_;
-  std::mutex mu_, run_mu_;
-  std::condition_variable cv_, done_;
-  const std::function<void(int)>* fn_ = nullptr;
-  int n_ = 0, active_ = 0;
-  std::atomic<int> next_{0};
-  uint64_t gen_ = 0;
-  bool stop_ = false;
-};
+using rag::Pool;
 
 }  // namespace mcts_detail
 
 using mcts_detail::Leaf;
 using mcts_detail::Node;
 using mcts_detail::NodeArena;
-using mcts_detail::Pool;
 using mcts_detail::Wave;
 using mcts_detail::N_EXPANDED;
 using mcts_detail::N_NEW;
@@ -230,8 +169,12 @@ class Search {
   int nthreads() const { return pool_.size(); }
 
   // ------------------------------------------------------------------ selection
+  // vl and state are changed by concurrent descents (descend_parallel): read them atomically
+  static int32_t vl_of(const Node& c) { return __atomic_load_n(&c.vl, __ATOMIC_RELAXED); }
+  static uint8_t state_of(const Node& c) { return __atomic_load_n(&c.state, __ATOMIC_RELAXED); }
+
   float child_score(const Node& c, float sq) const {
-    const float vl = (float)(c.vl * n_vl);
+    const float vl = (float)(vl_of(c) * n_vl);
     const bool use_r = lambda > 0.f;
     const bool use_v = lambda < 1.f;
     float q = 0.f;
@@ -252,7 +195,7 @@ class Search {
 
   int select_child(int p) const {
     const Node& pn = nodes_[p];
-    const float np = (float)(pn.n + pn.vl * n_vl);
+    const float np = (float)(pn.n + vl_of(pn) * n_vl);
     const float sq = std::sqrt(std::max(np, 1.f));
     int best = pn.first;
     float bv = -1e30f;
@@ -268,9 +211,8 @@ class Search {
 
   // Returns (wave id, number of leaves); id -1 when nothing was selected.
   //
-  // Three phases: (1) serial tree walks with virtual loss that track only what the walk needs
-  // (player to move, the last two moves and the move count decide the end of the game, exactly
-  // as Board::play_unchecked does); (2) the leaf boards (root copy + the path's moves) are built
+  // Three phases: (1) tree walks with virtual loss (descend(); on the pool for B >=
+  // parallel_select_min, see descend_parallel); (2) the leaf boards (root copy + the path's moves) are built
   // in parallel on the pool; (3) descents that ended on a terminal position are scored on their
   // board and backed up at once (their virtual loss, taken in phase 1 so that later walks of the
   // same wave avoid them, is dropped again).
@@ -280,43 +222,27 @@ class Search {
     std::vector<uint8_t> term;
     paths.reserve(B);
     term.reserve(B);
-    int attempts = 0, nleaf = 0;
-    const Board& rb = root_board_;
-    while (nleaf < B && attempts < 4 * B) {
-      ++attempts;
-      std::vector<int32_t> path;
-      path.reserve(32);
-      int node = root_;
-      path.push_back(node);
-      int depth = 0;
-      int ptm = rb.current_player(), l1 = rb.last1(), l2 = rb.last2(), nm = rb.nmoves();
-      bool end = rb.end_of_game();
-      while (nodes_[node].state == N_EXPANDED && nodes_[node].nchild > 0 && !end &&
-             depth < max_depth) {
-        node = select_child(node);
-        path.push_back(node);
-        ++depth;
-        ++nm;
-        l2 = l1;
-        l1 = nodes_[node].move;
-        ptm = -ptm;
-        if (nm > 1 && l1 == PASS && l2 == PASS && ptm == WHITE) end = true;
-      }
-      const bool terminal = end || depth >= max_depth ||
-                            (nodes_[node].state == N_EXPANDED && nodes_[node].nchild == 0);
-      if (!terminal) {
-        if (nodes_[node].state == N_PENDING) {  // already waiting for its evaluation
+    if (B >= parallel_select_min && pool_.size() > 1) {
+      descend_parallel(B, paths, term);
+    } else {
+      int attempts = 0, claimed = 0;
+      while (claimed < B && attempts < 4 * B) {
+        ++attempts;
+        std::vector<int32_t> path;
+        bool terminal = false;
+        if (!descend(path, terminal, false)) {
           ++collisions_;
           continue;
         }
-        nodes_[node].state = N_PENDING;
-        ++nleaf;
+        if (!terminal) ++claimed;
+        paths.push_back(std::move(path));
+        term.push_back(terminal ? 1 : 0);
       }
-      for (int id : path) nodes_[id].vl += 1;
-      paths.push_back(std::move(path));
-      term.push_back(terminal ? 1 : 0);
     }
+    const Board& rb = root_board_;
     const int nd = (int)paths.size();
+    int nleaf = 0;
+    for (int i = 0; i < nd; ++i) nleaf += term[i] ? 0 : 1;
     // leaf boards go straight into a recycled wave (its Leaf storage is reused: no fresh pages);
     // terminal descents get a scratch board
     std::unique_ptr<Wave> wave = take_wave();
@@ -355,6 +281,98 @@ class Search {
     const int id = next_wave_++;
     waves_[id] = std::move(wave);
     return {id, n};
+  }
+
+  // Descents of one wave in parallel on the pool (AlphaGo's asynchronous search threads):
+  // virtual loss is taken on every node of a path as the walk passes it (atomic adds), so
+  // concurrent walks spread over the tree; a leaf is claimed by one N_NEW -> N_PENDING
+  // compare-and-swap, a walk that loses it (or arrives after B leaves are claimed) gives its
+  // virtual loss back and is counted as a collision. Which leaves a wave gets then depends on
+  // thread timing; select(B) with B < parallel_select_min (or one thread) is the serial,
+  // deterministic walk.
+  int parallel_select_min = 64;
+
+  void descend_parallel(int B, std::vector<std::vector<int32_t>>& paths,
+                        std::vector<uint8_t>& term) {
+    std::atomic<int> nleaf{0}, attempts{0}, coll{0};
+    std::mutex mu;
+    const int nw = pool_.size();
+    pool_.run(nw, [&](int) {
+      std::vector<std::vector<int32_t>> mine;
+      std::vector<uint8_t> mterm;
+      while (nleaf.load(std::memory_order_relaxed) < B &&
+             attempts.fetch_add(1, std::memory_order_relaxed) < 4 * B) {
+        std::vector<int32_t> path;
+        bool terminal = false;
+        if (!descend(path, terminal, true)) {
+          coll.fetch_add(1, std::memory_order_relaxed);
+          continue;
+        }
+        if (!terminal && nleaf.fetch_add(1) >= B) {  // over-claimed: hand the leaf back
+          __atomic_store_n(&nodes_[path.back()].state, (uint8_t)N_NEW, __ATOMIC_RELAXED);
+          for (int id : path) __atomic_fetch_sub(&nodes_[id].vl, 1, __ATOMIC_RELAXED);
+          break;
+        }
+        mine.push_back(std::move(path));
+        mterm.push_back(terminal ? 1 : 0);
+      }
+      std::lock_guard<std::mutex> g(mu);
+      for (size_t k = 0; k < mine.size(); ++k) {
+        paths.push_back(std::move(mine[k]));
+        term.push_back(mterm[k]);
+      }
+    });
+    collisions_ = coll.load();
+  }
+
+  // One walk from the root with virtual loss. Tracks only what the walk needs (player to move,
+  // the last two moves and the move count decide the end of the game, exactly as
+  // Board::play_unchecked does). Returns false (virtual loss already given back) when the walk
+  // ends on a leaf that another descent is waiting for; terminal = end of game / depth limit /
+  // a node without children (its virtual loss stays until its immediate backup).
+  bool descend(std::vector<int32_t>& path, bool& terminal, bool concurrent) {
+    const Board& rb = root_board_;
+    path.clear();
+    path.reserve(32);
+    int node = root_;
+    path.push_back(node);
+    if (concurrent) __atomic_fetch_add(&nodes_[node].vl, 1, __ATOMIC_RELAXED);
+    int depth = 0;
+    int ptm = rb.current_player(), l1 = rb.last1(), l2 = rb.last2(), nm = rb.nmoves();
+    bool end = rb.end_of_game();
+    while (state_of(nodes_[node]) == N_EXPANDED && nodes_[node].nchild > 0 && !end &&
+           depth < max_depth) {
+      node = select_child(node);
+      path.push_back(node);
+      if (concurrent) __atomic_fetch_add(&nodes_[node].vl, 1, __ATOMIC_RELAXED);
+      ++depth;
+      ++nm;
+      l2 = l1;
+      l1 = nodes_[node].move;
+      ptm = -ptm;
+      if (nm > 1 && l1 == PASS && l2 == PASS && ptm == WHITE) end = true;
+    }
+    Node& leaf = nodes_[node];
+    terminal = end || depth >= max_depth || (state_of(leaf) == N_EXPANDED && leaf.nchild == 0);
+    if (!terminal) {
+      bool claimed;
+      if (concurrent) {
+        uint8_t expect = N_NEW;
+        claimed = __atomic_compare_exchange_n(&leaf.state, &expect, (uint8_t)N_PENDING, false,
+                                              __ATOMIC_RELAXED, __ATOMIC_RELAXED);
+      } else {
+        claimed = leaf.state != N_PENDING;
+        if (claimed) leaf.state = N_PENDING;
+      }
+      if (!claimed) {  // already waiting for its evaluation
+        if (concurrent)
+          for (int id : path) __atomic_fetch_sub(&nodes_[id].vl, 1, __ATOMIC_RELAXED);
+        return false;
+      }
+    }
+    if (!concurrent)
+      for (int id : path) nodes_[id].vl += 1;
+    return true;
   }
 
   Wave& wave(int id) {

@@ -4,6 +4,7 @@
 // the tree. Driven by tests/test_sanitizers.py:
 //   g++ -std=c++17 -O1 -g -fsanitize=thread  ... && ./selftest
 //   g++ -std=c++17 -O1 -g -fsanitize=address,undefined ... && ./selftest
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <memory>
@@ -11,6 +12,7 @@
 #include <vector>
 
 #include "../engine/go_engine.hpp"
+#include "../engine/thread_pool.hpp"
 #include "../mcts/rollout.hpp"
 #include "../mcts/search.hpp"
 
@@ -67,6 +69,23 @@ int main() {
     for (int p = 0; p < S * S; ++p)
       if (c.color(p) == EMPTY) (void)c.is_ladder_capture(p, -1, 80);
   }
+  // 1b. the journaled ladder reader on the shared pool == the copying reader
+  {
+    std::vector<uint8_t> got(positions.size() * 2 * S * S);
+    shared_pool(4).run((int)positions.size(), [&](int i) {
+      thread_local LadderReader reader;
+      uint8_t* o = got.data() + (size_t)i * 2 * S * S;
+      ladder_planes(positions[i], o, o + S * S, &reader);
+    });
+    for (size_t i = 0; i < positions.size(); ++i) {
+      const Board& b = positions[i];
+      for (int p = 0; p < S * S; ++p) {
+        const bool e = b.color(p) == EMPTY;
+        CHECK(got[i * 2 * S * S + p] == (e && b.is_ladder_capture(p, -1, 80)));
+        CHECK(got[i * 2 * S * S + S * S + p] == (e && b.is_ladder_escape(p, -1, 80)));
+      }
+    }
+  }
   // 2. multi-threaded rollouts
   {
     mcts_detail::Pool pool(4);
@@ -107,6 +126,27 @@ int main() {
     CHECK(w.first >= 0);
     s.backup_value(w.first, nullptr, 0, values.data());
     s.finish_rollouts(w.first);
+  }
+  // 4. parallel descents (descend_parallel): distinct leaves per wave, virtual loss balanced
+  {
+    Board root(S, 7.5, false, z);
+    Search s(root, 4);
+    s.lambda = 0.5f;
+    s.parallel_select_min = 8;
+    std::vector<float> values(64, 0.1f);
+    for (int wave = 0; wave < 10; ++wave) {
+      auto w = s.select(48);
+      if (w.first < 0) continue;
+      std::vector<int> ids;
+      for (const Leaf& L : s.wave(w.first).leaves) ids.push_back(L.path.back());
+      std::sort(ids.begin(), ids.end());
+      CHECK(std::adjacent_find(ids.begin(), ids.end()) == ids.end());
+      s.start_rollouts(w.first);
+      s.backup_value(w.first, nullptr, 0, values.data());
+      s.finish_rollouts(w.first);
+    }
+    CHECK(s.pending_waves() == 0);
+    CHECK(s.root_visits() > 200);
   }
   std::printf("native selftest ok: %zu positions\n", positions.size());
   return 0;

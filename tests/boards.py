@@ -25,3 +25,45 @@ def parse(diagram):
                 assert ch not in marks, "duplicate marker %s" % ch
                 marks[ch] = (r, c)
     return state, marks
+
+
+def random_games(n, size, seed, lo, hi):
+    """n positions from rollout-policy games of lo..hi moves (ladder-rich mid/late game)."""
+    import numpy as np
+    from rocalphago_amd._native import engine
+    rp = engine().RolloutPolicy()
+    rs = np.random.RandomState(seed)
+    out = []
+    for _ in range(n):
+        st = GameState(size=size)
+        for _k in range(int(rs.randint(lo, hi))):
+            mv = rp.sample(st.native, int(rs.randint(1 << 30)))
+            st.do_move(None if mv < 0 else divmod(mv, size))
+            if st.is_end_of_game:
+                break
+        out.append(st)
+    return out
+
+
+def ladder_scenarios():
+    """The reference ladder scenarios (its tests/test_ladders.py) at each step, both colours."""
+    boards = [
+        ("d b c . . . .|B W a . . . .|. B . . . . .|. . . . . . .|. . . . . . .|"
+         ". . . . . W .|", ["a", "b"]),
+        (". B . . . . .|B W a . . W .|B b . . . . .|. c . . . . .|. . . . . . .|"
+         ". . . . . W .|", ["a", "b"]),
+        (". B . . . . .|B W B . . W .|B a c . . . .|. b . . . . .|. . . . . . .|"
+         ". W . . . . .|. . . . . . .|", ["a"]),
+    ]
+    out = []
+    for text, moves in boards:
+        for first in (BLACK, WHITE):
+            st, m = parse(text)
+            st.current_player = first
+            out.append(st.copy())
+            for mv in moves:
+                if not st.is_legal(m[mv]):
+                    break
+                st.do_move(m[mv])
+                out.append(st.copy())
+    return out

@@ -234,3 +234,28 @@ def test_network_evaluator_cpu(lmbda):
     mv = mc.get_move(st)
     assert st.is_legal(mv)
     assert mc.stats["sims"] >= 90
+
+
+def test_parallel_select_claims_distinct_leaves():
+    """Waves of B >= parallel_select_min descend on the pool (atomic virtual loss + leaf claim):
+    exactly B distinct leaves, virtual loss returned on backup."""
+    st = GameState(size=9)
+    s = rg.Search(st.native, 4)
+    s.lmbda = 0.5
+    s.parallel_select_min = 16
+    rs = np.random.RandomState(0)
+    total = 0
+    for _ in range(12):
+        wid, n = s.select(64)
+        if n == 0:
+            continue
+        nodes = s.leaf_nodes(wid)
+        assert len(nodes) == n == len(set(nodes))
+        pri = rs.dirichlet(np.ones(81), size=n).astype(np.float32)
+        s.backup_value(wid, pri, rs.uniform(-1, 1, n).astype(np.float32))
+        s.backup_rollout(wid, rs.uniform(-1, 1, n).astype(np.float32))
+        total += n
+    assert s.pending_waves == 0
+    assert s.root_visits == total > 600
+    mv, vis, _, _ = s.root_stats()
+    assert vis.sum() == total - 1

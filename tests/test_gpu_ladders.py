@@ -6,9 +6,8 @@ import pytest
 import torch
 
 from rocalphago_amd._native import engine
-from rocalphago_amd.engine.gamestate import BLACK, WHITE, GameState
 
-from boards import parse
+from boards import ladder_scenarios, random_games
 
 pytestmark = pytest.mark.gpu
 rg = engine()
@@ -21,19 +20,7 @@ def dev():
     return torch.device("cuda")
 
 
-def _games(n, size, seed, lo, hi):
-    rs = np.random.RandomState(seed)
-    rp = rg.RolloutPolicy()
-    out = []
-    for i in range(n):
-        st = GameState(size=size)
-        for k in range(int(rs.randint(lo, hi))):
-            mv = rp.sample(st.native, int(rs.randint(1 << 30)))
-            st.do_move(None if mv < 0 else divmod(mv, size))
-            if st.is_end_of_game:
-                break
-        out.append(st)
-    return out
+_games = random_games
 
 
 def _compare(dev, states):
@@ -64,28 +51,7 @@ def test_gpu_ladders_match_native(dev, size, seed, lo, hi):
     assert n > 0, "no ladder in the sample: the comparison would be vacuous"
 
 
-def _reference_scenarios():
-    """The reference ladder scenarios (tests/test_ladders.py) at each step, both colours."""
-    boards = [
-        ("d b c . . . .|B W a . . . .|. B . . . . .|. . . . . . .|. . . . . . .|"
-         ". . . . . W .|", ["a", "b"]),
-        (". B . . . . .|B W a . . W .|B b . . . . .|. c . . . . .|. . . . . . .|"
-         ". . . . . W .|. . . . . . .|", ["a", "b"]),
-        (". B . . . . .|B W B . . W .|B a c . . . .|. b . . . . .|. . . . . . .|"
-         ". W . . . . .|. . . . . . .|", ["a"]),
-    ]
-    out = []
-    for text, moves in boards:
-        for first in (BLACK, WHITE):
-            st, m = parse(text)
-            st.current_player = first
-            out.append(st.copy())
-            for mv in moves:
-                if not st.is_legal(m[mv]):
-                    break
-                st.do_move(m[mv])
-                out.append(st.copy())
-    return out
+_reference_scenarios = ladder_scenarios
 
 
 def test_gpu_ladders_reference_scenarios(dev):

@@ -1,0 +1,65 @@
+"""The journaled single-copy ladder reader (csrc/engine/ladder.cpp) gives exactly the planes of
+the copying recursive reader (csrc/engine/go_engine.cpp, the shape of the reference's
+go.py:329-463), on the reference scenarios and on random games of three board sizes, and the
+feature extractor's ladder planes (preprocessing.py:172-187) come from it."""
+import time
+
+import numpy as np
+import pytest
+
+from rocalphago_amd._native import engine
+from rocalphago_amd.features.preprocessing import Preprocess
+
+from boards import ladder_scenarios, random_games
+
+rg = engine()
+
+
+def _check(states):
+    hits = 0
+    for i, st in enumerate(states):
+        want = rg.ladder_planes(st.native, True)
+        got = rg.ladder_planes(st.native, False)
+        if not np.array_equal(got, want):
+            k, p = np.argwhere(got != want)[0]
+            raise AssertionError("state %d %s at %s: journaled %d copying %d" % (
+                i, ("capture", "escape")[k], divmod(int(p), st.size), got[k, p], want[k, p]))
+        hits += int(want.sum())
+    return hits
+
+
+def test_reference_scenarios():
+    assert _check(ladder_scenarios()) > 0
+
+
+@pytest.mark.parametrize("size,seed,lo,hi", [(19, 11, 40, 250), (19, 12, 150, 400),
+                                             (13, 13, 20, 200), (9, 14, 10, 120)])
+def test_random_games(size, seed, lo, hi):
+    assert _check(random_games(96, size, seed, lo, hi)) > 0
+
+
+def test_feature_planes_use_reader():
+    states = random_games(24, 19, 5, 100, 300)
+    pre = Preprocess(["ladder_capture", "ladder_escape"])
+    x = rg.batch_features([s.native for s in states], pre.feature_ids, 2)
+    for st, planes in zip(states, x):
+        want = rg.ladder_planes(st.native, True).reshape(2, st.size, st.size)
+        assert np.array_equal(planes, want)
+
+
+def test_superko_board_uses_copying_reader():
+    st = random_games(1, 9, 3, 30, 60)[0]
+    st.enforce_superko = True
+    assert np.array_equal(rg.ladder_planes(st.native, False), rg.ladder_planes(st.native, True))
+
+
+def test_reader_is_faster():
+    states = random_games(48, 19, 12, 150, 400)
+    t0 = time.perf_counter()
+    for st in states:
+        rg.ladder_planes(st.native, True)
+    t1 = time.perf_counter()
+    for st in states:
+        rg.ladder_planes(st.native, False)
+    t2 = time.perf_counter()
+    assert (t2 - t1) < (t1 - t0)

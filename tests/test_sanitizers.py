@@ -12,7 +12,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRCS = [os.path.join(ROOT, "csrc", p) for p in
         ("tests/native_selftest.cpp", "engine/go_engine.cpp", "engine/features.cpp",
-         "mcts/rollout.cpp")]
+         "engine/ladder.cpp", "mcts/rollout.cpp")]
 
 
 @pytest.mark.slow
