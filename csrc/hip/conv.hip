@@ -561,6 +561,10 @@ bool rag_conv_slab_launch(const bf16* x, const bf16* w, const float* bias, bf16*
                           const bf16* mk, const bf16* res, int B, int S, int HI, int WO, int HO,
                           int CIN, int COUTP, int YC, int KS, int relu, int HM,
                           hipStream_t stream);  // conv_slab.hip
+bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* y,
+                         const bf16* mk, const bf16* res, int M, int S, int WI, int shift, int WO,
+                         int HO, int CIN, int COUTP, int YC, int KS, int relu, int HM,
+                         long total_rows, hipStream_t stream);  // conv_tap.hip
 
 // Conv forward / dgrad.  X: padded input (halo HI, CIN channels, CIN % 32 == 0).  W: packed
 // bf16 weights [taps][WROWS][CIN].  Y: padded output (halo HO, YC channels, COUTP % 32 == 0,
@@ -587,6 +591,9 @@ RAG_API int rag_conv_igemm(const void* X, const void* W, const float* bias, void
   }();
   if (rag_conv_slab_launch(x, w, bias, y, mk, res, B, S, HI, WO, HO, CIN, COUTP, YC, KS, relu,
                            HM, stream))
+    return (int)hipGetLastError();
+  if (use_pipe && rag_conv_tap_launch(x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN,
+                                      COUTP, YC, KS, relu, HM, (long)B * WI * WI, stream))
     return (int)hipGetLastError();
   if (use_pipe && rag_conv_pipe_launch(x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN,
                                        COUTP, YC, KS, relu, HM, stream))

@@ -45,6 +45,8 @@ SIGNATURES = {
     "rag_ladders": [P, P, I, I, P, P, P],
     # conv_slab.hip
     "rag_conv_slab_mode": [I],
+    "rag_conv_order": [I],
+    "rag_conv_tap_mode": [I],
 }
 
 RESTYPES = {"rag_conv_wgrad_workspace": SZ, "rag_head_bwd_workspace": SZ,
