@@ -53,6 +53,26 @@ __device__ __forceinline__ int swz_tr(int r) {
   }
 }
 
+// Transposed 16x16x32 fragment read (2 x ds_read_b64_tr_b16) as inline asm. Through the
+// __builtin_amdgcn_ds_read_tr16_b64 builtin hipcc cannot tell these LDS reads from in-flight
+// global_load_lds writes and drains them all (s_waitcnt vmcnt(0)) before the first read of every
+// staging step (seen in wgrad_slab's .s), which serialises a multi-stage LDS ring. The caller
+// retires the reads with lds_reads_done() before their MFMAs (guide §5.4 rule 18: the
+// sched_barrier keeps hipcc from hoisting the MFMAs above the asm wait).
+__device__ __forceinline__ uint32_t lds_addr(const bf16* p) {
+  return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((LDS_PTR(const bf16))p));
+}
+__device__ __forceinline__ bf16x8 tr_frag(const bf16* p0, const bf16* p1) {
+  bf16x4 lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(lds_addr(p0)));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(lds_addr(p1)));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+__device__ __forceinline__ void lds_reads_done() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 __device__ __forceinline__ int wave_id() {
   return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 }

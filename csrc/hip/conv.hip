@@ -308,9 +308,7 @@ conv_wgrad_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
         const int r0 = rb + 8 * g + q, r1 = r0 + 4;
         const bf16* p0 = lg + r0 * GROW + (((col >> 3) ^ swz_tr<GCH>(r0)) << 3) + (col & 7);
         const bf16* p1 = lg + r1 * GROW + (((col >> 3) ^ swz_tr<GCH>(r1)) << 3) + (col & 7);
-        bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_PTR(bf16x4))p0);
-        bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_PTR(bf16x4))p1);
-        fa[a] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        fa[a] = tr_frag(p0, p1);
       }
 #pragma unroll
       for (int c = 0; c < NTC; ++c) {
@@ -318,10 +316,9 @@ conv_wgrad_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
         const int r0 = rb + 8 * g + q, r1 = r0 + 4;
         const bf16* p0 = lx + r0 * XROW + (((col >> 3) ^ swz_tr<XCH>(r0)) << 3) + (col & 7);
         const bf16* p1 = lx + r1 * XROW + (((col >> 3) ^ swz_tr<XCH>(r1)) << 3) + (col & 7);
-        bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_PTR(bf16x4))p0);
-        bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_PTR(bf16x4))p1);
-        fb[c] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        fb[c] = tr_frag(p0, p1);
       }
+      lds_reads_done();
 #pragma unroll
       for (int a = 0; a < NTN; ++a)
 #pragma unroll

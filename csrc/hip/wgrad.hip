@@ -156,29 +156,32 @@ wgrad_taps_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
     const bf16* lb = lds + (s % NBUF) * kStageElems;
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
+      // fragments are read in tap groups of TG (registers: 9 taps x 2 would spill at 2 blocks/CU)
+      constexpr int TG = (NT > 5 && NT % 3 == 0) ? 3 : NT;
       bf16x8 fa[2];
 #pragma unroll
       for (int a = 0; a < 2; ++a) {
         const bf16* p0 = lb + gbase + (32 * hh) * kRS + a * 16;
-        bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_PTR(bf16x4))p0);
-        bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_PTR(bf16x4))(p0 + 16 * kRS));
-        fa[a] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        fa[a] = tr_frag(p0, p0 + 16 * kRS);
       }
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        bf16x8 fb[2];
+      for (int t0 = 0; t0 < NT; t0 += TG) {
+        bf16x8 fb[TG][2];
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          const bf16* p0 = lb + xbase[t] + (32 * hh) * kRS + c * 16;
-          bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_PTR(bf16x4))p0);
-          bf16x4 hi =
-              __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_PTR(bf16x4))(p0 + 16 * kRS));
-          fb[c] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        }
+        for (int u = 0; u < TG; ++u)
 #pragma unroll
-        for (int a = 0; a < 2; ++a)
+          for (int c = 0; c < 2; ++c) {
+            const bf16* p0 = lb + xbase[t0 + u] + (32 * hh) * kRS + c * 16;
+            fb[u][c] = tr_frag(p0, p0 + 16 * kRS);
+          }
+        lds_reads_done();
 #pragma unroll
-          for (int c = 0; c < 2; ++c) acc[t][a][c] = mfma16(fa[a], fb[c], acc[t][a][c]);
+        for (int u = 0; u < TG; ++u)
+#pragma unroll
+          for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+              acc[t0 + u][a][c] = mfma16(fa[a], fb[u][c], acc[t0 + u][a][c]);
       }
     }
     if (do_bias && (int)threadIdx.x < 64) {

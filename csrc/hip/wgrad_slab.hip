@@ -13,7 +13,7 @@
 // 64-row stages. Per stage it stages the 64 G rows (all 192 channels) and one 112-row X slab of
 // its 32 channels that covers every tap's shifted window: ~18 B/clk/CU at the MFMA rate.
 //
-// LDS layouts (no padding; 3-stage ring, 93 KB):
+// LDS layouts (no padding; kNBUF-stage ring of 31 KB stages):
 //   * G [64][192]: fragments are transposed reads (ds_read_b64_tr_b16) of 8 rows x 32 B per
 //     32-lane half. Rows are 384 B (= 32 words mod 64 banks), so the 32-byte unit index is XORed
 //     with row bits 1..2: the 8 rows of a half then hit 8 distinct 8-word bank windows.
@@ -36,7 +36,6 @@ constexpr int kXRows = 112;                     // X slab rows (7 glds x 16 rows
 constexpr int kXWaves = kXRows / 16;            // waves that stage X
 constexpr int kGElems = kRows * kN;
 constexpr int kStage = kGElems + kXRows * kC;
-constexpr int kNBUF = 3;
 constexpr int kWaves = 12;
 static_assert(kRows * kGChunks == kWaves * 2 * 64, "two G glds per wave");
 
@@ -44,18 +43,28 @@ __device__ __forceinline__ int swz_x(int row) { return ((row >> 2) & 1) << 1; }
 __device__ __forceinline__ int swz_g(int row) { return ((row >> 1) & 3) << 1; }
 __device__ __forceinline__ int krow(int g, int q) { return (g & 1) * 4 + q + (g >> 1) * 8; }
 
-__device__ __forceinline__ bf16x8 tr_frag(const bf16* p0, const bf16* p1) {
-  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_PTR(bf16x4))p0);
-  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((LDS_PTR(bf16x4))p1);
-  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+// vmcnt(N) with N = `young` stages of this wave's loads (PER glds each) left in flight
+template <int PER>
+__device__ __forceinline__ void wait_young(int young) {
+  switch (young) {
+    case 0: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PER) : "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * PER) : "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(3 * PER) : "memory"); break;
+  }
 }
 
+// kNBUF-stage LDS ring, kNBUF-1 stages in flight. ALL LDS (staging and the bias reduction) lives
+// in the one __shared__ array: a second __shared__ object made hipcc drain every in-flight
+// global_load_lds (s_waitcnt vmcnt(0)) before the first ds_read of each stage (guide §5,
+// "Projection GEMM" item 4(a); seen in this kernel's .s).
+template <int kNBUF>
 __global__ void __launch_bounds__(768)
 wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
                   float* __restrict__ part, float* __restrict__ bpart, int R, int WP, int GC,
                   int CIN, int spc, int CINP) {
   __shared__ __attribute__((aligned(16))) bf16 lds[kNBUF * kStage];
-  __shared__ float bred[kWaves * 64];
+  static_assert(kNBUF * kStage * 2 >= kWaves * 64 * 4, "bias scratch fits the staging array");
 
   const int lane = lane_id();
   const int w = wave_id();
@@ -126,35 +135,37 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
   const int brow = tid >> 5;                 // rows brow, brow + 24, brow + 48
   float bsum = 0.f;
 
-  if (nsteps > 0) stage(0, 0);
-  if (nsteps > 1) stage(1, 1);
+#pragma unroll
+  for (int k = 0; k < kNBUF - 1; ++k)
+    if (k < nsteps) stage(k, k);
   for (int s = 0; s < nsteps; ++s) {
-    // retire stage s; stage s+1 (2 or 3 glds of this wave) may stay in flight
-    if (s + 1 < nsteps) {
-      if (xw)
-        asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    }
+    // retire stage s; up to kNBUF-2 younger stages (2 or 3 glds of this wave each) stay in flight
+    int young = nsteps - 1 - s;
+    young = young < kNBUF - 2 ? young : kNBUF - 2;
+    if (xw)
+      wait_young<3>(young);
+    else
+      wait_young<2>(young);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (s + 2 < nsteps) stage(s + 2, (s + 2) % kNBUF);
+    if (s + kNBUF - 1 < nsteps) stage(s + kNBUF - 1, (s + kNBUF - 1) % kNBUF);
     const bf16* lb = lds + (s % kNBUF) * kStage;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int ro = kk * 32;  // rows; bits 1..2 unchanged, so the swizzles are unchanged
-      bf16x8 fa[2];
+      bf16x8 fa[2], fb[9];
 #pragma unroll
       for (int a = 0; a < 2; ++a)
         fa[a] = tr_frag(lb + goff[a] + ro * kN, lb + goff[a] + (ro + 16) * kN);
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+        fb[t] = tr_frag(lb + xoff[t] + ro * kC, lb + xoff[t] + (ro + 16) * kC);
+      lds_reads_done();
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
-        const bf16x8 fb = tr_frag(lb + xoff[t] + ro * kC, lb + xoff[t] + (ro + 16) * kC);
-        acc[t][0] = mfma16(fa[0], fb, acc[t][0]);
-        acc[t][1] = mfma16(fa[1], fb, acc[t][1]);
+        acc[t][0] = mfma16(fa[0], fb[t], acc[t][0]);
+        acc[t][1] = mfma16(fa[1], fb[t], acc[t][1]);
       }
       __builtin_amdgcn_s_setprio(0);
     }
@@ -177,6 +188,8 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
     }
   }
   if (do_bias) {
+    float* bred = reinterpret_cast<float*>(lds);
+    __syncthreads();  // every wave is done reading the staging ring
     bred[tid] = bsum;
     __syncthreads();
     if (tid < 32 && bcol < kN) {
@@ -213,9 +226,33 @@ int rag_wgrad_slab_nchunks(int R, int CINP, int* spc) {
   return (steps + s - 1) / s;
 }
 
+static int g_wslab_nbuf = -1;  // RAG_WGRAD_NBUF (3..5), read on first use
+
+RAG_API int rag_wgrad_slab_nbuf(int n) {
+  const int old = g_wslab_nbuf;
+  g_wslab_nbuf = n;
+  return old;
+}
+
 int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpart, int R, int WP,
                           int GC, int CIN, int spc, int CINP, int nchunks, hipStream_t stream) {
-  wgrad_slab_kernel<<<nchunks * (CINP / kC), 64 * kWaves, 0, stream>>>(G, X, part, bpart, R, WP,
-                                                                      GC, CIN, spc, CINP);
+  if (g_wslab_nbuf < 0) {
+    const char* e = getenv("RAG_WGRAD_NBUF");
+    g_wslab_nbuf = e ? atoi(e) : 3;
+  }
+  const dim3 grid(nchunks * (CINP / kC));
+  switch (g_wslab_nbuf) {
+    case 4:
+      wgrad_slab_kernel<4><<<grid, 64 * kWaves, 0, stream>>>(G, X, part, bpart, R, WP, GC, CIN,
+                                                             spc, CINP);
+      break;
+    case 5:
+      wgrad_slab_kernel<5><<<grid, 64 * kWaves, 0, stream>>>(G, X, part, bpart, R, WP, GC, CIN,
+                                                             spc, CINP);
+      break;
+    default:
+      wgrad_slab_kernel<3><<<grid, 64 * kWaves, 0, stream>>>(G, X, part, bpart, R, WP, GC, CIN,
+                                                             spc, CINP);
+  }
   return (int)hipGetLastError();
 }

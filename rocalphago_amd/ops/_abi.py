@@ -47,6 +47,7 @@ SIGNATURES = {
     "rag_conv_slab_mode": [I],
     "rag_conv_order": [I],
     "rag_conv_tap_mode": [I],
+    "rag_wgrad_slab_nbuf": [I],
 }
 
 RESTYPES = {"rag_conv_wgrad_workspace": SZ, "rag_head_bwd_workspace": SZ,

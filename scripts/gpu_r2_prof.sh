@@ -1,0 +1,6 @@
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+mkdir -p $R/gpurun_out/prof
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof/sl -- python3 $R/bench.py --steps 20 --warmup 3 --no-mcts > $R/gpurun_out/prof/sl.log 2>&1 && \
+timeout -k 10 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE --output-format csv -d $R/gpurun_out/prof/pmc -- python3 $R/scripts/dbg/conv_ab.py > $R/gpurun_out/prof/pmc.log 2>&1
