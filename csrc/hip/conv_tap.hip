@@ -43,6 +43,60 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// epilogue (as conv_pipe): lane owns channels n..n+3 of pixel m for every (j, i) tile
+__device__ __forceinline__ void epilogue(const f32x4 (&acc)[kNT][kMT], int mw, int nw, int M,
+                                         int S, int WO, int HO, int YC, int HM,
+                                         const float* __restrict__ bias,
+                                         const bf16* __restrict__ res, int relu,
+                                         const bf16* __restrict__ mask, bf16* __restrict__ Y,
+                                         int frow, int fq) {
+  const int S2 = S * S;
+#pragma unroll
+  for (int i = 0; i < kMT; ++i) {
+    const int m = mw + i * 16 + frow;
+    if (m >= M) continue;
+    const int b = m / S2;
+    const int rem = m - b * S2;
+    const int pi = rem / S;
+    const int pj = rem - pi * S;
+    const size_t orow = (size_t)((b * WO + pi + HO) * WO + pj + HO) * YC;
+    const int WMK = S + 2 * HM;
+    const size_t mrow = (size_t)((b * WMK + pi + HM) * WMK + pj + HM) * YC;
+#pragma unroll
+    for (int j = 0; j < kNT; ++j) {
+      const int n = nw + j * 16 + fq * 4;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[j][i][r];
+      if (bias) {
+        const float4 bb = *reinterpret_cast<const float4*>(bias + n);
+        v[0] += bb.x;
+        v[1] += bb.y;
+        v[2] += bb.z;
+        v[3] += bb.w;
+      }
+      if (res) {
+        const bf16x4 rv = *reinterpret_cast<const bf16x4*>(res + orow + n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += (float)rv[r];
+      }
+      if (relu) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      }
+      if (mask) {
+        const bf16x4 mk = *reinterpret_cast<const bf16x4*>(mask + mrow + n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = ((float)mk[r] > 0.f) ? v[r] : 0.f;
+      }
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (bf16)v[r];
+      *reinterpret_cast<bf16x4*>(Y + orow + n) = o;
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256, 2)
 conv_tap_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                 const float* __restrict__ bias, bf16* __restrict__ Y,
@@ -173,65 +227,184 @@ conv_tap_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
     }
   }
 
-  // epilogue (as conv_pipe): lane owns channels n..n+3 of pixel m for every (j, i) tile
-#pragma unroll
-  for (int i = 0; i < kMT; ++i) {
-    const int m = m0 + wm * (16 * kMT) + i * 16 + frow;
-    if (m >= M) continue;
+  epilogue(acc, m0 + wm * (16 * kMT), n0 + wn * (16 * kNT), M, S, WO, HO, YC, HM, bias, res, relu,
+           mask, Y, frow, fq);
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// 8-wave variant: one 512-thread block per CU owns 384 pixels x 192 channels (waves 4 (M) x 2 (N)
+// of 96 x 96, the same wave tile), so every weight tile is staged once per 384 pixels instead of
+// once per 192, and the weight ring is NB deep (NB-1 steps in flight, against the ~1 us LDS-DMA
+// latency under load: MI355X_MICROARCH.md 'ldsdma-fill'). Slab: <= 554 rows for any 384-pixel
+// run, staged as 640 rows (5 glds per wave). Weight tile: 12 glds per step, 2 for waves 0-3 and
+// 1 for waves 4-7 (the counted waits use each wave's own count).
+constexpr int k8BM = 384;
+constexpr int k8SlabRows = 640;
+constexpr int k8Slab = k8SlabRows * kBK;
+constexpr int k8AL = k8SlabRows / 128;
+
+__device__ __forceinline__ void wait_vm_rt(int n) {
+  switch (n) {
+    case 0: wait_vm<0>(); break;
+    case 1: wait_vm<1>(); break;
+    case 2: wait_vm<2>(); break;
+    case 3: wait_vm<3>(); break;
+    case 4: wait_vm<4>(); break;
+    case 5: wait_vm<5>(); break;
+    case 6: wait_vm<6>(); break;
+    case 7: wait_vm<7>(); break;
+    case 8: wait_vm<8>(); break;
+    case 9: wait_vm<9>(); break;
+    case 10: wait_vm<10>(); break;
+    case 11: wait_vm<11>(); break;
+    case 12: wait_vm<12>(); break;
+    default: wait_vm<13>(); break;
+  }
+}
+
+template <int NB>
+__global__ void __launch_bounds__(512)
+conv_tap8_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
+                 const float* __restrict__ bias, bf16* __restrict__ Y,
+                 const bf16* __restrict__ mask, const bf16* __restrict__ res, int M, int S,
+                 int WI, int shift, int WO, int HO, int CIN, int WROWS, int YC, int relu, int HM,
+                 long total_rows) {
+  constexpr int kL = 2 * k8Slab + NB * kBTile;
+  __shared__ __attribute__((aligned(16))) bf16 lds[kL];
+  const int lane = lane_id();
+  const int w = wave_id();
+  const int wm = w & 3, wn = w >> 2;
+  const int nblk_m = (M + k8BM - 1) / k8BM;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bm = bid % nblk_m, bn = bid / nblk_m;
+  const int m0 = bm * k8BM;
+  const int n0 = bn * kBN;
+  const int S2 = S * S;
+  auto prow = [&](int m) {
     const int b = m / S2;
     const int rem = m - b * S2;
-    const int pi = rem / S;
-    const int pj = rem - pi * S;
-    const size_t orow = (size_t)((b * WO + pi + HO) * WO + pj + HO) * YC;
-    const int WMK = S + 2 * HM;
-    const size_t mrow = (size_t)((b * WMK + pi + HM) * WMK + pj + HM) * YC;
+    const int i = rem / S;
+    const int j = rem - i * S;
+    return (long)(b * WI + i + shift) * WI + j + shift;
+  };
+  const long base = prow(m0);
+
+  const bf16* asrc[k8AL];
 #pragma unroll
-    for (int j = 0; j < kNT; ++j) {
-      const int n = n0 + wn * (16 * kNT) + j * 16 + fq * 4;
-      float v[4];
+  for (int k = 0; k < k8AL; ++k) {
+    const int r = (w + 8 * k) * 16 + (lane >> 2);
+    long g = base + r;
+    g = g < total_rows ? g : total_rows - 1;
+    asrc[k] = X + g * CIN + (((lane & 3) ^ swz4(r)) * 8);
+  }
+  // weight rows: instruction i = w (all waves) and i = 8 + w (waves 0-3) of the 12 per step
+  const int bl = w < 4 ? 2 : 1;
+  const bf16* bsrc[2];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = acc[j][i][r];
-      if (bias) {
-        const float4 bb = *reinterpret_cast<const float4*>(bias + n);
-        v[0] += bb.x;
-        v[1] += bb.y;
-        v[2] += bb.z;
-        v[3] += bb.w;
+  for (int k = 0; k < 2; ++k) {
+    const int i = w + 8 * k;
+    const int r = (i < 12 ? i : 0) * 16 + (lane >> 2);
+    bsrc[k] = Wt + (long)(n0 + r) * CIN + (((lane & 3) ^ swz4(r)) * 8);
+  }
+  const long tap_stride = (long)WROWS * CIN;
+  auto stage_a = [&](int q) {
+    bf16* dst = lds + (q & 1) * k8Slab;
+#pragma unroll
+    for (int k = 0; k < k8AL; ++k) glds16(asrc[k] + q * kBK, dst + (w + 8 * k) * 16 * kBK);
+  };
+  auto stage_b = [&](int s) {
+    const int q = s / 9, t = s - q * 9;
+    bf16* dst = lds + 2 * k8Slab + (s % NB) * kBTile;
+    const long off = t * tap_stride + q * kBK;
+    glds16(bsrc[0] + off, dst + w * 16 * kBK);
+    if (w < 4) glds16(bsrc[1] + off, dst + (8 + w) * 16 * kBK);
+  };
+
+  const int frow = lane & 15;
+  const int fq = lane >> 4;
+  int prel[kMT];
+#pragma unroll
+  for (int i = 0; i < kMT; ++i) {
+    int m = m0 + wm * (16 * kMT) + i * 16 + frow;
+    m = m < M ? m : M - 1;
+    prel[i] = (int)(prow(m) - base);
+  }
+  int boffs[kNT];
+#pragma unroll
+  for (int j = 0; j < kNT; ++j) {
+    const int row = wn * (16 * kNT) + j * 16 + frow;
+    boffs[j] = row * kBK + ((fq ^ swz4(row)) * 8);
+  }
+
+  f32x4 acc[kNT][kMT];
+#pragma unroll
+  for (int j = 0; j < kNT; ++j)
+#pragma unroll
+    for (int i = 0; i < kMT; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int cchunks = CIN / kBK;
+  const int nsteps = 9 * cchunks;
+  constexpr int D = NB - 1;  // weight tiles in flight ahead of the current step
+  stage_a(0);
+#pragma unroll
+  for (int k = 0; k < D; ++k)
+    if (k < nsteps) stage_b(k);
+
+  for (int q = 0; q < cchunks; ++q) {
+    const bool more = q + 1 < cchunks;
+    const bf16* slab = lds + (q & 1) * k8Slab;
+    int ky = 0, kx = 0;
+#pragma unroll 1
+    for (int t = 0; t < 9; ++t) {
+      const int s = q * 9 + t;
+      // younger than B(s): B(s+1 .. s+D-1) and, at taps 1..D, the next chunk's slab (issued at
+      // tap 0 after B(q*9+D))
+      int yb = nsteps - 1 - s;
+      yb = yb < D - 1 ? yb : D - 1;
+      wait_vm_rt(yb * bl + ((more && t >= 1 && t <= D) ? k8AL : 0));
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (s + D < nsteps) stage_b(s + D);
+      if (t == 0 && more) stage_a(q + 1);
+      const bf16* bt = lds + 2 * k8Slab + (s % NB) * kBTile;
+      const int toff = ky * WI + kx;
+      bf16x8 xa[kMT], wb[kNT];
+#pragma unroll
+      for (int i = 0; i < kMT; ++i) {
+        const int r = prel[i] + toff;
+        xa[i] = *reinterpret_cast<const bf16x8*>(slab + r * kBK + ((fq ^ swz4(r)) * 8));
       }
-      if (res) {
-        const bf16x4 rv = *reinterpret_cast<const bf16x4*>(res + orow + n);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += (float)rv[r];
+      for (int j = 0; j < kNT; ++j) wb[j] = *reinterpret_cast<const bf16x8*>(bt + boffs[j]);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < kNT; ++j)
+#pragma unroll
+        for (int i = 0; i < kMT; ++i) acc[j][i] = mfma16(wb[j], xa[i], acc[j][i]);
+      __builtin_amdgcn_s_setprio(0);
+      if (++kx == 3) {
+        kx = 0;
+        ++ky;
       }
-      if (relu) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-      }
-      if (mask) {
-        const bf16x4 mk = *reinterpret_cast<const bf16x4*>(mask + mrow + n);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = ((float)mk[r] > 0.f) ? v[r] : 0.f;
-      }
-      bf16x4 o;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = (bf16)v[r];
-      *reinterpret_cast<bf16x4*>(Y + orow + n) = o;
     }
   }
+  epilogue(acc, m0 + wm * (16 * kMT), n0 + wn * (16 * kNT), M, S, WO, HO, YC, HM, bias, res, relu,
+           mask, Y, frow, fq);
 }
 
 int g_tap_mode = -1;  // -1: read RAG_CONV_TAP on first use (default on)
 
-// Worst-case slab extent of a kBM-pixel run (host check of the kernel's kSlabRows assumption).
-int max_slab_rows(int S, int WI, int shift) {
+// Worst-case slab extent of a bm-pixel run (host check of the kernels' slab-row assumptions).
+int max_slab_rows(int S, int WI, int shift, int bm) {
   const int S2 = S * S;
   auto prow = [&](long m) {
     const long b = m / S2, rem = m - b * S2, i = rem / S, j = rem - i * S;
     return (b * WI + i + shift) * WI + j + shift;
   };
   long mx = 0;
-  for (long m0 = 0; m0 < 4L * S2 + kBM; m0 += kBM)
-    mx = std::max(mx, prow(m0 + kBM - 1) + 2 * WI + 2 - prow(m0) + 1);
+  for (long m0 = 0; m0 < (long)S2 * bm + bm; m0 += bm)
+    mx = std::max(mx, prow(m0 + bm - 1) + 2 * WI + 2 - prow(m0) + 1);
   return (int)mx;
 }
 
@@ -245,6 +418,10 @@ RAG_API int rag_conv_tap_mode(int mode) {
 
 // Returns true if the tap-slab kernel handled the launch: 3x3, 192-multiple output channels,
 // input channels a multiple of 32, and every 192-pixel run's nine-tap slab fits kSlabRows.
+// Returns true if a tap-slab kernel handled the launch: 3x3, 192-multiple output channels,
+// input channels a multiple of 32, and every pixel run's nine-tap slab fits the kernel's slab.
+// Mode (RAG_CONV_TAP / rag_conv_tap_mode): 0 off, 1 = 4-wave 192-pixel kernel (default),
+// 2 / 3 = 8-wave 384-pixel kernel with a 4- / 5-deep weight ring (measured slower: docs/KERNELS.md).
 bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* y,
                          const bf16* mk, const bf16* res, int M, int S, int WI, int shift, int WO,
                          int HO, int CIN, int COUTP, int YC, int KS, int relu, int HM, long total_rows,
@@ -254,11 +431,23 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
     g_tap_mode = e ? atoi(e) : 1;
   }
   if (!g_tap_mode || KS != 3 || COUTP % kBN || CIN % kBK || CIN < kBK) return false;
-  static int cached_key = -1, cached_rows = 0;
+  static int cached_key = -1, cached_rows = 0, cached_rows8 = 0;
   const int key = S * 4096 + WI * 8 + shift;
   if (key != cached_key) {
-    cached_rows = max_slab_rows(S, WI, shift);
+    cached_rows = max_slab_rows(S, WI, shift, kBM);
+    cached_rows8 = max_slab_rows(S, WI, shift, k8BM);
     cached_key = key;
+  }
+  if ((g_tap_mode == 2 || g_tap_mode == 3) && cached_rows8 <= k8SlabRows) {
+    const int nblk_m = (M + k8BM - 1) / k8BM;
+    dim3 grid(nblk_m * (COUTP / kBN));
+    if (g_tap_mode == 3)
+      conv_tap8_kernel<5><<<grid, 512, 0, stream>>>(x, w, bias, y, mk, res, M, S, WI, shift, WO,
+                                                    HO, CIN, COUTP, YC, relu, HM, total_rows);
+    else
+      conv_tap8_kernel<4><<<grid, 512, 0, stream>>>(x, w, bias, y, mk, res, M, S, WI, shift, WO,
+                                                    HO, CIN, COUTP, YC, relu, HM, total_rows);
+    return true;
   }
   if (cached_rows > kSlabRows) return false;
   const int nblk_m = (M + kBM - 1) / kBM;

@@ -1,6 +1,7 @@
 """A/B of the forward/dgrad conv kernels in one process, interleaved rounds (guide rule 24):
 variant 0 = conv_pipe tap-major, 1 = conv_pipe channel-chunk-major, 2 = conv_tap (tap-shared
-slab, 3x3 only). 3x3 192->192 fwd and dgrad and 5x5 48->192 fwd at B=256, plus an output check
+slab, 3x3 only), 3 / 4 = 8-wave 384-pixel conv_tap8 with a 4- / 5-deep weight ring (variant v
+selects rag_conv_tap_mode(v - 1)). 3x3 192->192 fwd and dgrad and 5x5 48->192 fwd at B=256, plus an output check
 of every variant against an fp32 torch reference."""
 import json
 import os
@@ -48,11 +49,11 @@ for (cin, cout, ks) in [(192, 192, 3), (48, 192, 5)]:
         cases["dgrad3"] = (lambda g=g, wb=wb, dx=dx, xp=xp, cinp=cinp, coutp=coutp:
                            ops.conv_igemm(g, wb, None, dx, B, S, 1, 1, coutp, cinp, 3, False,
                                           mask=xp), dx)
-VARIANTS = (0, 1, 2)
+VARIANTS = tuple(int(v) for v in os.environ.get("VARIANTS", "1,2,3,4").split(","))
 
 
 def select(v):
-    _lib().rag_conv_tap_mode(1 if v == 2 else 0)
+    _lib().rag_conv_tap_mode(max(v - 1, 0))
     _lib().rag_conv_order(1 if v >= 1 else 0)
 
 

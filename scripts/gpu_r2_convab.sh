@@ -1,7 +1,6 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-mkdir -p $R/gpurun_out/cab
+mkdir -p $R/gpurun_out/cab2
 cd $R
-timeout -k 10 120 python scripts/dbg/conv_ab.py > gpurun_out/cab/ab.log 2>&1 && \
-timeout -k 10 300 python -u -m pytest tests/test_hip_kernels.py tests/test_gpu_models.py -x -q --timeout 120 --timeout-method thread > gpurun_out/cab/tests.log 2>&1 && \
-timeout -k 10 200 python bench.py --no-mcts > gpurun_out/cab/bench.log 2>&1
+VARIANTS=2,8,9 timeout -k 10 120 python scripts/dbg/conv_ab.py > gpurun_out/cab2/ab.log 2>&1
+
