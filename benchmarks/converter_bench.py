@@ -1,0 +1,60 @@
+"""SGF -> HDF5 conversion throughput (games/s and positions/s): the bulk native converter at
+1..N threads against the python replay, on copies of the reference fixture games (48 planes,
+19x19; the reference itself converts one game at a time in python, game_converter.py:102-140)."""
+import argparse
+import glob
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from rocalphago_amd.features.converter import GameConverter  # noqa: E402
+from rocalphago_amd.features.preprocessing import DEFAULT_FEATURES  # noqa: E402
+
+REF = "/root/reference/tests/test_data/sgf"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--copies", type=int, default=40)
+    ap.add_argument("--threads", default="1,4,16")
+    ap.add_argument("--sgf-dir", default=REF)
+    args = ap.parse_args()
+    src = sorted(glob.glob(os.path.join(args.sgf_dir, "*.sgf")))
+    d = tempfile.mkdtemp()
+    try:
+        files = []
+        for k in range(args.copies):
+            for f in src:
+                dst = os.path.join(d, "%03d_%s" % (k, os.path.basename(f)))
+                shutil.copy(f, dst)
+                files.append(dst)
+        conv = GameConverter(list(DEFAULT_FEATURES))
+        out = {"games": len(files), "features": 48}
+        t = time.perf_counter()
+        npos = 0
+        for f in files[:len(src)]:
+            st, ac, _ = conv._python_game(f, 19)
+            npos += len(ac)
+        dt = time.perf_counter() - t
+        out["python_games_per_s"] = round(len(src) / dt, 2)
+        out["python_positions_per_s"] = round(npos / dt, 1)
+        for nt in [int(x) for x in args.threads.split(",")]:
+            t = time.perf_counter()
+            conv.sgfs_to_hdf5(files, os.path.join(d, "o%d.h5" % nt), nthreads=nt, batch=64)
+            dt = time.perf_counter() - t
+            out["native_games_per_s_t%d" % nt] = round(len(files) / dt, 2)
+            size = os.path.getsize(os.path.join(d, "o%d.h5" % nt))
+            out["native_positions_per_s_t%d" % nt] = round(npos * args.copies / dt, 1)
+            out["hdf5_bytes"] = size
+        print(json.dumps(out))
+    finally:
+        shutil.rmtree(d)
+
+
+if __name__ == "__main__":
+    main()

@@ -15,6 +15,9 @@ namespace rag {
 size_t lzf_decompress(const uint8_t* in, size_t n, uint8_t* out, size_t cap);
 size_t lzf_compress(const uint8_t* in, size_t n, uint8_t* out, size_t cap);
 void register_search(py::module_& m);
+int convert_sgf_game(const char* text, size_t len, int bd_size,
+                     const std::shared_ptr<const Zobrist>& zob, const int* fids, int nf,
+                     std::vector<uint8_t>& states, std::vector<uint8_t>& actions);
 void register_rollout(py::module_& m);
 }  // namespace rag
 
@@ -284,6 +287,45 @@ PYBIND11_MODULE(_rocgo, m) {
         return out;
       },
       py::arg("board"), py::arg("copying") = false);
+
+  // Bulk SGF conversion (converter.cpp): games converted in parallel on the shared pool.
+  // Returns one (status, states uint8 [n, F, S, S], actions uint8 [n, 2]) per game; status 0 ok,
+  // 1 illegal move (positions up to and including it), 3 = convert this game in python.
+  m.def(
+      "convert_games",
+      [](const std::vector<py::bytes>& texts, const std::vector<int>& fids, int bd_size,
+         py::array_t<uint64_t, py::array::c_style> zw, py::array_t<uint64_t, py::array::c_style> zb,
+         int nthreads) {
+        auto zob = make_zobrist(zw, zb);
+        const int n = (int)texts.size();
+        std::vector<std::string> buf(n);
+        for (int i = 0; i < n; ++i) buf[i] = texts[i];
+        std::vector<std::vector<uint8_t>> st(n), ac(n);
+        std::vector<int> status(n, 0);
+        {
+          py::gil_scoped_release nogil;
+          parallel_for(n, nthreads, [&](int i) {
+            status[i] = convert_sgf_game(buf[i].data(), buf[i].size(), bd_size, zob, fids.data(),
+                                         (int)fids.size(), st[i], ac[i]);
+          });
+        }
+        const int F = total_planes(fids), P = bd_size * bd_size;
+        py::list out;
+        for (int i = 0; i < n; ++i) {
+          const py::ssize_t rows = (py::ssize_t)(ac[i].size() / 2);
+          py::array_t<uint8_t> sa({rows, (py::ssize_t)F, (py::ssize_t)bd_size,
+                                   (py::ssize_t)bd_size});
+          py::array_t<uint8_t> aa({rows, (py::ssize_t)2});
+          if (rows) {
+            std::memcpy(sa.mutable_data(), st[i].data(), (size_t)rows * F * P);
+            std::memcpy(aa.mutable_data(), ac[i].data(), (size_t)rows * 2);
+          }
+          out.append(py::make_tuple(status[i], sa, aa));
+        }
+        return out;
+      },
+      py::arg("texts"), py::arg("fids"), py::arg("bd_size"), py::arg("zobrist_white"),
+      py::arg("zobrist_black"), py::arg("nthreads") = 8);
 
   m.def("feature_planes", &feature_planes);
 

@@ -1,31 +1,75 @@
-"""SGF -> HDF5 training-data converter — reference AlphaGo/preprocessing/game_converter.py.
+"""SGF -> HDF5 training-data converter (reference AlphaGo/preprocessing/game_converter.py API).
 
-Output layout (SURVEY §2.5 c), written by our own HDF5 writer (io/h5lite.py):
+Bulk path: game files are read in batches, the native converter (csrc/engine/converter.cpp)
+replays and featurises every game of a batch in parallel on the shared thread pool, and the
+rows are appended to the datasets in file order as whole 64-row LZF chunks (io/h5lite.py
+``WDataset.append``). A game the native parser does not reproduce exactly (parse error, a board
+size other than ``bd_size``, non-ASCII syntax, unusual coordinates) is converted by the Python
+replay below instead, which raises and is reported exactly as by the reference.
+
+Output layout (SURVEY §2.5 c, a file-format contract):
   states   uint8 (N, F, S, S), maxshape (None, F, S, S), chunks (64, F, S, S), LZF
   actions  uint8 (N, 2) as (x, y), chunks (1024, 2), LZF
   file_offsets/<path with '/' -> ':'> = [start, length]
   features = "board,ones,..." (comma-joined feature list)
-The file is written to ``.tmp.<name>`` and atomically renamed on success; per-game errors are
-handled like the reference (IllegalMove drops the remainder of a game, parse errors and board
-size mismatches skip the game, anything else warns when ``ignore_errors``).
-
-Speed: features for all positions of a game are computed by the native engine; with
-``workers > 1`` games are converted in parallel processes (positions streamed in file order).
+The file is written as ``.tmp.<name>`` and renamed when complete. Per-game outcomes follow the
+reference: an illegal move keeps the game's positions up to it, unparsable games and games of
+another board size are skipped, anything else is a warning (``ignore_errors``) or raised.
 """
 import os
 import sys
+import time
 import warnings
 
 import numpy as np
 
+from .._native import engine as _engine
 from ..engine import gamestate as go
 from ..io import h5lite, sgf
 from ..utils.go_util import sgf_iter_states
 from .preprocessing import DEFAULT_FEATURES, Preprocess
 
+_rg = _engine()
+_NATIVE_OK, _NATIVE_ILLEGAL = 0, 1
+
 
 class SizeMismatchError(Exception):
     pass
+
+
+class _Sink(object):
+    """The output file: datasets + per-file offsets, rows appended in order."""
+
+    def __init__(self, path, features, n_planes, size):
+        self.path = path
+        self.f = h5lite.File(path, "w")
+        shp = (n_planes, size, size)
+        self.states = self.f.require_dataset(
+            "states", dtype=np.uint8, shape=(0,) + shp, maxshape=(None,) + shp, exact=False,
+            chunks=(64,) + shp, compression="lzf")
+        self.actions = self.f.require_dataset(
+            "actions", dtype=np.uint8, shape=(0, 2), maxshape=(None, 2), exact=False,
+            chunks=(1024, 2), compression="lzf")
+        self.offsets = self.f.require_group("file_offsets")
+        self.f["features"] = np.bytes_(",".join(features))
+        self.rows = 0
+
+    def add(self, file_name, states, actions):
+        n = len(actions)
+        if n == 0:
+            return 0
+        self.states.append(states)
+        self.actions.append(np.asarray(actions, dtype=np.uint8).reshape(n, 2))
+        self.offsets[file_name.replace("/", ":")] = np.array([self.rows, n], dtype=np.int64)
+        self.rows += n
+        return n
+
+    def close(self):
+        self.f.close()
+
+    def abort(self):
+        self.f._fh.close()
+        os.remove(self.path)
 
 
 class GameConverter(object):
@@ -33,136 +77,151 @@ class GameConverter(object):
     def __init__(self, features):
         self.feature_processor = Preprocess(features)
         self.n_features = self.feature_processor.output_dim
+        self.games_per_s = None
 
+    # ---- reference API: one game as a python generator --------------------------------------
     def convert_game(self, file_name, bd_size):
         """Yield (features (1, F, S, S), move (x, y)) for every non-pass move of the game."""
-        with open(file_name, 'r') as file_object:
-            state_action_iterator = sgf_iter_states(file_object.read(), include_end=False)
-        for (state, move, player) in state_action_iterator:
+        with open(file_name, "r") as fh:
+            replay = sgf_iter_states(fh.read(), include_end=False)
+        for state, move, _player in replay:
             if state.size != bd_size:
                 raise SizeMismatchError()
-            if move != go.PASS_MOVE:
-                nn_input = self.feature_processor.state_to_tensor(state)
-                yield (nn_input, move)
+            if move is not go.PASS_MOVE:
+                yield self.feature_processor.state_to_tensor(state), move
 
-    def _game_arrays(self, file_name, bd_size):
-        """All (states uint8 [n,F,S,S], actions uint8 [n,2]) of a game, plus the error."""
-        states, actions, err = [], [], None
+    def _python_game(self, file_name, bd_size):
+        """(states [n, F, S, S] uint8, actions [(x, y)], the exception that ended the game)."""
+        planes, moves = [], []
         try:
-            for st, mv in self.convert_game(file_name, bd_size):
-                states.append(st[0].astype(np.uint8))
-                actions.append(mv)
-        except Exception as e:  # classified by the caller, like the reference
-            err = e
-        return states, actions, err
+            for tensor, move in self.convert_game(file_name, bd_size):
+                planes.append(tensor[0].astype(np.uint8))
+                moves.append(move)
+        except Exception as e:  # classified by the caller
+            return planes, moves, e
+        return planes, moves, None
 
-    def sgfs_to_hdf5(self, sgf_files, hdf5_file, bd_size=19, ignore_errors=True, verbose=False):
-        tmp_file = os.path.join(os.path.dirname(hdf5_file), ".tmp." + os.path.basename(hdf5_file))
-        h5f = h5lite.File(tmp_file, 'w')
-        try:
-            states = h5f.require_dataset(
-                'states', dtype=np.uint8, shape=(1, self.n_features, bd_size, bd_size),
-                maxshape=(None, self.n_features, bd_size, bd_size), exact=False,
-                chunks=(64, self.n_features, bd_size, bd_size), compression="lzf")
-            actions = h5f.require_dataset(
-                'actions', dtype=np.uint8, shape=(1, 2), maxshape=(None, 2), exact=False,
-                chunks=(1024, 2), compression="lzf")
-            file_offsets = h5f.require_group('file_offsets')
-            h5f['features'] = np.bytes_(','.join(self.feature_processor.feature_list))
-            if verbose:
-                print("created HDF5 dataset in {}".format(tmp_file))
-            next_idx = 0
-            for file_name in sgf_files:
-                if verbose:
-                    print(file_name)
-                n_pairs = 0
-                file_start_idx = next_idx
-                game_states, game_actions, err = self._game_arrays(file_name, bd_size)
-                if isinstance(err, (sgf.SGFParseError, SizeMismatchError)):
-                    game_states, game_actions = [], []
-                for st, mv in zip(game_states, game_actions):
-                    if next_idx >= len(states):
-                        states.resize((next_idx + 1, self.n_features, bd_size, bd_size))
-                        actions.resize((next_idx + 1, 2))
-                    states[next_idx] = st
-                    actions[next_idx] = mv
-                    n_pairs += 1
-                    next_idx += 1
-                if isinstance(err, go.IllegalMove):
-                    warnings.warn("Illegal Move encountered in %s\n"
-                                  "\tdropping the remainder of the game" % file_name)
-                elif isinstance(err, sgf.SGFParseError):
-                    warnings.warn("Could not parse %s\n\tdropping game" % file_name)
-                elif isinstance(err, SizeMismatchError):
-                    warnings.warn("Skipping %s; wrong board size" % file_name)
-                elif err is not None:
-                    if ignore_errors:
-                        warnings.warn("Unkown exception with file %s\n\t%s" % (file_name, err),
-                                      stacklevel=2)
-                    else:
-                        raise err
-                if n_pairs > 0:
-                    file_name_key = file_name.replace('/', ':')
-                    file_offsets[file_name_key] = np.array([file_start_idx, n_pairs],
-                                                           dtype=np.int64)
-                    if verbose:
-                        print("\t%d state/action pairs extracted" % n_pairs)
-                elif verbose:
-                    print("\t-no usable data-")
-            if next_idx == 0:
-                states.resize((0, self.n_features, bd_size, bd_size))
-                actions.resize((0, 2))
-        except Exception as e:
-            print("sgfs_to_hdf5 failed")
-            h5f._fh.close()
-            os.remove(tmp_file)
-            raise e
+    # ---- bulk conversion ----------------------------------------------------------------------
+    def _batch(self, names, bd_size, nthreads):
+        """Per game of a batch: (states array or list, actions, error or None)."""
+        texts, native_idx = [], []
+        for i, name in enumerate(names):
+            try:
+                with open(name, "rb") as fh:
+                    raw = fh.read()
+                raw.decode("utf-8")  # undecodable files take the python path (and its error)
+            except (OSError, UnicodeDecodeError):
+                continue
+            texts.append(raw)
+            native_idx.append(i)
+        done = [None] * len(names)
+        if texts:
+            zw, zb, _ = go._zobrist(bd_size)
+            res = _rg.convert_games(texts, list(self.feature_processor.feature_ids), bd_size,
+                                    np.ascontiguousarray(zw.ravel()),
+                                    np.ascontiguousarray(zb.ravel()), nthreads)
+            for i, (status, st, ac) in zip(native_idx, res):
+                if status == _NATIVE_OK:
+                    done[i] = (st, ac, None)
+                elif status == _NATIVE_ILLEGAL:
+                    done[i] = (st, ac, go.IllegalMove("illegal move in SGF replay"))
+        for i, name in enumerate(names):
+            if done[i] is None:
+                done[i] = self._python_game(name, bd_size)
+        return done
+
+    def sgfs_to_hdf5(self, sgf_files, hdf5_file, bd_size=19, ignore_errors=True, verbose=False,
+                     batch=64, nthreads=8):
+        tmp = os.path.join(os.path.dirname(hdf5_file), ".tmp." + os.path.basename(hdf5_file))
+        sink = _Sink(tmp, self.feature_processor.feature_list, self.n_features, bd_size)
         if verbose:
-            print("finished. renaming %s to %s" % (tmp_file, hdf5_file))
-        h5f.close()
-        os.rename(tmp_file, hdf5_file)
+            print("created HDF5 dataset in {}".format(tmp))
+        t0, ngames = time.time(), 0
+        files = iter(sgf_files)
+        try:
+            while True:
+                names = [n for _, n in zip(range(batch), files)]
+                if not names:
+                    break
+                for name, (states, moves, err) in zip(names, self._batch(names, bd_size,
+                                                                          nthreads)):
+                    ngames += 1
+                    if verbose:
+                        print(name)
+                    if isinstance(err, (sgf.SGFParseError, SizeMismatchError)):
+                        states, moves = [], []
+                    n = sink.add(name, states, moves)
+                    self._report(name, err, ignore_errors)
+                    if verbose:
+                        print("\t%d state/action pairs extracted" % n if n else
+                              "\t-no usable data-")
+        except Exception:
+            print("sgfs_to_hdf5 failed")
+            sink.abort()
+            raise
+        self.games_per_s = ngames / max(time.time() - t0, 1e-9)
+        if verbose:
+            print("finished (%.1f games/s). renaming %s to %s" % (self.games_per_s, tmp,
+                                                                 hdf5_file))
+        sink.close()
+        os.rename(tmp, hdf5_file)
+
+    @staticmethod
+    def _report(name, err, ignore_errors):
+        if err is None:
+            return
+        if isinstance(err, go.IllegalMove):
+            warnings.warn("Illegal Move encountered in %s\n\tdropping the remainder of the game"
+                          % name)
+        elif isinstance(err, sgf.SGFParseError):
+            warnings.warn("Could not parse %s\n\tdropping game" % name)
+        elif isinstance(err, SizeMismatchError):
+            warnings.warn("Skipping %s; wrong board size" % name)
+        elif ignore_errors:
+            warnings.warn("Unknown exception with file %s\n\t%s" % (name, err), stacklevel=2)
+        else:
+            raise err
+
+
+def _sgf_files(directory, recurse):
+    if not recurse:
+        return (os.path.join(directory, f) for f in sorted(os.listdir(directory))
+                if f.strip().endswith(".sgf"))
+    return (os.path.join(d, f) for d, _, fs in os.walk(directory) for f in sorted(fs)
+            if f.strip().endswith(".sgf"))
 
 
 def run_game_converter(cmd_line_args=None):
+    """CLI of the reference converter (game_converter.py:154-229), plus --threads."""
     import argparse
-    parser = argparse.ArgumentParser(
-        description='Prepare SGF Go game files for training the neural network model.',
+    ap = argparse.ArgumentParser(
+        description="Prepare SGF Go game files for training the neural network model.",
         epilog="Available features are: board, ones, turns_since, liberties, capture_size, "
                "self_atari_size, liberties_after, ladder_capture, ladder_escape, sensibleness, "
                "zeros, legal and color")
-    parser.add_argument("--features", "-f", help="Comma-separated list of features to compute and store or 'all'", default='all')  # noqa: E501
-    parser.add_argument("--outfile", "-o", help="Destination to write data (hdf5 file)", required=True)  # noqa: E501
-    parser.add_argument("--recurse", "-R", help="Set to recurse through directories searching for SGF files", default=False, action="store_true")  # noqa: E501
-    parser.add_argument("--directory", "-d", help="Directory containing SGF files to process. if not present, expects files from stdin", default=None)  # noqa: E501
-    parser.add_argument("--size", "-s", help="Size of the game board. SGFs not matching this are discarded with a warning", type=int, default=19)  # noqa: E501
-    parser.add_argument("--verbose", "-v", help="Turn on verbose mode", default=False, action="store_true")  # noqa: E501
-    if cmd_line_args is None:
-        args = parser.parse_args()
-    else:
-        args = parser.parse_args(cmd_line_args)
-    if args.features.lower() == 'all':
-        feature_list = list(DEFAULT_FEATURES)
-    else:
-        feature_list = args.features.split(",")
+    ap.add_argument("--features", "-f", default="all",
+                    help="Comma-separated list of features to compute and store or 'all'")
+    ap.add_argument("--outfile", "-o", required=True, help="Destination to write data (hdf5 file)")
+    ap.add_argument("--recurse", "-R", default=False, action="store_true",
+                    help="Set to recurse through directories searching for SGF files")
+    ap.add_argument("--directory", "-d", default=None,
+                    help="Directory containing SGF files to process. if not present, expects "
+                         "files from stdin")
+    ap.add_argument("--size", "-s", type=int, default=19,
+                    help="Size of the game board. SGFs not matching this are discarded with a "
+                         "warning")
+    ap.add_argument("--verbose", "-v", default=False, action="store_true",
+                    help="Turn on verbose mode")
+    ap.add_argument("--threads", type=int, default=8,
+                    help="native converter threads (games of a batch in parallel)")
+    args = ap.parse_args(cmd_line_args)
+    features = list(DEFAULT_FEATURES) if args.features.lower() == "all" else \
+        args.features.split(",")
     if args.verbose:
-        print("using features", feature_list)
-    converter = GameConverter(feature_list)
-
-    def _is_sgf(fname):
-        return fname.strip()[-4:] == ".sgf"
-
-    def _walk_all_sgfs(root):
-        for (dirpath, dirname, files) in os.walk(root):
-            for filename in sorted(files):
-                if _is_sgf(filename):
-                    yield os.path.join(dirpath, filename)
-
-    def _list_sgfs(path):
-        files = sorted(os.listdir(path))
-        return (os.path.join(path, f) for f in files if _is_sgf(f))
-
+        print("using features", features)
     if args.directory:
-        files = _walk_all_sgfs(args.directory) if args.recurse else _list_sgfs(args.directory)
+        files = _sgf_files(args.directory, args.recurse)
     else:
-        files = (f.strip() for f in sys.stdin if _is_sgf(f))
-    converter.sgfs_to_hdf5(files, args.outfile, bd_size=args.size, verbose=args.verbose)
+        files = (line.strip() for line in sys.stdin if line.strip().endswith(".sgf"))
+    GameConverter(features).sgfs_to_hdf5(files, args.outfile, bd_size=args.size,
+                                         verbose=args.verbose, nthreads=args.threads)

@@ -747,6 +747,32 @@ class WDataset(object):
         self._pending[i - self._pending_start] = value
         self._max_written = max(self._max_written, i + 1)
 
+    def append(self, rows):
+        """Append a block of rows at the end of a chunked dataset (grows it), copying whole
+        chunk-sized slices and flushing every chunk as soon as it is full."""
+        rows = np.asarray(rows, dtype=self.dtype)
+        if self.chunks is None or rows.shape[1:] != self._row_shape:
+            raise ValueError("append needs a chunked dataset and rows of shape %r" %
+                             (self._row_shape,))
+        start = self._max_written
+        n = rows.shape[0]
+        if start < self._pending_start:
+            raise NotImplementedError("h5lite chunked datasets are append-only")
+        if start + n > self.shape[0]:
+            self.resize((start + n,) + self._row_shape)
+        c = self.chunks[0]
+        done = 0
+        while done < n:
+            i = start + done
+            while i >= self._pending_start + c:
+                self._flush_pending()
+            off = i - self._pending_start
+            take = min(c - off, n - done)
+            self._pending[off:off + take] = rows[done:done + take]
+            done += take
+            self._max_written = i + take
+        return start
+
     def __getitem__(self, key):
         if self.chunks is None:
             return self._data[key]

@@ -1,10 +1,9 @@
-"""Board/SGF utilities — reference AlphaGo/util.py:1-231.
+"""Board/SGF utilities with the reference's AlphaGo/util.py interface (util.py:1-231).
 
-flatten_idx/unflatten_idx (util.py:11-18), SGF move parsing and game-state reconstruction
-(util.py:21-63,100-128), the simplified SGF writer (util.py:66-97) and the optional matplotlib
-heat-map (util.py:131-231).
+flatten_idx/unflatten_idx (util.py:11-18), SGF move parsing and game-state reconstruction on our
+own SGF parser (util.py:21-63,100-128), a main-line SGF writer (util.py:66-97 file contract) and
+an optional matplotlib heat map of a network's move distribution (util.py:131-231 signature).
 """
-import itertools
 import os
 
 import numpy as np
@@ -103,93 +102,102 @@ def sgf_to_gamestate(sgf_string):
     return gs
 
 
+def _sgf_point(move):
+    """SGF coordinate of a move: two lower-case letters (column, row) or 'tt' for a pass."""
+    if move is None:
+        return "tt"
+    return LETTERS[move[0]].lower() + LETTERS[move[1]].lower()
+
+
 def gamestate_to_sgf_string(gamestate, black_player_name='Unknown', white_player_name='Unknown',
                             size=19, komi=7.5):
-    str_list = ['(;GM[1]FF[4]CA[UTF-8]', 'SZ[{}]'.format(size), 'KM[{}]'.format(komi),
-                'PB[{}]'.format(black_player_name), 'PW[{}]'.format(white_player_name)]
-    cycle_string = 'BW'
-    if len(gamestate.handicaps) > 0:
-        cycle_string = 'WB'
-        str_list.append('HA[{}]'.format(len(gamestate.handicaps)))
-        str_list.append(';AB')
-        for handicap in gamestate.handicaps:
-            str_list.append('[{}{}]'.format(LETTERS[handicap[0]].lower(),
-                                            LETTERS[handicap[1]].lower()))
-    for move, color in zip(gamestate.history, itertools.cycle(cycle_string)):
-        str_list.append(';{}'.format(color))
-        if move is None:
-            str_list.append('[tt]')
-        else:
-            str_list.append('[{}{}]'.format(LETTERS[move[0]].lower(), LETTERS[move[1]].lower()))
-    str_list.append(')')
-    return ''.join(str_list)
+    """Main-line SGF of a game: a root node with the game info, one AB setup node for handicap
+    stones (then white moves first), and one node per history move. Same file contract as the
+    reference writer (util.py:66-97); read back by sgf_iter_states."""
+    info = [("GM", 1), ("FF", 4), ("CA", "UTF-8"), ("SZ", size), ("KM", komi),
+            ("PB", black_player_name), ("PW", white_player_name)]
+    handicaps = list(gamestate.handicaps)
+    if handicaps:
+        info.append(("HA", len(handicaps)))
+    nodes = [";" + "".join("%s[%s]" % kv for kv in info)]
+    if handicaps:
+        nodes.append(";AB" + "".join("[%s]" % _sgf_point(h) for h in handicaps))
+    colours = "WB" if handicaps else "BW"
+    nodes.extend(";%s[%s]" % (colours[k % 2], _sgf_point(mv))
+                 for k, mv in enumerate(gamestate.history))
+    return "(" + "".join(nodes) + ")"
 
 
 def save_gamestate_to_sgf(gamestate, path, filename, black_player_name='Unknown',
                           white_player_name='Unknown', size=19, komi=7.5):
-    """Simplified SGF writer (reference util.py:66-97)."""
+    """Write gamestate_to_sgf_string to path/filename (reference util.py:66-97 signature)."""
+    text = gamestate_to_sgf_string(gamestate, black_player_name, white_player_name, size, komi)
     with open(os.path.join(path, filename), "w") as f:
-        f.write(gamestate_to_sgf_string(gamestate, black_player_name, white_player_name, size,
-                                        komi))
+        f.write(text)
+
+
+def _axis_labels(size, western_column_notation):
+    """(x tick labels, y tick labels, x ticks on top) for a size x size board."""
+    numbers = list(range(1, size + 1))
+    if western_column_notation:
+        return numbers, numbers[::-1], False
+    columns = [c for c in LETTERS if c != 'I'][:size]
+    return columns, numbers, True
 
 
 def plot_network_output(scores, board, history, out_directory, output_file,
                         should_plot=False, western_column_notation=True):
-    """Heat-map of network output over the board (optional matplotlib dependency)."""
+    """Heat map of a network's move distribution over the board (reference util.py:131-231
+    signature; matplotlib is an optional dependency, imported on use).
+
+    Points holding at least 0.1 % of the probability mass are drawn as discs coloured by their
+    probability and labelled in percent; stones are drawn on top (black / white) and the last
+    move, if any, is marked with a small red square. The figure is saved to
+    out_directory/output_file (if given) and shown when should_plot is set."""
     try:
         import matplotlib
-        matplotlib.use("Agg") if not should_plot else None
+        if not should_plot:
+            matplotlib.use("Agg")
         import matplotlib.pyplot as plt
-        import matplotlib.cm as cm
-    except ImportError as e:
-        print('Failed to import matplotlib. This is an optional dependency; install it to use '
-              'the plotting functions.')
-        raise e
+    except ImportError:
+        print("plot_network_output needs matplotlib (an optional dependency)")
+        raise
     size = board.shape[0]
+    probs = np.asarray(scores, dtype=np.float64).reshape(size, size)
     fig, ax = plt.subplots(figsize=(10, 10))
-    plt.xlim([0, size + 1])
-    plt.ylim([0, size + 1])
-    ax.set_facecolor('#fec97b')
-    plt.gca().invert_yaxis()
-    ax.tick_params(axis='both', length=0, width=0)
-    if western_column_notation:
-        plt.xticks(range(1, size + 1), range(1, size + 1))
-        plt.yticks(range(1, size + 1), reversed(range(1, size + 1)))
-    else:
+    ax.set_xlim(0, size + 1)
+    ax.set_ylim(size + 1, 0)  # row 1 at the top
+    ax.set_facecolor("#e8b96a")
+    ax.tick_params(length=0)
+    xl, yl, top = _axis_labels(size, western_column_notation)
+    ax.set_xticks(range(1, size + 1))
+    ax.set_xticklabels(xl)
+    ax.set_yticks(range(1, size + 1))
+    ax.set_yticklabels(yl)
+    if top:
         ax.xaxis.tick_top()
-        plt.xticks(range(1, size + 1), [x for x in LETTERS[:size + 1] if x != 'I'])
-        plt.yticks(range(1, size + 1), range(1, size + 1))
-    for i in range(size):
-        plt.plot([1, size], [i + 1, i + 1], lw=1, color='k', zorder=0)
-        plt.plot([i + 1, i + 1], [1, size], lw=1, color='k', zorder=0)
-    reshaped = np.reshape(scores, (size, size))
-    xs, ys, vals = [], [], []
-    for i in range(size):
-        for j in range(size):
-            if reshaped[i][j] * 100 >= 0.1:
-                xs.append(i + 1)
-                ys.append(j + 1)
-                vals.append(reshaped[i][j])
-    norm = matplotlib.colors.Normalize(vmin=np.amin(scores), vmax=np.amax(scores))
-    coloring = cm.ScalarMappable(norm=norm, cmap=cm.cool).to_rgba(vals)
-    plt.scatter(xs, ys, marker='o', s=700, c=coloring, edgecolor='k', zorder=1)
-    for i, txt in enumerate(vals):
-        ax.annotate('{0:.1f}'.format(txt * 100), (xs[i], ys[i]), color='k', ha='center',
-                    va='center', size=10, zorder=3)
-    sx, sy, sc = [], [], []
-    for i in range(size):
-        for j in range(size):
-            if board[i][j] != go.EMPTY:
-                sx.append(i + 1)
-                sy.append(j + 1)
-                sc.append((0, 0, 0) if board[i][j] == go.BLACK else (1, 1, 1))
-    plt.scatter(sx, sy, marker='o', edgecolors='k', s=700, c=sc, zorder=4)
-    if len(history) != 0 and history[-1] != go.PASS_MOVE:
-        last = history[-1]
-        plt.scatter(last[0] + 1, last[1] + 1, marker='s', color='r', edgecolors='k', s=100,
-                    zorder=5)
+    grid = np.arange(1, size + 1)
+    for g in grid:
+        ax.plot([1, size], [g, g], color="black", linewidth=0.8, zorder=0)
+        ax.plot([g, g], [1, size], color="black", linewidth=0.8, zorder=0)
+    xi, yi = np.nonzero(probs >= 1e-3)
+    if len(xi):
+        val = probs[xi, yi]
+        ax.scatter(xi + 1, yi + 1, s=650, c=val, cmap="cool", vmin=probs.min(), vmax=probs.max(),
+                   edgecolors="black", zorder=1)
+        for x, y, v in zip(xi, yi, val):
+            ax.text(x + 1, y + 1, "%.1f" % (100 * v), ha="center", va="center", fontsize=9,
+                    zorder=3)
+    stones = np.asarray(board)
+    for colour, face in ((go.BLACK, "black"), (go.WHITE, "white")):
+        sx, sy = np.nonzero(stones == colour)
+        if len(sx):
+            ax.scatter(sx + 1, sy + 1, s=650, c=face, edgecolors="black", zorder=4)
+    if len(history) and history[-1] is not go.PASS_MOVE:
+        lx, ly = history[-1]
+        ax.scatter([lx + 1], [ly + 1], marker="s", s=90, c="red", edgecolors="black", zorder=5)
     if output_file is not None:
-        plt.savefig(os.path.join(out_directory, output_file), bbox_inches='tight')
+        fig.savefig(os.path.join(out_directory, output_file), bbox_inches="tight")
     if should_plot:
         plt.show()
-    plt.close()
+    plt.close(fig)

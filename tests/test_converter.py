@@ -1,0 +1,87 @@
+"""Bulk SGF converter (csrc/engine/converter.cpp through features/converter.py): the native
+replay gives exactly the python replay's planes, moves and per-game outcome (reference
+game_converter.py:32-151 semantics), on the fixture games and on edge cases."""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from rocalphago_amd.engine import gamestate as go
+from rocalphago_amd.features.converter import GameConverter, SizeMismatchError
+from rocalphago_amd.features.preprocessing import DEFAULT_FEATURES
+from rocalphago_amd.io import h5lite, sgf
+
+REF = "/root/reference/tests/test_data"
+
+CASES = {
+    "plain": "(;GM[1]SZ[9];B[cc];W[gg];B[];W[tt];B[cd])",
+    "root_setup_pl": "(;SZ[9]AB[aa][bb]AW[cc]PL[W];W[dd];B[ee])",
+    "rect_setup": "(;SZ[9]AB[aa:bb];W[dd];B[ee])",
+    "handicap_node": "(;SZ[9];AB[cc][gg];W[ee];B[ce])",
+    "late_setup": "(;SZ[9];B[ee];AB[aa]AW[ii];W[dd])",
+    "w_wins_tie": "(;SZ[9];W[ee]B[cc];B[dd])",
+    "illegal": "(;SZ[9];B[ee];W[ee];B[dd])",
+    "variation": "(;SZ[9];B[ee](;W[dd];B[cc])(;W[aa]))",
+    "escapes": "(;SZ[9]C[x \\] y];B[ee];W[ff])",
+    "wrong_size": "(;SZ[13];B[ee];W[ff])",
+    "parse_error": "(;SZ[9];B[ee];W[ff]",
+    "off_board": "(;SZ[9];B[jj];W[ff])",
+    "upper_case": "(;SZ[9];B[EE];W[Ff])",
+}
+
+
+def _compare(conv, files, size):
+    native = conv._batch(files, size, 4)
+    for f, (st, ac, err) in zip(files, native):
+        pst, pac, perr = conv._python_game(f, size)
+        assert type(err) is type(perr) or (isinstance(err, go.IllegalMove) and
+                                           isinstance(perr, go.IllegalMove)), f
+        assert [tuple(a) for a in ac] == [tuple(a) for a in pac], f
+        if len(pac):
+            assert np.array_equal(np.asarray(st), np.stack(pst)), f
+
+
+def test_fixture_games_match_python():
+    files = sorted(glob.glob(os.path.join(REF, "**", "*.sgf"), recursive=True))
+    assert len(files) >= 6
+    _compare(GameConverter(list(DEFAULT_FEATURES) + ["color"]), files, 19)
+
+
+def test_edge_cases_match_python(tmp_path):
+    files = []
+    for name, text in CASES.items():
+        p = tmp_path / (name + ".sgf")
+        p.write_text(text)
+        files.append(str(p))
+    _compare(GameConverter(list(DEFAULT_FEATURES)), files, 9)
+
+
+def test_bulk_file_outcomes(tmp_path):
+    files = []
+    for name in ("plain", "illegal", "wrong_size", "parse_error", "handicap_node"):
+        p = tmp_path / (name + ".sgf")
+        p.write_text(CASES[name])
+        files.append(str(p))
+    out = str(tmp_path / "o.h5")
+    conv = GameConverter(["board", "ones", "legal"])
+    with pytest.warns(UserWarning) as rec:
+        conv.sgfs_to_hdf5(files, out, bd_size=9, batch=2)
+    msgs = " ".join(str(w.message) for w in rec)
+    assert "Illegal Move" in msgs and "wrong board size" in msgs and "Could not parse" in msgs
+    f = h5lite.File(out)
+    keys = sorted(k.split(":")[-1] for k in f["file_offsets"].keys())
+    assert keys == ["handicap_node.sgf", "illegal.sgf", "plain.sgf"]
+    # illegal: B[ee] kept, then W[ee] (the illegal move's position is kept, as in the reference)
+    n = {k.split(":")[-1]: f["file_offsets"][k][()] for k in f["file_offsets"].keys()}
+    assert n["illegal.sgf"][1] == 2 and n["plain.sgf"][1] == 3
+    assert f["states"].shape == (sum(v[1] for v in n.values()), 5, 9, 9)
+    assert conv.games_per_s > 0
+    assert not os.path.exists(os.path.join(str(tmp_path), ".tmp.o.h5"))
+
+
+def test_classification_helpers():
+    with pytest.raises(ValueError):
+        GameConverter._report("x", ValueError("boom"), ignore_errors=False)
+    assert issubclass(SizeMismatchError, Exception)
+    assert issubclass(sgf.SGFParseError, Exception)
