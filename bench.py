@@ -188,12 +188,18 @@ def main():
                                         args.filters, args.layers, nparams)
         result["baseline_note"] = "no published baseline for the residual policy"
     if not args.no_mcts and args.model == "policy":
-        # one independent search per GPU (root parallelism); whole-job sims/s = sum over ranks.
+        # N = 1: the pipelined single-GPU search. N > 1: ONE search whose leaf waves are dealt
+        # to all N GPUs (search/distributed.py) — the whole job's sims/s is that search's.
         # Every rank reaches the all-reduce whether or not its measurement worked (no hang).
         r, err = None, None
         try:
-            from benchmarks.mcts_bench import measure
-            r = measure(dev, playouts=args.mcts_playouts)
+            if dp.world > 1:
+                from benchmarks.mcts_bench import measure_distributed
+                r = measure_distributed(dp, dev, playouts=args.mcts_playouts * dp.world)
+                r = r or {"sims_per_s": 0.0, "rollouts_per_s": 0.0}
+            else:
+                from benchmarks.mcts_bench import measure
+                r = measure(dev, playouts=args.mcts_playouts)
         except Exception as e:  # the SL metric stands on its own
             err = str(e)[:200]
         tot = torch.tensor([r["sims_per_s"] if r else 0.0,
@@ -205,8 +211,13 @@ def main():
             result["mcts_rollouts_per_s"] = round(float(tot[1]), 1)
             result["mcts_config"] = "APV-MCTS 19x19, policy 48x192x13 + value 49x192x13+FC256 " \
                                     "on GPU, lambda 0.5, %d GPU rollouts/leaf, wave %d, %d " \
-                                    "playouts/move, one search per GPU" % (
-                                        r["rollouts_per_leaf"], r["batch"], args.mcts_playouts)
+                                    "playouts/move, %s" % (
+                                        r["rollouts_per_leaf"] if "rollouts_per_leaf" in r
+                                        else 1, 256, args.mcts_playouts * dp.world,
+                                        "one search over %d GPUs" % dp.world if dp.world > 1
+                                        else "1 GPU")
+            if dp.is_root and "leaves_per_rank" in r:
+                result["mcts_leaves_per_rank"] = r["leaves_per_rank"]
         else:
             result["mcts_error"] = err or "MCTS measurement failed on %d rank(s)" % (
                 dp.world - int(tot[2]))

@@ -18,14 +18,37 @@ from rocalphago_amd.features.preprocessing import DEFAULT_FEATURES  # noqa: E402
 REF = "/root/reference/tests/test_data/sgf"
 
 
+def _synthetic_games(d, n):
+    import numpy as np
+    from rocalphago_amd._native import engine
+    from rocalphago_amd.engine.gamestate import GameState
+    from rocalphago_amd.utils.go_util import save_gamestate_to_sgf
+    rp = engine().RolloutPolicy()
+    rs = np.random.RandomState(0)
+    out = []
+    for g in range(n):
+        st = GameState()
+        for _ in range(int(rs.randint(150, 300))):
+            mv = rp.sample(st.native, int(rs.randint(1 << 30)))
+            st.do_move(None if mv < 0 else divmod(mv, 19))
+            if st.is_end_of_game:
+                break
+        name = "synthetic%d.sgf" % g
+        save_gamestate_to_sgf(st, d, name)
+        out.append(os.path.join(d, name))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--copies", type=int, default=40)
     ap.add_argument("--threads", default="1,4,16")
     ap.add_argument("--sgf-dir", default=REF)
     args = ap.parse_args()
-    src = sorted(glob.glob(os.path.join(args.sgf_dir, "*.sgf")))
     d = tempfile.mkdtemp()
+    src = sorted(glob.glob(os.path.join(args.sgf_dir, "*.sgf")))
+    if not src:  # no fixture games here: rollout-policy self-play games of 150-300 moves
+        src = _synthetic_games(d, 5)
     try:
         files = []
         for k in range(args.copies):

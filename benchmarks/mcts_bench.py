@@ -62,6 +62,53 @@ def measure(device, playouts=8192, warmup=512, moves=1, **kw):
     return out
 
 
+def measure_distributed(dp, device, playouts=8192, warmup=512, moves=1, filters=192,
+                        layers=12, batch=256, rollouts_per_leaf=1, lmbda=0.5, nthreads=16,
+                        seed=1, rollout_delay=6):
+    """ONE search whose leaf waves are evaluated on all ranks (search/distributed.py).
+    Collective: every rank calls it; rank 0's dict has the search's sims/s, the others None."""
+    import torch
+    from rocalphago_amd.engine.gamestate import GameState
+    from rocalphago_amd.features.preprocessing import DEFAULT_FEATURES
+    from rocalphago_amd.models.policy import CNNPolicy
+    from rocalphago_amd.models.value import CNNValue
+    from rocalphago_amd.search.distributed import DistributedMCTS
+    pol = CNNPolicy(DEFAULT_FEATURES, board=19, filters_per_layer=filters, layers=layers,
+                    device=device, seed=seed)
+    val = CNNValue(DEFAULT_FEATURES + ["color"], board=19, filters_per_layer=filters,
+                   layers=layers, device=device, seed=seed + 1)
+    mc = DistributedMCTS(pol, val, dp=dp, lmbda=lmbda, batch=batch, nthreads=nthreads,
+                         rollouts_per_leaf=rollouts_per_leaf, seed=seed,
+                         rollout_delay=rollout_delay)
+    st = GameState()
+    mc.n_playout = warmup
+    mv = mc.get_move(st)  # compiles / allocates; the tree is discarded below
+    mc._search = None
+    mc.n_playout = playouts
+    mc.stats = {"waves": 0, "sims": 0}
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(moves):
+        mv = mc.get_move(st)
+        if dp.rank == 0:
+            st.do_move(mv)
+        mc.update_with_move(mv)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    counts = mc.leaf_counts()
+    if dp.rank != 0:
+        return None
+    s = mc.stats
+    out = {"sims_per_s": s["sims"] / dt, "sims": s["sims"], "seconds": dt, "waves": s["waves"],
+           "batch": batch, "rollouts_per_leaf": rollouts_per_leaf, "rollout_device": "gpu",
+           "gpus": dp.world, "leaves_per_rank": [int(c) for c in counts]}
+    if lmbda > 0:
+        out["rollouts_per_s"] = s["sims"] * rollouts_per_leaf / dt
+    for k in ("t_select", "t_eval", "t_backup"):
+        out[k + "_frac"] = round(s.get(k, 0.0) / dt, 3)
+    return out
+
+
 def measure_sims_per_s(device, **kw):
     return measure(device, **kw)["sims_per_s"]
 
@@ -80,8 +127,26 @@ def main():
     ap.add_argument("--max-inflight", type=int, default=8, help="rollout waves in flight")
     ap.add_argument("--rollout-group", type=int, default=3, help="waves per rollout launch")
     ap.add_argument("--moves", type=int, default=1)
+    ap.add_argument("--rollout-delay", type=int, default=6,
+                    help="--distributed: rounds a wave's rollouts may stay in flight")
+    ap.add_argument("--distributed", action="store_true",
+                    help="one search over all torchrun ranks (search/distributed.py)")
     args = ap.parse_args()
     import torch
+    if args.distributed:
+        from rocalphago_amd.parallel.dp import DPContext
+        dp = DPContext()
+        r = measure_distributed(dp, dp.device, playouts=args.playouts, batch=args.batch,
+                                moves=args.moves, rollouts_per_leaf=args.rollouts_per_leaf,
+                                lmbda=args.lmbda, filters=args.filters, nthreads=args.threads,
+                                rollout_delay=args.rollout_delay)
+        if r is not None:
+            r.update({"metric": "MCTS simulations/s (19x19 APV-MCTS, one search over %d GPUs)"
+                      % dp.world, "lmbda": args.lmbda})
+            print(json.dumps({k: (round(v, 2) if isinstance(v, float) else v)
+                              for k, v in r.items()}))
+        dp.shutdown()
+        return
     dev = torch.device("cuda")
     r = measure(dev, playouts=args.playouts, batch=args.batch, moves=args.moves,
                 rollout_device=args.rollout_device, rollouts_per_leaf=args.rollouts_per_leaf,

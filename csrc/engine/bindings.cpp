@@ -327,6 +327,35 @@ PYBIND11_MODULE(_rocgo, m) {
       py::arg("texts"), py::arg("fids"), py::arg("bd_size"), py::arg("zobrist_white"),
       py::arg("zobrist_black"), py::arg("nthreads") = 8);
 
+  // Leaf boards rebuilt from shipped arrays (distributed search workers; Board::from_arrays).
+  m.def(
+      "boards_from_arrays",
+      [](py::array_t<int8_t, py::array::c_style> colors, py::object ages,
+         py::array_t<int32_t, py::array::c_style> meta8, int S, double komi,
+         py::array_t<uint64_t, py::array::c_style> zw, py::array_t<uint64_t, py::array::c_style> zb) {
+        const int P = S * S;
+        const int n = (int)(colors.size() / P);
+        if (colors.size() != (py::ssize_t)n * P || meta8.size() < (py::ssize_t)n * 8)
+          throw std::invalid_argument("colors [n, S*S] and meta8 [n, 8] expected");
+        py::array_t<int16_t, py::array::c_style | py::array::forcecast> ag;
+        const int16_t* ap = nullptr;
+        if (!ages.is_none()) {
+          ag = py::array_t<int16_t, py::array::c_style | py::array::forcecast>(ages);
+          if (ag.size() != (py::ssize_t)n * P) throw std::invalid_argument("ages [n, S*S]");
+          ap = ag.data();
+        }
+        auto zob = make_zobrist(zw, zb);
+        std::vector<Board> out;
+        out.reserve(n);
+        for (int i = 0; i < n; ++i)
+          out.push_back(Board::from_arrays(S, komi, zob, colors.data() + (size_t)i * P,
+                                           ap ? ap + (size_t)i * P : nullptr,
+                                           meta8.data() + (size_t)i * 8));
+        return out;
+      },
+      py::arg("colors"), py::arg("ages"), py::arg("meta8"), py::arg("size"), py::arg("komi"),
+      py::arg("zobrist_white"), py::arg("zobrist_black"));
+
   m.def("feature_planes", &feature_planes);
 
   m.def("lzf_decompress", [](py::bytes data, size_t out_size) {

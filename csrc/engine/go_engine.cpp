@@ -91,6 +91,63 @@ void Board::copy_from(const Board& o) {
   std::memcpy(placed_, o.placed_, sizeof(uint32_t) * P_);
 }
 
+Board Board::from_arrays(int S, double komi, std::shared_ptr<const Zobrist> zob,
+                         const int8_t* colors, const int16_t* ages, const int32_t* meta8) {
+  Board b(S, komi, false, std::move(zob));
+  b.light_ = true;
+  const int P = b.P_;
+  const Geometry& g = *b.g_;
+  // stone ages: age = clock - placed; a clock above every age keeps placed >= 0
+  b.clock_ = 1u << 20;
+  for (int p = 0; p < P; ++p) {
+    b.color_[p] = colors[p];
+    if (colors[p] != EMPTY) {
+      const int age = ages ? std::max<int>(ages[p], 0) : 0;
+      b.placed_[p] = b.clock_ - (uint32_t)age;
+      b.hash_ ^= colors[p] == WHITE ? b.zob_->white[p] : b.zob_->black[p];
+    }
+  }
+  // groups: flood fill into circular lists headed by their first point
+  int stack[MAXP];
+  for (int p = 0; p < P; ++p) {
+    if (b.color_[p] == EMPTY || b.head_[p] >= 0) continue;
+    const int c = b.color_[p];
+    int n = 0, prev = p;
+    stack[n++] = p;
+    b.head_[p] = (int16_t)p;
+    int size = 0;
+    while (n) {
+      const int q = stack[--n];
+      ++size;
+      if (q != p) {
+        b.nxt_[prev] = (int16_t)q;
+        prev = q;
+      }
+      for (int i = 0; i < g.nnbr[q]; ++i) {
+        const int r = g.nbr[q][i];
+        if (b.color_[r] == c && b.head_[r] < 0) {
+          b.head_[r] = (int16_t)p;
+          stack[n++] = r;
+        }
+      }
+    }
+    b.nxt_[prev] = (int16_t)p;
+    b.gsize_[p] = (int16_t)size;
+    b.recount_libs(p);
+  }
+  if (meta8) {
+    b.current_player_ = meta8[0];
+    b.ko_ = meta8[1];
+    b.last1_ = meta8[2];
+    b.last2_ = meta8[3];
+    b.passes_black_ = meta8[4];
+    b.passes_white_ = meta8[5];
+    b.nmoves_ = meta8[6];
+    b.end_of_game_ = meta8[7] != 0;
+  }
+  return b;
+}
+
 void Board::push_history(int a) {
   nmoves_++;
   last2_ = last1_;

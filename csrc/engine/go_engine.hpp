@@ -90,6 +90,11 @@ class Board {
     return *this;
   }
   void copy_from(const Board& o);
+  // A light board (no history, superko off) rebuilt from the per-point arrays a search leaf is
+  // shipped as (search/distributed.py): colours, stone ages (-1 = empty, may be null) and meta
+  // = (player, ko, last move, second-to-last, black passes, white passes, moves, end of game).
+  static Board from_arrays(int S, double komi, std::shared_ptr<const Zobrist> zob,
+                           const int8_t* colors, const int16_t* ages, const int32_t* meta8);
 
   // ----- reference API (go.py) -----
   bool is_suicide(int a) const;

@@ -74,11 +74,20 @@ class GpuFeatures(object):
     def __call__(self, boards, out=None, sens_out=None):
         """Planes [n, F, S, S] on the device; with ``sens_out`` (uint8 [n, S*S] or [n, 1, S, S])
         also the sensibleness mask (legal, not an own true eye) from the same native inputs."""
-        n = len(boards)
-        S = boards[0].size
         host = self.ladders and (self.ladder_device == "host" or
                                  any(b.enforce_superko for b in boards))
         colors, ages, meta, illegal, lad = _rg.gpu_feature_inputs(boards, host, self.nthreads)
+        return self.from_arrays(colors, ages, meta, illegal, lad, out, sens_out)
+
+    def from_arrays(self, colors, ages, meta, illegal, lad, out=None, sens_out=None):
+        """Planes from the native inputs directly: colours [n, S*S] int8, stone ages int16,
+        meta [n, 4] int32 (player, ko, superko flag, 0), the superko-illegal mask (or None) and
+        the ladder planes [n, 2, S*S] (or None: read on the GPU) — e.g. leaves shipped to another
+        rank (search/distributed.py)."""
+        n = colors.shape[0]
+        S = int(round(np.sqrt(colors.shape[1])))
+        if illegal is not None and not np.any(illegal):
+            illegal = None
         c, a, m, il, ld = (_h2d(x, self.device) for x in (colors, ages, meta, illegal, lad))
         if self.ladders and ld is None:
             ld, self._work = gpu_ladders(c, m, S, work=self._work)

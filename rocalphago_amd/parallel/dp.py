@@ -37,7 +37,9 @@ class DPContext(object):
         if self.enabled and not dist.is_initialized():
             if self.device.type == "cuda":
                 torch.cuda.set_device(self.device)
-            backend = backend or ("nccl" if self.device.type == "cuda" else "gloo")
+            # RAG_DIST_BACKEND=gloo: rehearse several ranks on one GPU (RCCL wants one GPU per rank)
+            backend = backend or os.environ.get("RAG_DIST_BACKEND") or \
+                ("nccl" if self.device.type == "cuda" else "gloo")
             kw = {}
             if backend == "nccl" and self.device.type == "cuda":
                 kw["device_id"] = self.device

@@ -1,0 +1,353 @@
+"""One APV-MCTS search on several GPUs (the reference's ParallelMCTS is an
+empty stub, AlphaGo/mcts.py:219-220).
+
+Design (one process per GPU, torch.distributed "nccl" = RCCL between them; gloo in CPU tests):
+
+  * rank 0 owns the only tree (the native ``_rocgo.Search``). Every *round* it selects one wave of
+    ``batch`` leaves per rank (virtual loss keeps the waves apart), packs each wave's leaves as
+    flat per-point records (LeafCodec: colours, stone ages, player / ko / last moves / passes, and
+    — only for boards that enforce positional superko — the superko-illegal mask and the ladder
+    planes the master computed) and broadcasts them;
+  * every rank, rank 0 included, rebuilds its wave's leaf boards from the records
+    (``Board.from_arrays``), reads the ladders on its own host thread pool, builds the feature
+    planes with the HIP feature kernel, runs the policy and value networks and starts the wave's
+    fast rollouts on its rollout streams (WaveEvaluator). It returns the priors, values and
+    sensible-move masks of this round's wave and the rollout results of the wave it started
+    ``rollout_delay`` rounds earlier (rollouts take longer than a network pass; the native tree
+    keeps such a wave's virtual loss until its rollout backup, as in the single-GPU pipeline);
+  * results come back with one all-gather; rank 0 backs them up and selects the next round.
+
+So the tree, the selection and the backups stay on one host (no tree synchronisation), and all
+the per-leaf work that scales — ladder reading, features, both networks, rollouts — is split
+over the GPUs and their host threads. Root parallelism (independent trees, visit counts
+all-reduced) remains available as ``ParallelMCTS(dp=...)``.
+"""
+import collections
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .._native import engine as _engine
+from ..engine import gamestate as go
+from ..engine.gamestate import PASS_MOVE
+from .apv import ParallelMCTS
+
+_rg = _engine()
+
+CMD_ROUND, CMD_MOVE, CMD_STOP = 0, 1, 2
+HDR = 8  # header words before the per-rank leaf counts
+
+
+class LeafCodec(object):
+    """Per-leaf byte records: colours [P] int8 | ages [P] int16 | meta8 [8] int32 |
+    superko-illegal [P] uint8 | ladder planes [2, P] uint8 (the last two only meaningful when the
+    wave's boards enforce superko)."""
+
+    def __init__(self, S):
+        self.S = S
+        P = self.P = S * S
+        self.o_age = P
+        self.o_meta = 3 * P
+        self.o_ill = 3 * P + 32
+        self.o_lad = 4 * P + 32
+        self.L = (6 * P + 32 + 7) // 8 * 8
+
+    def pack(self, search, wid, nthreads):
+        boards = search.leaf_boards(wid)
+        _, meta8 = search.rollout_inputs(wid)
+        superko = boards[0].enforce_superko
+        colors, ages, _, illegal, lad = _rg.gpu_feature_inputs(boards, superko, nthreads)
+        n, P = len(boards), self.P
+        rec = np.zeros((n, self.L), np.uint8)
+        rec[:, :P] = colors.view(np.uint8)
+        rec[:, self.o_age:self.o_meta] = np.ascontiguousarray(ages).view(np.uint8)
+        rec[:, self.o_meta:self.o_ill] = np.ascontiguousarray(meta8).view(np.uint8)
+        if superko:
+            if illegal is not None:
+                rec[:, self.o_ill:self.o_lad] = illegal
+            rec[:, self.o_lad:self.o_lad + 2 * P] = lad.reshape(n, 2 * P)
+        return rec, superko
+
+    def unpack(self, rec):
+        P = self.P
+        colors = np.ascontiguousarray(rec[:, :P]).view(np.int8)
+        ages = np.ascontiguousarray(rec[:, self.o_age:self.o_meta]).view(np.int16)
+        meta8 = np.ascontiguousarray(rec[:, self.o_meta:self.o_ill]).view(np.int32)
+        illegal = np.ascontiguousarray(rec[:, self.o_ill:self.o_lad])
+        lad = np.ascontiguousarray(rec[:, self.o_lad:self.o_lad + 2 * P]).reshape(-1, 2, P)
+        return colors, ages, meta8, illegal, lad
+
+
+class WaveEvaluator(object):
+    """Evaluates one shipped wave on this rank: (priors [n, P], values [n], sensible [n, P]) and
+    a rollout handle whose ``result()`` is the mean outcome per leaf for BLACK."""
+
+    def __init__(self, net, rollout, lmbda, rollouts_per_leaf=1, rollout_limit=500, nthreads=8):
+        self.net = net  # a NetworkEvaluator
+        self.rollout = rollout
+        self.lmbda = lmbda
+        self.R = int(rollouts_per_leaf)
+        self.limit = int(rollout_limit)
+        self.nthreads = nthreads
+        model = net.policy if net.policy is not None else net.value
+        self.device = model.model.net.device
+        self.gpu = self.device.type == "cuda"
+        self._gro = None
+
+    def _boards(self, colors, ages, meta8, S, komi):
+        zw, zb, _ = go._zobrist(S)
+        return _rg.boards_from_arrays(colors, ages, meta8, S, komi, zw.ravel(), zb.ravel())
+
+    def __call__(self, codec, rec, superko, komi, seed):
+        colors, ages, meta8, illegal, lad = codec.unpack(rec)
+        boards = self._boards(colors, ages, meta8, codec.S, komi)
+        pend = self._rollouts(boards, colors, meta8, codec.S, komi, seed) \
+            if self.lmbda > 0 else None
+        if self.gpu:
+            pr, v, sens = self._gpu_eval(boards, colors, ages, meta8, illegal, lad, superko)
+        else:
+            pr, v, sens = self.net(boards)
+        return pr, v, sens, pend
+
+    def _gpu_eval(self, boards, colors, ages, meta8, illegal, lad, superko):
+        ev = self.net
+        plans = ev._plans()
+        n = len(boards)
+
+        def planes(key):
+            if superko:  # the master's superko-aware ladder planes and illegal mask
+                meta4 = np.zeros((n, 4), np.int32)
+                meta4[:, :2] = meta8[:, :2]
+                meta4[:, 2] = 1
+                return ev.gpu[key].from_arrays(colors, ages, meta4, illegal, lad)
+            return ev.gpu[key](boards)
+
+        if ev.shared or ev.value is None:
+            x = planes("p")
+            xp, xv = (x[:, :ev.npol].contiguous() if ev.shared else x), x
+        else:
+            xp = planes("p") if ev.policy is not None else None
+            xv = planes("v")
+            x = xp if xp is not None else xv
+        ppol, pval = plans
+        with torch.no_grad():
+            sens = x[:, ev._sens_off].reshape(n, -1) if ev._sens_off is not None else None
+            pr = ppol.forward(xp) if ppol is not None else None
+            v = pval.forward(xv).reshape(-1) if pval is not None else None
+        return (None if pr is None else pr.float().cpu().numpy(),
+                None if v is None else v.float().cpu().numpy(),
+                None if sens is None else sens.cpu().numpy())
+
+    def _rollouts(self, boards, colors, meta8, S, komi, seed):
+        if self.gpu:
+            if self._gro is None:
+                from .gpu_rollout import GpuRollouts
+                self._gro = GpuRollouts(self.rollout, self.device)
+            from .gpu_rollout import _Pending
+            ev, w, _, _ = self._gro._launch(colors, meta8, S, komi, self.R, self.limit, seed)
+            return _Pending(ev, w, colors.shape[0], self.R)
+        win = self.rollout.rollouts(boards, seed=seed, limit=self.limit, nthreads=self.nthreads)
+        z = np.where(win == go.BLACK, 1.0, np.where(win == go.WHITE, -1.0, 0.0))
+
+        class _Done(object):
+            def result(self_inner):
+                return z.astype(np.float32)
+        return _Done()
+
+
+class DistributedMCTS(ParallelMCTS):
+    """One search tree on rank 0, leaf evaluation spread over all ranks (see module doc).
+
+    Call ``get_move(state)`` on EVERY rank (all ranks return the same move; only rank 0's
+    ``state`` is read) and ``update_with_move(move)`` on every rank after playing it."""
+
+    def __init__(self, policy=None, value=None, rollout=None, dp=None, rollout_delay=6, **kw):
+        kw.setdefault("pipeline", 1)
+        super(DistributedMCTS, self).__init__(policy, value, rollout, dp=None, **kw)
+        self.ddp = dp
+        self.world = dp.world if dp is not None and dp.enabled else 1
+        self.rank = dp.rank if dp is not None and dp.enabled else 0
+        self.device = dp.device if dp is not None else torch.device("cpu")
+        if self.world > 1 and dist.get_backend() == "gloo":
+            self.device = torch.device("cpu")  # gloo collectives on host tensors
+        self.delay = max(0, int(rollout_delay)) if self.lmbda > 0 else 0
+        self.leaf_eval = WaveEvaluator(self.evaluator, self.rollout, self.lmbda,
+                                       self.rollouts_per_leaf, self.rollout_limit,
+                                       self.nthreads)
+        self._pending = collections.deque()  # (round, rollout handle) of this rank's waves
+        self.rank_leaves = 0
+        self._round = 0
+
+    # ------------------------------------------------------------------ collectives
+    def _bcast(self, t):
+        if self.world > 1:
+            dist.broadcast(t, 0)
+        return t
+
+    def _header(self, cmd, counts, extra=0, superko=0, komi=7.5, S=19):
+        h = torch.zeros(HDR + self.world, dtype=torch.int64, device=self.device)
+        if self.rank == 0:
+            h[:HDR] = torch.tensor([cmd, self._round, extra, superko, int(komi * 2), S, 0, 0])
+            if counts is not None:
+                h[HDR:] = torch.tensor(counts, dtype=torch.int64)
+        return self._bcast(h).cpu().numpy()
+
+    def _round_trip(self, codec, recs, counts, superko, komi):
+        """One round on every rank: ship the waves, evaluate this rank's, gather the results.
+        Returns (on rank 0) per rank (priors, values, sens, (round, z) or None)."""
+        P = codec.P
+        B = self.batch
+        payload = torch.zeros((self.world, B, codec.L), dtype=torch.uint8, device=self.device)
+        if self.rank == 0:
+            for r, rec in enumerate(recs):
+                if rec is not None and len(rec):
+                    payload[r, :len(rec)] = torch.from_numpy(rec).to(self.device)
+        self._bcast(payload)
+        n = int(counts[self.rank])
+        W = 2 * P + 4
+        out = np.zeros((B, W), np.float32)
+        meta = np.zeros(4, np.float32)  # [n, z round, z count, 0]
+        if n:
+            mine = payload[self.rank, :n].cpu().numpy()
+            seed = (self.seed * 7919 + self._round * 131 + self.rank) & 0x7FFFFFFF
+            pr, v, sens, pend = self.leaf_eval(codec, mine, superko, komi, seed)
+            if pr is not None:
+                out[:n, :P] = pr[:, :P]
+            if sens is not None:
+                out[:n, P:2 * P] = sens
+            if v is not None:
+                out[:n, 2 * P] = v
+            if pend is not None:
+                self._pending.append((self._round, pend))
+            self.rank_leaves += n
+        meta[0] = n
+        if self._pending and (self._pending[0][0] <= self._round - self.delay or
+                              n == 0):
+            rnd, pend = self._pending.popleft()
+            z = pend.result()
+            out[:len(z), 2 * P + 1] = z
+            meta[1], meta[2] = rnd, len(z)
+        flat = torch.from_numpy(np.concatenate([out.reshape(-1), meta])).to(self.device)
+        if self.world > 1:
+            gathered = [torch.empty_like(flat) for _ in range(self.world)]
+            dist.all_gather(gathered, flat)
+        else:
+            gathered = [flat]
+        if self.rank != 0:
+            return None
+        res = []
+        for g in gathered:
+            g = g.cpu().numpy()
+            o, m = g[:-4].reshape(B, W), g[-4:]
+            k = int(m[0])
+            zr = (int(m[1]), o[:int(m[2]), 2 * P + 1].copy()) if m[2] > 0 else None
+            res.append((o[:k, :P], o[:k, 2 * P], o[:k, P:2 * P] > 0.5, zr))
+        return res
+
+    # ------------------------------------------------------------------ rank 0: the search
+    def search(self, state, n_playout=None):
+        s = self._sync_root(state)
+        codec = LeafCodec(state.size)
+        target = s.root_visits + (n_playout or self.n_playout)
+        waves = {}  # (round, rank) -> wave id still waiting for its rollout results
+        stall = 0
+        t_sel = t_rt = t_back = 0.0
+        while True:
+            t0 = time.perf_counter()
+            recs, counts, wids = [], [], []
+            superko = int(s.root_board.enforce_superko)
+            room = target - s.root_visits
+            for r in range(self.world):
+                want = min(self.batch, max(room, 0))
+                wid, n = s.select(want) if want > 0 else (-1, 0)
+                if n > 0:
+                    rec, _ = codec.pack(s, wid, self.nthreads)
+                    room -= n
+                else:
+                    rec = None
+                recs.append(rec)
+                counts.append(n)
+                wids.append(wid if n > 0 else -1)
+            t1 = time.perf_counter()
+            if sum(counts) == 0 and not waves:
+                stall += 1
+                if stall > 3 or s.root_visits >= target:
+                    break
+                continue
+            stall = 0
+            self._header(CMD_ROUND, counts, superko=superko, komi=state.komi, S=state.size)
+            res = self._round_trip(codec, recs, counts, superko, state.komi)
+            t2 = time.perf_counter()
+            for r, (pr, v, sens, zr) in enumerate(res):
+                if counts[r]:
+                    s.backup_value(wids[r], pr if self.evaluator.policy is not None else None,
+                                   v if self.evaluator.value is not None else None,
+                                   sens.astype(np.uint8) if self._has_sens() else None)
+                    if self.lmbda > 0:
+                        waves[(self._round, r)] = wids[r]
+                if zr is not None:
+                    s.backup_rollout(waves.pop((zr[0], r)), zr[1])
+            self.stats["waves"] += sum(1 for c in counts if c)
+            self.stats["sims"] += sum(counts)
+            self._round += 1
+            t_sel += t1 - t0
+            t_rt += t2 - t1
+            t_back += time.perf_counter() - t2
+            if s.root_visits >= target and not waves:
+                break
+        self._acc("t_select", t_sel)
+        self._acc("t_eval", t_rt)
+        self._acc("t_backup", t_back)
+        return s
+
+    def _has_sens(self):
+        self.evaluator._plans()
+        return self.evaluator._sens_off is not None
+
+    def get_move(self, state):
+        if self.world == 1:
+            return super(DistributedMCTS, self).get_move(state)
+        if self.rank != 0:
+            return self.serve()
+        try:
+            s = self.search(state)
+        except BaseException:
+            self.stop()  # release the serving ranks before failing
+            raise
+        a = s.best_move()
+        self._header(CMD_MOVE, [0] * self.world, extra=int(a))
+        return PASS_MOVE if a < 0 else divmod(int(a), state.size)
+
+    def update_with_move(self, last_move):
+        if self.rank == 0:
+            super(DistributedMCTS, self).update_with_move(last_move)
+
+    # ------------------------------------------------------------------ ranks > 0
+    def serve(self):
+        """Evaluate rounds until rank 0 decides a move (returned) or stops (None)."""
+        while True:
+            h = self._header(None, None)
+            cmd, self._round = int(h[0]), int(h[1])
+            if cmd == CMD_MOVE:
+                a = int(h[2])
+                S = int(h[5]) or 19
+                return PASS_MOVE if a < 0 else divmod(a, S)
+            if cmd == CMD_STOP:
+                return None
+            codec = LeafCodec(int(h[5]))
+            self._round_trip(codec, None, h[HDR:], int(h[3]), h[4] / 2.0)
+
+    def stop(self):
+        """Rank 0: release the serving ranks (their serve() returns None)."""
+        if self.world > 1 and self.rank == 0:
+            self._header(CMD_STOP, [0] * self.world)
+
+    def leaf_counts(self):
+        """Leaves evaluated by each rank (collective: call on every rank)."""
+        t = torch.zeros(self.world, dtype=torch.float64, device=self.device)
+        t[self.rank] = self.rank_leaves
+        if self.world > 1:
+            dist.all_reduce(t)
+        return t.cpu().numpy()

@@ -1,0 +1,119 @@
+"""Multi-GPU single-tree search plumbing (search/distributed.py): leaves shipped as arrays are
+rebuilt into boards that give exactly the original planes; a 2-rank gloo run of one search
+splits the leaf evaluations over the ranks and plays the same move on every rank."""
+import numpy as np
+
+from rocalphago_amd._native import engine
+from rocalphago_amd.engine import gamestate as go
+from rocalphago_amd.features.preprocessing import DEFAULT_FEATURES, Preprocess
+
+from boards import random_games
+
+rg = engine()
+
+
+def _arrays(states):
+    S = states[0].size
+    boards = [s.native for s in states]
+    colors, ages, meta4, _, _ = rg.gpu_feature_inputs(boards, False, 2)
+    meta8 = np.zeros((len(boards), 8), np.int32)
+    for i, b in enumerate(boards):
+        l1, l2 = b.last_moves
+        meta8[i] = [b.current_player, b.ko, l1, l2, b.passes_black, b.passes_white,
+                    b.move_count, int(b.end_of_game)]
+    return colors, ages, meta8, S
+
+
+def test_boards_from_arrays_reproduce_features():
+    states = random_games(48, 19, 7, 30, 300) + random_games(16, 9, 8, 5, 80)
+    fids = Preprocess(list(DEFAULT_FEATURES) + ["color"]).feature_ids
+    for group in (states[:48], states[48:]):
+        colors, ages, meta8, S = _arrays(group)
+        zw, zb, _ = go._zobrist(S)
+        rebuilt = rg.boards_from_arrays(colors, ages, meta8, S, 7.5, zw.ravel().copy(),
+                                        zb.ravel().copy())
+        want = rg.batch_features([s.native for s in group], fids, 2)
+        got = rg.batch_features(rebuilt, fids, 2)
+        assert np.array_equal(got, want)
+        for s, b in zip(group, rebuilt):
+            assert b.current_player == s.native.current_player and b.ko == s.native.ko
+            assert b.last_moves == s.native.last_moves
+
+
+def _dist_worker(rank, world, port, outdir):
+    import os
+    import torch
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from rocalphago_amd.engine.gamestate import GameState
+    from rocalphago_amd.models.policy import CNNPolicy
+    from rocalphago_amd.models.value import CNNValue
+    from rocalphago_amd.parallel.dp import DPContext
+    from rocalphago_amd.search.distributed import DistributedMCTS
+    dp = DPContext(device="cpu")
+    feats = ["board", "ones", "turns_since", "liberties", "sensibleness"]
+    pol = CNNPolicy(feats, board=7, filters_per_layer=8, layers=2, device="cpu", seed=3)
+    val = CNNValue(feats + ["color"], board=7, filters_per_layer=8, layers=2, device="cpu",
+                   seed=4)
+    mc = DistributedMCTS(pol, val, dp=dp, lmbda=0.5, n_playout=96, batch=12, rollout_limit=80,
+                         nthreads=1, rollout_delay=1)
+    st = GameState(size=7)
+    moves = []
+    for _ in range(3):
+        mv = mc.get_move(st if rank == 0 else None)
+        moves.append(-1 if mv is None else mv[0] * 7 + mv[1])
+        if rank == 0:
+            st.do_move(mv)
+        mc.update_with_move(mv)
+    counts = mc.leaf_counts()
+    np.save(os.path.join(outdir, "mv%d.npy" % rank), np.array(moves))
+    np.save(os.path.join(outdir, "cnt%d.npy" % rank), counts)
+    if rank == 0:
+        np.save(os.path.join(outdir, "sims.npy"), np.array([mc.stats["sims"],
+                                                             mc._search.rollouts]))
+    dp.shutdown()
+
+
+def test_one_search_two_ranks(tmp_path):
+    """One tree on rank 0, leaves evaluated on both ranks (2 gloo processes): every rank plays
+    the same move and the leaf evaluations are split over the ranks."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.spawn(_dist_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    m0, m1 = np.load(tmp_path / "mv0.npy"), np.load(tmp_path / "mv1.npy")
+    assert np.array_equal(m0, m1)
+    c = np.load(tmp_path / "cnt0.npy")
+    sims, rollouts = np.load(tmp_path / "sims.npy")
+    assert c[0] > 0 and c[1] > 0, c
+    assert c.sum() == sims >= 3 * 96 - 3
+    assert rollouts == sims  # every leaf's rollout came back and was backed up
+
+
+@__import__("pytest").mark.gpu
+def test_distributed_search_gpu_single_rank(cuda):
+    """The GPU leaf path of the multi-GPU search (rebuilt boards, host ladders, HIP features,
+    fused networks, GPU rollouts) on one rank: a full search plays a legal move and every
+    simulation's rollout is backed up."""
+    from rocalphago_amd.engine.gamestate import GameState
+    from rocalphago_amd.models.policy import CNNPolicy
+    from rocalphago_amd.models.value import CNNValue
+    from rocalphago_amd.search.distributed import DistributedMCTS
+    dev = cuda
+    pol = CNNPolicy(DEFAULT_FEATURES, board=19, filters_per_layer=64, layers=4, device=dev,
+                    seed=1)
+    val = CNNValue(list(DEFAULT_FEATURES) + ["color"], board=19, filters_per_layer=64, layers=4,
+                   device=dev, seed=2)
+    mc = DistributedMCTS(pol, val, dp=None, lmbda=0.5, n_playout=1024, batch=128, nthreads=8)
+    st = GameState()
+    for _ in range(2):
+        mv = mc.get_move(st)
+        assert mv is None or st.is_legal(mv)
+        st.do_move(mv)
+        mc.update_with_move(mv)
+    assert mc.stats["sims"] >= 2 * 1024 - 2
+    assert mc._search.rollouts == mc._search.sims
