@@ -33,10 +33,12 @@ policy_head_fwd_kernel(const bf16* __restrict__ H, const float* __restrict__ w, 
                        const float* __restrict__ pbias, float* __restrict__ probs,
                        const int64_t* __restrict__ labels, const float* __restrict__ sweight,
                        float* __restrict__ loss, float* __restrict__ dz, float* __restrict__ hit,
-                       int S, int KP, int K, int mode, float gscale) {
+                       const float* __restrict__ pass_w, const float* __restrict__ pass_b,
+                       float* __restrict__ zout, float* __restrict__ dpass, int S, int KP, int K,
+                       int mode, float gscale) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* z = smem;                    // S*S logits
-  float* ws = smem + ((S * S + 3) & ~3);  // KP weights
+  float* z = smem;                        // S*S logits (+ the pass logit)
+  float* ws = smem + ((S * S + 4) & ~3);  // KP weights
   __shared__ float red[16];
   const int b = blockIdx.x;
   const int S2 = S * S, WP = S + 2;
@@ -55,27 +57,51 @@ policy_head_fwd_kernel(const bf16* __restrict__ H, const float* __restrict__ w, 
     z[p] = acc + bias0 + (pbias ? pbias[p] : 0.f);
   }
   __syncthreads();
+  // optional pass logit (PassLogit layer): W . z + b over the position logits, the
+  // softmax then runs over C = S*S + 1 classes with pass last
+  const bool has_pass = pass_w != nullptr;
+  const int C = S2 + (has_pass ? 1 : 0);
+  if (has_pass) {
+    float pd = 0.f;
+    for (int p = threadIdx.x; p < S2; p += blockDim.x) {
+      pd += pass_w[p] * z[p];
+      if (zout) zout[(size_t)b * S2 + p] = z[p];
+    }
+    pd = block_reduce(pd, red, false);
+    if (threadIdx.x == 0) z[S2] = pd + *pass_b;
+    __syncthreads();
+  }
   float mx = -INFINITY;
   int amax = 0;
-  for (int p = threadIdx.x; p < S2; p += blockDim.x)
+  for (int p = threadIdx.x; p < C; p += blockDim.x)
     if (z[p] > mx) {
       mx = z[p];
       amax = p;
     }
   const float gmax = block_reduce(mx, red, true);
   float se = 0.f;
-  for (int p = threadIdx.x; p < S2; p += blockDim.x) se += __expf(z[p] - gmax);
+  for (int p = threadIdx.x; p < C; p += blockDim.x) se += __expf(z[p] - gmax);
   const float sum = block_reduce(se, red, false);
   const float inv = 1.f / sum;
   const int64_t lab = (mode && labels) ? labels[b] : -1;
   const float sw = sweight ? sweight[b] : 1.f;
-  const float cls = (mode == 2) ? 1.f / (float)S2 : 1.f;
+  const float cls = (mode == 2) ? 1.f / (float)C : 1.f;
+  // dL/d(pass logit): it also flows back into every position logit through W
+  float dp = 0.f;
+  if (has_pass) {
+    const float pp = __expf(z[S2] - gmax) * inv;
+    dp = (pp - (lab == S2 ? 1.f : 0.f)) * sw * cls * gscale;
+    if (threadIdx.x == 0) {
+      probs[(size_t)b * C + S2] = pp;
+      if (mode && dpass) dpass[b] = dp;
+    }
+  }
   for (int p = threadIdx.x; p < S2; p += blockDim.x) {
     const float pr = __expf(z[p] - gmax) * inv;
-    probs[(size_t)b * S2 + p] = pr;
+    probs[(size_t)b * C + p] = pr;
     if (mode && dz) {
       const float y = (p == lab) ? 1.f : 0.f;
-      dz[(size_t)b * S2 + p] = (pr - y) * sw * cls * gscale;
+      dz[(size_t)b * S2 + p] = (pr - y) * sw * cls * gscale + (has_pass ? dp * pass_w[p] : 0.f);
     }
   }
   if (mode && threadIdx.x == 0 && lab >= 0) {
@@ -306,10 +332,29 @@ RAG_API int rag_policy_head_fwd(const void* H, const float* w, const float* b0,
                                 const float* sweight, float* loss, float* dz, float* hit, int B,
                                 int S, int KP, int K, int mode, float gscale,
                                 hipStream_t stream) {
-  const size_t sm = (size_t)(((S * S + 3) & ~3) + KP) * sizeof(float);
+  const size_t sm = (size_t)(((S * S + 4) & ~3) + KP) * sizeof(float);
   policy_head_fwd_kernel<<<B, kHeadThreads, sm, stream>>>((const bf16*)H, w, b0, pbias, probs,
-                                                          labels, sweight, loss, dz, hit, S, KP,
-                                                          K, mode, gscale);
+                                                          labels, sweight, loss, dz, hit, nullptr,
+                                                          nullptr, nullptr, nullptr, S, KP, K,
+                                                          mode, gscale);
+  return (int)hipGetLastError();
+}
+
+// With a pass logit (pass_w [S*S], pass_b [1]): probs [B, S*S + 1], labels may be S*S (pass),
+// zout [B, S*S] receives the position logits and dpass [B] dL/d(pass logit) for the PassLogit
+// weight gradients (dW = dpass^T zout, db = sum dpass); dz already carries dpass * pass_w.
+RAG_API int rag_policy_head_pass_fwd(const void* H, const float* w, const float* b0,
+                                     const float* pbias, const float* pass_w,
+                                     const float* pass_b, float* probs, const int64_t* labels,
+                                     const float* sweight, float* loss, float* dz, float* hit,
+                                     float* zout, float* dpass, int B, int S, int KP, int K,
+                                     int mode, float gscale, hipStream_t stream) {
+  if (!pass_w || !pass_b) return -1;
+  const size_t sm = (size_t)(((S * S + 4) & ~3) + KP) * sizeof(float);
+  policy_head_fwd_kernel<<<B, kHeadThreads, sm, stream>>>((const bf16*)H, w, b0, pbias, probs,
+                                                          labels, sweight, loss, dz, hit, pass_w,
+                                                          pass_b, zout, dpass, S, KP, K, mode,
+                                                          gscale);
   return (int)hipGetLastError();
 }
 

@@ -29,6 +29,7 @@ void register_search(py::module_& m) {
       .def("select", &Search::select, py::arg("batch"),
            py::call_guard<py::gil_scoped_release>())
       .def_readwrite("parallel_select_min", &Search::parallel_select_min)
+      .def_readwrite("pass_prior", &Search::pass_prior)
       .def("leaf_nodes",
            [](Search& s, int id) {
              std::vector<int32_t> v;

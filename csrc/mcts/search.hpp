@@ -145,6 +145,9 @@ class Search {
  public:
   float c_puct = 5.f, lambda = 0.5f;
   int n_vl = 3, rollout_limit = 500, max_depth = 722;
+  // networks with a pass logit: priors rows carry S*S + 1 entries and every
+  // expanded node also gets a PASS child with the network's pass prior
+  bool pass_prior = false;
   uint64_t seed = 1;
   std::shared_ptr<RolloutPolicy> rollout_policy;
 
@@ -418,12 +421,13 @@ class Search {
       }
       cnt[i] = c;
     });
+    const bool with_pass = pass_prior && priors != nullptr && stride > P;
     std::vector<int32_t> first(n, -1);
     size_t total = nodes_.size();
     for (int i = 0; i < n; ++i) {
       if (cnt[i] < 0) continue;
       first[i] = (int32_t)total;
-      total += cnt[i] == 0 ? 1 : cnt[i];
+      total += nchildren(cnt[i], with_pass);
     }
     nodes_.resize(total);
     // pass 2 (parallel): write the children into their block
@@ -434,13 +438,14 @@ class Search {
       if (sensible) {
         const uint8_t* m = sensible + (size_t)i * P;
         int k = 0;
-        fill_children(node, first[i], cnt[i], pri, [&]() {
+        fill_children(node, first[i], cnt[i], with_pass, pri, P, [&]() {
           while (!m[k]) ++k;
           return k++;
         });
       } else {
         size_t k = 0;
-        fill_children(node, first[i], cnt[i], pri, [&]() { return moves[i][k++]; });
+        fill_children(node, first[i], cnt[i], with_pass, pri, P,
+                      [&]() { return moves[i][k++]; });
       }
     });
     for (int i = 0; i < n; ++i) {
@@ -448,7 +453,7 @@ class Search {
       if (first[i] >= 0) {
         Node& nd = nodes_[L.path.back()];
         nd.first = first[i];
-        nd.nchild = (int16_t)(cnt[i] == 0 ? 1 : cnt[i]);
+        nd.nchild = (int16_t)nchildren(cnt[i], with_pass);
         nd.state = N_EXPANDED;
       }
       backup_value_path(L.path, values ? values[i] : 0.f, lambda <= 0.f);
@@ -623,17 +628,24 @@ class Search {
     waves_.clear();
   }
 
-  // children of `node` for its `count` sensible moves (PASS alone when there are none), moves in
-  // increasing point order from `next_move()`, priors renormalised over them, written into the
-  // preallocated slots [first, first + max(count, 1))
+  static int nchildren(int count, bool with_pass) {
+    return with_pass ? count + 1 : (count == 0 ? 1 : count);
+  }
+
+  // children of `node` for its `count` sensible moves (PASS alone when there are none; PASS
+  // always, last, with the network's pass prior pri[P] when `with_pass`), moves in increasing
+  // point order from `next_move()`, priors renormalised over them, written into the
+  // preallocated slots [first, first + nchildren(count, with_pass))
   template <class F>
-  void fill_children(int node, int first, int count, const float* pri, F&& next_move) {
-    const int nc = count == 0 ? 1 : count;
+  void fill_children(int node, int first, int count, bool with_pass, const float* pri, int P,
+                     F&& next_move) {
+    const int nc = nchildren(count, with_pass);
     float tot = 0.f;
     for (int k = 0; k < nc; ++k) {
-      const int mv = count == 0 ? PASS : next_move();
+      const int mv = k < count ? next_move() : PASS;
       float p = 1.f;
       if (pri && mv != PASS) p = std::max(pri[mv], 0.f);
+      if (pri && mv == PASS && with_pass) p = std::max(pri[P], 0.f);
       tot += p;
       nodes_[first + k] = Node{node, -1, 0, (int16_t)mv, p, 0, 0, 0, 0.f, 0.f, N_NEW};
     }

@@ -379,10 +379,11 @@ class ResTrunk(_PackedConvs):
 class PolicyHeadEngine(object):
     """1x1 conv (K->1, scalar bias) -> Flatten -> per-position Bias -> softmax."""
 
-    def __init__(self, trunk, K):
+    def __init__(self, trunk, K, pass_logit=False):
         self.trunk = trunk
         self.K = K
         self.S = trunk.S
+        self.pass_logit = pass_logit
         self._B = 0
 
     def ensure(self, B):
@@ -390,20 +391,34 @@ class PolicyHeadEngine(object):
             return
         dev = self.trunk.device
         S2 = self.S * self.S
-        self.probs = torch.empty((B, S2), device=dev)
+        self.probs = torch.empty((B, S2 + (1 if self.pass_logit else 0)), device=dev)
         self.dz = torch.empty((B, S2), device=dev)
         self.loss = torch.empty((B,), device=dev)
         self.hit = torch.empty((B,), device=dev)
+        if self.pass_logit:
+            self.zpos = torch.empty((B, S2), device=dev)
+            self.dpass = torch.empty((B,), device=dev)
         self._B = B
 
-    def forward(self, B, w, b0, pbias, labels=None, sweight=None, mode=0, gscale=1.0):
+    def forward(self, B, w, b0, pbias, labels=None, sweight=None, mode=0, gscale=1.0,
+                pass_params=None):
+        """pass_params: (W [S*S], b [1]) of a PassLogit layer, or None."""
         self.ensure(B)
         h = self.trunk.output(B)
+        pk = {}
+        if pass_params is not None:
+            pk = dict(pass_w=pass_params[0], pass_b=pass_params[1], zout=self.zpos[:B],
+                      dpass=self.dpass[:B] if mode else None)
         ops.policy_head_fwd(h, w, b0, pbias, self.probs[:B], self.K, labels=labels,
                             sweight=sweight, loss=self.loss[:B] if mode else None,
                             dz=self.dz[:B] if mode else None, hit=self.hit[:B] if mode else None,
-                            mode=mode, gscale=gscale)
+                            mode=mode, gscale=gscale, **pk)
         return self.probs[:B]
+
+    def pass_grads(self, B, dW, db):
+        """PassLogit weight gradients after a training forward: dW = dpass^T z, db = sum dpass."""
+        torch.matmul(self.dpass[:B], self.zpos[:B], out=dW)
+        db.copy_(self.dpass[:B].sum().reshape(1))
 
     def backward(self, B, w, dz, dw, db0, dpbias):
         """dz [B, S*S] -> head param grads + trunk top gradient (ReLU-masked) in grad buffer 0."""

@@ -3,7 +3,7 @@
 ``detect_plan`` pattern-matches a kerasish Sequential model:
 
   PolicyPlan:  [Conv2D 'same' (+ReLU)]* -> Conv2D 1x1 (1 filter, linear) -> Flatten -> Bias ->
-               Activation(softmax)                      (CNNPolicy, reference policy.py:96-136)
+               [PassLogit] -> Activation(softmax)       (CNNPolicy, reference policy.py:96-136)
   ValuePlan:   [Conv2D 'same' (+ReLU)]* -> Conv2D 1x1 (1 filter) -> Flatten -> Dense(H) ->
                Dense(1, tanh)                          (CNNValue / reference value.py:14-28)
   ResnetPlan:  (functional) Conv2D linear -> [n_skip x (BN -> ReLU -> Conv2D linear) + sum-merge]*
@@ -50,6 +50,9 @@ def detect_plan(model):
         return None
     if rest == ["Flatten", "Bias", "Activation"] and L[-1].config["activation"] == "softmax":
         return PolicyPlan(model, L[:n - 1], head, L[n + 1])
+    if rest == ["Flatten", "Bias", "PassLogit", "Activation"] and \
+            L[-1].config["activation"] == "softmax":
+        return PolicyPlan(model, L[:n - 1], head, L[n + 1], L[n + 2])
     if rest == ["Flatten", "Dense", "Dense"] and L[-1].config["output_dim"] == 1 and \
             L[-1].config.get("activation") == "tanh" and \
             L[n + 1].config.get("activation", "linear") in ("relu", "linear", "tanh"):
@@ -119,17 +122,21 @@ class _TrunkPlan(object):
 
 
 class PolicyPlan(_TrunkPlan):
-    def __init__(self, model, convs, head_conv, bias_layer):
+    def __init__(self, model, convs, head_conv, bias_layer, pass_layer=None):
         super(PolicyPlan, self).__init__(model, convs, head_conv)
         self.bias_name = bias_layer.name
-        self.head = PolicyHeadEngine(self.trunk, self.K)
+        self.pass_name = pass_layer.name if pass_layer is not None else None
+        self.head = PolicyHeadEngine(self.trunk, self.K, pass_logit=pass_layer is not None)
+
+    def _pass_params(self):
+        return self.net.params_of(self.pass_name) if self.pass_name else None
 
     def forward(self, x, index=None, transforms=None):
         B = self.prepare(x, index, transforms)
         self.trunk.forward(B)
         w, b0 = self.head_params()
         pb = self.net.params_of(self.bias_name)[0]
-        return self.head.forward(B, w, b0, pb).clone()
+        return self.head.forward(B, w, b0, pb, pass_params=self._pass_params()).clone()
 
     @staticmethod
     def loss_mode(loss):
@@ -161,7 +168,11 @@ class PolicyPlan(_TrunkPlan):
         self.trunk.forward(B, training=True)
         w, b0 = self.head_params()
         pb = self.net.params_of(self.bias_name)[0]
-        self.head.forward(B, w, b0, pb, labels=labels, sweight=sw, mode=mode, gscale=gscale)
+        self.head.forward(B, w, b0, pb, labels=labels, sweight=sw, mode=mode, gscale=gscale,
+                          pass_params=self._pass_params())
+        if self.pass_name:
+            dW, db = self.net.grads_of(self.pass_name)
+            self.head.pass_grads(B, dW, db)
         dw, db0 = self.head_grads()
         dpb = self.net.grads_of(self.bias_name)[0]
         self.head.backward(B, w, self.head.dz[:B], dw, db0, dpb)
@@ -312,4 +323,5 @@ class ResnetPlan(PolicyPlan):
         self.head_name = head_conv.name
         self.K = specs[-1].cout
         self.bias_name = bias_layer.name
+        self.pass_name = None
         self.head = PolicyHeadEngine(self.trunk, self.K)

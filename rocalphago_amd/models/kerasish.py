@@ -6,7 +6,7 @@ This module re-creates exactly that surface over our own execution engine:
 
   * the Keras-1 JSON model spec is interpreted (Sequential and functional ``Model``; layers
     Convolution2D, Dense, Flatten, Activation, Bias, BatchNormalization, Merge, InputLayer,
-    Dropout) and re-emitted by ``to_json`` (nn_util.py:79,100);
+    Dropout, and the optional PassLogit) and re-emitted by ``to_json`` (nn_util.py:79,100);
   * weights live in ONE flat fp32 buffer (parameters are views), in Keras order/shapes (conv OIHW,
     Dense (in, out), Bias (S*S,)) so ``get_weights``/``set_weights`` and the HDF5 layout
     (nn_util.py:81,104; random_minimodel_weights.hdf5) match the reference;
@@ -84,6 +84,8 @@ class Layer(object):
             return (None, int(np.prod(s[1:])))
         if c == "Dense":
             return (None, cfg["output_dim"])
+        if c == "PassLogit":
+            return (None, s[1] + 1)
         return s
 
     def weight_specs(self, in_shape):
@@ -102,6 +104,8 @@ class Layer(object):
             return specs
         if c == "Bias":
             return [("param_0", tuple(in_shape[1:]), "zero")]
+        if c == "PassLogit":
+            return [(n + "_W", (in_shape[1],), "zero"), (n + "_b", (1,), "zero")]
         if c == "BatchNormalization":
             axis = cfg.get("axis", -1)
             dim = in_shape[axis]
@@ -147,6 +151,13 @@ def Activation(activation, name=None):
 
 def BiasLayer(name=None):
     return Layer("Bias", {"name": name, "trainable": True})
+
+
+def PassLogit(name=None):
+    """Optional pass move for the policy head (off by default): appends one logit
+    ``W . z + b`` computed from the S*S position logits z, so the softmax runs over S*S + 1
+    classes with pass last. Parameters W (S*S,) and b (1,) start at zero."""
+    return Layer("PassLogit", {"name": name, "trainable": True})
 
 
 def BatchNormalization(epsilon=1e-3, mode=0, axis=-1, momentum=0.99, name=None):
@@ -378,6 +389,8 @@ class KerasNet(torch.nn.Module):
             return x.reshape(x.shape[0], -1)
         if c == "Bias":
             return x + params[0]
+        if c == "PassLogit":
+            return torch.cat([x, (x @ params[0] + params[1]).unsqueeze(-1)], dim=-1)
         if c == "Activation":
             return _act(x, cfg["activation"])
         if c == "Dense":

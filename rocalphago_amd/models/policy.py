@@ -2,12 +2,14 @@
 
 CNNPolicy: 'same' conv K1xK1 (default 5x5) + ReLU, (layers-1) x conv 3x3 + ReLU, 1x1 conv to one
 plane (linear, scalar bias), Flatten, per-position Bias, softmax over S*S points (no pass logit,
-quirk Q17). On a GPU the whole network (forward, fused softmax/loss, backward, SGD) runs on the
-hand-written gfx950 kernels (models/fused.py). Defaults follow the reference (128 filters, 12
+quirk Q17; ``pass_logit=True`` adds one, softmax over S*S + 1 with pass last). On a GPU the
+whole network (forward, fused softmax/loss, backward, SGD) runs on the hand-written gfx950
+kernels (models/fused.py). Defaults follow the reference (128 filters, 12
 layers); the north-star benchmark model is 48 planes / 192 filters / 12+1 layers.
 """
 import numpy as np
 
+from ..engine.gamestate import PASS_MOVE
 from ..utils.go_util import flatten_idx
 from . import kerasish as K
 from .nn_util import Bias, NeuralNetBase, neuralnet
@@ -20,7 +22,9 @@ class CNNPolicy(NeuralNetBase):
     def _select_moves_and_normalize(self, nn_output, moves, size):
         if len(moves) == 0:
             return []
-        move_indices = [flatten_idx(m, size) for m in moves]
+        if len(nn_output) > size * size:  # pass-logit network: pass is a move like any other
+            moves = list(moves) + ([PASS_MOVE] if PASS_MOVE not in moves else [])
+        move_indices = [size * size if m is PASS_MOVE else flatten_idx(m, size) for m in moves]
         distribution = nn_output[move_indices]
         distribution = distribution / distribution.sum()
         return list(zip(moves, distribution))
@@ -49,7 +53,8 @@ class CNNPolicy(NeuralNetBase):
     @staticmethod
     def create_network(**kwargs):
         """Keyword args (reference policy.py:66-80): input_dim, board (19), filters_per_layer
-        (128), filters_per_layer_K, layers (12), filter_width_K (3; 5 for K=1). Extra: seed."""
+        (128), filters_per_layer_K, layers (12), filter_width_K (3; 5 for K=1). Extra: seed,
+        pass_logit (False): a learned pass logit, softmax over S*S + 1."""
         defaults = {
             "board": 19,
             "filters_per_layer": 128,
@@ -72,6 +77,8 @@ class CNNPolicy(NeuralNetBase):
                                       border_mode='same'))
         layers.append(K.Flatten())
         layers.append(Bias())
+        if params.get("pass_logit"):
+            layers.append(K.PassLogit())
         layers.append(K.Activation('softmax'))
         return K.Sequential(layers, device=params.get("device"), seed=params.get("seed"))
 
@@ -142,6 +149,13 @@ class ResnetPolicy(CNNPolicy):
         out = add(K.Activation('softmax'), [path])
         return K.Model(layers, functional=True, inputs=[inp.name], outputs=[out],
                        device=params.get("device"), seed=params.get("seed"))
+
+
+def has_pass_logit(policy):
+    """True for a policy network built with ``pass_logit=True`` (output S*S + 1, pass last)."""
+    model = getattr(policy, "model", None)
+    return model is not None and any(getattr(ld, "class_name", None) == "PassLogit"
+                                     for ld in getattr(model, "layers", []))
 
 
 def policy_probabilities(policy, states):

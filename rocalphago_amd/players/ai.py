@@ -46,13 +46,15 @@ def _device_moves(policy, states, beta, greedy_rows, rng):
     sens = torch.empty((n, S * S), dtype=torch.uint8, device=model.device)
     x = gf([st.native for st in states], sens_out=sens)
     probs = policy.forward_device(x)
+    if probs.shape[1] == S * S + 1:  # pass-logit network: pass is always a candidate
+        sens = torch.cat([sens, torch.ones((n, 1), dtype=torch.uint8, device=model.device)], 1)
     greedy = None
     if any(greedy_rows):
         greedy = torch.tensor([1 if g else 0 for g in greedy_rows],
                               dtype=torch.uint8).to(model.device)
     seed = (int(rng.randint(0, 2 ** 31 - 1)) << 31) | int(rng.randint(0, 2 ** 31 - 1))
     mv = ops.sample_moves(probs, sens, beta, greedy, seed).cpu().numpy()
-    return [go.PASS_MOVE if m < 0 else (int(m) // S, int(m) % S) for m in mv]
+    return [go.PASS_MOVE if m < 0 or m >= S * S else (int(m) // S, int(m) % S) for m in mv]
 
 
 class GreedyPolicyPlayer(object):

@@ -243,6 +243,8 @@ class ParallelMCTS(object):
 
     # ------------------------------------------------------------------ tree management
     def _configure(self, s):
+        from ..models.policy import has_pass_logit
+        s.pass_prior = has_pass_logit(getattr(self.evaluator, "policy", None))
         s.c_puct = self.c_puct
         s.lmbda = self.lmbda
         s.n_vl = self.virtual_loss
