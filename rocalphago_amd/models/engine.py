@@ -417,7 +417,7 @@ class PolicyHeadEngine(object):
 
     def pass_grads(self, B, dW, db):
         """PassLogit weight gradients after a training forward: dW = dpass^T z, db = sum dpass."""
-        torch.matmul(self.dpass[:B], self.zpos[:B], out=dW)
+        dW.copy_(torch.mv(self.zpos[:B].t(), self.dpass[:B]).reshape(dW.shape))
         db.copy_(self.dpass[:B].sum().reshape(1))
 
     def backward(self, B, w, dz, dw, db0, dpbias):

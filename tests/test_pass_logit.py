@@ -2,7 +2,6 @@
 ``PassLogit`` layer appends W . z + b to the S*S position logits, softmax over S*S + 1 classes.
 Off by default; on: JSON/HDF5 round trip, players and both searches may pass, and the fused HIP
 head matches the fp32 torch reference (GPU tests)."""
-import os
 
 import numpy as np
 import pytest
@@ -100,10 +99,21 @@ def test_hip_pass_head_matches_torch(cuda):
         m.model.compile(loss="categorical_crossentropy", optimizer=K.SGD(lr=0.1))
     Y = np.zeros((8, 362), np.float32)
     Y[np.arange(8), [361, 3, 361, 50, 7, 361, 200, 100]] = 1
+    w0 = c.model.get_weights()
     lg, lc = g.model.train_on_batch(X, Y), c.model.train_on_batch(X, Y)
     assert abs(lg - lc) < 1e-2 * abs(lc)
-    for a, b in zip(g.model.get_weights(), c.model.get_weights()):
-        assert np.abs(a - b).max() < 2e-2 * max(1e-3, np.abs(b).max())
+    rel = []
+    for a, b, b0 in zip(g.model.get_weights(), c.model.get_weights(), w0):
+        rel.append(float(np.abs(a - b).max() / max(np.abs(b - b0).max(), 1e-6)))
+    # the head-level parameters (position Bias, PassLogit W and b: fp32 logits on both sides)
+    # match to 2 % of their update; the conv tensors carry the bf16 trunk's rounding (<= 20 %
+    # of a tensor's largest update, which is ~1e-3 here)
+    assert max(rel[-3:]) < 2e-2, rel
+    assert max(rel) < 0.2, rel
+    dWg = g.model.get_weights()[-2] - w0[-2]
+    dWc = c.model.get_weights()[-2] - w0[-2]
+    assert np.abs(dWc).max() > 1e-4
+    assert np.abs(dWg - dWc).max() < 2e-2 * np.abs(dWc).max()
 
 
 @pytest.mark.gpu
