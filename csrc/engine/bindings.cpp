@@ -374,6 +374,37 @@ PYBIND11_MODULE(_rocgo, m) {
     return py::bytes(out);
   });
 
+  // Compress k equal-size chunks (a contiguous uint8 block [k, chunk]) in parallel on the shared
+  // pool: one bytes object per chunk, None where a chunk does not compress (h5lite.WDataset
+  // bulk appends).
+  m.def(
+      "lzf_compress_chunks",
+      [](py::array_t<uint8_t, py::array::c_style> block, size_t chunk, int nthreads) {
+        if (chunk == 0 || block.size() % chunk) throw std::invalid_argument("bad chunk size");
+        const int k = (int)(block.size() / chunk);
+        const uint8_t* src = block.data();
+        std::vector<std::string> out(k);
+        std::vector<size_t> len(k, 0);
+        {
+          py::gil_scoped_release nogil;
+          parallel_for(k, nthreads, [&](int i) {
+            out[i].resize(chunk + 64);
+            len[i] = lzf_compress(src + (size_t)i * chunk, chunk, (uint8_t*)&out[i][0], chunk);
+          });
+        }
+        py::list res;
+        for (int i = 0; i < k; ++i) {
+          if (len[i] == 0) {
+            res.append(py::none());
+          } else {
+            out[i].resize(len[i]);
+            res.append(py::bytes(out[i]));
+          }
+        }
+        return res;
+      },
+      py::arg("block"), py::arg("chunk"), py::arg("nthreads") = 8);
+
   register_search(m);
   register_rollout(m);
 }

@@ -53,18 +53,33 @@ class _Sink(object):
         self.offsets = self.f.require_group("file_offsets")
         self.f["features"] = np.bytes_(",".join(features))
         self.rows = 0
+        self._queue = []
 
     def add(self, file_name, states, actions):
+        """Queue one game's rows (written by flush(), in order)."""
         n = len(actions)
         if n == 0:
             return 0
-        self.states.append(states)
-        self.actions.append(np.asarray(actions, dtype=np.uint8).reshape(n, 2))
+        self._queue.append((np.asarray(states, dtype=np.uint8),
+                            np.asarray(actions, dtype=np.uint8).reshape(n, 2)))
         self.offsets[file_name.replace("/", ":")] = np.array([self.rows, n], dtype=np.int64)
         self.rows += n
         return n
 
+    def flush(self):
+        """Append the queued games as one block: whole 64-row chunks compress in parallel."""
+        if not self._queue:
+            return
+        st = np.concatenate([q[0] for q in self._queue]) if len(self._queue) > 1 else \
+            self._queue[0][0]
+        ac = np.concatenate([q[1] for q in self._queue]) if len(self._queue) > 1 else \
+            self._queue[0][1]
+        self._queue = []
+        self.states.append(st)
+        self.actions.append(ac)
+
     def close(self):
+        self.flush()
         self.f.close()
 
     def abort(self):
@@ -155,6 +170,7 @@ class GameConverter(object):
                     if verbose:
                         print("\t%d state/action pairs extracted" % n if n else
                               "\t-no usable data-")
+                sink.flush()
         except Exception:
             print("sgfs_to_hdf5 failed")
             sink.abort()

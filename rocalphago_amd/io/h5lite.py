@@ -717,9 +717,7 @@ class WDataset(object):
                 raise ValueError("resize beyond maxshape")
         self.shape = shape
 
-    def _flush_pending(self):
-        raw = self._pending.tobytes()
-        comp = _lzf_compress(raw) if self.compression == "lzf" else None
+    def _store_chunk(self, raw, comp):
         mask = 0
         if self.compression == "lzf" and comp is None:
             comp, mask = raw, 1  # incompressible: store raw with the filter skipped
@@ -727,7 +725,26 @@ class WDataset(object):
         addr = self._f._append_raw(data)
         self._flushed.append((self._pending_start, addr, len(data), mask))
         self._pending_start += self.chunks[0]
+
+    def _flush_pending(self):
+        raw = self._pending.tobytes()
+        self._store_chunk(raw, _lzf_compress(raw) if self.compression == "lzf" else None)
         self._pending[...] = 0
+
+    def _flush_full_chunks(self, rows, nthreads=8):
+        """With the pending chunk empty: write every whole chunk of ``rows`` directly
+        (LZF-compressed in parallel, natively); returns the number of rows consumed."""
+        c = self.chunks[0]
+        k = rows.shape[0] // c
+        if k < 2 or self.compression not in (None, "lzf"):
+            return 0
+        block = np.ascontiguousarray(rows[:k * c]).reshape(-1).view(np.uint8)
+        csize = block.size // k
+        comps = _engine().lzf_compress_chunks(block, csize, nthreads) \
+            if self.compression == "lzf" else [None] * k
+        for i in range(k):
+            self._store_chunk(block[i * csize:(i + 1) * csize].tobytes(), comps[i])
+        return k * c
 
     def __setitem__(self, key, value):
         if self.chunks is None:
@@ -764,6 +781,12 @@ class WDataset(object):
         done = 0
         while done < n:
             i = start + done
+            if i == self._pending_start and n - done >= 2 * c:
+                took = self._flush_full_chunks(rows[done:])
+                if took:
+                    done += took
+                    self._max_written = start + done
+                    continue
             while i >= self._pending_start + c:
                 self._flush_pending()
             off = i - self._pending_start
