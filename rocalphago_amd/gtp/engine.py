@@ -465,6 +465,20 @@ def main(argv=None):
     ap.add_argument("--temperature", type=float, default=0.67)
     ap.add_argument("--playouts", type=int, default=800)
     ap.add_argument("--name", default="RocAlphaGo-MI355X")
+    ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16",
+                    help="GPU compute precision of the networks (bf16 = fused HIP kernels)")
+    ap.add_argument("--value", default=None, help="value network JSON (mcts player)")
+    ap.add_argument("--value-weights", default=None)
+    ap.add_argument("--lmbda", type=float, default=None,
+                    help="value/rollout mix (default 0.5 with a value net, else 1 = rollouts)")
+    ap.add_argument("--c-puct", type=float, default=5.0)
+    ap.add_argument("--mcts-threads", type=int, default=8,
+                    help="host threads of the parallel tree descent / leaf featurisation")
+    ap.add_argument("--leaf-batch", type=int, default=256,
+                    help="leaves evaluated per GPU batch (one search wave)")
+    ap.add_argument("--virtual-loss", type=int, default=3,
+                    help="virtual visits added along a pending descent path")
+    ap.add_argument("--rollout-limit", type=int, default=500)
     args = ap.parse_args(argv)
     if args.model is None:
         class _Pass(object):
@@ -474,7 +488,7 @@ def main(argv=None):
     else:
         from ..models.nn_util import NeuralNetBase
         from ..players import ai
-        policy = NeuralNetBase.load_model(args.model)
+        policy = NeuralNetBase.load_model(args.model).set_dtype(args.dtype)
         if args.weights:
             policy.model.load_weights(args.weights)
         if args.player == "greedy":
@@ -483,7 +497,17 @@ def main(argv=None):
             player = ai.ProbabilisticPolicyPlayer(policy, temperature=args.temperature)
         else:
             from ..search.apv import ParallelMCTSPlayer
-            player = ParallelMCTSPlayer(policy, n_playout=args.playouts)
+            value = None
+            if args.value:
+                value = NeuralNetBase.load_model(args.value).set_dtype(args.dtype)
+                if args.value_weights:
+                    value.model.load_weights(args.value_weights)
+            lmbda = args.lmbda if args.lmbda is not None else (0.5 if value is not None else 1.0)
+            player = ParallelMCTSPlayer(policy, value, lmbda=lmbda, c_puct=args.c_puct,
+                                        n_playout=args.playouts, batch=args.leaf_batch,
+                                        virtual_loss=args.virtual_loss,
+                                        nthreads=args.mcts_threads,
+                                        rollout_limit=args.rollout_limit)
     run_gtp(player, name=args.name, version="1.0")
 
 

@@ -46,6 +46,17 @@ def default_device():
     return torch.device("cpu")
 
 
+PRECISIONS = ("bf16", "fp32")
+
+
+def default_precision():
+    """GPU compute precision of new models: ``RAG_DTYPE`` (bf16 | fp32), default bf16."""
+    p = os.environ.get("RAG_DTYPE", "bf16").lower()
+    if p not in PRECISIONS:
+        raise ValueError("RAG_DTYPE must be one of %s, got %r" % (PRECISIONS, p))
+    return p
+
+
 # --------------------------------------------------------------------------- layers
 
 _COUNTERS = {}
@@ -316,6 +327,10 @@ class KerasNet(torch.nn.Module):
         self.version = 0
         self._engine = None
         self.training_mode = False
+        # compute precision on the GPU: "bf16" = the fused HIP plans / HipConv2dFn (bf16
+        # operands, fp32 accumulation); "fp32" = reference precision through the generic
+        # executor with fp32 torch convolutions (parity checks against fp32 checkpoints)
+        self.precision = default_precision()
 
     # ---- weights
     def params_of(self, lname):
@@ -380,7 +395,7 @@ class KerasNet(torch.nn.Module):
         if c == "Convolution2D":
             W = params[0]
             b = params[1] if len(params) > 1 else None
-            if x.is_cuda and not _native.torch_fallback_allowed():
+            if x.is_cuda and self.precision == "bf16" and not _native.torch_fallback_allowed():
                 y = HipConv2dFn.apply(x, W, b)
             else:
                 y = F.conv2d(x, W, b, padding=cfg["nb_row"] // 2)
@@ -655,6 +670,19 @@ class Model(object):
         self._plan, self._plan_checked = None, False
         return self
 
+    @property
+    def precision(self):
+        return self.net.precision
+
+    def set_precision(self, precision):
+        """``"bf16"`` (default: fused HIP kernels) or ``"fp32"`` (reference precision, generic
+        executor with fp32 convolutions; no fused plan)."""
+        if precision not in PRECISIONS:
+            raise ValueError("precision must be one of %s, got %r" % (PRECISIONS, precision))
+        self.net.precision = precision
+        self._plan, self._plan_checked = None, False
+        return self
+
     # ---- serialisation
     def get_config(self):
         if not self.functional:
@@ -731,7 +759,8 @@ class Model(object):
     def _plan_for(self):
         if not self._plan_checked:
             from .fused import detect_plan
-            self._plan = detect_plan(self) if self.net.device.type == "cuda" else None
+            self._plan = detect_plan(self) if (self.net.device.type == "cuda" and
+                                               self.net.precision == "bf16") else None
             self._plan_checked = True
         return self._plan
 

@@ -58,6 +58,12 @@ class NeuralNetBase(object):
         new_net.forward = new_net._model_forward()
         return new_net
 
+    def set_dtype(self, dtype):
+        """GPU compute precision: ``"bf16"`` (fused HIP kernels, default) or ``"fp32"``
+        (reference precision through the generic executor)."""
+        self.model.set_precision(dtype)
+        return self
+
     def save_model(self, json_file, weights_file=None):
         object_specs = {
             'class': self.__class__.__name__,

@@ -165,6 +165,7 @@ def run_training(cmd_line_args=None):
     parser.add_argument("--resume", help="Load latest weights in out_directory and resume", default=False, action="store_true")  # noqa: E501
     parser.add_argument("--update", help="per_game (reference) or batched (default with >1 rank)", choices=["per_game", "batched"], default=None)  # noqa: E501
     parser.add_argument("--verbose", "-v", help="Turn on verbose mode", default=False, action="store_true")  # noqa: E501
+    parser.add_argument("--dtype", help="GPU compute precision: bf16 (fused HIP kernels) or fp32 (reference precision, generic executor). Default: bf16", choices=["bf16", "fp32"], default="bf16")  # noqa: E501
     if cmd_line_args is None:
         args = parser.parse_args()
     else:
@@ -203,12 +204,12 @@ def run_training(cmd_line_args=None):
         player_weights = os.path.basename(args.initial_weights)
     dp.barrier()
 
-    policy = CNNPolicy.load_model(args.model_json, device=dp.device)
+    policy = CNNPolicy.load_model(args.model_json, device=dp.device).set_dtype(args.dtype)
     policy.model.load_weights(args.initial_weights)
     dp.broadcast_model(policy.model)
     player = ProbabilisticPolicyPlayer(policy, temperature=args.policy_temp,
                                        move_limit=args.move_limit)
-    opp_policy = CNNPolicy.load_model(args.model_json, device=dp.device)
+    opp_policy = CNNPolicy.load_model(args.model_json, device=dp.device).set_dtype(args.dtype)
     opponent = ProbabilisticPolicyPlayer(opp_policy, temperature=args.policy_temp,
                                          move_limit=args.move_limit)
     if args.verbose and dp.is_root:

@@ -204,6 +204,7 @@ def run_training(cmd_line_args=None):
     parser.add_argument("--train-val-test", help="Fraction of data to use for training/val/test. Must sum to 1. Invalid if restarting training", nargs=3, type=float, default=[0.93, .05, .02])  # noqa: E501
     parser.add_argument("--symmetries", help="Comma-separated list of transforms, subset of noop,rot90,rot180,rot270,fliplr,flipud,diag1,diag2", default='noop,rot90,rot180,rot270,fliplr,flipud,diag1,diag2')  # noqa: E501
     parser.add_argument("--seed", help="RNG seed for shuffling / symmetries", type=int, default=None)  # noqa: E501
+    parser.add_argument("--dtype", help="GPU compute precision: bf16 (fused HIP kernels) or fp32 (reference precision, generic executor). Default: bf16", choices=["bf16", "fp32"], default="bf16")  # noqa: E501
     if cmd_line_args is None:
         args = parser.parse_args()
     else:
@@ -221,7 +222,7 @@ def run_training(cmd_line_args=None):
         else:
             print("starting fresh output directory %s" % args.out_directory)
 
-    policy = CNNPolicy.load_model(args.model, device=dp.device)
+    policy = CNNPolicy.load_model(args.model, device=dp.device).set_dtype(args.dtype)
     model_features = policy.preprocessor.feature_list
     model = policy.model
     if resume:

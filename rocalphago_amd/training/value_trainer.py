@@ -200,12 +200,13 @@ def run_training(cmd_line_args=None):
     parser.add_argument("--symmetries", default='noop,rot90,rot180,rot270,fliplr,flipud,diag1,diag2')  # noqa: E501
     parser.add_argument("--weights", default=None, help="resume from weights in out_directory")
     parser.add_argument("--seed", type=int, default=0)
+    parser.add_argument("--dtype", help="GPU compute precision: bf16 (fused HIP kernels) or fp32 (reference precision, generic executor). Default: bf16", choices=["bf16", "fp32"], default="bf16")  # noqa: E501
     parser.add_argument("--verbose", "-v", default=False, action="store_true")
     args = parser.parse_args(cmd_line_args)
 
     dp = DPContext()
     resume = args.weights is not None
-    net = CNNValue.load_model(args.model, device=dp.device)
+    net = CNNValue.load_model(args.model, device=dp.device).set_dtype(args.dtype)
     model = net.model
     if resume:
         model.load_weights(os.path.join(args.out_directory, args.weights))

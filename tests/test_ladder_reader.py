@@ -54,12 +54,16 @@ def test_superko_board_uses_copying_reader():
 
 
 def test_reader_is_faster():
+    """Best of several passes each (robust to a loaded host / parallel test workers)."""
     states = random_games(48, 19, 12, 150, 400)
-    t0 = time.perf_counter()
-    for st in states:
-        rg.ladder_planes(st.native, True)
-    t1 = time.perf_counter()
-    for st in states:
-        rg.ladder_planes(st.native, False)
-    t2 = time.perf_counter()
-    assert (t2 - t1) < (t1 - t0)
+
+    def best(copying):
+        ts = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            for st in states:
+                rg.ladder_planes(st.native, copying)
+            ts.append(time.perf_counter() - t0)
+        return min(ts)
+
+    assert best(False) < best(True)
