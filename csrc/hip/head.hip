@@ -414,6 +414,7 @@ RAG_API int rag_value_mlp_fwd(const float* z, const float* W1, const float* b1, 
   const int nblk = (B + kMlpRows - 1) / kMlpRows * ntile;
   value_mlp_part_kernel<<<nblk, 64 * kMlpWaves, sm, stream>>>(z, W1, b1, W2, work, hout, B, P, H,
                                                               act);
-  value_mlp_out_kernel<<<(B + 255) / 256, 256, 0, stream>>>(work, b2, out, B, ntile);
+  // out == null (training): the column partials in `work` feed rag_value_mlp_bwd instead
+  if (out) value_mlp_out_kernel<<<(B + 255) / 256, 256, 0, stream>>>(work, b2, out, B, ntile);
   return (int)hipGetLastError();
 }

@@ -429,7 +429,8 @@ class PolicyHeadEngine(object):
 
 class ValueHeadEngine(object):
     """1x1 conv (K->1) on HIP; Dense(S*S->H) + act; Dense(H->1) + tanh: inference through the
-    fused value_mlp_fwd HIP kernel (fused.ValuePlan.forward), training through torch GEMMs."""
+    fused value_mlp_fwd HIP kernel (fused.ValuePlan.forward), training through
+    ops.value_mlp_train (head.hip + value_bwd.hip: loss and every head gradient on HIP)."""
 
     def __init__(self, trunk, K):
         self.trunk = trunk
@@ -441,7 +442,12 @@ class ValueHeadEngine(object):
         if B <= self._B:
             return
         self.z = torch.empty((B, self.S * self.S), device=self.trunk.device)
+        self.dz = torch.empty((B, self.S * self.S), device=self.trunk.device)
         self._B = B
+
+    def dz_buffer(self, B):
+        self.ensure(B)
+        return self.dz[:B]
 
     def conv_out(self, B, w, b0):
         self.ensure(B)

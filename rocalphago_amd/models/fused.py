@@ -224,25 +224,14 @@ class ValuePlan(_TrunkPlan):
         w, b0 = self.head_params()
         z = self.head.conv_out(B, w, b0)
         W1, b1, W2, b2 = self._dense_params()
-        # z @ W1 + b1 on the value-MLP HIP kernel (a library GEMM puts this 256 x 256 output on
-        # one workgroup); autograd from the pre-activation on; dW1 / db1 / dz by hand below.
-        h = torch.empty((B, W1.shape[1]), dtype=torch.float32, device=z.device)
-        ops.value_mlp_fwd(z, W1, b1, W2, b2, act=self.act1, hout=h)
-        h.requires_grad_()
-        W2p, b2p = W2.detach().requires_grad_(), b2.detach().requires_grad_()
-        v = self._mlp_tail(h, W2p, b2p)
-        per = ((v - y) ** 2).mean(-1)
-        if sw is not None:
-            per = per * sw / (sw != 0).float().mean().clamp_min(1e-12)
-        lossv = per.mean()
-        dh, dW2, db2 = torch.autograd.grad(lossv, [h, W2p, b2p])
+        # the whole MLP head (forward, MSE loss, dW1 / db1 / dW2 / db2 / dz) on HIP kernels
+        # (ops.value_mlp_train: head.hip forward partials + value_bwd.hip)
         gW1, gb1, gW2, gb2 = self.net.grads_of(self.d1) + self.net.grads_of(self.d2)
-        with torch.no_grad():
-            gW1.copy_(z.t() @ dh)
-            gb1.copy_(dh.sum(0))
-            gW2.copy_(dW2)
-            gb2.copy_(db2)
-            dz = dh @ W1.t()
+        dz = self.head.dz_buffer(B)
+        yv = y.reshape(-1).float().contiguous()
+        swv = sw.reshape(-1).float().contiguous() if sw is not None else None
+        lossv = ops.value_mlp_train(z, W1, b1, W2, b2, yv, swv, self.act1, gW1, gb1, gW2, gb2,
+                                    dz=dz).sum()
         dw, db0 = self.head_grads()
         self.head.backward_conv(B, w, dz, dw, db0)
         dWs, dbs = self._grads()

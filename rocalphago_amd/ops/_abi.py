@@ -27,6 +27,8 @@ SIGNATURES = {
     "rag_head_linear": [P, P, P, P, I, I, I, I, P],
     "rag_value_mlp_fwd": [P, P, P, P, P, P, P, P, I, I, I, I, P],
     "rag_value_mlp_workspace": [I, I],
+    "rag_value_mlp_bwd": [P] * 16 + [I, I, I, I, P],
+    "rag_value_mlp_bwd_workspace": [I, I],
     # optim.hip
     "rag_sgd": [P, P, P, I64, F, F, F, I, P],
     # rollout.hip
@@ -53,7 +55,7 @@ SIGNATURES = {
 
 RESTYPES = {"rag_conv_wgrad_workspace": SZ, "rag_head_bwd_workspace": SZ,
             "rag_ladder_workspace": SZ,
-            "rag_value_mlp_workspace": SZ}
+            "rag_value_mlp_workspace": SZ, "rag_value_mlp_bwd_workspace": SZ}
 
 
 def declare(lib):

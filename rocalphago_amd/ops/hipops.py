@@ -274,6 +274,47 @@ def value_mlp_fwd(z, W1, b1, W2, b2, act="linear", out=None, hout=None):
     return out
 
 
+_mlp_train_ws = {}
+
+
+def value_mlp_train(z, W1, b1, W2, b2, y, sw, act, dW1, db1, dW2, db2, dz=None, vout=None):
+    """Forward + backward of the value MLP head under the MSE loss, all on HIP kernels
+    (head.hip value_mlp_part_kernel, value_bwd.hip): writes dW1 [P, H], db1 [H], dW2 [H],
+    db2 [1] and (optional) dz [B, P] = dL/dz; returns the per-board loss terms [B] (their sum is
+    the batch loss). y: targets [B] or [B, 1]; sw: optional sample weights [B]."""
+    B, P = z.shape
+    H = W1.shape[1]
+    if (W1.shape != (P, H) or b1.numel() != H or W2.numel() != H or b2.numel() != 1
+            or act not in MLP_ACTS or y.numel() != B or (sw is not None and sw.numel() != B)):
+        raise ValueError("value_mlp_train: bad shapes/activation %s %s %s" %
+                         (tuple(z.shape), tuple(W1.shape), act))
+    for t in (z, W1, b1, W2, b2, y, sw, dW1, db1, dW2, db2, dz, vout):
+        if t is not None and (t.dtype != torch.float32 or not t.is_contiguous()):
+            raise ValueError("value_mlp_train expects contiguous fp32 tensors")
+    if dW1.numel() != P * H or db1.numel() != H or dW2.numel() != H or db2.numel() != 1 or \
+            (dz is not None and dz.shape != (B, P)) or (vout is not None and vout.numel() != B):
+        raise ValueError("value_mlp_train: bad gradient shapes")
+    lib = _lib()
+    stream = _stream()
+    key = (z.device, stream.value)
+    ws = _mlp_train_ws.get(key)
+    npart, nbwd = lib.rag_value_mlp_workspace(B, H), lib.rag_value_mlp_bwd_workspace(B, H)
+    if ws is None or ws[0].numel() < npart or ws[1].numel() < B * H or ws[2].numel() < nbwd \
+            or ws[3].numel() < B:
+        ws = tuple(torch.empty(n, dtype=torch.float32, device=z.device)
+                   for n in (npart, B * H, nbwd, B))
+        _mlp_train_ws[key] = ws
+    part, hpre, work, loss = ws
+    _check(lib.rag_value_mlp_fwd(_ptr(z), _ptr(W1), _ptr(b1), _ptr(W2), _ptr(b2), _ptr(None),
+                                 _ptr(part), _ptr(hpre), B, P, H, MLP_ACTS[act], stream),
+           "value_mlp_fwd")
+    _check(lib.rag_value_mlp_bwd(_ptr(z), _ptr(W1), _ptr(W2), _ptr(b2), _ptr(hpre), _ptr(part),
+                                 _ptr(y), _ptr(sw), _ptr(work), _ptr(loss), _ptr(vout),
+                                 _ptr(dW1), _ptr(db1), _ptr(dW2), _ptr(db2), _ptr(dz), B, P, H,
+                                 MLP_ACTS[act], stream), "value_mlp_bwd")
+    return loss[:B]
+
+
 def sample_moves(probs, mask, beta=1.0, greedy=None, seed=0, out=None):
     """Per row: a move drawn from probs^beta restricted to ``mask`` (uint8 [B, >=P]), or the
     masked argmax where ``greedy`` (uint8 [B]) is set; -1 for rows without candidates

@@ -65,9 +65,9 @@ def test_value_net_gpu(cuda):
 
 
 
-@pytest.mark.parametrize("dense_act", ["relu", "linear"])
+@pytest.mark.parametrize("dense_act", ["relu", "linear", "tanh"])
 def test_value_train_step_matches_cpu(cuda, dense_act):
-    """HIP value plan (value-MLP kernel forward + hand-written dW1/db1/dz) vs torch autograd."""
+    """HIP value plan (value-MLP forward + value_bwd.hip head gradients) vs torch autograd."""
     from rocalphago_amd.features.preprocessing import VALUE_FEATURES
     g, c = _pair(CNNValue, VALUE_FEATURES, filters_per_layer=32, layers=3,
                  dense_activation=dense_act)
@@ -93,7 +93,7 @@ def test_value_train_step_matches_cpu(cuda, dense_act):
     print(dense_act, ["%s:%.4f" % (a.shape, e) for a, e in zip(gw, errs)])
     # relu: bf16-level differences of z flip the ReLU mask of near-zero units, which moves the
     # W1/b1 updates by ~8 %; the kernel itself is pinned to 1e-4 by test_value_mlp_fwd
-    assert max(errs[-4:]) < (2e-2 if dense_act == "linear" else 0.15), errs
+    assert max(errs[-4:]) < (2e-2 if dense_act != "relu" else 0.15), errs
     assert max(errs) < 0.25, errs
 
 def test_resnet_uses_hip_convs(cuda):

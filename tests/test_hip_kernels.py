@@ -260,7 +260,50 @@ def test_value_mlp_fwd(ops, B, P, H, act):
     h = z.double() @ W1.double() + b1.double()
     h = {"linear": h, "relu": torch.relu(h), "tanh": torch.tanh(h)}[act]
     ref = torch.tanh(h @ W2.double() + b2.double()).float()
-    out = ops.value_mlp_fwd(z, W1, b1, W2, b2, act=act)
+    hout = torch.empty(B, H, device=dev)
+    out = ops.value_mlp_fwd(z, W1, b1, W2, b2, act=act, hout=hout)
     torch.cuda.synchronize()
     assert out.shape == (B, 1)
     assert (out - ref).abs().max().item() < 1e-4
+    href = (z.double() @ W1.double() + b1.double()).float()
+    assert rel_err(hout, href) < 1e-5
+
+
+@pytest.mark.parametrize("B,P,H,act,weighted", [(256, 361, 256, "relu", False),
+                                                (100, 361, 256, "tanh", True),
+                                                (7, 49, 200, "linear", True),
+                                                (1, 81, 64, "relu", False),
+                                                (130, 361, 300, "tanh", False)])
+def test_value_mlp_train(ops, B, P, H, act, weighted):
+    """Loss and every head gradient of the HIP value-MLP training path vs fp64 autograd."""
+    dev = torch.device("cuda")
+    torch.manual_seed(5)
+    z = torch.randn(B, P, device=dev)
+    W1 = torch.randn(P, H, device=dev) * 0.05
+    b1 = torch.randn(H, device=dev) * 0.1
+    W2 = torch.randn(H, 1, device=dev) * 0.1
+    b2 = torch.randn(1, device=dev) * 0.1
+    y = torch.rand(B, device=dev) * 2 - 1
+    sw = None
+    if weighted:
+        sw = torch.rand(B, device=dev) * 2 - 1
+        sw[::3] = 0
+    ps = [t.double().requires_grad_() for t in (z, W1, b1, W2, b2)]
+    h = ps[0] @ ps[1] + ps[2]
+    h = {"linear": h, "relu": torch.relu(h), "tanh": torch.tanh(h)}[act]
+    v = torch.tanh(h @ ps[3] + ps[4]).reshape(-1)
+    per = (v - y.double()) ** 2
+    if sw is not None:
+        per = per * sw.double() / (sw != 0).double().mean()
+    lref = per.mean()
+    grads = torch.autograd.grad(lref, ps)
+    g = [torch.full(t.shape, float("nan"), device=dev) for t in (W1, b1, W2, b2)]
+    dz = torch.full((B, P), float("nan"), device=dev)
+    vout = torch.empty(B, device=dev)
+    loss = ops.value_mlp_train(z, W1, b1, W2, b2, y, sw, act, *g, dz=dz, vout=vout)
+    torch.cuda.synchronize()
+    assert abs(loss.sum().item() - lref.item()) < 1e-5 * max(1.0, abs(lref.item()))
+    assert (vout - v.detach().float()).abs().max().item() < 1e-5
+    for name, got, want in zip(["dz", "dW1", "db1", "dW2", "db2"], [dz] + g, grads):
+        assert torch.isfinite(got).all(), name
+        assert rel_err(got.reshape(want.shape), want.float()) < 1e-4, name
