@@ -33,7 +33,9 @@ using namespace rag;
 
 namespace {
 
-constexpr int kWaves = 4;  // games per 256-thread block
+// games (waves) per block: 4 (256 threads, 26 KB LDS) or 1 (64 threads, 6.5 KB LDS, so a
+// block fits next to two 76 KB conv blocks on a CU while the search's nets run): RAG_ROLLOUT_GPB
+
 constexpr uint8_t kOff = 3;  // colour code of an off-board neighbour
 
 template <int PM>
@@ -46,9 +48,9 @@ struct GameLds {
   uint8_t dirty[PM];
 };
 
-template <int PM>
+template <int PM, int GPB>
 struct BlockLds {
-  GameLds<PM> g[kWaves];
+  GameLds<PM> g[GPB];
 };
 
 // ring slot k of the 3x3 neighbourhood, clockwise from north ((x, y+1) first)
@@ -367,9 +369,9 @@ struct Game {
 };
 
 // meta: [cur, ko, last1, last2, passes_b, passes_w, nmoves, end]
-template <int SC, int NPL, int PM>
+template <int SC, int NPL, int PM, int GPB>
 __device__ __forceinline__ void rollout_body(
-    BlockLds<PM>& sh, const int8_t* __restrict__ colors, const int32_t* __restrict__ meta,
+    BlockLds<PM, GPB>& sh, const int8_t* __restrict__ colors, const int32_t* __restrict__ meta,
     int n_pos, int R, int S_rt, float komi, int limit, const float* __restrict__ w,
     const float* __restrict__ pattern, uint32_t seed, int8_t* __restrict__ winner,
     int16_t* __restrict__ length, float* __restrict__ dbg_logits) {
@@ -377,7 +379,7 @@ __device__ __forceinline__ void rollout_body(
   const int P = S * S;
   const int wv = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
-  const int game = blockIdx.x * kWaves + wv;
+  const int game = blockIdx.x * GPB + wv;
   if (game >= n_pos * R) return;  // whole wave exits together
   const int pos = game / R;
   GameLds<PM>& L = sh.g[wv];
@@ -583,17 +585,17 @@ __device__ __forceinline__ void rollout_body(
 // The same playout body at two register budgets: the compiler's choice (146 VGPRs for 19x19,
 // 3 waves per SIMD) and a cap at 128 VGPRs (4 waves per SIMD, a few spills outside the move
 // loop). RAG_ROLLOUT_WPE=3|4 picks one (default measured: see docs/KERNELS.md).
-template <int SC, int NPL, int PM>
-__global__ void __launch_bounds__(256) rollout_kernel(RAG_RO_ARGS) {
-  __shared__ BlockLds<PM> sh;
-  rollout_body<SC, NPL, PM>(sh, RAG_RO_FWD);
+template <int SC, int NPL, int PM, int GPB>
+__global__ void __launch_bounds__(64 * GPB) rollout_kernel(RAG_RO_ARGS) {
+  __shared__ BlockLds<PM, GPB> sh;
+  rollout_body<SC, NPL, PM, GPB>(sh, RAG_RO_FWD);
 }
 
-template <int SC, int NPL, int PM>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+template <int SC, int NPL, int PM, int GPB>
+__global__ void __launch_bounds__(64 * GPB) __attribute__((amdgpu_waves_per_eu(4)))
 rollout_kernel_w4(RAG_RO_ARGS) {
-  __shared__ BlockLds<PM> sh;
-  rollout_body<SC, NPL, PM>(sh, RAG_RO_FWD);
+  __shared__ BlockLds<PM, GPB> sh;
+  rollout_body<SC, NPL, PM, GPB>(sh, RAG_RO_FWD);
 }
 
 int rollout_wpe() {
@@ -604,18 +606,39 @@ int rollout_wpe() {
   return v;
 }
 
-template <int SC, int NPL, int PM>
-void launch(dim3 grid, hipStream_t st, const int8_t* c, const int32_t* meta, int n_pos, int R,
-            int S, float komi, int limit, const float* w, const float* pattern, unsigned seed,
-            void* winner, void* length, float* dbg) {
+int rollout_gpb() {
+  static int v = [] {
+    const char* e = getenv("RAG_ROLLOUT_GPB");
+    return e && atoi(e) == 4 ? 4 : 1;
+  }();
+  return v;
+}
+
+template <int SC, int NPL, int PM, int GPB>
+void launch_gpb(hipStream_t st, const int8_t* c, const int32_t* meta, int n_pos, int R, int S,
+                float komi, int limit, const float* w, const float* pattern, unsigned seed,
+                void* winner, void* length, float* dbg) {
+  const dim3 grid((n_pos * R + GPB - 1) / GPB);
   if (rollout_wpe() == 4)
-    rollout_kernel_w4<SC, NPL, PM><<<grid, 256, 0, st>>>(c, meta, n_pos, R, S, komi, limit, w,
-                                                         pattern, seed, (int8_t*)winner,
-                                                         (int16_t*)length, dbg);
+    rollout_kernel_w4<SC, NPL, PM, GPB><<<grid, 64 * GPB, 0, st>>>(
+        c, meta, n_pos, R, S, komi, limit, w, pattern, seed, (int8_t*)winner, (int16_t*)length,
+        dbg);
   else
-    rollout_kernel<SC, NPL, PM><<<grid, 256, 0, st>>>(c, meta, n_pos, R, S, komi, limit, w,
-                                                      pattern, seed, (int8_t*)winner,
-                                                      (int16_t*)length, dbg);
+    rollout_kernel<SC, NPL, PM, GPB><<<grid, 64 * GPB, 0, st>>>(
+        c, meta, n_pos, R, S, komi, limit, w, pattern, seed, (int8_t*)winner, (int16_t*)length,
+        dbg);
+}
+
+template <int SC, int NPL, int PM>
+void launch(hipStream_t st, const int8_t* c, const int32_t* meta, int n_pos, int R, int S,
+            float komi, int limit, const float* w, const float* pattern, unsigned seed,
+            void* winner, void* length, float* dbg) {
+  if (rollout_gpb() == 4)
+    launch_gpb<SC, NPL, PM, 4>(st, c, meta, n_pos, R, S, komi, limit, w, pattern, seed, winner,
+                               length, dbg);
+  else
+    launch_gpb<SC, NPL, PM, 1>(st, c, meta, n_pos, R, S, komi, limit, w, pattern, seed, winner,
+                               length, dbg);
 }
 
 }  // namespace
@@ -628,12 +651,10 @@ RAG_API int rag_rollouts(const void* colors, const int32_t* meta, int n_pos, int
                          unsigned seed, void* winner, void* length, float* dbg_logits,
                          hipStream_t stream) {
   if (S < 2 || S > 25 || n_pos <= 0 || R <= 0) return -1;
-  const int games = n_pos * R;
-  dim3 grid((games + kWaves - 1) / kWaves);
   const int8_t* c = (const int8_t*)colors;
-#define RAG_RO(SC, NPL, PM)                                                                    \
-  launch<SC, NPL, PM>(grid, stream, c, meta, n_pos, R, S, komi, limit, w, pattern, seed, winner, \
-                      length, dbg_logits)
+#define RAG_RO(SC, NPL, PM)                                                                     \
+  launch<SC, NPL, PM>(stream, c, meta, n_pos, R, S, komi, limit, w, pattern, seed, winner, length, \
+                      dbg_logits)
   if (S == 19) RAG_RO(19, 6, 384);
   else if (S == 13) RAG_RO(13, 3, 192);
   else if (S == 9) RAG_RO(9, 2, 128);
