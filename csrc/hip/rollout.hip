@@ -46,6 +46,7 @@ struct GameLds {
   uint8_t cell[PM];
   uint8_t chg[PM];
   uint8_t dirty[PM];
+  int16_t list[PM];  // compacted dirty points (refresh)
 };
 
 template <int PM, int GPB>
@@ -302,8 +303,10 @@ struct Game {
   }
 
   // mark the 3x3 neighbourhoods of changed cells dirty, recompute their bases, clear the flags.
-  // The recompute gathers every dirty point's neighbourhood first and then issues all pattern
-  // loads together (one global round trip per move, not one per point).
+  // The dirty points (typically 10-40 of 361) are compacted into a list with a ballot per lane
+  // slot, so the base recompute (8-cell gather, two pattern loads, ~150 instructions of
+  // base_from) runs once per lane per 64 dirty points instead of once per lane slot with most
+  // lanes masked off; one global round trip per 64 dirty points.
   __device__ void refresh(const float* __restrict__ w, const float* __restrict__ pattern) {
     const int P_ = P();
     uint8_t ch[NPL];
@@ -325,44 +328,47 @@ struct Game {
         if (q[j] >= 0) L->dirty[q[j]] = 1;
     }
     wave_sync();
-    uint8_t d[NPL], cs[NPL];
+    uint8_t d[NPL];
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
       const int p = lane + 64 * k;
       d[k] = p < P_ ? L->dirty[p] : (uint8_t)0;
-      cs[k] = p < P_ ? L->cell[p] : (uint8_t)0;
     }
-    uint64_t r8[NPL];
+    int n = 0;
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
       const int p = lane + 64 * k;
-      r8[k] = (d[k] && !(cs[k] & 3)) ? gather(p) : 0;
-    }
-    float pv[NPL][2];
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) {
-      pv[k][0] = pv[k][1] = 0.f;
-      if (d[k] && !(cs[k] & 3) && pattern) {
-        int pb, pw;
-        pattern_idx(r8[k], pb, pw);
-        pv[k][0] = pattern[pb];
-        pv[k][1] = pattern[pw];
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) {
-      const int p = lane + 64 * k;
-      if (p >= P_) continue;
+      const uint64_t m = __ballot(d[k] != 0);
+      const int slot =
+          n + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
       if (d[k]) {
-        if (cs[k] & 3) {
-          L->base[0][p] = -INFINITY;
-          L->base[1][p] = -INFINITY;
-        } else {
-          base_from(p, r8[k], pv[k][0], pv[k][1], w);
-        }
+        L->list[slot] = (int16_t)p;
         L->dirty[p] = 0;
       }
       if (ch[k]) L->chg[p] = 0;
+      n += __popcll(m);
+    }
+    wave_sync();
+    for (int r = 0; r < n; r += 64) {
+      const int i = r + lane;
+      if (i < n) {
+        const int p = L->list[i];
+        if (L->cell[p] & 3) {
+          L->base[0][p] = -INFINITY;
+          L->base[1][p] = -INFINITY;
+        } else {
+          const uint64_t r8 = gather(p);
+          float pb = 0.f, pw = 0.f;
+          if (pattern) {
+            int ib, iw;
+            pattern_idx(r8, ib, iw);
+            pb = pattern[ib];
+            pw = pattern[iw];
+          }
+          base_from(p, r8, pb, pw, w);
+        }
+      }
     }
     wave_sync();
   }
@@ -418,15 +424,14 @@ __device__ __forceinline__ void rollout_body(
   LaneRng rng{hash32(seed ^ hash32(game * 0x9E3779B9u + lane * 0x85EBCA6Bu + 1u))};
 
   // logit of lane point k = cached base + last-move terms
+  // (branch-free: selects instead of early returns; adding 0 to a finite logit and anything to
+  // -inf leave it unchanged, so the values equal the branchy form bit for bit)
   auto full_logit = [&](int k, int own_idx, int l1x, int l1y, int l2x, int l2y) -> float {
-    const int p = lane + 64 * k;
-    if (p >= P || p == ko) return -INFINITY;
-    float v = L.base[own_idx][p];
-    if (v == -INFINITY) return v;
+    const int p = lane + 64 * k;  // < PM: the base read is in bounds even for p >= P
+    float v = (p < P && p != ko) ? L.base[own_idx][p] : -INFINITY;
     const int d1x = abs(px[k] - l1x), d1y = abs(py[k] - l1y);
-    if (d1x <= 1 && d1y <= 1) v += wl[0];
-    else if (d1x + d1y <= 2) v += wl[4];
-    if (abs(px[k] - l2x) <= 1 && abs(py[k] - l2y) <= 1) v += wl[5];
+    v += (d1x <= 1 && d1y <= 1) ? wl[0] : (d1x + d1y <= 2 ? wl[4] : 0.f);
+    v += (abs(px[k] - l2x) <= 1 && abs(py[k] - l2y) <= 1) ? wl[5] : 0.f;
     return v;
   };
 
@@ -452,12 +457,15 @@ __device__ __forceinline__ void rollout_body(
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
       const float lg = full_logit(k, own - 1, l1x, l1y, l2x, l2y);
-      if (lg == -INFINITY) continue;
-      const float kk = lg - __logf(-__logf(rng.uniform()));
-      if (kk > key) {
-        key = kk;
-        idx = lane + 64 * k;
-      }
+      // the lane's generator advances only on candidates (as the branchy form did)
+      const bool cand = lg != -INFINITY;
+      const uint32_t s1 = rng.s * 1664525u + 1013904223u;
+      rng.s = cand ? s1 : rng.s;
+      const float u = ((hash32(s1) >> 8) + 0.5f) * (1.0f / 16777216.0f);
+      const float kk = cand ? lg - __logf(-__logf(u)) : -INFINITY;
+      const bool better = kk > key;
+      key = better ? kk : key;
+      idx = better ? lane + 64 * k : idx;
     }
     wave_argmax(key, idx);
     const int mv = key == -INFINITY ? -1 : idx;  // -1 = pass

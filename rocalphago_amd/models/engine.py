@@ -108,6 +108,7 @@ class HipTrunk(_PackedConvs):
     def ensure_batch(self, B):
         if B <= self._B:
             return
+        self.gen = getattr(self, "gen", 0) + 1  # buffers moved (captured graphs)
         B = max(B, 1)
         S = self.S
         self.halo = self._halos()
@@ -260,6 +261,7 @@ class ResTrunk(_PackedConvs):
     def ensure_batch(self, B):
         if B <= self._B:
             return
+        self.gen = getattr(self, "gen", 0) + 1  # buffers moved (captured graphs)
         B = max(B, 1)
         S, KP, dev = self.S, self.KP, self.device
         alloc = ops.alloc_padded
@@ -389,6 +391,7 @@ class PolicyHeadEngine(object):
     def ensure(self, B):
         if B <= self._B:
             return
+        self.gen = getattr(self, "gen", 0) + 1  # buffers moved (captured graphs)
         dev = self.trunk.device
         S2 = self.S * self.S
         self.probs = torch.empty((B, S2 + (1 if self.pass_logit else 0)), device=dev)
@@ -441,6 +444,7 @@ class ValueHeadEngine(object):
     def ensure(self, B):
         if B <= self._B:
             return
+        self.gen = getattr(self, "gen", 0) + 1  # buffers moved (captured graphs)
         self.z = torch.empty((B, self.S * self.S), device=self.trunk.device)
         self.dz = torch.empty((B, self.S * self.S), device=self.trunk.device)
         self._B = B

@@ -76,6 +76,12 @@ class _TrunkPlan(object):
         self.head_name = head_conv.name
         self.K = specs[-1].cout
 
+    def sync_weights(self):
+        """Repack the bf16 trunk weights if the fp32 masters changed (a replayed graph reads the
+        packed copies at fixed addresses)."""
+        Ws, bs = self._params()
+        self.trunk.sync_weights(Ws, bs, self.net.weights_version())
+
     def _params(self):
         Ws, bs = [], []
         for name in self.conv_names:

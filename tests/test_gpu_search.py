@@ -131,3 +131,54 @@ def test_apv_with_gpu_networks(gro):
     mv = mc.get_move(st)
     assert st.is_legal(mv)
     assert mc.stats["sims"] >= 500
+
+
+def test_graph_replayed_evaluation_matches_eager(monkeypatch):
+    """NetworkEvaluator.submit replays a captured HIP graph from the second wave of a size on;
+    its priors / values / sensibleness equal the eager pass, also after a weight update."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from rocalphago_amd.features.preprocessing import DEFAULT_FEATURES
+    from rocalphago_amd.models.policy import CNNPolicy
+    from rocalphago_amd.models.value import CNNValue
+    from rocalphago_amd.search.apv import NetworkEvaluator
+    dev = torch.device("cuda")
+    pol = CNNPolicy(DEFAULT_FEATURES, board=19, filters_per_layer=64, layers=4, device=dev,
+                    seed=3)
+    val = CNNValue(DEFAULT_FEATURES + ["color"], board=19, filters_per_layer=64, layers=4,
+                   device=dev, seed=4)
+    boards = [s.native for s in _random_positions(40, 19, 7)]
+    other = [s.native for s in _random_positions(40, 19, 8)]
+    monkeypatch.setenv("RAG_EVAL_GRAPH", "0")
+    eager = NetworkEvaluator(pol, val)
+    ref = [eager.submit(b).result() for b in (boards, other)]
+    monkeypatch.setenv("RAG_EVAL_GRAPH", "1")
+    ev = NetworkEvaluator(pol, val)
+    for rep in range(3):  # eager, capture + replay, replay
+        for b, r in zip((boards, other), ref):
+            got = ev.submit(b).result()
+            for g, e in zip(got, r):
+                assert np.array_equal(g, e), rep
+    assert len(ev._graphs) == 1
+    # a larger wave reallocates the activations: graphs of the smaller size must be re-captured
+    small = boards[:20]
+    monkeypatch.setenv("RAG_EVAL_GRAPH", "0")
+    ref_small = NetworkEvaluator(pol, val).submit(small).result()
+    monkeypatch.setenv("RAG_EVAL_GRAPH", "1")
+    ev2 = NetworkEvaluator(pol, val)
+    for b in (small, small, small, boards + other, small, small):
+        got = ev2.submit(b).result()
+        if len(b) == 20:
+            for g, e in zip(got, ref_small):
+                assert np.array_equal(g, e)
+    # a weight update reaches the replayed graph through the packed-weight refresh
+    w = pol.model.get_weights()
+    w[0] = w[0] * 0.5
+    pol.model.set_weights(w)
+    monkeypatch.setenv("RAG_EVAL_GRAPH", "0")
+    ref2 = NetworkEvaluator(pol, val).submit(boards).result()
+    monkeypatch.setenv("RAG_EVAL_GRAPH", "1")
+    got2 = ev.submit(boards).result()
+    assert not np.array_equal(ref2[0], ref[0][0])
+    for g, e in zip(got2, ref2):
+        assert np.array_equal(g, e)
