@@ -114,13 +114,23 @@ class DPContext(object):
 class BucketedAllReduce(object):
     """Async all-reduce of a flat gradient buffer in layer-aligned buckets (back to front)."""
 
-    def __init__(self, ctx, flat_grad, layer_offsets, bucket_bytes=4 << 20, timer=None):
+    def __init__(self, ctx, flat_grad, layer_offsets, bucket_bytes=4 << 20, timer=None,
+                 comm_dtype=None):
         """layer_offsets: ascending start offsets (elements) of each trunk layer's params in
         ``flat_grad``; the tail after the last offset (head params) joins the last bucket.
-        ``timer`` (utils.metrics.CommTimer) brackets the exposed wait in ``finish``."""
+        ``timer`` (utils.metrics.CommTimer) brackets the exposed wait in ``finish``.
+        ``comm_dtype`` (default: env RAG_GRAD_ALLREDUCE_DTYPE, fp32): ``"bf16"`` sends each bucket
+        as bf16 (half the xGMI bytes; the sum is rounded to bf16 — every rank receives the same
+        values, so replicas stay identical) and widens it back into the fp32 buffer."""
         self.ctx = ctx
         self.flat = flat_grad
         self.timer = timer
+        comm_dtype = comm_dtype or os.environ.get("RAG_GRAD_ALLREDUCE_DTYPE", "fp32")
+        if comm_dtype not in ("fp32", "bf16"):
+            raise ValueError("gradient all-reduce dtype must be fp32 or bf16, got %r"
+                             % comm_dtype)
+        self.comm = torch.empty(flat_grad.numel(), dtype=torch.bfloat16,
+                                device=flat_grad.device) if comm_dtype == "bf16" else None
         self.handles = []
         n = flat_grad.numel()
         # build buckets from the end: [start, end)
@@ -151,8 +161,15 @@ class BucketedAllReduce(object):
         bi = self.trigger.get(layer)
         if bi is None or bi in self._launched or not self.ctx.enabled:
             return
+        self._launch(bi)
+
+    def _launch(self, bi):
         s, e = self.bounds[bi]
-        self.handles.append(dist.all_reduce(self.flat[s:e], async_op=True))
+        buf = self.flat[s:e]
+        if self.comm is not None:
+            buf = self.comm[s:e]
+            buf.copy_(self.flat[s:e])
+        self.handles.append(dist.all_reduce(buf, async_op=True))
         self._launched.add(bi)
 
     def finish(self):
@@ -160,12 +177,14 @@ class BucketedAllReduce(object):
             return
         if self.timer is not None:
             self.timer.start()
-        for bi, (s, e) in enumerate(self.bounds):
+        for bi in range(len(self.bounds)):
             if bi not in self._launched:
-                self.handles.append(dist.all_reduce(self.flat[s:e], async_op=True))
+                self._launch(bi)
         for h in self.handles:
             h.wait()
         if self.timer is not None:
             self.timer.stop()
+        if self.comm is not None:
+            self.flat.copy_(self.comm)
         self.flat.div_(self.ctx.world)
         self.reset()

@@ -25,9 +25,11 @@ def _over_limit(state, move_limit):
     return move_limit is not None and len(state.history) > move_limit
 
 
-def _device_moves(policy, states, beta, greedy_rows, rng):
+def _device_moves(policy, states, beta, greedy_rows, rng, player=None):
     """Batched move choice on the GPU, or None when the policy is not a HIP model (CPU model,
-    duck-typed test policy, unsupported board size)."""
+    duck-typed test policy, unsupported board size). The feature planes the choice was made on
+    stay on the device as ``player.last_planes`` ([n, F, S, S] uint8; RL self-play learns from
+    them instead of re-extracting the positions on the host)."""
     model = getattr(policy, "model", None)
     if model is None or not hasattr(policy, "forward_device") or \
             getattr(model, "device", None) is None or model.device.type != "cuda":
@@ -45,6 +47,8 @@ def _device_moves(policy, states, beta, greedy_rows, rng):
     n = len(states)
     sens = torch.empty((n, S * S), dtype=torch.uint8, device=model.device)
     x = gf([st.native for st in states], sens_out=sens)
+    if player is not None:
+        player.last_planes = x
     probs = policy.forward_device(x)
     if probs.shape[1] == S * S + 1:  # pass-logit network: pass is always a candidate
         sens = torch.cat([sens, torch.ones((n, 1), dtype=torch.uint8, device=model.device)], 1)
@@ -82,8 +86,9 @@ class GreedyPolicyPlayer(object):
     def get_moves(self, states):
         if len(states) == 0:
             return []
-        dev = _device_moves(self.policy, states, 1.0, [True] * len(states), np.random) \
-            if self.device_select else None
+        self.last_planes = None
+        dev = _device_moves(self.policy, states, 1.0, [True] * len(states), np.random,
+                            self) if self.device_select else None
         if dev is not None:
             return [go.PASS_MOVE if _over_limit(st, self.move_limit) else m
                     for st, m in zip(states, dev)]
@@ -146,7 +151,8 @@ class ProbabilisticPolicyPlayer(object):
             return []
         greedy = [self.greedy_start is not None and len(st.history) >= self.greedy_start
                   for st in states]
-        dev = _device_moves(self.policy, states, self.beta, greedy, self.rng) \
+        self.last_planes = None
+        dev = _device_moves(self.policy, states, self.beta, greedy, self.rng, self) \
             if self.device_select else None
         if dev is not None:
             return [go.PASS_MOVE if _over_limit(st, self.move_limit) else m

@@ -66,7 +66,13 @@ def _play_games(learner, opponent, states, num_games):
         learnable = [k for k, mv in enumerate(moves)
                      if current is learner and mv is not go.PASS_MOVE]
         if learnable:
-            feats = preprocessor.states_to_tensor_u8([sts[k] for k in learnable])
+            planes = getattr(current, "last_planes", None)
+            if planes is not None and planes.shape[0] == len(sts):
+                # the GPU player's own feature planes, gathered on the device (no second,
+                # host-side extraction of the same positions)
+                feats = planes[torch.tensor(learnable, device=planes.device)]
+            else:
+                feats = preprocessor.states_to_tensor_u8([sts[k] for k in learnable])
             for j, k in enumerate(learnable):
                 state_feats[idxs[k]].append(feats[j])
                 state_moves[idxs[k]].append(flatten_idx(moves[k], sts[k].size))
@@ -79,6 +85,13 @@ def _play_games(learner, opponent, states, num_games):
             del unfinished[idx]
         current, other = other, current
     return state_feats, state_moves, learner_color
+
+
+def _stack(rows):
+    """Position rows -> one batch: device rows (the GPU player's planes) stay on the device."""
+    if isinstance(rows[0], torch.Tensor):
+        return torch.stack(rows)
+    return torch.from_numpy(np.stack(rows))
 
 
 def run_n_games(optimizer, learner, opponent, num_games, mock_states=[], mode="per_game",
@@ -103,7 +116,7 @@ def run_n_games(optimizer, learner, opponent, num_games, mock_states=[], mode="p
             if not f:
                 continue
             optimizer.lr = abs(optimizer.lr) * (+1 if w else -1)
-            X = np.stack(f)
+            X = _stack(f)
             Y = np.zeros((len(m), S2), np.float32)
             Y[np.arange(len(m)), m] = 1
             model.train_on_batch(X, Y)
@@ -125,7 +138,7 @@ def _batched_update(model, optimizer, feats, moves, won, S2, dp):
     dev = model.device
     net = model.net
     if X:
-        x = torch.from_numpy(np.stack(X)).to(dev)
+        x = _stack(X).to(dev)
         labels = torch.tensor(lab, dtype=torch.int64, device=dev)
         w = torch.tensor(sw, dtype=torch.float32, device=dev)
         plan = model._plan_for()

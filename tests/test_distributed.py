@@ -64,14 +64,14 @@ def _sl_worker(rank, world, port, outdir, steps, local_b):
     dp.shutdown()
 
 
-def _bucket_worker(rank, world, port, outdir):
+def _bucket_worker(rank, world, port, outdir, comm_dtype="fp32"):
     _setup(rank, world, port)
     from rocalphago_amd.parallel.dp import BucketedAllReduce, DPContext
     dp = DPContext(device="cpu")
     n = 1000
     offsets = [0, 100, 250, 600, 900]
     g = torch.arange(n, dtype=torch.float32) * (rank + 1)
-    br = BucketedAllReduce(dp, g, offsets, bucket_bytes=200 * 4)
+    br = BucketedAllReduce(dp, g, offsets, bucket_bytes=200 * 4, comm_dtype=comm_dtype)
     for layer in reversed(range(len(offsets))):
         br.layer_done(layer)
     br.finish()
@@ -112,12 +112,16 @@ def test_dp_sl_training_matches_single_process(tmp_path):
 
 
 @pytest.mark.timeout(300)
-def test_bucketed_allreduce_mean(tmp_path):
-    _spawn(_bucket_worker, (str(tmp_path),))
+@pytest.mark.parametrize("comm_dtype", ["fp32", "bf16"])
+def test_bucketed_allreduce_mean(tmp_path, comm_dtype):
+    _spawn(_bucket_worker, (str(tmp_path), comm_dtype))
     n = 1000
     want = np.arange(n, dtype=np.float32) * 1.5  # mean of x1 and x2
+    rtol = 1e-6 if comm_dtype == "fp32" else 2 ** -7  # bf16: 8-bit significand
+    got = [np.load(tmp_path / ("bucket%d.npy" % r)) for r in range(2)]
+    assert np.array_equal(got[0], got[1])  # replicas identical either way
     for r in range(2):
-        np.testing.assert_allclose(np.load(tmp_path / ("bucket%d.npy" % r)), want, rtol=1e-6)
+        np.testing.assert_allclose(got[r], want, rtol=rtol)
         np.testing.assert_allclose(np.load(tmp_path / ("bucket_b%d.npy" % r)),
                                    np.full(n, 1.5, np.float32))
 

@@ -100,3 +100,31 @@ def test_resnet_uses_hip_convs(cuda):
     g, c = _pair(ResnetPolicy, ["board", "ones"], filters_per_layer=32, layers=3)
     x = g.preprocessor.state_to_tensor(GameState())
     assert np.abs(g.forward(x) - c.forward(x)).max() < 2e-3
+
+
+def test_rl_selfplay_learns_from_device_planes(cuda):
+    """RL self-play keeps the GPU player's feature planes (no host re-extraction); they equal the
+    host extraction of the same positions, and a batched REINFORCE update runs from them."""
+    import torch
+    from rocalphago_amd.players.ai import ProbabilisticPolicyPlayer
+    from rocalphago_amd.training import reinforcement as rl
+    feats = ["board", "ones", "turns_since", "liberties", "sensibleness"]
+    pol = CNNPolicy(feats, board=9, layers=2, filters_per_layer=16, device=cuda, seed=5)
+    pol.model.compile(loss=rl.log_loss, optimizer=K.SGD(lr=0.01))
+    learner = ProbabilisticPolicyPlayer(pol, move_limit=40, rng=np.random.RandomState(1))
+    opp = ProbabilisticPolicyPlayer(pol, move_limit=40, rng=np.random.RandomState(2))
+    sts = [GameState(size=9) for _ in range(3)]
+    for st, mv in zip(sts, [(2, 2), (4, 4), None]):
+        st.do_move(mv)
+    learner.get_moves(sts)
+    assert learner.last_planes is not None and learner.last_planes.is_cuda
+    host = pol.preprocessor.states_to_tensor_u8(sts)
+    assert np.array_equal(learner.last_planes.cpu().numpy(), host)
+    games = [GameState(size=9) for _ in range(4)]
+    f, m, colors = rl._play_games(learner, opp, games, 4)
+    rows = [r for g in f for r in g]
+    assert rows and all(isinstance(r, torch.Tensor) and r.is_cuda for r in rows)
+    w0 = pol.model.get_weights()[0].copy()
+    rl._batched_update(pol.model, pol.model.optimizer, f, m, [True, False, True, False], 81,
+                       None)
+    assert not np.array_equal(pol.model.get_weights()[0], w0)
