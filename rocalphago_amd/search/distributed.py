@@ -36,7 +36,7 @@ from .apv import ParallelMCTS
 
 _rg = _engine()
 
-CMD_ROUND, CMD_MOVE, CMD_STOP = 0, 1, 2
+CMD_ROUND, CMD_MOVE, CMD_STOP, CMD_FLUSH = 0, 1, 2, 3
 HDR = 8  # header words before the per-rank leaf counts
 
 
@@ -95,21 +95,32 @@ class WaveEvaluator(object):
         self.device = model.model.net.device
         self.gpu = self.device.type == "cuda"
         self._gro = None
+        # the networks run on their own stream: the collectives queued on the default stream
+        # (and the host syncs on their results) must not wait for a wave still being evaluated
+        self.stream = torch.cuda.Stream(self.device) if self.gpu else None
 
     def _boards(self, colors, ages, meta8, S, komi):
         zw, zb, _ = go._zobrist(S)
         return _rg.boards_from_arrays(colors, ages, meta8, S, komi, zw.ravel(), zb.ravel())
 
     def __call__(self, codec, rec, superko, komi, seed):
+        ev, pend = self.submit(codec, rec, superko, komi, seed)
+        pr, v, sens = ev.result()
+        return pr, v, sens, pend
+
+    def submit(self, codec, rec, superko, komi, seed):
+        """Start the wave's evaluation: (handle whose result() is (priors, values, sensible) as
+        numpy, rollout handle or None). On the GPU the networks run asynchronously into pinned
+        host buffers, so the caller can take part in collectives meanwhile."""
         colors, ages, meta8, illegal, lad = codec.unpack(rec)
         boards = self._boards(colors, ages, meta8, codec.S, komi)
         pend = self._rollouts(boards, colors, meta8, codec.S, komi, seed) \
             if self.lmbda > 0 else None
         if self.gpu:
-            pr, v, sens = self._gpu_eval(boards, colors, ages, meta8, illegal, lad, superko)
-        else:
-            pr, v, sens = self.net(boards)
-        return pr, v, sens, pend
+            with torch.cuda.stream(self.stream):
+                return self._gpu_eval(boards, colors, ages, meta8, illegal, lad, superko), pend
+        res = self.net(boards)
+        return _Done(tuple(res[:3]) if len(res) > 2 else (res[0], res[1], None)), pend
 
     def _gpu_eval(self, boards, colors, ages, meta8, illegal, lad, superko):
         ev = self.net
@@ -136,9 +147,17 @@ class WaveEvaluator(object):
             sens = x[:, ev._sens_off].reshape(n, -1) if ev._sens_off is not None else None
             pr = ppol.forward(xp) if ppol is not None else None
             v = pval.forward(xv).reshape(-1) if pval is not None else None
-        return (None if pr is None else pr.float().cpu().numpy(),
-                None if v is None else v.float().cpu().numpy(),
-                None if sens is None else sens.cpu().numpy())
+        host = []
+        for t in (pr, v, sens):
+            if t is None:
+                host.append(None)
+                continue
+            h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+            h.copy_(t, non_blocking=True)
+            host.append(h)
+        done = torch.cuda.Event()
+        done.record()
+        return _Copied(done, host)
 
     def _rollouts(self, boards, colors, meta8, S, komi, seed):
         if self.gpu:
@@ -150,11 +169,27 @@ class WaveEvaluator(object):
             return _Pending(ev, w, colors.shape[0], self.R)
         win = self.rollout.rollouts(boards, seed=seed, limit=self.limit, nthreads=self.nthreads)
         z = np.where(win == go.BLACK, 1.0, np.where(win == go.WHITE, -1.0, 0.0))
+        return _Done(z.astype(np.float32))
 
-        class _Done(object):
-            def result(self_inner):
-                return z.astype(np.float32)
-        return _Done()
+
+class _Done(object):
+    def __init__(self, value):
+        self.value = value
+
+    def result(self):
+        return self.value
+
+
+class _Copied(object):
+    """Device results copied into pinned host tensors; valid once ``event`` completed."""
+
+    def __init__(self, event, host):
+        self.event, self.host = event, host
+
+    def result(self):
+        self.event.synchronize()
+        return tuple(None if h is None else h.float().numpy() if h.dtype != torch.uint8
+                     else h.numpy() for h in self.host)
 
 
 class DistributedMCTS(ParallelMCTS):
@@ -186,79 +221,103 @@ class DistributedMCTS(ParallelMCTS):
             dist.broadcast(t, 0)
         return t
 
-    def _header(self, cmd, counts, extra=0, superko=0, komi=7.5, S=19):
+    def _header(self, cmd, counts, extra=0, superko=0, komi=7.5, S=19, gather=0):
         h = torch.zeros(HDR + self.world, dtype=torch.int64, device=self.device)
         if self.rank == 0:
-            h[:HDR] = torch.tensor([cmd, self._round, extra, superko, int(komi * 2), S, 0, 0])
+            h[:HDR] = torch.tensor([cmd, self._round, extra, superko, int(komi * 2), S,
+                                    int(gather), 0])
             if counts is not None:
                 h[HDR:] = torch.tensor(counts, dtype=torch.int64)
         return self._bcast(h).cpu().numpy()
 
-    def _round_trip(self, codec, recs, counts, superko, komi):
-        """One round on every rank: ship the waves, evaluate this rank's, gather the results.
-        Returns (on rank 0) per rank (priors, values, sens, (round, z) or None)."""
+    def _ship(self, codec, recs, counts, superko, komi):
+        """Phase 1 of a round on every rank: receive the waves, start evaluating this rank's."""
+        B = self.batch
+        rnd = self._round
+        n = int(counts[self.rank])
+        if int(np.sum(counts)) == 0:  # an empty round only carries rollout results back
+            return (rnd, 0, None, codec)
+        if self.world > 1:
+            payload = torch.zeros((self.world, B, codec.L), dtype=torch.uint8,
+                                  device=self.device)
+            if self.rank == 0:
+                for r, rec in enumerate(recs):
+                    if rec is not None and len(rec):
+                        payload[r, :len(rec)] = torch.from_numpy(rec).to(self.device)
+            self._bcast(payload)
+        handle = None
+        if n:
+            mine = payload[self.rank, :n].cpu().numpy() if self.world > 1 else recs[0]
+            seed = (self.seed * 7919 + rnd * 131 + self.rank) & 0x7FFFFFFF
+            handle, pend = self.leaf_eval.submit(codec, mine, superko, komi, seed)
+            if pend is not None:
+                self._pending.append((rnd, pend))
+            self.rank_leaves += n
+        return (rnd, n, handle, codec)
+
+    def _collect(self, shipped):
+        """Phase 2: this rank's results of a shipped round (and the rollout results of the wave
+        it started ``rollout_delay`` rounds earlier) all-gathered to rank 0. Returns (on rank 0)
+        per rank (priors, values, sens, (round, z) or None)."""
+        rnd, n, handle, codec = shipped
         P = codec.P
         B = self.batch
-        payload = torch.zeros((self.world, B, codec.L), dtype=torch.uint8, device=self.device)
-        if self.rank == 0:
-            for r, rec in enumerate(recs):
-                if rec is not None and len(rec):
-                    payload[r, :len(rec)] = torch.from_numpy(rec).to(self.device)
-        self._bcast(payload)
-        n = int(counts[self.rank])
         W = 2 * P + 4
         out = np.zeros((B, W), np.float32)
         meta = np.zeros(4, np.float32)  # [n, z round, z count, 0]
         if n:
-            mine = payload[self.rank, :n].cpu().numpy()
-            seed = (self.seed * 7919 + self._round * 131 + self.rank) & 0x7FFFFFFF
-            pr, v, sens, pend = self.leaf_eval(codec, mine, superko, komi, seed)
+            pr, v, sens = handle.result()
             if pr is not None:
                 out[:n, :P] = pr[:, :P]
             if sens is not None:
                 out[:n, P:2 * P] = sens
             if v is not None:
                 out[:n, 2 * P] = v
-            if pend is not None:
-                self._pending.append((self._round, pend))
-            self.rank_leaves += n
         meta[0] = n
-        if self._pending and (self._pending[0][0] <= self._round - self.delay or
-                              n == 0):
-            rnd, pend = self._pending.popleft()
+        if self._pending and (self._pending[0][0] <= rnd - self.delay or n == 0):
+            zr, pend = self._pending.popleft()
             z = pend.result()
             out[:len(z), 2 * P + 1] = z
-            meta[1], meta[2] = rnd, len(z)
-        flat = torch.from_numpy(np.concatenate([out.reshape(-1), meta])).to(self.device)
+            meta[1], meta[2] = zr, len(z)
+        flat = np.concatenate([out.reshape(-1), meta])
         if self.world > 1:
+            flat = torch.from_numpy(flat).to(self.device)
             gathered = [torch.empty_like(flat) for _ in range(self.world)]
             dist.all_gather(gathered, flat)
+            gathered = [g.cpu().numpy() for g in gathered] if self.rank == 0 else None
         else:
             gathered = [flat]
         if self.rank != 0:
             return None
         res = []
         for g in gathered:
-            g = g.cpu().numpy()
             o, m = g[:-4].reshape(B, W), g[-4:]
             k = int(m[0])
             zr = (int(m[1]), o[:int(m[2]), 2 * P + 1].copy()) if m[2] > 0 else None
             res.append((o[:k, :P], o[:k, 2 * P], o[:k, P:2 * P] > 0.5, zr))
         return res
 
+    def _round_trip(self, codec, recs, counts, superko, komi):
+        """Ship and collect one round (unpipelined)."""
+        return self._collect(self._ship(codec, recs, counts, superko, komi))
+
     # ------------------------------------------------------------------ rank 0: the search
     def search(self, state, n_playout=None):
+        """Two rounds in flight: rank 0 selects and ships round k+1 while every GPU still
+        evaluates round k, then collects and backs up round k (virtual loss keeps the two rounds'
+        leaves apart, as in the single-GPU pipeline)."""
         s = self._sync_root(state)
         codec = LeafCodec(state.size)
         target = s.root_visits + (n_playout or self.n_playout)
         waves = {}  # (round, rank) -> wave id still waiting for its rollout results
+        inflight = None  # (shipped, counts, wids) of the round not collected yet
         stall = 0
         t_sel = t_rt = t_back = 0.0
+        superko = int(s.root_board.enforce_superko)
         while True:
             t0 = time.perf_counter()
             recs, counts, wids = [], [], []
-            superko = int(s.root_board.enforce_superko)
-            room = target - s.root_visits
+            room = target - s.root_visits - (sum(inflight[1]) if inflight else 0)
             for r in range(self.world):
                 want = min(self.batch, max(room, 0))
                 wid, n = s.select(want) if want > 0 else (-1, 0)
@@ -271,36 +330,55 @@ class DistributedMCTS(ParallelMCTS):
                 counts.append(n)
                 wids.append(wid if n > 0 else -1)
             t1 = time.perf_counter()
-            if sum(counts) == 0 and not waves:
+            if sum(counts) == 0 and inflight is None and not waves:
                 stall += 1
                 if stall > 3 or s.root_visits >= target:
                     break
                 continue
             stall = 0
-            self._header(CMD_ROUND, counts, superko=superko, komi=state.komi, S=state.size)
-            res = self._round_trip(codec, recs, counts, superko, state.komi)
+            shipped = None
+            if sum(counts) or not inflight:
+                # a new round (possibly empty: it only brings rollout results back)
+                self._header(CMD_ROUND, counts, superko=superko, komi=state.komi, S=state.size,
+                             gather=inflight is not None)
+                shipped = self._ship(codec, recs, counts, superko, state.komi)
+                self._round += 1
+            else:
+                self._header(CMD_FLUSH, [0] * self.world, gather=1)
+            res = self._collect(inflight[0]) if inflight is not None else None
             t2 = time.perf_counter()
-            for r, (pr, v, sens, zr) in enumerate(res):
-                if counts[r]:
-                    s.backup_value(wids[r], pr if self.evaluator.policy is not None else None,
-                                   v if self.evaluator.value is not None else None,
-                                   sens.astype(np.uint8) if self._has_sens() else None)
-                    if self.lmbda > 0:
-                        waves[(self._round, r)] = wids[r]
-                if zr is not None:
-                    s.backup_rollout(waves.pop((zr[0], r)), zr[1])
-            self.stats["waves"] += sum(1 for c in counts if c)
-            self.stats["sims"] += sum(counts)
-            self._round += 1
+            if res is not None:
+                self._backup(s, res, inflight, waves)
+            inflight = (shipped, counts, wids) if shipped is not None else None
             t_sel += t1 - t0
             t_rt += t2 - t1
             t_back += time.perf_counter() - t2
-            if s.root_visits >= target and not waves:
+            if s.root_visits >= target and not waves and inflight is None:
+                break
+            if s.root_visits >= target and not waves and inflight is not None and \
+                    sum(inflight[1]) == 0:
+                self._header(CMD_FLUSH, [0] * self.world, gather=1)
+                self._backup(s, self._collect(inflight[0]), inflight, waves)
                 break
         self._acc("t_select", t_sel)
         self._acc("t_eval", t_rt)
         self._acc("t_backup", t_back)
         return s
+
+    def _backup(self, s, res, inflight, waves):
+        shipped, counts, wids = inflight
+        rnd = shipped[0]
+        for r, (pr, v, sens, zr) in enumerate(res):
+            if counts[r]:
+                s.backup_value(wids[r], pr if self.evaluator.policy is not None else None,
+                               v if self.evaluator.value is not None else None,
+                               sens.astype(np.uint8) if self._has_sens() else None)
+                if self.lmbda > 0:
+                    waves[(rnd, r)] = wids[r]
+            if zr is not None:
+                s.backup_rollout(waves.pop((zr[0], r)), zr[1])
+        self.stats["waves"] += sum(1 for c in counts if c)
+        self.stats["sims"] += sum(counts)
 
     def _has_sens(self):
         self.evaluator._plans()
@@ -327,6 +405,7 @@ class DistributedMCTS(ParallelMCTS):
     # ------------------------------------------------------------------ ranks > 0
     def serve(self):
         """Evaluate rounds until rank 0 decides a move (returned) or stops (None)."""
+        inflight = None
         while True:
             h = self._header(None, None)
             cmd, self._round = int(h[0]), int(h[1])
@@ -336,8 +415,14 @@ class DistributedMCTS(ParallelMCTS):
                 return PASS_MOVE if a < 0 else divmod(a, S)
             if cmd == CMD_STOP:
                 return None
-            codec = LeafCodec(int(h[5]))
-            self._round_trip(codec, None, h[HDR:], int(h[3]), h[4] / 2.0)
+            if cmd == CMD_FLUSH:
+                self._collect(inflight)
+                inflight = None
+                continue
+            shipped = self._ship(LeafCodec(int(h[5])), None, h[HDR:], int(h[3]), h[4] / 2.0)
+            if int(h[6]):
+                self._collect(inflight)
+            inflight = shipped
 
     def stop(self):
         """Rank 0: release the serving ranks (their serve() returns None)."""
