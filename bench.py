@@ -50,7 +50,7 @@ def main():
                          "resnet: ResnetPolicy SL training (batch-statistics BN)")
     ap.add_argument("--no-mcts", action="store_true",
                     help="skip the APV-MCTS sims/s measurement (run after the timed SL steps)")
-    ap.add_argument("--mcts-playouts", type=int, default=4096)
+    ap.add_argument("--mcts-playouts", type=int, default=8192)
     ap.add_argument("--trace", default=None,
                     help="also write a Chrome trace (torch.profiler) of 5 untimed steps here")
     args = ap.parse_args()
@@ -199,7 +199,7 @@ def main():
                 r = r or {"sims_per_s": 0.0, "rollouts_per_s": 0.0}
             else:
                 from benchmarks.mcts_bench import measure
-                r = measure(dev, playouts=args.mcts_playouts)
+                r = measure(dev, playouts=args.mcts_playouts, moves=2)
         except Exception as e:  # the SL metric stands on its own
             err = str(e)[:200]
         tot = torch.tensor([r["sims_per_s"] if r else 0.0,
@@ -213,7 +213,8 @@ def main():
                                     "on GPU, lambda 0.5, %d GPU rollouts/leaf, wave %d, %d " \
                                     "playouts/move, %s" % (
                                         r["rollouts_per_leaf"] if "rollouts_per_leaf" in r
-                                        else 1, 256, args.mcts_playouts * dp.world,
+                                        else 1, r.get("batch", 512),
+                                        args.mcts_playouts * dp.world,
                                         "one search over %d GPUs" % dp.world if dp.world > 1
                                         else "1 GPU")
             if dp.is_root and "leaves_per_rank" in r:

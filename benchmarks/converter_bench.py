@@ -58,11 +58,11 @@ def main():
                 files.append(dst)
         conv = GameConverter(list(DEFAULT_FEATURES))
         out = {"games": len(files), "features": 48}
+        npos = sum(len(conv._python_game(f, 19)[1]) for f in files[:len(src)])
+        # end to end (parse, replay, features, LZF, HDF5) for every path; threads 0 = the
+        # per-game Python replay on the first copy of the games
         t = time.perf_counter()
-        npos = 0
-        for f in files[:len(src)]:
-            st, ac, _ = conv._python_game(f, 19)
-            npos += len(ac)
+        conv.sgfs_to_hdf5(files[:len(src)], os.path.join(d, "py.h5"), nthreads=0, batch=64)
         dt = time.perf_counter() - t
         out["python_games_per_s"] = round(len(src) / dt, 2)
         out["python_positions_per_s"] = round(npos / dt, 1)

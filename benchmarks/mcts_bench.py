@@ -16,8 +16,8 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def build_search(device, filters=192, layers=12, batch=256, rollout_device="gpu",
-                 rollouts_per_leaf=1, lmbda=0.5, nthreads=16, seed=1, pipeline=2,
+def build_search(device, filters=192, layers=12, batch=512, rollout_device="gpu",
+                 rollouts_per_leaf=1, lmbda=0.5, nthreads=16, seed=1, pipeline=3,
                  max_inflight=8, rollout_group=3):
     from rocalphago_amd.features.preprocessing import DEFAULT_FEATURES
     from rocalphago_amd.models.policy import CNNPolicy
@@ -63,7 +63,7 @@ def measure(device, playouts=8192, warmup=512, moves=1, **kw):
 
 
 def measure_distributed(dp, device, playouts=8192, warmup=512, moves=1, filters=192,
-                        layers=12, batch=256, rollouts_per_leaf=1, lmbda=0.5, nthreads=16,
+                        layers=12, batch=512, rollouts_per_leaf=1, lmbda=0.5, nthreads=16,
                         seed=1, rollout_delay=6):
     """ONE search whose leaf waves are evaluated on all ranks (search/distributed.py).
     Collective: every rank calls it; rank 0's dict has the search's sims/s, the others None."""
@@ -116,14 +116,16 @@ def measure_sims_per_s(device, **kw):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--playouts", type=int, default=8192)
-    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--batch", type=int, default=512,
+                    help="leaves per wave (512 with pipeline 3 measured best: "
+                         "profiles/mcts_sweep_r2.txt)")
     ap.add_argument("--rollout-device", default="gpu", choices=["gpu", "cpu"])
     ap.add_argument("--rollouts-per-leaf", type=int, default=1,
                     help="playouts per leaf (1 = AlphaGo's APV-MCTS: one rollout per simulation)")
     ap.add_argument("--lmbda", type=float, default=0.5)
     ap.add_argument("--filters", type=int, default=192)
     ap.add_argument("--threads", type=int, default=16)
-    ap.add_argument("--pipeline", type=int, default=2, help="waves in flight (1 = serial)")
+    ap.add_argument("--pipeline", type=int, default=3, help="waves in flight (1 = serial)")
     ap.add_argument("--max-inflight", type=int, default=8, help="rollout waves in flight")
     ap.add_argument("--rollout-group", type=int, default=3, help="waves per rollout launch")
     ap.add_argument("--moves", type=int, default=1)

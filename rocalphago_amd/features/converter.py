@@ -118,7 +118,10 @@ class GameConverter(object):
 
     # ---- bulk conversion ----------------------------------------------------------------------
     def _batch(self, names, bd_size, nthreads):
-        """Per game of a batch: (states array or list, actions, error or None)."""
+        """Per game of a batch: (states array or list, actions, error or None). ``nthreads``
+        0 converts every game with the Python replay (the reference's path; benchmarks)."""
+        if nthreads == 0:
+            return [self._python_game(name, bd_size) for name in names]
         texts, native_idx = [], []
         for i, name in enumerate(names):
             try:

@@ -474,7 +474,7 @@ def main(argv=None):
     ap.add_argument("--c-puct", type=float, default=5.0)
     ap.add_argument("--mcts-threads", type=int, default=8,
                     help="host threads of the parallel tree descent / leaf featurisation")
-    ap.add_argument("--leaf-batch", type=int, default=256,
+    ap.add_argument("--leaf-batch", type=int, default=512,
                     help="leaves evaluated per GPU batch (one search wave)")
     ap.add_argument("--virtual-loss", type=int, default=3,
                     help="virtual visits added along a pending descent path")

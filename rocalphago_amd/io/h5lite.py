@@ -743,7 +743,8 @@ class WDataset(object):
         comps = _engine().lzf_compress_chunks(block, csize, nthreads) \
             if self.compression == "lzf" else [None] * k
         for i in range(k):
-            self._store_chunk(block[i * csize:(i + 1) * csize].tobytes(), comps[i])
+            # the raw bytes are only written when a chunk did not compress: no copy otherwise
+            self._store_chunk(memoryview(block[i * csize:(i + 1) * csize]), comps[i])
         return k * c
 
     def __setitem__(self, key, value):

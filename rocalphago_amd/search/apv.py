@@ -263,9 +263,9 @@ class ParallelMCTS(object):
     """
 
     def __init__(self, policy=None, value=None, rollout=None, lmbda=0.5, c_puct=5.0,
-                 n_playout=1600, batch=256, virtual_loss=3, rollout_limit=500,
+                 n_playout=1600, batch=512, virtual_loss=3, rollout_limit=500,
                  playout_depth=722, nthreads=8, rollout_device="cpu", rollouts_per_leaf=1,
-                 seed=1, evaluator=None, max_inflight=8, pipeline=2, dp=None,
+                 seed=1, evaluator=None, max_inflight=8, pipeline=3, dp=None,
                  rollout_group=3):
         # dp (parallel/dp.DPContext, world > 1): root parallelism over ranks — every rank
         # searches the same position with its own seed on its own GPU, and get_move() sums the
