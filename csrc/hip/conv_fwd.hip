@@ -288,7 +288,8 @@ bool launch_ks(int nt, int mt, bool pf, dim3 grid, hipStream_t st, const bf16* X
 
 // Pixel-tile height (MT 16-row fragments per wave, BM = 32*MT): the candidate that fills the
 // 512 resident-block slots (2 per CU) best — e.g. K=128 at B=256 (M=92416): MT=4 gives 722
-// blocks (two rounds, the second 41% full), MT=6 gives 482 blocks (one round, 94% full).
+// blocks (two rounds, the second 41% full), MT=6 gives 482 blocks (one round, 94% full); on a
+// tie (within 2 %) the taller tile.
 int pick_mt(int M, int nt, int ntiles_n) {
   const int cands[3] = {4, 6, 8};
   const int ncand = nt == 6 ? 2 : 3;
@@ -299,7 +300,9 @@ int pick_mt(int M, int nt, int ntiles_n) {
     const long nblk = (long)((M + 32 * mt - 1) / (32 * mt)) * ntiles_n;
     const long rounds = (nblk + 511) / 512;
     const double eff = (double)nblk / (double)(rounds * 512);
-    if (eff > best_eff + 0.02) {
+    // the taller tile wins unless it fills the slots >2 % worse (more reuse per staged weight
+    // tile: at B=512 the 5x5 layer took 165 us with MT=4 vs ~2 x 64 us per 256 with MT=6)
+    if (eff > best_eff - 0.02) {
       best_eff = eff;
       best = mt;
     }
