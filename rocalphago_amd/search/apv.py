@@ -191,7 +191,9 @@ class NetworkEvaluator(object):
             side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(side):
                 self._run_nets(xs, ppol, pval)  # buffers sized before capture
-                with torch.cuda.graph(g, stream=side):
+                # thread-local capture: rollout launches of other threads (RAG_ASYNC_EVAL) may
+                # run while this thread captures
+                with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
                     out = self._run_nets(xs, ppol, pval)
             torch.cuda.current_stream().wait_stream(side)
             ent = graphs[key] = (g, out, gens())
