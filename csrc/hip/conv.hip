@@ -769,32 +769,34 @@ RAG_API int rag_pack_weights(const float* W, void* Wf, void* Wb, int COUT, int C
 // bias_out (or 0), first element index; elements of a layer = taps*COUTP*CINP + COUTP.
 namespace {
 constexpr int kPackFields = 11;
-__global__ void pack_trunk_kernel(const int64_t* __restrict__ table, int nlayers, int64_t total) {
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    int l = 0;
-    while (l + 1 < nlayers && table[(l + 1) * kPackFields + 10] <= idx) ++l;
-    const int64_t* t = table + l * kPackFields;
-    const float* W = (const float*)t[0];
-    const float* b = (const float*)t[1];
-    const int COUT = (int)t[2], CIN = (int)t[3], KS = (int)t[4], COUTP = (int)t[5],
-              CINP = (int)t[6];
-    bf16* Wf = (bf16*)t[7];
-    bf16* Wb = (bf16*)t[8];
-    float* bo = (float*)t[9];
-    const int taps = KS * KS;
-    const int64_t local = idx - t[10];
-    const int64_t wtotal = (int64_t)taps * COUTP * CINP;
+// blockIdx.y = layer (its table row read once per block, not searched per element); 32-bit
+// index math (a layer holds < 2^31 elements): the per-element 64-bit divisions and table walk of
+// a flat grid-stride version cost 31 us per SL step
+__global__ void pack_trunk_kernel(const int64_t* __restrict__ table, int nlayers) {
+  const int64_t* t = table + (size_t)blockIdx.y * kPackFields;
+  const float* W = (const float*)t[0];
+  const float* b = (const float*)t[1];
+  const int COUT = (int)t[2], CIN = (int)t[3], KS = (int)t[4], COUTP = (int)t[5],
+            CINP = (int)t[6];
+  bf16* Wf = (bf16*)t[7];
+  bf16* Wb = (bf16*)t[8];
+  float* bo = (float*)t[9];
+  const int taps = KS * KS;
+  const int wtotal = taps * COUTP * CINP;
+  const int total = wtotal + COUTP;
+  for (int local = blockIdx.x * blockDim.x + threadIdx.x; local < total;
+       local += gridDim.x * blockDim.x) {
     if (local < wtotal) {
-      const int c = (int)(local % CINP);
-      const int n = (int)((local / CINP) % COUTP);
-      const int tap = (int)(local / ((int64_t)CINP * COUTP));
+      const int row = local / CINP;
+      const int c = local - row * CINP;
+      const int tap = row / COUTP;
+      const int n = row - tap * COUTP;
       float v = 0.f;
-      if (n < COUT && c < CIN) v = W[((size_t)n * CIN + c) * taps + tap];
+      if (n < COUT && c < CIN) v = W[(n * CIN + c) * taps + tap];
       Wf[local] = (bf16)v;
-      if (Wb) Wb[((size_t)(taps - 1 - tap) * CINP + c) * COUTP + n] = (bf16)v;
+      if (Wb) Wb[((taps - 1 - tap) * CINP + c) * COUTP + n] = (bf16)v;
     } else if (bo) {
-      const int n = (int)(local - wtotal);
+      const int n = local - wtotal;
       bo[n] = (b && n < COUT) ? b[n] : 0.f;
     }
   }
@@ -802,9 +804,11 @@ __global__ void pack_trunk_kernel(const int64_t* __restrict__ table, int nlayers
 }  // namespace
 
 RAG_API int rag_pack_trunk(const int64_t* table, int nlayers, int64_t total, hipStream_t stream) {
-  const int64_t blocks64 = (total + 255) / 256;
-  const int blocks = blocks64 < 8192 ? (int)blocks64 : 8192;
-  pack_trunk_kernel<<<blocks, 256, 0, stream>>>(table, nlayers, total);
+  if (nlayers <= 0) return 0;
+  // blocks per layer: enough for the largest layer in ~4 grid-stride passes
+  const int64_t per = (total / nlayers + 1023) / 1024;
+  const dim3 grid((unsigned)(per < 1 ? 1 : (per > 1024 ? 1024 : per)), (unsigned)nlayers);
+  pack_trunk_kernel<<<grid, 256, 0, stream>>>(table, nlayers);
   return (int)hipGetLastError();
 }
 

@@ -34,8 +34,8 @@ policy_head_fwd_kernel(const bf16* __restrict__ H, const float* __restrict__ w, 
                        const int64_t* __restrict__ labels, const float* __restrict__ sweight,
                        float* __restrict__ loss, float* __restrict__ dz, float* __restrict__ hit,
                        const float* __restrict__ pass_w, const float* __restrict__ pass_b,
-                       float* __restrict__ zout, float* __restrict__ dpass, int S, int KP, int K,
-                       int mode, float gscale) {
+                       float* __restrict__ zout, float* __restrict__ dpass,
+                       float* __restrict__ acc, int S, int KP, int K, int mode, float gscale) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* z = smem;                        // S*S logits (+ the pass logit)
   float* ws = smem + ((S * S + 4) & ~3);  // KP weights
@@ -107,7 +107,9 @@ policy_head_fwd_kernel(const bf16* __restrict__ H, const float* __restrict__ w, 
   if (mode && threadIdx.x == 0 && lab >= 0) {
     float pl = __expf(z[lab] - gmax) * inv;
     pl = fminf(fmaxf(pl, 1e-7f), 1.f - 1e-7f);
-    if (loss) loss[b] = -__logf(pl) * sw * cls;
+    const float lb = -__logf(pl) * sw * cls;
+    if (loss) loss[b] = lb;
+    if (acc) atomicAdd(&acc[0], lb);  // running metric sums (training loops read them lazily)
   }
   // top-1 hit (ties -> lowest index, like argmax)
   if (mode && hit) {
@@ -121,6 +123,7 @@ policy_head_fwd_kernel(const bf16* __restrict__ H, const float* __restrict__ w, 
       int best = 0x7fffffff;
       for (int k = 0; k < (int)(blockDim.x >> 6); ++k) best = min(best, __float_as_int(red[k]));
       hit[b] = (best == lab) ? 1.f : 0.f;
+      if (acc && best == lab) atomicAdd(&acc[1], 1.f);
     }
   }
 }
@@ -329,14 +332,15 @@ __global__ void value_mlp_out_kernel(const float* __restrict__ part, const float
 
 RAG_API int rag_policy_head_fwd(const void* H, const float* w, const float* b0,
                                 const float* pbias, float* probs, const int64_t* labels,
-                                const float* sweight, float* loss, float* dz, float* hit, int B,
-                                int S, int KP, int K, int mode, float gscale,
+                                const float* sweight, float* loss, float* dz, float* hit,
+                                float* acc, int B, int S, int KP, int K, int mode, float gscale,
                                 hipStream_t stream) {
+  // acc (optional, float[2]): += sum of the batch's losses, += number of top-1 hits
   const size_t sm = (size_t)(((S * S + 4) & ~3) + KP) * sizeof(float);
   policy_head_fwd_kernel<<<B, kHeadThreads, sm, stream>>>((const bf16*)H, w, b0, pbias, probs,
                                                           labels, sweight, loss, dz, hit, nullptr,
-                                                          nullptr, nullptr, nullptr, S, KP, K,
-                                                          mode, gscale);
+                                                          nullptr, nullptr, nullptr, acc, S, KP,
+                                                          K, mode, gscale);
   return (int)hipGetLastError();
 }
 
@@ -347,14 +351,14 @@ RAG_API int rag_policy_head_pass_fwd(const void* H, const float* w, const float*
                                      const float* pbias, const float* pass_w,
                                      const float* pass_b, float* probs, const int64_t* labels,
                                      const float* sweight, float* loss, float* dz, float* hit,
-                                     float* zout, float* dpass, int B, int S, int KP, int K,
-                                     int mode, float gscale, hipStream_t stream) {
+                                     float* zout, float* dpass, float* acc, int B, int S, int KP,
+                                     int K, int mode, float gscale, hipStream_t stream) {
   if (!pass_w || !pass_b) return -1;
   const size_t sm = (size_t)(((S * S + 4) & ~3) + KP) * sizeof(float);
   policy_head_fwd_kernel<<<B, kHeadThreads, sm, stream>>>((const bf16*)H, w, b0, pbias, probs,
                                                           labels, sweight, loss, dz, hit, pass_w,
-                                                          pass_b, zout, dpass, S, KP, K, mode,
-                                                          gscale);
+                                                          pass_b, zout, dpass, acc, S, KP, K,
+                                                          mode, gscale);
   return (int)hipGetLastError();
 }
 

@@ -404,8 +404,9 @@ class PolicyHeadEngine(object):
         self._B = B
 
     def forward(self, B, w, b0, pbias, labels=None, sweight=None, mode=0, gscale=1.0,
-                pass_params=None):
-        """pass_params: (W [S*S], b [1]) of a PassLogit layer, or None."""
+                pass_params=None, acc=None):
+        """pass_params: (W [S*S], b [1]) of a PassLogit layer, or None. acc: fp32 [2] running
+        (loss sum, hit count), added to in the kernel."""
         self.ensure(B)
         h = self.trunk.output(B)
         pk = {}
@@ -415,7 +416,7 @@ class PolicyHeadEngine(object):
         ops.policy_head_fwd(h, w, b0, pbias, self.probs[:B], self.K, labels=labels,
                             sweight=sweight, loss=self.loss[:B] if mode else None,
                             dz=self.dz[:B] if mode else None, hit=self.hit[:B] if mode else None,
-                            mode=mode, gscale=gscale, **pk)
+                            mode=mode, gscale=gscale, acc=acc, **pk)
         return self.probs[:B]
 
     def pass_grads(self, B, dW, db):

@@ -169,13 +169,14 @@ class PolicyPlan(_TrunkPlan):
         acc = float(self.head.hit[:B].mean()) if want_acc else None
         return lossv, acc
 
-    def fwd_bwd(self, B, labels, sw, mode, gscale, on_layer_grads=None):
-        """Forward + fused loss + full backward into net.flat_grad (no host syncs)."""
+    def fwd_bwd(self, B, labels, sw, mode, gscale, on_layer_grads=None, metrics=None):
+        """Forward + fused loss + full backward into net.flat_grad (no host syncs). metrics:
+        fp32 [2] device accumulator of (loss sum, top-1 hits), updated in the head kernel."""
         self.trunk.forward(B, training=True)
         w, b0 = self.head_params()
         pb = self.net.params_of(self.bias_name)[0]
         self.head.forward(B, w, b0, pb, labels=labels, sweight=sw, mode=mode, gscale=gscale,
-                          pass_params=self._pass_params())
+                          pass_params=self._pass_params(), acc=metrics)
         if self.pass_name:
             dW, db = self.net.grads_of(self.pass_name)
             self.head.pass_grads(B, dW, db)

@@ -20,8 +20,9 @@ SIGNATURES = {
     "rag_unpack": [P, P, I, I, I, I, I, P],
     "rag_pack_nchw": [P, P, I, I, I, I, I, P],
     # head.hip
-    "rag_policy_head_fwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, P],
-    "rag_policy_head_pass_fwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, P],
+    "rag_policy_head_fwd": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, P],
+    "rag_policy_head_pass_fwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F,
+                                 P],
     "rag_head_bwd": [P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "rag_head_bwd_workspace": [I, I, I],
     "rag_head_linear": [P, P, P, P, I, I, I, I, P],

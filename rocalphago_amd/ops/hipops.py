@@ -197,22 +197,26 @@ def pack_nchw(t, H, CP, out=None):
 
 def policy_head_fwd(h, w, b0, pbias, probs, K, labels=None, sweight=None, loss=None, dz=None,
                     hit=None, mode=0, gscale=1.0, pass_w=None, pass_b=None, zout=None,
-                    dpass=None):
+                    dpass=None, acc=None):
     """Fused 1x1 conv + bias + softmax (+ loss / dL/dz). With ``pass_w``/``pass_b`` (PassLogit)
     probs are [B, S*S + 1] (pass last), ``zout`` gets the position logits and ``dpass`` the
-    pass-logit gradient for the PassLogit weight gradients."""
+    pass-logit gradient for the PassLogit weight gradients. ``acc`` (fp32 [2], optional): the
+    batch's loss sum and top-1 hit count are added to it in the kernel."""
     B, WP, _, KP = h.shape
     S = WP - 2
+    if acc is not None and (acc.dtype != torch.float32 or acc.numel() < 2):
+        raise ValueError("acc must be an fp32 tensor of >= 2 elements")
     if pass_w is not None:
         _check(_lib().rag_policy_head_pass_fwd(
             _ptr(h), _ptr(w), _ptr(b0), _ptr(pbias), _ptr(pass_w), _ptr(pass_b), _ptr(probs),
             _ptr(labels), _ptr(sweight), _ptr(loss), _ptr(dz), _ptr(hit), _ptr(zout),
-            _ptr(dpass), B, S, KP, K, mode, float(gscale), _stream()), "policy_head_pass_fwd")
+            _ptr(dpass), _ptr(acc), B, S, KP, K, mode, float(gscale), _stream()),
+            "policy_head_pass_fwd")
         return
     _check(_lib().rag_policy_head_fwd(_ptr(h), _ptr(w), _ptr(b0), _ptr(pbias), _ptr(probs),
                                       _ptr(labels), _ptr(sweight), _ptr(loss), _ptr(dz),
-                                      _ptr(hit), B, S, KP, K, mode, float(gscale), _stream()),
-           "policy_head_fwd")
+                                      _ptr(hit), _ptr(acc), B, S, KP, K, mode, float(gscale),
+                                      _stream()), "policy_head_fwd")
 
 
 _head_ws = {}

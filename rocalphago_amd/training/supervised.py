@@ -103,6 +103,7 @@ class SupervisedTrainer(object):
         self.sync_bn = dp is not None and dp.enabled and bool(policy_model.net.buffer_views())
         self.loss_sum = torch.zeros((), device=dataset.device)
         self.hit_sum = torch.zeros((), device=dataset.device)
+        self.metric_acc = torch.zeros(2, device=dataset.device)  # fused-plan (loss, hits)
         self.count = 0
 
     def _transforms(self, n):
@@ -119,12 +120,12 @@ class SupervisedTrainer(object):
             B = self.plan.prepare(self.ds.states, index=index, transforms=tf)
             mode = self.plan.loss_mode(self.loss)
             hook = self.bucketer.layer_done if self.bucketer else None
-            self.plan.fwd_bwd(B, labels, None, mode, 1.0 / B, on_layer_grads=hook)
+            # loss / hit sums accumulate in the head kernel (no per-step reduction launches)
+            self.plan.fwd_bwd(B, labels, None, mode, 1.0 / B, on_layer_grads=hook,
+                              metrics=self.metric_acc)
             if self.bucketer:
                 self.bucketer.finish()
             model.optimizer.apply(model.net)
-            self.loss_sum += self.plan.head.loss[:B].sum()
-            self.hit_sum += self.plan.head.hit[:B].sum()
         else:
             X, Y = self.ds.host_batch(index, tf)
             saved = model.grad_allreduce
@@ -143,13 +144,14 @@ class SupervisedTrainer(object):
 
     def pop_metrics(self):
         """(mean loss, accuracy) since the last call, averaged over all ranks."""
-        t = torch.stack([self.loss_sum, self.hit_sum,
+        t = torch.stack([self.loss_sum + self.metric_acc[0], self.hit_sum + self.metric_acc[1],
                          torch.tensor(float(self.count), device=self.loss_sum.device)])
         if self.dp is not None and self.dp.enabled:
             self.dp.allreduce_sum_(t)
         t = t.cpu().numpy()
         self.loss_sum.zero_()
         self.hit_sum.zero_()
+        self.metric_acc.zero_()
         self.count = 0
         return float(t[0] / max(t[2], 1)), float(t[1] / max(t[2], 1))
 
