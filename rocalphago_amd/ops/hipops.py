@@ -278,6 +278,26 @@ def value_mlp_fwd(z, W1, b1, W2, b2, act="linear", out=None, hout=None):
     return out
 
 
+def sl_batch(index, labels, tf_table, sym, seed, step, tf_out=None, lab_out=None):
+    """One launch per SL step (batch.hip): a random allowed dihedral transform per sampled row
+    (int32 [B]) and the transformed target index (int64 [B])."""
+    B = index.numel()
+    dev = index.device
+    for t, dt in ((index, torch.int64), (labels, torch.int64), (tf_table, torch.int64),
+                  (sym, torch.int32)):
+        if t.dtype != dt or not t.is_contiguous():
+            raise ValueError("sl_batch: bad dtype / layout")
+    if tf_out is None:
+        tf_out = torch.empty(B, dtype=torch.int32, device=dev)
+    if lab_out is None:
+        lab_out = torch.empty(B, dtype=torch.int64, device=dev)
+    _check(_lib().rag_sl_batch(_ptr(index), _ptr(labels), _ptr(tf_table), tf_table.shape[1],
+                               _ptr(sym), sym.numel(), ctypes.c_uint(seed & 0xFFFFFFFF),
+                               ctypes.c_uint(step & 0xFFFFFFFF), _ptr(tf_out), _ptr(lab_out), B,
+                               _stream()), "sl_batch")
+    return tf_out, lab_out
+
+
 _mlp_train_ws = {}
 
 

@@ -24,6 +24,7 @@ from ..features.preprocessing import Preprocess
 from ..io import h5lite
 from ..models import kerasish as K
 from ..models.policy import CNNPolicy
+from ..ops import hipops as ops
 from ..parallel.dp import BucketedAllReduce, DPContext
 from ..utils.metrics import RankMetrics
 from .data import BOARD_TRANSFORMATIONS, DeviceDataset, transform_ids
@@ -93,6 +94,7 @@ class SupervisedTrainer(object):
                                 device=dataset.device)
         self.gen = torch.Generator(device=dataset.device)
         self.gen.manual_seed(seed + (dp.rank if dp else 0))
+        self.seed = (seed * 1000003 + (dp.rank if dp else 0)) & 0xFFFFFFFF
         self.plan = policy_model._plan_for() if dataset.device.type == "cuda" else None
         self.bucketer = None
         if self.plan is not None and dp is not None and dp.enabled:
@@ -113,10 +115,13 @@ class SupervisedTrainer(object):
 
     def step(self, index):
         n = index.numel()
-        tf = self._transforms(n)
         model = self.model
         if self.plan is not None:
-            labels = self.ds.batch_labels(index, tf)
+            # one launch for the transforms and transformed labels, seeded by (trainer seed,
+            # optimizer iteration) so a resumed run draws the same transforms
+            tf, labels = ops.sl_batch(index.long().contiguous(), self.ds.labels,
+                                      self.ds.tf_table, self.sym, self.seed,
+                                      getattr(model.optimizer, "iterations", self.count))
             B = self.plan.prepare(self.ds.states, index=index, transforms=tf)
             mode = self.plan.loss_mode(self.loss)
             hook = self.bucketer.layer_done if self.bucketer else None
@@ -127,7 +132,7 @@ class SupervisedTrainer(object):
                 self.bucketer.finish()
             model.optimizer.apply(model.net)
         else:
-            X, Y = self.ds.host_batch(index, tf)
+            X, Y = self.ds.host_batch(index, self._transforms(n))
             saved = model.grad_allreduce
             if self.dp is not None and self.dp.enabled:
                 model.grad_allreduce = self.dp.allreduce_mean_

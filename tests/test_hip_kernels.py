@@ -307,3 +307,23 @@ def test_value_mlp_train(ops, B, P, H, act, weighted):
     for name, got, want in zip(["dz", "dW1", "db1", "dW2", "db2"], [dz] + g, grads):
         assert torch.isfinite(got).all(), name
         assert rel_err(got.reshape(want.shape), want.float()) < 1e-4, name
+
+
+def test_sl_batch_prep(ops):
+    """Fused per-step transform draw + transformed labels (batch.hip) vs torch indexing."""
+    from rocalphago_amd.training.data import label_transform_table, transform_ids
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev)
+    g.manual_seed(3)
+    labels = torch.randint(0, 361, (5000,), generator=g, device=dev)
+    index = torch.randint(0, 5000, (256,), generator=g, device=dev)
+    table = torch.from_numpy(label_transform_table(19)).to(dev)
+    sym = torch.tensor(transform_ids(["noop", "rot90", "fliplr"]), dtype=torch.int32, device=dev)
+    tf, lab = ops.sl_batch(index, labels, table, sym, seed=7, step=11)
+    torch.cuda.synchronize()
+    assert set(tf.cpu().tolist()) <= set(sym.cpu().tolist())
+    assert len(set(tf.cpu().tolist())) == 3  # 256 draws hit every allowed transform
+    assert torch.equal(lab, table[tf.long(), labels[index]])
+    tf2, _ = ops.sl_batch(index, labels, table, sym, seed=7, step=11)
+    tf3, _ = ops.sl_batch(index, labels, table, sym, seed=7, step=12)
+    assert torch.equal(tf, tf2) and not torch.equal(tf, tf3)
