@@ -350,6 +350,7 @@ conv_wgrad_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
 // per float4 quad of the [tap][n][c] slab walks the chunks (4 loads in flight): every chunk read
 // is a coalesced stream. Measured against a variant that splits the chunks over 4 waves of a
 // block (more blocks, 16 loads in flight per quad): that one was 15-20 % slower on MI355X.
+template <int U>
 __global__ void wgrad_reduce_kernel(const float* __restrict__ part, const float* __restrict__ bpart,
                                     float* __restrict__ dW, float* __restrict__ db, int nchunks,
                                     int taps, int COUT, int CIN, int COUTP, int CINP, int KS,
@@ -368,11 +369,15 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ part, const float*
       const size_t st = slab / 4;
       float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
       int k = 0;
-      for (; k + 3 < nchunks; k += 4) {
-        const float4 a = p[k * st], b = p[(k + 1) * st], c = p[(k + 2) * st],
-                     d = p[(k + 3) * st];
-        s0.x += a.x + c.x; s0.y += a.y + c.y; s0.z += a.z + c.z; s0.w += a.w + c.w;
-        s1.x += b.x + d.x; s1.y += b.y + d.y; s1.z += b.z + d.z; s1.w += b.w + d.w;
+      for (; k + U - 1 < nchunks; k += U) {
+        float4 a[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) a[j] = p[(k + j) * st];
+#pragma unroll
+        for (int j = 0; j < U; j += 2) {
+          s0.x += a[j].x; s0.y += a[j].y; s0.z += a[j].z; s0.w += a[j].w;
+          s1.x += a[j + 1].x; s1.y += a[j + 1].y; s1.z += a[j + 1].z; s1.w += a[j + 1].w;
+        }
       }
       for (; k < nchunks; ++k) {
         const float4 a = p[k * st];
@@ -749,8 +754,21 @@ RAG_API int rag_conv_wgrad(const void* G, const void* X, float* dW, float* db, f
     rs = reduce_stream;
   }
   const int total = taps * COUTP * CINP / 4 + COUTP;
-  wgrad_reduce_kernel<<<(total + 255) / 256, 256, 0, rs>>>(part, bpart, dW, db, nchunks, taps,
-                                                          COUT, CIN, COUTP, CINP, KS, accumulate);
+  static int unroll = -1;  // RAG_WRED_UNROLL (4 | 8 | 16): chunk loads in flight per thread
+  if (unroll < 0) {
+    const char* e = getenv("RAG_WRED_UNROLL");
+    unroll = e ? atoi(e) : 4;
+  }
+  const int blocks = (total + 255) / 256;
+  if (unroll >= 16)
+    wgrad_reduce_kernel<16><<<blocks, 256, 0, rs>>>(part, bpart, dW, db, nchunks, taps, COUT, CIN,
+                                                    COUTP, CINP, KS, accumulate);
+  else if (unroll >= 8)
+    wgrad_reduce_kernel<8><<<blocks, 256, 0, rs>>>(part, bpart, dW, db, nchunks, taps, COUT, CIN,
+                                                   COUTP, CINP, KS, accumulate);
+  else
+    wgrad_reduce_kernel<4><<<blocks, 256, 0, rs>>>(part, bpart, dW, db, nchunks, taps, COUT, CIN,
+                                                   COUTP, CINP, KS, accumulate);
   return (int)hipGetLastError();
 }
 
@@ -769,10 +787,11 @@ RAG_API int rag_pack_weights(const float* W, void* Wf, void* Wb, int COUT, int C
 // bias_out (or 0), first element index; elements of a layer = taps*COUTP*CINP + COUTP.
 namespace {
 constexpr int kPackFields = 11;
-// blockIdx.y = layer (its table row read once per block, not searched per element); 32-bit
-// index math (a layer holds < 2^31 elements): the per-element 64-bit divisions and table walk of
-// a flat grid-stride version cost 31 us per SL step
-__global__ void pack_trunk_kernel(const int64_t* __restrict__ table, int nlayers) {
+// Block = one 64 (n) x 64 (c) tile of one tap of one layer (blockIdx.y = layer; blocks past a
+// layer's tile count exit). The tile goes through LDS so that both bf16 layouts are written
+// coalesced: the forward layout [tap][n][c] along c, the dgrad layout [tap'][c][n] along n. The
+// element-per-thread version wrote the dgrad layout 2 bytes per 384-byte stride (29 us/step).
+__global__ void __launch_bounds__(256) pack_trunk_kernel(const int64_t* __restrict__ table) {
   const int64_t* t = table + (size_t)blockIdx.y * kPackFields;
   const float* W = (const float*)t[0];
   const float* b = (const float*)t[1];
@@ -782,33 +801,42 @@ __global__ void pack_trunk_kernel(const int64_t* __restrict__ table, int nlayers
   bf16* Wb = (bf16*)t[8];
   float* bo = (float*)t[9];
   const int taps = KS * KS;
-  const int wtotal = taps * COUTP * CINP;
-  const int total = wtotal + COUTP;
-  for (int local = blockIdx.x * blockDim.x + threadIdx.x; local < total;
-       local += gridDim.x * blockDim.x) {
-    if (local < wtotal) {
-      const int row = local / CINP;
-      const int c = local - row * CINP;
-      const int tap = row / COUTP;
-      const int n = row - tap * COUTP;
-      float v = 0.f;
-      if (n < COUT && c < CIN) v = W[(n * CIN + c) * taps + tap];
-      Wf[local] = (bf16)v;
-      if (Wb) Wb[((taps - 1 - tap) * CINP + c) * COUTP + n] = (bf16)v;
-    } else if (bo) {
-      const int n = local - wtotal;
-      bo[n] = (b && n < COUT) ? b[n] : 0.f;
+  const int ntn = (COUTP + 63) / 64, ntc = (CINP + 63) / 64;
+  int tile = blockIdx.x;
+  if (tile >= taps * ntn * ntc) return;
+  const int ct = tile % ntc;
+  tile /= ntc;
+  const int nt = tile % ntn;
+  const int tap = tile / ntn;
+  __shared__ float tl[64][65];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll 4
+  for (int i = 0; i < 16; ++i) {
+    const int nl = ty + 4 * i;
+    const int n = nt * 64 + nl, c = ct * 64 + tx;
+    const float v = (n < COUT && c < CIN) ? W[(n * CIN + c) * taps + tap] : 0.f;
+    tl[nl][tx] = v;
+    if (n < COUTP && c < CINP) Wf[(tap * COUTP + n) * CINP + c] = (bf16)v;
+  }
+  if (Wb) {
+    __syncthreads();
+#pragma unroll 4
+    for (int i = 0; i < 16; ++i) {
+      const int cl = ty + 4 * i;
+      const int c = ct * 64 + cl, n = nt * 64 + tx;
+      if (c < CINP && n < COUTP) Wb[((taps - 1 - tap) * CINP + c) * COUTP + n] = (bf16)tl[tx][cl];
     }
   }
+  if (bo && blockIdx.x == 0)
+    for (int n = threadIdx.x; n < COUTP; n += blockDim.x) bo[n] = (b && n < COUT) ? b[n] : 0.f;
 }
 }  // namespace
 
 RAG_API int rag_pack_trunk(const int64_t* table, int nlayers, int64_t total, hipStream_t stream) {
-  if (nlayers <= 0) return 0;
-  // blocks per layer: enough for the largest layer in ~4 grid-stride passes
-  const int64_t per = (total / nlayers + 1023) / 1024;
-  const dim3 grid((unsigned)(per < 1 ? 1 : (per > 1024 ? 1024 : per)), (unsigned)nlayers);
-  pack_trunk_kernel<<<grid, 256, 0, stream>>>(table, nlayers);
+  // total: 64x64 tiles (x taps) of the largest layer = grid width
+  if (nlayers <= 0 || total <= 0) return 0;
+  const dim3 grid((unsigned)total, (unsigned)nlayers);
+  pack_trunk_kernel<<<grid, 256, 0, stream>>>(table);
   return (int)hipGetLastError();
 }
 

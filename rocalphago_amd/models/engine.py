@@ -11,7 +11,8 @@ preallocated padded channels-last bf16 activations (layout: csrc/hip/conv.hip), 
 
 Heads: ``PolicyHeadEngine`` (1x1 conv -> per-position Bias -> softmax, with the cross-entropy /
 REINFORCE loss fused into the same kernel) and ``ValueHeadEngine`` (1x1 conv on HIP, then the two
-dense layers as plain library GEMMs — hipBLASLt via torch.matmul — and tanh).
+dense layers + tanh in csrc/hip/head.hip ``value_mlp_*`` for inference and csrc/hip/value_bwd.hip
+for training: forward, MSE tail and all head gradients in two launches, no library GEMMs).
 
 No autograd graph is built on the hot path; ``models/kerasish.py`` exposes these engines through
 torch.autograd.Function wrappers for generic use and calls ``train_step`` directly for speed.
@@ -67,7 +68,9 @@ class _PackedConvs(object):
                              self._wb[l].data_ptr(), self._bias[l].data_ptr(), start])
                 start += s.ks * s.ks * s.coutp * s.cinp + s.coutp
             self._pack_table = torch.tensor(rows, dtype=torch.int64).to(self.device)
-            self._pack_total = start
+            # grid width: 64x64 tiles of the largest layer
+            self._pack_total = max(s.ks * s.ks * (-(-s.coutp // 64)) * (-(-s.cinp // 64))
+                                   for s in self.specs)
             self._pack_key = key
             self._pack_keep = ws  # keep contiguous copies alive while the table points at them
         ops.pack_trunk(self._pack_table, len(self.specs), self._pack_total)

@@ -54,7 +54,7 @@ def pack_weights(w, coutp, cinp, wf=None, wb=None):
 
 def pack_trunk(table, nlayers, total):
     """Repack every layer of a trunk in one launch (table: device int64 [nlayers, 11], see
-    rag_pack_trunk in csrc/hip/conv.hip)."""
+    rag_pack_trunk in csrc/hip/conv.hip; ``total`` = 64x64 tap tiles of the largest layer)."""
     _check(_lib().rag_pack_trunk(_ptr(table), nlayers, int(total), _stream()), "pack_trunk")
 
 
