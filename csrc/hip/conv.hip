@@ -435,15 +435,19 @@ __device__ __forceinline__ void dihedral(int t, int n, int i, int j, int& si, in
 
 // uint8 feature planes [B][F][S][S] (optionally gathered by index and dihedral-transformed)
 // -> padded channels-last bf16 [B][S+2H][S+2H][CP]   (K08 fused with layout conversion)
+// One thread per (pixel, 8-channel group): 8x the threads of a per-pixel loop, so the byte
+// gathers of one pixel's planes are in flight together and a wave's 16-byte stores are contiguous.
 template <typename T>
 __global__ void pack_input_kernel(const T* __restrict__ F, const int64_t* __restrict__ index,
                                   const int* __restrict__ tf, bf16* __restrict__ X, int B, int NF,
                                   int S, int H, int CP) {
   const int S2 = S * S;
-  const int total = B * S2;
+  const int G = CP / 8;
+  const int total = B * S2 * G;
   const int WP = S + 2 * H;
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += gridDim.x * blockDim.x) {
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const int idx = t / G;
+    const int c8 = (t - idx * G) * 8;
     const int b = idx / S2;
     const int rem = idx - b * S2;
     const int i = rem / S, j = rem - (rem / S) * S;
@@ -452,15 +456,13 @@ __global__ void pack_input_kernel(const T* __restrict__ F, const int64_t* __rest
     const int64_t sb = index ? index[b] : b;
     const T* src = F + (size_t)sb * NF * S2 + si * S + sj;
     bf16* dst = X + ((size_t)(b * WP + i + H) * WP + j + H) * CP;
-    for (int c8 = 0; c8 < CP; c8 += 8) {
-      bf16x8 v;
+    bf16x8 v;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int c = c8 + k;
-        v[k] = (bf16)(c < NF ? (float)src[(size_t)c * S2] : 0.f);
-      }
-      *reinterpret_cast<bf16x8*>(dst + c8) = v;
+    for (int k = 0; k < 8; ++k) {
+      const int c = c8 + k;
+      v[k] = (bf16)(c < NF ? (float)src[(size_t)c * S2] : 0.f);
     }
+    *reinterpret_cast<bf16x8*>(dst + c8) = v;
   }
 }
 
@@ -472,10 +474,12 @@ __global__ void pack_input_bits_kernel(const uint64_t* __restrict__ Fb,
                                        const int* __restrict__ tf, bf16* __restrict__ X, int B,
                                        int NF, int S, int H, int CP) {
   const int S2 = S * S;
-  const int total = B * S2;
+  const int G = CP / 8;
+  const int total = B * S2 * G;
   const int WP = S + 2 * H;
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += gridDim.x * blockDim.x) {
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const int idx = t / G;
+    const int c8 = (t - idx * G) * 8;
     const int b = idx / S2;
     const int rem = idx - b * S2;
     const int i = rem / S, j = rem - (rem / S) * S;
@@ -484,15 +488,13 @@ __global__ void pack_input_bits_kernel(const uint64_t* __restrict__ Fb,
     const int64_t sb = index ? index[b] : b;
     const uint64_t word = Fb[(size_t)sb * S2 + si * S + sj];
     bf16* dst = X + ((size_t)(b * WP + i + H) * WP + j + H) * CP;
-    for (int c8 = 0; c8 < CP; c8 += 8) {
-      bf16x8 v;
+    bf16x8 v;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int c = c8 + k;
-        v[k] = (bf16)((c < NF && ((word >> c) & 1ull)) ? 1.f : 0.f);
-      }
-      *reinterpret_cast<bf16x8*>(dst + c8) = v;
+    for (int k = 0; k < 8; ++k) {
+      const int c = c8 + k;
+      v[k] = (bf16)((c < NF && ((word >> c) & 1ull)) ? 1.f : 0.f);
     }
+    *reinterpret_cast<bf16x8*>(dst + c8) = v;
   }
 }
 
@@ -618,6 +620,10 @@ bool rag_wgrad_taps_fits(int WP, int KS, int RG);  // wgrad.hip
 int rag_wgrad_taps_target_blocks();  // wgrad.hip
 bool rag_wgrad_slab_ok(int S, int H, int HG, int GC, int COUTP, int CINP, int KS);  // wgrad_slab.hip
 int rag_wgrad_slab_nchunks(int R, int CINP, int* spc);                            // wgrad_slab.hip
+bool rag_wgrad_slab_bf16();                                                        // wgrad_slab.hip
+int rag_launch_wgrad_slab_reduce(const void* part, const float* bpart, float* dW, float* db,
+                                 int nchunks, int CINP, int COUT, int CIN, int accumulate,
+                                 hipStream_t stream);                              // wgrad_slab.hip
 int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpart, int R, int WP,
                           int GC, int CIN, int spc, int CINP, int nchunks, hipStream_t stream);
 
@@ -705,7 +711,9 @@ RAG_API int rag_conv_wgrad(const void* G, const void* X, float* dW, float* db, f
   int nchunks;
   float* part = work;
   float* bpart;
+  bool bf16_part = false;
   if (rag_wgrad_slab_ok(S, HI, HG, GC, COUTP, CINP, KS)) {
+    bf16_part = rag_wgrad_slab_bf16();
     const int WP = S + 2 * HI;
     const int R = B * WP * WP;
     int spc = 1;
@@ -753,6 +761,9 @@ RAG_API int rag_conv_wgrad(const void* G, const void* X, float* dW, float* db, f
     if (hipStreamWaitEvent(reduce_stream, ev, 0) != hipSuccess) return -3;
     rs = reduce_stream;
   }
+  if (bf16_part)
+    return rag_launch_wgrad_slab_reduce(part, bpart, dW, db, nchunks, CINP, COUT, CIN, accumulate,
+                                        rs);
   const int total = taps * COUTP * CINP / 4 + COUTP;
   static int unroll = -1;  // RAG_WRED_UNROLL (4 | 8 | 16): chunk loads in flight per thread
   if (unroll < 0) {
@@ -842,8 +853,8 @@ RAG_API int rag_pack_trunk(const int64_t* table, int nlayers, int64_t total, hip
 
 RAG_API int rag_pack_input_u8(const uint8_t* F, const int64_t* index, const int* tf, void* X,
                               int B, int NF, int S, int H, int CP, hipStream_t stream) {
-  const int total = B * S * S;
-  const int blocks = (total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096;
+  const int total = B * S * S * (CP / 8);
+  const int blocks = (total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192;
   pack_input_kernel<uint8_t><<<blocks, 256, 0, stream>>>(F, index, tf, (bf16*)X, B, NF, S, H, CP);
   return (int)hipGetLastError();
 }
@@ -851,16 +862,16 @@ RAG_API int rag_pack_input_u8(const uint8_t* F, const int64_t* index, const int*
 RAG_API int rag_pack_input_bits(const uint64_t* Fb, const int64_t* index, const int* tf, void* X,
                                 int B, int NF, int S, int H, int CP, hipStream_t stream) {
   if (NF > 64) return -1;
-  const int total = B * S * S;
-  const int blocks = (total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096;
+  const int total = B * S * S * (CP / 8);
+  const int blocks = (total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192;
   pack_input_bits_kernel<<<blocks, 256, 0, stream>>>(Fb, index, tf, (bf16*)X, B, NF, S, H, CP);
   return (int)hipGetLastError();
 }
 
 RAG_API int rag_pack_input_f32(const float* F, const int64_t* index, const int* tf, void* X,
                                int B, int NF, int S, int H, int CP, hipStream_t stream) {
-  const int total = B * S * S;
-  const int blocks = (total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096;
+  const int total = B * S * S * (CP / 8);
+  const int blocks = (total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192;
   pack_input_kernel<float><<<blocks, 256, 0, stream>>>(F, index, tf, (bf16*)X, B, NF, S, H, CP);
   return (int)hipGetLastError();
 }

@@ -21,7 +21,14 @@
 //     chunk's bit 1 with row bit 2 makes any 8 consecutive rows hit 8 distinct windows (rows r and
 //     r+4 share r mod 4 and differ in bit 2).
 // The MFMA k index is permuted (krow) exactly as in wgrad.hip, identically for both operands.
-// fp32 partials go to part[chunk][tap][n][c] and are summed by wgrad_reduce_kernel (conv.hip).
+//
+// Partials: by default each block stores its 9 x 192 x 32 accumulators as bf16 in the MFMA C
+// layout ([chunk][ctile][tap][a][wave][lane][4]: one contiguous 8-byte store per lane and tile,
+// 512 B per wave instruction) and wgrad_slab_reduce_kernel sums the chunks in fp32 and scatters
+// to OIHW. The slab round trip (42 chunks x 1.33 MB in fp32) was ~1/4 of the wgrad time; bf16
+// halves it. Each partial already sums 42 x 64 rows in fp32, so the rounding is one bf16 ulp per
+// partial on a gradient that bf16 autocast training would round to bf16 as a whole.
+// RAG_WGRAD_PART=fp32 keeps the fp32 part[chunk][tap][n][c] slabs + wgrad_reduce_kernel.
 #include "common.h"
 
 using namespace rag;
@@ -58,7 +65,9 @@ __device__ __forceinline__ void wait_young(int young) {
 // in the one __shared__ array: a second __shared__ object made hipcc drain every in-flight
 // global_load_lds (s_waitcnt vmcnt(0)) before the first ds_read of each stage (guide §5,
 // "Projection GEMM" item 4(a); seen in this kernel's .s).
-template <int kNBUF>
+constexpr int kBlkElems = 9 * kN * kC;  // accumulators per block (bf16 partial slab)
+
+template <int kNBUF, bool kBF>
 __global__ void __launch_bounds__(768)
 wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
                   float* __restrict__ part, float* __restrict__ bpart, int R, int WP, int GC,
@@ -175,6 +184,19 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
     }
   }
 
+  if (kBF) {
+    // bf16 partials in the MFMA C layout: [chunk][ctile][tap][a][wave][lane][4]
+    bf16* dst = reinterpret_cast<bf16*>(part) + (size_t)wid * kBlkElems + (w * 64 + lane) * 4;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (bf16)acc[t][a][r];
+        *reinterpret_cast<bf16x4*>(dst + (t * 2 + a) * (kWaves * 256)) = o;
+      }
+  } else {
   // partial slab part[chunk][tap][n][c]; C layout: col = lane&15, row = 4*(lane>>4) + r
 #pragma unroll
   for (int t = 0; t < 9; ++t) {
@@ -187,6 +209,7 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
       for (int r = 0; r < 4; ++r) dst[(size_t)(n + r) * CINP + cc] = acc[t][a][r];
     }
   }
+  }
   if (do_bias) {
     float* bred = reinterpret_cast<float*>(lds);
     __syncthreads();  // every wave is done reading the staging ring
@@ -196,6 +219,90 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
       float v = 0.f;
       for (int k = 0; k < 24; ++k) v += bred[k * 32 + tid];
       bpart[(size_t)chunk * kN + bcol] = v;
+    }
+  }
+}
+
+// Sums the bf16 partial slabs of wgrad_slab_kernel<.., true> over chunks in fp32 and scatters
+// to OIHW dW [COUT][CIN][3][3] (+ the fp32 bias partials). A 256-thread block owns 64 "octs"
+// (8 consecutive partial elements = two lanes' 4-value C fragments); its 4 waves split the chunks
+// (wave s sums chunks s, s+4, ...: a 16-byte load per chunk, U in flight) and combine through
+// LDS. 4x the threads of one-thread-per-oct, so the ~28 MB of partials stream at HBM rate.
+constexpr int kRedSplit = 4;
+template <int U>
+__global__ void __launch_bounds__(256)
+wgrad_slab_reduce_kernel(const bf16* __restrict__ part, const float* __restrict__ bpart,
+                         float* __restrict__ dW, float* __restrict__ db, int nchunks, int ntc,
+                         int COUT, int CIN, int accumulate) {
+  __shared__ float red[kRedSplit - 1][64][9];  // 9: odd stride, conflict-free
+  const size_t slab = (size_t)ntc * kBlkElems;  // elements per chunk
+  const int octs = (int)(slab / 8);
+  const int oblocks = (octs + 63) / 64;
+  const int tid = threadIdx.x;
+  if ((int)blockIdx.x >= oblocks) {  // bias blocks
+    const int n = ((int)blockIdx.x - oblocks) * 256 + tid;
+    if (!db || !bpart || n >= COUT) return;
+    float v = 0.f;
+    for (int k = 0; k < nchunks; ++k) v += bpart[(size_t)k * kN + n];
+    db[n] = accumulate ? db[n] + v : v;
+    return;
+  }
+  const int lo = tid & 63, sp = tid >> 6;
+  int q = blockIdx.x * 64 + lo;
+  const bool live = q < octs;
+  q = live ? q : octs - 1;
+  const uint4* p = reinterpret_cast<const uint4*>(part) + q;
+  const size_t st = slab / 8;
+  float s[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = 0.f;
+  auto add = [&](const uint4& v) {
+    const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s[2 * j] += __uint_as_float(u[j] << 16);
+      s[2 * j + 1] += __uint_as_float(u[j] & 0xffff0000u);
+    }
+  };
+  int k = sp;
+  for (; k + (U - 1) * kRedSplit < nchunks; k += U * kRedSplit) {
+    uint4 a[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) a[j] = p[(size_t)(k + j * kRedSplit) * st];
+#pragma unroll
+    for (int j = 0; j < U; ++j) add(a[j]);
+  }
+  for (; k < nchunks; k += kRedSplit) add(p[(size_t)k * st]);
+  if (sp > 0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[sp - 1][lo][j] = s[j];
+  }
+  __syncthreads();
+  if (sp > 0 || !live) return;
+#pragma unroll
+  for (int r = 0; r < kRedSplit - 1; ++r)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] += red[r][lo][j];
+  const int e = q * 8;
+  const int ctile = e / kBlkElems;
+  const int loc = e - ctile * kBlkElems;
+  const int lane0 = (loc >> 2) & 63;
+  const int wv = (loc >> 8) % kWaves;
+  const int ta = (loc >> 8) / kWaves;
+  const int a = ta & 1, t = ta >> 1;
+  const int nb = ((wv % 6) * 2 + a) * 16;
+  const int cb = ctile * kC + (wv / 6) * 16;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int lane = lane0 + h;
+    const int c = cb + (lane & 15);
+    if (c >= CIN) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = nb + (lane >> 4) * 4 + r;
+      if (n >= COUT) continue;
+      const size_t o = ((size_t)n * CIN + c) * 9 + t;
+      dW[o] = accumulate ? dW[o] + s[h * 4 + r] : s[h * 4 + r];
     }
   }
 }
@@ -227,6 +334,32 @@ int rag_wgrad_slab_nchunks(int R, int CINP, int* spc) {
 }
 
 static int g_wslab_nbuf = -1;  // RAG_WGRAD_NBUF (3..5), read on first use
+static int g_wslab_bf = -1;    // bf16 partial slabs unless RAG_WGRAD_PART=fp32
+
+RAG_API int rag_wgrad_slab_part_bf16(int on) {
+  const int old = g_wslab_bf;
+  g_wslab_bf = on;
+  return old;
+}
+
+bool rag_wgrad_slab_bf16() {
+  if (g_wslab_bf < 0) {
+    const char* e = getenv("RAG_WGRAD_PART");
+    g_wslab_bf = (e && e[0] == 'f') ? 0 : 1;
+  }
+  return g_wslab_bf != 0;
+}
+
+int rag_launch_wgrad_slab_reduce(const void* part, const float* bpart, float* dW, float* db,
+                                 int nchunks, int CINP, int COUT, int CIN, int accumulate,
+                                 hipStream_t stream) {
+  const int ntc = CINP / kC;
+  const int octs = (int)((size_t)ntc * kBlkElems / 8);
+  const int blocks = (octs + 63) / 64 + (kN + 255) / 256;
+  wgrad_slab_reduce_kernel<4><<<blocks, 256, 0, stream>>>(
+      (const bf16*)part, bpart, dW, db, nchunks, ntc, COUT, CIN, accumulate);
+  return (int)hipGetLastError();
+}
 
 RAG_API int rag_wgrad_slab_nbuf(int n) {
   const int old = g_wslab_nbuf;
@@ -241,18 +374,20 @@ int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpar
     g_wslab_nbuf = e ? atoi(e) : 3;
   }
   const dim3 grid(nchunks * (CINP / kC));
+#define RAG_WSLAB(NB, BF)                                                                   \
+  wgrad_slab_kernel<NB, BF><<<grid, 64 * kWaves, 0, stream>>>(G, X, part, bpart, R, WP, GC, \
+                                                              CIN, spc, CINP)
+  const bool bf = rag_wgrad_slab_bf16();
   switch (g_wslab_nbuf) {
     case 4:
-      wgrad_slab_kernel<4><<<grid, 64 * kWaves, 0, stream>>>(G, X, part, bpart, R, WP, GC, CIN,
-                                                             spc, CINP);
+      if (bf) RAG_WSLAB(4, true); else RAG_WSLAB(4, false);
       break;
     case 5:
-      wgrad_slab_kernel<5><<<grid, 64 * kWaves, 0, stream>>>(G, X, part, bpart, R, WP, GC, CIN,
-                                                             spc, CINP);
+      if (bf) RAG_WSLAB(5, true); else RAG_WSLAB(5, false);
       break;
     default:
-      wgrad_slab_kernel<3><<<grid, 64 * kWaves, 0, stream>>>(G, X, part, bpart, R, WP, GC, CIN,
-                                                             spc, CINP);
+      if (bf) RAG_WSLAB(3, true); else RAG_WSLAB(3, false);
   }
+#undef RAG_WSLAB
   return (int)hipGetLastError();
 }

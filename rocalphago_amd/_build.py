@@ -63,8 +63,13 @@ def build_engine(force=False, verbose=False, debug=False, sanitize=None):
     return target
 
 
-def build_hip(force=False, verbose=False):
-    """Compile every csrc/hip/*.hip into one gfx950 shared object (C ABI, loaded via ctypes)."""
+def build_hip(force=False, verbose=False, jobs=None):
+    """Compile every csrc/hip/*.hip into one gfx950 shared object (C ABI, loaded via ctypes).
+
+    Each source compiles to its own object under build/hip/ (in parallel, incremental on the
+    source and header mtimes), then one hipcc link produces the shared object."""
+    from concurrent.futures import ThreadPoolExecutor
+
     srcs = sorted(glob.glob(os.path.join(CSRC, "hip", "*.hip")))
     hdrs = glob.glob(os.path.join(CSRC, "hip", "*.h"))
     if not srcs:
@@ -72,10 +77,23 @@ def build_hip(force=False, verbose=False):
     if not force and not _stale(HIP_SO, srcs + hdrs):
         return HIP_SO
     hipcc = os.path.join(ROCM, "bin", "hipcc")
-    cmd = ([hipcc, "--offload-arch=" + GPU_ARCH, "-O3", "-std=c++17", "-shared", "-fPIC",
-            "-munsafe-fp-atomics", "-Wno-unused-result", "-I" + os.path.join(CSRC, "hip")] +
-           srcs + ["-o", HIP_SO + ".tmp"])
-    _run(cmd, verbose)
+    objdir = os.path.join(ROOT, "build", "hip")
+    os.makedirs(objdir, exist_ok=True)
+    flags = ["--offload-arch=" + GPU_ARCH, "-O3", "-std=c++17", "-fPIC", "-munsafe-fp-atomics",
+             "-Wno-unused-result", "-I" + os.path.join(CSRC, "hip")]
+    objs = [os.path.join(objdir, os.path.basename(s)[:-4] + ".o") for s in srcs]
+
+    def compile_one(so):
+        src, obj = so
+        if force or _stale(obj, [src] + hdrs):
+            _run([hipcc] + flags + ["-c", src, "-o", obj + ".tmp"], verbose)
+            os.replace(obj + ".tmp", obj)
+
+    jobs = jobs or min(len(srcs), max(1, min(os.cpu_count() or 1, 8)))
+    with ThreadPoolExecutor(jobs) as ex:
+        list(ex.map(compile_one, zip(srcs, objs)))
+    _run([hipcc, "--offload-arch=" + GPU_ARCH, "-shared", "-fPIC"] + objs +
+         ["-o", HIP_SO + ".tmp"], verbose)
     os.replace(HIP_SO + ".tmp", HIP_SO)
     return HIP_SO
 

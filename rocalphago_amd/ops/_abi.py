@@ -53,6 +53,7 @@ SIGNATURES = {
     "rag_conv_order": [I],
     "rag_conv_tap_mode": [I],
     "rag_wgrad_slab_nbuf": [I],
+    "rag_wgrad_slab_part_bf16": [I],
 }
 
 RESTYPES = {"rag_conv_wgrad_workspace": SZ, "rag_head_bwd_workspace": SZ,

@@ -327,3 +327,33 @@ def test_sl_batch_prep(ops):
     tf2, _ = ops.sl_batch(index, labels, table, sym, seed=7, step=11)
     tf3, _ = ops.sl_batch(index, labels, table, sym, seed=7, step=12)
     assert torch.equal(tf, tf2) and not torch.equal(tf, tf3)
+
+
+@pytest.mark.gpu
+def test_wgrad_slab_bf16_partials_match_fp32(ops):
+    """wgrad_slab's default bf16 partial slabs (MFMA C layout + wgrad_slab_reduce_kernel) vs the
+    fp32 part[chunk][tap][n][c] path and fp32 PyTorch, with accumulate on and off."""
+    dev = torch.device("cuda")
+    torch.manual_seed(5)
+    B, C, S = 64, 192, 19
+    x = F.relu(torch.randn(B, C, S, S, device=dev))
+    g = torch.randn(B, C, S, S, device=dev)
+    ref = torch.nn.grad.conv2d_weight(bf(x), (C, C, 3, 3), bf(g), padding=1)
+    xp, gp = ops.pack_nchw(x, 1, C), ops.pack_nchw(g, 1, C)
+    lib = ops._lib()
+    out = {}
+    for mode in (1, 0):
+        prev = lib.rag_wgrad_slab_part_bf16(mode)
+        try:
+            dw = torch.full((C, C, 3, 3), 0.5, device=dev)
+            db = torch.full((C,), 0.5, device=dev)
+            ops.conv_wgrad(gp, xp, dw, db, B, S, 1, C, C, C, C, 3, accumulate=True, hg=1)
+            ops.conv_wgrad(gp, xp, dw, db, B, S, 1, C, C, C, C, 3, accumulate=True, hg=1)
+            torch.cuda.synchronize()
+            out[mode] = (dw - 0.5, db - 0.5)
+        finally:
+            lib.rag_wgrad_slab_part_bf16(prev)
+    for mode in (1, 0):
+        assert rel_err(out[mode][0], 2 * ref) < 1e-2
+        assert rel_err(out[mode][1], 2 * bf(g).sum((0, 2, 3))) < 1e-2
+    assert rel_err(out[1][0], out[0][0]) < 5e-3
