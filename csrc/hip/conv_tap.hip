@@ -44,7 +44,8 @@ __device__ __forceinline__ void wait_vm() {
 }
 
 // epilogue (as conv_pipe): lane owns channels n..n+3 of pixel m for every (j, i) tile
-__device__ __forceinline__ void epilogue(const f32x4 (&acc)[kNT][kMT], int mw, int nw, int M,
+template <int NT = kNT>
+__device__ __forceinline__ void epilogue(const f32x4 (&acc)[NT][kMT], int mw, int nw, int M,
                                          int S, int WO, int HO, int YC, int HM,
                                          const float* __restrict__ bias,
                                          const bf16* __restrict__ res, int relu,
@@ -63,7 +64,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[kNT][kMT], int mw, i
     const int WMK = S + 2 * HM;
     const size_t mrow = (size_t)((b * WMK + pi + HM) * WMK + pj + HM) * YC;
 #pragma unroll
-    for (int j = 0; j < kNT; ++j) {
+    for (int j = 0; j < NT; ++j) {
       const int n = nw + j * 16 + fq * 4;
       float v[4];
 #pragma unroll
@@ -393,6 +394,143 @@ conv_tap8_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
            mask, Y, frow, fq);
 }
 
+// ---------------------------------------------------------------------------------------------
+// 8-wave variant of the same 192 x 192 block tile: waves 2 (M) x 4 (N) of 96 x 48, capped at 128
+// VGPRs so two blocks give FOUR waves per SIMD (conv_tap_kernel: two). Each wave reads 6 slab + 3
+// weight fragments for 18 MFMAs per step; the LDS layout, swizzles, staging ring and counted
+// waits are conv_tap_kernel's, with the 20 slab / 12 weight glds of a step split 3+2 / 2+1
+// between waves 0-3 and 4-7 (each wave waits on its own count).
+constexpr int k16NT = 3;
+
+__global__ void __launch_bounds__(512, 4)  // 4 waves per SIMD (EU): <= 128 VGPRs
+conv_tap16_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
+                  const float* __restrict__ bias, bf16* __restrict__ Y,
+                  const bf16* __restrict__ mask, const bf16* __restrict__ res, int M, int S,
+                  int WI, int shift, int WO, int HO, int CIN, int WROWS, int YC, int relu, int HM,
+                  long total_rows) {
+  __shared__ __attribute__((aligned(16))) bf16 lds[kLds];
+  const int lane = lane_id();
+  const int w = wave_id();
+  const bool lo4 = w < 4;
+  const int wm = w & 1, wn = w >> 1;
+  const int nblk_m = (M + kBM - 1) / kBM;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bm = bid % nblk_m, bn = bid / nblk_m;
+  const int m0 = bm * kBM;
+  const int n0 = bn * kBN;
+  const int S2 = S * S;
+  auto prow = [&](int m) {
+    const int b = m / S2;
+    const int rem = m - b * S2;
+    const int i = rem / S;
+    const int j = rem - i * S;
+    return (long)(b * WI + i + shift) * WI + j + shift;
+  };
+  const long base = prow(m0);
+
+  // slab glds i = w + 8k (k = 0, 1, and 2 for waves 0-3): rows 16 i .. 16 i + 15; weight glds
+  // i = w + 8k (k = 0, and 1 for waves 0-3). Source addresses are recomputed at each issue (a few
+  // VALU per glds) instead of held in 64-bit registers, to stay within 128 VGPRs.
+  const int lrow = lane >> 2;
+  const int lcol = lane & 3;
+  const long tap_stride = (long)WROWS * CIN;
+  auto stage_a = [&](int q) {
+    bf16* dst = lds + (q & 1) * kSlab;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      if (k == 2 && !lo4) break;
+      const int r = (w + 8 * k) * 16 + lrow;
+      long g = base + r;
+      g = g < total_rows ? g : total_rows - 1;
+      glds16(X + g * CIN + ((lcol ^ swz4(r)) * 8) + q * kBK, dst + (w + 8 * k) * 16 * kBK);
+    }
+  };
+  auto stage_b = [&](int s) {  // step s = chunk * 9 + tap
+    const int q = s / 9, t = s - q * 9;
+    bf16* dst = lds + 2 * kSlab + (s % 3) * kBTile;
+    const bf16* src = Wt + t * tap_stride + q * kBK;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (k == 1 && !lo4) break;
+      const int r = (w + 8 * k) * 16 + lrow;
+      glds16(src + (long)(n0 + r) * CIN + ((lcol ^ swz4(r)) * 8), dst + (w + 8 * k) * 16 * kBK);
+    }
+  };
+
+  const int frow = lane & 15;
+  const int fq = lane >> 4;
+  int prel[kMT];
+#pragma unroll
+  for (int i = 0; i < kMT; ++i) {
+    int m = m0 + wm * (16 * kMT) + i * 16 + frow;
+    m = m < M ? m : M - 1;
+    prel[i] = (int)(prow(m) - base);
+  }
+  int boffs[k16NT];
+#pragma unroll
+  for (int j = 0; j < k16NT; ++j) {
+    const int row = wn * (16 * k16NT) + j * 16 + frow;
+    boffs[j] = row * kBK + ((fq ^ swz4(row)) * 8);
+  }
+
+  f32x4 acc[k16NT][kMT];
+#pragma unroll
+  for (int j = 0; j < k16NT; ++j)
+#pragma unroll
+    for (int i = 0; i < kMT; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int cchunks = CIN / kBK;
+  const int nsteps = 9 * cchunks;
+  stage_a(0);
+  stage_b(0);
+  stage_b(1);
+
+  for (int q = 0; q < cchunks; ++q) {
+    const bool more = q + 1 < cchunks;
+    const bf16* slab = lds + (q & 1) * kSlab;
+    int ky = 0, kx = 0;
+#pragma unroll 1
+    for (int t = 0; t < 9; ++t) {
+      const int s = q * 9 + t;
+      // as conv_tap_kernel: younger than B(s) are B(s+1) and, at taps 1-2, the next slab
+      const bool last = t == 8 && !more;
+      const bool with_a = more && (t == 1 || t == 2);
+      if (lo4) {
+        if (last) wait_vm<0>(); else if (with_a) wait_vm<5>(); else wait_vm<2>();
+      } else {
+        if (last) wait_vm<0>(); else if (with_a) wait_vm<3>(); else wait_vm<1>();
+      }
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (s + 2 < nsteps) stage_b(s + 2);
+      if (t == 0 && more) stage_a(q + 1);
+      const bf16* bt = lds + 2 * kSlab + (s % 3) * kBTile;
+      const int toff = ky * WI + kx;
+      bf16x8 xa[kMT], wb[k16NT];
+#pragma unroll
+      for (int i = 0; i < kMT; ++i) {
+        const int r = prel[i] + toff;
+        xa[i] = *reinterpret_cast<const bf16x8*>(slab + r * kBK + ((fq ^ swz4(r)) * 8));
+      }
+#pragma unroll
+      for (int j = 0; j < k16NT; ++j) wb[j] = *reinterpret_cast<const bf16x8*>(bt + boffs[j]);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < k16NT; ++j)
+#pragma unroll
+        for (int i = 0; i < kMT; ++i) acc[j][i] = mfma16(wb[j], xa[i], acc[j][i]);
+      __builtin_amdgcn_s_setprio(0);
+      if (++kx == 3) {
+        kx = 0;
+        ++ky;
+      }
+    }
+  }
+
+  epilogue<k16NT>(acc, m0 + wm * (16 * kMT), n0 + wn * (16 * k16NT), M, S, WO, HO, YC, HM, bias,
+                  res, relu, mask, Y, frow, fq);
+}
+
 int g_tap_mode = -1;  // -1: read RAG_CONV_TAP on first use (default on)
 
 // Worst-case slab extent of a bm-pixel run (host check of the kernels' slab-row assumptions).
@@ -421,7 +559,8 @@ RAG_API int rag_conv_tap_mode(int mode) {
 // Returns true if a tap-slab kernel handled the launch: 3x3, 192-multiple output channels,
 // input channels a multiple of 32, and every pixel run's nine-tap slab fits the kernel's slab.
 // Mode (RAG_CONV_TAP / rag_conv_tap_mode): 0 off, 1 = 4-wave 192-pixel kernel (default),
-// 2 / 3 = 8-wave 384-pixel kernel with a 4- / 5-deep weight ring (measured slower: docs/KERNELS.md).
+// 2 / 3 = 8-wave 384-pixel kernel with a 4- / 5-deep weight ring (measured slower: docs/KERNELS.md),
+// 4 = 8-wave 192-pixel kernel, four waves per SIMD (conv_tap16_kernel).
 bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* y,
                          const bf16* mk, const bf16* res, int M, int S, int WI, int shift, int WO,
                          int HO, int CIN, int COUTP, int YC, int KS, int relu, int HM, long total_rows,
@@ -452,6 +591,11 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
   if (cached_rows > kSlabRows) return false;
   const int nblk_m = (M + kBM - 1) / kBM;
   dim3 grid(nblk_m * (COUTP / kBN));
+  if (g_tap_mode == 4) {
+    conv_tap16_kernel<<<grid, 512, 0, stream>>>(x, w, bias, y, mk, res, M, S, WI, shift, WO, HO,
+                                                CIN, COUTP, YC, relu, HM, total_rows);
+    return true;
+  }
   conv_tap_kernel<<<grid, 256, 0, stream>>>(x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN,
                                             COUTP, YC, relu, HM, total_rows);
   return true;
