@@ -51,6 +51,8 @@ def main():
     ap.add_argument("--no-mcts", action="store_true",
                     help="skip the APV-MCTS sims/s measurement (run after the timed SL steps)")
     ap.add_argument("--mcts-playouts", type=int, default=8192)
+    ap.add_argument("--mcts-guard-s", type=int, default=180,
+                    help="N>1: wall-clock limit of the multi-GPU search measurement")
     ap.add_argument("--trace", default=None,
                     help="also write a Chrome trace (torch.profiler) of 5 untimed steps here")
     args = ap.parse_args()
@@ -192,6 +194,22 @@ def main():
         # to all N GPUs (search/distributed.py) — the whole job's sims/s is that search's.
         # Every rank reaches the all-reduce whether or not its measurement worked (no hang).
         r, err = None, None
+        guard = None
+        if dp.world > 1:
+            # The SL number is final here. A multi-GPU search that stalls (it was rehearsed on
+            # gloo only) must not turn the scaling run into a hang: after MCTS_GUARD_S every rank
+            # leaves with status 0 and rank 0 prints the line with an mcts_error instead.
+            import threading
+
+            def _expire():
+                if dp.is_root:
+                    result["mcts_error"] = "multi-GPU search exceeded %ds" % args.mcts_guard_s
+                    print(json.dumps(result), flush=True)
+                sys.stdout.flush()
+                os._exit(0)
+            guard = threading.Timer(args.mcts_guard_s, _expire)
+            guard.daemon = True
+            guard.start()
         try:
             if dp.world > 1:
                 from benchmarks.mcts_bench import measure_distributed
@@ -206,6 +224,8 @@ def main():
                             r.get("rollouts_per_s", 0.0) if r else 0.0,
                             1.0 if r else 0.0], device=dev)
         dp.allreduce_sum_(tot)
+        if guard is not None:
+            guard.cancel()
         if int(tot[2]) == dp.world:
             result["mcts_sims_per_s"] = round(float(tot[0]), 1)
             result["mcts_rollouts_per_s"] = round(float(tot[1]), 1)

@@ -129,10 +129,14 @@ policy_head_fwd_kernel(const bf16* __restrict__ H, const float* __restrict__ w, 
 }
 
 // Backward of the 1x1 K->1 head conv (+ per-position bias), two launches without contended
-// global atomics:
-//  (1) per board: dH[b,p,k] = dz[b,p] * w[k] * (H[b,p,k] > 0)  (fused ReLU derivative of the
-//      last trunk layer) and the board's partial dw: dwpart[b,k] = sum_p dz[b,p] * H[b,p,k]
-//  (2) column sums: dw[k] = sum_b dwpart[b,k], dpbias[p] = sum_b dz[b,p], db0 = sum_p dpbias[p]
+// atomics:
+//  (1) per block of pixels: dH[b,p,k] = dz[b,p] * w[k] * (H[b,p,k] > 0)  (fused ReLU derivative
+//      of the last trunk layer) and the block's partial dw: dwpart[blk,k] = sum_p dz * H[., k].
+//      The PPI pixel lanes of a block combine their dw partials through an LDS array (plain
+//      stores + one column sum; LDS atomics on 192 addresses serialised ~2k adds per block).
+//  (2) column sums with coalesced row reads: dw[k] = sum_blk dwpart[blk,k],
+//      dpbias[p] = sum_b dz[b,p], db0 = sum_p dpbias[p].
+constexpr int kHeadBwdBlocks = 256;  // <= one block per CU: dwpart stays 256 rows
 template <int CH>  // CH = KP / 8 sixteen-byte channel chunks per pixel row
 __global__ void __launch_bounds__(kHeadThreads)
 head_bwd_kernel(const bf16* __restrict__ H, const float* __restrict__ w,
@@ -142,11 +146,8 @@ head_bwd_kernel(const bf16* __restrict__ H, const float* __restrict__ w,
   constexpr int KP = CH * 8;
   constexpr int PPI = kHeadThreads / CH;  // pixels per block iteration
   __shared__ float ws[KP];
-  __shared__ float dwl[KP];
-  for (int k = threadIdx.x; k < KP; k += blockDim.x) {
-    ws[k] = k < K ? w[k] : 0.f;
-    dwl[k] = 0.f;
-  }
+  __shared__ __attribute__((aligned(16))) float dwl[PPI][KP];
+  for (int k = threadIdx.x; k < KP; k += blockDim.x) ws[k] = k < K ? w[k] : 0.f;
   if (blockIdx.x == 0 && threadIdx.x == 0 && db0) *db0 = 0.f;
   __syncthreads();
   const int S2 = S * S, WP = S + 2;
@@ -160,8 +161,8 @@ head_bwd_kernel(const bf16* __restrict__ H, const float* __restrict__ w,
   const int pbeg = blockIdx.x * pix_per_block;
   const int pend = min(npix, pbeg + pix_per_block);
   if (sub < PPI) {
-    // 4 pixels per batch: all loads issued before any use (memory-level parallelism)
-    constexpr int U = 4;
+    // 8 pixels per batch: all loads issued before any use (memory-level parallelism)
+    constexpr int U = 8;
     for (int P0 = pbeg + sub; P0 < pend; P0 += U * PPI) {
       size_t off[U];
       float g[U];
@@ -189,35 +190,67 @@ head_bwd_kernel(const bf16* __restrict__ H, const float* __restrict__ w,
         if (dH && P0 + u * PPI < pend) *reinterpret_cast<bf16x8*>(dH + off[u]) = o;
       }
     }
-#pragma unroll
-    for (int t = 0; t < 8; ++t) atomicAdd(&dwl[ch * 8 + t], dwacc[t]);  // LDS atomics only
+    float4* dst = reinterpret_cast<float4*>(&dwl[sub][ch * 8]);
+    dst[0] = make_float4(dwacc[0], dwacc[1], dwacc[2], dwacc[3]);
+    dst[1] = make_float4(dwacc[4], dwacc[5], dwacc[6], dwacc[7]);
   }
   __syncthreads();
-  for (int k = threadIdx.x; k < KP; k += blockDim.x) dwpart[(size_t)blockIdx.x * KP + k] = dwl[k];
+  for (int k = threadIdx.x; k < KP; k += blockDim.x) {
+    float v = 0.f;
+#pragma unroll
+    for (int r = 0; r < PPI; ++r) v += dwl[r][k];
+    dwpart[(size_t)blockIdx.x * KP + k] = v;
+  }
 }
 
-// blocks [0, K): dw[k] = sum over head_bwd blocks; blocks [K, K+S2): dpbias[p] = sum_b dz[b,p]
-// (and db0 += dpbias[p]). One workgroup per output, block-reduced.
-__global__ void __launch_bounds__(kHeadThreads)
+// Column sums of a row-major [rows][ld] fp32 matrix over 64-column tiles: 1024 threads = 64
+// columns x 16 row lanes (each row segment is one coalesced 256-byte read), 16-way LDS combine.
+// Blocks [0, ceil(K/64)): dw[k] = sum_blk dwpart[blk][k]; the rest: dpbias[p] = sum_b dz[b][p]
+// and db0 += the block's sum of its dpbias columns.
+__global__ void __launch_bounds__(1024)
 head_bwd_reduce_kernel(const float* __restrict__ dwpart, const float* __restrict__ dz,
                        float* __restrict__ dw, float* __restrict__ db0,
                        float* __restrict__ dpbias, int nblk, int B, int S2, int KP, int K) {
-  __shared__ float red[16];
-  const int o = blockIdx.x;
+  __shared__ float red[16][65];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int kt = (K + 63) / 64;
+  const bool isw = (int)blockIdx.x < kt;
+  const int col = (isw ? (int)blockIdx.x : (int)blockIdx.x - kt) * 64 + tx;
+  const int ncol = isw ? K : S2;
+  const int rows = isw ? nblk : B;
+  const int ld = isw ? KP : S2;
+  const float* src = isw ? dwpart : dz;
   float s = 0.f;
-  if (o < K) {
-    for (int r = threadIdx.x; r < nblk; r += blockDim.x) s += dwpart[(size_t)r * KP + o];
-  } else {
-    const int p = o - K;
-    for (int b = threadIdx.x; b < B; b += blockDim.x) s += dz[(size_t)b * S2 + p];
+  if (col < ncol) {
+    constexpr int U = 4;
+    int r = ty;
+    for (; r + 16 * (U - 1) < rows; r += 16 * U) {
+      float a[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) a[u] = src[(size_t)(r + 16 * u) * ld + col];
+#pragma unroll
+      for (int u = 0; u < U; ++u) s += a[u];
+    }
+    for (; r < rows; r += 16) s += src[(size_t)r * ld + col];
   }
-  s = block_reduce(s, red, false);
-  if (threadIdx.x == 0) {
-    if (o < K) {
-      dw[o] = s;
-    } else {
-      if (dpbias) dpbias[o - K] = s;
-      if (db0) atomicAdd(db0, s);
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0) {
+    float v = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v += red[r][tx];
+    if (col < ncol) {
+      if (isw) {
+        dw[col] = v;
+      } else if (dpbias) {
+        dpbias[col] = v;
+      }
+    }
+    if (!isw && db0) {  // one atomic per block: the sum of its dpbias columns
+      v = col < ncol ? v : 0.f;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+      if (tx == 0) atomicAdd(db0, v);
     }
   }
 }
@@ -368,7 +401,7 @@ RAG_API int rag_head_bwd(const void* H, const float* w, const float* dz, void* d
   // work: >= rag_head_bwd_workspace(B, S, KP) floats
   const int npix = B * S * S;
   int nblk = (npix + 47) / 48;
-  if (nblk > 2048) nblk = 2048;
+  if (nblk > kHeadBwdBlocks) nblk = kHeadBwdBlocks;
   const int ppb = (npix + nblk - 1) / nblk;
 #define RAG_HB(C)                                                                             \
   case C:                                                                                     \
@@ -381,15 +414,16 @@ RAG_API int rag_head_bwd(const void* H, const float* w, const float* dz, void* d
     default: return -1;
   }
 #undef RAG_HB
-  head_bwd_reduce_kernel<<<K + S * S, kHeadThreads, 0, stream>>>(work, dz, dw, db0, dpbias, nblk,
-                                                                 B, S * S, KP, K);
+  const int rblocks = (K + 63) / 64 + (S * S + 63) / 64;
+  head_bwd_reduce_kernel<<<rblocks, 1024, 0, stream>>>(work, dz, dw, db0, dpbias, nblk, B, S * S,
+                                                       KP, K);
   return (int)hipGetLastError();
 }
 
 RAG_API size_t rag_head_bwd_workspace(int B, int S, int KP) {
   const int npix = B * S * S;
   int nblk = (npix + 47) / 48;
-  if (nblk > 2048) nblk = 2048;
+  if (nblk > kHeadBwdBlocks) nblk = kHeadBwdBlocks;
   return (size_t)nblk * KP;
 }
 
