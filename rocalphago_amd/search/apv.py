@@ -70,6 +70,10 @@ class NetworkEvaluator(object):
     def __init__(self, policy=None, value=None, nthreads=8):
         self.policy = policy
         self.value = value
+        # policy and value trunks of a wave on two streams (default; RAG_EVAL_STREAMS=1: one):
+        # 95.4k vs 92.8k sims/s, profiles/mcts_eval_streams_r2.txt
+        self.two_streams = os.environ.get("RAG_EVAL_STREAMS", "2") == "2"
+
         self.nthreads = nthreads
         self.pfids = policy.preprocessor.feature_ids if policy is not None else None
         self.vfids = value.preprocessor.feature_ids if value is not None else None
@@ -155,6 +159,21 @@ class NetworkEvaluator(object):
             xp, xv = (x[:, :self.npol].contiguous() if self.shared else x), x
         else:
             xp, xv = xs
+        if ppol is not None and pval is not None and self.two_streams:
+            # the value trunk on its own stream: its blocks fill the partial last block wave of
+            # each policy conv (a B = 512 trunk conv is 964 blocks on 512 slots) and vice versa.
+            # The two plans own separate activations/workspaces, so they may run concurrently.
+            main = torch.cuda.current_stream()
+            side = self.__dict__.get("_vstream")
+            if side is None:
+                side = self._vstream = torch.cuda.Stream(xp.device)
+            side.wait_stream(main)
+            pr = ppol.forward(xp)
+            with torch.cuda.stream(side):
+                v = pval.forward(xv).reshape(-1)
+            main.wait_stream(side)
+            v.record_stream(main)
+            return pr, v
         pr = ppol.forward(xp) if ppol is not None else None
         v = pval.forward(xv).reshape(-1) if pval is not None else None
         return pr, v
@@ -268,7 +287,7 @@ class ParallelMCTS(object):
                  n_playout=1600, batch=512, virtual_loss=3, rollout_limit=500,
                  playout_depth=722, nthreads=8, rollout_device="cpu", rollouts_per_leaf=1,
                  seed=1, evaluator=None, max_inflight=8, pipeline=3, dp=None,
-                 rollout_group=3):
+                 rollout_group=6):
         # dp (parallel/dp.DPContext, world > 1): root parallelism over ranks — every rank
         # searches the same position with its own seed on its own GPU, and get_move() sums the
         # root visit counts over ranks (one all-reduce of S*S+1 counts), so all

@@ -182,3 +182,32 @@ def test_graph_replayed_evaluation_matches_eager(monkeypatch):
     assert not np.array_equal(ref2[0], ref[0][0])
     for g, e in zip(got2, ref2):
         assert np.array_equal(g, e)
+
+
+def test_two_stream_evaluation_matches_one_stream(monkeypatch):
+    """RAG_EVAL_STREAMS=2 runs the value trunk on a second stream; priors / values /
+    sensibleness equal the single-stream pass for repeated waves of two sizes."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from rocalphago_amd.features.preprocessing import DEFAULT_FEATURES
+    from rocalphago_amd.models.policy import CNNPolicy
+    from rocalphago_amd.models.value import CNNValue
+    from rocalphago_amd.search.apv import NetworkEvaluator
+    dev = torch.device("cuda")
+    pol = CNNPolicy(DEFAULT_FEATURES, board=19, filters_per_layer=192, layers=4, device=dev,
+                    seed=3)
+    val = CNNValue(DEFAULT_FEATURES + ["color"], board=19, filters_per_layer=192, layers=4,
+                   device=dev, seed=4)
+    waves = [[s.native for s in _random_positions(n, 19, 11 + n)] for n in (64, 33)]
+    monkeypatch.setenv("RAG_EVAL_GRAPH", "0")
+    monkeypatch.setenv("RAG_EVAL_STREAMS", "1")
+    one = NetworkEvaluator(pol, val)
+    ref = [one.submit(b).result() for b in waves]
+    monkeypatch.setenv("RAG_EVAL_STREAMS", "2")
+    two = NetworkEvaluator(pol, val)
+    assert two.two_streams
+    for rep in range(3):
+        pend = [two.submit(b) for b in waves]  # both waves in flight before reading either
+        for p, r in zip(pend, ref):
+            for g, e in zip(p.result(), r):
+                assert np.array_equal(g, e), rep
