@@ -67,7 +67,18 @@ __device__ __forceinline__ void wait_young(int young) {
 // "Projection GEMM" item 4(a); seen in this kernel's .s).
 constexpr int kBlkElems = 9 * kN * kC;  // accumulators per block (bf16 partial slab)
 
-template <int kNBUF, bool kBF>
+// Wave -> tile map (kMAP): the block's 12 n-frags x 2 c-frags x 9 taps = 216 MFMA tiles, 18 per
+// wave. kMAP 0: 2 n-frags x 1 c-frag x 9 taps per wave (11 transposed fragment reads per k-step);
+// kMAP 1: 6 n-frags x 1 c-frag x 3 taps (one kernel row; 9 reads per k-step, -18 % LDS reads).
+template <int kMAP> struct WMap {
+  static constexpr int NA = kMAP ? 6 : 2;  // n-frags per wave
+  static constexpr int NT = kMAP ? 3 : 9;  // taps per wave
+  __device__ static int nf0(int w) { return kMAP ? (w & 1) * 6 : (w % 6) * 2; }
+  __device__ static int cf(int w) { return kMAP ? (w >> 1) & 1 : w / 6; }
+  __device__ static int tap(int w, int i) { return kMAP ? (w >> 2) * 3 + i : i; }
+};
+
+template <int kNBUF, bool kBF, int kMAP>
 __global__ void __launch_bounds__(768)
 wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
                   float* __restrict__ part, float* __restrict__ bpart, int R, int WP, int GC,
@@ -123,22 +134,27 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
 
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
   const int kr = krow(g, q);
-  const int nf0 = (w % 6) * 2;  // this wave's two 16-channel n fragments
-  const int cf = w / 6;         // and its 16-channel c fragment
-  int goff[2];
+  using M = WMap<kMAP>;
+  constexpr int NA = M::NA, NT = M::NT;
+  const int nf0 = M::nf0(w);  // this wave's NA 16-channel n fragments
+  const int cf = M::cf(w);    // its 16-channel c fragment
+  int goff[NA];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < NA; ++a)
     goff[a] = kr * kN + ((((nf0 + a) * 2 + (p >> 1)) ^ swz_g(kr)) * 8) + 4 * (p & 1);
-  int xoff[9];
+  int xoff[NT];
 #pragma unroll
-  for (int t = 0; t < 9; ++t) {
+  for (int i = 0; i < NT; ++i) {
+    const int t = M::tap(w, i);
     const int xr = kr + (t / 3) * WP + (t % 3);
-    xoff[t] = kGElems + xr * kC + (((cf * 2 + (p >> 1)) ^ swz_x(xr)) * 8) + 4 * (p & 1);
+    xoff[i] = kGElems + xr * kC + (((cf * 2 + (p >> 1)) ^ swz_x(xr)) * 8) + 4 * (p & 1);
   }
 
-  f32x4 acc[9][2];
+  f32x4 acc[NT][NA];
 #pragma unroll
-  for (int t = 0; t < 9; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < NT; ++i)
+#pragma unroll
+    for (int a = 0; a < NA; ++a) acc[i][a] = f32x4{0.f, 0.f, 0.f, 0.f};
   const bool do_bias = bpart != nullptr;
   const int bcol = ctile * 32 + (tid & 31);  // bias columns: this c-tile's 32 of the 192
   const int brow = tid >> 5;                 // rows brow, brow + 24, brow + 48
@@ -162,20 +178,19 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int ro = kk * 32;  // rows; bits 1..2 unchanged, so the swizzles are unchanged
-      bf16x8 fa[2], fb[9];
+      bf16x8 fa[NA], fb[NT];
 #pragma unroll
-      for (int a = 0; a < 2; ++a)
+      for (int a = 0; a < NA; ++a)
         fa[a] = tr_frag(lb + goff[a] + ro * kN, lb + goff[a] + (ro + 16) * kN);
 #pragma unroll
-      for (int t = 0; t < 9; ++t)
-        fb[t] = tr_frag(lb + xoff[t] + ro * kC, lb + xoff[t] + (ro + 16) * kC);
+      for (int i = 0; i < NT; ++i)
+        fb[i] = tr_frag(lb + xoff[i] + ro * kC, lb + xoff[i] + (ro + 16) * kC);
       lds_reads_done();
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        acc[t][0] = mfma16(fa[0], fb[t], acc[t][0]);
-        acc[t][1] = mfma16(fa[1], fb[t], acc[t][1]);
-      }
+      for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int a = 0; a < NA; ++a) acc[i][a] = mfma16(fa[a], fb[i], acc[i][a]);
       __builtin_amdgcn_s_setprio(0);
     }
     if (do_bias && bcol < kN) {
@@ -185,28 +200,28 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
   }
 
   if (kBF) {
-    // bf16 partials in the MFMA C layout: [chunk][ctile][tap][a][wave][lane][4]
+    // bf16 partials in the MFMA C layout: [chunk][ctile][i * NA + a][wave][lane][4]
     bf16* dst = reinterpret_cast<bf16*>(part) + (size_t)wid * kBlkElems + (w * 64 + lane) * 4;
 #pragma unroll
-    for (int t = 0; t < 9; ++t)
+    for (int i = 0; i < NT; ++i)
 #pragma unroll
-      for (int a = 0; a < 2; ++a) {
+      for (int a = 0; a < NA; ++a) {
         bf16x4 o;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = (bf16)acc[t][a][r];
-        *reinterpret_cast<bf16x4*>(dst + (t * 2 + a) * (kWaves * 256)) = o;
+        for (int r = 0; r < 4; ++r) o[r] = (bf16)acc[i][a][r];
+        *reinterpret_cast<bf16x4*>(dst + (i * NA + a) * (kWaves * 256)) = o;
       }
   } else {
   // partial slab part[chunk][tap][n][c]; C layout: col = lane&15, row = 4*(lane>>4) + r
 #pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    float* dst = part + ((size_t)(chunk * 9 + t) * kN) * CINP;
+  for (int i = 0; i < NT; ++i) {
+    float* dst = part + ((size_t)(chunk * 9 + M::tap(w, i)) * kN) * CINP;
 #pragma unroll
-    for (int a = 0; a < 2; ++a) {
+    for (int a = 0; a < NA; ++a) {
       const int n = (nf0 + a) * 16 + g * 4;
       const int cc = c0 + cf * 16 + (lane & 15);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) dst[(size_t)(n + r) * CINP + cc] = acc[t][a][r];
+      for (int r = 0; r < 4; ++r) dst[(size_t)(n + r) * CINP + cc] = acc[i][a][r];
     }
   }
   }
@@ -233,7 +248,7 @@ template <int U>
 __global__ void __launch_bounds__(256)
 wgrad_slab_reduce_kernel(const bf16* __restrict__ part, const float* __restrict__ bpart,
                          float* __restrict__ dW, float* __restrict__ db, int nchunks, int ntc,
-                         int COUT, int CIN, int accumulate) {
+                         int COUT, int CIN, int accumulate, int map) {
   __shared__ float red[kRedSplit - 1][64][9];  // 9: odd stride, conflict-free
   const size_t slab = (size_t)ntc * kBlkElems;  // elements per chunk
   const int octs = (int)(slab / 8);
@@ -288,10 +303,19 @@ wgrad_slab_reduce_kernel(const bf16* __restrict__ part, const float* __restrict_
   const int loc = e - ctile * kBlkElems;
   const int lane0 = (loc >> 2) & 63;
   const int wv = (loc >> 8) % kWaves;
-  const int ta = (loc >> 8) / kWaves;
-  const int a = ta & 1, t = ta >> 1;
-  const int nb = ((wv % 6) * 2 + a) * 16;
-  const int cb = ctile * kC + (wv / 6) * 16;
+  const int slot = (loc >> 8) / kWaves;  // i * NA + a
+  int nb, cb, t;
+  if (map) {
+    const int a = slot % 6, i = slot / 6;
+    t = (wv >> 2) * 3 + i;
+    nb = ((wv & 1) * 6 + a) * 16;
+    cb = ctile * kC + ((wv >> 1) & 1) * 16;
+  } else {
+    const int a = slot & 1;
+    t = slot >> 1;
+    nb = ((wv % 6) * 2 + a) * 16;
+    cb = ctile * kC + (wv / 6) * 16;
+  }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int lane = lane0 + h;
@@ -335,6 +359,21 @@ int rag_wgrad_slab_nchunks(int R, int CINP, int* spc) {
 
 static int g_wslab_nbuf = -1;  // RAG_WGRAD_NBUF (3..5), read on first use
 static int g_wslab_bf = -1;    // bf16 partial slabs unless RAG_WGRAD_PART=fp32
+static int g_wslab_map = -1;   // wave -> tile map (WMap), RAG_WGRAD_MAP
+
+static int wslab_map() {
+  if (g_wslab_map < 0) {
+    const char* e = getenv("RAG_WGRAD_MAP");
+    g_wslab_map = e ? (atoi(e) != 0) : 1;
+  }
+  return g_wslab_map;
+}
+
+RAG_API int rag_wgrad_slab_map(int m) {
+  const int old = g_wslab_map;
+  g_wslab_map = m;
+  return old;
+}
 
 RAG_API int rag_wgrad_slab_part_bf16(int on) {
   const int old = g_wslab_bf;
@@ -357,7 +396,7 @@ int rag_launch_wgrad_slab_reduce(const void* part, const float* bpart, float* dW
   const int octs = (int)((size_t)ntc * kBlkElems / 8);
   const int blocks = (octs + 63) / 64 + (kN + 255) / 256;
   wgrad_slab_reduce_kernel<4><<<blocks, 256, 0, stream>>>(
-      (const bf16*)part, bpart, dW, db, nchunks, ntc, COUT, CIN, accumulate);
+      (const bf16*)part, bpart, dW, db, nchunks, ntc, COUT, CIN, accumulate, wslab_map());
   return (int)hipGetLastError();
 }
 
@@ -374,10 +413,13 @@ int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpar
     g_wslab_nbuf = e ? atoi(e) : 3;
   }
   const dim3 grid(nchunks * (CINP / kC));
-#define RAG_WSLAB(NB, BF)                                                                   \
-  wgrad_slab_kernel<NB, BF><<<grid, 64 * kWaves, 0, stream>>>(G, X, part, bpart, R, WP, GC, \
-                                                              CIN, spc, CINP)
+#define RAG_WSLAB2(NB, BF, MP)                                                                 \
+  wgrad_slab_kernel<NB, BF, MP><<<grid, 64 * kWaves, 0, stream>>>(G, X, part, bpart, R, WP, GC, \
+                                                                  CIN, spc, CINP)
+#define RAG_WSLAB(NB, BF) \
+  if (mp) RAG_WSLAB2(NB, BF, 1); else RAG_WSLAB2(NB, BF, 0)
   const bool bf = rag_wgrad_slab_bf16();
+  const int mp = wslab_map();
   switch (g_wslab_nbuf) {
     case 4:
       if (bf) RAG_WSLAB(4, true); else RAG_WSLAB(4, false);
@@ -389,5 +431,6 @@ int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpar
       if (bf) RAG_WSLAB(3, true); else RAG_WSLAB(3, false);
   }
 #undef RAG_WSLAB
+#undef RAG_WSLAB2
   return (int)hipGetLastError();
 }

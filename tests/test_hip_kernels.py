@@ -330,9 +330,10 @@ def test_sl_batch_prep(ops):
 
 
 @pytest.mark.gpu
-def test_wgrad_slab_bf16_partials_match_fp32(ops):
+@pytest.mark.parametrize("wmap", [0, 1])
+def test_wgrad_slab_bf16_partials_match_fp32(ops, wmap):
     """wgrad_slab's default bf16 partial slabs (MFMA C layout + wgrad_slab_reduce_kernel) vs the
-    fp32 part[chunk][tap][n][c] path and fp32 PyTorch, with accumulate on and off."""
+    fp32 part[chunk][tap][n][c] path and fp32 PyTorch, accumulating, for both wave->tile maps."""
     dev = torch.device("cuda")
     torch.manual_seed(5)
     B, C, S = 64, 192, 19
@@ -342,6 +343,7 @@ def test_wgrad_slab_bf16_partials_match_fp32(ops):
     xp, gp = ops.pack_nchw(x, 1, C), ops.pack_nchw(g, 1, C)
     lib = ops._lib()
     out = {}
+    prev_map = lib.rag_wgrad_slab_map(wmap)
     for mode in (1, 0):
         prev = lib.rag_wgrad_slab_part_bf16(mode)
         try:
@@ -353,6 +355,7 @@ def test_wgrad_slab_bf16_partials_match_fp32(ops):
             out[mode] = (dw - 0.5, db - 0.5)
         finally:
             lib.rag_wgrad_slab_part_bf16(prev)
+    lib.rag_wgrad_slab_map(prev_map)
     for mode in (1, 0):
         assert rel_err(out[mode][0], 2 * ref) < 1e-2
         assert rel_err(out[mode][1], 2 * bf(g).sum((0, 2, 3))) < 1e-2
