@@ -18,6 +18,7 @@
 // The MFMA is issued as C^T = W * X^T so each lane owns 4 consecutive output channels of one
 // pixel: the epilogue (bias, ReLU, ReLU-mask, bf16 pack) stores 8 bytes per lane.
 #include "common.h"
+#include "wgrad_part.h"
 
 using namespace rag;
 
@@ -568,13 +569,31 @@ bool rag_conv_slab_launch(const bf16* x, const bf16* w, const float* bias, bf16*
 bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* y,
                          const bf16* mk, const bf16* res, int M, int S, int WI, int shift, int WO,
                          int HO, int CIN, int COUTP, int YC, int KS, int relu, int HM,
-                         long total_rows, hipStream_t stream);  // conv_tap.hip
+                         long total_rows, hipStream_t stream, const WgradRed* red);  // conv_tap.hip
 
 // Conv forward / dgrad.  X: padded input (halo HI, CIN channels, CIN % 32 == 0).  W: packed
 // bf16 weights [taps][WROWS][CIN].  Y: padded output (halo HO, YC channels, COUTP % 32 == 0,
 // COUTP <= YC).  bias: fp32 [COUTP] or null.  mask: the dgrad ReLU mask (layer input), null or
 // laid out like Y but with its own halo HM.  res: null or a residual added before the activation
 // (ResNet sum-merge), laid out like Y (may alias Y: each element is read then written by one lane).
+// Deferred wgrad reduction (rag_conv_wgrad_deferred): the bf16 partial-slab reduction of one
+// layer waits here and rides along the next conv_tap launch on the same stream as extra blocks
+// (that launch fills 482 of 512 block slots at B = 256, so the reduction runs in otherwise idle
+// slots instead of as a 14 us kernel of its own). One slot: a second deferral, a launch on
+// another stream or rag_wgrad_flush launches the pending reduction as a standalone kernel.
+int rag_launch_wgrad_slab_reduce(const WgradRed& r, hipStream_t stream);  // wgrad_slab.hip
+static WgradRed g_pending;
+static hipStream_t g_pending_stream = nullptr;
+static bool g_has_pending = false;
+
+static int flush_pending(hipStream_t stream) {
+  if (!g_has_pending) return 0;
+  g_has_pending = false;
+  return rag_launch_wgrad_slab_reduce(g_pending, stream ? stream : g_pending_stream);
+}
+
+RAG_API int rag_wgrad_flush(hipStream_t stream) { return flush_pending(stream); }
+
 RAG_API int rag_conv_igemm(const void* X, const void* W, const float* bias, void* Y,
                            const void* mask, const void* resid, int B, int S, int HI, int HO,
                            int CIN, int COUTP, int YC, int KS, int relu, int HM,
@@ -593,12 +612,25 @@ RAG_API int rag_conv_igemm(const void* X, const void* W, const float* bias, void
     const char* e = getenv("RAG_CONV_PIPE");
     return !(e && e[0] == '0');
   }();
+  const WgradRed* red = (g_has_pending && g_pending_stream == stream) ? &g_pending : nullptr;
+  if (g_has_pending && !red) {
+    const int rc = flush_pending(nullptr);
+    if (rc) return rc;
+  }
   if (rag_conv_slab_launch(x, w, bias, y, mk, res, B, S, HI, WO, HO, CIN, COUTP, YC, KS, relu,
-                           HM, stream))
-    return (int)hipGetLastError();
+                           HM, stream)) {
+    const int rc = red ? flush_pending(stream) : 0;  // opt-in slab conv: reduce on its own
+    return rc ? rc : (int)hipGetLastError();
+  }
   if (use_pipe && rag_conv_tap_launch(x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN,
-                                      COUTP, YC, KS, relu, HM, (long)B * WI * WI, stream))
+                                      COUTP, YC, KS, relu, HM, (long)B * WI * WI, stream, red)) {
+    if (red) g_has_pending = false;
     return (int)hipGetLastError();
+  }
+  if (red) {  // not a tap-slab launch: the reduction goes out on its own first
+    const int rc = flush_pending(stream);
+    if (rc) return rc;
+  }
   if (use_pipe && rag_conv_pipe_launch(x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN,
                                        COUTP, YC, KS, relu, HM, stream))
     return (int)hipGetLastError();
@@ -621,9 +653,9 @@ int rag_wgrad_taps_target_blocks();  // wgrad.hip
 bool rag_wgrad_slab_ok(int S, int H, int HG, int GC, int COUTP, int CINP, int KS);  // wgrad_slab.hip
 int rag_wgrad_slab_nchunks(int R, int CINP, int* spc);                            // wgrad_slab.hip
 bool rag_wgrad_slab_bf16();                                                        // wgrad_slab.hip
-int rag_launch_wgrad_slab_reduce(const void* part, const float* bpart, float* dW, float* db,
-                                 int nchunks, int CINP, int COUT, int CIN, int accumulate,
-                                 hipStream_t stream);                              // wgrad_slab.hip
+WgradRed rag_wgrad_slab_red(const void* part, const float* bpart, float* dW, float* db,
+                            int nchunks, int CINP, int COUT, int CIN, int accumulate);
+int rag_launch_wgrad_slab_reduce(const WgradRed& r, hipStream_t stream);        // wgrad_slab.hip
 int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpart, int R, int WP,
                           int GC, int CIN, int spc, int CINP, int nchunks, hipStream_t stream);
 
@@ -699,10 +731,14 @@ static void launch_wgrad_ks(int ntn, int ntc, dim3 grid, hipStream_t st, const b
 
 // Weight + bias gradient. G: dL/d(pre-activation) in padded layout (halo 1, GC channels).
 // X: the layer input (halo HI, CINP channels). dW: OIHW fp32 [COUT][CIN][KS][KS]. db: [COUT].
-RAG_API int rag_conv_wgrad(const void* G, const void* X, float* dW, float* db, float* work,
+static int conv_wgrad_impl(const void* G, const void* X, float* dW, float* db, float* work,
                            int B, int S, int HI, int HG, int GC, int COUT, int COUTP, int CIN,
                            int CINP, int KS, int accumulate, hipStream_t stream,
-                           hipStream_t reduce_stream) {
+                           hipStream_t reduce_stream, bool defer) {
+  {  // a pending reduction reads the partial slabs this wgrad is about to overwrite
+    const int rc = flush_pending(nullptr);
+    if (rc) return rc;
+  }
   if (COUTP % 32 || CINP % 32) return -1;
   const int taps = KS * KS;
   const bf16* g = (const bf16*)G;
@@ -761,9 +797,17 @@ RAG_API int rag_conv_wgrad(const void* G, const void* X, float* dW, float* db, f
     if (hipStreamWaitEvent(reduce_stream, ev, 0) != hipSuccess) return -3;
     rs = reduce_stream;
   }
-  if (bf16_part)
-    return rag_launch_wgrad_slab_reduce(part, bpart, dW, db, nchunks, CINP, COUT, CIN, accumulate,
-                                        rs);
+  if (bf16_part) {
+    const WgradRed r = rag_wgrad_slab_red(part, bpart, dW, db, nchunks, CINP, COUT, CIN,
+                                          accumulate);
+    if (defer && rs == stream) {
+      g_pending = r;
+      g_pending_stream = stream;
+      g_has_pending = true;
+      return 0;
+    }
+    return rag_launch_wgrad_slab_reduce(r, rs);
+  }
   const int total = taps * COUTP * CINP / 4 + COUTP;
   static int unroll = -1;  // RAG_WRED_UNROLL (4 | 8 | 16): chunk loads in flight per thread
   if (unroll < 0) {
@@ -781,6 +825,24 @@ RAG_API int rag_conv_wgrad(const void* G, const void* X, float* dW, float* db, f
     wgrad_reduce_kernel<4><<<blocks, 256, 0, rs>>>(part, bpart, dW, db, nchunks, taps, COUT, CIN,
                                                    COUTP, CINP, KS, accumulate);
   return (int)hipGetLastError();
+}
+
+RAG_API int rag_conv_wgrad(const void* G, const void* X, float* dW, float* db, float* work,
+                           int B, int S, int HI, int HG, int GC, int COUT, int COUTP, int CIN,
+                           int CINP, int KS, int accumulate, hipStream_t stream,
+                           hipStream_t reduce_stream) {
+  return conv_wgrad_impl(G, X, dW, db, work, B, S, HI, HG, GC, COUT, COUTP, CIN, CINP, KS,
+                         accumulate, stream, reduce_stream, false);
+}
+
+// As rag_conv_wgrad, but a bf16 partial-slab reduction is left pending for the next conv launch
+// on `stream` (see g_pending); dW / db are complete once that launch (or rag_wgrad_flush) ran.
+RAG_API int rag_conv_wgrad_deferred(const void* G, const void* X, float* dW, float* db,
+                                    float* work, int B, int S, int HI, int HG, int GC, int COUT,
+                                    int COUTP, int CIN, int CINP, int KS, int accumulate,
+                                    hipStream_t stream) {
+  return conv_wgrad_impl(G, X, dW, db, work, B, S, HI, HG, GC, COUT, COUTP, CIN, CINP, KS,
+                         accumulate, stream, nullptr, true);
 }
 
 RAG_API int rag_pack_weights(const float* W, void* Wf, void* Wb, int COUT, int CIN, int KS,

@@ -20,6 +20,7 @@
 #include <algorithm>
 
 #include "common.h"
+#include "wgrad_part.h"
 
 using namespace rag;
 
@@ -98,18 +99,25 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NT][kMT], int mw, in
   }
 }
 
+// Blocks [nconv, gridDim.x) are not convolution tiles: they run a deferred wgrad partial-slab
+// reduction (wgrad_part.h) in the block slots the convolution grid leaves free.
+constexpr int kRedU = 14;  // chunk loads in flight per reduce thread
 __global__ void __launch_bounds__(256, 2)
 conv_tap_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                 const float* __restrict__ bias, bf16* __restrict__ Y,
                 const bf16* __restrict__ mask, const bf16* __restrict__ res, int M, int S,
                 int WI, int shift, int WO, int HO, int CIN, int WROWS, int YC, int relu, int HM,
-                long total_rows) {
+                long total_rows, int nconv, WgradRed red) {
   __shared__ __attribute__((aligned(16))) bf16 lds[kLds];
+  if ((int)blockIdx.x >= nconv) {
+    wslab_reduce_blocks<kRedU>(red, (int)blockIdx.x - nconv, (int)gridDim.x - nconv);
+    return;
+  }
   const int lane = lane_id();
   const int w = wave_id();
   const int wm = w & 1, wn = w >> 1;
   const int nblk_m = (M + kBM - 1) / kBM;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bid = xcd_remap(blockIdx.x, nconv);
   const int bm = bid % nblk_m, bn = bid / nblk_m;
   const int m0 = bm * kBM;
   const int n0 = bn * kBN;
@@ -561,10 +569,12 @@ RAG_API int rag_conv_tap_mode(int mode) {
 // Mode (RAG_CONV_TAP / rag_conv_tap_mode): 0 off, 1 = 4-wave 192-pixel kernel (default),
 // 2 / 3 = 8-wave 384-pixel kernel with a 4- / 5-deep weight ring (measured slower: docs/KERNELS.md),
 // 4 = 8-wave 192-pixel kernel, four waves per SIMD (conv_tap16_kernel).
+int rag_launch_wgrad_slab_reduce(const WgradRed& r, hipStream_t stream);  // wgrad_slab.hip
+
 bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* y,
                          const bf16* mk, const bf16* res, int M, int S, int WI, int shift, int WO,
                          int HO, int CIN, int COUTP, int YC, int KS, int relu, int HM, long total_rows,
-                         hipStream_t stream) {
+                         hipStream_t stream, const WgradRed* red) {
   if (g_tap_mode < 0) {
     const char* e = getenv("RAG_CONV_TAP");
     g_tap_mode = e ? atoi(e) : 1;
@@ -578,6 +588,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
     cached_key = key;
   }
   if ((g_tap_mode == 2 || g_tap_mode == 3) && cached_rows8 <= k8SlabRows) {
+    if (red) rag_launch_wgrad_slab_reduce(*red, stream);
     const int nblk_m = (M + k8BM - 1) / k8BM;
     dim3 grid(nblk_m * (COUTP / kBN));
     if (g_tap_mode == 3)
@@ -592,11 +603,21 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
   const int nblk_m = (M + kBM - 1) / kBM;
   dim3 grid(nblk_m * (COUTP / kBN));
   if (g_tap_mode == 4) {
+    if (red) rag_launch_wgrad_slab_reduce(*red, stream);
     conv_tap16_kernel<<<grid, 512, 0, stream>>>(x, w, bias, y, mk, res, M, S, WI, shift, WO, HO,
                                                 CIN, COUTP, YC, relu, HM, total_rows);
     return true;
   }
-  conv_tap_kernel<<<grid, 256, 0, stream>>>(x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN,
-                                            COUTP, YC, relu, HM, total_rows);
+  // reduce blocks: the slots two-blocks-per-CU leave free on 256 CUs (30 at B = 256), at least 8
+  const int nconv = (int)grid.x;
+  int nred = 0;
+  WgradRed r{};
+  if (red) {
+    r = *red;
+    nred = std::min(64, std::max(8, 2 * 256 - nconv));
+  }
+  conv_tap_kernel<<<nconv + nred, 256, 0, stream>>>(x, w, bias, y, mk, res, M, S, WI, shift, WO,
+                                                    HO, CIN, COUTP, YC, relu, HM, total_rows,
+                                                    nconv, r);
   return true;
 }

@@ -1,0 +1,104 @@
+// bf16 partial slabs of wgrad_slab_kernel (wgrad_slab.hip) and their chunk reduction, shared by
+// the standalone reduce kernel and the reduce blocks fused into the next dgrad launch
+// (conv_tap.hip).
+//
+// Layout per chunk: [ctile][slot][wave][lane][4] bf16, slot = i * NA + a (WMap: wave w owns NA
+// n-frags starting at nf0(w), c-frag cf(w) and NT taps tap(w, i)); an "oct" is 8 consecutive
+// elements = the 4-value C fragments of two adjacent lanes.
+#pragma once
+#include "common.h"
+
+namespace rag {
+
+constexpr int kWsN = 192;                   // output channels (all of them per block)
+constexpr int kWsC = 32;                    // input channels per block (c-tile)
+constexpr int kWsWaves = 12;                // waves per wgrad_slab block
+constexpr int kWsBlk = 9 * kWsN * kWsC;     // accumulators per block
+
+// Everything a chunk reduction needs (passed by value into kernels).
+struct WgradRed {
+  const bf16* part;    // [nchunks][ntc * kWsBlk] bf16 partials
+  const float* bpart;  // [nchunks][kWsN] fp32 bias partials (or null)
+  float* dW;           // OIHW [COUT][CIN][3][3]
+  float* db;           // [COUT] (or null)
+  int nchunks, ntc, COUT, CIN, accumulate, map;
+};
+
+__device__ __forceinline__ void wslab_add8(float (&s)[8], const uint4& v) {
+  const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    s[2 * j] += __uint_as_float(u[j] << 16);
+    s[2 * j + 1] += __uint_as_float(u[j] & 0xffff0000u);
+  }
+}
+
+// Scatter the chunk sum of oct q to OIHW dW.
+__device__ __forceinline__ void wslab_store_oct(const WgradRed& r, int q, const float (&s)[8]) {
+  const int e = q * 8;
+  const int ctile = e / kWsBlk;
+  const int loc = e - ctile * kWsBlk;
+  const int lane0 = (loc >> 2) & 63;
+  const int wv = (loc >> 8) % kWsWaves;
+  const int slot = (loc >> 8) / kWsWaves;  // i * NA + a
+  int nb, cb, t;
+  if (r.map) {
+    const int a = slot % 6, i = slot / 6;
+    t = (wv >> 2) * 3 + i;
+    nb = ((wv & 1) * 6 + a) * 16;
+    cb = ctile * kWsC + ((wv >> 1) & 1) * 16;
+  } else {
+    const int a = slot & 1;
+    t = slot >> 1;
+    nb = ((wv % 6) * 2 + a) * 16;
+    cb = ctile * kWsC + (wv / 6) * 16;
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int lane = lane0 + h;
+    const int c = cb + (lane & 15);
+    if (c >= r.CIN) continue;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int n = nb + (lane >> 4) * 4 + k;
+      if (n >= r.COUT) continue;
+      const size_t o = ((size_t)n * r.CIN + c) * 9 + t;
+      r.dW[o] = r.accumulate ? r.dW[o] + s[h * 4 + k] : s[h * 4 + k];
+    }
+  }
+}
+
+// Reduce blocks fused into another kernel: block b of nb handles octs b*T + tid, stepping nb*T,
+// each summed over all chunks with U 16-byte loads in flight; block 0 also sums the bias.
+template <int U>
+__device__ __forceinline__ void wslab_reduce_blocks(const WgradRed& r, int b, int nb) {
+  const int T = blockDim.x, tid = threadIdx.x;
+  const int octs = r.ntc * kWsBlk / 8;
+  const size_t st = (size_t)r.ntc * kWsBlk / 8;  // uint4 stride between chunks
+  const uint4* base = reinterpret_cast<const uint4*>(r.part);
+  for (int q = b * T + tid; q < octs; q += nb * T) {
+    float s[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] = 0.f;
+    const uint4* p = base + q;
+    int k = 0;
+    for (; k + U <= r.nchunks; k += U) {
+      uint4 a[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j) a[j] = p[(size_t)(k + j) * st];
+#pragma unroll
+      for (int j = 0; j < U; ++j) wslab_add8(s, a[j]);
+    }
+    for (; k < r.nchunks; ++k) wslab_add8(s, p[(size_t)k * st]);
+    wslab_store_oct(r, q, s);
+  }
+  if (b == 0 && r.db && r.bpart) {
+    for (int n = tid; n < r.COUT; n += T) {
+      float v = 0.f;
+      for (int k = 0; k < r.nchunks; ++k) v += r.bpart[(size_t)k * kWsN + n];
+      r.db[n] = r.accumulate ? r.db[n] + v : v;
+    }
+  }
+}
+
+}  // namespace rag

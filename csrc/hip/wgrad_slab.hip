@@ -30,6 +30,7 @@
 // partial on a gradient that bf16 autocast training would round to bf16 as a whole.
 // RAG_WGRAD_PART=fp32 keeps the fp32 part[chunk][tap][n][c] slabs + wgrad_reduce_kernel.
 #include "common.h"
+#include "wgrad_part.h"
 
 using namespace rag;
 
@@ -244,91 +245,53 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
 // (wave s sums chunks s, s+4, ...: a 16-byte load per chunk, U in flight) and combine through
 // LDS. 4x the threads of one-thread-per-oct, so the ~28 MB of partials stream at HBM rate.
 constexpr int kRedSplit = 4;
+static_assert(kBlkElems == kWsBlk && kWaves == kWsWaves && kN == kWsN && kC == kWsC,
+              "wgrad_part.h layout constants");
 template <int U>
 __global__ void __launch_bounds__(256)
-wgrad_slab_reduce_kernel(const bf16* __restrict__ part, const float* __restrict__ bpart,
-                         float* __restrict__ dW, float* __restrict__ db, int nchunks, int ntc,
-                         int COUT, int CIN, int accumulate, int map) {
-  __shared__ float red[kRedSplit - 1][64][9];  // 9: odd stride, conflict-free
-  const size_t slab = (size_t)ntc * kBlkElems;  // elements per chunk
+wgrad_slab_reduce_kernel(WgradRed red) {
+  __shared__ float part_sums[kRedSplit - 1][64][9];  // 9: odd stride, conflict-free
+  const size_t slab = (size_t)red.ntc * kBlkElems;  // elements per chunk
   const int octs = (int)(slab / 8);
   const int oblocks = (octs + 63) / 64;
   const int tid = threadIdx.x;
   if ((int)blockIdx.x >= oblocks) {  // bias blocks
     const int n = ((int)blockIdx.x - oblocks) * 256 + tid;
-    if (!db || !bpart || n >= COUT) return;
+    if (!red.db || !red.bpart || n >= red.COUT) return;
     float v = 0.f;
-    for (int k = 0; k < nchunks; ++k) v += bpart[(size_t)k * kN + n];
-    db[n] = accumulate ? db[n] + v : v;
+    for (int k = 0; k < red.nchunks; ++k) v += red.bpart[(size_t)k * kN + n];
+    red.db[n] = red.accumulate ? red.db[n] + v : v;
     return;
   }
   const int lo = tid & 63, sp = tid >> 6;
   int q = blockIdx.x * 64 + lo;
   const bool live = q < octs;
   q = live ? q : octs - 1;
-  const uint4* p = reinterpret_cast<const uint4*>(part) + q;
+  const uint4* p = reinterpret_cast<const uint4*>(red.part) + q;
   const size_t st = slab / 8;
   float s[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) s[j] = 0.f;
-  auto add = [&](const uint4& v) {
-    const uint32_t u[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      s[2 * j] += __uint_as_float(u[j] << 16);
-      s[2 * j + 1] += __uint_as_float(u[j] & 0xffff0000u);
-    }
-  };
   int k = sp;
-  for (; k + (U - 1) * kRedSplit < nchunks; k += U * kRedSplit) {
+  for (; k + (U - 1) * kRedSplit < red.nchunks; k += U * kRedSplit) {
     uint4 a[U];
 #pragma unroll
     for (int j = 0; j < U; ++j) a[j] = p[(size_t)(k + j * kRedSplit) * st];
 #pragma unroll
-    for (int j = 0; j < U; ++j) add(a[j]);
+    for (int j = 0; j < U; ++j) wslab_add8(s, a[j]);
   }
-  for (; k < nchunks; k += kRedSplit) add(p[(size_t)k * st]);
+  for (; k < red.nchunks; k += kRedSplit) wslab_add8(s, p[(size_t)k * st]);
   if (sp > 0) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) red[sp - 1][lo][j] = s[j];
+    for (int j = 0; j < 8; ++j) part_sums[sp - 1][lo][j] = s[j];
   }
   __syncthreads();
   if (sp > 0 || !live) return;
 #pragma unroll
   for (int r = 0; r < kRedSplit - 1; ++r)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s[j] += red[r][lo][j];
-  const int e = q * 8;
-  const int ctile = e / kBlkElems;
-  const int loc = e - ctile * kBlkElems;
-  const int lane0 = (loc >> 2) & 63;
-  const int wv = (loc >> 8) % kWaves;
-  const int slot = (loc >> 8) / kWaves;  // i * NA + a
-  int nb, cb, t;
-  if (map) {
-    const int a = slot % 6, i = slot / 6;
-    t = (wv >> 2) * 3 + i;
-    nb = ((wv & 1) * 6 + a) * 16;
-    cb = ctile * kC + ((wv >> 1) & 1) * 16;
-  } else {
-    const int a = slot & 1;
-    t = slot >> 1;
-    nb = ((wv % 6) * 2 + a) * 16;
-    cb = ctile * kC + (wv / 6) * 16;
-  }
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int lane = lane0 + h;
-    const int c = cb + (lane & 15);
-    if (c >= CIN) continue;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = nb + (lane >> 4) * 4 + r;
-      if (n >= COUT) continue;
-      const size_t o = ((size_t)n * CIN + c) * 9 + t;
-      dW[o] = accumulate ? dW[o] + s[h * 4 + r] : s[h * 4 + r];
-    }
-  }
+    for (int j = 0; j < 8; ++j) s[j] += part_sums[r][lo][j];
+  wslab_store_oct(red, q, s);
 }
 
 }  // namespace
@@ -389,14 +352,26 @@ bool rag_wgrad_slab_bf16() {
   return g_wslab_bf != 0;
 }
 
-int rag_launch_wgrad_slab_reduce(const void* part, const float* bpart, float* dW, float* db,
-                                 int nchunks, int CINP, int COUT, int CIN, int accumulate,
-                                 hipStream_t stream) {
-  const int ntc = CINP / kC;
-  const int octs = (int)((size_t)ntc * kBlkElems / 8);
+WgradRed rag_wgrad_slab_red(const void* part, const float* bpart, float* dW, float* db,
+                            int nchunks, int CINP, int COUT, int CIN, int accumulate) {
+  WgradRed r;
+  r.part = (const bf16*)part;
+  r.bpart = bpart;
+  r.dW = dW;
+  r.db = db;
+  r.nchunks = nchunks;
+  r.ntc = CINP / kC;
+  r.COUT = COUT;
+  r.CIN = CIN;
+  r.accumulate = accumulate;
+  r.map = wslab_map();
+  return r;
+}
+
+int rag_launch_wgrad_slab_reduce(const WgradRed& r, hipStream_t stream) {
+  const int octs = (int)((size_t)r.ntc * kBlkElems / 8);
   const int blocks = (octs + 63) / 64 + (kN + 255) / 256;
-  wgrad_slab_reduce_kernel<4><<<blocks, 256, 0, stream>>>(
-      (const bf16*)part, bpart, dW, db, nchunks, ntc, COUT, CIN, accumulate, wslab_map());
+  wgrad_slab_reduce_kernel<4><<<blocks, 256, 0, stream>>>(r);
   return (int)hipGetLastError();
 }
 

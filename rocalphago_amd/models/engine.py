@@ -92,6 +92,8 @@ class HipTrunk(_PackedConvs):
         self._init_packing(specs, device)
         self._work = None
         self._rstream = None
+        # wgrad slab reductions ride along the next dgrad launch (RAG_WGRAD_DEFER=0: own kernels)
+        self.defer_reduce = os.environ.get("RAG_WGRAD_DEFER", "1") != "0"
 
     # ------------------------------------------------------------------ buffers
     def _halos(self):
@@ -185,19 +187,16 @@ class HipTrunk(_PackedConvs):
             slot = i & 1 if rs is not None else 0
             if rs is not None and self._wevt[slot] is not None:
                 main.wait_event(self._wevt[slot])  # the reduction that last read this slab
+            # without a reduce stream, layer l's slab reduction is deferred into the free block
+            # slots of its own dgrad launch (conv.hip g_pending); dW[l] is final after that
+            defer = rs is None and self.defer_reduce
             ops.conv_wgrad(g, x, dws[l], dbs[l], B, S, self.halo[l], s.cout, s.coutp, s.cin,
                            s.cinp, s.ks, accumulate=accumulate, work=self._work[slot],
-                           hg=self.halo[l], reduce_stream=rs)
+                           hg=self.halo[l], reduce_stream=rs, defer=defer)
             if rs is not None:
                 ev = torch.cuda.Event()
                 ev.record(rs)
                 self._wevt[slot] = ev
-            if on_layer_done is not None:
-                if rs is not None:
-                    with torch.cuda.stream(rs):  # the bucket all-reduce follows the reduction
-                        on_layer_done(l)
-                else:
-                    on_layer_done(l)
             if l > 0:
                 below = self.specs[l - 1]
                 which ^= 1
@@ -205,9 +204,19 @@ class HipTrunk(_PackedConvs):
                 ops.conv_igemm(g, self._wb[l], None, gout, B, S, self.halo[l],
                                self.halo[l - 1], s.coutp, s.cinp, s.ks, False,
                                mask=x if below.relu else None, mask_halo=self.halo[l])
+            elif defer:
+                ops.wgrad_flush()
+            if on_layer_done is not None:
+                if rs is not None:
+                    with torch.cuda.stream(rs):  # the bucket all-reduce follows the reduction
+                        on_layer_done(l)
+                else:
+                    on_layer_done(l)
         # weight / bias gradients complete before anything on the main stream reads them
         if rs is not None:
             main.wait_stream(rs)
+        elif self.defer_reduce:
+            ops.wgrad_flush()
 
 
 class BNSpec(object):

@@ -12,6 +12,8 @@ SIGNATURES = {
     "rag_conv_igemm": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P],
     "rag_conv_wgrad_workspace": [I, I, I, I, I, P],
     "rag_conv_wgrad": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, P],
+    "rag_conv_wgrad_deferred": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P],
+    "rag_wgrad_flush": [P],
     "rag_pack_weights": [P, P, P, I, I, I, I, I, P],
     "rag_pack_trunk": [P, I, I64, P],
     "rag_pack_input_u8": [P, P, P, P, I, I, I, I, I, P],

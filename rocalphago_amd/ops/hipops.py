@@ -139,19 +139,32 @@ def wgrad_workspace(B, S, coutp, cinp, ks, device):
 
 
 def conv_wgrad(g, x, dw, db, B, S, hi, cout, coutp, cin, cinp, ks, accumulate=False, work=None,
-               hg=None, reduce_stream=None):
+               hg=None, reduce_stream=None, defer=False):
     """dW (OIHW fp32) and db from dL/dpre g [pad hg] and the layer input x [pad hi].
     ``reduce_stream`` (a torch stream): run the partial-slab reduction there, ordered after the
     wgrad kernel by an event, so it overlaps the following kernels of the current stream; the
-    caller then owns the ordering of ``work`` reuse and of ``dw``/``db`` consumers."""
+    caller then owns the ordering of ``work`` reuse and of ``dw``/``db`` consumers.
+    ``defer``: leave a bf16 partial-slab reduction pending; the next ``conv_igemm`` on this stream
+    runs it in its free block slots (or ``wgrad_flush()`` launches it). ``dw``/``db`` are final
+    only after that."""
     if work is None:
         work = wgrad_workspace(B, S, coutp, cinp, ks, g.device)
     if hg is None:
         hg = (g.shape[1] - S) // 2
+    if defer and reduce_stream is None:
+        _check(_lib().rag_conv_wgrad_deferred(_ptr(g), _ptr(x), _ptr(dw), _ptr(db), _ptr(work), B,
+                                              S, hi, hg, g.shape[-1], cout, coutp, cin, cinp, ks,
+                                              int(accumulate), _stream()), "conv_wgrad_deferred")
+        return
     rs = ctypes.c_void_p(reduce_stream.cuda_stream) if reduce_stream is not None else None
     _check(_lib().rag_conv_wgrad(_ptr(g), _ptr(x), _ptr(dw), _ptr(db), _ptr(work), B, S, hi, hg,
                                  g.shape[-1], cout, coutp, cin, cinp, ks, int(accumulate),
                                  _stream(), rs), "conv_wgrad")
+
+
+def wgrad_flush():
+    """Launch a reduction left pending by ``conv_wgrad(defer=True)`` (no-op if none)."""
+    _check(_lib().rag_wgrad_flush(_stream()), "wgrad_flush")
 
 
 def pack_input(features, out, H, index=None, transforms=None, nplanes=None):

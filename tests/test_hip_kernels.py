@@ -360,3 +360,36 @@ def test_wgrad_slab_bf16_partials_match_fp32(ops, wmap):
         assert rel_err(out[mode][0], 2 * ref) < 1e-2
         assert rel_err(out[mode][1], 2 * bf(g).sum((0, 2, 3))) < 1e-2
     assert rel_err(out[1][0], out[0][0]) < 5e-3
+
+
+@pytest.mark.gpu
+def test_deferred_wgrad_reduce_fused_into_dgrad(ops):
+    """conv_wgrad(defer=True) leaves the bf16 partial-slab reduction pending; the next conv_igemm
+    (a tap-slab dgrad) runs it in extra blocks, or wgrad_flush() launches it. dW / db equal the
+    standalone reduction and the dgrad output is unchanged."""
+    dev = torch.device("cuda")
+    torch.manual_seed(9)
+    B, C, S = 64, 192, 19
+    x = F.relu(torch.randn(B, C, S, S, device=dev))
+    g = torch.randn(B, C, S, S, device=dev)
+    w = torch.randn(C, C, 3, 3, device=dev) * 0.05
+    xp, gp = ops.pack_nchw(x, 1, C), ops.pack_nchw(g, 1, C)
+    _, wb = ops.pack_weights(w, C, C, wb=torch.empty(9, C, C, dtype=torch.bfloat16, device=dev))
+    ref_dw, ref_db = torch.zeros(C, C, 3, 3, device=dev), torch.zeros(C, device=dev)
+    ops.conv_wgrad(gp, xp, ref_dw, ref_db, B, S, 1, C, C, C, C, 3, hg=1)
+    ref_dx = ops.alloc_padded(B, S, 1, C, dev)
+    ops.conv_igemm(gp, wb, None, ref_dx, B, S, 1, 1, C, C, 3, False, mask=xp)
+    # fused into the dgrad launch
+    dw, db = torch.full((C, C, 3, 3), 7.0, device=dev), torch.full((C,), 7.0, device=dev)
+    ops.conv_wgrad(gp, xp, dw, db, B, S, 1, C, C, C, C, 3, hg=1, defer=True)
+    dx = ops.alloc_padded(B, S, 1, C, dev)
+    ops.conv_igemm(gp, wb, None, dx, B, S, 1, 1, C, C, 3, False, mask=xp)
+    torch.cuda.synchronize()
+    assert torch.equal(dx, ref_dx)
+    assert rel_err(dw, ref_dw) < 1e-5 and rel_err(db, ref_db) < 1e-5
+    # explicit flush, accumulating on top
+    ops.conv_wgrad(gp, xp, dw, db, B, S, 1, C, C, C, C, 3, accumulate=True, hg=1, defer=True)
+    ops.wgrad_flush()
+    ops.wgrad_flush()  # nothing pending: no-op
+    torch.cuda.synchronize()
+    assert rel_err(dw, 2 * ref_dw) < 1e-5 and rel_err(db, 2 * ref_db) < 1e-5
