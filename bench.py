@@ -217,7 +217,8 @@ def main():
                 r = r or {"sims_per_s": 0.0, "rollouts_per_s": 0.0}
             else:
                 from benchmarks.mcts_bench import measure
-                r = measure(dev, playouts=args.mcts_playouts, moves=2)
+                # untimed warmup of 8 waves (allocations, a full 6-wave rollout group), 4 moves timed
+                r = measure(dev, playouts=args.mcts_playouts, warmup=4096, moves=4)
         except Exception as e:  # the SL metric stands on its own
             err = str(e)[:200]
         tot = torch.tensor([r["sims_per_s"] if r else 0.0,
