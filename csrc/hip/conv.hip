@@ -576,7 +576,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
 // COUTP <= YC).  bias: fp32 [COUTP] or null.  mask: the dgrad ReLU mask (layer input), null or
 // laid out like Y but with its own halo HM.  res: null or a residual added before the activation
 // (ResNet sum-merge), laid out like Y (may alias Y: each element is read then written by one lane).
-// Deferred wgrad reduction (rag_conv_wgrad_deferred): the bf16 partial-slab reduction of one
+// Deferred wgrad reduction (rag_conv_wgrad_deferred): the fp16 partial-slab reduction of one
 // layer waits here and rides along the next conv_tap launch on the same stream as extra blocks
 // (that launch fills 482 of 512 block slots at B = 256, so the reduction runs in otherwise idle
 // slots instead of as a 14 us kernel of its own). One slot: a second deferral, a launch on
@@ -835,7 +835,7 @@ RAG_API int rag_conv_wgrad(const void* G, const void* X, float* dW, float* db, f
                          accumulate, stream, reduce_stream, false);
 }
 
-// As rag_conv_wgrad, but a bf16 partial-slab reduction is left pending for the next conv launch
+// As rag_conv_wgrad, but an fp16 partial-slab reduction is left pending for the next conv launch
 // on `stream` (see g_pending); dW / db are complete once that launch (or rag_wgrad_flush) ran.
 RAG_API int rag_conv_wgrad_deferred(const void* G, const void* X, float* dW, float* db,
                                     float* work, int B, int S, int HI, int HG, int GC, int COUT,

@@ -1,8 +1,11 @@
-// bf16 partial slabs of wgrad_slab_kernel (wgrad_slab.hip) and their chunk reduction, shared by
+// Block-scaled fp16 partial slabs of wgrad_slab_kernel (wgrad_slab.hip) and their chunk reduction, shared by
 // the standalone reduce kernel and the reduce blocks fused into the next dgrad launch
 // (conv_tap.hip).
 //
-// Layout per chunk: [ctile][slot][wave][lane][4] bf16, slot = i * NA + a (WMap: wave w owns NA
+// Partials are fp16 with one power-of-two scale per block (block floating point: the block's
+// largest |partial| maps into [2^14, 2^15), 11 mantissa bits instead of bf16's 8 at the same
+// bytes); scale[chunk * ntc + ctile] holds the inverse factor.
+// Layout per chunk: [ctile][slot][wave][lane][4] fp16, slot = i * NA + a (WMap: wave w owns NA
 // n-frags starting at nf0(w), c-frag cf(w) and NT taps tap(w, i)); an "oct" is 8 consecutive
 // elements = the 4-value C fragments of two adjacent lanes.
 #pragma once
@@ -16,20 +19,26 @@ constexpr int kWsWaves = 12;                // waves per wgrad_slab block
 constexpr int kWsBlk = 9 * kWsN * kWsC;     // accumulators per block
 
 // Everything a chunk reduction needs (passed by value into kernels).
+typedef _Float16 f16;
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
 struct WgradRed {
-  const bf16* part;    // [nchunks][ntc * kWsBlk] bf16 partials
+  const f16* part;     // [nchunks][ntc * kWsBlk] scaled fp16 partials
+  const float* scale;  // [nchunks * ntc] inverse block scales
   const float* bpart;  // [nchunks][kWsN] fp32 bias partials (or null)
   float* dW;           // OIHW [COUT][CIN][3][3]
   float* db;           // [COUT] (or null)
   int nchunks, ntc, COUT, CIN, accumulate, map;
 };
 
-__device__ __forceinline__ void wslab_add8(float (&s)[8], const uint4& v) {
+__device__ __forceinline__ void wslab_add8(float (&s)[8], const uint4& v, float sc) {
   const uint32_t u[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    s[2 * j] += __uint_as_float(u[j] << 16);
-    s[2 * j + 1] += __uint_as_float(u[j] & 0xffff0000u);
+    const f16x2 h = __builtin_bit_cast(f16x2, u[j]);
+    s[2 * j] += sc * (float)h[0];
+    s[2 * j + 1] += sc * (float)h[1];
   }
 }
 
@@ -81,15 +90,16 @@ __device__ __forceinline__ void wslab_reduce_blocks(const WgradRed& r, int b, in
 #pragma unroll
     for (int j = 0; j < 8; ++j) s[j] = 0.f;
     const uint4* p = base + q;
+    const float* sc = r.scale + (q * 8) / kWsBlk;  // + chunk * ntc
     int k = 0;
     for (; k + U <= r.nchunks; k += U) {
       uint4 a[U];
 #pragma unroll
       for (int j = 0; j < U; ++j) a[j] = p[(size_t)(k + j) * st];
 #pragma unroll
-      for (int j = 0; j < U; ++j) wslab_add8(s, a[j]);
+      for (int j = 0; j < U; ++j) wslab_add8(s, a[j], sc[(k + j) * r.ntc]);
     }
-    for (; k < r.nchunks; ++k) wslab_add8(s, p[(size_t)k * st]);
+    for (; k < r.nchunks; ++k) wslab_add8(s, p[(size_t)k * st], sc[k * r.ntc]);
     wslab_store_oct(r, q, s);
   }
   if (b == 0 && r.db && r.bpart) {

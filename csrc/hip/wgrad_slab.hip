@@ -29,6 +29,8 @@
 // halves it. Each partial already sums 42 x 64 rows in fp32, so the rounding is one bf16 ulp per
 // partial on a gradient that bf16 autocast training would round to bf16 as a whole.
 // RAG_WGRAD_PART=fp32 keeps the fp32 part[chunk][tap][n][c] slabs + wgrad_reduce_kernel.
+#include <cstring>
+
 #include "common.h"
 #include "wgrad_part.h"
 
@@ -66,7 +68,13 @@ __device__ __forceinline__ void wait_young(int young) {
 // in the one __shared__ array: a second __shared__ object made hipcc drain every in-flight
 // global_load_lds (s_waitcnt vmcnt(0)) before the first ds_read of each stage (guide §5,
 // "Projection GEMM" item 4(a); seen in this kernel's .s).
-constexpr int kBlkElems = 9 * kN * kC;  // accumulators per block (bf16 partial slab)
+constexpr int kBlkElems = 9 * kN * kC;  // accumulators per block (fp16 partial slab)
+
+// inverse block scales follow the fp16 partials of all nblk blocks in the workspace
+__host__ __device__ inline float* part_scale(float* part, int nblk) {
+  return reinterpret_cast<float*>(reinterpret_cast<char*>(part) +
+                                  (size_t)nblk * kBlkElems * sizeof(_Float16));
+}
 
 // Wave -> tile map (kMAP): the block's 12 n-frags x 2 c-frags x 9 taps = 216 MFMA tiles, 18 per
 // wave. kMAP 0: 2 n-frags x 1 c-frag x 9 taps per wave (11 transposed fragment reads per k-step);
@@ -201,16 +209,35 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
   }
 
   if (kBF) {
-    // bf16 partials in the MFMA C layout: [chunk][ctile][i * NA + a][wave][lane][4]
-    bf16* dst = reinterpret_cast<bf16*>(part) + (size_t)wid * kBlkElems + (w * 64 + lane) * 4;
+    // scaled fp16 partials in the MFMA C layout: [chunk][ctile][i * NA + a][wave][lane][4];
+    // the block's max |acc| picks a power-of-two scale into [2^14, 2^15) (wgrad_part.h)
+    float mx = 0.f;
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+      for (int a = 0; a < NA; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, fabsf(acc[i][a][r]));
+    mx = warp_max(mx);
+    float* red = reinterpret_cast<float*>(lds);
+    __syncthreads();  // every wave is done reading the staging ring
+    if (lane == 0) red[w] = mx;
+    __syncthreads();
+    mx = red[0];
+#pragma unroll
+    for (int k = 1; k < kWaves; ++k) mx = fmaxf(mx, red[k]);
+    const int e = mx > 0.f ? ilogbf(mx) : 0;
+    const float up = ldexpf(1.f, 14 - e);
+    if (tid == 0) part_scale(part, gridDim.x)[wid] = ldexpf(1.f, e - 14);
+    f16* dst = reinterpret_cast<f16*>(part) + (size_t)wid * kBlkElems + (w * 64 + lane) * 4;
 #pragma unroll
     for (int i = 0; i < NT; ++i)
 #pragma unroll
       for (int a = 0; a < NA; ++a) {
-        bf16x4 o;
+        f16x4 o;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = (bf16)acc[i][a][r];
-        *reinterpret_cast<bf16x4*>(dst + (i * NA + a) * (kWaves * 256)) = o;
+        for (int r = 0; r < 4; ++r) o[r] = (f16)(acc[i][a][r] * up);
+        *reinterpret_cast<f16x4*>(dst + (i * NA + a) * (kWaves * 256)) = o;
       }
   } else {
   // partial slab part[chunk][tap][n][c]; C layout: col = lane&15, row = 4*(lane>>4) + r
@@ -239,7 +266,7 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
   }
 }
 
-// Sums the bf16 partial slabs of wgrad_slab_kernel<.., true> over chunks in fp32 and scatters
+// Sums the fp16 partial slabs of wgrad_slab_kernel<.., true> over chunks in fp32 and scatters
 // to OIHW dW [COUT][CIN][3][3] (+ the fp32 bias partials). A 256-thread block owns 64 "octs"
 // (8 consecutive partial elements = two lanes' 4-value C fragments); its 4 waves split the chunks
 // (wave s sums chunks s, s+4, ...: a 16-byte load per chunk, U in flight) and combine through
@@ -268,6 +295,7 @@ wgrad_slab_reduce_kernel(WgradRed red) {
   const bool live = q < octs;
   q = live ? q : octs - 1;
   const uint4* p = reinterpret_cast<const uint4*>(red.part) + q;
+  const float* sc = red.scale + (q * 8) / kBlkElems;  // + chunk * ntc
   const size_t st = slab / 8;
   float s[8];
 #pragma unroll
@@ -278,9 +306,9 @@ wgrad_slab_reduce_kernel(WgradRed red) {
 #pragma unroll
     for (int j = 0; j < U; ++j) a[j] = p[(size_t)(k + j * kRedSplit) * st];
 #pragma unroll
-    for (int j = 0; j < U; ++j) wslab_add8(s, a[j]);
+    for (int j = 0; j < U; ++j) wslab_add8(s, a[j], sc[(k + j * kRedSplit) * red.ntc]);
   }
-  for (; k < red.nchunks; k += kRedSplit) wslab_add8(s, p[(size_t)k * st]);
+  for (; k < red.nchunks; k += kRedSplit) wslab_add8(s, p[(size_t)k * st], sc[k * red.ntc]);
   if (sp > 0) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) part_sums[sp - 1][lo][j] = s[j];
@@ -321,7 +349,7 @@ int rag_wgrad_slab_nchunks(int R, int CINP, int* spc) {
 }
 
 static int g_wslab_nbuf = -1;  // RAG_WGRAD_NBUF (3..5), read on first use
-static int g_wslab_bf = -1;    // bf16 partial slabs unless RAG_WGRAD_PART=fp32
+static int g_wslab_bf = -1;    // block-scaled fp16 partial slabs unless RAG_WGRAD_PART=fp32
 static int g_wslab_map = -1;   // wave -> tile map (WMap), RAG_WGRAD_MAP
 
 static int wslab_map() {
@@ -347,7 +375,7 @@ RAG_API int rag_wgrad_slab_part_bf16(int on) {
 bool rag_wgrad_slab_bf16() {
   if (g_wslab_bf < 0) {
     const char* e = getenv("RAG_WGRAD_PART");
-    g_wslab_bf = (e && e[0] == 'f') ? 0 : 1;
+    g_wslab_bf = (e && strcmp(e, "fp32") == 0) ? 0 : 1;
   }
   return g_wslab_bf != 0;
 }
@@ -355,7 +383,8 @@ bool rag_wgrad_slab_bf16() {
 WgradRed rag_wgrad_slab_red(const void* part, const float* bpart, float* dW, float* db,
                             int nchunks, int CINP, int COUT, int CIN, int accumulate) {
   WgradRed r;
-  r.part = (const bf16*)part;
+  r.part = (const f16*)part;
+  r.scale = part_scale((float*)part, nchunks * (CINP / kC));
   r.bpart = bpart;
   r.dW = dW;
   r.db = db;

@@ -144,7 +144,7 @@ def conv_wgrad(g, x, dw, db, B, S, hi, cout, coutp, cin, cinp, ks, accumulate=Fa
     ``reduce_stream`` (a torch stream): run the partial-slab reduction there, ordered after the
     wgrad kernel by an event, so it overlaps the following kernels of the current stream; the
     caller then owns the ordering of ``work`` reuse and of ``dw``/``db`` consumers.
-    ``defer``: leave a bf16 partial-slab reduction pending; the next ``conv_igemm`` on this stream
+    ``defer``: leave an fp16 partial-slab reduction pending; the next ``conv_igemm`` on this stream
     runs it in its free block slots (or ``wgrad_flush()`` launches it). ``dw``/``db`` are final
     only after that."""
     if work is None:

@@ -25,7 +25,7 @@ from rocalphago_amd.parallel.dp import DPContext  # noqa: E402
 from rocalphago_amd.training.data import DeviceDataset  # noqa: E402
 from rocalphago_amd.training.supervised import SupervisedTrainer  # noqa: E402
 
-STEPS, LOCAL_B = 4, 32
+STEPS, LOCAL_B = int(os.environ.get("DP_CHECK_STEPS", "4")), 32
 
 
 def make(dev):

@@ -332,7 +332,7 @@ def test_sl_batch_prep(ops):
 @pytest.mark.gpu
 @pytest.mark.parametrize("wmap", [0, 1])
 def test_wgrad_slab_bf16_partials_match_fp32(ops, wmap):
-    """wgrad_slab's default bf16 partial slabs (MFMA C layout + wgrad_slab_reduce_kernel) vs the
+    """wgrad_slab's default block-scaled fp16 partial slabs (MFMA C layout + reduce) vs the
     fp32 part[chunk][tap][n][c] path and fp32 PyTorch, accumulating, for both wave->tile maps."""
     dev = torch.device("cuda")
     torch.manual_seed(5)
@@ -359,7 +359,8 @@ def test_wgrad_slab_bf16_partials_match_fp32(ops, wmap):
     for mode in (1, 0):
         assert rel_err(out[mode][0], 2 * ref) < 1e-2
         assert rel_err(out[mode][1], 2 * bf(g).sum((0, 2, 3))) < 1e-2
-    assert rel_err(out[1][0], out[0][0]) < 5e-3
+    print("fp16-vs-fp32 partials rel err", rel_err(out[1][0], out[0][0]))
+    assert rel_err(out[1][0], out[0][0]) < 1e-3
 
 
 @pytest.mark.gpu
