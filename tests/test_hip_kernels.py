@@ -331,7 +331,7 @@ def test_sl_batch_prep(ops):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("wmap", [0, 1])
-def test_wgrad_slab_bf16_partials_match_fp32(ops, wmap):
+def test_wgrad_slab_fp16_partials_match_fp32(ops, wmap):
     """wgrad_slab's default block-scaled fp16 partial slabs (MFMA C layout + reduce) vs the
     fp32 part[chunk][tap][n][c] path and fp32 PyTorch, accumulating, for both wave->tile maps."""
     dev = torch.device("cuda")
