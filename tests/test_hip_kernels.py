@@ -394,3 +394,27 @@ def test_deferred_wgrad_reduce_fused_into_dgrad(ops):
     ops.wgrad_flush()  # nothing pending: no-op
     torch.cuda.synchronize()
     assert rel_err(dw, 2 * ref_dw) < 1e-5 and rel_err(db, 2 * ref_db) < 1e-5
+
+
+@pytest.mark.gpu
+def test_trunk_repack_matches_per_layer_packer(ops):
+    """pack_trunk (one launch, 32x32 all-tap tiles) equals pack_weights per layer for both bf16
+    GEMM layouts and the padded biases: a 5x5 48->192 layer, odd widths, 3x3 layers."""
+    from rocalphago_amd.models.engine import ConvSpec, HipTrunk
+    dev = torch.device("cuda")
+    torch.manual_seed(4)
+    specs = [ConvSpec(5, 48, 192, True), ConvSpec(3, 192, 192, True), ConvSpec(3, 192, 40, True),
+             ConvSpec(3, 40, 64, True), ConvSpec(1, 64, 1, False)]
+    tr = HipTrunk(specs, 19, dev)
+    ws = [torch.randn(s.cout, s.cin, s.ks, s.ks, device=dev) for s in specs]
+    bs = [torch.randn(s.cout, device=dev) for s in specs]
+    tr.sync_weights(ws, bs, 1)
+    torch.cuda.synchronize()
+    for l, s in enumerate(specs):
+        wb = torch.empty(s.ks * s.ks, s.cinp, s.coutp, dtype=torch.bfloat16, device=dev)
+        wf, wb = ops.pack_weights(ws[l], s.coutp, s.cinp, wb=wb)
+        assert torch.equal(tr._wf[l], wf), l
+        assert torch.equal(tr._wb[l], wb), l
+        ref_b = torch.zeros(s.coutp, device=dev)
+        ref_b[:s.cout] = bs[l]
+        assert torch.equal(tr._bias[l], ref_b), l
