@@ -165,8 +165,9 @@ class WaveEvaluator(object):
                 from .gpu_rollout import GpuRollouts
                 self._gro = GpuRollouts(self.rollout, self.device)
             from .gpu_rollout import _Pending
-            ev, w, _, _ = self._gro._launch(colors, meta8, S, komi, self.R, self.limit, seed)
-            return _Pending(ev, w, colors.shape[0], self.R)
+            ev, _, _, _, host = self._gro._launch(colors, meta8, S, komi, self.R, self.limit,
+                                                  seed)
+            return _Pending(ev, host, colors.shape[0], self.R)
         win = self.rollout.rollouts(boards, seed=seed, limit=self.limit, nthreads=self.nthreads)
         z = np.where(win == go.BLACK, 1.0, np.where(win == go.WHITE, -1.0, 0.0))
         return _Done(z.astype(np.float32))

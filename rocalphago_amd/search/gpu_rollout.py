@@ -15,9 +15,13 @@ from ..ops.hipops import _check, _lib, _ptr
 
 
 class _Pending(object):
-    def __init__(self, event, winners, n, R):
+    """One launch's winners, copied to pinned host memory on the rollout's own stream: reading
+    them waits for that stream only. (A ``.cpu()`` here ran on the main stream and so waited for
+    every network wave queued there, stalling the search pipeline at each rollout backup.)"""
+
+    def __init__(self, event, host_winners, n, R):
         self.event = event
-        self.winners = winners
+        self.host = host_winners
         self.n = n
         self.R = R
 
@@ -27,8 +31,8 @@ class _Pending(object):
     def result(self):
         """Mean result per leaf from BLACK's point of view, numpy float32 [n]."""
         self.event.synchronize()
-        w = self.winners.view(self.n, self.R).float().mean(1)
-        return w.cpu().numpy()
+        w = self.host.numpy().reshape(self.n, self.R).astype(np.float32)
+        return w[:, 0].copy() if self.R == 1 else w.mean(1, dtype=np.float32)
 
 
 class _Group(object):
@@ -98,8 +102,8 @@ class RolloutBatcher(object):
         S, komi, R, limit, seed = self.args
         colors = np.concatenate(g.colors) if len(g.colors) > 1 else g.colors[0]
         meta = np.concatenate(g.meta) if len(g.meta) > 1 else g.meta[0]
-        ev, winners, _, _ = self.gr._launch(colors, meta, S, komi, R, limit, seed)
-        g.pending = _Pending(ev, winners, colors.shape[0], R)
+        ev, _, _, _, host = self.gr._launch(colors, meta, S, komi, R, limit, seed)
+        g.pending = _Pending(ev, host, colors.shape[0], R)
 
 
 class GpuRollouts(object):
@@ -145,16 +149,18 @@ class GpuRollouts(object):
                                        _ptr(lengths), _ptr(logits),
                                        ctypes.c_void_p(stream.cuda_stream)),
                    "rollouts")
+            host = torch.empty(games, dtype=torch.int8, pin_memory=True)
+            host.copy_(winners, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(stream)
-        return ev, winners, lengths, logits
+        return ev, winners, lengths, logits, host
 
     def launch(self, search, wave, R, limit, seed=1):
         """Start R playouts for every leaf of a native Search wave (non-blocking)."""
         colors, meta = search.rollout_inputs(wave)
         b = search.root_board
-        ev, winners, _, _ = self._launch(colors, meta, b.size, b.komi, R, limit, seed)
-        return _Pending(ev, winners, colors.shape[0], R)
+        ev, _, _, _, host = self._launch(colors, meta, b.size, b.komi, R, limit, seed)
+        return _Pending(ev, host, colors.shape[0], R)
 
     # ---------------------------------------------------------------- direct use / tests
     @staticmethod
@@ -174,17 +180,20 @@ class GpuRollouts(object):
     def run(self, states, R=1, limit=500, seed=1):
         """(winners [n, R] int8, lengths [n, R] int16) as numpy."""
         colors, meta = self.encode(states)
-        ev, w, ln, _ = self._launch(colors, meta, states[0].size, states[0].komi, R, limit,
-                                    seed, length=True)
+        ev, _, ln, _, host = self._launch(colors, meta, states[0].size, states[0].komi, R, limit,
+                                          seed, length=True)
         ev.synchronize()
         n = len(states)
-        return w.view(n, R).cpu().numpy(), ln.view(n, R).cpu().numpy()
+        with torch.cuda.stream(self.streams[0]):  # lengths: read after the launch's own event
+            torch.cuda.current_stream().wait_event(ev)
+            lens = ln.view(n, R).cpu().numpy()
+        return host.numpy().reshape(n, R).copy(), lens
 
     def initial_logits(self, states):
         """Debug: candidate logits at each state's position ([n, S*S], -inf = not a legal
         candidate), for parity with RolloutPolicy.candidates."""
         colors, meta = self.encode(states)
-        ev, _, _, lg = self._launch(colors, meta, states[0].size, states[0].komi, 1, 0, 1,
-                                    dbg=True)
+        ev, _, _, lg, _ = self._launch(colors, meta, states[0].size, states[0].komi, 1, 0, 1,
+                                       dbg=True)
         ev.synchronize()
         return lg.cpu().numpy()
