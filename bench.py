@@ -217,7 +217,7 @@ def main():
                 r = r or {"sims_per_s": 0.0, "rollouts_per_s": 0.0}
             else:
                 from benchmarks.mcts_bench import measure
-                # untimed warmup of 8 waves (allocations, a full 6-wave rollout group), 4 moves timed
+                # untimed warmup: 8 waves (allocations, a full 6-wave rollout group); 4 moves timed
                 r = measure(dev, playouts=args.mcts_playouts, warmup=4096, moves=4)
         except Exception as e:  # the SL metric stands on its own
             err = str(e)[:200]

@@ -17,6 +17,8 @@
 // source rows, lane-linear LDS image, swizzle applied on the source address), double-buffered.
 // The MFMA is issued as C^T = W * X^T so each lane owns 4 consecutive output channels of one
 // pixel: the epilogue (bias, ReLU, ReLU-mask, bf16 pack) stores 8 bytes per lane.
+#include <mutex>
+
 #include "common.h"
 #include "wgrad_part.h"
 
@@ -581,15 +583,29 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
 // (that launch fills 482 of 512 block slots at B = 256, so the reduction runs in otherwise idle
 // slots instead of as a 14 us kernel of its own). One slot: a second deferral, a launch on
 // another stream or rag_wgrad_flush launches the pending reduction as a standalone kernel.
+// The slot is guarded by a mutex (a search thread may launch convolutions while a trainer runs);
+// a pending reduction is taken out of the slot before anything is launched with it.
 int rag_launch_wgrad_slab_reduce(const WgradRed& r, hipStream_t stream);  // wgrad_slab.hip
+static std::mutex g_pending_mu;
 static WgradRed g_pending;
 static hipStream_t g_pending_stream = nullptr;
 static bool g_has_pending = false;
 
-static int flush_pending(hipStream_t stream) {
-  if (!g_has_pending) return 0;
+// Take the pending reduction if there is one: returns false if the slot was empty.
+static bool take_pending(WgradRed* r, hipStream_t* st) {
+  std::lock_guard<std::mutex> lk(g_pending_mu);
+  if (!g_has_pending) return false;
+  *r = g_pending;
+  *st = g_pending_stream;
   g_has_pending = false;
-  return rag_launch_wgrad_slab_reduce(g_pending, stream ? stream : g_pending_stream);
+  return true;
+}
+
+static int flush_pending(hipStream_t stream) {
+  WgradRed r;
+  hipStream_t st;
+  if (!take_pending(&r, &st)) return 0;
+  return rag_launch_wgrad_slab_reduce(r, stream ? stream : st);
 }
 
 RAG_API int rag_wgrad_flush(hipStream_t stream) { return flush_pending(stream); }
@@ -612,23 +628,27 @@ RAG_API int rag_conv_igemm(const void* X, const void* W, const float* bias, void
     const char* e = getenv("RAG_CONV_PIPE");
     return !(e && e[0] == '0');
   }();
-  const WgradRed* red = (g_has_pending && g_pending_stream == stream) ? &g_pending : nullptr;
-  if (g_has_pending && !red) {
-    const int rc = flush_pending(nullptr);
-    if (rc) return rc;
+  WgradRed pend;
+  hipStream_t pend_stream = nullptr;
+  const WgradRed* red = nullptr;
+  if (take_pending(&pend, &pend_stream)) {
+    if (pend_stream == stream) {
+      red = &pend;  // rides along this launch (or goes out on its own just below)
+    } else {
+      const int rc = rag_launch_wgrad_slab_reduce(pend, pend_stream);
+      if (rc) return rc;
+    }
   }
   if (rag_conv_slab_launch(x, w, bias, y, mk, res, B, S, HI, WO, HO, CIN, COUTP, YC, KS, relu,
                            HM, stream)) {
-    const int rc = red ? flush_pending(stream) : 0;  // opt-in slab conv: reduce on its own
+    const int rc = red ? rag_launch_wgrad_slab_reduce(*red, stream) : 0;  // opt-in slab conv
     return rc ? rc : (int)hipGetLastError();
   }
   if (use_pipe && rag_conv_tap_launch(x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN,
-                                      COUTP, YC, KS, relu, HM, (long)B * WI * WI, stream, red)) {
-    if (red) g_has_pending = false;
+                                      COUTP, YC, KS, relu, HM, (long)B * WI * WI, stream, red))
     return (int)hipGetLastError();
-  }
   if (red) {  // not a tap-slab launch: the reduction goes out on its own first
-    const int rc = flush_pending(stream);
+    const int rc = rag_launch_wgrad_slab_reduce(*red, stream);
     if (rc) return rc;
   }
   if (use_pipe && rag_conv_pipe_launch(x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN,
@@ -801,6 +821,7 @@ static int conv_wgrad_impl(const void* G, const void* X, float* dW, float* db, f
     const WgradRed r = rag_wgrad_slab_red(part, bpart, dW, db, nchunks, CINP, COUT, CIN,
                                           accumulate);
     if (defer && rs == stream) {
+      std::lock_guard<std::mutex> lk(g_pending_mu);
       g_pending = r;
       g_pending_stream = stream;
       g_has_pending = true;
