@@ -61,7 +61,10 @@ Board::Board(int size, double komi, bool enforce_superko, std::shared_ptr<const 
 
 void Board::copy_from(const Board& o) {
   g_ = o.g_;
-  zob_ = o.zob_;
+  // shared pointers are assigned only when they differ: search threads copy one root board into
+  // recycled leaf boards that already share its tables, and an unconditional assignment would
+  // bounce the control blocks' reference counts between all of them
+  if (zob_ != o.zob_) zob_ = o.zob_;
   S_ = o.S_;
   P_ = o.P_;
   W_ = o.W_;
@@ -80,9 +83,9 @@ void Board::copy_from(const Board& o) {
   komi_ = o.komi_;
   hash_ = o.hash_;
   clock_ = o.clock_;
-  history_ = o.history_;          // copy-on-write
-  prev_hashes_ = o.prev_hashes_;  // copy-on-write
-  handicaps_ = o.handicaps_;
+  if (history_ != o.history_) history_ = o.history_;                // copy-on-write
+  if (prev_hashes_ != o.prev_hashes_) prev_hashes_ = o.prev_hashes_;  // copy-on-write
+  if (!(handicaps_.empty() && o.handicaps_.empty())) handicaps_ = o.handicaps_;
   std::memcpy(color_, o.color_, P_);
   std::memcpy(head_, o.head_, sizeof(int16_t) * P_);
   std::memcpy(nxt_, o.nxt_, sizeof(int16_t) * P_);

@@ -440,10 +440,12 @@ __device__ __forceinline__ void dihedral(int t, int n, int i, int j, int& si, in
 // -> padded channels-last bf16 [B][S+2H][S+2H][CP]   (K08 fused with layout conversion)
 // One thread per (pixel, 8-channel group): 8x the threads of a per-pixel loop, so the byte
 // gathers of one pixel's planes are in flight together and a wave's 16-byte stores are contiguous.
+// FS = planes per position in F (>= NF: e.g. the policy net reads the first 48 of the search's
+// shared 49-plane policy+value input in place).
 template <typename T>
 __global__ void pack_input_kernel(const T* __restrict__ F, const int64_t* __restrict__ index,
                                   const int* __restrict__ tf, bf16* __restrict__ X, int B, int NF,
-                                  int S, int H, int CP) {
+                                  int FS, int S, int H, int CP) {
   const int S2 = S * S;
   const int G = CP / 8;
   const int total = B * S2 * G;
@@ -457,7 +459,7 @@ __global__ void pack_input_kernel(const T* __restrict__ F, const int64_t* __rest
     int si = i, sj = j;
     if (tf) dihedral(tf[b], S, i, j, si, sj);
     const int64_t sb = index ? index[b] : b;
-    const T* src = F + (size_t)sb * NF * S2 + si * S + sj;
+    const T* src = F + (size_t)sb * FS * S2 + si * S + sj;
     bf16* dst = X + ((size_t)(b * WP + i + H) * WP + j + H) * CP;
     bf16x8 v;
 #pragma unroll
@@ -935,10 +937,12 @@ RAG_API int rag_pack_trunk(const int64_t* table, int nlayers, int64_t total, hip
 }
 
 RAG_API int rag_pack_input_u8(const uint8_t* F, const int64_t* index, const int* tf, void* X,
-                              int B, int NF, int S, int H, int CP, hipStream_t stream) {
+                              int B, int NF, int FS, int S, int H, int CP, hipStream_t stream) {
+  if (FS < NF) return -1;
   const int total = B * S * S * (CP / 8);
   const int blocks = (total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192;
-  pack_input_kernel<uint8_t><<<blocks, 256, 0, stream>>>(F, index, tf, (bf16*)X, B, NF, S, H, CP);
+  pack_input_kernel<uint8_t><<<blocks, 256, 0, stream>>>(F, index, tf, (bf16*)X, B, NF, FS, S, H,
+                                                         CP);
   return (int)hipGetLastError();
 }
 
@@ -952,10 +956,11 @@ RAG_API int rag_pack_input_bits(const uint64_t* Fb, const int64_t* index, const 
 }
 
 RAG_API int rag_pack_input_f32(const float* F, const int64_t* index, const int* tf, void* X,
-                               int B, int NF, int S, int H, int CP, hipStream_t stream) {
+                               int B, int NF, int FS, int S, int H, int CP, hipStream_t stream) {
+  if (FS < NF) return -1;
   const int total = B * S * S * (CP / 8);
   const int blocks = (total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192;
-  pack_input_kernel<float><<<blocks, 256, 0, stream>>>(F, index, tf, (bf16*)X, B, NF, S, H, CP);
+  pack_input_kernel<float><<<blocks, 256, 0, stream>>>(F, index, tf, (bf16*)X, B, NF, FS, S, H, CP);
   return (int)hipGetLastError();
 }
 

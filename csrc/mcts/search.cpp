@@ -11,7 +11,31 @@ namespace rag {
 
 namespace {
 using FArr = py::array_t<float, py::array::c_style | py::array::forcecast>;
+
+// A writable [n, ...] output view for pack_inputs: dtype itemsize `isz`, at least `row` items per
+// row, contiguous within a row (rows may be strided, e.g. columns of a record array).
+template <class T>
+T* out_view(py::object o, int n, size_t row, size_t& stride, const char* what) {
+  if (o.is_none()) return nullptr;
+  py::array a = py::reinterpret_borrow<py::array>(o);
+  if (!a.writeable()) throw std::invalid_argument(std::string(what) + ": not writeable");
+  if (a.itemsize() != (py::ssize_t)sizeof(T))
+    throw std::invalid_argument(std::string(what) + ": wrong dtype");
+  if (a.ndim() < 2 || a.shape(0) < n)
+    throw std::invalid_argument(std::string(what) + ": need [num_leaves, ...]");
+  size_t inner = 1;
+  for (py::ssize_t d = 1; d < a.ndim(); ++d) inner *= (size_t)a.shape(d);
+  if (inner < row) throw std::invalid_argument(std::string(what) + ": rows too short");
+  py::ssize_t expect = (py::ssize_t)sizeof(T);
+  for (py::ssize_t d = a.ndim() - 1; d >= 1; --d) {
+    if (a.shape(d) > 1 && a.strides(d) != expect)
+      throw std::invalid_argument(std::string(what) + ": rows must be contiguous");
+    expect *= a.shape(d);
+  }
+  stride = (size_t)a.strides(0);
+  return static_cast<T*>(a.mutable_data());
 }
+}  // namespace
 
 void register_search(py::module_& m) {
   py::class_<Search>(m, "Search")
@@ -78,9 +102,30 @@ void register_search(py::module_& m) {
              s.rollout_inputs(id, c.mutable_data(), m.mutable_data());
              return py::make_tuple(c, m);
            })
+      .def("pack_inputs",
+           [](Search& s, int id, py::object colors, py::object ages, py::object meta4,
+              py::object meta8, py::object illegal, py::object ladders) {
+             const int n = s.num_leaves(id);
+             const size_t P = (size_t)s.root_board().npoints();
+             PackOut o;
+             o.colors = out_view<int8_t>(colors, n, P, o.s_colors, "colors");
+             o.ages = out_view<int16_t>(ages, n, P, o.s_ages, "ages");
+             o.meta4 = out_view<int32_t>(meta4, n, 4, o.s_meta4, "meta4");
+             o.meta8 = out_view<int32_t>(meta8, n, 8, o.s_meta8, "meta8");
+             o.illegal = out_view<uint8_t>(illegal, n, P, o.s_illegal, "illegal");
+             o.ladders = out_view<uint8_t>(ladders, n, 2 * P, o.s_ladders, "ladders");
+             py::gil_scoped_release nogil;
+             s.pack_inputs(id, o);
+           },
+           py::arg("wave"), py::arg("colors") = py::none(), py::arg("ages") = py::none(),
+           py::arg("meta4") = py::none(), py::arg("meta8") = py::none(),
+           py::arg("illegal") = py::none(), py::arg("ladders") = py::none(),
+           "Write the wave's leaf inputs (feature-kernel colours / stone ages / meta, rollout "
+           "meta8, superko-illegal masks, host ladder planes) into caller arrays [n, ...]")
       .def("backup_rollout",
            [](Search& s, int id, FArr z) {
              if (z.size() < s.num_leaves(id)) throw std::invalid_argument("need one z per leaf");
+             py::gil_scoped_release nogil;
              s.backup_rollout(id, z.data());
            })
       .def("start_rollouts", &Search::start_rollouts)
@@ -103,6 +148,26 @@ void register_search(py::module_& m) {
       .def_property_readonly("terminal", &Search::terminal)
       .def_property_readonly("collisions", &Search::collisions)
       .def_property_readonly("num_nodes", &Search::num_nodes)
+      .def_property_readonly("num_edges", &Search::num_edges)
+      .def("root_deltas",
+           [](Search& s) {
+             const int M = s.root_board().npoints() + 1;
+             py::array_t<float> out({4, M});
+             s.root_deltas(out.mutable_data());
+             return out;
+           },
+           "[4, P+1] (visits, value sum, rollouts, rollout sum) this rank added at the root's "
+           "children since the previous call (index P = pass)")
+      .def("set_root_external",
+           [](Search& s, FArr ext) {
+             const int M = s.root_board().npoints() + 1;
+             if (ext.size() != 4 * M) throw std::invalid_argument("external stats must be [4, P+1]");
+             const float* e = ext.data();
+             s.set_root_external(e, e + M, e + 2 * M, e + 3 * M);
+           },
+           "Other ranks' cumulative root-child statistics [4, P+1], mixed into root selection")
+      .def("clear_root_external", &Search::clear_root_external)
+      .def_property_readonly("timers", &Search::timers)
       .def_property_readonly("root_visits", &Search::root_visits)
       .def_property_readonly("root_board", &Search::root_board,
                              py::return_value_policy::reference_internal);

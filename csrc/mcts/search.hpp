@@ -17,16 +17,31 @@
 // used, value losses otherwise). Values are from the perspective of the player to move at the
 // leaf; a node stores them for the player who played its move (negamax signs on backup).
 //
+// Tree layout (host memory is the bound of a GPU-fed search, profiles/mcts_null_r3.txt):
+//   * an expansion writes one 12-byte *edge* (move, prior, child index) per sensible move; the
+//     32-byte child *node* (statistics) is allocated only when a descent first selects the edge.
+//     Most children of a 19x19 node are never visited, so a simulation writes ~4 KB instead of
+//     ~14 KB of nodes;
+//   * the first kSorted edges of a node are its highest priors in descending order (partial sort
+//     at expansion). Every unvisited child scores c_puct P sqrt(N), monotone in P, so a descent
+//     only scores the edges up to the first never-selected one (the node's high-water mark)
+//     instead of all ~360; nodes whose mark passed the sorted prefix are scanned in full;
+//   * node and edge storage are address-stable arenas (reserved virtual ranges, bump allocation,
+//     never moved, so concurrent descents may allocate), recycled process-wide with their pages
+//     already faulted in, and a helper thread faults the next megabytes in ahead of the
+//     allocation frontier: fresh-page faults cost 8 us per simulation before (19x19, 8 threads).
+//
 // Children are created for the leaf's sensible moves (legal, not an own true eye — the set the
 // players use) with priors renormalised over them; PASS is the only child when no sensible move
 // exists. Terminal leaves (end of game) are scored exactly and backed up at once.
 #pragma once
 
 #include <algorithm>
-#include <cstring>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <condition_variable>
+#include <cstring>
 #include <functional>
 #include <map>
 #include <memory>
@@ -42,6 +57,10 @@
 #include "../engine/thread_pool.hpp"
 #include "rollout.hpp"
 
+#ifndef MADV_POPULATE_WRITE
+#define MADV_POPULATE_WRITE 23
+#endif
+
 namespace rag {
 
 namespace mcts_detail {
@@ -49,67 +68,127 @@ namespace mcts_detail {
 enum : uint8_t { N_NEW = 0, N_PENDING = 1, N_EXPANDED = 2 };
 
 struct Node {
-  int32_t parent;
-  int32_t first;   // first child (children are contiguous)
-  int16_t nchild;
-  int16_t move;    // flat index, PASS = -1
-  float prior;
+  int32_t edges;   // first edge in the edge arena (valid once state == N_EXPANDED)
+  int16_t nedge;   // number of children
+  int16_t move;    // flat index of the move that leads here, PASS = -1
   int32_t n;       // value-net visits (every completed evaluation)
   int32_t nr;      // rollouts
   int32_t vl;      // in-flight descents through this node
   float w;         // value-net sum, for the player who played `move`
   float wr;        // rollout sum, same perspective
+  int16_t hwm;     // 1 + the highest edge index whose child node exists
   uint8_t state;
+  uint8_t pad;
 };
+static_assert(sizeof(Node) == 32, "Node must stay 32 bytes (two per cache line)");
 
-// Node storage: one anonymous mapping reserved up front (virtual until written, transparent
-// huge pages requested), so the tree never moves while it grows, and resize() leaves the new
-// slots uninitialised (backup_value fills them in parallel). A std::vector would zero-fill new
-// slots serially and copy the whole tree on every doubling.
-class NodeArena {
+struct Edge {
+  int32_t child;   // node index, -1 until a descent first selects this edge
+  float prior;
+  int16_t move;
+  int16_t pad;
+};
+static_assert(sizeof(Edge) == 12, "Edge must stay 12 bytes");
+
+// ------------------------------------------------------------------ memory
+// Process-wide cache of reserved anonymous mappings: an arena returns its range here with the
+// number of bytes whose pages are already resident ("warm"), and the next arena of the same size
+// (a compaction, a new Search) takes it back instead of faulting fresh pages in.
+class MapCache {
  public:
-  NodeArena() = default;
-  ~NodeArena() { unmap(p_, cap_); }
-  NodeArena(const NodeArena&) = delete;
-  NodeArena& operator=(const NodeArena&) = delete;
-  void reserve(size_t cap) {
-    if (cap > cap_) grow(cap);
+  static MapCache& get() {
+    static MapCache* c = new MapCache();  // leaked: arenas may outlive static destruction
+    return *c;
   }
-  size_t size() const { return n_; }
-  size_t capacity() const { return cap_; }
-  Node& operator[](size_t i) { return p_[i]; }
-  const Node& operator[](size_t i) const { return p_[i]; }
-  void clear() { n_ = 0; }
-  void push_back(const Node& x) {
-    if (n_ == cap_) grow(cap_ ? 2 * cap_ : (size_t)1 << 16);
-    p_[n_++] = x;
+  void* take(size_t bytes, size_t& warm) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (size_t i = 0; i < free_.size(); ++i)
+        if (free_[i].bytes == bytes) {
+          Entry e = free_[i];
+          free_.erase(free_.begin() + i);
+          warm_total_ -= e.warm;
+          warm = e.warm;
+          return e.p;
+        }
+    }
+    void* m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE,
+                   MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    if (m == MAP_FAILED) throw std::bad_alloc();
+    madvise(m, bytes, MADV_HUGEPAGE);
+    warm = 0;
+    return m;
   }
-  void resize(size_t n) {
-    if (n > cap_) grow(std::max(n, 2 * cap_));
-    n_ = n;
-  }
-  void swap(NodeArena& o) {
-    std::swap(p_, o.p_);
-    std::swap(n_, o.n_);
-    std::swap(cap_, o.cap_);
+  void give(void* p, size_t bytes, size_t warm) {
+    std::lock_guard<std::mutex> g(mu_);
+    // keep a bounded amount of resident memory; beyond it the range is unmapped
+    if (free_.size() < 8 && warm_total_ + warm <= (size_t(6) << 30)) {
+      free_.push_back(Entry{p, bytes, warm});
+      warm_total_ += warm;
+    } else {
+      munmap(p, bytes);
+    }
   }
 
  private:
-  static void unmap(Node* p, size_t cap) {
-    if (p) munmap(p, cap * sizeof(Node));
+  struct Entry {
+    void* p;
+    size_t bytes, warm;
+  };
+  std::mutex mu_;
+  std::vector<Entry> free_;
+  size_t warm_total_ = 0;
+};
+
+// Address-stable bump arena of T over a reserved virtual range (never moves: descents on other
+// threads hold references while it grows).
+template <class T>
+class Arena {
+ public:
+  explicit Arena(size_t cap) : cap_(cap) {
+    size_t warm = 0;
+    p_ = static_cast<T*>(MapCache::get().take(cap_ * sizeof(T), warm));
+    warm_.store(warm);
   }
-  void grow(size_t cap) {
-    void* m = mmap(nullptr, cap * sizeof(Node), PROT_READ | PROT_WRITE,
-                   MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
-    if (m == MAP_FAILED) throw std::bad_alloc();
-    madvise(m, cap * sizeof(Node), MADV_HUGEPAGE);
-    if (n_) std::memcpy(m, p_, n_ * sizeof(Node));
-    unmap(p_, cap_);
-    p_ = static_cast<Node*>(m);
-    cap_ = cap;
+  ~Arena() {
+    if (p_) MapCache::get().give(p_, cap_ * sizeof(T), std::max(warm_.load(), bytes_used()));
   }
-  Node* p_ = nullptr;
-  size_t n_ = 0, cap_ = 0;
+  Arena(const Arena&) = delete;
+  Arena& operator=(const Arena&) = delete;
+
+  T& operator[](size_t i) { return p_[i]; }
+  const T& operator[](size_t i) const { return p_[i]; }
+  size_t size() const { return n_.load(std::memory_order_relaxed); }
+  size_t capacity() const { return cap_; }
+  bool room(size_t k) const { return size() + k <= cap_; }
+  // callers check room() for the whole batch before the (possibly concurrent) allocations
+  size_t alloc(size_t k) { return n_.fetch_add(k, std::memory_order_relaxed); }
+  void clear() { n_.store(0); }
+  size_t bytes_used() const { return size() * sizeof(T); }
+  size_t warm_bytes() const { return warm_.load(std::memory_order_relaxed); }
+  // Fault pages in up to `upto` bytes (helper thread; contents are never modified).
+  void populate(size_t upto) {
+    upto = std::min(upto, cap_ * sizeof(T));
+    const size_t chunk = size_t(2) << 20;
+    size_t w = warm_.load();
+    while (w < upto) {
+      const size_t len = std::min(chunk, cap_ * sizeof(T) - w);
+      char* base = reinterpret_cast<char*>(p_) + w;
+      if (madvise(base, len, MADV_POPULATE_WRITE) != 0) {
+        // kernels without MADV_POPULATE_WRITE: a no-op read-modify-write per page
+        for (size_t off = 0; off < len; off += 4096)
+          __atomic_fetch_or(reinterpret_cast<uint32_t*>(base + off), 0u, __ATOMIC_RELAXED);
+      }
+      w += len;
+      warm_.store(w);
+    }
+  }
+
+ private:
+  T* p_ = nullptr;
+  size_t cap_ = 0;
+  std::atomic<size_t> n_{0};
+  std::atomic<size_t> warm_{0};
 };
 
 struct Leaf {
@@ -127,19 +206,50 @@ struct Wave {
 
 using rag::Pool;
 
+inline void atomic_addf(float* p, float v) {
+  uint32_t* u = reinterpret_cast<uint32_t*>(p);
+  uint32_t old = __atomic_load_n(u, __ATOMIC_RELAXED), nw;
+  do {
+    float f;
+    std::memcpy(&f, &old, 4);
+    f += v;
+    std::memcpy(&nw, &f, 4);
+  } while (!__atomic_compare_exchange_n(u, &old, nw, true, __ATOMIC_RELAXED, __ATOMIC_RELAXED));
+}
+
+inline void atomic_max16(int16_t* p, int16_t v) {
+  int16_t cur = __atomic_load_n(p, __ATOMIC_RELAXED);
+  while (cur < v &&
+         !__atomic_compare_exchange_n(p, &cur, v, true, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
+  }
+}
+
 }  // namespace mcts_detail
 
+using mcts_detail::Edge;
 using mcts_detail::Leaf;
 using mcts_detail::Node;
-using mcts_detail::NodeArena;
 using mcts_detail::Wave;
 using mcts_detail::N_EXPANDED;
 using mcts_detail::N_NEW;
 using mcts_detail::N_PENDING;
 
-// Node pool capacity reserved up front: growth by reallocation copies the whole tree (tens of
-// MB per doubling) inside backup_value; the reservation is virtual until nodes are written.
-constexpr size_t kNodeReserve = size_t(1) << 23;
+// Reserved (virtual) capacities: 32 M nodes (1 GiB) and 128 M edges (1.5 GiB) — about 350 k
+// 19x19 simulations per move; pages become resident only as they are written.
+constexpr size_t kNodeCap = size_t(1) << 25;
+constexpr size_t kEdgeCap = size_t(1) << 27;
+
+// Output views of pack_inputs(): a null pointer skips that output; `stride` is the distance in
+// bytes between consecutive leaves (rows), so outputs may be columns of one record array.
+struct PackOut {
+  int8_t* colors = nullptr;    // [P]
+  int16_t* ages = nullptr;     // [P] stone ages (-1 empty, clamped to 32767)
+  int32_t* meta4 = nullptr;    // player, ko, superko flag, 0
+  int32_t* meta8 = nullptr;    // rollout kernel meta (see rollout_inputs)
+  uint8_t* illegal = nullptr;  // [P] positional-superko-illegal points (superko boards)
+  uint8_t* ladders = nullptr;  // [2][P] ladder capture / escape planes
+  size_t s_colors = 0, s_ages = 0, s_meta4 = 0, s_meta8 = 0, s_illegal = 0, s_ladders = 0;
+};
 
 class Search {
  public:
@@ -150,77 +260,190 @@ class Search {
   bool pass_prior = false;
   uint64_t seed = 1;
   std::shared_ptr<RolloutPolicy> rollout_policy;
+  // waves of at least this many leaves descend (and back up) on the pool; smaller ones run
+  // serially and deterministically
+  int parallel_select_min = 64;
+  static constexpr int kSorted = 32;
 
   explicit Search(const Board& root, int nthreads = 8)
-      : rollout_policy(std::make_shared<RolloutPolicy>()), pool_(std::max(nthreads, 1)) {
+      : rollout_policy(std::make_shared<RolloutPolicy>()),
+        nodes_(std::make_unique<mcts_detail::Arena<Node>>(kNodeCap)),
+        edges_(std::make_unique<mcts_detail::Arena<Edge>>(kEdgeCap)),
+        pool_(std::max(nthreads, 1)) {
     reset(root);
   }
-  ~Search() { drop_waves(); }
+  ~Search() {
+    drop_waves();
+    stop_prefault();
+  }
   Search(const Search&) = delete;
   Search& operator=(const Search&) = delete;
 
   void reset(const Board& root) {
     drop_waves();
     root_board_ = root;
-    nodes_.clear();
-    nodes_.reserve(kNodeReserve);
-    nodes_.push_back(Node{-1, -1, 0, (int16_t)PASS, 1.f, 0, 0, 0, 0.f, 0.f, N_NEW});
-    root_ = 0;
+    nodes_->clear();
+    edges_->clear();
+    root_ = new_node((int16_t)PASS);
+    clear_root_external();
+    prefault();
   }
 
   const Board& root_board() const { return root_board_; }
   int nthreads() const { return pool_.size(); }
 
   // ------------------------------------------------------------------ selection
-  // vl and state are changed by concurrent descents (descend_parallel): read them atomically
-  static int32_t vl_of(const Node& c) { return __atomic_load_n(&c.vl, __ATOMIC_RELAXED); }
-  static uint8_t state_of(const Node& c) { return __atomic_load_n(&c.state, __ATOMIC_RELAXED); }
+  // Shared statistics are changed by concurrent descents and backups: read them atomically.
+  template <class T>
+  static T ld(const T& x) {
+    return __atomic_load_n(&x, __ATOMIC_RELAXED);
+  }
+  static float ld(const float& x) {
+    float f;
+    __atomic_load(&x, &f, __ATOMIC_RELAXED);
+    return f;
+  }
+  static uint8_t state_of(const Node& c) { return __atomic_load_n(&c.state, __ATOMIC_ACQUIRE); }
 
-  float child_score(const Node& c, float sq) const {
-    const float vl = (float)(vl_of(c) * n_vl);
+  // PUCT score from explicit statistics (value visits / sum, rollouts / sum, in-flight descents)
+  float score(float n, float w, float nr, float wr, int vlc, float prior, float sq) const {
+    const float vl = (float)(vlc * n_vl);
     const bool use_r = lambda > 0.f;
     const bool use_v = lambda < 1.f;
     float q = 0.f;
     if (use_r && use_v) {
-      const float qv = c.n > 0 ? c.w / c.n : 0.f;
-      const float den = c.nr + vl;
-      const float qr = den > 0.f ? (c.wr - vl) / den : qv;
+      const float qv = n > 0.f ? w / n : 0.f;
+      const float den = nr + vl;
+      const float qr = den > 0.f ? (wr - vl) / den : qv;
       q = (1.f - lambda) * qv + lambda * qr;
     } else if (use_r) {
-      const float den = c.nr + vl;
-      q = den > 0.f ? (c.wr - vl) / den : 0.f;
+      const float den = nr + vl;
+      q = den > 0.f ? (wr - vl) / den : 0.f;
     } else {
-      const float den = c.n + vl;
-      q = den > 0.f ? (c.w - vl) / den : 0.f;
+      const float den = n + vl;
+      q = den > 0.f ? (w - vl) / den : 0.f;
     }
-    return q + c_puct * c.prior * sq / (1.f + (float)c.n + vl);
+    return q + c_puct * prior * sq / (1.f + n + vl);
+  }
+  float child_score(const Node& c, float prior, float sq) const {
+    return score((float)ld(c.n), ld(c.w), (float)ld(c.nr), ld(c.wr), ld(c.vl), prior, sq);
   }
 
-  int select_child(int p) const {
-    const Node& pn = nodes_[p];
-    const float np = (float)(pn.n + vl_of(pn) * n_vl);
+  // Edge index of the PUCT argmax at expanded node p (first maximum in edge order).
+  int select_edge(int p) const {
+    const Node& pn = (*nodes_)[p];
+    const int ne = pn.nedge;
+    const Edge* E = &(*edges_)[pn.edges];
+    if (p == root_ && has_ext_) return select_root_ext(pn, E, ne);
+    const float np = (float)(ld(pn.n) + ld(pn.vl) * n_vl);
     const float sq = std::sqrt(std::max(np, 1.f));
-    int best = pn.first;
+    // edges past the high-water mark have no node yet (unvisited): within the sorted prefix the
+    // first of them is the best of them all
+    const int h = ld(pn.hwm);
+    const int lim = h < std::min(ne, (int)kSorted) ? h + 1 : ne;
+    int best = 0;
     float bv = -1e30f;
-    for (int k = 0; k < pn.nchild; ++k) {
-      const float v = child_score(nodes_[pn.first + k], sq);
+    for (int k = 0; k < lim; ++k) {
+      const int32_t c = __atomic_load_n(&E[k].child, __ATOMIC_ACQUIRE);
+      const float v = c < 0 ? c_puct * E[k].prior * sq : child_score((*nodes_)[c], E[k].prior, sq);
       if (v > bv) {
         bv = v;
-        best = pn.first + k;
+        best = k;
       }
     }
     return best;
   }
 
+  // ------------------------------------------------------------------ shared root statistics
+  // Distributed search (search/distributed.py SharedRootMCTS): every rank grows its own tree
+  // from the same root, and the ranks exchange the statistics of the root's children each
+  // round. The other ranks' totals enter this rank's root selection as *external* statistics
+  // (indexed by move; PASS at P), so all ranks steer their descents by the job-wide root values
+  // and visit counts. root_deltas() reports what this rank added since its previous call.
+  void set_root_external(const float* n, const float* w, const float* nr, const float* wr) {
+    // written between waves (the search's own thread); sized once, updated in place
+    const int M = root_board_.npoints() + 1;
+    if (ext_.size() != 4 * (size_t)M) ext_.assign(4 * (size_t)M, 0.f);
+    ext_total_n_ = 0.f;
+    for (int m = 0; m < M; ++m) {
+      ext_[m] = n[m];
+      ext_[M + m] = w[m];
+      ext_[2 * M + m] = nr[m];
+      ext_[3 * M + m] = wr[m];
+      ext_total_n_ += n[m];
+    }
+    has_ext_ = true;
+  }
+  void clear_root_external() {
+    ext_.clear();
+    snap_.clear();
+    has_ext_ = false;
+    ext_total_n_ = 0.f;
+  }
+  // out: [4][P+1] (n, w, nr, wr) added by this rank at the root's children since the last call
+  void root_deltas(float* out) {
+    const int M = root_board_.npoints() + 1;
+    if (snap_.size() != 4 * (size_t)M) snap_.assign(4 * (size_t)M, 0.f);
+    std::fill(out, out + 4 * (size_t)M, 0.f);
+    const Node& r = (*nodes_)[root_];
+    if (ld(r.state) != N_EXPANDED) return;
+    const Edge* E = &(*edges_)[r.edges];
+    for (int k = 0; k < r.nedge; ++k) {
+      const int32_t c = __atomic_load_n(&E[k].child, __ATOMIC_ACQUIRE);
+      if (c < 0) continue;
+      const Node& nd = (*nodes_)[c];
+      const int m = E[k].move < 0 ? M - 1 : E[k].move;
+      const float cur[4] = {(float)ld(nd.n), ld(nd.w), (float)ld(nd.nr), ld(nd.wr)};
+      for (int j = 0; j < 4; ++j) {
+        out[j * M + m] = cur[j] - snap_[j * M + m];
+        snap_[j * M + m] = cur[j];
+      }
+    }
+  }
+
+ private:
+  int select_root_ext(const Node& pn, const Edge* E, int ne) const {
+    const int M = root_board_.npoints() + 1;
+    const float np = (float)(ld(pn.n) + ld(pn.vl) * n_vl) + ext_total_n_;
+    const float sq = std::sqrt(std::max(np, 1.f));
+    int best = 0;
+    float bv = -1e30f;
+    for (int k = 0; k < ne; ++k) {
+      const int m = E[k].move < 0 ? M - 1 : E[k].move;
+      float n = ext_[m], w = ext_[M + m], nr = ext_[2 * M + m], wr = ext_[3 * M + m];
+      int vl = 0;
+      const int32_t c = __atomic_load_n(&E[k].child, __ATOMIC_ACQUIRE);
+      if (c >= 0) {
+        const Node& nd = (*nodes_)[c];
+        n += (float)ld(nd.n);
+        w += ld(nd.w);
+        nr += (float)ld(nd.nr);
+        wr += ld(nd.wr);
+        vl = ld(nd.vl);
+      }
+      const float v = score(n, w, nr, wr, vl, E[k].prior, sq);
+      if (v > bv) {
+        bv = v;
+        best = k;
+      }
+    }
+    return best;
+  }
+
+ public:
   // Returns (wave id, number of leaves); id -1 when nothing was selected.
   //
   // Three phases: (1) tree walks with virtual loss (descend(); on the pool for B >=
-  // parallel_select_min, see descend_parallel); (2) the leaf boards (root copy + the path's moves) are built
-  // in parallel on the pool; (3) descents that ended on a terminal position are scored on their
-  // board and backed up at once (their virtual loss, taken in phase 1 so that later walks of the
-  // same wave avoid them, is dropped again).
+  // parallel_select_min, see descend_parallel); (2) the leaf boards (root copy + the path's
+  // moves) are built in parallel on the pool; (3) descents that ended on a terminal position are
+  // scored on their board and backed up at once (their virtual loss, taken in phase 1 so that
+  // later walks of the same wave avoid them, is dropped again).
   std::pair<int, int> select(int B) {
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
     collisions_ = 0;
+    if (!nodes_->room((size_t)4 * B + 16))
+      throw std::runtime_error("search tree full (node arena); advance() or reset()");
     std::vector<std::vector<int32_t>> paths;
     std::vector<uint8_t> term;
     paths.reserve(B);
@@ -233,7 +456,7 @@ class Search {
         ++attempts;
         std::vector<int32_t> path;
         bool terminal = false;
-        if (!descend(path, terminal, false)) {
+        if (!descend(path, terminal)) {
           ++collisions_;
           continue;
         }
@@ -242,6 +465,7 @@ class Search {
         term.push_back(terminal ? 1 : 0);
       }
     }
+    const auto t1 = clk::now();
     const Board& rb = root_board_;
     const int nd = (int)paths.size();
     int nleaf = 0;
@@ -260,7 +484,7 @@ class Search {
       b = rb;
       b.set_light(light);
       const std::vector<int32_t>& path = paths[i];
-      for (size_t d = 1; d < path.size(); ++d) b.play_unchecked(nodes_[path[d]].move);
+      for (size_t d = 1; d < path.size(); ++d) b.play_unchecked((*nodes_)[path[d]].move);
       if (!term[i]) {
         Leaf& L = wave->leaves[slot[i]];
         L.path.swap(paths[i]);
@@ -276,11 +500,16 @@ class Search {
       if (lambda > 0.f) backup_rollout_path(paths[i], v, false);
       ++terminal_;
     }
+    const auto t2 = clk::now();
+    t_descend_ += std::chrono::duration<double>(t1 - t0).count();
+    t_build_ += std::chrono::duration<double>(t2 - t1).count();
+    prefault();
     const int n = (int)wave->leaves.size();
     if (n == 0) {
       recycle(std::move(wave));
       return {-1, 0};
     }
+    std::lock_guard<std::mutex> g(wmu_);
     const int id = next_wave_++;
     waves_[id] = std::move(wave);
     return {id, n};
@@ -293,8 +522,6 @@ class Search {
   // virtual loss back and is counted as a collision. Which leaves a wave gets then depends on
   // thread timing; select(B) with B < parallel_select_min (or one thread) is the serial,
   // deterministic walk.
-  int parallel_select_min = 64;
-
   void descend_parallel(int B, std::vector<std::vector<int32_t>>& paths,
                         std::vector<uint8_t>& term) {
     std::atomic<int> nleaf{0}, attempts{0}, coll{0};
@@ -307,13 +534,13 @@ class Search {
              attempts.fetch_add(1, std::memory_order_relaxed) < 4 * B) {
         std::vector<int32_t> path;
         bool terminal = false;
-        if (!descend(path, terminal, true)) {
+        if (!descend(path, terminal)) {
           coll.fetch_add(1, std::memory_order_relaxed);
           continue;
         }
         if (!terminal && nleaf.fetch_add(1) >= B) {  // over-claimed: hand the leaf back
-          __atomic_store_n(&nodes_[path.back()].state, (uint8_t)N_NEW, __ATOMIC_RELAXED);
-          for (int id : path) __atomic_fetch_sub(&nodes_[id].vl, 1, __ATOMIC_RELAXED);
+          __atomic_store_n(&(*nodes_)[path.back()].state, (uint8_t)N_NEW, __ATOMIC_RELEASE);
+          for (int id : path) __atomic_fetch_sub(&(*nodes_)[id].vl, 1, __ATOMIC_RELAXED);
           break;
         }
         mine.push_back(std::move(path));
@@ -328,57 +555,51 @@ class Search {
     collisions_ = coll.load();
   }
 
-  // One walk from the root with virtual loss. Tracks only what the walk needs (player to move,
-  // the last two moves and the move count decide the end of the game, exactly as
-  // Board::play_unchecked does). Returns false (virtual loss already given back) when the walk
-  // ends on a leaf that another descent is waiting for; terminal = end of game / depth limit /
-  // a node without children (its virtual loss stays until its immediate backup).
-  bool descend(std::vector<int32_t>& path, bool& terminal, bool concurrent) {
+  // One walk from the root with virtual loss (atomic adds as the walk passes each node, so
+  // concurrent walks spread). Tracks only what the walk needs (player to move, the last two
+  // moves and the move count decide the end of the game, exactly as Board::play_unchecked
+  // does). Returns false (virtual loss already given back) when the walk ends on a leaf that
+  // another descent is waiting for; terminal = end of game / depth limit / a node without
+  // children (its virtual loss stays until its immediate backup).
+  bool descend(std::vector<int32_t>& path, bool& terminal) {
+    NodeArena& N = *nodes_;
     const Board& rb = root_board_;
     path.clear();
     path.reserve(32);
     int node = root_;
     path.push_back(node);
-    if (concurrent) __atomic_fetch_add(&nodes_[node].vl, 1, __ATOMIC_RELAXED);
+    __atomic_fetch_add(&N[node].vl, 1, __ATOMIC_RELAXED);
     int depth = 0;
     int ptm = rb.current_player(), l1 = rb.last1(), l2 = rb.last2(), nm = rb.nmoves();
     bool end = rb.end_of_game();
-    while (state_of(nodes_[node]) == N_EXPANDED && nodes_[node].nchild > 0 && !end &&
-           depth < max_depth) {
-      node = select_child(node);
+    while (state_of(N[node]) == N_EXPANDED && N[node].nedge > 0 && !end && depth < max_depth) {
+      node = child_of(node, select_edge(node));
       path.push_back(node);
-      if (concurrent) __atomic_fetch_add(&nodes_[node].vl, 1, __ATOMIC_RELAXED);
+      __atomic_fetch_add(&N[node].vl, 1, __ATOMIC_RELAXED);
       ++depth;
       ++nm;
       l2 = l1;
-      l1 = nodes_[node].move;
+      l1 = N[node].move;
       ptm = -ptm;
       if (nm > 1 && l1 == PASS && l2 == PASS && ptm == WHITE) end = true;
     }
-    Node& leaf = nodes_[node];
-    terminal = end || depth >= max_depth || (state_of(leaf) == N_EXPANDED && leaf.nchild == 0);
+    Node& leaf = N[node];
+    const uint8_t st = state_of(leaf);
+    terminal = end || depth >= max_depth || (st == N_EXPANDED && leaf.nedge == 0);
     if (!terminal) {
-      bool claimed;
-      if (concurrent) {
-        uint8_t expect = N_NEW;
-        claimed = __atomic_compare_exchange_n(&leaf.state, &expect, (uint8_t)N_PENDING, false,
-                                              __ATOMIC_RELAXED, __ATOMIC_RELAXED);
-      } else {
-        claimed = leaf.state != N_PENDING;
-        if (claimed) leaf.state = N_PENDING;
-      }
+      uint8_t expect = N_NEW;
+      const bool claimed = __atomic_compare_exchange_n(&leaf.state, &expect, (uint8_t)N_PENDING,
+                                                       false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE);
       if (!claimed) {  // already waiting for its evaluation
-        if (concurrent)
-          for (int id : path) __atomic_fetch_sub(&nodes_[id].vl, 1, __ATOMIC_RELAXED);
+        for (int id : path) __atomic_fetch_sub(&N[id].vl, 1, __ATOMIC_RELAXED);
         return false;
       }
     }
-    if (!concurrent)
-      for (int id : path) nodes_[id].vl += 1;
     return true;
   }
 
   Wave& wave(int id) {
+    std::lock_guard<std::mutex> g(wmu_);
     auto it = waves_.find(id);
     if (it == waves_.end()) throw std::invalid_argument("unknown or finished wave");
     return *it->second;
@@ -390,6 +611,50 @@ class Search {
     return v;
   }
 
+  // ------------------------------------------------------------------ leaf packing
+  // Everything the GPU side needs about a wave's leaves, written in parallel straight into the
+  // caller's (pinned) buffers: feature-kernel inputs, rollout-kernel meta and, optionally, the
+  // host-read ladder planes / superko-illegal masks.
+  void pack_inputs(int id, const PackOut& o) {
+    Wave& wv = wave(id);
+    const int n = (int)wv.leaves.size();
+    const int P = root_board_.npoints();
+    pool_.run(n, [&](int i) {
+      const Board& b = wv.leaves[i].board;
+      if (o.colors) {
+        int8_t* c = reinterpret_cast<int8_t*>(reinterpret_cast<char*>(o.colors) + i * o.s_colors);
+        for (int p = 0; p < P; ++p) c[p] = (int8_t)b.color(p);
+      }
+      if (o.ages) {
+        int16_t* a = reinterpret_cast<int16_t*>(reinterpret_cast<char*>(o.ages) + i * o.s_ages);
+        for (int p = 0; p < P; ++p) a[p] = (int16_t)std::min(b.stone_age(p), 32767);
+      }
+      if (o.meta4) {
+        int32_t* m = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(o.meta4) + i * o.s_meta4);
+        m[0] = b.current_player();
+        m[1] = b.ko();
+        m[2] = b.enforce_superko() ? 1 : 0;
+        m[3] = 0;
+      }
+      if (o.meta8) {
+        int32_t* m = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(o.meta8) + i * o.s_meta8);
+        write_meta8(b, m);
+      }
+      if (o.illegal) {
+        uint8_t* il = o.illegal + i * o.s_illegal;
+        for (int p = 0; p < P; ++p)
+          il[p] = (b.enforce_superko() && b.color(p) == EMPTY && p != b.ko() &&
+                   !b.is_suicide(p) && b.is_positional_superko(p))
+                      ? 1 : 0;
+      }
+      if (o.ladders) {
+        thread_local LadderReader reader;
+        uint8_t* l0 = o.ladders + i * o.s_ladders;
+        ladder_planes(b, l0, l0 + P, &reader);
+      }
+    });
+  }
+
   // ------------------------------------------------------------------ value backup
   // priors: [n][stride] network move probabilities (nullptr => uniform); values: [n] (nullptr
   // => value statistics untouched: rollouts only).
@@ -398,18 +663,21 @@ class Search {
   // are generated natively on the pool.
   void backup_value(int id, const float* priors, int stride, const float* values,
                     const uint8_t* sensible = nullptr) {
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
     Wave& wv = wave(id);
     if (wv.value_done) throw std::runtime_error("value backup twice");
     const int n = (int)wv.leaves.size();
     const int P = root_board_.npoints();
+    const bool par = n >= parallel_select_min && pool_.size() > 1;
     // pass 1 (parallel): children per leaf still to expand — the sensible-move mask's count, or
-    // natively generated moves; then one contiguous block for all of them (the leaves of one
-    // wave are distinct nodes: select() skips pending ones, so the blocks never overlap)
+    // natively generated moves; then one contiguous edge block for all of them (the leaves of
+    // one wave are distinct nodes: select() skips pending ones, so the blocks never overlap)
     std::vector<int32_t> cnt(n, -1);
     std::vector<std::vector<int>> moves(sensible ? 0 : n);
     pool_.run(n, [&](int i) {
       const Leaf& L = wv.leaves[i];
-      if (nodes_[L.path.back()].state == N_EXPANDED) return;
+      if (state_of((*nodes_)[L.path.back()]) == N_EXPANDED) return;
       int c = 0;
       if (sensible) {
         const uint8_t* m = sensible + (size_t)i * P;
@@ -422,44 +690,50 @@ class Search {
       cnt[i] = c;
     });
     const bool with_pass = pass_prior && priors != nullptr && stride > P;
-    std::vector<int32_t> first(n, -1);
-    size_t total = nodes_.size();
+    std::vector<int64_t> first(n, -1);
+    size_t total = 0;
     for (int i = 0; i < n; ++i) {
       if (cnt[i] < 0) continue;
-      first[i] = (int32_t)total;
+      first[i] = (int64_t)total;
       total += nchildren(cnt[i], with_pass);
     }
-    nodes_.resize(total);
-    // pass 2 (parallel): write the children into their block
-    pool_.run(n, [&](int i) {
-      if (first[i] < 0) return;
-      const int node = wv.leaves[i].path.back();
-      const float* pri = priors ? priors + (size_t)i * stride : nullptr;
-      if (sensible) {
-        const uint8_t* m = sensible + (size_t)i * P;
-        int k = 0;
-        fill_children(node, first[i], cnt[i], with_pass, pri, P, [&]() {
-          while (!m[k]) ++k;
-          return k++;
-        });
-      } else {
-        size_t k = 0;
-        fill_children(node, first[i], cnt[i], with_pass, pri, P,
-                      [&]() { return moves[i][k++]; });
-      }
-    });
-    for (int i = 0; i < n; ++i) {
+    if (!edges_->room(total))
+      throw std::runtime_error("search tree full (edge arena); advance() or reset()");
+    const size_t base = edges_->alloc(total);
+    // pass 2: write the edges, publish the expansion, back the value up the path
+    auto body = [&](int i) {
       Leaf& L = wv.leaves[i];
       if (first[i] >= 0) {
-        Node& nd = nodes_[L.path.back()];
-        nd.first = first[i];
-        nd.nchild = (int16_t)nchildren(cnt[i], with_pass);
-        nd.state = N_EXPANDED;
+        const float* pri = priors ? priors + (size_t)i * stride : nullptr;
+        const size_t e0 = base + (size_t)first[i];
+        if (sensible) {
+          const uint8_t* m = sensible + (size_t)i * P;
+          int k = 0;
+          fill_edges(e0, cnt[i], with_pass, pri, P, [&]() {
+            while (!m[k]) ++k;
+            return k++;
+          });
+        } else {
+          size_t k = 0;
+          fill_edges(e0, cnt[i], with_pass, pri, P, [&]() { return moves[i][k++]; });
+        }
+        Node& nd = (*nodes_)[L.path.back()];
+        nd.edges = (int32_t)e0;
+        nd.nedge = (int16_t)nchildren(cnt[i], with_pass);
+        nd.hwm = 0;
+        __atomic_store_n(&nd.state, (uint8_t)N_EXPANDED, __ATOMIC_RELEASE);
       }
       backup_value_path(L.path, values ? values[i] : 0.f, lambda <= 0.f);
+    };
+    if (par) {
+      pool_.run(n, body);
+    } else {
+      for (int i = 0; i < n; ++i) body(i);
     }
     wv.value_done = true;
     sims_ += n;
+    t_backup_ += std::chrono::duration<double>(clk::now() - t0).count();
+    prefault();
     if (lambda <= 0.f) finish(id);
   }
 
@@ -468,21 +742,23 @@ class Search {
   // (player to move, ko, last move, second-to-last move, black passes, white passes,
   // moves played, end-of-game flag).
   void rollout_inputs(int id, int8_t* colors, int32_t* meta) {
-    Wave& wv = wave(id);
+    PackOut o;
     const int P = root_board_.npoints();
-    for (size_t i = 0; i < wv.leaves.size(); ++i) {
-      const Board& b = wv.leaves[i].board;
-      for (int p = 0; p < P; ++p) colors[i * P + p] = (int8_t)b.color(p);
-      int32_t* m = meta + i * 8;
-      m[0] = b.current_player();
-      m[1] = b.ko();
-      m[2] = b.last1();
-      m[3] = b.last2();
-      m[4] = b.passes_black();
-      m[5] = b.passes_white();
-      m[6] = b.nmoves();
-      m[7] = b.end_of_game() ? 1 : 0;
-    }
+    o.colors = colors;
+    o.s_colors = P;
+    o.meta8 = meta;
+    o.s_meta8 = 8 * sizeof(int32_t);
+    pack_inputs(id, o);
+  }
+  static void write_meta8(const Board& b, int32_t* m) {
+    m[0] = b.current_player();
+    m[1] = b.ko();
+    m[2] = b.last1();
+    m[3] = b.last2();
+    m[4] = b.passes_black();
+    m[5] = b.passes_white();
+    m[6] = b.nmoves();
+    m[7] = b.end_of_game() ? 1 : 0;
   }
 
   // black_z: mean rollout result per leaf from BLACK's point of view
@@ -493,13 +769,19 @@ class Search {
       wv.worker.join();
       wv.rolling = false;
     }
-    for (size_t i = 0; i < wv.leaves.size(); ++i) {
+    const int n = (int)wv.leaves.size();
+    auto body = [&](int i) {
       Leaf& L = wv.leaves[i];
       float z = L.z;
       if (black_z) z = L.board.current_player() == BLACK ? black_z[i] : -black_z[i];
       backup_rollout_path(L.path, z, true);
+    };
+    if (n >= parallel_select_min && pool_.size() > 1) {
+      pool_.run(n, body);
+    } else {
+      for (int i = 0; i < n; ++i) body(i);
     }
-    rollouts_ += (long)wv.leaves.size();
+    rollouts_ += (long)n;
     release(id);
   }
 
@@ -527,7 +809,10 @@ class Search {
 
   void finish_rollouts(int id) { backup_rollout(id, nullptr); }
 
-  int pending_waves() const { return (int)waves_.size(); }
+  int pending_waves() const {
+    std::lock_guard<std::mutex> g(wmu_);
+    return (int)waves_.size();
+  }
 
   // ------------------------------------------------------------------ results / tree reuse
   float node_q(const Node& c) const {
@@ -539,42 +824,62 @@ class Search {
   }
 
   int best_move() const {
-    const Node& r = nodes_[root_];
-    if (r.state != N_EXPANDED || r.nchild == 0) return PASS;
-    int best = r.first;
-    for (int k = 1; k < r.nchild; ++k)
-      if (nodes_[r.first + k].n > nodes_[best].n) best = r.first + k;
-    return nodes_[best].move;
+    const Node& r = (*nodes_)[root_];
+    if (r.state != N_EXPANDED || r.nedge == 0) return PASS;
+    const Edge* E = &(*edges_)[r.edges];
+    int best = 0, bn = -1;
+    for (int k = 0; k < r.nedge; ++k) {
+      const int v = E[k].child >= 0 ? (*nodes_)[E[k].child].n : 0;
+      // most visits; ties to the lower point (pass last) whatever the edge order
+      if (v > bn || (v == bn && move_key(E[k].move) < move_key(E[best].move))) {
+        bn = v;
+        best = k;
+      }
+    }
+    return E[best].move;
   }
 
-  // (moves, visits, Q, prior) of the root's children
+  // (moves, visits, Q, prior) of the root's children, in increasing point order (pass last)
   void root_stats(std::vector<int32_t>& mv, std::vector<int32_t>& vis, std::vector<float>& q,
                   std::vector<float>& pr) const {
-    const Node& r = nodes_[root_];
-    const int nc = r.state == N_EXPANDED ? r.nchild : 0;
+    const Node& r = (*nodes_)[root_];
+    const int nc = r.state == N_EXPANDED ? r.nedge : 0;
+    std::vector<int> order(nc);
+    for (int k = 0; k < nc; ++k) order[k] = k;
+    const Edge* E = nc ? &(*edges_)[r.edges] : nullptr;
+    std::sort(order.begin(), order.end(),
+              [&](int a, int b) { return move_key(E[a].move) < move_key(E[b].move); });
     mv.resize(nc);
     vis.resize(nc);
     q.resize(nc);
     pr.resize(nc);
-    for (int k = 0; k < nc; ++k) {
-      const Node& c = nodes_[r.first + k];
-      mv[k] = c.move;
-      vis[k] = c.n;
-      q[k] = node_q(c);
-      pr[k] = c.prior;
+    for (int j = 0; j < nc; ++j) {
+      const Edge& e = E[order[j]];
+      mv[j] = e.move;
+      pr[j] = e.prior;
+      if (e.child >= 0) {
+        const Node& c = (*nodes_)[e.child];
+        vis[j] = c.n;
+        q[j] = node_q(c);
+      } else {
+        vis[j] = 0;
+        q[j] = 0.f;
+      }
     }
   }
 
   // Re-root at the child reached by `move` (played on the root board). All waves must have
   // been finished. Returns true when the subtree was kept.
   bool advance(int move) {
-    if (!waves_.empty()) throw std::runtime_error("advance() with waves in flight");
+    if (pending_waves()) throw std::runtime_error("advance() with waves in flight");
     root_board_.do_move(move, 0);
-    const Node& r = nodes_[root_];
+    const Node& r = (*nodes_)[root_];
     int child = -1;
     if (r.state == N_EXPANDED)
-      for (int k = 0; k < r.nchild; ++k)
-        if (nodes_[r.first + k].move == move) child = r.first + k;
+      for (int k = 0; k < r.nedge; ++k) {
+        const Edge& e = (*edges_)[r.edges + k];
+        if (e.move == move) child = e.child;
+      }
     if (child < 0) {
       Board b = root_board_;
       reset(b);
@@ -588,10 +893,40 @@ class Search {
   long rollouts() const { return rollouts_; }
   long terminal() const { return terminal_; }
   int collisions() const { return collisions_; }
-  size_t num_nodes() const { return nodes_.size(); }
-  int root_visits() const { return nodes_[root_].n; }
+  size_t num_nodes() const { return nodes_->size(); }
+  size_t num_edges() const { return edges_->size(); }
+  int root_visits() const { return (*nodes_)[root_].n; }
+  // accumulated host seconds: descents, leaf-board construction, value backups
+  std::tuple<double, double, double> timers() const { return {t_descend_, t_build_, t_backup_}; }
 
  private:
+  using NodeArena = mcts_detail::Arena<Node>;
+
+  static int move_key(int m) { return m < 0 ? (1 << 20) : m; }
+
+  int new_node(int16_t move) {
+    const int idx = (int)nodes_->alloc(1);
+    (*nodes_)[idx] = Node{-1, 0, move, 0, 0, 0, 0.f, 0.f, 0, N_NEW, 0};
+    return idx;
+  }
+
+  // Child node of edge k of p, allocated on first selection. Concurrent first selections race on
+  // the edge's child slot; the loser's node stays unused.
+  int child_of(int p, int k) {
+    Node& pn = (*nodes_)[p];
+    Edge& e = (*edges_)[pn.edges + k];
+    int32_t c = __atomic_load_n(&e.child, __ATOMIC_ACQUIRE);
+    if (c >= 0) return c;
+    const int idx = new_node(e.move);
+    // the mark first: a descent that sees the child also sees the edge inside the mark
+    mcts_detail::atomic_max16(&pn.hwm, (int16_t)(k + 1));
+    int32_t expect = -1;
+    if (__atomic_compare_exchange_n(&e.child, &expect, idx, false, __ATOMIC_ACQ_REL,
+                                    __ATOMIC_ACQUIRE))
+      return idx;
+    return expect;
+  }
+
   void finish(int id) {
     Wave& wv = wave(id);
     if (wv.rolling) {
@@ -604,6 +939,7 @@ class Search {
   // finished waves are kept (up to a few) and handed out again by select(): their leaf boards
   // and paths keep their storage, so a new wave touches no fresh memory
   std::unique_ptr<Wave> take_wave() {
+    std::lock_guard<std::mutex> g(wmu_);
     if (free_waves_.empty()) return std::make_unique<Wave>();
     std::unique_ptr<Wave> w = std::move(free_waves_.back());
     free_waves_.pop_back();
@@ -612,17 +948,23 @@ class Search {
   void recycle(std::unique_ptr<Wave> w) {
     w->value_done = false;
     w->rolling = false;
+    std::lock_guard<std::mutex> g(wmu_);
     if (free_waves_.size() < 16) free_waves_.push_back(std::move(w));
   }
   void release(int id) {
-    auto it = waves_.find(id);
-    if (it == waves_.end()) return;
-    std::unique_ptr<Wave> w = std::move(it->second);
-    waves_.erase(it);
+    std::unique_ptr<Wave> w;
+    {
+      std::lock_guard<std::mutex> g(wmu_);
+      auto it = waves_.find(id);
+      if (it == waves_.end()) return;
+      w = std::move(it->second);
+      waves_.erase(it);
+    }
     recycle(std::move(w));
   }
 
   void drop_waves() {
+    std::lock_guard<std::mutex> g(wmu_);
     for (auto& kv : waves_)
       if (kv.second->rolling) kv.second->worker.join();
     waves_.clear();
@@ -632,14 +974,14 @@ class Search {
     return with_pass ? count + 1 : (count == 0 ? 1 : count);
   }
 
-  // children of `node` for its `count` sensible moves (PASS alone when there are none; PASS
-  // always, last, with the network's pass prior pri[P] when `with_pass`), moves in increasing
-  // point order from `next_move()`, priors renormalised over them, written into the
-  // preallocated slots [first, first + nchildren(count, with_pass))
+  // edges of a leaf for its `count` sensible moves (PASS alone when there are none; PASS always,
+  // with the network's pass prior pri[P], when `with_pass`), moves from `next_move()`, priors
+  // renormalised over them; the kSorted highest priors first, in descending order (ties: lower
+  // point first, pass last)
   template <class F>
-  void fill_children(int node, int first, int count, bool with_pass, const float* pri, int P,
-                     F&& next_move) {
+  void fill_edges(size_t e0, int count, bool with_pass, const float* pri, int P, F&& next_move) {
     const int nc = nchildren(count, with_pass);
+    Edge* E = &(*edges_)[e0];
     float tot = 0.f;
     for (int k = 0; k < nc; ++k) {
       const int mv = k < count ? next_move() : PASS;
@@ -647,12 +989,14 @@ class Search {
       if (pri && mv != PASS) p = std::max(pri[mv], 0.f);
       if (pri && mv == PASS && with_pass) p = std::max(pri[P], 0.f);
       tot += p;
-      nodes_[first + k] = Node{node, -1, 0, (int16_t)mv, p, 0, 0, 0, 0.f, 0.f, N_NEW};
+      E[k] = Edge{-1, p, (int16_t)mv, 0};
     }
-    for (int k = 0; k < nc; ++k) {
-      Node& c = nodes_[first + k];
-      c.prior = tot > 0.f ? c.prior / tot : 1.f / nc;
-    }
+    for (int k = 0; k < nc; ++k) E[k].prior = tot > 0.f ? E[k].prior / tot : 1.f / nc;
+    auto before = [](const Edge& a, const Edge& b) {
+      return a.prior > b.prior || (a.prior == b.prior && move_key(a.move) < move_key(b.move));
+    };
+    if (nc > kSorted) std::nth_element(E, E + kSorted, E + nc, before);
+    std::sort(E, E + std::min(nc, (int)kSorted), before);
   }
 
   // v: value for the player to move at the leaf; a node at depth d stores it for its mover,
@@ -660,64 +1004,145 @@ class Search {
   void backup_value_path(const std::vector<int32_t>& path, float v, bool drop_vl) {
     const int D = (int)path.size() - 1;
     for (int d = D; d >= 0; --d) {
-      Node& nd = nodes_[path[d]];
-      nd.n += 1;
-      if (drop_vl) nd.vl -= 1;
-      nd.w += ((D - d) & 1) ? v : -v;
+      Node& nd = (*nodes_)[path[d]];
+      __atomic_fetch_add(&nd.n, 1, __ATOMIC_RELAXED);
+      if (drop_vl) __atomic_fetch_sub(&nd.vl, 1, __ATOMIC_RELAXED);
+      mcts_detail::atomic_addf(&nd.w, ((D - d) & 1) ? v : -v);
     }
   }
   void backup_rollout_path(const std::vector<int32_t>& path, float z, bool drop_vl) {
     const int D = (int)path.size() - 1;
     for (int d = D; d >= 0; --d) {
-      Node& nd = nodes_[path[d]];
-      nd.nr += 1;
-      if (drop_vl) nd.vl -= 1;
-      nd.wr += ((D - d) & 1) ? z : -z;
+      Node& nd = (*nodes_)[path[d]];
+      __atomic_fetch_add(&nd.nr, 1, __ATOMIC_RELAXED);
+      if (drop_vl) __atomic_fetch_sub(&nd.vl, 1, __ATOMIC_RELAXED);
+      mcts_detail::atomic_addf(&nd.wr, ((D - d) & 1) ? z : -z);
     }
   }
 
-  // copy the subtree under `keep` into a fresh pool (BFS keeps children contiguous)
+  // copy the subtree under `keep` into fresh (recycled) arenas; children of a node keep their
+  // edge order, nodes are renumbered breadth-first
   void compact(int keep) {
-    NodeArena out;
-    out.reserve(std::max<size_t>(nodes_.capacity(), kNodeReserve));
-    std::vector<int32_t> q{keep};
-    Node r = nodes_[keep];
-    r.parent = -1;
-    r.vl = 0;
-    if (r.state == N_PENDING) r.state = N_NEW;
-    out.push_back(r);
-    std::vector<int32_t> newid{0};
+    auto nn = std::make_unique<mcts_detail::Arena<Node>>(kNodeCap);
+    auto ne = std::make_unique<mcts_detail::Arena<Edge>>(kEdgeCap);
+    std::vector<std::pair<int32_t, int32_t>> q;  // (old, new)
+    auto copy_node = [&](int old) {
+      const int nid = (int)nn->alloc(1);
+      Node c = (*nodes_)[old];
+      c.vl = 0;
+      if (c.state == N_PENDING) c.state = N_NEW;
+      (*nn)[nid] = c;
+      q.emplace_back(old, nid);
+      return nid;
+    };
+    copy_node(keep);
     for (size_t h = 0; h < q.size(); ++h) {
-      const Node& old = nodes_[q[h]];
-      const int nid = newid[h];
-      if (old.state != N_EXPANDED || old.nchild == 0) continue;
-      const int first = (int)out.size();
-      for (int k = 0; k < old.nchild; ++k) {
-        Node c = nodes_[old.first + k];
-        c.parent = nid;
-        c.vl = 0;
-        if (c.state == N_PENDING) c.state = N_NEW;
-        out.push_back(c);
-        q.push_back(old.first + k);
-        newid.push_back(first + k);
+      const int old = q[h].first, nid = q[h].second;
+      const Node o = (*nodes_)[old];
+      if (o.state != N_EXPANDED || o.nedge == 0) continue;
+      const size_t e0 = ne->alloc(o.nedge);
+      (*nn)[nid].edges = (int32_t)e0;
+      for (int k = 0; k < o.nedge; ++k) {
+        Edge e = (*edges_)[o.edges + k];
+        if (e.child >= 0) e.child = copy_node(e.child);
+        (*ne)[e0 + k] = e;
       }
-      out[nid].first = first;
     }
-    nodes_.swap(out);
+    quiesce_prefault();  // the helper must not be inside the arenas that leave
+    nodes_.swap(nn);
+    edges_.swap(ne);
     root_ = 0;
+    clear_root_external();  // the exchanged statistics were about the old root's children
+    prefault();
+  }
+
+  // ------------------------------------------------------------------ page prefaulting
+  // The helper thread keeps the pages just past each arena's allocation frontier resident.
+  void prefault() {
+    const size_t want_n = nodes_->bytes_used() + (size_t(8) << 20);
+    const size_t want_e = edges_->bytes_used() + (size_t(48) << 20);
+    if (nodes_->warm_bytes() >= want_n && edges_->warm_bytes() >= want_e) return;
+    {
+      std::lock_guard<std::mutex> g(pf_mu_);
+      pf_nodes_ = nodes_.get();
+      pf_edges_ = edges_.get();
+      pf_want_n_ = want_n;
+      pf_want_e_ = want_e;
+      ++pf_gen_;
+      if (!pf_thread_.joinable()) pf_thread_ = std::thread([this] { prefault_loop(); });
+    }
+    pf_cv_.notify_one();
+  }
+  void prefault_loop() {
+    uint64_t seen = 0;
+    while (true) {
+      mcts_detail::Arena<Node>* an;
+      mcts_detail::Arena<Edge>* ae;
+      size_t wn, we;
+      {
+        std::unique_lock<std::mutex> lk(pf_mu_);
+        pf_cv_.wait(lk, [&] { return pf_gen_ != seen || pf_stop_; });
+        if (pf_stop_) return;
+        seen = pf_gen_;
+        an = pf_nodes_;
+        ae = pf_edges_;
+        wn = pf_want_n_;
+        we = pf_want_e_;
+        pf_busy_ = true;
+      }
+      if (an) an->populate(wn);
+      if (ae) ae->populate(we);
+      {
+        std::lock_guard<std::mutex> g(pf_mu_);
+        pf_busy_ = false;
+      }
+      pf_done_cv_.notify_all();
+    }
+  }
+  // Arenas leave the search (compaction swaps, destruction) only when the helper is idle.
+  void quiesce_prefault() {
+    std::unique_lock<std::mutex> lk(pf_mu_);
+    pf_done_cv_.wait(lk, [&] { return !pf_busy_; });
+    pf_nodes_ = nullptr;
+    pf_edges_ = nullptr;
+  }
+  void stop_prefault() {
+    {
+      std::lock_guard<std::mutex> g(pf_mu_);
+      pf_stop_ = true;
+    }
+    pf_cv_.notify_all();
+    if (pf_thread_.joinable()) pf_thread_.join();
   }
 
   Board root_board_;
-  NodeArena nodes_;
+  std::unique_ptr<mcts_detail::Arena<Node>> nodes_;
+  std::unique_ptr<mcts_detail::Arena<Edge>> edges_;
   int root_ = 0;
+  // waves_ / free_waves_ / next_wave_: select() may run on one host thread while another backs
+  // an earlier wave up (the pipelined search); the tree itself is updated atomically
+  mutable std::mutex wmu_;
   std::map<int, std::unique_ptr<Wave>> waves_;
   std::vector<std::unique_ptr<Wave>> free_waves_;
   int next_wave_ = 0;
-  Pool pool_;                    // expansions
+  Pool pool_;                    // descents, leaf boards, expansions, backups
   std::unique_ptr<Pool> rpool_;  // CPU rollouts (run from a wave's worker thread)
   long sims_ = 0, rollouts_ = 0, terminal_ = 0;
   int collisions_ = 0;
-};
+  double t_descend_ = 0, t_build_ = 0, t_backup_ = 0;
+  // external root statistics [4][P+1] (other ranks), this rank's last reported root totals
+  std::vector<float> ext_, snap_;
+  float ext_total_n_ = 0.f;
+  bool has_ext_ = false;
 
+  std::thread pf_thread_;
+  std::mutex pf_mu_;
+  std::condition_variable pf_cv_, pf_done_cv_;
+  mcts_detail::Arena<Node>* pf_nodes_ = nullptr;
+  mcts_detail::Arena<Edge>* pf_edges_ = nullptr;
+  size_t pf_want_n_ = 0, pf_want_e_ = 0;
+  uint64_t pf_gen_ = 0;
+  bool pf_busy_ = false, pf_stop_ = false;
+};
 
 }  // namespace rag

@@ -107,7 +107,9 @@ class _TrunkPlan(object):
         self.trunk.sync_weights(Ws, bs, self.net.weights_version())
         if x.dtype not in (torch.uint8, torch.float32, torch.int64):
             x = x.float()
-        ops.pack_input(x.contiguous(), self.trunk.input_buffer(B), self.trunk.halo[0],
+        # planes beyond the first conv's inputs (e.g. the value net's colour plane in the search's
+        # shared input) are skipped in place by the packer
+        ops.pack_input(x, self.trunk.input_buffer(B), self.trunk.halo[0],
                        index=index, transforms=transforms, nplanes=self.trunk.specs[0].cin)
         return B
 
@@ -137,12 +139,15 @@ class PolicyPlan(_TrunkPlan):
     def _pass_params(self):
         return self.net.params_of(self.pass_name) if self.pass_name else None
 
-    def forward(self, x, index=None, transforms=None):
+    def forward(self, x, index=None, transforms=None, clone=True):
+        """Move probabilities [B, S*S (+1)]. clone=False returns the head's own output buffer
+        (valid until the next forward of this plan; the search copies it to the host at once)."""
         B = self.prepare(x, index, transforms)
         self.trunk.forward(B)
         w, b0 = self.head_params()
         pb = self.net.params_of(self.bias_name)[0]
-        return self.head.forward(B, w, b0, pb, pass_params=self._pass_params()).clone()
+        out = self.head.forward(B, w, b0, pb, pass_params=self._pass_params())
+        return out.clone() if clone else out
 
     @staticmethod
     def loss_mode(loss):

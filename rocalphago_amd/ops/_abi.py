@@ -16,8 +16,8 @@ SIGNATURES = {
     "rag_wgrad_flush": [P],
     "rag_pack_weights": [P, P, P, I, I, I, I, I, P],
     "rag_pack_trunk": [P, I, I64, P],
-    "rag_pack_input_u8": [P, P, P, P, I, I, I, I, I, P],
-    "rag_pack_input_f32": [P, P, P, P, I, I, I, I, I, P],
+    "rag_pack_input_u8": [P, P, P, P, I, I, I, I, I, I, P],
+    "rag_pack_input_f32": [P, P, P, P, I, I, I, I, I, I, P],
     "rag_pack_input_bits": [P, P, P, P, I, I, I, I, I, P],
     "rag_unpack": [P, P, I, I, I, I, I, P],
     "rag_pack_nchw": [P, P, I, I, I, I, I, P],

@@ -79,6 +79,18 @@ class GpuFeatures(object):
         colors, ages, meta, illegal, lad = _rg.gpu_feature_inputs(boards, host, self.nthreads)
         return self.from_arrays(colors, ages, meta, illegal, lad, out, sens_out)
 
+    def run(self, c, a, m, il, ld, n, S, out=None):
+        """Planes from device inputs (colours [n, S*S] int8, ages int16, meta [n, 4] int32,
+        superko-illegal mask or None, ladder planes [n, 2, S*S] or None: read on the GPU)."""
+        if self.ladders and ld is None:
+            ld, self._work = gpu_ladders(c, m, S, work=self._work)
+        if out is None:
+            out = torch.empty((n, self.F, S, S), dtype=torch.uint8, device=self.device)
+        _check(_lib().rag_features(_ptr(c), _ptr(a), _ptr(m), _ptr(il), _ptr(ld), n, S,
+                                   _ptr(self.fids_dev), len(self.fids), self.F, _ptr(out),
+                                   _stream()), "features")
+        return out
+
     def from_arrays(self, colors, ages, meta, illegal, lad, out=None, sens_out=None):
         """Planes from the native inputs directly: colours [n, S*S] int8, stone ages int16,
         meta [n, 4] int32 (player, ko, superko flag, 0), the superko-illegal mask (or None) and
@@ -89,13 +101,7 @@ class GpuFeatures(object):
         if illegal is not None and not np.any(illegal):
             illegal = None
         c, a, m, il, ld = (_h2d(x, self.device) for x in (colors, ages, meta, illegal, lad))
-        if self.ladders and ld is None:
-            ld, self._work = gpu_ladders(c, m, S, work=self._work)
-        if out is None:
-            out = torch.empty((n, self.F, S, S), dtype=torch.uint8, device=self.device)
-        _check(_lib().rag_features(_ptr(c), _ptr(a), _ptr(m), _ptr(il), _ptr(ld), n, S,
-                                   _ptr(self.fids_dev), len(self.fids), self.F, _ptr(out),
-                                   _stream()), "features")
+        out = self.run(c, a, m, il, ld, n, S, out)
         if sens_out is not None:
             if sens_out.numel() != n * S * S or sens_out.dtype != torch.uint8:
                 raise ValueError("sens_out must be uint8 with n*S*S elements")

@@ -168,9 +168,10 @@ def wgrad_flush():
 
 
 def pack_input(features, out, H, index=None, transforms=None, nplanes=None):
-    """[N, F, S, S] uint8/float32 planes, or bit-packed int64 words [N, S, S] with ``nplanes``
-    (training/replay.py), optionally gathered by ``index`` [B] and dihedral-transformed by
-    ``transforms`` [B] int32 -> padded bf16 ``out`` [B, S+2H, S+2H, CP]."""
+    """[N, F, S, S] uint8/float32 planes (the first ``nplanes`` of them when given), or
+    bit-packed int64 words [N, S, S] with ``nplanes`` (training/replay.py), optionally gathered
+    by ``index`` [B] and dihedral-transformed by ``transforms`` [B] int32 -> padded bf16 ``out``
+    [B, S+2H, S+2H, CP]."""
     B = out.shape[0]
     S = features.shape[-1]
     CP = out.shape[-1]
@@ -181,11 +182,14 @@ def pack_input(features, out, H, index=None, transforms=None, nplanes=None):
                                           _ptr(out), B, int(nplanes), S, H, CP, _stream()),
                "pack_input_bits")
         return out
-    NF = features.shape[1]
-    fn = _lib().rag_pack_input_u8 if features.dtype == torch.uint8 else _lib().rag_pack_input_f32
+    FS = features.shape[1]  # planes per position in the source
+    NF = FS if nplanes is None else min(FS, int(nplanes))  # planes packed
     if features.dtype not in (torch.uint8, torch.float32):
         features = features.float()
-    _check(fn(_ptr(features), _ptr(index), _ptr(transforms), _ptr(out), B, NF, S, H, CP,
+    if not features.is_contiguous():
+        features = features.contiguous()
+    fn = _lib().rag_pack_input_u8 if features.dtype == torch.uint8 else _lib().rag_pack_input_f32
+    _check(fn(_ptr(features), _ptr(index), _ptr(transforms), _ptr(out), B, NF, FS, S, H, CP,
               _stream()), "pack_input")
     return out
 

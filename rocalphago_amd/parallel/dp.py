@@ -46,6 +46,7 @@ class DPContext(object):
             dist.init_process_group(backend=backend,
                                     timeout=datetime.timedelta(seconds=timeout_s), **kw)
         self.is_root = self.rank == 0
+        self.backend = dist.get_backend() if self.enabled else None
 
     def broadcast_(self, t, src=0):
         if self.enabled:

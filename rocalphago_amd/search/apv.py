@@ -31,6 +31,38 @@ from ..features.preprocessing import _FID
 _rg = _engine()
 
 
+class _nullctx(object):
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False
+
+
+class _Slots(object):
+    """Round-robin pool of _Slot buffers for the pipelined search (at most ``depth`` waves in
+    flight; a slot is handed out again only after its previous wave was backed up)."""
+
+    def __init__(self, device, depth):
+        self.device = device
+        self.depth = max(1, int(depth))
+        self.pool = []
+        self.next = 0
+
+    def take(self, n, S, F, PW, host_ladders, cap=0):
+        if self.pool and (self.pool[0].B < n or self.pool[0].S != S or
+                          self.pool[0].planes.shape[1] != F or
+                          self.pool[0].o_pri.shape[1] != PW or
+                          ("ladders" in self.pool[0].h) != host_ladders):
+            self.pool = []
+        if len(self.pool) < self.depth:
+            self.pool.append(_Slot(max(n, cap, 64), S, F, PW, self.device, host_ladders))
+            return self.pool[-1]
+        s = self.pool[self.next % len(self.pool)]
+        self.next += 1
+        return s
+
+
 class _Ready(object):
     """An evaluation that finished synchronously."""
 
@@ -62,6 +94,59 @@ class _Pending(object):
     def result(self):
         self.event.synchronize()
         return tuple(None if h is None else h.numpy() for h in self.host)
+
+
+class _Slot(object):
+    """Pinned host staging and device buffers of one in-flight wave (up to ``B`` leaves):
+    the native search packs the leaves straight into the pinned inputs (Search.pack_inputs),
+    the GPU pass copies them in, builds the planes, runs both networks and copies priors,
+    values and sensible masks back into the pinned outputs. Reused round-robin: a slot is
+    recycled only after its wave's backup read the outputs."""
+
+    def __init__(self, B, S, F, PW, device, host_ladders):
+        P = S * S
+
+        def pin(shape, dt):
+            return torch.empty(shape, dtype=dt, pin_memory=True)
+
+        def dev(t):
+            return torch.empty(t.shape, dtype=t.dtype, device=device)
+
+        self.B, self.S, self.P = B, S, P
+        self.h = {"colors": pin((B, P), torch.int8), "ages": pin((B, P), torch.int16),
+                  "meta4": pin((B, 4), torch.int32)}
+        if host_ladders:
+            self.h["ladders"] = pin((B, 2, P), torch.uint8)
+        self.d = {k: dev(v) for k, v in self.h.items()}
+        self.n = {k: v.numpy() for k, v in self.h.items()}
+        self.h_ill = self.d_ill = None
+        self.planes = torch.empty((B, F, S, S), dtype=torch.uint8, device=device)
+        self.o_pri = pin((B, PW), torch.float32)
+        self.o_val = pin((B,), torch.float32)
+        self.o_sens = pin((B, P), torch.uint8)
+        self.event = torch.cuda.Event()
+
+    def illegal(self, device):
+        if self.h_ill is None:
+            self.h_ill = torch.empty((self.B, self.P), dtype=torch.uint8, pin_memory=True)
+            self.d_ill = torch.empty((self.B, self.P), dtype=torch.uint8, device=device)
+        return self.h_ill.numpy()
+
+
+class _SlotResult(object):
+    """Handle of a wave evaluated into a slot: result() waits for the slot's event and returns
+    numpy views of its pinned outputs (priors, values, sensible)."""
+
+    def __init__(self, slot, n, has_pri, has_val, has_sens):
+        self.slot, self.n = slot, n
+        self.flags = (has_pri, has_val, has_sens)
+
+    def result(self):
+        s, n = self.slot, self.n
+        s.event.synchronize()
+        return (s.o_pri[:n].numpy() if self.flags[0] else None,
+                s.o_val[:n].numpy() if self.flags[1] else None,
+                s.o_sens[:n].numpy() if self.flags[2] else None)
 
 
 class NetworkEvaluator(object):
@@ -141,6 +226,111 @@ class NetworkEvaluator(object):
         ev = torch.cuda.Event()
         ev.record()
         return _Pending(ev, *host)
+
+    # ------------------------------------------------------------------ packed wave path
+    def wave_capable(self, S):
+        """True when submit_wave() can evaluate waves of board size S: fused HIP plans for every
+        network, one shared GPU feature extractor (the value planes extend the policy planes, or
+        a single network) and the sensibleness plane among the features."""
+        plans = self._plans()
+        return (plans is not None and self.gpu is not None and "v" not in self.gpu and
+                self.gpu["p"].supports(S) and self._sens_off is not None)
+
+    def submit_wave(self, search, wid, n, slots, cap=0):
+        """Evaluate wave ``wid`` of the native search through a pinned slot (see _Slot): the
+        leaves are packed natively into pinned memory (host ladder reads on the search pool),
+        then copies in, feature kernel, both networks and copies out are queued on the current
+        stream (a captured HIP graph for full waves, RAG_EVAL_GRAPH=1). Returns a handle whose
+        result() gives numpy (priors, values, sensible)."""
+        S = search.root_board.size
+        gf = self.gpu["p"]
+        superko = bool(search.root_board.enforce_superko)
+        host_lad = gf.ladders and (gf.ladder_device == "host" or superko)
+        slot = slots.take(n, S, gf.F, self._pw(S), host_lad, cap)
+        nv = slot.n
+        search.pack_inputs(wid, colors=nv["colors"], ages=nv["ages"], meta4=nv["meta4"],
+                           ladders=nv.get("ladders") if host_lad else None,
+                           illegal=slot.illegal(gf.device) if superko else None)
+        if superko and not slot.n["meta4"][:n, 2].any():
+            superko = False
+        ppol, pval = self._plans()
+        key = (n, S, superko, host_lad)
+        if (os.environ.get("RAG_EVAL_GRAPH", "0") == "1" and n == slot.B and
+                self._graph_ok(slot, key)):
+            for plan in (ppol, pval):
+                if plan is not None:
+                    plan.sync_weights()
+            slot.graphs[key][0].replay()
+        else:
+            self._slot_pass(slot, n, S, superko, host_lad, ppol, pval)
+        slot.event.record()
+        return _SlotResult(slot, n, self.policy is not None, self.value is not None, True)
+
+    def _pw(self, S):
+        from ..models.policy import has_pass_logit
+        return S * S + (1 if has_pass_logit(self.policy) else 0)
+
+    def _slot_pass(self, slot, n, S, superko, host_lad, ppol, pval):
+        gf = self.gpu["p"]
+        d, h = slot.d, slot.h
+        with torch.no_grad():
+            for k in d:
+                d[k][:n].copy_(h[k][:n], non_blocking=True)
+            il = None
+            if superko:
+                slot.d_ill[:n].copy_(slot.h_ill[:n], non_blocking=True)
+                il = slot.d_ill[:n]
+            x = slot.planes[:n]
+            gf.run(d["colors"][:n], d["ages"][:n], d["meta4"][:n], il,
+                   d["ladders"][:n] if host_lad else None, n, S, out=x)
+            slot.o_sens[:n].copy_(x[:, self._sens_off].reshape(n, -1), non_blocking=True)
+            # the policy packer reads its first planes of the shared input in place
+            side = None
+            if ppol is not None and pval is not None and self.two_streams:
+                # the value trunk on its own stream fills the partial last block wave of each
+                # policy conv and vice versa (separate plans, separate buffers)
+                side = self.__dict__.get("_vstream")
+                if side is None:
+                    side = self._vstream = torch.cuda.Stream(x.device)
+                side.wait_stream(torch.cuda.current_stream())
+            if ppol is not None:
+                pr = ppol.forward(x, clone=False)
+                slot.o_pri[:n].copy_(pr, non_blocking=True)
+            if pval is not None:
+                with torch.cuda.stream(side) if side is not None else _nullctx():
+                    v = pval.forward(x).reshape(-1)
+                    slot.o_val[:n].copy_(v, non_blocking=True)
+                if side is not None:
+                    torch.cuda.current_stream().wait_stream(side)
+
+    def _graph_ok(self, slot, key):
+        """Capture the slot pass of this shape once (after one eager run warmed it up)."""
+        graphs = slot.__dict__.setdefault("graphs", {})
+        ppol, pval = self._plans()
+
+        def gens():
+            return tuple(getattr(o, "gen", 0) for p in (ppol, pval) if p is not None
+                         for o in (p.trunk, p.head))
+
+        ent = graphs.get(key)
+        if ent is not None and ent[1] == gens():
+            return True
+        seen = slot.__dict__.setdefault("seen", set())
+        if key not in seen:
+            seen.add(key)
+            return False  # eager first: allocations and weight packing happen outside capture
+        n, S, superko, host_lad = key
+        g = torch.cuda.CUDAGraph()
+        side = self.__dict__.get("_cap_stream")
+        if side is None:
+            side = self._cap_stream = torch.cuda.Stream(slot.planes.device)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
+                self._slot_pass(slot, n, S, superko, host_lad, ppol, pval)
+        torch.cuda.current_stream().wait_stream(side)
+        graphs[key] = (g, gens())
+        return True
 
     def _xbuf(self, key, n, S):
         """Persistent device input planes per (network, wave size, board size): a captured
@@ -423,18 +613,22 @@ class ParallelMCTS(object):
         return self._gpu_rollout.add(s, wid, self.rollouts_per_leaf, self.rollout_limit,
                                      seed=self.seed * 7919 + self.stats["waves"])
 
-    def search(self, state, n_playout=None):
+    def search(self, state, n_playout=None, tick=None):
+        """Run ``n_playout`` simulations from ``state`` (tree reused when possible). ``tick(s)``,
+        if given, runs after every wave's value backup."""
         s = self._sync_root(state)
         target = s.root_visits + (n_playout or self.n_playout)
         submit = getattr(self.evaluator, "submit", None)
         if self.pipeline > 1 and submit is not None:
-            self._search_pipelined(s, target, submit)
+            self._search_pipelined(s, target, submit, tick)
         else:
             stall = 0
             while s.root_visits < target:
                 want = min(self.batch, target - s.root_visits)
                 before = s.root_visits
                 self._wave(s, want)
+                if tick is not None:
+                    tick(s)
                 stall = stall + 1 if s.root_visits == before else 0
                 if stall > 3:
                     break
@@ -445,7 +639,7 @@ class ParallelMCTS(object):
         self._acc("t_rollout_wait", time.perf_counter() - t)
         return s
 
-    def _search_pipelined(self, s, target, submit):
+    def _search_pipelined(self, s, target, submit, tick=None):
         """Up to ``pipeline`` waves in flight: while the GPU evaluates wave k (features, policy
         and value nets, copies back to pinned memory) the host selects wave k+1 — virtual loss
         keeps the two apart — builds its feature inputs and launches its rollouts; then it
@@ -453,13 +647,22 @@ class ParallelMCTS(object):
         queue = collections.deque()
         queued = 0
         stall = 0
+        # packed path: leaves go from the native tree straight into pinned slot buffers (no
+        # Python board objects), one graph-capturable GPU pass per wave
+        slots = None
+        cap = getattr(self.evaluator, "wave_capable", None)
+        if cap is not None and os.environ.get("RAG_PACKED_WAVES", "1") == "1" and \
+                cap(s.root_board.size):
+            slots = self.__dict__.get("_slots")
+            if slots is None or slots.depth != self.pipeline:
+                slots = self._slots = _Slots(self.evaluator.gpu["p"].device, self.pipeline)
         while True:
             t0 = time.perf_counter()
             if len(queue) < self.pipeline and s.root_visits + queued < target:
                 want = min(self.batch, target - s.root_visits - queued)
                 wid, n = s.select(want)
                 if n > 0:
-                    boards = s.leaf_boards(wid)
+                    boards = None if slots is not None else s.leaf_boards(wid)
                     pending = None
                     if self.lmbda > 0:
                         if self.rollout_device == "gpu":
@@ -467,7 +670,9 @@ class ParallelMCTS(object):
                         else:
                             s.start_rollouts(wid)
                     t1 = time.perf_counter()
-                    if self.async_eval:
+                    if slots is not None:
+                        handle = self.evaluator.submit_wave(s, wid, n, slots, self.batch)
+                    elif self.async_eval:
                         if self._pool is None:
                             self._pool = concurrent.futures.ThreadPoolExecutor(1)
                         handle = _Async(self._pool.submit(submit, boards))
@@ -505,6 +710,8 @@ class ParallelMCTS(object):
             self._acc("t_eval", t2 - t1)
             self._acc("t_backup", t3 - t2)
             self._acc("t_rollout_wait", t4 - t3)
+            if tick is not None:
+                tick(s)  # e.g. the distributed search's root-statistics exchange
 
     def get_move(self, state):
         s = self.search(state)

@@ -1,7 +1,19 @@
-"""One APV-MCTS search on several GPUs (the reference's ParallelMCTS is an
-empty stub, AlphaGo/mcts.py:219-220).
+"""APV-MCTS on several GPUs (the reference's ParallelMCTS is an empty stub,
+AlphaGo/mcts.py:219-220). One process per GPU, torch.distributed "nccl" = RCCL between them
+(gloo in the CPU tests). Two designs:
 
-Design (one process per GPU, torch.distributed "nccl" = RCCL between them; gloo in CPU tests):
+SharedRootMCTS (default; ``benchmarks/mcts_bench.py --distributed``) — every rank runs the full
+single-GPU pipelined search (its own native tree, its own host threads, its own GPU) on the same
+position, and after every wave the ranks all-reduce the statistics their trees added at the
+root's children (4 x 362 floats, asynchronous, one wave of lag). Each rank mixes the other ranks'
+totals into its root selection (Search.set_root_external), so the job explores the root as one
+search — the "root parallelisation with shared root statistics" family of parallel MCTS — while
+everything below the root stays rank-local. No host funnels the job: the r2 master design below
+needs rank 0 to select, pack and back up every leaf of every GPU, whose null-evaluator ceiling
+(benchmarks/mcts_null_bench.py) is below 8x one GPU's rate. The move is the most visited root
+child over all ranks (one final all-reduce of visit counts), identical on every rank.
+
+DistributedMCTS (``mode="master"``) — one tree on rank 0, leaf evaluation spread over all ranks:
 
   * rank 0 owns the only tree (the native ``_rocgo.Search``). Every *round* it selects one wave of
     ``batch`` leaves per rank (virtual loss keeps the waves apart), packs each wave's leaves as
@@ -19,9 +31,10 @@ Design (one process per GPU, torch.distributed "nccl" = RCCL between them; gloo 
 
 So the tree, the selection and the backups stay on one host (no tree synchronisation), and all
 the per-leaf work that scales — ladder reading, features, both networks, rollouts — is split
-over the GPUs and their host threads. Root parallelism (independent trees, visit counts
-all-reduced) remains available as ``ParallelMCTS(dp=...)``.
+over the GPUs and their host threads. Plain root parallelism (independent trees, visit counts
+all-reduced only at the end) remains available as ``ParallelMCTS(dp=...)``.
 """
+import math
 import collections
 import time
 
@@ -437,3 +450,113 @@ class DistributedMCTS(ParallelMCTS):
         if self.world > 1:
             dist.all_reduce(t)
         return t.cpu().numpy()
+
+
+class RootExchange(object):
+    """Asynchronous all-reduce (sum) of a small float32 vector, one in flight: exchange(v) posts
+    v and returns the (sum, own contribution) of the previous exchange (None the first time).
+    On GPUs the collective runs on its own stream (RCCL), staged through pinned memory, so it
+    never waits for the search's network work queued on the other streams."""
+
+    def __init__(self, n, device):
+        self.n = int(n)
+        self.gpu = device.type == "cuda"
+        self.device = device
+        self.pending = None
+        self.k = 0
+        if self.gpu:
+            self.stream = torch.cuda.Stream(device)
+            self.dev = [torch.empty(self.n, dtype=torch.float32, device=device) for _ in range(2)]
+            self.hin = [torch.empty(self.n, dtype=torch.float32, pin_memory=True)
+                        for _ in range(2)]
+            self.hout = [torch.empty(self.n, dtype=torch.float32, pin_memory=True)
+                         for _ in range(2)]
+            self.events = [torch.cuda.Event() for _ in range(2)]
+
+    def exchange(self, vec):
+        prev = self.wait()
+        self._post(np.asarray(vec, np.float32))
+        return prev
+
+    def wait(self):
+        """Result of the exchange in flight (None if none)."""
+        p, self.pending = self.pending, None
+        if p is None:
+            return None
+        if self.gpu:
+            ev, hout, own = p
+            ev.synchronize()
+            return hout.numpy().copy(), own
+        work, t, own = p
+        work.wait()
+        return t.numpy(), own
+
+    def _post(self, vec):
+        if vec.size != self.n:
+            raise ValueError("exchange vector of %d, expected %d" % (vec.size, self.n))
+        if not self.gpu:
+            t = torch.from_numpy(vec.copy())
+            self.pending = (dist.all_reduce(t, async_op=True), t, vec.copy())
+            return
+        k = self.k = (self.k + 1) % 2
+        hin, buf, hout, ev = self.hin[k], self.dev[k], self.hout[k], self.events[k]
+        hin.numpy()[:] = vec  # the previous use of this buffer completed (waited above)
+        with torch.cuda.stream(self.stream):
+            buf.copy_(hin, non_blocking=True)
+            work = dist.all_reduce(buf, async_op=True)
+            work.wait()  # the exchange stream waits for the collective (no host block)
+            hout.copy_(buf, non_blocking=True)
+            ev.record(self.stream)
+        self.pending = (ev, hout, vec.copy())
+
+
+class SharedRootMCTS(ParallelMCTS):
+    """APV-MCTS over all ranks of ``dp`` with shared root statistics (see the module doc).
+
+    Call ``get_move(state)`` on every rank with the same state (all ranks return the same move)
+    and ``update_with_move(move)`` on every rank. ``n_playout`` is the whole job's budget per
+    move; each rank runs its share."""
+
+    def __init__(self, policy=None, value=None, rollout=None, dp=None, **kw):
+        super(SharedRootMCTS, self).__init__(policy, value, rollout, dp=dp, **kw)
+        self.world = self.dp.world if self.dp is not None else 1
+        self.exchanges = 0
+
+    def search(self, state, n_playout=None, tick=None):
+        total = int(n_playout or self.n_playout)
+        if self.world == 1:
+            return super(SharedRootMCTS, self).search(state, total, tick)
+        M = state.size * state.size + 1
+        dev = self.dp.device
+        if self.dp.backend == "gloo":
+            dev = torch.device("cpu")
+        xch = RootExchange(4 * M + 2, dev)
+        ext = np.zeros((4, M), np.float32)
+        state_box = {"all_done": False}
+
+        def step(s, done):
+            d = s.root_deltas()
+            vec = np.concatenate([d.reshape(-1), np.array([1.0 if done else 0.0,
+                                                           float(d[0].sum())], np.float32)])
+            prev = xch.exchange(vec)
+            self.exchanges += 1
+            if prev is None:
+                return
+            tot, own = prev
+            ext[:] += (tot[:4 * M] - own[:4 * M]).reshape(4, M)
+            s.set_root_external(ext)
+            state_box["all_done"] = tot[4 * M] >= self.world - 0.5
+
+        def on_wave(s):
+            step(s, False)
+            if tick is not None:
+                tick(s)
+
+        share = int(math.ceil(total / float(self.world)))
+        s = super(SharedRootMCTS, self).search(state, share, on_wave)
+        # this rank is done: keep exchanging (zero deltas, done flag) until every rank is, so
+        # that all ranks issue the same sequence of collectives
+        while not state_box["all_done"]:
+            step(s, True)
+        xch.wait()
+        return s

@@ -117,3 +117,87 @@ def test_distributed_search_gpu_single_rank(cuda):
         mc.update_with_move(mv)
     assert mc.stats["sims"] >= 2 * 1024 - 2
     assert mc._search.rollouts == mc._search.sims
+
+
+def test_root_deltas_and_external_stats_steer_root_selection():
+    """Search.root_deltas reports what a tree added at the root's children since the previous
+    call; statistics given as external (another rank's) steer this tree's root selection."""
+    st = go.GameState(size=7)
+    P = 49
+    pri = np.full((64, P), 1.0 / P, np.float32)
+    a = rg.Search(st.native, 1)
+    a.lmbda = 0.0
+    w, n = a.select(1)
+    a.backup_value(w, pri[:1], np.zeros(1, np.float32))
+    w, n = a.select(16)
+    a.backup_value(w, pri[:n], np.zeros(n, np.float32))
+    d = a.root_deltas()
+    assert d.shape == (4, P + 1)
+    assert d[0].sum() == 16 and (d[0] <= 1).all()
+    assert not a.root_deltas().any(), "a second call reports nothing new"
+    # a fresh tree of the same root: external statistics saying move 24 won 50 of 50 visits
+    b = rg.Search(st.native, 1)
+    b.lmbda = 0.0
+    w, n = b.select(1)
+    b.backup_value(w, pri[:1], np.zeros(1, np.float32))
+    ext = np.zeros((4, P + 1), np.float32)
+    ext[0, 24], ext[1, 24] = 50.0, 50.0
+    b.set_root_external(ext)
+    for _ in range(3):
+        w, n = b.select(1)
+        assert b.leaf_boards(w)[0].color_at(24) == go.BLACK  # the descent went through 24
+        b.backup_value(w, pri[:1], np.zeros(1, np.float32))
+    b.clear_root_external()
+    w, n = b.select(1)
+    assert b.leaf_boards(w)[0].color_at(24) == go.EMPTY  # 3 local visits at 0: explore others
+
+
+def _shared_worker(rank, world, port, outdir):
+    import os
+    import torch
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from rocalphago_amd.engine.gamestate import GameState
+    from rocalphago_amd.models.policy import CNNPolicy
+    from rocalphago_amd.models.value import CNNValue
+    from rocalphago_amd.parallel.dp import DPContext
+    from rocalphago_amd.search.distributed import SharedRootMCTS
+    dp = DPContext(device="cpu")
+    feats = ["board", "ones", "turns_since", "liberties", "sensibleness"]
+    pol = CNNPolicy(feats, board=7, filters_per_layer=8, layers=2, device="cpu", seed=3)
+    val = CNNValue(feats + ["color"], board=7, filters_per_layer=8, layers=2, device="cpu",
+                   seed=4)
+    # rank 1 gets a smaller wave: the ranks run different numbers of waves and must still
+    # issue matching collectives
+    mc = SharedRootMCTS(pol, val, dp=dp, lmbda=0.5, n_playout=128, batch=12 if rank else 16,
+                        rollout_limit=80, nthreads=1)
+    st = GameState(size=7)
+    moves = []
+    for _ in range(3):
+        mv = mc.get_move(st)
+        moves.append(-1 if mv is None else mv[0] * 7 + mv[1])
+        st.do_move(mv)
+        mc.update_with_move(mv)
+    np.save(os.path.join(outdir, "mv%d.npy" % rank), np.array(moves))
+    np.save(os.path.join(outdir, "st%d.npy" % rank), np.array([mc.stats["sims"],
+                                                               mc.exchanges]))
+    dp.shutdown()
+
+
+def test_shared_root_search_two_ranks(tmp_path):
+    """SharedRootMCTS on 2 gloo ranks: each rank runs its share of the playouts, root
+    statistics are exchanged after every wave, and every rank plays the same move."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.spawn(_shared_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    m0, m1 = np.load(tmp_path / "mv0.npy"), np.load(tmp_path / "mv1.npy")
+    assert np.array_equal(m0, m1)
+    for r in (0, 1):
+        sims, xch = np.load(tmp_path / ("st%d.npy" % r))
+        assert sims >= 3 * 64 - 3, (r, sims)
+        assert xch >= 3 * 4, (r, xch)

@@ -211,3 +211,43 @@ def test_two_stream_evaluation_matches_one_stream(monkeypatch):
         for p, r in zip(pend, ref):
             for g, e in zip(p.result(), r):
                 assert np.array_equal(g, e), rep
+
+
+@pytest.mark.parametrize("superko,graph", [(False, "0"), (False, "1"), (True, "0")])
+def test_packed_wave_matches_board_path(monkeypatch, superko, graph):
+    """submit_wave (leaves packed natively into pinned slots, one GPU pass per wave, optionally
+    graph-replayed) gives the same priors / values / sensible masks as evaluating the wave's
+    board objects (NetworkEvaluator.submit), for a mid-game root, also with positional superko."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from rocalphago_amd.features.preprocessing import DEFAULT_FEATURES
+    from rocalphago_amd.models.policy import CNNPolicy
+    from rocalphago_amd.models.value import CNNValue
+    from rocalphago_amd.search.apv import NetworkEvaluator, _Slots
+    dev = torch.device("cuda")
+    pol = CNNPolicy(DEFAULT_FEATURES, board=19, filters_per_layer=64, layers=4, device=dev,
+                    seed=5)
+    val = CNNValue(DEFAULT_FEATURES + ["color"], board=19, filters_per_layer=64, layers=4,
+                   device=dev, seed=6)
+    st = _random_positions(1, 19, 21)[0]
+    root = GameState(size=19, enforce_superko=superko)
+    for mv in st.history:
+        root.do_move(mv)
+    monkeypatch.setenv("RAG_EVAL_GRAPH", graph)
+    ev = NetworkEvaluator(pol, val)
+    assert ev.wave_capable(19)
+    slots = _Slots(dev, 2)
+    s = rg.Search(root.native, 4)
+    s.lmbda = 0.0
+    s.parallel_select_min = 1 << 20  # serial, deterministic descents
+    rs = np.random.RandomState(0)
+    for rep in range(4):  # eager, eager (graph: capture), replay, replay
+        wid, n = s.select(48)
+        assert n == 48
+        ref = ev.submit(s.leaf_boards(wid)).result()
+        got = ev.submit_wave(s, wid, n, slots, 48).result()
+        for g, e in zip(got, ref):
+            assert g.shape == e.shape
+            assert np.array_equal(g, e), rep
+        s.backup_value(wid, np.ascontiguousarray(got[0]), rs.uniform(-1, 1, n).astype(np.float32),
+                       got[2])
