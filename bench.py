@@ -55,6 +55,10 @@ def main():
                     help="N>1: wall-clock limit of the multi-GPU search measurement")
     ap.add_argument("--trace", default=None,
                     help="also write a Chrome trace (torch.profiler) of 5 untimed steps here")
+    ap.add_argument("--stall-timeout", type=float, default=120.0,
+                    help="N>1: a rank without progress for this long prints which rank(s) "
+                         "stalled and exits non-zero (parallel/watchdog.py); collectives time "
+                         "out shortly after")
     args = ap.parse_args()
     if args.filters is None:
         args.filters = 128 if args.model == "resnet" else 192
@@ -68,6 +72,9 @@ def main():
                "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
         sys.exit(subprocess.call(cmd))
 
+    if "WORLD_SIZE" in os.environ:
+        # a failed / timed-out RCCL collective tears the rank down instead of hanging it
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     import torch
 
     from rocalphago_amd.features.preprocessing import DEFAULT_FEATURES
@@ -77,8 +84,11 @@ def main():
     from rocalphago_amd.training.data import TRANSFORM_NAMES, DeviceDataset
     from rocalphago_amd.training.supervised import SupervisedTrainer
 
-    dp = DPContext()
+    from rocalphago_amd.parallel.watchdog import RankWatchdog, inject_stall
+    dp = DPContext(timeout_s=int(args.stall_timeout) + 60)
     dev = dp.device
+    wd = RankWatchdog(dp.rank, dp.world, args.stall_timeout, phase="setup") \
+        if dp.world > 1 else None
     if dev.type != "cuda":
         raise SystemExit("bench.py needs a GPU")
     torch.manual_seed(1234)
@@ -118,21 +128,42 @@ def main():
     if trainer.plan is None:
         raise SystemExit("HIP fused plan not active for the %s network" % args.model)
 
+    counter = [0]
+
     def step():
+        # heartbeat 2k: step k started; 2k+1: its gradients reached the all-reduce
+        k = counter[0]
+        counter[0] += 1
+        inject_stall(dp.rank, k)  # RAG_STALL_RANK / RAG_STALL_STEP rehearsal of a hung rank
+        if wd is not None:
+            wd.beat(2 * k)
         idx = torch.randint(0, N, (args.batch,), generator=gen, device=dev)
         trainer.step(idx)
+        if wd is not None:
+            wd.beat(2 * k + 1)
 
+    if wd is not None:
+        wd.set_phase("sl-warmup")
     for _ in range(args.warmup):
         step()
     dp.barrier()
     torch.cuda.synchronize()
+    if wd is not None:
+        wd.set_phase("sl-timed")
+        counter[0] = 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
     dp.barrier()
     dt = time.perf_counter() - t0
-    dt = dp.max_scalar(dt)
+    # per-rank step time and the number of ranks that reached this point (self-check)
+    rank_t = torch.zeros(dp.world, dtype=torch.float64, device=dev)
+    rank_t[dp.rank] = dt
+    dp.allreduce_sum_(rank_t)
+    per_rank_ms = [round(float(x) / args.steps * 1e3, 3) for x in rank_t.cpu()]
+    ranks_seen = int((rank_t > 0).sum())
+    dt = float(rank_t.max())
     if args.trace:
         # host + device timeline of a few extra (untimed) steps, Chrome-trace JSON
         from torch.profiler import ProfilerActivity, profile
@@ -170,6 +201,8 @@ def main():
                    "global_batch": args.batch * dp.world, "per_gpu_batch": args.batch,
                    "seq_len": 361, "parallelism": "dp%d" % dp.world},
         "train_loss": round(loss, 4),
+        "ranks_seen": ranks_seen,
+        "per_rank_ms_per_step": per_rank_ms,
         "baseline_note": "vs_baseline = value / 3000 positions/s (paper-derived SL throughput, "
                          "BASELINE.md; the reference publishes no numbers)",
     }
@@ -189,6 +222,8 @@ def main():
                                     "column BN + ReLU + residual units), %d params" % (
                                         args.filters, args.layers, nparams)
         result["baseline_note"] = "no published baseline for the residual policy"
+    if wd is not None:
+        wd.set_phase("mcts", limit_s=max(args.stall_timeout, args.mcts_guard_s + 30))
     if not args.no_mcts and args.model == "policy":
         # N = 1: the pipelined single-GPU search. N > 1: ONE search whose leaf waves are dealt
         # to all N GPUs (search/distributed.py) — the whole job's sims/s is that search's.
@@ -245,6 +280,8 @@ def main():
                 dp.world - int(tot[2]))
     if dp.is_root:
         print(json.dumps(result), flush=True)
+    if wd is not None:
+        wd.stop()
     dp.shutdown()
 
 

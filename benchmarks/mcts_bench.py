@@ -64,9 +64,14 @@ def measure(device, playouts=8192, warmup=512, moves=1, **kw):
 
 def measure_distributed(dp, device, playouts=8192, warmup=512, moves=1, filters=192,
                         layers=12, batch=512, rollouts_per_leaf=1, lmbda=0.5, nthreads=16,
-                        seed=1, rollout_delay=6):
-    """ONE search whose leaf waves are evaluated on all ranks (search/distributed.py).
-    Collective: every rank calls it; rank 0's dict has the search's sims/s, the others None."""
+                        seed=1, rollout_delay=6, mode="shared"):
+    """One search over all ranks (search/distributed.py). mode "shared" (default): every rank
+    runs the pipelined single-GPU search with shared root statistics (SharedRootMCTS);
+    "master": one tree on rank 0 with leaf waves dealt to all ranks (DistributedMCTS).
+    Collective: every rank calls it; rank 0's dict has the job's sims/s, the others None."""
+    if mode == "shared":
+        return _measure_shared(dp, device, playouts, warmup, moves, filters, layers, batch,
+                               rollouts_per_leaf, lmbda, nthreads, seed)
     import torch
     from rocalphago_amd.engine.gamestate import GameState
     from rocalphago_amd.features.preprocessing import DEFAULT_FEATURES
@@ -109,6 +114,63 @@ def measure_distributed(dp, device, playouts=8192, warmup=512, moves=1, filters=
     return out
 
 
+def _measure_shared(dp, device, playouts, warmup, moves, filters, layers, batch,
+                    rollouts_per_leaf, lmbda, nthreads, seed):
+    import torch
+    from rocalphago_amd.engine.gamestate import GameState
+    from rocalphago_amd.features.preprocessing import DEFAULT_FEATURES
+    from rocalphago_amd.models.policy import CNNPolicy
+    from rocalphago_amd.models.value import CNNValue
+    from rocalphago_amd.search.distributed import SharedRootMCTS
+    pol = CNNPolicy(DEFAULT_FEATURES, board=19, filters_per_layer=filters, layers=layers,
+                    device=device, seed=seed)
+    val = CNNValue(DEFAULT_FEATURES + ["color"], board=19, filters_per_layer=filters,
+                   layers=layers, device=device, seed=seed + 1)
+    gpu = device.type == "cuda"
+    mc = SharedRootMCTS(pol, val, dp=dp, lmbda=lmbda, batch=batch, nthreads=nthreads,
+                        rollout_device="gpu" if gpu else "cpu",
+                        rollouts_per_leaf=rollouts_per_leaf, seed=seed, pipeline=3)
+    st = GameState()
+    mc.search(st, warmup * dp.world)  # compiles / allocates; the tree is discarded below
+    mc._search = None
+    mc.stats = {"waves": 0, "sims": 0}
+    if gpu:
+        torch.cuda.synchronize()
+    dp.barrier()
+    t0 = time.perf_counter()
+    for _ in range(moves):
+        mc.n_playout = playouts
+        mv = mc.get_move(st)
+        st.do_move(mv)
+        mc.update_with_move(mv)
+    if gpu:
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    s = mc.stats
+    t = torch.tensor([float(s["sims"]), dt, float(mc.exchanges)], dtype=torch.float64,
+                     device=device if dp.backend != "gloo" else "cpu")
+    if dp.world > 1:
+        import torch.distributed as dist
+        per = [torch.zeros_like(t) for _ in range(dp.world)]
+        dist.all_gather(per, t)
+        per = [p.cpu().numpy() for p in per]
+    else:
+        per = [t.cpu().numpy()]
+    if dp.rank != 0:
+        return None
+    tot = sum(p[0] for p in per)
+    dtm = max(p[1] for p in per)
+    out = {"sims_per_s": tot / dtm, "sims": int(tot), "seconds": dtm, "batch": batch,
+           "rollouts_per_leaf": rollouts_per_leaf, "rollout_device": mc.rollout_device,
+           "gpus": dp.world, "mode": "shared-root", "leaves_per_rank": [int(p[0]) for p in per],
+           "root_exchanges_per_rank": [int(p[2]) for p in per]}
+    if lmbda > 0:
+        out["rollouts_per_s"] = tot * rollouts_per_leaf / dtm
+    for k in ("t_select", "t_submit", "t_eval", "t_backup"):
+        out[k + "_frac"] = round(s.get(k, 0.0) / dt, 3)
+    return out
+
+
 def measure_sims_per_s(device, **kw):
     return measure(device, **kw)["sims_per_s"]
 
@@ -133,6 +195,8 @@ def main():
                     help="--distributed: rounds a wave's rollouts may stay in flight")
     ap.add_argument("--distributed", action="store_true",
                     help="one search over all torchrun ranks (search/distributed.py)")
+    ap.add_argument("--mode", default="shared", choices=["shared", "master"],
+                    help="--distributed: shared root statistics (default) or rank-0 master")
     args = ap.parse_args()
     import torch
     if args.distributed:
@@ -141,7 +205,7 @@ def main():
         r = measure_distributed(dp, dp.device, playouts=args.playouts, batch=args.batch,
                                 moves=args.moves, rollouts_per_leaf=args.rollouts_per_leaf,
                                 lmbda=args.lmbda, filters=args.filters, nthreads=args.threads,
-                                rollout_delay=args.rollout_delay)
+                                rollout_delay=args.rollout_delay, mode=args.mode)
         if r is not None:
             r.update({"metric": "MCTS simulations/s (19x19 APV-MCTS, one search over %d GPUs)"
                       % dp.world, "lmbda": args.lmbda})
