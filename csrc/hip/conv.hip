@@ -581,41 +581,48 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
 // laid out like Y but with its own halo HM.  res: null or a residual added before the activation
 // (ResNet sum-merge), laid out like Y (may alias Y: each element is read then written by one lane).
 // Deferred wgrad reduction (rag_conv_wgrad_deferred): the fp16 partial-slab reduction of one
-// layer waits here and rides along the next conv_tap launch on the same stream as extra blocks
-// (that launch fills 482 of 512 block slots at B = 256, so the reduction runs in otherwise idle
-// slots instead of as a 14 us kernel of its own). One slot: a second deferral, a launch on
-// another stream or rag_wgrad_flush launches the pending reduction as a standalone kernel.
-// The slot is guarded by a mutex (a search thread may launch convolutions while a trainer runs);
-// a pending reduction is taken out of the slot before anything is launched with it.
+// layer waits in a caller-owned handle (PendingRed: the trainer's trunk owns one) and rides along
+// the next conv_tap launch that the caller hands the same handle, on the same stream, as extra
+// blocks (that launch fills 482 of 512 block slots at B = 256, so the reduction runs in otherwise
+// idle slots instead of as a 14 us kernel of its own). Launches without the handle never see it;
+// a launch with the handle on another stream, a second deferral or rag_wgrad_flush(handle)
+// launches the pending reduction as a standalone kernel. No process-wide state: two trainers (or
+// a trainer and a search) may interleave their launches on one stream.
 int rag_launch_wgrad_slab_reduce(const WgradRed& r, hipStream_t stream);  // wgrad_slab.hip
-static std::mutex g_pending_mu;
-static WgradRed g_pending;
-static hipStream_t g_pending_stream = nullptr;
-static bool g_has_pending = false;
+struct PendingRed {
+  int valid;
+  hipStream_t stream;
+  WgradRed r;
+};
 
-// Take the pending reduction if there is one: returns false if the slot was empty.
-static bool take_pending(WgradRed* r, hipStream_t* st) {
-  std::lock_guard<std::mutex> lk(g_pending_mu);
-  if (!g_has_pending) return false;
-  *r = g_pending;
-  *st = g_pending_stream;
-  g_has_pending = false;
+RAG_API size_t rag_wgrad_pending_bytes() { return sizeof(PendingRed); }
+
+// Take the handle's reduction if there is one: returns false if it was empty.
+static bool take_pending(void* h, WgradRed* r, hipStream_t* st) {
+  PendingRed* p = static_cast<PendingRed*>(h);
+  if (!p || !p->valid) return false;
+  *r = p->r;
+  *st = p->stream;
+  p->valid = 0;
   return true;
 }
 
-static int flush_pending(hipStream_t stream) {
+static int flush_pending(void* h, hipStream_t stream) {
   WgradRed r;
   hipStream_t st;
-  if (!take_pending(&r, &st)) return 0;
+  if (!take_pending(h, &r, &st)) return 0;
   return rag_launch_wgrad_slab_reduce(r, stream ? stream : st);
 }
 
-RAG_API int rag_wgrad_flush(hipStream_t stream) { return flush_pending(stream); }
+RAG_API int rag_wgrad_flush(hipStream_t stream, void* pending) {
+  return flush_pending(pending, stream);
+}
 
+// `pending`: null, or the caller's deferred-reduction handle (see PendingRed above).
 RAG_API int rag_conv_igemm(const void* X, const void* W, const float* bias, void* Y,
                            const void* mask, const void* resid, int B, int S, int HI, int HO,
                            int CIN, int COUTP, int YC, int KS, int relu, int HM,
-                           hipStream_t stream) {
+                           hipStream_t stream, void* pending) {
   if (CIN % 32 || COUTP % 32 || YC < COUTP || HI < KS / 2) return -1;
   const int M = B * S * S;
   const int nt = pick_nt(COUTP);
@@ -633,7 +640,7 @@ RAG_API int rag_conv_igemm(const void* X, const void* W, const float* bias, void
   WgradRed pend;
   hipStream_t pend_stream = nullptr;
   const WgradRed* red = nullptr;
-  if (take_pending(&pend, &pend_stream)) {
+  if (take_pending(pending, &pend, &pend_stream)) {
     if (pend_stream == stream) {
       red = &pend;  // rides along this launch (or goes out on its own just below)
     } else {
@@ -756,11 +763,12 @@ static void launch_wgrad_ks(int ntn, int ntc, dim3 grid, hipStream_t st, const b
 static int conv_wgrad_impl(const void* G, const void* X, float* dW, float* db, float* work,
                            int B, int S, int HI, int HG, int GC, int COUT, int COUTP, int CIN,
                            int CINP, int KS, int accumulate, hipStream_t stream,
-                           hipStream_t reduce_stream, bool defer) {
+                           hipStream_t reduce_stream, void* pending) {
   {  // a pending reduction reads the partial slabs this wgrad is about to overwrite
-    const int rc = flush_pending(nullptr);
+    const int rc = flush_pending(pending, nullptr);
     if (rc) return rc;
   }
+  const bool defer = pending != nullptr;
   if (COUTP % 32 || CINP % 32) return -1;
   const int taps = KS * KS;
   const bf16* g = (const bf16*)G;
@@ -823,10 +831,10 @@ static int conv_wgrad_impl(const void* G, const void* X, float* dW, float* db, f
     const WgradRed r = rag_wgrad_slab_red(part, bpart, dW, db, nchunks, CINP, COUT, CIN,
                                           accumulate);
     if (defer && rs == stream) {
-      std::lock_guard<std::mutex> lk(g_pending_mu);
-      g_pending = r;
-      g_pending_stream = stream;
-      g_has_pending = true;
+      PendingRed* p = static_cast<PendingRed*>(pending);
+      p->r = r;
+      p->stream = stream;
+      p->valid = 1;
       return 0;
     }
     return rag_launch_wgrad_slab_reduce(r, rs);
@@ -855,17 +863,19 @@ RAG_API int rag_conv_wgrad(const void* G, const void* X, float* dW, float* db, f
                            int CINP, int KS, int accumulate, hipStream_t stream,
                            hipStream_t reduce_stream) {
   return conv_wgrad_impl(G, X, dW, db, work, B, S, HI, HG, GC, COUT, COUTP, CIN, CINP, KS,
-                         accumulate, stream, reduce_stream, false);
+                         accumulate, stream, reduce_stream, nullptr);
 }
 
-// As rag_conv_wgrad, but an fp16 partial-slab reduction is left pending for the next conv launch
-// on `stream` (see g_pending); dW / db are complete once that launch (or rag_wgrad_flush) ran.
+// As rag_conv_wgrad, but an fp16 partial-slab reduction is left pending in the caller's handle
+// for the next conv launch given that handle on `stream`; dW / db are complete once that launch
+// (or rag_wgrad_flush(handle)) ran. A reduction already pending in the handle is launched first.
 RAG_API int rag_conv_wgrad_deferred(const void* G, const void* X, float* dW, float* db,
                                     float* work, int B, int S, int HI, int HG, int GC, int COUT,
                                     int COUTP, int CIN, int CINP, int KS, int accumulate,
-                                    hipStream_t stream) {
+                                    hipStream_t stream, void* pending) {
+  if (!pending) return -4;
   return conv_wgrad_impl(G, X, dW, db, work, B, S, HI, HG, GC, COUT, COUTP, CIN, CINP, KS,
-                         accumulate, stream, nullptr, true);
+                         accumulate, stream, nullptr, pending);
 }
 
 RAG_API int rag_pack_weights(const float* W, void* Wf, void* Wb, int COUT, int CIN, int KS,

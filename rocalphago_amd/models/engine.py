@@ -94,6 +94,7 @@ class HipTrunk(_PackedConvs):
         self._rstream = None
         # wgrad slab reductions ride along the next dgrad launch (RAG_WGRAD_DEFER=0: own kernels)
         self.defer_reduce = os.environ.get("RAG_WGRAD_DEFER", "1") != "0"
+        self._pending = ops.PendingReduction() if device.type == "cuda" else None
 
     # ------------------------------------------------------------------ buffers
     def _halos(self):
@@ -188,11 +189,13 @@ class HipTrunk(_PackedConvs):
             if rs is not None and self._wevt[slot] is not None:
                 main.wait_event(self._wevt[slot])  # the reduction that last read this slab
             # without a reduce stream, layer l's slab reduction is deferred into the free block
-            # slots of its own dgrad launch (conv.hip g_pending); dW[l] is final after that
+            # slots of its own dgrad launch (this trunk's PendingReduction handle, passed to that
+            # launch explicitly); dW[l] is final after that
             defer = rs is None and self.defer_reduce
             ops.conv_wgrad(g, x, dws[l], dbs[l], B, S, self.halo[l], s.cout, s.coutp, s.cin,
                            s.cinp, s.ks, accumulate=accumulate, work=self._work[slot],
-                           hg=self.halo[l], reduce_stream=rs, defer=defer)
+                           hg=self.halo[l], reduce_stream=rs, defer=defer,
+                           pending=self._pending if defer else None)
             if rs is not None:
                 ev = torch.cuda.Event()
                 ev.record(rs)
@@ -203,9 +206,10 @@ class HipTrunk(_PackedConvs):
                 gout = self.grad_buffer(l - 1, which, B)
                 ops.conv_igemm(g, self._wb[l], None, gout, B, S, self.halo[l],
                                self.halo[l - 1], s.coutp, s.cinp, s.ks, False,
-                               mask=x if below.relu else None, mask_halo=self.halo[l])
+                               mask=x if below.relu else None, mask_halo=self.halo[l],
+                               pending=self._pending if defer else None)
             elif defer:
-                ops.wgrad_flush()
+                ops.wgrad_flush(self._pending)
             if on_layer_done is not None:
                 if rs is not None:
                     with torch.cuda.stream(rs):  # the bucket all-reduce follows the reduction
@@ -216,7 +220,7 @@ class HipTrunk(_PackedConvs):
         if rs is not None:
             main.wait_stream(rs)
         elif self.defer_reduce:
-            ops.wgrad_flush()
+            ops.wgrad_flush(self._pending)
 
 
 class BNSpec(object):

@@ -9,11 +9,12 @@ SZ = C.c_size_t
 
 SIGNATURES = {
     # conv.hip
-    "rag_conv_igemm": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P],
+    "rag_conv_igemm": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P, P],
     "rag_conv_wgrad_workspace": [I, I, I, I, I, P],
     "rag_conv_wgrad": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, P],
-    "rag_conv_wgrad_deferred": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P],
-    "rag_wgrad_flush": [P],
+    "rag_conv_wgrad_deferred": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, P],
+    "rag_wgrad_flush": [P, P],
+    "rag_wgrad_pending_bytes": [],
     "rag_pack_weights": [P, P, P, I, I, I, I, I, P],
     "rag_pack_trunk": [P, I, I64, P],
     "rag_pack_input_u8": [P, P, P, P, I, I, I, I, I, I, P],
@@ -60,7 +61,7 @@ SIGNATURES = {
 }
 
 RESTYPES = {"rag_conv_wgrad_workspace": SZ, "rag_head_bwd_workspace": SZ,
-            "rag_ladder_workspace": SZ,
+            "rag_ladder_workspace": SZ, "rag_wgrad_pending_bytes": SZ,
             "rag_value_mlp_workspace": SZ, "rag_value_mlp_bwd_workspace": SZ}
 
 

@@ -58,11 +58,30 @@ def pack_trunk(table, nlayers, total):
     _check(_lib().rag_pack_trunk(_ptr(table), nlayers, int(total), _stream()), "pack_trunk")
 
 
+class PendingReduction(object):
+    """Caller-owned handle of a deferred wgrad partial-slab reduction (conv.hip PendingRed):
+    ``conv_wgrad(defer=True, pending=h)`` leaves the reduction in ``h``; the next
+    ``conv_igemm(..., pending=h)`` on the same stream runs it in its free block slots, and
+    ``wgrad_flush(h)`` launches it on its own. Launches without the handle never touch it."""
+
+    def __init__(self):
+        self.buf = ctypes.create_string_buffer(int(_lib().rag_wgrad_pending_bytes()))
+
+    @property
+    def ptr(self):
+        return ctypes.cast(self.buf, ctypes.c_void_p)
+
+
+def _hptr(pending):
+    return None if pending is None else pending.ptr
+
+
 def conv_igemm(x, wpack, bias, y, B, S, hi, ho, cinp, coutp, ks, relu, mask=None,
-               mask_halo=None, residual=None):
+               mask_halo=None, residual=None, pending=None):
     """y[pad ho] = act(conv_ks(x[pad hi]) + bias [+ residual]), or the dgrad form with a ReLU
     mask (the layer input: y's channel count, its own halo ``mask_halo``, default ho).
-    ``residual`` (ResNet sum-merge) has y's layout and may be y itself."""
+    ``residual`` (ResNet sum-merge) has y's layout and may be y itself. ``pending``: a
+    PendingReduction whose deferred wgrad reduction rides along this launch."""
     hm = ho if mask_halo is None else mask_halo
     if mask is not None and (mask.shape[1] != S + 2 * hm or mask.shape[-1] != y.shape[-1]):
         raise ValueError("mask layout does not match (halo %d, %d channels)" % (hm, y.shape[-1]))
@@ -70,7 +89,7 @@ def conv_igemm(x, wpack, bias, y, B, S, hi, ho, cinp, coutp, ks, relu, mask=None
         raise ValueError("residual layout does not match the output")
     _check(_lib().rag_conv_igemm(_ptr(x), _ptr(wpack), _ptr(bias), _ptr(y), _ptr(mask),
                                  _ptr(residual), B, S, hi, ho, cinp, coutp, y.shape[-1], ks,
-                                 int(relu), hm, _stream()), "conv_igemm")
+                                 int(relu), hm, _stream(), _hptr(pending)), "conv_igemm")
     return y
 
 
@@ -139,22 +158,26 @@ def wgrad_workspace(B, S, coutp, cinp, ks, device):
 
 
 def conv_wgrad(g, x, dw, db, B, S, hi, cout, coutp, cin, cinp, ks, accumulate=False, work=None,
-               hg=None, reduce_stream=None, defer=False):
+               hg=None, reduce_stream=None, defer=False, pending=None):
     """dW (OIHW fp32) and db from dL/dpre g [pad hg] and the layer input x [pad hi].
     ``reduce_stream`` (a torch stream): run the partial-slab reduction there, ordered after the
     wgrad kernel by an event, so it overlaps the following kernels of the current stream; the
     caller then owns the ordering of ``work`` reuse and of ``dw``/``db`` consumers.
-    ``defer``: leave an fp16 partial-slab reduction pending; the next ``conv_igemm`` on this stream
-    runs it in its free block slots (or ``wgrad_flush()`` launches it). ``dw``/``db`` are final
-    only after that."""
+    ``defer``: leave an fp16 partial-slab reduction pending in ``pending`` (a PendingReduction,
+    required); the next ``conv_igemm(..., pending=pending)`` on this stream runs it in its free
+    block slots (or ``wgrad_flush(pending)`` launches it). ``dw``/``db`` are final only after
+    that."""
     if work is None:
         work = wgrad_workspace(B, S, coutp, cinp, ks, g.device)
     if hg is None:
         hg = (g.shape[1] - S) // 2
     if defer and reduce_stream is None:
+        if pending is None:
+            raise ValueError("conv_wgrad(defer=True) needs a PendingReduction handle")
         _check(_lib().rag_conv_wgrad_deferred(_ptr(g), _ptr(x), _ptr(dw), _ptr(db), _ptr(work), B,
                                               S, hi, hg, g.shape[-1], cout, coutp, cin, cinp, ks,
-                                              int(accumulate), _stream()), "conv_wgrad_deferred")
+                                              int(accumulate), _stream(), pending.ptr),
+               "conv_wgrad_deferred")
         return
     rs = ctypes.c_void_p(reduce_stream.cuda_stream) if reduce_stream is not None else None
     _check(_lib().rag_conv_wgrad(_ptr(g), _ptr(x), _ptr(dw), _ptr(db), _ptr(work), B, S, hi, hg,
@@ -162,9 +185,9 @@ def conv_wgrad(g, x, dw, db, B, S, hi, cout, coutp, cin, cinp, ks, accumulate=Fa
                                  _stream(), rs), "conv_wgrad")
 
 
-def wgrad_flush():
-    """Launch a reduction left pending by ``conv_wgrad(defer=True)`` (no-op if none)."""
-    _check(_lib().rag_wgrad_flush(_stream()), "wgrad_flush")
+def wgrad_flush(pending):
+    """Launch the reduction left in ``pending`` by ``conv_wgrad(defer=True)`` (no-op if none)."""
+    _check(_lib().rag_wgrad_flush(_stream(), pending.ptr), "wgrad_flush")
 
 
 def pack_input(features, out, H, index=None, transforms=None, nplanes=None):

@@ -381,19 +381,63 @@ def test_deferred_wgrad_reduce_fused_into_dgrad(ops):
     ref_dx = ops.alloc_padded(B, S, 1, C, dev)
     ops.conv_igemm(gp, wb, None, ref_dx, B, S, 1, 1, C, C, 3, False, mask=xp)
     # fused into the dgrad launch
+    h = ops.PendingReduction()
     dw, db = torch.full((C, C, 3, 3), 7.0, device=dev), torch.full((C,), 7.0, device=dev)
-    ops.conv_wgrad(gp, xp, dw, db, B, S, 1, C, C, C, C, 3, hg=1, defer=True)
+    ops.conv_wgrad(gp, xp, dw, db, B, S, 1, C, C, C, C, 3, hg=1, defer=True, pending=h)
     dx = ops.alloc_padded(B, S, 1, C, dev)
-    ops.conv_igemm(gp, wb, None, dx, B, S, 1, 1, C, C, 3, False, mask=xp)
+    ops.conv_igemm(gp, wb, None, dx, B, S, 1, 1, C, C, 3, False, mask=xp, pending=h)
     torch.cuda.synchronize()
     assert torch.equal(dx, ref_dx)
     assert rel_err(dw, ref_dw) < 1e-5 and rel_err(db, ref_db) < 1e-5
     # explicit flush, accumulating on top
-    ops.conv_wgrad(gp, xp, dw, db, B, S, 1, C, C, C, C, 3, accumulate=True, hg=1, defer=True)
-    ops.wgrad_flush()
-    ops.wgrad_flush()  # nothing pending: no-op
+    ops.conv_wgrad(gp, xp, dw, db, B, S, 1, C, C, C, C, 3, accumulate=True, hg=1, defer=True,
+                   pending=h)
+    ops.wgrad_flush(h)
+    ops.wgrad_flush(h)  # nothing pending: no-op
     torch.cuda.synchronize()
     assert rel_err(dw, 2 * ref_dw) < 1e-5 and rel_err(db, 2 * ref_db) < 1e-5
+
+
+@pytest.mark.gpu
+def test_deferred_reductions_of_two_trunks_interleave_on_one_stream(ops):
+    """Each trunk owns its pending-reduction handle: launches of another network (or without a
+    handle) on the same stream neither run nor drop it."""
+    dev = torch.device("cuda")
+    torch.manual_seed(11)
+    B, C, S = 32, 192, 19
+    nets = []
+    for k in range(2):
+        x = F.relu(torch.randn(B, C, S, S, device=dev))
+        g = torch.randn(B, C, S, S, device=dev)
+        w = torch.randn(C, C, 3, 3, device=dev) * 0.05
+        xp, gp = ops.pack_nchw(x, 1, C), ops.pack_nchw(g, 1, C)
+        _, wb = ops.pack_weights(w, C, C,
+                                 wb=torch.empty(9, C, C, dtype=torch.bfloat16, device=dev))
+        rdw, rdb = torch.zeros(C, C, 3, 3, device=dev), torch.zeros(C, device=dev)
+        ops.conv_wgrad(gp, xp, rdw, rdb, B, S, 1, C, C, C, C, 3, hg=1)
+        nets.append((xp, gp, wb, rdw, rdb))
+    torch.cuda.synchronize()
+    ha, hb = ops.PendingReduction(), ops.PendingReduction()
+    (xa, ga, wba, rdwa, rdba), (xb, gb, wbb, rdwb, rdbb) = nets
+    dwa, dba = torch.zeros_like(rdwa), torch.zeros_like(rdba)
+    dwb, dbb = torch.zeros_like(rdwb), torch.zeros_like(rdbb)
+    wsa = ops.wgrad_workspace(B, S, C, C, 3, dev).clone()  # separate partial-slab workspaces
+    wsb = ops.wgrad_workspace(B, S, C, C, 3, dev).clone()
+    ops.conv_wgrad(ga, xa, dwa, dba, B, S, 1, C, C, C, C, 3, hg=1, defer=True, pending=ha,
+                   work=wsa)
+    # trunk B's wgrad + dgrad and a handle-less launch run in between: A's reduction waits
+    ops.conv_wgrad(gb, xb, dwb, dbb, B, S, 1, C, C, C, C, 3, hg=1, defer=True, pending=hb,
+                   work=wsb)
+    dxb = ops.alloc_padded(B, S, 1, C, dev)
+    ops.conv_igemm(gb, wbb, None, dxb, B, S, 1, 1, C, C, 3, False, mask=xb, pending=hb)
+    ops.conv_igemm(ga, wba, None, ops.alloc_padded(B, S, 1, C, dev), B, S, 1, 1, C, C, 3, False)
+    torch.cuda.synchronize()
+    assert rel_err(dwb, rdwb) < 1e-5 and rel_err(dbb, rdbb) < 1e-5
+    assert float(dwa.abs().max()) == 0.0, "A's reduction must still be pending"
+    dxa = ops.alloc_padded(B, S, 1, C, dev)
+    ops.conv_igemm(ga, wba, None, dxa, B, S, 1, 1, C, C, 3, False, mask=xa, pending=ha)
+    torch.cuda.synchronize()
+    assert rel_err(dwa, rdwa) < 1e-5 and rel_err(dba, rdba) < 1e-5
 
 
 @pytest.mark.gpu
