@@ -226,7 +226,9 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
     mx = red[0];
 #pragma unroll
     for (int k = 1; k < kWaves; ++k) mx = fmaxf(mx, red[k]);
-    const int e = mx > 0.f ? ilogbf(mx) : 0;
+    // floor the exponent: a block of (near-)denormal partials must not scale by 2^(14-e) beyond
+    // float range (inf * value, NaN * 0); below 2^-100 its fp16 values are 0 anyway
+    const int e = mx > 0.f ? max(ilogbf(mx), -100) : 0;
     const float up = ldexpf(1.f, 14 - e);
     if (tid == 0) part_scale(part, gridDim.x)[wid] = ldexpf(1.f, e - 14);
     f16* dst = reinterpret_cast<f16*>(part) + (size_t)wid * kBlkElems + (w * 64 + lane) * 4;

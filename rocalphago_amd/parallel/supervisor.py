@@ -12,7 +12,8 @@ lost (/root/reference/AlphaGo/training/supervised_policy_trainer.py:134-135 only
   supervisor never re-execs itself or the job;
 * when the child exits non-zero, or writes no progress for ``--hang-timeout`` seconds (a
   watchdog on the modification time of everything in OUT_DIR, e.g. the per-rank
-  ``metrics.rank*.jsonl`` streams, checkpoints and metadata), the whole process group is killed
+  ``metrics.rank*.jsonl`` streams, the trainers' ``heartbeat`` file touched every few seconds,
+  checkpoints and metadata), the whole process group is killed
   and the job is relaunched from the newest ``weights.NNNNN.hdf5`` in OUT_DIR: ``--weights`` is
   set to that file and ``--epochs`` reduced by the epochs already completed. The trainers
   restore the optimizer step count and data cursor from the ``.opt.json`` sidecar, so the
@@ -33,13 +34,25 @@ _CKPT = re.compile(r"weights\.(\d+)\.hdf5$")
 
 
 def latest_checkpoint(out_dir):
-    """(epoch, basename) of the newest ``weights.NNNNN.hdf5`` in ``out_dir``, or None."""
-    best = None
+    """(epoch, basename) of the newest complete ``weights.NNNNN.hdf5`` in ``out_dir``, or None.
+
+    Complete = the weights file has its ``.opt.json`` sidecar (the trainers write the sidecar
+    first and each file through an atomic rename, training/supervised.save_checkpoint), so a
+    job killed while saving resumes from the previous epoch instead of a truncated file or a
+    reset optimizer schedule. Directories whose checkpoints carry no sidecars at all (RL runs)
+    fall back to the newest weights file."""
+    found = []
     for p in glob.glob(os.path.join(out_dir, "weights.*.hdf5")):
         m = _CKPT.search(os.path.basename(p))
-        if m and (best is None or int(m.group(1)) > best[0]):
-            best = (int(m.group(1)), os.path.basename(p))
-    return best
+        if m:
+            side = os.path.splitext(p)[0] + ".opt.json"
+            found.append((int(m.group(1)), os.path.basename(p), os.path.exists(side)))
+    if not found:
+        return None
+    complete = [f for f in found if f[2]]
+    pool = complete if complete else found
+    best = max(pool)
+    return best[0], best[1]
 
 
 def _get_opt(cmd, names):

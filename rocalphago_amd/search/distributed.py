@@ -275,23 +275,24 @@ class DistributedMCTS(ParallelMCTS):
         per rank (priors, values, sens, (round, z) or None)."""
         rnd, n, handle, codec = shipped
         P = codec.P
+        PW = self._prior_width(P)  # P, or P + 1 with the network's pass probability
         B = self.batch
-        W = 2 * P + 4
+        W = PW + P + 3  # priors | sensible | value | rollout z | pad
         out = np.zeros((B, W), np.float32)
         meta = np.zeros(4, np.float32)  # [n, z round, z count, 0]
         if n:
             pr, v, sens = handle.result()
             if pr is not None:
-                out[:n, :P] = pr[:, :P]
+                out[:n, :PW] = pr[:, :PW]
             if sens is not None:
-                out[:n, P:2 * P] = sens
+                out[:n, PW:PW + P] = sens
             if v is not None:
-                out[:n, 2 * P] = v
+                out[:n, PW + P] = v
         meta[0] = n
         if self._pending and (self._pending[0][0] <= rnd - self.delay or n == 0):
             zr, pend = self._pending.popleft()
             z = pend.result()
-            out[:len(z), 2 * P + 1] = z
+            out[:len(z), PW + P + 1] = z
             meta[1], meta[2] = zr, len(z)
         flat = np.concatenate([out.reshape(-1), meta])
         if self.world > 1:
@@ -307,9 +308,14 @@ class DistributedMCTS(ParallelMCTS):
         for g in gathered:
             o, m = g[:-4].reshape(B, W), g[-4:]
             k = int(m[0])
-            zr = (int(m[1]), o[:int(m[2]), 2 * P + 1].copy()) if m[2] > 0 else None
-            res.append((o[:k, :P], o[:k, 2 * P], o[:k, P:2 * P] > 0.5, zr))
+            zr = (int(m[1]), o[:int(m[2]), PW + P + 1].copy()) if m[2] > 0 else None
+            res.append((np.ascontiguousarray(o[:k, :PW]), o[:k, PW + P], o[:k, PW:PW + P] > 0.5,
+                        zr))
         return res
+
+    def _prior_width(self, P):
+        from ..models.policy import has_pass_logit
+        return P + (1 if has_pass_logit(self.evaluator.policy) else 0)
 
     def _round_trip(self, codec, recs, counts, superko, komi):
         """Ship and collect one round (unpipelined)."""

@@ -72,8 +72,7 @@ class MetadataWriterCallback(K.Callback):
         if logs.get(key) < best_loss:
             self.metadata["best_epoch"] = epoch
         if K._is_rank0():
-            with open(self.file, "w") as f:
-                json.dump(self.metadata, f, indent=2)
+            _atomic_json(self.file, self.metadata, indent=2)
 
 
 class SupervisedTrainer(object):
@@ -322,7 +321,8 @@ def run_training(cmd_line_args=None):
     if opt_state:
         sgd.iterations = int(opt_state["iterations"])
         cursor = int(opt_state.get("cursor", 0))
-    epoch_base = len(meta_writer.metadata.get("epochs", []))
+    epoch_base = resume_epoch_base(meta_writer.metadata, opt_state)
+    heartbeat = Heartbeat(args.out_directory, dp.is_root)
 
     if args.packed:
         from .replay import PackedDataset
@@ -355,6 +355,7 @@ def run_training(cmd_line_args=None):
             trainer.step(dev_train[pos])
             cursor = (cursor + gb) % n_train
             seen += args.minibatch
+            heartbeat(sgd.iterations)
         loss, acc = trainer.pop_metrics()
         dt = time.time() - t0
         rank_metrics.log(epoch=epoch_base + epoch, step=int(sgd.iterations))
@@ -363,13 +364,12 @@ def run_training(cmd_line_args=None):
             vl, va = trainer.evaluate(dev_val)
             logs["val_loss"], logs["val_acc"] = vl, va
         gepoch = epoch_base + epoch
+        # checkpoint (sidecar, then weights) before the metadata that records the epoch
+        save_checkpoint(checkpointer, gepoch, logs,
+                        {"iterations": int(sgd.iterations), "cursor": int(cursor),
+                         "lr": args.learning_rate, "decay": args.decay})
         meta_writer.on_epoch_end(gepoch, logs)
-        checkpointer.on_epoch_end(gepoch, logs)
         if dp.is_root:
-            ckpt = checkpointer.filepath.format(epoch=gepoch, **logs)
-            with open(os.path.splitext(ckpt)[0] + ".opt.json", "w") as f:
-                json.dump({"iterations": int(sgd.iterations), "cursor": int(cursor),
-                           "epoch": gepoch, "lr": args.learning_rate, "decay": args.decay}, f)
             with open(metrics_file, "a") as f:
                 f.write(json.dumps(dict(logs, epoch=gepoch, seconds=round(dt, 3),
                                         positions_per_s=round(seen * dp.world / max(dt, 1e-9), 1),
@@ -386,6 +386,62 @@ def _opt_sidecar(weights_path):
         with open(p) as f:
             return json.load(f)
     return None
+
+
+def _atomic_json(path, obj, **kw):
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
+        json.dump(obj, f, **kw)
+    os.replace(tmp, path)
+
+
+def save_checkpoint(checkpointer, epoch, logs, opt_state):
+    """Epoch checkpoint that a killed job can always resume from (the supervisor's
+    watchdog may SIGKILL at any instant): the optimizer/data-cursor sidecar
+    ``weights.NNNNN.opt.json`` is written first, then the weights file — both through a
+    temporary file and an atomic rename — so a ``weights.*.hdf5`` that exists is complete and has
+    its sidecar (parallel/supervisor.latest_checkpoint only resumes from such pairs)."""
+    if not K._is_rank0():
+        checkpointer.on_epoch_end(epoch, logs)  # no-op off rank 0
+        return
+    path = checkpointer.filepath.format(epoch=epoch, **logs)
+    _atomic_json(os.path.splitext(path)[0] + ".opt.json", dict(opt_state, epoch=epoch))
+    checkpointer.on_epoch_end(epoch, logs)
+
+
+class Heartbeat(object):
+    """Touches OUT_DIR/heartbeat at most every ``every_s`` seconds from the training loop (rank
+    0), so the supervisor's no-progress watchdog sees a live job within long epochs."""
+
+    def __init__(self, out_dir, enabled=True, every_s=10.0):
+        self.path = os.path.join(out_dir, "heartbeat")
+        self.enabled = enabled
+        self.every = every_s
+        self.last = 0.0
+
+    def __call__(self, step):
+        if not self.enabled:
+            return
+        now = time.time()
+        if now - self.last < self.every:
+            return
+        self.last = now
+        with open(self.path, "w") as f:
+            f.write("%d %.3f\n" % (step, now))
+
+
+def resume_epoch_base(metadata, opt_state):
+    """First epoch number of a resumed run: one past the checkpoint's own epoch (from its
+    sidecar), with the metadata's epoch log cut back to it (an epoch logged after the last
+    complete checkpoint is re-run, not skipped)."""
+    epochs = metadata.setdefault("epochs", [])
+    if opt_state is None or "epoch" not in opt_state:
+        return len(epochs)
+    base = int(opt_state["epoch"]) + 1
+    del epochs[base:]
+    if metadata.get("best_epoch", 0) >= max(1, len(epochs)):
+        metadata["best_epoch"] = 0
+    return base
 
 
 def _fault_step(rank):

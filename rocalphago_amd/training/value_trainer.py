@@ -26,7 +26,8 @@ from ..models.value import CNNValue
 from ..parallel.dp import BucketedAllReduce, DPContext
 from .data import transform_ids
 from ..utils.metrics import RankMetrics
-from .supervised import MetadataWriterCallback, _fault_step, _opt_sidecar
+from .supervised import (Heartbeat, MetadataWriterCallback, _fault_step, _opt_sidecar,
+                         resume_epoch_base, save_checkpoint)
 
 
 def generate_value_dataset(player, n_games, out_file=None, board=19, features=VALUE_FEATURES,
@@ -239,7 +240,8 @@ def run_training(cmd_line_args=None):
     if opt_state:
         sgd.iterations = int(opt_state["iterations"])
         cursor = int(opt_state.get("cursor", 0))
-    epoch_base = len(meta.metadata.get("epochs", []))
+    epoch_base = resume_epoch_base(meta.metadata, opt_state)
+    heartbeat = Heartbeat(args.out_directory, dp.is_root)
     perm = np.random.RandomState(args.seed).permutation(n)
     rank_metrics = RankMetrics(args.out_directory, dp.rank, dp.world, dp.device)
     trainer = ValueTrainer(model, states, values, args.minibatch, args.symmetries.split(","), dp,
@@ -261,19 +263,18 @@ def run_training(cmd_line_args=None):
                 raise RuntimeError("injected fault at step %d (RAG_FAULT_AT_STEP)" % fault)
             trainer.step(tr[(cursor + dp.rank * args.minibatch + arange) % n_train])
             cursor = (cursor + gb) % n_train
+            heartbeat(sgd.iterations)
         logs = {"loss": trainer.pop_loss()}
         if va.numel():
             logs["val_loss"] = trainer.evaluate(va)
         dt = time.time() - t0
         gepoch = epoch_base + epoch
         rank_metrics.log(epoch=gepoch, step=int(sgd.iterations))
+        save_checkpoint(ckpt, gepoch, logs,
+                        {"iterations": int(sgd.iterations), "cursor": int(cursor),
+                         "lr": args.learning_rate, "decay": args.decay})
         meta.on_epoch_end(gepoch, logs)
-        ckpt.on_epoch_end(gepoch, logs)
         if dp.is_root:
-            path = ckpt.filepath.format(epoch=gepoch, **logs)
-            with open(os.path.splitext(path)[0] + ".opt.json", "w") as f:
-                json.dump({"iterations": int(sgd.iterations), "cursor": int(cursor),
-                           "epoch": gepoch, "lr": args.learning_rate, "decay": args.decay}, f)
             with open(os.path.join(args.out_directory, "metrics.jsonl"), "a") as f:
                 f.write(json.dumps(dict(logs, epoch=gepoch, seconds=round(dt, 3),
                                         positions_per_s=round(steps * gb / max(dt, 1e-9), 1),

@@ -23,12 +23,18 @@ import torch
 
 class CommTimer(object):
     """Records (start, end) event pairs on the current stream around the exposed part of each
-    step's gradient all-reduce; resolved lazily in ``pop``."""
+    step's gradient all-reduce. Pairs are resolved as they complete (a bounded ring: once more
+    than ``ring`` pairs are outstanding the oldest is waited for), so a long epoch keeps O(ring)
+    events alive instead of two per step until ``pop``."""
 
-    def __init__(self, device):
+    def __init__(self, device, ring=64):
         self.cuda = torch.device(device).type == "cuda"
         self.pairs = []
+        self.ring = int(ring)
+        self.done_ms = 0.0
+        self.done_n = 0
         self.host_ms = 0.0
+        self.host_n = 0
         self._t = None
 
     def start(self):
@@ -44,18 +50,38 @@ class CommTimer(object):
             e = torch.cuda.Event(enable_timing=True)
             e.record()
             self.pairs[-1][1] = e
+            self._resolve(block=len(self.pairs) > self.ring)
         elif self._t is not None:
             self.host_ms += (time.perf_counter() - self._t) * 1e3
+            self.host_n += 1
             self._t = None
 
+    def _resolve(self, block=False):
+        """Fold completed pairs (oldest first) into the running total; with ``block`` wait for
+        the oldest pair so the ring stays bounded."""
+        while self.pairs and self.pairs[0][1] is not None:
+            a, b = self.pairs[0]
+            if not b.query():
+                if not block:
+                    return
+                b.synchronize()
+            block = False
+            self.done_ms += a.elapsed_time(b)
+            self.done_n += 1
+            self.pairs.pop(0)
+
+    def pending(self):
+        return len(self.pairs)
+
     def pop(self):
-        """Total exposed all-reduce ms since the last pop (synchronises on the last event)."""
-        ms = self.host_ms
-        if self.pairs:
+        """(total exposed all-reduce ms, number of steps) since the last pop (synchronises on the
+        last event)."""
+        if self.pairs and self.pairs[-1][1] is not None:
             self.pairs[-1][1].synchronize()
-            ms += sum(a.elapsed_time(b) for a, b in self.pairs if b is not None)
-        n = len(self.pairs)
-        self.pairs, self.host_ms = [], 0.0
+        self._resolve()
+        ms, n = self.done_ms + self.host_ms, self.done_n + self.host_n
+        self.done_ms = self.host_ms = 0.0
+        self.done_n = self.host_n = 0
         return ms, n
 
 

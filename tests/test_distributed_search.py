@@ -40,7 +40,7 @@ def test_boards_from_arrays_reproduce_features():
             assert b.last_moves == s.native.last_moves
 
 
-def _dist_worker(rank, world, port, outdir):
+def _dist_worker(rank, world, port, outdir, pass_logit=False):
     import os
     import torch
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
@@ -53,7 +53,8 @@ def _dist_worker(rank, world, port, outdir):
     from rocalphago_amd.search.distributed import DistributedMCTS
     dp = DPContext(device="cpu")
     feats = ["board", "ones", "turns_since", "liberties", "sensibleness"]
-    pol = CNNPolicy(feats, board=7, filters_per_layer=8, layers=2, device="cpu", seed=3)
+    pol = CNNPolicy(feats, board=7, filters_per_layer=8, layers=2, device="cpu", seed=3,
+                    pass_logit=pass_logit)
     val = CNNValue(feats + ["color"], board=7, filters_per_layer=8, layers=2, device="cpu",
                    seed=4)
     mc = DistributedMCTS(pol, val, dp=dp, lmbda=0.5, n_playout=96, batch=12, rollout_limit=80,
@@ -72,6 +73,8 @@ def _dist_worker(rank, world, port, outdir):
     if rank == 0:
         np.save(os.path.join(outdir, "sims.npy"), np.array([mc.stats["sims"],
                                                              mc._search.rollouts]))
+        mv, vis, _, _ = mc._search.root_stats()
+        np.save(os.path.join(outdir, "rootmoves.npy"), np.asarray(mv))
     dp.shutdown()
 
 
@@ -92,6 +95,20 @@ def test_one_search_two_ranks(tmp_path):
     assert c[0] > 0 and c[1] > 0, c
     assert c.sum() == sims >= 3 * 96 - 3
     assert rollouts == sims  # every leaf's rollout came back and was backed up
+
+
+def test_one_search_two_ranks_pass_logit(tmp_path):
+    """With a pass-logit policy the shipped priors carry the pass column: rank 0's tree gets a
+    PASS child at every expansion, as the single-GPU search does."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.spawn(_dist_worker, args=(2, port, str(tmp_path), True), nprocs=2, join=True)
+    assert np.array_equal(np.load(tmp_path / "mv0.npy"), np.load(tmp_path / "mv1.npy"))
+    assert -1 in set(np.load(tmp_path / "rootmoves.npy").tolist())
 
 
 @__import__("pytest").mark.gpu

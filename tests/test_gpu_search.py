@@ -241,6 +241,9 @@ def test_packed_wave_matches_board_path(monkeypatch, superko, graph):
     s.lmbda = 0.0
     s.parallel_select_min = 1 << 20  # serial, deterministic descents
     rs = np.random.RandomState(0)
+    wid, n = s.select(1)  # expand the root first
+    r0 = ev.submit(s.leaf_boards(wid)).result()
+    s.backup_value(wid, np.ascontiguousarray(r0[0]), r0[1], r0[2])
     for rep in range(4):  # eager, eager (graph: capture), replay, replay
         wid, n = s.select(48)
         assert n == 48

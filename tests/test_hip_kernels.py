@@ -462,3 +462,25 @@ def test_trunk_repack_matches_per_layer_packer(ops):
         ref_b = torch.zeros(s.coutp, device=dev)
         ref_b[:s.cout] = bs[l]
         assert torch.equal(tr._bias[l], ref_b), l
+
+
+@pytest.mark.gpu
+def test_wgrad_denormal_scale_gradients_stay_finite(ops):
+    """Block-scaled fp16 partial slabs with a block max near 2^-110 (dead / vanishing channels):
+    the scale exponent is floored, so dW stays finite and proportional (2^(14-e)
+    overflowed to inf, turning zeros into NaN)."""
+    dev = torch.device("cuda")
+    torch.manual_seed(13)
+    B, C, S = 16, 192, 19
+    x = F.relu(torch.randn(B, C, S, S, device=dev))
+    g = torch.randn(B, C, S, S, device=dev)
+    g[:, :64] = 0.0  # exact zeros next to tiny values
+    xp = ops.pack_nchw(x, 1, C)
+    ref_dw, ref_db = torch.zeros(C, C, 3, 3, device=dev), torch.zeros(C, device=dev)
+    ops.conv_wgrad(ops.pack_nchw(g, 1, C), xp, ref_dw, ref_db, B, S, 1, C, C, C, C, 3, hg=1)
+    tiny = 2.0 ** -112
+    dw, db = torch.zeros_like(ref_dw), torch.zeros_like(ref_db)
+    ops.conv_wgrad(ops.pack_nchw(g * tiny, 1, C), xp, dw, db, B, S, 1, C, C, C, C, 3, hg=1)
+    torch.cuda.synchronize()
+    assert torch.isfinite(dw).all() and torch.isfinite(db).all()
+    assert rel_err(dw / tiny, ref_dw) < 5e-2

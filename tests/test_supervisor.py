@@ -64,3 +64,27 @@ def test_supervisor_watchdog_kills_hung_job(tmp_path):
                         hang_timeout=2, poll_s=0.2, log=logs.append)
     assert rc != 0
     assert any("no progress" in l for l in logs)
+
+
+def test_resume_skips_incomplete_checkpoints(tmp_path):
+    """A job killed while saving epoch 2 (weights without sidecar, or a sidecar whose weights
+    never landed) resumes from epoch 1; the metadata's epoch log is cut back to the checkpoint
+    so the lost epoch is re-run rather than skipped (supervisor resume)."""
+    from rocalphago_amd.parallel.supervisor import latest_checkpoint
+    from rocalphago_amd.training.supervised import resume_epoch_base
+    d = tmp_path
+    for e in (0, 1):
+        (d / ("weights.%05d.hdf5" % e)).write_bytes(b"x")
+        (d / ("weights.%05d.opt.json" % e)).write_text('{"epoch": %d, "iterations": 5}' % e)
+    (d / "weights.00002.hdf5").write_bytes(b"trunc")  # killed before its sidecar... (legacy order)
+    (d / "weights.00003.opt.json").write_text('{"epoch": 3}')  # ...or before its weights
+    assert latest_checkpoint(str(d)) == (1, "weights.00001.hdf5")
+    meta = {"epochs": [{"loss": 3.0}, {"loss": 2.0}, {"loss": 1.0}], "best_epoch": 2}
+    assert resume_epoch_base(meta, {"epoch": 1, "iterations": 5}) == 2
+    assert len(meta["epochs"]) == 2 and meta["best_epoch"] == 0
+    # RL-style directories (no sidecars at all): newest weights file
+    rl = tmp_path / "rl"
+    rl.mkdir()
+    for e in (0, 4, 2):
+        (rl / ("weights.%05d.hdf5" % e)).write_bytes(b"x")
+    assert latest_checkpoint(str(rl)) == (4, "weights.00004.hdf5")

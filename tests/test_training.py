@@ -179,3 +179,25 @@ def test_rl_cli_one_iteration(ref_data, tmp_path):
                      "--game-batch", "2", "--iterations", "1", "--move-limit", "12",
                      "--resume"])
     assert os.path.exists(os.path.join(out, "weights.00002.hdf5"))
+
+
+def test_comm_timer_resolves_events_as_it_goes():
+    """CommTimer keeps a bounded number of event pairs alive (one pair per step used
+    to pile up until the per-epoch pop); host mode counts every start/stop pair."""
+    import torch
+    from rocalphago_amd.utils.metrics import CommTimer
+    t = CommTimer("cpu")
+    for _ in range(50):
+        t.start()
+        t.stop()
+    ms, n = t.pop()
+    assert n == 50 and ms >= 0.0
+    assert t.pop() == (0.0, 0)
+    if torch.cuda.is_available():
+        g = CommTimer("cuda", ring=8)
+        for _ in range(100):
+            g.start()
+            g.stop()
+            assert g.pending() <= 9
+        ms, n = g.pop()
+        assert n == 100 and g.pending() == 0
