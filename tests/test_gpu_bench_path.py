@@ -40,18 +40,62 @@ def _rel(a, b):
     return float((a.double() - b.double()).norm() / max(float(b.double().norm()), 1e-30))
 
 
-def _trunk_ref(x, Ws, bs):
+class _Inject(torch.autograd.Function):
+    """Forward: the kernels' own stored activation of a layer (so the next layer consumes
+    exactly what the MFMA kernels consumed); backward: the ReLU derivative from that same
+    activation, applied to the fp32 gradient."""
+
+    @staticmethod
+    def forward(ctx, pre, act, store_bf16):
+        ctx.save_for_backward(act)
+        ctx.store_bf16 = store_bf16
+        return act.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        act, = ctx.saved_tensors
+        g = g * (act > 0).to(g.dtype)
+        # the kernels keep dL/d(pre-activation) of every layer in bf16 buffers
+        return (_bf(g) if ctx.store_bf16 else g), None, None
+
+
+def _trunk_ref(x, Ws, bs, acts=None, store_bf16=True):
     """fp32 trunk on bf16-rounded weights and layer inputs (autograd through the roundings is
-    the identity: straight-through)."""
+    the identity: straight-through). ``acts``: the kernels' stored activations per layer
+    (NCHW fp32), injected as each layer's output — the backward is then fp32 autograd of the
+    exact forward point the kernels differentiated."""
     h = x
-    for W, b in zip(Ws, bs):
+    for l, (W, b) in enumerate(zip(Ws, bs)):
         hin = h + (_bf(h) - h).detach()
         Wq = W + (_bf(W) - W).detach()
-        h = F.relu(F.conv2d(hin, Wq, b, padding=W.shape[-1] // 2))
+        pre = F.conv2d(hin, Wq, b, padding=W.shape[-1] // 2)
+        h = F.relu(pre) if acts is None else _Inject.apply(pre, acts[l], store_bf16)
     return h + (_bf(h) - h).detach()
 
 
+def _gpu_acts(plan, B):
+    from rocalphago_amd.ops import hipops as ops
+    out = []
+    for a, s in zip(plan.trunk.acts[1:], plan.trunk.specs):
+        out.append(ops.unpack(a[:B], s.cout, (a.shape[1] - plan.S) // 2))
+    return out
+
+
 def test_north_star_sl_step_matches_fp32(cuda):
+    """Gradients of one bench-path step vs fp32 autograd, two references:
+    (a) fp32 autograd at the kernels' own forward point (their stored bf16 activations injected
+        as each layer's output, ReLU masks from them, dL/d(pre-activation) rounded to bf16 where
+        the kernels store it) — pins the whole backward arithmetic: head, dgrad, fp32
+        accumulation, fp16 block-scaled partial slabs reduced inside the next dgrad launch.
+        Every tensor within 2e-2. Without the bf16 storage rounding the top layer's bias
+        gradient (a sum that cancels to a few % of its terms at init) differs by ~5 %.
+    (b) an independent fp32 forward + backward (bf16-rounded weights / layer inputs) — within
+        0.25. Its forward activations differ from the kernels' by 0.2-0.6 % (accumulation order
+        changes bf16 roundings, scripts/dbg/bench_path_err.py), and at random init the 12-layer
+        trunk's activations are nearly constant over the board, so the gradient
+        sum_p x(p) (p(p) - y(p)) cancels to a few % of its terms and amplifies that into ~12 %
+        per tensor (3 layers: 1-4 %; identical with fp32 partial slabs and without deferred
+        reductions, i.e. not a kernel error)."""
     torch.backends.cudnn.allow_tf32 = False
     torch.backends.cuda.matmul.allow_tf32 = False
     pol = CNNPolicy(DEFAULT_FEATURES, board=19, filters_per_layer=192, layers=12, device=cuda,
@@ -72,23 +116,32 @@ def test_north_star_sl_step_matches_fp32(cuda):
     tr.step(idx)
     torch.cuda.synchronize()
     got = {n: [t.detach().clone() for t in net.grads_of(n)] for n in params}
-    # fp32 reference
-    leaf = {n: [p.clone().requires_grad_(True) for p in ps] for n, ps in params.items()}
+    acts = _gpu_acts(plan, 256)
     x = ds.states[idx].float()
-    h = _trunk_ref(x, [leaf[n][0] for n in plan.conv_names],
-                   [leaf[n][1] for n in plan.conv_names])
-    hw, hb = leaf[plan.head_name]
-    z = F.conv2d(h, hw, hb).reshape(256, -1) + leaf[plan.bias_name][0]
-    loss = F.cross_entropy(z, ds.labels[idx])
-    loss.backward()
-    errs = {}
-    for n in params:
-        for k, (a, p) in enumerate(zip(got[n], leaf[n])):
-            errs["%s/%d" % (n, k)] = _rel(a, p.grad)
-    worst = max(errs.values())
-    print("per-tensor gradient rel. error (max %.3g):" % worst,
-          " ".join("%s=%.2g" % kv for kv in errs.items()))
-    assert worst <= 2e-2, errs
+    cases = (("kernels' forward point, bf16-stored grads", True, True, 2e-2),
+             ("kernels' forward point, fp32 grads", True, False, 0.1),
+             ("independent fp32", False, False, 0.25))
+    for label, inject, store, bound in cases:
+        leaf = {n: [p.clone().requires_grad_(True) for p in ps] for n, ps in params.items()}
+        h = _trunk_ref(x, [leaf[n][0] for n in plan.conv_names],
+                       [leaf[n][1] for n in plan.conv_names], acts if inject else None, store)
+        hw, hb = leaf[plan.head_name]
+        z = F.conv2d(h, hw, hb).reshape(256, -1) + leaf[plan.bias_name][0]
+        loss = F.cross_entropy(z, ds.labels[idx])
+        loss.backward()
+        errs = {}
+        for n in params:
+            for k, (a, p) in enumerate(zip(got[n], leaf[n])):
+                if n == plan.head_name and k == 1:
+                    # the head's scalar bias: softmax gradients sum to zero over the board, so its
+                    # true gradient is 0 up to rounding noise — compare against the batch scale
+                    errs["%s/%d" % (n, k)] = float((a - p.grad).abs().max()) / 1e-3
+                    continue
+                errs["%s/%d" % (n, k)] = _rel(a, p.grad)
+        worst = max(errs.values())
+        print("[%s] per-tensor gradient rel. error (max %.3g):" % (label, worst),
+              " ".join("%s=%.2g" % kv for kv in errs.items()))
+        assert worst <= bound, (label, errs)
 
 
 def _port():
@@ -137,7 +190,7 @@ def test_value_step_matches_fp32(cuda):
     got = {n: [t.detach().clone() for t in net.grads_of(n)] for n in names}
     leaf = {n: [p.clone().requires_grad_(True) for p in ps] for n, ps in params.items()}
     h = _trunk_ref(X, [leaf[n][0] for n in plan.conv_names],
-                   [leaf[n][1] for n in plan.conv_names])
+                   [leaf[n][1] for n in plan.conv_names], _gpu_acts(plan, B))
     hw, hb = leaf[plan.head_name]
     z = F.conv2d(h, hw, hb).reshape(B, -1)
     W1, b1 = leaf[plan.d1]
