@@ -99,6 +99,57 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NT][kMT], int mw, in
   }
 }
 
+// Block-level epilogue through LDS (no residual): every wave writes its bias (+ReLU) tile as bf16
+// into an LDS image [BM pixels][192 + 8 channels] (the 16-byte pad makes the 16 pixel rows of a
+// ds_write_b64 lane group land on distinct banks), then the whole block writes pixel rows of
+// 192 channels (384 contiguous bytes in the channels-last activation) with 16-byte lane chunks,
+// applying the dgrad ReLU mask from equally coalesced reads. The register epilogue above writes
+// 16 pixels x 32 bytes per store instruction; this one writes whole rows.
+constexpr int kEpRow = kBN + 8;  // bf16 per LDS image row
+template <int BM>
+__device__ __forceinline__ void epilogue_lds(const f32x4 (&acc)[kNT][kMT], bf16* __restrict__ img,
+                                             int mwl, int nwl, int m0, int n0, int M, int S,
+                                             int WO, int HO, int YC, int HM,
+                                             const float* __restrict__ bias, int relu,
+                                             const bf16* __restrict__ mask,
+                                             bf16* __restrict__ Y, int frow, int fq) {
+#pragma unroll
+  for (int j = 0; j < kNT; ++j) {
+    const int n = nwl + j * 16 + fq * 4;
+    float4 bb = {0.f, 0.f, 0.f, 0.f};
+    if (bias) bb = *reinterpret_cast<const float4*>(bias + n0 + n);
+#pragma unroll
+    for (int i = 0; i < kMT; ++i) {
+      float v[4] = {acc[j][i][0] + bb.x, acc[j][i][1] + bb.y, acc[j][i][2] + bb.z,
+                    acc[j][i][3] + bb.w};
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (bf16)(relu ? fmaxf(v[r], 0.f) : v[r]);
+      *reinterpret_cast<bf16x4*>(img + (mwl + i * 16 + frow) * kEpRow + n) = o;
+    }
+  }
+  __syncthreads();
+  const int S2 = S * S, WMK = S + 2 * HM;
+  constexpr int kChunks = kBN / 8;  // 16-byte chunks per pixel row
+  for (int c = threadIdx.x; c < BM * kChunks; c += blockDim.x) {
+    const int row = c / kChunks, k8 = (c - row * kChunks) * 8;
+    const int m = m0 + row;
+    if (m >= M) continue;
+    const int b = m / S2;
+    const int rem = m - b * S2;
+    const int pi = rem / S, pj = rem - pi * S;
+    bf16x8 v = *reinterpret_cast<const bf16x8*>(img + row * kEpRow + k8);
+    if (mask) {
+      const bf16x8 mk = *reinterpret_cast<const bf16x8*>(
+          mask + (size_t)((b * WMK + pi + HM) * WMK + pj + HM) * YC + n0 + k8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = ((float)mk[e] > 0.f) ? v[e] : (bf16)0.f;
+    }
+    *reinterpret_cast<bf16x8*>(Y + (size_t)((b * WO + pi + HO) * WO + pj + HO) * YC + n0 + k8) =
+        v;
+  }
+}
+
 // Blocks [nconv, gridDim.x) are not convolution tiles: they run a deferred wgrad partial-slab
 // reduction (wgrad_part.h) in the block slots the convolution grid leaves free.
 constexpr int kRedU = 14;  // chunk loads in flight per reduce thread
@@ -107,7 +158,8 @@ conv_tap_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                 const float* __restrict__ bias, bf16* __restrict__ Y,
                 const bf16* __restrict__ mask, const bf16* __restrict__ res, int M, int S,
                 int WI, int shift, int WO, int HO, int CIN, int WROWS, int YC, int relu, int HM,
-                long total_rows, int nconv, WgradRed red) {
+                long total_rows, int nconv, WgradRed red, int ep_lds) {
+  static_assert(kLds >= kBM * kEpRow, "the LDS ring must hold the epilogue image");
   __shared__ __attribute__((aligned(16))) bf16 lds[kLds];
   if ((int)blockIdx.x >= nconv) {
     wslab_reduce_blocks<kRedU>(red, (int)blockIdx.x - nconv, (int)gridDim.x - nconv);
@@ -236,8 +288,14 @@ conv_tap_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
     }
   }
 
-  epilogue(acc, m0 + wm * (16 * kMT), n0 + wn * (16 * kNT), M, S, WO, HO, YC, HM, bias, res, relu,
-           mask, Y, frow, fq);
+  if (ep_lds && !res) {
+    __syncthreads();  // every wave is past its last LDS read: the ring becomes the output image
+    epilogue_lds<kBM>(acc, lds, wm * (16 * kMT), wn * (16 * kNT), m0, n0, M, S, WO, HO, YC, HM,
+                      bias, relu, mask, Y, frow, fq);
+  } else {
+    epilogue(acc, m0 + wm * (16 * kMT), n0 + wn * (16 * kNT), M, S, WO, HO, YC, HM, bias, res,
+             relu, mask, Y, frow, fq);
+  }
 }
 
 
@@ -268,7 +326,14 @@ __device__ __forceinline__ void wait_vm_rt(int n) {
     case 10: wait_vm<10>(); break;
     case 11: wait_vm<11>(); break;
     case 12: wait_vm<12>(); break;
-    default: wait_vm<13>(); break;
+    case 13: wait_vm<13>(); break;
+    case 14: wait_vm<14>(); break;
+    case 15: wait_vm<15>(); break;
+    case 16: wait_vm<16>(); break;
+    case 17: wait_vm<17>(); break;
+    case 18: wait_vm<18>(); break;
+    case 19: wait_vm<19>(); break;
+    default: wait_vm<20>(); break;
   }
 }
 
@@ -539,7 +604,315 @@ conv_tap16_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                   res, relu, mask, Y, frow, fq);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Ping-pong 8-wave kernel (conv_tap_pp_kernel): one 512-thread block per CU owns 384 pixels x 192
+// channels with the same 96 x 96 wave tiles, split into two wave GROUPS that alternate roles at
+// every barrier so that the two waves sharing a SIMD (wave w and w + 4) never want the matrix pipe
+// at the same time:
+//
+//   phase A(s):  group 0 reads step s's fragments (and issues the staging loads)
+//                group 1 runs the MFMAs of step s - 1
+//   ---- s_barrier ----
+//   phase B(s):  group 0 runs the MFMAs of step s
+//                group 1 reads step s's fragments
+//   ---- s_barrier ----
+//
+// Each wave still holds ONE fragment set (read(s) is always after its own MFMA(s-1)), so no second
+// register set is needed; the pipe alternates between the two partners' 36-MFMA segments while
+// the other partner's LDS reads / DMA issue run beside them. Group 0 (waves 0-3, pixels 0-191)
+// issues every global->LDS load (3 weight glds per step, 10 slab glds per chunk per wave), so
+// only its waves wait on vmcnt; group 1 (waves 4-7, pixels 192-383) only reads LDS and multiplies.
+// LDS: 2 slabs x 640 rows (>= 554 for any 384-pixel run) + NB weight slots: 80 + NB x 12 KB.
+// Hazards (RAW / WAR) are ordered by the two barriers per step: B(s) is retired by group 0's
+// counted wait before X_s and read by group 0 in A(s) and group 1 in B(s); slot (s+D) % NB is
+// rewritten after X_s, when its previous tile's last reader (group 1 in B(s+D-NB)) has passed
+// X_{s+D-NB+1} (D <= NB-1); every read burst ends with lgkmcnt(0) before the wave's next barrier.
+constexpr int kPPBM = 384;
+constexpr int kPPSlabRows = 640;
+constexpr int kPPSlab = kPPSlabRows * kBK;
+constexpr int kPPAL = kPPSlabRows / 64;  // slab glds per loader wave (4 loader waves x 16 rows)
+constexpr int kPPBL = kBN / 64;          // weight glds per loader wave per step
+
+// DIAG (diagnostic builds only, wrong results): bit 0 = no staging inside the loop, bit 1 = no
+// fragment reads (MFMAs on stale registers), bit 2 = clock stamps (s_memtime / s_memrealtime of
+// wave 0 around the main loop into `stamps`).
+template <int NB, int DIAG = 0, int ISSUE = 0>
+__global__ void __launch_bounds__(512)
+conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
+                   const float* __restrict__ bias, bf16* __restrict__ Y,
+                   const bf16* __restrict__ mask, const bf16* __restrict__ res, int M, int S,
+                   int WI, int shift, int WO, int HO, int CIN, int WROWS, int YC, int relu, int HM,
+                   long total_rows, int nconv, WgradRed red, long long* stamps = nullptr) {
+  constexpr int kLoop = 2 * kPPSlab + NB * kBTile;
+  constexpr int kL = kLoop > kPPBM * kEpRow ? kLoop : kPPBM * kEpRow;  // loop ring | epilogue image
+  // weight tiles staged ahead of the current step (issued in the MFMA segment, the slot's last
+  // reader is one phase further back: NB tiles ahead are safe)
+  constexpr int D = ISSUE ? NB : NB - 1;
+  __shared__ __attribute__((aligned(16))) bf16 lds[kL];
+  if ((int)blockIdx.x >= nconv) {
+    wslab_reduce_blocks<kRedU>(red, (int)blockIdx.x - nconv, (int)gridDim.x - nconv);
+    return;
+  }
+  long long r_entry = 0;
+  if constexpr (DIAG & 4) r_entry = __builtin_amdgcn_s_memrealtime();
+  const int lane = lane_id();
+  const int w = wave_id();
+  const int grp = w >> 2;  // wave-uniform: waves w and w + 4 share a SIMD
+  const int wl = w & 3;
+  const int wm = grp * 2 + (wl & 1), wn = wl >> 1;
+  const int nblk_m = (M + kPPBM - 1) / kPPBM;
+  const int bid = xcd_remap(blockIdx.x, nconv);
+  const int bm = bid % nblk_m, bn = bid / nblk_m;
+  const int m0 = bm * kPPBM;
+  const int n0 = bn * kBN;
+  const int S2 = S * S;
+  auto prow = [&](int m) {
+    const int b = m / S2;
+    const int rem = m - b * S2;
+    const int i = rem / S;
+    const int j = rem - i * S;
+    return (long)(b * WI + i + shift) * WI + j + shift;
+  };
+  const long base = prow(m0);
+  const long tap_stride = (long)WROWS * CIN;
+  const int lrow = lane >> 2, lcol = lane & 3;
+
+  // group 0's weight sources (row (wl + 4k)*16 + lane/4 of the 192-row tile)
+  const bf16* bsrc[kPPBL];
+#pragma unroll
+  for (int k = 0; k < kPPBL; ++k) {
+    const int r = (wl + 4 * k) * 16 + lrow;
+    bsrc[k] = Wt + (long)(n0 + r) * CIN + ((lcol ^ swz4(r)) * 8);
+  }
+  auto stage_a = [&](int q) {  // slab of chunk q: rows (wl + 4k)*16 .. +15 per glds
+    bf16* dst = lds + (q & 1) * kPPSlab;
+#pragma unroll
+    for (int k = 0; k < kPPAL; ++k) {
+      const int r = (wl + 4 * k) * 16 + lrow;
+      long g = base + r;
+      g = g < total_rows ? g : total_rows - 1;
+      glds16(X + g * CIN + ((lcol ^ swz4(r)) * 8) + q * kBK, dst + (wl + 4 * k) * 16 * kBK);
+    }
+  };
+  auto stage_b = [&](int s) {  // step s = chunk * 9 + tap
+    const int q = s / 9, t = s - q * 9;
+    bf16* dst = lds + 2 * kPPSlab + (s % NB) * kBTile;
+    const long off = t * tap_stride + q * kBK;
+#pragma unroll
+    for (int k = 0; k < kPPBL; ++k) glds16(bsrc[k] + off, dst + (wl + 4 * k) * 16 * kBK);
+  };
+
+  const int frow = lane & 15;
+  const int fq = lane >> 4;
+  int prel[kMT];
+#pragma unroll
+  for (int i = 0; i < kMT; ++i) {
+    int m = m0 + wm * (16 * kMT) + i * 16 + frow;
+    m = m < M ? m : M - 1;
+    prel[i] = (int)(prow(m) - base);
+  }
+  int boffs[kNT];
+#pragma unroll
+  for (int j = 0; j < kNT; ++j) {
+    const int row = wn * (16 * kNT) + j * 16 + frow;
+    boffs[j] = row * kBK + ((fq ^ swz4(row)) * 8);
+  }
+
+  f32x4 acc[kNT][kMT];
+#pragma unroll
+  for (int j = 0; j < kNT; ++j)
+#pragma unroll
+    for (int i = 0; i < kMT; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int cchunks = CIN / kBK;
+  const int nsteps = 9 * cchunks;
+  bf16x8 xa[kMT], wb[kNT];
+  auto read_frags = [&](int s) {
+    if constexpr (DIAG & 2) {
+      asm volatile("" : "+v"(xa[0]), "+v"(wb[0]));
+      return;
+    }
+    const int q = s / 9, t = s - q * 9;
+    const bf16* slab = lds + (q & 1) * kPPSlab;
+    const bf16* bt = lds + 2 * kPPSlab + (s % NB) * kBTile;
+    const int ky = t / 3, kx = t - ky * 3;
+    const int toff = ky * WI + kx;
+#pragma unroll
+    for (int i = 0; i < kMT; ++i) {
+      const int r = prel[i] + toff;
+      xa[i] = *reinterpret_cast<const bf16x8*>(slab + r * kBK + ((fq ^ swz4(r)) * 8));
+    }
+#pragma unroll
+    for (int j = 0; j < kNT; ++j) wb[j] = *reinterpret_cast<const bf16x8*>(bt + boffs[j]);
+    lds_reads_done();  // retire this burst before the wave's next barrier (WAR on the LDS)
+  };
+  auto mfmas = [&]() {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int j = 0; j < kNT; ++j)
+#pragma unroll
+      for (int i = 0; i < kMT; ++i) acc[j][i] = mfma16(wb[j], xa[i], acc[j][i]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // MFMA segment with staging loads issued between its MFMA rows (ISSUE = 1)
+  auto mfmas_staged = [&](int sb) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int j = 0; j < kNT; ++j) {
+#pragma unroll
+      for (int i = 0; i < kMT; ++i) acc[j][i] = mfma16(wb[j], xa[i], acc[j][i]);
+      if (j < kPPBL && sb >= 0) {
+        const int q = sb / 9, t = sb - q * 9;
+        bf16* dst = lds + 2 * kPPSlab + (sb % NB) * kBTile;
+        glds16(bsrc[j] + t * tap_stride + q * kBK, dst + (wl + 4 * j) * 16 * kBK);
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  long long t0 = 0, r0 = 0;
+  if constexpr (DIAG & 4) {
+    t0 = __builtin_amdgcn_s_memtime();
+    r0 = __builtin_amdgcn_s_memrealtime();
+  }
+  if constexpr (DIAG & 2) {  // random-looking operands (zeros would let the clock rise)
+#pragma unroll
+    for (int i = 0; i < kMT; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) xa[i][e] = (bf16)(((lane * 37 + i * 11 + e * 5) % 29) * 0.07f - 1.f);
+#pragma unroll
+    for (int j = 0; j < kNT; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) wb[j][e] = (bf16)(((lane * 13 + j * 7 + e * 3) % 31) * 0.06f - 0.9f);
+  }
+  // DIAG & 8: per-wave cycle accounting of the loop's segments (s_memtime), lane 0 of waves 0 / 4
+  long long acc_t[5] = {0, 0, 0, 0, 0};
+  auto now = [&]() -> long long {
+    if constexpr (DIAG & 8) return __builtin_amdgcn_s_memtime();
+    return 0;
+  };
+  // Staging split between the groups, each in its own read phase: group 0 stages the slab (10 glds
+  // per wave per chunk, at tap 0), group 1 the weight tiles (3 glds per wave per step, after its
+  // fragment reads). Each group waits only for its own loads, before the barrier that precedes
+  // the first read of that data (always group 0's, at the next X barrier).
+  if (grp == 0) {
+    stage_a(0);
+    wait_vm<0>();
+#pragma unroll 1
+    for (int s = 0; s < nsteps; ++s) {
+      const int q = s / 9, t = s - q * 9;
+      const bool more = q + 1 < cchunks;
+      const long long c1 = now();
+      __builtin_amdgcn_s_barrier();  // X_s
+      asm volatile("" ::: "memory");
+      const long long c2 = now();
+      if constexpr (!(DIAG & 1)) {
+        if (t == 0 && more) stage_a(q + 1);
+      }
+      read_frags(s);
+      const long long c3 = now();
+      __builtin_amdgcn_s_barrier();  // Y_s
+      asm volatile("" ::: "memory");
+      const long long c4 = now();
+      mfmas();
+      const long long c5 = now();
+      if (t == 8 && more) wait_vm<0>();  // slab(q+1) complete before X of the next chunk
+      const long long c6 = now();
+      if constexpr (DIAG & 8) {  // X wait, stage+read, Y wait, MFMA issue, vm wait
+        acc_t[0] += c2 - c1;
+        acc_t[1] += c3 - c2;
+        acc_t[2] += c4 - c3;
+        acc_t[3] += c5 - c4;
+        acc_t[4] += c6 - c5;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < D; ++k)
+      if (k < nsteps) stage_b(k);
+    wait_vm_rt((nsteps - 1 < D - 1 ? nsteps - 1 : D - 1) * kPPBL);  // B(0) complete
+#pragma unroll 1
+    for (int s = 0; s < nsteps; ++s) {
+      const long long c0 = now();
+      __builtin_amdgcn_s_barrier();  // X_s
+      asm volatile("" ::: "memory");
+      const long long c1 = now();
+      if constexpr (ISSUE && !(DIAG & 1)) {
+        // step s - 1's MFMAs carry the loads of B(s - 1 + D)
+        if (s > 0) mfmas_staged(s - 1 + D < nsteps ? s - 1 + D : -1);
+      } else {
+        if (s > 0) mfmas();          // step s - 1, beside group 0's reads of step s
+      }
+      const long long c2 = now();
+      __builtin_amdgcn_s_barrier();  // Y_s
+      asm volatile("" ::: "memory");
+      const long long c3 = now();
+      read_frags(s);                 // beside group 0's MFMAs of step s
+      const long long c4 = now();
+      if constexpr (!(DIAG & 1)) {
+        if constexpr (ISSUE) {
+          // B(s+1) complete before X_{s+1}: issued so far are B(.. min(s-1+D, nsteps-1))
+          int last = s - 1 + D < nsteps - 1 ? s - 1 + D : nsteps - 1;
+          const int yb = last - (s + 1);
+          wait_vm_rt(yb > 0 ? yb * kPPBL : 0);
+        } else {
+          if (s + D < nsteps) stage_b(s + D);
+          // B(s+1) complete before X_{s+1}: younger are B(s+2 .. min(s+D, nsteps-1))
+          int yb = nsteps - 2 - s;
+          yb = yb < D - 1 ? yb : D - 1;
+          wait_vm_rt(yb > 0 ? yb * kPPBL : 0);
+        }
+      }
+      const long long c5 = now();
+      if constexpr (DIAG & 8) {  // X wait, MFMA issue, Y wait, read, stage + vm wait
+        acc_t[0] += c1 - c0;
+        acc_t[1] += c2 - c1;
+        acc_t[2] += c3 - c2;
+        acc_t[3] += c4 - c3;
+        acc_t[4] += c5 - c4;
+      }
+    }
+    mfmas();
+  }
+  if constexpr (DIAG & 8) {
+    if (lane == 0 && (w == 0 || w == 4) && stamps) {
+      long long* o = stamps + 6 * 4096 + (size_t)blockIdx.x * 10 + (w == 4 ? 5 : 0);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) o[k] = acc_t[k];
+    }
+  }
+  long long t1 = 0, r1 = 0;
+  if constexpr (DIAG & 4) {
+    t1 = __builtin_amdgcn_s_memtime();
+    r1 = __builtin_amdgcn_s_memrealtime();
+  }
+  if (res) {
+    epilogue(acc, m0 + wm * (16 * kMT), n0 + wn * (16 * kNT), M, S, WO, HO, YC, HM, bias, res,
+             relu, mask, Y, frow, fq);
+  } else {
+    __syncthreads();  // every wave is past its last LDS read: the ring becomes the output image
+    epilogue_lds<kPPBM>(acc, lds, wm * (16 * kMT), wn * (16 * kNT), m0, n0, M, S, WO, HO, YC, HM,
+                        bias, relu, mask, Y, frow, fq);
+  }
+  if constexpr (DIAG & 4) {
+    // per block: loop cycles, loop ticks, then absolute ticks at entry / loop start / loop end /
+    // exit (wave 0; 100 MHz)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const long long r2 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0 && stamps) {
+      long long* o = stamps + 6 * blockIdx.x;
+      o[0] = t1 - t0;
+      o[1] = r1 - r0;
+      o[2] = r_entry;
+      o[3] = r0;
+      o[4] = r1;
+      o[5] = r2;
+    }
+  }
+}
+
 int g_tap_mode = -1;  // -1: read RAG_CONV_TAP on first use (default on)
+int g_ep_lds_override = -1;  // rag_conv_ep_lds(): A/B switch of conv_tap_kernel's epilogue
 
 // Worst-case slab extent of a bm-pixel run (host check of the kernels' slab-row assumptions).
 int max_slab_rows(int S, int WI, int shift, int bm) {
@@ -554,7 +927,56 @@ int max_slab_rows(int S, int WI, int shift, int bm) {
   return (int)mx;
 }
 
+long long* g_stamps = nullptr;
 }  // namespace
+
+// Diagnostic launches of the ping-pong kernel (results are WRONG for diag 1-3): diag bit 0 = no
+// staging, bit 1 = no fragment reads; every diag launch records per-block (cycles, 100 MHz ticks)
+// of the main loop, read back with rag_conv_diag_stamps. 3x3 forward/dgrad shapes only.
+RAG_API int rag_conv_pp_diag(int diag, const void* X, const void* W, const float* bias, void* Y,
+                             const void* mask, int B, int S, int HI, int HO, int CIN, int COUTP,
+                             int YC, int relu, int HM, hipStream_t stream) {
+  if (!g_stamps && hipMalloc(&g_stamps, 16 * 4096 * sizeof(long long)) != hipSuccess) return -3;
+  const int M = B * S * S, WI = S + 2 * HI, WO = S + 2 * HO, shift = HI - 1;
+  const int nconv = ((M + kPPBM - 1) / kPPBM) * (COUTP / kBN);
+  if (nconv > 4096 || COUTP % kBN || CIN % kBK) return -1;
+  const long total = (long)B * WI * WI;
+  const bf16 *x = (const bf16*)X, *w = (const bf16*)W, *mk = (const bf16*)mask;
+  bf16* y = (bf16*)Y;
+  WgradRed r{};
+#define RAG_PPD(D)                                                                               \
+  conv_tap_pp_kernel<4, D><<<nconv, 512, 0, stream>>>(x, w, bias, y, mk, nullptr, M, S, WI,      \
+                                                      shift, WO, HO, CIN, COUTP, YC, relu, HM,  \
+                                                      total, nconv, r, g_stamps)
+  switch (diag & 11) {
+    case 0: RAG_PPD(4); break;
+    case 1: RAG_PPD(5); break;
+    case 2: RAG_PPD(6); break;
+    case 3: RAG_PPD(7); break;
+    default: RAG_PPD(12); break;  // 8: segment accounting of the full kernel
+  }
+#undef RAG_PPD
+  return (int)hipGetLastError();
+}
+
+RAG_API int rag_conv_diag_stamps(long long* host, int nblocks) {
+  if (!g_stamps) return -1;
+  if (hipDeviceSynchronize() != hipSuccess) return -2;
+  return (int)hipMemcpy(host, g_stamps, 6 * nblocks * sizeof(long long), hipMemcpyDeviceToHost);
+}
+
+RAG_API int rag_conv_diag_segments(long long* host, int nblocks) {
+  if (!g_stamps) return -1;
+  if (hipDeviceSynchronize() != hipSuccess) return -2;
+  return (int)hipMemcpy(host, g_stamps + 6 * 4096, 10 * nblocks * sizeof(long long),
+                        hipMemcpyDeviceToHost);
+}
+
+RAG_API int rag_conv_ep_lds(int on) {
+  const int old = g_ep_lds_override;
+  g_ep_lds_override = on;
+  return old;
+}
 
 RAG_API int rag_conv_tap_mode(int mode) {
   const int old = g_tap_mode;
@@ -566,9 +988,11 @@ RAG_API int rag_conv_tap_mode(int mode) {
 // input channels a multiple of 32, and every 192-pixel run's nine-tap slab fits kSlabRows.
 // Returns true if a tap-slab kernel handled the launch: 3x3, 192-multiple output channels,
 // input channels a multiple of 32, and every pixel run's nine-tap slab fits the kernel's slab.
-// Mode (RAG_CONV_TAP / rag_conv_tap_mode): 0 off, 1 = 4-wave 192-pixel kernel (default),
+// Mode (RAG_CONV_TAP / rag_conv_tap_mode): 0 off, 1 = 4-wave 192-pixel kernel (round-2 default),
 // 2 / 3 = 8-wave 384-pixel kernel with a 4- / 5-deep weight ring (measured slower: docs/KERNELS.md),
-// 4 = 8-wave 192-pixel kernel, four waves per SIMD (conv_tap16_kernel).
+// 4 = 8-wave 192-pixel kernel, four waves per SIMD (conv_tap16_kernel), 5 / 6 / 7 = ping-pong
+// 8-wave 384-pixel kernel with a 4- / 3- / 5-deep weight ring (conv_tap_pp_kernel; 6 = default),
+// 8 / 9 = the same with the weight loads issued inside the MFMA segment (measured slower).
 int rag_launch_wgrad_slab_reduce(const WgradRed& r, hipStream_t stream);  // wgrad_slab.hip
 
 bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* y,
@@ -577,7 +1001,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
                          hipStream_t stream, const WgradRed* red) {
   if (g_tap_mode < 0) {
     const char* e = getenv("RAG_CONV_TAP");
-    g_tap_mode = e ? atoi(e) : 1;
+    g_tap_mode = e ? atoi(e) : 6;  // ping-pong, 3-deep ring: profiles/conv_pp_r3.txt
   }
   if (!g_tap_mode || KS != 3 || COUTP % kBN || CIN % kBK || CIN < kBK) return false;
   static int cached_key = -1, cached_rows = 0, cached_rows8 = 0;
@@ -599,6 +1023,37 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
                                                     HO, CIN, COUTP, YC, relu, HM, total_rows);
     return true;
   }
+  if ((g_tap_mode >= 5 && g_tap_mode <= 9) && cached_rows8 <= kPPSlabRows) {
+    // ping-pong kernel: one block per CU; reduce blocks fill the CUs its last round leaves free
+    const int nconv = ((M + kPPBM - 1) / kPPBM) * (COUTP / kBN);
+    int nred = 0;
+    WgradRed r{};
+    if (red) {
+      r = *red;
+      nred = std::max(8, (256 - nconv % 256) % 256);
+    }
+    if (g_tap_mode == 5)
+      conv_tap_pp_kernel<4><<<nconv + nred, 512, 0, stream>>>(
+          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
+          nconv, r);
+    else if (g_tap_mode == 7)
+      conv_tap_pp_kernel<5><<<nconv + nred, 512, 0, stream>>>(
+          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
+          nconv, r);
+    else if (g_tap_mode == 8)
+      conv_tap_pp_kernel<3, 0, 1><<<nconv + nred, 512, 0, stream>>>(
+          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
+          nconv, r);
+    else if (g_tap_mode == 9)
+      conv_tap_pp_kernel<4, 0, 1><<<nconv + nred, 512, 0, stream>>>(
+          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
+          nconv, r);
+    else
+      conv_tap_pp_kernel<3><<<nconv + nred, 512, 0, stream>>>(
+          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
+          nconv, r);
+    return true;
+  }
   if (cached_rows > kSlabRows) return false;
   const int nblk_m = (M + kBM - 1) / kBM;
   dim3 grid(nblk_m * (COUTP / kBN));
@@ -616,8 +1071,13 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
     r = *red;
     nred = std::min(64, std::max(8, 2 * 256 - nconv));
   }
+  static const int ep_lds = [] {  // RAG_EP_LDS=0: the register epilogue (A/B)
+    const char* e = getenv("RAG_EP_LDS");
+    return e ? atoi(e) : 1;
+  }();
   conv_tap_kernel<<<nconv + nred, 256, 0, stream>>>(x, w, bias, y, mk, res, M, S, WI, shift, WO,
                                                     HO, CIN, COUTP, YC, relu, HM, total_rows,
-                                                    nconv, r);
+                                                    nconv, r, g_ep_lds_override >= 0
+                                                                  ? g_ep_lds_override : ep_lds);
   return true;
 }

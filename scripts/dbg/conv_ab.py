@@ -1,7 +1,8 @@
 """A/B of the forward/dgrad conv kernels in one process, interleaved rounds (guide rule 24):
 variant 0 = conv_pipe tap-major, 1 = conv_pipe channel-chunk-major, 2 = conv_tap (tap-shared
-slab, 3x3 only), 3 / 4 = 8-wave 384-pixel conv_tap8 with a 4- / 5-deep weight ring (variant v
-selects rag_conv_tap_mode(v - 1)). 3x3 192->192 fwd and dgrad and 5x5 48->192 fwd at B=256, plus an output check
+slab, 3x3 only), 3 / 4 = 8-wave 384-pixel conv_tap8 with a 4- / 5-deep weight ring, 6 / 7 = ping-pong
+conv_tap_pp with a 4- / 3-deep ring, 8 = conv_tap_pp with a 5-deep ring (variant v selects
+rag_conv_tap_mode(v - 1)), 99 = conv_tap with the register epilogue instead of the LDS-staged one. 3x3 192->192 fwd and dgrad and 5x5 48->192 fwd at B=256, plus an output check
 of every variant against an fp32 torch reference."""
 import json
 import os
@@ -53,8 +54,10 @@ VARIANTS = tuple(int(v) for v in os.environ.get("VARIANTS", "1,2,3,4").split(","
 
 
 def select(v):
-    _lib().rag_conv_tap_mode(max(v - 1, 0))
+    # v = 99: conv_tap (mode 1) with the round-2 register epilogue (RAG_EP_LDS A/B)
+    _lib().rag_conv_tap_mode(1 if v == 99 else max(v - 1, 0))
     _lib().rag_conv_order(1 if v >= 1 else 0)
+    _lib().rag_conv_ep_lds(0 if v == 99 else -1)
 
 
 out = {}

@@ -1,14 +1,24 @@
-"""Per-step kernel time of a training step from a rocprofv3 kernel trace: steps are delimited by
-the input-packing kernel; prints the median step's kernels (time, count) and the step's busy
-fraction."""
+"""Per-step kernel time of a training step from a rocprofv3 kernel trace (CSV, or the rocpd
+SQLite database rocprofv3 writes by default): steps are delimited by the input-packing kernel;
+prints the median step's kernels (time, count) and the step's busy fraction."""
 import csv
 import sys
 
 
-def main(path, marker="pack_input_kernel"):
+def load(path):
+    """(start ns, end ns, kernel name) from a rocprofv3 kernel-trace CSV or rocpd database."""
+    if path.endswith(".db"):
+        import sqlite3
+        c = sqlite3.connect(path)
+        return sorted((int(s), int(e), n) for s, e, n in
+                      c.execute("select start, end, name from kernels"))
     rows = list(csv.DictReader(open(path)))
-    ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
-                for r in rows)
+    return sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
+                  for r in rows)
+
+
+def main(path, marker="pack_input_kernel"):
+    ks = load(path)
     starts = [s for s, e, n in ks if marker in n]
     steps = list(zip(starts, starts[1:]))[-8:]
     a, b = sorted(steps, key=lambda ab: ab[1] - ab[0])[len(steps) // 2]
