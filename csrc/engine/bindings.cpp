@@ -19,9 +19,7 @@ int convert_sgf_game(const char* text, size_t len, int bd_size,
                      const std::shared_ptr<const Zobrist>& zob, const int* fids, int nf,
                      std::vector<uint8_t>& states, std::vector<uint8_t>& actions);
 void register_rollout(py::module_& m);
-}  // namespace rag
-
-namespace {
+void register_gamebatch(py::module_& m);
 
 std::shared_ptr<const Zobrist> make_zobrist(py::array_t<uint64_t, py::array::c_style> w,
                                            py::array_t<uint64_t, py::array::c_style> b) {
@@ -30,6 +28,9 @@ std::shared_ptr<const Zobrist> make_zobrist(py::array_t<uint64_t, py::array::c_s
   z->black.assign(b.data(), b.data() + b.size());
   return z;
 }
+}  // namespace rag
+
+namespace {
 
 py::array_t<int8_t> board_array(const Board& b) {
   const int S = b.size();
@@ -406,5 +407,6 @@ PYBIND11_MODULE(_rocgo, m) {
       py::arg("block"), py::arg("chunk"), py::arg("nthreads") = 8);
 
   register_search(m);
+  register_gamebatch(m);
   register_rollout(m);
 }

@@ -54,6 +54,7 @@
 #include <sys/mman.h>
 
 #include "../engine/go_engine.hpp"
+#include "../engine/pack.hpp"
 #include "../engine/thread_pool.hpp"
 #include "rollout.hpp"
 
@@ -238,18 +239,6 @@ using mcts_detail::N_PENDING;
 // 19x19 simulations per move; pages become resident only as they are written.
 constexpr size_t kNodeCap = size_t(1) << 25;
 constexpr size_t kEdgeCap = size_t(1) << 27;
-
-// Output views of pack_inputs(): a null pointer skips that output; `stride` is the distance in
-// bytes between consecutive leaves (rows), so outputs may be columns of one record array.
-struct PackOut {
-  int8_t* colors = nullptr;    // [P]
-  int16_t* ages = nullptr;     // [P] stone ages (-1 empty, clamped to 32767)
-  int32_t* meta4 = nullptr;    // player, ko, superko flag, 0
-  int32_t* meta8 = nullptr;    // rollout kernel meta (see rollout_inputs)
-  uint8_t* illegal = nullptr;  // [P] positional-superko-illegal points (superko boards)
-  uint8_t* ladders = nullptr;  // [2][P] ladder capture / escape planes
-  size_t s_colors = 0, s_ages = 0, s_meta4 = 0, s_meta8 = 0, s_illegal = 0, s_ladders = 0;
-};
 
 class Search {
  public:
@@ -617,42 +606,7 @@ class Search {
   // host-read ladder planes / superko-illegal masks.
   void pack_inputs(int id, const PackOut& o) {
     Wave& wv = wave(id);
-    const int n = (int)wv.leaves.size();
-    const int P = root_board_.npoints();
-    pool_.run(n, [&](int i) {
-      const Board& b = wv.leaves[i].board;
-      if (o.colors) {
-        int8_t* c = reinterpret_cast<int8_t*>(reinterpret_cast<char*>(o.colors) + i * o.s_colors);
-        for (int p = 0; p < P; ++p) c[p] = (int8_t)b.color(p);
-      }
-      if (o.ages) {
-        int16_t* a = reinterpret_cast<int16_t*>(reinterpret_cast<char*>(o.ages) + i * o.s_ages);
-        for (int p = 0; p < P; ++p) a[p] = (int16_t)std::min(b.stone_age(p), 32767);
-      }
-      if (o.meta4) {
-        int32_t* m = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(o.meta4) + i * o.s_meta4);
-        m[0] = b.current_player();
-        m[1] = b.ko();
-        m[2] = b.enforce_superko() ? 1 : 0;
-        m[3] = 0;
-      }
-      if (o.meta8) {
-        int32_t* m = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(o.meta8) + i * o.s_meta8);
-        write_meta8(b, m);
-      }
-      if (o.illegal) {
-        uint8_t* il = o.illegal + i * o.s_illegal;
-        for (int p = 0; p < P; ++p)
-          il[p] = (b.enforce_superko() && b.color(p) == EMPTY && p != b.ko() &&
-                   !b.is_suicide(p) && b.is_positional_superko(p))
-                      ? 1 : 0;
-      }
-      if (o.ladders) {
-        thread_local LadderReader reader;
-        uint8_t* l0 = o.ladders + i * o.s_ladders;
-        ladder_planes(b, l0, l0 + P, &reader);
-      }
-    });
+    pool_.run((int)wv.leaves.size(), [&](int i) { pack_board(wv.leaves[i].board, i, o); });
   }
 
   // ------------------------------------------------------------------ value backup
@@ -750,17 +704,6 @@ class Search {
     o.s_meta8 = 8 * sizeof(int32_t);
     pack_inputs(id, o);
   }
-  static void write_meta8(const Board& b, int32_t* m) {
-    m[0] = b.current_player();
-    m[1] = b.ko();
-    m[2] = b.last1();
-    m[3] = b.last2();
-    m[4] = b.passes_black();
-    m[5] = b.passes_white();
-    m[6] = b.nmoves();
-    m[7] = b.end_of_game() ? 1 : 0;
-  }
-
   // black_z: mean rollout result per leaf from BLACK's point of view
   void backup_rollout(int id, const float* black_z) {
     Wave& wv = wave(id);

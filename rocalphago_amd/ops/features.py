@@ -79,9 +79,10 @@ class GpuFeatures(object):
         colors, ages, meta, illegal, lad = _rg.gpu_feature_inputs(boards, host, self.nthreads)
         return self.from_arrays(colors, ages, meta, illegal, lad, out, sens_out)
 
-    def run(self, c, a, m, il, ld, n, S, out=None):
+    def run(self, c, a, m, il, ld, n, S, out=None, sens_out=None):
         """Planes from device inputs (colours [n, S*S] int8, ages int16, meta [n, 4] int32,
-        superko-illegal mask or None, ladder planes [n, 2, S*S] or None: read on the GPU)."""
+        superko-illegal mask or None, ladder planes [n, 2, S*S] or None: read on the GPU);
+        with ``sens_out`` (uint8, n*S*S elements) also the sensibleness mask."""
         if self.ladders and ld is None:
             ld, self._work = gpu_ladders(c, m, S, work=self._work)
         if out is None:
@@ -89,7 +90,19 @@ class GpuFeatures(object):
         _check(_lib().rag_features(_ptr(c), _ptr(a), _ptr(m), _ptr(il), _ptr(ld), n, S,
                                    _ptr(self.fids_dev), len(self.fids), self.F, _ptr(out),
                                    _stream()), "features")
+        if sens_out is not None:
+            self._sensibleness(c, a, m, il, n, S, sens_out)
         return out
+
+    def _sensibleness(self, c, a, m, il, n, S, sens_out):
+        if sens_out.numel() != n * S * S or sens_out.dtype != torch.uint8:
+            raise ValueError("sens_out must be uint8 with n*S*S elements")
+        if self._sens_fid is None:
+            self._sens_fid = torch.tensor([_FID["sensibleness"]], dtype=torch.int32,
+                                          device=self.device)
+        _check(_lib().rag_features(_ptr(c), _ptr(a), _ptr(m), _ptr(il), None, n, S,
+                                   _ptr(self._sens_fid), 1, 1, _ptr(sens_out), _stream()),
+               "features(sensibleness)")
 
     def from_arrays(self, colors, ages, meta, illegal, lad, out=None, sens_out=None):
         """Planes from the native inputs directly: colours [n, S*S] int8, stone ages int16,
@@ -101,14 +114,4 @@ class GpuFeatures(object):
         if illegal is not None and not np.any(illegal):
             illegal = None
         c, a, m, il, ld = (_h2d(x, self.device) for x in (colors, ages, meta, illegal, lad))
-        out = self.run(c, a, m, il, ld, n, S, out)
-        if sens_out is not None:
-            if sens_out.numel() != n * S * S or sens_out.dtype != torch.uint8:
-                raise ValueError("sens_out must be uint8 with n*S*S elements")
-            if self._sens_fid is None:
-                self._sens_fid = torch.tensor([_FID["sensibleness"]], dtype=torch.int32,
-                                              device=self.device)
-            _check(_lib().rag_features(_ptr(c), _ptr(a), _ptr(m), _ptr(il), None, n, S,
-                                       _ptr(self._sens_fid), 1, 1, _ptr(sens_out), _stream()),
-                   "features(sensibleness)")
-        return out
+        return self.run(c, a, m, il, ld, n, S, out, sens_out)

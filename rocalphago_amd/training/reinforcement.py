@@ -6,8 +6,10 @@ Same CLI and output contract (``weights.00000.hdf5`` copy of the initial weights
 written with sort_keys + indent 2; ``--resume``).
 
 Self-play: all unfinished games advance in lock-step; each ply is ONE batched policy evaluation
-(native multi-threaded feature extraction + HIP forward) for every game in which that player is
-to move.
+for every game in which that player is to move. On a GPU the games live in a native
+``GameBatch`` and a ply is one native pack + one GPU pass (features, policy, sampling) + one
+native move application for all games (training/selfplay.py); otherwise GameState objects and
+the players' ``get_moves``.
 
 Update semantics (quirk Q7, the reference's *intended* behaviour): every game contributes the
 gradient of its mean REINFORCE log-loss over the learner's positions with learning-rate sign +1
@@ -104,12 +106,21 @@ def run_n_games(optimizer, learner, opponent, num_games, mock_states=[], mode="p
         raise ValueError("mode='per_game' cannot run data-parallel (WORLD_SIZE > 1); use "
                          "mode='batched' (one all-reduced REINFORCE update per game batch)")
     board_size = learner.policy.model.input_shape[-1]
-    states = [go.GameState(size=board_size) for _ in range(num_games)]
-    if mock_states:
-        states = mock_states
     model = learner.policy.model
-    feats, moves, learner_color = _play_games(learner, opponent, states, num_games)
-    won = [st.get_winner() == c for st, c in zip(states, learner_color)]
+    from .selfplay import NativeSelfPlay
+    if not mock_states and os.environ.get("RAG_NATIVE_SELFPLAY", "1") == "1" and \
+            NativeSelfPlay.supported(learner, opponent):
+        # games kept native, one GPU pass + one native call per ply (training/selfplay.py)
+        sp = NativeSelfPlay(learner, opponent)
+        feats, moves, learner_color, winners = sp.play(num_games, board_size)
+        won = [int(w) == c for w, c in zip(winners, learner_color)]
+        run_n_games.last_stats = sp.stats
+    else:
+        states = [go.GameState(size=board_size) for _ in range(num_games)]
+        if mock_states:
+            states = mock_states
+        feats, moves, learner_color = _play_games(learner, opponent, states, num_games)
+        won = [st.get_winner() == c for st, c in zip(states, learner_color)]
     S2 = board_size * board_size
     if mode == "per_game":
         for f, m, w in zip(feats, moves, won):

@@ -25,8 +25,14 @@ def main():
     ap.add_argument("--window", type=float, default=0.25)
     ap.add_argument("--long", default="rollout")
     a = ap.parse_args()
-    rows = list(csv.DictReader(open(a.trace)))
-    ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows]
+    if a.trace.endswith(".db"):  # rocpd SQLite (rocprofv3's default output)
+        import sqlite3
+        ks = [(int(s), int(e), n) for s, e, n in
+              sqlite3.connect(a.trace).execute("select start, end, name from kernels")]
+    else:
+        rows = list(csv.DictReader(open(a.trace)))
+        ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
+              for r in rows]
     end = max(e for _, e, _ in ks)
     t0 = end - int(a.window * 1e9)
     ks = [(max(s, t0), e, n) for s, e, n in ks if e > t0]
