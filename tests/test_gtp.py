@@ -3,6 +3,7 @@ match harness (interface/TestPlay.py)."""
 import io
 import multiprocessing as mp
 
+import numpy as np
 import pytest
 
 from rocalphago_amd.engine.gamestate import BLACK, WHITE, GameState
@@ -152,3 +153,39 @@ def test_recommended_handicaps_are_legal(n):
     vs = [gtp.parse_vertex(v) for v in gtp.ExtendedGtpEngine.recommended_handicaps[n].split()]
     st.place_handicaps([(x - 1, y - 1) for x, y in vs])
     assert len(st.handicaps) == n
+
+
+def test_match_vectorised_eyeish_matches_engine_rule():
+    """match.eyeish_owner (whole board at once) == GameState.is_eyeish point by point."""
+    from rocalphago_amd.gtp.match import eyeish_owner
+    rs = np.random.RandomState(4)
+    for size in (5, 9, 19):
+        st = GameState(size=size)
+        for _ in range(size * size // 2):
+            legal = st.get_legal_moves(include_eyes=True)
+            st.do_move(legal[rs.randint(len(legal))] if legal else None)
+        own = eyeish_owner(st.board)
+        for x in range(size):
+            for y in range(size):
+                want = BLACK if st.is_eyeish((x, y), BLACK) else \
+                    (WHITE if st.is_eyeish((x, y), WHITE) else 0)
+                assert own[x, y] == want
+
+
+def test_match_board_text_format():
+    """showboard layout (reference TestPlay.py:80-134 docstring): axis letters, x/o stones,
+    the last move in capitals and its mover after the first row."""
+    from rocalphago_amd.gtp.match import render_board
+    st = GameState(size=7)
+    for mv in [(3, 2), (2, 4), (1, 1)]:
+        st.do_move(mv)
+    assert render_board(st).split("\n") == [
+        "  a b c d e f g   ",
+        "a . . . . . . . a     ;B(bb)",
+        "b . B . . . . . b ",
+        "c . . . x . . . c ",
+        "d . . . . . . . d ",
+        "e . . o . . . . e ",
+        "f . . . . . . . f ",
+        "g . . . . . . . g ",
+        "  a b c d e f g   "]
