@@ -18,6 +18,9 @@ void register_search(py::module_& m);
 int convert_sgf_game(const char* text, size_t len, int bd_size,
                      const std::shared_ptr<const Zobrist>& zob, const int* fids, int nf,
                      std::vector<uint8_t>& states, std::vector<uint8_t>& actions);
+int replay_sgf_positions(const char* text, size_t len, int bd_size,
+                         const std::shared_ptr<const Zobrist>& zob, std::vector<Board>& boards,
+                         std::vector<uint8_t>& actions);
 void register_rollout(py::module_& m);
 void register_gamebatch(py::module_& m);
 
@@ -290,8 +293,11 @@ PYBIND11_MODULE(_rocgo, m) {
       py::arg("board"), py::arg("copying") = false);
 
   // Bulk SGF conversion (converter.cpp): games converted in parallel on the shared pool.
-  // Returns one (status, states uint8 [n, F, S, S], actions uint8 [n, 2]) per game; status 0 ok,
-  // 1 illegal move (positions up to and including it), 3 = convert this game in python.
+  // Converts a batch of SGF texts in parallel (dynamic scheduling over games). Returns
+  // (status int32 [n], rows int64 [n], states uint8 [sum rows, F, S, S], actions uint8
+  // [sum rows, 2]): the games' rows in batch order in ONE block (filled by a parallel copy), so
+  // the writer appends it without any per-game concatenation. Status 0 ok, 1 illegal move
+  // (positions up to and including it), 3 = convert this game in python (no rows).
   m.def(
       "convert_games",
       [](const std::vector<py::bytes>& texts, const std::vector<int>& fids, int bd_size,
@@ -301,29 +307,47 @@ PYBIND11_MODULE(_rocgo, m) {
         const int n = (int)texts.size();
         std::vector<std::string> buf(n);
         for (int i = 0; i < n; ++i) buf[i] = texts[i];
-        std::vector<std::vector<uint8_t>> st(n), ac(n);
-        std::vector<int> status(n, 0);
-        {
+        std::vector<std::vector<Board>> bd(n);
+        std::vector<std::vector<uint8_t>> ac(n);
+        py::array_t<int32_t> status(n);
+        py::array_t<int64_t> rows(n);
+        int32_t* sp = status.mutable_data();
+        int64_t* rp = rows.mutable_data();
+        {  // 1: parse + replay every game (boards copied at the training positions)
           py::gil_scoped_release nogil;
           parallel_for(n, nthreads, [&](int i) {
-            status[i] = convert_sgf_game(buf[i].data(), buf[i].size(), bd_size, zob, fids.data(),
-                                         (int)fids.size(), st[i], ac[i]);
+            sp[i] = replay_sgf_positions(buf[i].data(), buf[i].size(), bd_size, zob, bd[i], ac[i]);
+            if (sp[i] == 3) {
+              bd[i].clear();
+              ac[i].clear();
+            }
+            rp[i] = (int64_t)(ac[i].size() / 2);
           });
         }
         const int F = total_planes(fids), P = bd_size * bd_size;
-        py::list out;
-        for (int i = 0; i < n; ++i) {
-          const py::ssize_t rows = (py::ssize_t)(ac[i].size() / 2);
-          py::array_t<uint8_t> sa({rows, (py::ssize_t)F, (py::ssize_t)bd_size,
-                                   (py::ssize_t)bd_size});
-          py::array_t<uint8_t> aa({rows, (py::ssize_t)2});
-          if (rows) {
-            std::memcpy(sa.mutable_data(), st[i].data(), (size_t)rows * F * P);
-            std::memcpy(aa.mutable_data(), ac[i].data(), (size_t)rows * 2);
-          }
-          out.append(py::make_tuple(status[i], sa, aa));
+        std::vector<int64_t> off(n + 1, 0);
+        for (int i = 0; i < n; ++i) off[i + 1] = off[i] + rp[i];
+        const py::ssize_t total = (py::ssize_t)off[n];
+        py::array_t<uint8_t> sa({total, (py::ssize_t)F, (py::ssize_t)bd_size,
+                                 (py::ssize_t)bd_size});
+        py::array_t<uint8_t> aa({total, (py::ssize_t)2});
+        uint8_t* sd = sa.mutable_data();
+        uint8_t* ad = aa.mutable_data();
+        for (int i = 0; i < n; ++i)
+          if (rp[i]) std::memcpy(ad + (size_t)off[i] * 2, ac[i].data(), (size_t)rp[i] * 2);
+        std::vector<int> game_of((size_t)total);
+        for (int i = 0; i < n; ++i)
+          for (int64_t r = off[i]; r < off[i + 1]; ++r) game_of[(size_t)r] = i;
+        {  // 2: the planes of every position of the batch, straight into the output block
+          py::gil_scoped_release nogil;
+          const int nf = (int)fids.size();
+          parallel_for((int)total, nthreads, [&](int r) {
+            const int g = game_of[(size_t)r];
+            extract_features(bd[g][(size_t)(r - off[g])], fids.data(), nf,
+                             sd + (size_t)r * F * P);
+          });
         }
-        return out;
+        return py::make_tuple(status, rows, sa, aa);
       },
       py::arg("texts"), py::arg("fids"), py::arg("bd_size"), py::arg("zobrist_white"),
       py::arg("zobrist_black"), py::arg("nthreads") = 8);

@@ -191,10 +191,11 @@ int flat(int x, int y, int S) { return (x >= S || y >= S) ? -3 : x * S + y; }
 
 }  // namespace
 
-int convert_sgf_game(const char* text, size_t len, int bd_size,
-                     const std::shared_ptr<const Zobrist>& zob, const int* fids, int nf,
-                     std::vector<uint8_t>& states, std::vector<uint8_t>& actions) {
-  states.clear();
+// The replay shared by both entry points: on_position(board) sees every position that yields a
+// training row (before its move is played).
+template <class OnPosition>
+int replay_sgf(const char* text, size_t len, int bd_size, const std::shared_ptr<const Zobrist>& zob,
+               std::vector<uint8_t>& actions, OnPosition&& on_position) {
   actions.clear();
   std::vector<SgfNode> line;
   SgfParser parser(text, len);
@@ -208,9 +209,6 @@ int convert_sgf_game(const char* text, size_t len, int bd_size,
     S = std::stoi(v);
   }
   if (S != bd_size) return kFallback;  // size-mismatch / setup-error ordering: python decides
-  const int P = S * S;
-  int planes = 0;
-  for (int i = 0; i < nf; ++i) planes += feature_planes(fids[i]);
   try {
     Board b(S, 7.5, false, zob);
     std::vector<std::pair<int, int>> pts;
@@ -253,10 +251,8 @@ int convert_sgf_game(const char* text, size_t len, int bd_size,
       const int kind = parse_point(v, x, y);
       if (kind < 0) return kFallback;
       const int color = w ? WHITE : BLACK;
-      if (kind == 0) {  // planes of the position before the move
-        const size_t at = states.size();
-        states.resize(at + (size_t)planes * P);
-        extract_features(b, fids, nf, states.data() + at);
+      if (kind == 0) {  // the position before the move
+        on_position(b);
         actions.push_back((uint8_t)x);
         actions.push_back((uint8_t)y);
         b.do_move(flat(x, y, S), color);
@@ -270,6 +266,31 @@ int convert_sgf_game(const char* text, size_t len, int bd_size,
     return kFallback;
   }
   return kOk;
+}
+
+int convert_sgf_game(const char* text, size_t len, int bd_size,
+                     const std::shared_ptr<const Zobrist>& zob, const int* fids, int nf,
+                     std::vector<uint8_t>& states, std::vector<uint8_t>& actions) {
+  states.clear();
+  const int P = bd_size * bd_size;
+  int planes = 0;
+  for (int i = 0; i < nf; ++i) planes += feature_planes(fids[i]);
+  return replay_sgf(text, len, bd_size, zob, actions, [&](const Board& b) {
+    const size_t at = states.size();
+    states.resize(at + (size_t)planes * P);
+    extract_features(b, fids, nf, states.data() + at);
+  });
+}
+
+// Replay only: a copy of the board at every training position (the batch converter then
+// extracts the planes of all positions of all games in one fine-grained parallel loop, so a
+// long game does not serialise the tail of a batch).
+int replay_sgf_positions(const char* text, size_t len, int bd_size,
+                         const std::shared_ptr<const Zobrist>& zob, std::vector<Board>& boards,
+                         std::vector<uint8_t>& actions) {
+  boards.clear();
+  return replay_sgf(text, len, bd_size, zob, actions,
+                    [&](const Board& b) { boards.push_back(b); });
 }
 
 }  // namespace rag

@@ -1023,7 +1023,14 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
                                                     HO, CIN, COUTP, YC, relu, HM, total_rows);
     return true;
   }
-  if ((g_tap_mode >= 5 && g_tap_mode <= 9) && cached_rows8 <= kPPSlabRows) {
+  // Small batches (self-play plies, short search waves): fewer 384-pixel blocks than CUs leave
+  // most of the chip idle, so the 192-pixel kernel (twice the blocks) runs them instead.
+  static const int pp_min = [] {
+    const char* e = getenv("RAG_PP_MIN_BLOCKS");
+    return e ? atoi(e) : 200;  // B = 256 at 19x19 is 241 blocks: stays on the ping-pong kernel
+  }();
+  const bool pp_fills = ((M + kPPBM - 1) / kPPBM) * (COUTP / kBN) >= pp_min;
+  if ((g_tap_mode >= 5 && g_tap_mode <= 9) && cached_rows8 <= kPPSlabRows && pp_fills) {
     // ping-pong kernel: one block per CU; reduce blocks fill the CUs its last round leaves free
     const int nconv = ((M + kPPBM - 1) / kPPBM) * (COUTP / kBN);
     int nred = 0;

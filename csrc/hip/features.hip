@@ -1,13 +1,14 @@
-// Input feature planes on the GPU: one wavefront builds every plane of one
-// position, bit-exact with the native extractor (csrc/engine/features.cpp, itself pinned to the
-// reference preprocessing.py:14-205 by tests/test_features.py).
+// Input feature planes on the GPU: one workgroup (one lane per board
+// point, ceil(S*S/64) waves) builds every plane of one position, bit-exact with the native
+// extractor (csrc/engine/features.cpp, itself pinned to the reference preprocessing.py:14-205
+// by tests/test_features.py).
 //
 // Per position (LDS, S <= 19):
 //   * colours, stone ages; group labels by min-label propagation over same-coloured neighbours;
 //   * per label: stone count, liberty count, and the group's stone set and liberty set as 361-bit
 //     bitsets (built with LDS 64-bit atomic ORs), so "liberties after playing p" is an exact set
 //     union + popcount per candidate instead of a flood fill;
-//   * each lane then evaluates its points: board / ones / zeros / color / turns_since /
+//   * each lane then evaluates its point: board / ones / zeros / color / turns_since /
 //     liberties / legal (suicide, ko; superko via a host-provided mask) / capture_size /
 //     self_atari_size / liberties_after (captured stones adjacent to the merged group become
 //     liberties: bitset dilation, only on capturing moves) / sensibleness (the recursive true-eye
@@ -20,10 +21,12 @@ using namespace rag;
 
 namespace {
 
-constexpr int kFW = 2;    // positions per 128-thread block
+// One point per lane: the per-position latency (label propagation, per-point capture /
+// liberties-after / true-eye work) is what bounds this kernel at the 64-512-position batches of
+// self-play and search, so the position is spread over up to 6 waves instead of one wave
+// walking 6 points per lane (164 -> ~30 us per 128-position ply, profiles/rl_bench_r3.txt).
 constexpr int kNW = 6;    // 64-bit words of a 361-point set
 constexpr int kPMAX = 384;
-constexpr int kNPL = 6;   // points per lane
 
 // feature ids (csrc/engine/go_engine.hpp FeatureId)
 enum { F_BOARD = 0, F_ONES, F_TURNS_SINCE, F_LIBERTIES, F_CAPTURE_SIZE, F_SELF_ATARI_SIZE,
@@ -31,19 +34,13 @@ enum { F_BOARD = 0, F_ONES, F_TURNS_SINCE, F_LIBERTIES, F_CAPTURE_SIZE, F_SELF_A
        F_COLOR };
 
 struct FShared {
-  unsigned long long libbits[kFW][kPMAX][kNW];
-  unsigned long long stonebits[kFW][kPMAX][kNW];
-  int lib[kFW][kPMAX];
-  int gsz[kFW][kPMAX];
-  int16_t lab[kFW][kPMAX];
-  int8_t col[kFW][kPMAX];
+  unsigned long long libbits[kPMAX][kNW];
+  unsigned long long stonebits[kPMAX][kNW];
+  int lib[kPMAX];
+  int gsz[kPMAX];
+  int16_t lab[kPMAX];
+  int8_t col[kPMAX];
 };
-
-__device__ __forceinline__ void wsync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 struct Pos {
   int S, P;
@@ -150,79 +147,64 @@ __device__ __forceinline__ int popc6(const unsigned long long* s) {
   return c;
 }
 
-__global__ void __launch_bounds__(64 * kFW)
+__global__ void __launch_bounds__(kPMAX)
 features_kernel(const int8_t* __restrict__ colors, const int16_t* __restrict__ ages,
                 const int32_t* __restrict__ meta, const uint8_t* __restrict__ extra_illegal,
                 const uint8_t* __restrict__ ladders, int n_pos, int S, const int* __restrict__ fids,
-                int nf, int F, uint8_t* __restrict__ out) {
+                int nf, int F, uint8_t* __restrict__ out, uint8_t* __restrict__ sens) {
   __shared__ FShared sh;
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int pos = blockIdx.x * kFW + wv;
-  if (pos >= n_pos) return;
+  const int pos = blockIdx.x;
+  const int p = threadIdx.x;
   const int P = S * S;
-  int8_t* col = sh.col[wv];
-  int16_t* lab = sh.lab[wv];
-  int* lib = sh.lib[wv];
-  int* gsz = sh.gsz[wv];
-  Pos g{S, P, col, lab, lib, gsz, sh.libbits[wv], sh.stonebits[wv]};
+  const bool on = p < P;
+  int8_t* col = sh.col;
+  int16_t* lab = sh.lab;
+  int* lib = sh.lib;
+  int* gsz = sh.gsz;
+  Pos g{S, P, col, lab, lib, gsz, sh.libbits, sh.stonebits};
   const int me = meta[pos * 4 + 0];
   const int ko = meta[pos * 4 + 1];
 
+  int c = 0;
+  if (on) {
+    c = colors[(size_t)pos * P + p];
+    col[p] = (int8_t)c;
+    lab[p] = c ? (int16_t)p : (int16_t)-1;
+    lib[p] = 0;
+    gsz[p] = 0;
 #pragma unroll
-  for (int k = 0; k < kNPL; ++k) {
-    const int p = lane + 64 * k;
-    if (p < P) col[p] = colors[(size_t)pos * P + p];
+    for (int w = 0; w < kNW; ++w) {
+      sh.libbits[p][w] = 0ull;
+      sh.stonebits[p][w] = 0ull;
+    }
   }
-  wsync();
-  // labels: min stone index of the group
-#pragma unroll
-  for (int k = 0; k < kNPL; ++k) {
-    const int p = lane + 64 * k;
-    if (p < P) lab[p] = col[p] ? (int16_t)p : (int16_t)-1;
-  }
-  wsync();
+  __syncthreads();
+  // labels: min stone index of the group. Lanes of other waves may read a neighbour's label
+  // while it is lowered; every value read is the index of a stone of the same group and labels
+  // only decrease, so the race is benign, and an iteration in which no lane changed anything saw
+  // a fixpoint.
   for (int it = 0; it < 2 * kPMAX; ++it) {
     int changed = 0;
-#pragma unroll
-    for (int k = 0; k < kNPL; ++k) {
-      const int p = lane + 64 * k;
-      if (p >= P || col[p] == 0) continue;
+    if (on && c != 0) {
       int m = lab[lab[p]];
       for (int i = 0; i < 4; ++i) {
         const int q = g.nb(p, i);
-        if (q >= 0 && col[q] == col[p]) m = min(m, (int)lab[q]);
+        if (q >= 0 && col[q] == c) m = min(m, (int)lab[q]);
       }
       if (m < lab[p]) {
         lab[p] = (int16_t)m;
         changed = 1;
       }
     }
-    wsync();
-    if (!__any(changed)) break;
+    if (!__syncthreads_or(changed)) break;
   }
   // per-label tables
-#pragma unroll
-  for (int k = 0; k < kNPL; ++k) {
-    const int p = lane + 64 * k;
-    if (p >= P) continue;
-    lib[p] = 0;
-    gsz[p] = 0;
-#pragma unroll
-    for (int w = 0; w < kNW; ++w) {
-      sh.libbits[wv][p][w] = 0ull;
-      sh.stonebits[wv][p][w] = 0ull;
-    }
-  }
-  wsync();
-#pragma unroll
-  for (int k = 0; k < kNPL; ++k) {
-    const int p = lane + 64 * k;
-    if (p >= P) continue;
+  if (on) {
     const unsigned long long bit = 1ull << (p & 63);
-    if (col[p] != 0) {
+    if (c != 0) {
       const int l = lab[p];
       atomicAdd(&gsz[l], 1);
-      atomicOr(&sh.stonebits[wv][l][p >> 6], bit);
+      atomicOr(&sh.stonebits[l][p >> 6], bit);
     } else {
       int seen[4], ns = 0;
       for (int i = 0; i < 4; ++i) {
@@ -234,19 +216,16 @@ features_kernel(const int8_t* __restrict__ colors, const int16_t* __restrict__ a
         if (dup) continue;
         seen[ns++] = l;
         atomicAdd(&lib[l], 1);
-        atomicOr(&sh.libbits[wv][l][p >> 6], bit);
+        atomicOr(&sh.libbits[l][p >> 6], bit);
       }
     }
   }
-  wsync();
+  __syncthreads();
+  if (!on) return;
 
   // plane offsets of the requested features
   uint8_t* o = out + (size_t)pos * F * P;
-#pragma unroll 1
-  for (int k = 0; k < kNPL; ++k) {
-    const int p = lane + 64 * k;
-    if (p >= P) continue;
-    const int c = col[p];
+  {
     // ---- legality, captures and the simulated move
     int own_l[4], cap_l[4], nown = 0, ncap = 0, empty_nb = 0;
     bool own_multi = false;
@@ -290,7 +269,7 @@ features_kernel(const int8_t* __restrict__ colors, const int16_t* __restrict__ a
       for (int j = 0; j < nown; ++j) {
         size_after += gsz[own_l[j]];
 #pragma unroll
-        for (int w = 0; w < kNW; ++w) ls[w] |= sh.libbits[wv][own_l[j]][w];
+        for (int w = 0; w < kNW; ++w) ls[w] |= sh.libbits[own_l[j]][w];
       }
       if (ncap > 0) {
         unsigned long long grp[kNW], cap[kNW];
@@ -302,10 +281,10 @@ features_kernel(const int8_t* __restrict__ colors, const int16_t* __restrict__ a
         grp[p >> 6] |= 1ull << (p & 63);
         for (int j = 0; j < nown; ++j)
 #pragma unroll
-          for (int w = 0; w < kNW; ++w) grp[w] |= sh.stonebits[wv][own_l[j]][w];
+          for (int w = 0; w < kNW; ++w) grp[w] |= sh.stonebits[own_l[j]][w];
         for (int j = 0; j < ncap; ++j)
 #pragma unroll
-          for (int w = 0; w < kNW; ++w) cap[w] |= sh.stonebits[wv][cap_l[j]][w];
+          for (int w = 0; w < kNW; ++w) cap[w] |= sh.stonebits[cap_l[j]][w];
         // captured stones orthogonally adjacent to the merged group become liberties
 #pragma unroll
         for (int w = 0; w < kNW; ++w) {
@@ -325,7 +304,13 @@ features_kernel(const int8_t* __restrict__ colors, const int16_t* __restrict__ a
       ls[p >> 6] &= ~(1ull << (p & 63));
       libs_after = popc6(ls);
     }
-    // ---- write the planes
+    // ---- write the planes (the true-eye DFS at most once per point)
+    int sensible = -1;
+    auto get_sensible = [&]() {
+      if (sensible < 0) sensible = legal && !g.is_eye(p, me);
+      return sensible;
+    };
+    if (sens) sens[(size_t)pos * P + p] = (uint8_t)get_sensible();
     int base = 0;
     for (int fi = 0; fi < nf; ++fi) {
       const int f = fids[fi];
@@ -389,7 +374,7 @@ features_kernel(const int8_t* __restrict__ colors, const int16_t* __restrict__ a
           base += 1;
           break;
         case F_SENSIBLENESS:
-          op[0] = legal && !g.is_eye(p, me);
+          op[0] = (uint8_t)get_sensible();
           base += 1;
           break;
         case F_LEGAL:
@@ -408,14 +393,16 @@ features_kernel(const int8_t* __restrict__ colors, const int16_t* __restrict__ a
 // colors [n][S*S] int8, ages [n][S*S] int16 (-1 = empty), meta [n][4] int32 (player to move,
 // ko point, 0, 0), extra_illegal [n][S*S] uint8 or null (positional-superko points),
 // ladders [n][2][S*S] uint8 or null (capture, escape), fids [nf] int32 on the device,
-// out [n][F][S*S] uint8. S <= 19.
+// out [n][F][S*S] uint8, sens [n][S*S] uint8 or null (the sensible-move mask of the player to
+// move, written in the same pass). S <= 19.
 RAG_API int rag_features(const void* colors, const void* ages, const int32_t* meta,
                          const uint8_t* extra_illegal, const uint8_t* ladders, int n_pos, int S,
-                         const int* fids, int nf, int F, uint8_t* out, hipStream_t stream) {
+                         const int* fids, int nf, int F, uint8_t* out, uint8_t* sens,
+                         hipStream_t stream) {
   if (S < 2 || S * S > kPMAX || n_pos <= 0) return -1;
-  dim3 grid((n_pos + kFW - 1) / kFW);
-  features_kernel<<<grid, 64 * kFW, 0, stream>>>((const int8_t*)colors, (const int16_t*)ages,
+  const int threads = (S * S + 63) / 64 * 64;
+  features_kernel<<<dim3(n_pos), threads, 0, stream>>>((const int8_t*)colors, (const int16_t*)ages,
                                                  meta, extra_illegal, ladders, n_pos, S, fids,
-                                                 nf, F, out);
+                                                 nf, F, out, sens);
   return (int)hipGetLastError();
 }

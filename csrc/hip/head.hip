@@ -361,7 +361,51 @@ __global__ void value_mlp_out_kernel(const float* __restrict__ part, const float
   out[b] = tanhf(s);
 }
 
+// PassLogit weight gradients: dW[j] = sum_b zout[b, j] * dpass[b] (one lane per point,
+// coalesced over j; the batch loop is 4-way unrolled), db = sum_b dpass[b] (block 0, wave
+// reduction). Overwrites dW / db.
+constexpr int kPassThreads = 128;
+
+__global__ void __launch_bounds__(kPassThreads)
+pass_grads_kernel(const float* __restrict__ z, const float* __restrict__ dpass,
+                  float* __restrict__ dW, float* __restrict__ db, int B, int P) {
+  const int j = blockIdx.x * kPassThreads + threadIdx.x;
+  if (j < P) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int b = 0;
+    for (; b + 4 <= B; b += 4) {
+      a0 += z[(size_t)b * P + j] * dpass[b];
+      a1 += z[(size_t)(b + 1) * P + j] * dpass[b + 1];
+      a2 += z[(size_t)(b + 2) * P + j] * dpass[b + 2];
+      a3 += z[(size_t)(b + 3) * P + j] * dpass[b + 3];
+    }
+    for (; b < B; ++b) a0 += z[(size_t)b * P + j] * dpass[b];
+    dW[j] = (a0 + a1) + (a2 + a3);
+  }
+  if (blockIdx.x == 0) {
+    __shared__ float red[kPassThreads / 64];
+    float s = 0.f;
+    for (int b = threadIdx.x; b < B; b += kPassThreads) s += dpass[b];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float t = 0.f;
+      for (int w = 0; w < kPassThreads / 64; ++w) t += red[w];
+      *db = t;
+    }
+  }
+}
+
 }  // namespace
+
+RAG_API int rag_pass_grads(const float* zout, const float* dpass, float* dW, float* db, int B,
+                           int P, hipStream_t stream) {
+  if (B <= 0 || P <= 0) return -1;
+  pass_grads_kernel<<<(P + kPassThreads - 1) / kPassThreads, kPassThreads, 0, stream>>>(
+      zout, dpass, dW, db, B, P);
+  return (int)hipGetLastError();
+}
 
 RAG_API int rag_policy_head_fwd(const void* H, const float* w, const float* b0,
                                 const float* pbias, float* probs, const int64_t* labels,

@@ -37,6 +37,31 @@ class SizeMismatchError(Exception):
     pass
 
 
+def _addr(a):
+    return a.__array_interface__["data"][0]
+
+
+def _join(arrs):
+    """Concatenate row blocks; a view when they are adjacent slices of one C-contiguous base."""
+    if len(arrs) == 1:
+        return arrs[0]
+    a0 = arrs[0]
+    base = a0.base
+    pos = _addr(a0)
+    adjacent = base is not None and a0.flags.c_contiguous
+    for a in arrs:
+        if not adjacent:
+            break
+        adjacent = a.base is base and a.flags.c_contiguous and _addr(a) == pos and \
+            a.shape[1:] == a0.shape[1:] and a.dtype == a0.dtype
+        pos += a.nbytes
+    if adjacent:
+        rows = sum(a.shape[0] for a in arrs)
+        return np.lib.stride_tricks.as_strided(a0, shape=(rows,) + a0.shape[1:],
+                                               strides=a0.strides, writeable=False)
+    return np.concatenate(arrs)
+
+
 class _Sink(object):
     """The output file: datasets + per-file offsets, rows appended in order."""
 
@@ -67,13 +92,13 @@ class _Sink(object):
         return n
 
     def flush(self):
-        """Append the queued games as one block: whole 64-row chunks compress in parallel."""
+        """Append the queued games as one block: whole 64-row chunks compress in parallel. Rows
+        of consecutive games that already sit back to back in one native block are appended as
+        a view of it (no concatenation)."""
         if not self._queue:
             return
-        st = np.concatenate([q[0] for q in self._queue]) if len(self._queue) > 1 else \
-            self._queue[0][0]
-        ac = np.concatenate([q[1] for q in self._queue]) if len(self._queue) > 1 else \
-            self._queue[0][1]
+        st = _join([q[0] for q in self._queue])
+        ac = _join([q[1] for q in self._queue])
         self._queue = []
         self.states.append(st)
         self.actions.append(ac)
@@ -135,13 +160,16 @@ class GameConverter(object):
         done = [None] * len(names)
         if texts:
             zw, zb, _ = go._zobrist(bd_size)
-            res = _rg.convert_games(texts, list(self.feature_processor.feature_ids), bd_size,
-                                    np.ascontiguousarray(zw.ravel()),
-                                    np.ascontiguousarray(zb.ravel()), nthreads)
-            for i, (status, st, ac) in zip(native_idx, res):
-                if status == _NATIVE_OK:
+            status, rows, block, acts = _rg.convert_games(
+                texts, list(self.feature_processor.feature_ids), bd_size,
+                np.ascontiguousarray(zw.ravel()), np.ascontiguousarray(zb.ravel()), nthreads)
+            at = 0
+            for i, code, n in zip(native_idx, status.tolist(), rows.tolist()):
+                st, ac = block[at:at + n], acts[at:at + n]
+                at += n
+                if code == _NATIVE_OK:
                     done[i] = (st, ac, None)
-                elif status == _NATIVE_ILLEGAL:
+                elif code == _NATIVE_ILLEGAL:
                     done[i] = (st, ac, go.IllegalMove("illegal move in SGF replay"))
         for i, name in enumerate(names):
             if done[i] is None:
@@ -149,20 +177,29 @@ class GameConverter(object):
         return done
 
     def sgfs_to_hdf5(self, sgf_files, hdf5_file, bd_size=19, ignore_errors=True, verbose=False,
-                     batch=64, nthreads=8):
+                     batch=256, nthreads=8):
         tmp = os.path.join(os.path.dirname(hdf5_file), ".tmp." + os.path.basename(hdf5_file))
         sink = _Sink(tmp, self.feature_processor.feature_list, self.n_features, bd_size)
         if verbose:
             print("created HDF5 dataset in {}".format(tmp))
+        sink.states.nthreads = max(1, nthreads)
         t0, ngames = time.time(), 0
         files = iter(sgf_files)
+        # the next batch converts on a helper thread (the native converter releases the GIL)
+        # while this one is compressed and written
+        from concurrent.futures import ThreadPoolExecutor
+        ex = ThreadPoolExecutor(1)
+
+        def submit():
+            names = [n for _, n in zip(range(batch), files)]
+            return (names, ex.submit(self._batch, names, bd_size, nthreads)) if names else None
         try:
-            while True:
-                names = [n for _, n in zip(range(batch), files)]
-                if not names:
-                    break
-                for name, (states, moves, err) in zip(names, self._batch(names, bd_size,
-                                                                          nthreads)):
+            nxt = submit()
+            while nxt is not None:
+                names, fut = nxt
+                results = fut.result()
+                nxt = submit()
+                for name, (states, moves, err) in zip(names, results):
                     ngames += 1
                     if verbose:
                         print(name)
@@ -176,8 +213,10 @@ class GameConverter(object):
                 sink.flush()
         except Exception:
             print("sgfs_to_hdf5 failed")
+            ex.shutdown(wait=True)
             sink.abort()
             raise
+        ex.shutdown(wait=True)
         self.games_per_s = ngames / max(time.time() - t0, 1e-9)
         if verbose:
             print("finished (%.1f games/s). renaming %s to %s" % (self.games_per_s, tmp,

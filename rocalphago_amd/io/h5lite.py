@@ -678,6 +678,7 @@ class WDataset(object):
         self.maxshape = tuple(maxshape) if maxshape is not None else None
         self.chunks = tuple(chunks) if chunks else None
         self.compression = compression
+        self.nthreads = 8  # LZF threads of whole-chunk appends
         self.attrs = Attributes()
         if compression not in (None, "lzf"):
             raise NotImplementedError("only lzf compression is supported by h5lite")
@@ -782,14 +783,16 @@ class WDataset(object):
         done = 0
         while done < n:
             i = start + done
+            # a full pending chunk goes out first, so a block that starts mid-chunk still
+            # reaches the parallel whole-chunk path once the partial chunk is topped up
+            while i >= self._pending_start + c:
+                self._flush_pending()
             if i == self._pending_start and n - done >= 2 * c:
-                took = self._flush_full_chunks(rows[done:])
+                took = self._flush_full_chunks(rows[done:], self.nthreads)
                 if took:
                     done += took
                     self._max_written = start + done
                     continue
-            while i >= self._pending_start + c:
-                self._flush_pending()
             off = i - self._pending_start
             take = min(c - off, n - done)
             self._pending[off:off + take] = rows[done:done + take]

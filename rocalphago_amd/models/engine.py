@@ -436,9 +436,9 @@ class PolicyHeadEngine(object):
         return self.probs[:B]
 
     def pass_grads(self, B, dW, db):
-        """PassLogit weight gradients after a training forward: dW = dpass^T z, db = sum dpass."""
-        dW.copy_(torch.mv(self.zpos[:B].t(), self.dpass[:B]).reshape(dW.shape))
-        db.copy_(self.dpass[:B].sum().reshape(1))
+        """PassLogit weight gradients after a training forward: dW = dpass^T z, db = sum dpass
+        (head.hip pass_grads_kernel)."""
+        ops.pass_grads(self.zpos[:B], self.dpass[:B], dW, db)
 
     def backward(self, B, w, dz, dw, db0, dpbias):
         """dz [B, S*S] -> head param grads + trunk top gradient (ReLU-masked) in grad buffer 0."""

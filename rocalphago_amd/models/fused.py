@@ -292,15 +292,18 @@ def _detect_resnet(model):
         units.append(n)
         cur, i = m.name, i + 1
     rest = L[i:]
-    if not units or len(rest) != 5 or not act(rest[0], cur, "relu") or \
+    pl = rest[4] if len(rest) == 6 and rest[4].class_name == "PassLogit" and \
+        rest[4].inbound == [rest[3].name] else None
+    if not units or len(rest) != (6 if pl is not None else 5) or \
+            not act(rest[0], cur, "relu") or \
             not conv(rest[1], rest[0].name, 1) or rest[1].config["nb_filter"] != 1 or \
             rest[2].class_name != "Flatten" or rest[3].class_name != "Bias" or \
-            not act(rest[4], rest[3].name, "softmax"):
+            not act(rest[-1], rest[-2].name, "softmax"):
         return None
     K = L[1].config["nb_filter"]
     if any(c.config["nb_filter"] != K for c in convs):
         return None
-    return ResnetPlan(model, convs, bns, units, rest[1], rest[3])
+    return ResnetPlan(model, convs, bns, units, rest[1], rest[3], pl)
 
 
 class ResnetPlan(PolicyPlan):
@@ -309,7 +312,7 @@ class ResnetPlan(PolicyPlan):
     statistics (and update the running averages); forward / evaluation use the running ones,
     like Keras' learning phase."""
 
-    def __init__(self, model, convs, bns, units, head_conv, bias_layer):
+    def __init__(self, model, convs, bns, units, head_conv, bias_layer, pass_layer=None):
         net = model.net
         self.model, self.net = model, net
         specs = []
@@ -324,5 +327,5 @@ class ResnetPlan(PolicyPlan):
         self.head_name = head_conv.name
         self.K = specs[-1].cout
         self.bias_name = bias_layer.name
-        self.pass_name = None
-        self.head = PolicyHeadEngine(self.trunk, self.K)
+        self.pass_name = pass_layer.name if pass_layer is not None else None
+        self.head = PolicyHeadEngine(self.trunk, self.K, pass_logit=pass_layer is not None)

@@ -88,7 +88,8 @@ class ResnetPolicy(CNNPolicy):
     """Residual policy (He et al. 2015) exactly as reference policy.py:141-271: linear input conv,
     units of n_skip_K x (BatchNorm -> ReLU -> conv) with sum-merge, final ReLU, 1x1 conv, Flatten,
     Bias, softmax. Note the reference's BatchNormalization uses Keras' default axis=-1 on 'th'
-    tensors; that axis is kept for checkpoint compatibility."""
+    tensors; that axis is kept for checkpoint compatibility. ``pass_logit=True`` adds the learned
+    pass logit of CNNPolicy (softmax over S*S + 1, pass last)."""
 
     @staticmethod
     def create_network(**kwargs):
@@ -146,6 +147,8 @@ class ResnetPolicy(CNNPolicy):
                                    border_mode='same'), [path])
         path = add(K.Flatten(), [path])
         path = add(Bias(), [path])
+        if params.get("pass_logit"):
+            path = add(K.PassLogit(), [path])
         out = add(K.Activation('softmax'), [path])
         return K.Model(layers, functional=True, inputs=[inp.name], outputs=[out],
                        device=params.get("device"), seed=params.get("seed"))

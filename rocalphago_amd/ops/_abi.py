@@ -47,7 +47,8 @@ SIGNATURES = {
     # sample.hip
     "rag_sample_moves": [P, P, I, P, I, I, F, C.c_uint64, P, P],
     # features.hip
-    "rag_features": [P, P, P, P, P, I, I, P, I, I, P, P],
+    "rag_pass_grads": [P, P, P, P, I, I, P],
+    "rag_features": [P, P, P, P, P, I, I, P, I, I, P, P, P],
     # ladder.hip
     "rag_ladder_workspace": [I, I],
     "rag_ladders": [P, P, I, I, P, P, P],

@@ -61,7 +61,6 @@ class GpuFeatures(object):
         self.fids_dev = torch.tensor(self.fids, dtype=torch.int32, device=self.device)
         self.ladders = any(f in _LADDERS for f in self.fids)
         self.nthreads = nthreads
-        self._sens_fid = None
         self._work = None
         self.ladder_device = ladders or _DEFAULT_LADDERS
         if self.ladder_device not in ("host", "gpu"):
@@ -87,22 +86,15 @@ class GpuFeatures(object):
             ld, self._work = gpu_ladders(c, m, S, work=self._work)
         if out is None:
             out = torch.empty((n, self.F, S, S), dtype=torch.uint8, device=self.device)
+        if sens_out is not None and (sens_out.numel() != n * S * S or
+                                     sens_out.dtype != torch.uint8 or
+                                     not sens_out.is_contiguous()):
+            raise ValueError("sens_out must be contiguous uint8 with n*S*S elements")
+        # one pass: the planes and (optionally) the sensible-move mask
         _check(_lib().rag_features(_ptr(c), _ptr(a), _ptr(m), _ptr(il), _ptr(ld), n, S,
                                    _ptr(self.fids_dev), len(self.fids), self.F, _ptr(out),
-                                   _stream()), "features")
-        if sens_out is not None:
-            self._sensibleness(c, a, m, il, n, S, sens_out)
+                                   _ptr(sens_out), _stream()), "features")
         return out
-
-    def _sensibleness(self, c, a, m, il, n, S, sens_out):
-        if sens_out.numel() != n * S * S or sens_out.dtype != torch.uint8:
-            raise ValueError("sens_out must be uint8 with n*S*S elements")
-        if self._sens_fid is None:
-            self._sens_fid = torch.tensor([_FID["sensibleness"]], dtype=torch.int32,
-                                          device=self.device)
-        _check(_lib().rag_features(_ptr(c), _ptr(a), _ptr(m), _ptr(il), None, n, S,
-                                   _ptr(self._sens_fid), 1, 1, _ptr(sens_out), _stream()),
-               "features(sensibleness)")
 
     def from_arrays(self, colors, ages, meta, illegal, lad, out=None, sens_out=None):
         """Planes from the native inputs directly: colours [n, S*S] int8, stone ages int16,

@@ -76,12 +76,32 @@ def _hptr(pending):
     return None if pending is None else pending.ptr
 
 
+_INT32_MAX = 2 ** 31 - 1
+
+
+def _index_range_ok(*tensors):
+    """The conv / BN / packing kernels index activations with 32-bit element offsets: refuse
+    (loudly, before launch) a batch whose padded activation reaches 2^31 elements instead of
+    faulting on a wrapped address. Callers split such batches (e.g. reinforcement.py)."""
+    for t in tensors:
+        if t is not None and t.numel() > _INT32_MAX:
+            raise ValueError("activation of %d elements exceeds the kernels' 32-bit indexing; "
+                             "split the batch (max rows ~ %d)" %
+                             (t.numel(), _INT32_MAX // max(1, t[0].numel())))
+
+
+def max_rows(S, halo, channels):
+    """Largest batch whose padded [B, S+2h, S+2h, C] activation the kernels can index."""
+    return _INT32_MAX // ((S + 2 * halo) ** 2 * channels)
+
+
 def conv_igemm(x, wpack, bias, y, B, S, hi, ho, cinp, coutp, ks, relu, mask=None,
                mask_halo=None, residual=None, pending=None):
     """y[pad ho] = act(conv_ks(x[pad hi]) + bias [+ residual]), or the dgrad form with a ReLU
     mask (the layer input: y's channel count, its own halo ``mask_halo``, default ho).
     ``residual`` (ResNet sum-merge) has y's layout and may be y itself. ``pending``: a
     PendingReduction whose deferred wgrad reduction rides along this launch."""
+    _index_range_ok(x, y, mask, residual)
     hm = ho if mask_halo is None else mask_halo
     if mask is not None and (mask.shape[1] != S + 2 * hm or mask.shape[-1] != y.shape[-1]):
         raise ValueError("mask layout does not match (halo %d, %d channels)" % (hm, y.shape[-1]))
@@ -167,6 +187,7 @@ def conv_wgrad(g, x, dw, db, B, S, hi, cout, coutp, cin, cinp, ks, accumulate=Fa
     required); the next ``conv_igemm(..., pending=pending)`` on this stream runs it in its free
     block slots (or ``wgrad_flush(pending)`` launches it). ``dw``/``db`` are final only after
     that."""
+    _index_range_ok(g, x)
     if work is None:
         work = wgrad_workspace(B, S, coutp, cinp, ks, g.device)
     if hg is None:
@@ -257,6 +278,15 @@ def policy_head_fwd(h, w, b0, pbias, probs, K, labels=None, sweight=None, loss=N
                                       _ptr(labels), _ptr(sweight), _ptr(loss), _ptr(dz),
                                       _ptr(hit), _ptr(acc), B, S, KP, K, mode, float(gscale),
                                       _stream()), "policy_head_fwd")
+
+
+def pass_grads(zout, dpass, dW, db):
+    """PassLogit weight gradients on the GPU: dW = dpass^T zout ([S*S]), db = sum(dpass)."""
+    B, P = zout.shape
+    if dpass.numel() != B or dW.numel() != P or db.numel() != 1 or not zout.is_contiguous():
+        raise ValueError("pass_grads: zout [B, P] contiguous, dpass [B], dW [P], db [1]")
+    _check(_lib().rag_pass_grads(_ptr(zout), _ptr(dpass), _ptr(dW), _ptr(db), B, P, _stream()),
+           "pass_grads")
 
 
 _head_ws = {}

@@ -90,7 +90,10 @@ def _play_games(learner, opponent, states, num_games):
 
 
 def _stack(rows):
-    """Position rows -> one batch: device rows (the GPU player's planes) stay on the device."""
+    """Position rows -> one batch: device rows (the GPU player's planes) stay on the device.
+    A game's rows may already be one [n, F, S, S] block (native self-play)."""
+    if isinstance(rows, torch.Tensor):
+        return rows
     if isinstance(rows[0], torch.Tensor):
         return torch.stack(rows)
     return torch.from_numpy(np.stack(rows))
@@ -124,7 +127,7 @@ def run_n_games(optimizer, learner, opponent, num_games, mock_states=[], mode="p
     S2 = board_size * board_size
     if mode == "per_game":
         for f, m, w in zip(feats, moves, won):
-            if not f:
+            if len(f) == 0:
                 continue
             optimizer.lr = abs(optimizer.lr) * (+1 if w else -1)
             X = _stack(f)
@@ -137,25 +140,38 @@ def run_n_games(optimizer, learner, opponent, num_games, mock_states=[], mode="p
     return float(wins) / num_games
 
 
+_UPDATE_CHUNK = 8192  # positions per fused fwd/bwd of the batched REINFORCE update
+
+
 def _batched_update(model, optimizer, feats, moves, won, S2, dp):
     """One SGD step on sum_g sign_g * grad(mean log-loss of game g), summed across ranks."""
     X, lab, sw = [], [], []
     for f, m, w in zip(feats, moves, won):
-        if not f:
+        if len(f) == 0:
             continue
-        X.extend(f)
+        X.append(_stack(f))
         lab.extend(m)
         sw.extend([(1.0 if w else -1.0) / len(f)] * len(f))
     dev = model.device
     net = model.net
     if X:
-        x = _stack(X).to(dev)
+        x = torch.cat([t.to(dev) for t in X])
         labels = torch.tensor(lab, dtype=torch.int64, device=dev)
         w = torch.tensor(sw, dtype=torch.float32, device=dev)
         plan = model._plan_for()
         if plan is not None:
-            B = plan.prepare(x)
-            plan.fwd_bwd(B, labels, w, 2, 1.0)
+            # the summed signed loss splits over micro-batches: a large game batch (hundreds
+            # of games x hundreds of moves) runs as chunks whose gradients are added up, which
+            # bounds the activation memory and keeps the kernels' 32-bit offsets in range
+            n = x.shape[0]
+            acc = None
+            for s in range(0, n, _UPDATE_CHUNK):
+                B = plan.prepare(x[s:s + _UPDATE_CHUNK])
+                plan.fwd_bwd(B, labels[s:s + _UPDATE_CHUNK], w[s:s + _UPDATE_CHUNK], 2, 1.0)
+                if n > _UPDATE_CHUNK:
+                    acc = net.flat_grad.clone() if acc is None else acc.add_(net.flat_grad)
+            if acc is not None:
+                net.flat_grad.copy_(acc)
         else:
             y = torch.zeros((len(lab), S2), device=dev)
             y[torch.arange(len(lab)), labels] = 1

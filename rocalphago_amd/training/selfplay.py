@@ -15,8 +15,12 @@ features are extracted, the batch is evaluated, and ``do_move`` is called game b
   3. ``GameBatch.play``: the whole ply applied natively in parallel (move limit -> pass, as
      ai.py's ``len(history) > move_limit``).
 
+The games are split into ``pipeline`` independent groups whose plies alternate: the chosen
+points come back through pinned memory behind an event, so while the GPU runs one group's ply
+the host applies and packs the other's (the host work of a ply is hidden behind GPU work).
+
 The learner's planes stay on the device for the REINFORCE update (rows of the positions where
-it did not pass, the reference's ``_make_training_pair`` rows).
+it did not pass, the reference's ``_make_training_pair`` rows), one [n, F, S, S] block per game.
 """
 import numpy as np
 import torch
@@ -39,9 +43,10 @@ def _player_kind(player):
 class NativeSelfPlay(object):
     """Lock-step games of ``learner`` vs ``opponent`` (policy players on HIP models)."""
 
-    def __init__(self, learner, opponent, nthreads=16):
+    def __init__(self, learner, opponent, nthreads=16, pipeline=2):
         self.learner, self.opponent = learner, opponent
         self.nthreads = nthreads
+        self.pipeline = max(1, int(pipeline))
         self.device = learner.policy.model.device
         self._gf = {}
         self._pinned = {}
@@ -83,7 +88,9 @@ class NativeSelfPlay(object):
         return t
 
     # ------------------------------------------------------------------ one ply
-    def _ply(self, batch, player, idx, S):
+    def _launch(self, batch, player, idx, S, slot=0, limit=None):
+        """Queue one ply of games ``idx`` (pack -> copies in -> features -> policy -> sampling
+        -> chosen points copied back into pinned memory) without waiting for the GPU."""
         import time
         from ..ops import hipops as ops
         t0 = time.perf_counter()
@@ -92,11 +99,11 @@ class NativeSelfPlay(object):
         policy = player.policy
         gf = self._features(policy)
         host_lad = gf.ladders and gf.ladder_device == "host"
-        h = {"colors": self._buf("colors", (n, P), torch.int8),
-             "ages": self._buf("ages", (n, P), torch.int16),
-             "meta4": self._buf("meta4", (n, 4), torch.int32)}
+        h = {"colors": self._buf("colors%d" % slot, (n, P), torch.int8),
+             "ages": self._buf("ages%d" % slot, (n, P), torch.int16),
+             "meta4": self._buf("meta4%d" % slot, (n, 4), torch.int32)}
         if host_lad:
-            h["ladders"] = self._buf("ladders", (n, 2, P), torch.uint8)
+            h["ladders"] = self._buf("ladders%d" % slot, (n, 2, P), torch.uint8)
         hv = {k: v[:n].numpy() for k, v in h.items()}
         batch.pack(idx, hv["colors"], hv["ages"], hv["meta4"], hv.get("ladders"))
         d = {k: v[:n].to(self.device, non_blocking=True) for k, v in h.items()}
@@ -120,43 +127,144 @@ class NativeSelfPlay(object):
         rng = getattr(player, "rng", np.random)
         seed = (int(rng.randint(0, 2 ** 31 - 1)) << 31) | int(rng.randint(0, 2 ** 31 - 1))
         mv = ops.sample_moves(probs, sens, beta, greedy, seed)
+        hm = self._buf("moves%d" % slot, (n,), mv.dtype)[:n]
+        hm.copy_(mv, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        if limit is None:
+            limit = player.move_limit if player.move_limit is not None else -1
+        self.stats["host_s"] += time.perf_counter() - t0
+        return {"idx": idx, "planes": planes, "moves": hm, "event": ev, "limit": limit,
+                "player": player}
+
+    def _finish(self, batch, job, S):
+        """Wait for a queued ply and apply it natively; returns (planes, played)."""
+        import time
+        t0 = time.perf_counter()
+        job["event"].synchronize()
         t1 = time.perf_counter()
-        mv = mv.cpu().numpy().astype(np.int32)  # the only sync of the ply
-        t2 = time.perf_counter()
-        mv[(mv < 0) | (mv >= P)] = -1
-        limit = player.move_limit if player.move_limit is not None else -1
-        _, played = batch.play(idx, mv, limit)
+        mv = job["moves"].numpy().astype(np.int32)
+        mv[(mv < 0) | (mv >= S * S)] = -1
+        _, played = batch.play(job["idx"], mv, job["limit"])
         self.stats["plies"] += 1
-        self.stats["positions"] += n
-        self.stats["gpu_wait_s"] += t2 - t1
-        self.stats["host_s"] += (t1 - t0) + (time.perf_counter() - t2)
-        return planes, played
+        self.stats["positions"] += len(job["idx"])
+        self.stats["gpu_wait_s"] += t1 - t0
+        self.stats["host_s"] += time.perf_counter() - t1
+        return job["planes"], played
+
+    def _ply(self, batch, player, idx, S, limit=None):
+        return self._finish(batch, self._launch(batch, player, idx, S, limit=limit), S)
+
+    def _groups(self, num_games):
+        """Games split into independent groups whose plies alternate on the GPU: while one
+        group's ply runs, the host applies the previous ply of the other and packs its next."""
+        # small batches (the 7x7 reference shape) are bound by per-ply overhead: one group
+        k = self.pipeline if num_games >= 64 * self.pipeline else 1
+        grp = np.zeros(num_games, np.int64)
+        for g, part in enumerate(np.array_split(np.arange(num_games), k)):
+            grp[part] = g
+        return k, grp
+
+    @staticmethod
+    def _active(batch, grp, k):
+        a = batch.active()
+        return a[grp[a] == k]
 
     # ------------------------------------------------------------------ games
     def play(self, num_games, size, komi=7.5):
         """Play ``num_games`` games (learner is BLACK in even games, WHITE in odd ones, as the
-        reference). Returns (per-game list of device plane rows, per-game list of flat learner
-        moves, learner colours, winners int8 [num_games])."""
+        reference). Returns (per game: the learner's device plane rows [n_g, F, S, S] in move
+        order, or [] if it never moved; per game: its flat moves; learner colours; winners int8
+        [num_games]). The rows are gathered once at the end (one index per ply, one sort by
+        game), not as per-position tensor views."""
         zw, zb, _ = go._zobrist(size)
         batch = _rg.GameBatch(num_games, size, komi, False, zw.ravel().copy(),
                               zb.ravel().copy(), self.nthreads)
-        feats = [[] for _ in range(num_games)]
-        moves = [[] for _ in range(num_games)]
         colors = [go.BLACK if i % 2 == 0 else go.WHITE for i in range(num_games)]
         odd = np.arange(1, num_games, 2, dtype=np.int32)
         if len(odd):
             self._ply(batch, self.opponent, odd, size)
-        current = self.learner
-        while True:
-            idx = batch.active()
-            if len(idx) == 0:
-                break
-            planes, played = self._ply(batch, current, idx, size)
-            if current is self.learner:
-                for r in np.nonzero(played >= 0)[0]:
-                    g = int(idx[r])
-                    feats[g].append(planes[int(r)])
-                    moves[g].append(int(played[r]))
-            current = self.opponent if current is self.learner else self.learner
+        K, grp = self._groups(num_games)
+        current = [self.learner] * K
+        jobs = [None] * K
+        recs = []  # (planes, rows of the ply the learner learns from, their games, moves)
+
+        def start(k):
+            idx = self._active(batch, grp, k)
+            return self._launch(batch, current[k], idx, size, slot=k) if len(idx) else None
+        for k in range(K):
+            jobs[k] = start(k)
+        while any(j is not None for j in jobs):
+            for k in range(K):
+                if jobs[k] is None:
+                    continue
+                idx = jobs[k]["idx"]
+                planes, played = self._finish(batch, jobs[k], size)
+                if current[k] is self.learner:
+                    r = np.nonzero(played >= 0)[0]
+                    if len(r):
+                        recs.append((planes, r, idx[r], played[r]))
+                current[k] = self.opponent if current[k] is self.learner else self.learner
+                jobs[k] = start(k)
         self.illegal = batch.illegal
+        feats, moves = self._per_game(recs, num_games)
         return feats, moves, colors, batch.winners()
+
+    def _per_game(self, recs, num_games):
+        if not recs:
+            return [[] for _ in range(num_games)], [[] for _ in range(num_games)]
+        dev = self.device
+        rows = torch.cat([pl[torch.from_numpy(r.astype(np.int64)).to(dev)]
+                          for pl, r, _, _ in recs])
+        gid = np.concatenate([g for _, _, g, _ in recs]).astype(np.int64)
+        mv = np.concatenate([m for _, _, _, m in recs]).astype(np.int64)
+        order = np.argsort(gid, kind="stable")  # plies were recorded in move order
+        counts = np.bincount(gid, minlength=num_games)
+        rows = rows[torch.from_numpy(order).to(dev)]
+        parts = torch.split(rows, counts.tolist())
+        mparts = np.split(mv[order], np.cumsum(counts)[:-1])
+        feats = [p if c else [] for p, c in zip(parts, counts)]
+        return feats, [m.tolist() for m in mparts]
+
+    def sample_positions(self, num_games, size, targets, move_limit, komi=7.5):
+        """Value-dataset self-play (``learner`` plays both colours): returns each game's native
+        board copied when it reached ``targets[g]`` moves (or its final board if it ended
+        earlier) and the winners int8 [num_games]. A game that reaches ``move_limit`` moves
+        passes out (the winner is that of the limit position, as the Python loop that stops
+        there)."""
+        zw, zb, _ = go._zobrist(size)
+        batch = _rg.GameBatch(num_games, size, komi, False, zw.ravel().copy(),
+                              zb.ravel().copy(), self.nthreads)
+        targets = np.asarray(targets, np.int64)
+        counts = np.zeros(num_games, np.int64)
+        snaps = [None] * num_games
+        pending = np.ones(num_games, bool)
+        own = self.learner.move_limit
+        # play() passes once move_count > limit: no real move at move_limit moves or later
+        limit = move_limit - 1 if own is None else min(move_limit - 1, own)
+        K, grp = self._groups(num_games)
+        jobs = [None] * K
+
+        def start(k):
+            idx = self._active(batch, grp, k)
+            if not len(idx):
+                return None
+            due = idx[pending[idx] & (counts[idx] >= targets[idx])]
+            for g in due:
+                snaps[int(g)] = batch.board(int(g)).copy()
+            pending[due] = False
+            return self._launch(batch, self.learner, idx, size, slot=k, limit=limit)
+        for k in range(K):
+            jobs[k] = start(k)
+        while any(j is not None for j in jobs):
+            for k in range(K):
+                if jobs[k] is None:
+                    continue
+                idx = jobs[k]["idx"]
+                self._finish(batch, jobs[k], size)
+                counts[idx] += 1
+                jobs[k] = start(k)
+        for g in np.nonzero(pending)[0]:
+            snaps[int(g)] = batch.board(int(g)).copy()
+        self.illegal = batch.illegal
+        return snaps, batch.winners()

@@ -30,47 +30,160 @@ from .supervised import (Heartbeat, MetadataWriterCallback, _fault_step, _opt_si
                          resume_epoch_base, save_checkpoint)
 
 
+def _python_value_games(player, n, board, move_limit, target):
+    """Lock-step Python self-play of ``n`` games; returns (snapshot states, final states)."""
+    states = [go.GameState(size=board) for _ in range(n)]
+    snap = [None] * n
+    unfinished = list(range(n))
+    while unfinished:
+        sts = [states[i] for i in unfinished]
+        for i, st in zip(unfinished, sts):
+            if snap[i] is None and len(st.history) >= target[i]:
+                snap[i] = st.copy()
+        moves = player.get_moves(sts)
+        nxt = []
+        for i, st, mv in zip(unfinished, sts, moves):
+            st.do_move(mv)
+            if not st.is_end_of_game and len(st.history) < move_limit:
+                nxt.append(i)
+        unfinished = nxt
+    snaps = [snap[i] if snap[i] is not None else states[i] for i in range(n)]
+    return snaps, [s.get_winner() for s in states]
+
+
+def _use_native(player, native):
+    if native is False:
+        return False
+    from .selfplay import NativeSelfPlay
+    ok = NativeSelfPlay.supported(player, player)
+    if native and not ok:
+        raise RuntimeError("native self-play needs a fused-HIP policy player on a GPU")
+    return ok
+
+
 def generate_value_dataset(player, n_games, out_file=None, board=19, features=VALUE_FEATURES,
-                           move_limit=500, rng=None, batch_games=64):
-    """Self-play ``n_games`` with ``player`` (needs get_moves); return (states, values)."""
+                           move_limit=500, rng=None, batch_games=64, rank=0, world=1,
+                           native=None):
+    """Self-play ``n_games`` with ``player`` (needs get_moves); return (states, values).
+
+    Data-parallel generation: with ``world`` > 1 every rank plays its slice of the games
+    (``rank::world``, its own random stream) and returns its rows; with ``out_file`` each rank
+    writes ``<out_file>.part<rank>`` and the caller merges them (``merge_value_shards``; the
+    ``generate`` CLI does this on rank 0 after a barrier). ``native`` (default: when the
+    player runs on the fused HIP path) advances all games of a ply in one native call and one
+    GPU pass (training/selfplay.py) instead of the per-game Python loop."""
     rng = rng or np.random.RandomState(0)
+    if world > 1:
+        rng = np.random.RandomState(rng.randint(0, 2 ** 31 - 1) + 7919 * rank)
+    mine = len(range(rank, n_games, world))
     pp = Preprocess(features)
+    use_native = _use_native(player, native)
+    sp = None
+    if use_native:
+        from .selfplay import NativeSelfPlay
+        sp = NativeSelfPlay(player, player)
+        zw, zb, _ = go._zobrist(board)
+        lookup = {go.WHITE: zw, go.BLACK: zb}
     all_states, all_values = [], []
     done = 0
-    while done < n_games:
-        n = min(batch_games, n_games - done)
-        states = [go.GameState(size=board) for _ in range(n)]
+    while done < mine:
+        n = min(batch_games, mine - done)
         target = [int(rng.randint(0, move_limit // 2)) for _ in range(n)]
-        snap = [None] * n
-        unfinished = list(range(n))
-        while unfinished:
-            sts = [states[i] for i in unfinished]
-            for i, st in zip(unfinished, sts):
-                if snap[i] is None and len(st.history) >= target[i]:
-                    snap[i] = st.copy()
-            moves = player.get_moves(sts)
-            nxt = []
-            for i, st, mv in zip(unfinished, sts, moves):
-                st.do_move(mv)
-                if not st.is_end_of_game and len(st.history) < move_limit:
-                    nxt.append(i)
-            unfinished = nxt
-        for i in range(n):
-            s = snap[i] if snap[i] is not None else states[i]
-            w = states[i].get_winner()
-            z = 0.0 if w == 0 else (1.0 if w == s.current_player else -1.0)
+        if use_native:
+            boards, winners = sp.sample_positions(n, board, target, move_limit)
+            snaps = [go.GameState._wrap(b, board, lookup) for b in boards]
+            winners = [int(w) for w in winners]
+        else:
+            snaps, winners = _python_value_games(player, n, board, move_limit, target)
+        for s, w in zip(snaps, winners):
             all_states.append(s)
-            all_values.append(z)
+            all_values.append(0.0 if w == 0 else (1.0 if w == s.current_player else -1.0))
         done += n
-    X = pp.states_to_tensor_u8(all_states)
+    F = pp.output_dim
+    X = pp.states_to_tensor_u8(all_states) if all_states else \
+        np.zeros((0, F, board, board), np.uint8)
     y = np.asarray(all_values, np.float32).reshape(-1, 1)
     if out_file:
-        with h5lite.File(out_file, "w") as f:
-            f.create_dataset("states", data=X, chunks=(64,) + X.shape[1:], compression="lzf",
-                             maxshape=(None,) + X.shape[1:])
-            f["values"] = y
-            f["features"] = np.bytes_(",".join(features))
+        path = out_file if world == 1 else "%s.part%03d" % (out_file, rank)
+        _write_value_file(path, X, y, features)
     return X, y
+
+
+def _write_value_file(path, X, y, features):
+    with h5lite.File(path, "w") as f:
+        f.create_dataset("states", data=X, chunks=(64,) + X.shape[1:], compression="lzf",
+                         maxshape=(None,) + X.shape[1:])
+        f["values"] = y
+        f["features"] = np.bytes_(",".join(features))
+
+
+def merge_value_shards(out_file, world, remove=True):
+    """Concatenate the per-rank ``<out_file>.partNNN`` files into ``out_file`` (streamed one
+    shard at a time; rank order)."""
+    parts = ["%s.part%03d" % (out_file, r) for r in range(world)]
+    values, feats, ds = [], None, None
+    with h5lite.File(out_file, "w") as f:
+        for p in parts:
+            src = h5lite.File(p)
+            X = src["states"][()]
+            values.append(np.asarray(src["values"][()], np.float32).reshape(-1, 1))
+            feats = src["features"][()]
+            if ds is None:
+                ds = f.create_dataset("states", shape=(0,) + X.shape[1:], dtype=np.uint8,
+                                      chunks=(64,) + X.shape[1:], compression="lzf",
+                                      maxshape=(None,) + X.shape[1:])
+            if len(X):
+                ds.append(X)
+            src.close()
+        f["values"] = np.concatenate(values) if values else np.zeros((0, 1), np.float32)
+        f["features"] = feats if feats is not None else np.bytes_("")
+    if remove:
+        for p in parts:
+            os.remove(p)
+    return out_file
+
+
+def run_generate(cmd_line_args=None):
+    """``generate`` CLI: self-play a value dataset with a policy, sharded over the ranks of a
+    ``torchrun`` job (one GPU each), merged by rank 0."""
+    import argparse
+    from ..models.policy import CNNPolicy
+    from ..players.ai import ProbabilisticPolicyPlayer
+    parser = argparse.ArgumentParser(description="Generate a value-network dataset by self-play.")
+    parser.add_argument("model", help="CNNPolicy JSON model file")
+    parser.add_argument("weights", help="policy weights (HDF5)")
+    parser.add_argument("out_file", help="output HDF5 (states, values, features)")
+    parser.add_argument("--games", "-n", type=int, default=1000)
+    parser.add_argument("--move-limit", type=int, default=500)
+    parser.add_argument("--temperature", type=float, default=0.67)
+    parser.add_argument("--batch-games", type=int, default=256)
+    parser.add_argument("--seed", type=int, default=0)
+    parser.add_argument("--python-loop", action="store_true",
+                        help="per-game Python self-play instead of the native batch")
+    args = parser.parse_args(cmd_line_args)
+    dp = DPContext()
+    pol = CNNPolicy.load_model(args.model, device=dp.device)
+    pol.model.load_weights(args.weights)
+    rng = np.random.RandomState(args.seed)
+    player = ProbabilisticPolicyPlayer(pol, temperature=args.temperature,
+                                       move_limit=args.move_limit, rng=rng)
+    board = pol.model.input_shape[-1]
+    features = list(pol.preprocessor.feature_list) + ["color"]
+    t0 = time.time()
+    X, _ = generate_value_dataset(player, args.games, out_file=args.out_file, board=board,
+                                  features=features, move_limit=args.move_limit, rng=rng,
+                                  batch_games=args.batch_games, rank=dp.rank, world=dp.world,
+                                  native=False if args.python_loop else None)
+    dp.barrier()
+    if dp.world > 1 and dp.is_root:
+        merge_value_shards(args.out_file, dp.world)
+    dp.barrier()
+    dt = time.time() - t0
+    if dp.is_root:
+        print(json.dumps({"games": args.games, "seconds": round(dt, 3),
+                          "games_per_s": round(args.games / max(dt, 1e-9), 3),
+                          "world": dp.world, "out_file": args.out_file}))
+    return args.out_file
 
 
 class ValueTrainer(object):
@@ -286,4 +399,8 @@ def run_training(cmd_line_args=None):
 
 
 if __name__ == '__main__':
-    run_training()
+    import sys
+    if len(sys.argv) > 1 and sys.argv[1] == "generate":
+        run_generate(sys.argv[2:])
+    else:
+        run_training()

@@ -154,6 +154,51 @@ def test_native_selfplay_matches_python_loop(cuda, monkeypatch):
     assert [int(x) for x in w1] == [st.get_winner() for st in states]
     for g in range(n):
         assert len(f1[g]) == len(f2[g])
-        if f1[g]:
-            assert torch.equal(torch.stack(f1[g]), torch.stack(f2[g]))
+        if len(f1[g]):
+            assert torch.equal(rl._stack(f1[g]), rl._stack(f2[g]))
     assert sp.stats["plies"] > 0 and sp.illegal == 0
+
+
+def test_native_value_generation_matches_python_loop(cuda):
+    """generate_value_dataset's native path (all games of a ply in one GameBatch call + one
+    GPU pass) samples the same positions and labels as the Python get_moves loop for a greedy
+    (deterministic) player."""
+    from rocalphago_amd.players.ai import GreedyPolicyPlayer
+    from rocalphago_amd.training import value_trainer as vt
+    feats = ["board", "ones", "turns_since", "liberties", "sensibleness"]
+    pol = CNNPolicy(feats, board=9, layers=3, filters_per_layer=32, device=cuda, seed=21)
+    player = GreedyPolicyPlayer(pol, move_limit=70)
+    kw = dict(board=9, features=feats + ["color"], move_limit=50, batch_games=5)
+    Xn, yn = vt.generate_value_dataset(player, 8, rng=np.random.RandomState(3), native=True, **kw)
+    Xp, yp = vt.generate_value_dataset(player, 8, rng=np.random.RandomState(3), native=False,
+                                       **kw)
+    assert Xn.shape == Xp.shape == (8, 3 + 1 + 8 + 8 + 1 + 1, 9, 9)
+    assert np.array_equal(yn, yp)
+    assert np.array_equal(Xn, Xp)
+
+
+def test_batched_reinforce_update_chunks_sum_to_full_batch(cuda, monkeypatch):
+    """The batched REINFORCE update splits large batches into micro-batches whose gradients add
+    up to the one-shot gradient (kernels index activations with 32-bit offsets)."""
+    import torch
+    from rocalphago_amd.training import reinforcement as rl
+    feats = ["board", "ones", "turns_since", "liberties", "sensibleness"]
+    pol = CNNPolicy(feats, board=9, layers=3, filters_per_layer=32, device=cuda, seed=7)
+    opt = K.SGD(lr=0.0)
+    pol.model.compile(loss=rl.log_loss, optimizer=opt)
+    rs = np.random.RandomState(0)
+    games = []
+    for g in range(5):
+        n = int(rs.randint(3, 12))
+        games.append(torch.from_numpy((rs.rand(n, 21, 9, 9) > 0.6).astype(np.uint8)).to(cuda))
+    moves = [list(rs.randint(0, 81, len(f))) for f in games]
+    won = [True, False, True, True, False]
+    rl._batched_update(pol.model, opt, games, moves, won, 81, None)
+    full = pol.model.net.flat_grad.clone()
+    monkeypatch.setattr(rl, "_UPDATE_CHUNK", 7)
+    rl._batched_update(pol.model, opt, games, moves, won, 81, None)
+    chunked = pol.model.net.flat_grad.clone()
+    torch.cuda.synchronize()
+    scale = full.abs().max().item()
+    assert scale > 0
+    assert (full - chunked).abs().max().item() < 1e-2 * scale

@@ -46,7 +46,7 @@ def test_pass_logit_forward_and_roundtrip(tmp_path):
     assert PASS_MOVE in probs and abs(sum(probs.values()) - 1) < 1e-5
     js, h5 = str(tmp_path / "p.json"), str(tmp_path / "p.h5")
     p.save_model(js, h5)
-    q = NeuralNetBase.load_model(js)
+    q = NeuralNetBase.load_model(js, device="cpu")  # the same (fp32) executor as p
     assert has_pass_logit(q)
     np.testing.assert_allclose(q.forward(x), out, rtol=1e-6, atol=1e-7)
 

@@ -181,3 +181,60 @@ def test_resnet_plan_train_step_matches_generic(ops, K, layers, board, n_skip):
         cos = torch.dot(gc, gg).item() / (nc * gg.norm().item() + 1e-12)
         assert cos > 0.98, (wname, cos)
         assert abs(gg.norm().item() / nc - 1) < 0.08, (wname, gg.norm().item(), nc)
+
+
+def test_pass_grads_kernel_matches_torch(ops):
+    """head.hip pass_grads_kernel: dW = dpass^T z, db = sum dpass (fp32 torch reference)."""
+    g = torch.Generator().manual_seed(0)
+    for B, P in [(1, 49), (7, 81), (256, 361)]:
+        z = torch.randn(B, P, generator=g).cuda()
+        dp = torch.randn(B, generator=g).cuda()
+        dW = torch.full((P,), 9.0, device="cuda")
+        db = torch.full((1,), 9.0, device="cuda")
+        ops.pass_grads(z, dp, dW, db)
+        torch.cuda.synchronize()
+        ref = (z.double().t() @ dp.double()).float()
+        assert torch.allclose(dW, ref, rtol=1e-5, atol=1e-4 * max(1.0, ref.abs().max().item()))
+        assert abs(db.item() - dp.double().sum().item()) < 1e-4 * B
+
+
+def test_resnet_plan_with_pass_logit_matches_generic(ops):
+    """ResnetPlan carries the PassLogit head (softmax over S*S + 1) in forward and training,
+    with the PassLogit gradients on HIP; the update matches the generic fp32 executor."""
+    from rocalphago_amd.models import kerasish as KZ
+    from rocalphago_amd.models.fused import ResnetPlan
+    cpu, gpu = _pair(32, 4, 9, {"pass_logit": True})
+    assert isinstance(gpu.model._plan_for(), ResnetPlan)
+    assert gpu.model._plan_for().pass_name is not None
+    rs = np.random.RandomState(4)
+    w = cpu.model.get_weights()
+    w[-2] = (rs.randn(81) * 0.05).astype(np.float32)
+    w[-1] = np.array([0.4], np.float32)
+    cpu.model.set_weights(w)
+    gpu.model.set_weights(w)
+    X = _planes(12, 9, 3)
+    pc, pg = cpu.model.predict(X), gpu.model.predict(X)
+    assert pg.shape == (12, 82) and np.abs(pg - pc).max() < 2e-2
+    Y = np.zeros((12, 82), np.float32)
+    Y[np.arange(12), rs.randint(0, 82, 12)] = 1
+    Y[:4, :] = 0
+    Y[:4, 81] = 1  # pass targets
+    for m in (cpu.model, gpu.model):
+        m.compile(loss="categorical_crossentropy", optimizer=KZ.SGD(lr=0.0))
+    lc, lg = cpu.model.train_on_batch(X, Y), gpu.model.train_on_batch(X, Y)
+    assert abs(lc - lg) < 0.05 * abs(lc)
+    net_c, net_g = cpu.model.net, gpu.model.net
+    names = [wn for _, wn, _ in net_c.weight_names]
+    for wname, gc, gg in zip(names, net_c._gviews, net_g._gviews):
+        if "running" in wname:
+            continue
+        gc, gg = gc.detach().reshape(-1), gg.detach().cpu().reshape(-1)
+        nc = gc.norm().item()
+        if nc < 1e-6:
+            continue
+        cos = torch.dot(gc, gg).item() / (nc * gg.norm().item() + 1e-12)
+        assert cos > 0.98, (wname, cos)
+    # the PassLogit tensors are the last two weights
+    for gc, gg in zip(net_c._gviews[-2:], net_g._gviews[-2:]):
+        gc, gg = gc.detach().reshape(-1), gg.detach().cpu().reshape(-1)
+        assert (gc - gg).abs().max().item() < 5e-2 * max(gc.abs().max().item(), 1e-3)

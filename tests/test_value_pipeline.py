@@ -36,3 +36,50 @@ def test_generate_dataset_and_train(tmp_path, device="cpu"):
     # resume
     vt.run_training([spec, data, out, "--epochs", "1", "--minibatch", "4",
                      "--weights", "weights.00001.hdf5"])
+
+
+def test_sharded_generation_merges_rank_slices(tmp_path):
+    """Data-parallel generation: each rank plays its slice (rank::world) with its own random
+    stream; the merged file holds every rank's rows in rank order."""
+    pol = CNNPolicy(["board", "ones", "sensibleness"], board=7, filters_per_layer=8, layers=2,
+                    device="cpu", seed=1)
+    out = str(tmp_path / "v.h5")
+    parts = []
+    for r in range(3):
+        player = ProbabilisticPolicyPlayer(pol, move_limit=40, rng=np.random.RandomState(r))
+        parts.append(vt.generate_value_dataset(player, 10, out_file=out, board=7, move_limit=40,
+                                               rng=np.random.RandomState(5), batch_games=3,
+                                               rank=r, world=3))
+    assert [len(x) for x, _ in parts] == [4, 3, 3]
+    vt.merge_value_shards(out, 3)
+    assert not os.path.exists(out + ".part000")
+    with h5lite.File(out) as f:
+        X = f["states"][()]
+        assert X.shape == (10, 49, 7, 7)
+        assert np.array_equal(X, np.concatenate([x for x, _ in parts]))
+        assert np.array_equal(f["values"][()], np.concatenate([y for _, y in parts]))
+
+
+def test_generate_cli_two_ranks(tmp_path):
+    """``value_trainer generate`` under torchrun (2 gloo ranks): shards merged by rank 0."""
+    import subprocess
+    import sys
+    pol = CNNPolicy(["board", "ones", "sensibleness"], board=7, filters_per_layer=8, layers=2,
+                    device="cpu", seed=1)
+    spec, weights = str(tmp_path / "p.json"), str(tmp_path / "p.hdf5")
+    pol.save_model(spec)
+    pol.model.save_weights(weights)
+    out = str(tmp_path / "gen.h5")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                        "29631", "-m", "rocalphago_amd.training.value_trainer", "generate", spec,
+                        weights, out, "--games", "6", "--move-limit", "30", "--batch-games", "2"],
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rep = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert rep["world"] == 2 and rep["games"] == 6
+    with h5lite.File(out) as f:
+        assert f["states"].shape == (6, 6, 7, 7)  # board 3 + ones + sensibleness + color
+        assert f["values"].shape == (6, 1)
