@@ -573,7 +573,10 @@ bool rag_conv_slab_launch(const bf16* x, const bf16* w, const float* bias, bf16*
 bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* y,
                          const bf16* mk, const bf16* res, int M, int S, int WI, int shift, int WO,
                          int HO, int CIN, int COUTP, int YC, int KS, int relu, int HM,
-                         long total_rows, hipStream_t stream, const WgradRed* red);  // conv_tap.hip
+                         long total_rows, hipStream_t stream, const WgradRed* red,
+                         const float* bnc, const float* mcoef);  // conv_tap.hip
+bool rag_conv_tap_bn_ok(int M, int S, int WI, int shift, int CIN, int COUTP, int KS);
+bool rag_wgrad_slab_ok(int S, int H, int HG, int GC, int COUTP, int CINP, int KS);
 
 // Conv forward / dgrad.  X: padded input (halo HI, CIN channels, CIN % 32 == 0).  W: packed
 // bf16 weights [taps][WROWS][CIN].  Y: padded output (halo HO, YC channels, COUTP % 32 == 0,
@@ -618,11 +621,47 @@ RAG_API int rag_wgrad_flush(hipStream_t stream, void* pending) {
   return flush_pending(pending, stream);
 }
 
+// BN prologue fusion (ResnetPolicy): true if rag_conv_igemm_bn / rag_conv_wgrad*_bn can run a
+// layer of this shape with its input given as the BN input x plus [3][S] column coefficients.
+RAG_API int rag_conv_bn_fusable(int B, int S, int HI, int CIN, int COUTP, int KS) {
+  return KS == 3 && HI == 1 && CIN == COUTP &&
+         rag_conv_tap_bn_ok(B * S * S, S, S + 2 * HI, HI - 1, CIN, COUTP, KS) &&
+         rag_wgrad_slab_ok(S, HI, HI, COUTP, COUTP, CIN, KS);
+}
+
+static int conv_igemm_impl(const void* X, const void* W, const float* bias, void* Y,
+                           const void* mask, const void* resid, int B, int S, int HI, int HO,
+                           int CIN, int COUTP, int YC, int KS, int relu, int HM,
+                           hipStream_t stream, void* pending, const float* bnc,
+                           const float* mcoef);
+
 // `pending`: null, or the caller's deferred-reduction handle (see PendingRed above).
 RAG_API int rag_conv_igemm(const void* X, const void* W, const float* bias, void* Y,
                            const void* mask, const void* resid, int B, int S, int HI, int HO,
                            int CIN, int COUTP, int YC, int KS, int relu, int HM,
                            hipStream_t stream, void* pending) {
+  return conv_igemm_impl(X, W, bias, Y, mask, resid, B, S, HI, HO, CIN, COUTP, YC, KS, relu, HM,
+                         stream, pending, nullptr, nullptr);
+}
+
+// As rag_conv_igemm with the BN prologue: X is the BN input x and the layer input is
+// U = ReLU(bnc[0][col] * x + bnc[2][col]) (forward), and/or the dgrad ReLU mask is recomputed
+// from `mask` = x and mcoef (no residual then). -5 if the shape has no fused kernel
+// (rag_conv_bn_fusable).
+RAG_API int rag_conv_igemm_bn(const void* X, const void* W, const float* bias, void* Y,
+                              const void* mask, const void* resid, int B, int S, int HI, int HO,
+                              int CIN, int COUTP, int YC, int relu, int HM, hipStream_t stream,
+                              void* pending, const float* bnc, const float* mcoef) {
+  if ((!bnc && !mcoef) || (mcoef && resid)) return -5;
+  return conv_igemm_impl(X, W, bias, Y, mask, resid, B, S, HI, HO, CIN, COUTP, YC, 3, relu, HM,
+                         stream, pending, bnc, mcoef);
+}
+
+static int conv_igemm_impl(const void* X, const void* W, const float* bias, void* Y,
+                           const void* mask, const void* resid, int B, int S, int HI, int HO,
+                           int CIN, int COUTP, int YC, int KS, int relu, int HM,
+                           hipStream_t stream, void* pending, const float* bnc,
+                           const float* mcoef) {
   if (CIN % 32 || COUTP % 32 || YC < COUTP || HI < KS / 2) return -1;
   const int M = B * S * S;
   const int nt = pick_nt(COUTP);
@@ -648,13 +687,21 @@ RAG_API int rag_conv_igemm(const void* X, const void* W, const float* bias, void
       if (rc) return rc;
     }
   }
+  if (bnc || mcoef) {  // BN prologue: the 128-channel ping-pong kernel or nothing
+    if (rag_conv_tap_launch(x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, KS,
+                            relu, HM, (long)B * WI * WI, stream, red, bnc, mcoef))
+      return (int)hipGetLastError();
+    if (red) rag_launch_wgrad_slab_reduce(*red, stream);
+    return -5;
+  }
   if (rag_conv_slab_launch(x, w, bias, y, mk, res, B, S, HI, WO, HO, CIN, COUTP, YC, KS, relu,
                            HM, stream)) {
     const int rc = red ? rag_launch_wgrad_slab_reduce(*red, stream) : 0;  // opt-in slab conv
     return rc ? rc : (int)hipGetLastError();
   }
   if (use_pipe && rag_conv_tap_launch(x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN,
-                                      COUTP, YC, KS, relu, HM, (long)B * WI * WI, stream, red))
+                                      COUTP, YC, KS, relu, HM, (long)B * WI * WI, stream, red,
+                                      nullptr, nullptr))
     return (int)hipGetLastError();
   if (red) {  // not a tap-slab launch: the reduction goes out on its own first
     const int rc = rag_launch_wgrad_slab_reduce(*red, stream);
@@ -686,7 +733,8 @@ WgradRed rag_wgrad_slab_red(const void* part, const float* bpart, float* dW, flo
                             int nchunks, int CINP, int COUT, int CIN, int accumulate);
 int rag_launch_wgrad_slab_reduce(const WgradRed& r, hipStream_t stream);        // wgrad_slab.hip
 int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpart, int R, int WP,
-                          int GC, int CIN, int spc, int CINP, int nchunks, hipStream_t stream);
+                          int GC, int CIN, int spc, int CINP, int nchunks, hipStream_t stream,
+                          const float* xcoef, int S);
 
 namespace {
 // all-taps variant applicability and plan (see wgrad.hip)
@@ -763,7 +811,8 @@ static void launch_wgrad_ks(int ntn, int ntc, dim3 grid, hipStream_t st, const b
 static int conv_wgrad_impl(const void* G, const void* X, float* dW, float* db, float* work,
                            int B, int S, int HI, int HG, int GC, int COUT, int COUTP, int CIN,
                            int CINP, int KS, int accumulate, hipStream_t stream,
-                           hipStream_t reduce_stream, void* pending) {
+                           hipStream_t reduce_stream, void* pending,
+                           const float* xcoef = nullptr) {
   {  // a pending reduction reads the partial slabs this wgrad is about to overwrite
     const int rc = flush_pending(pending, nullptr);
     if (rc) return rc;
@@ -778,7 +827,9 @@ static int conv_wgrad_impl(const void* G, const void* X, float* dW, float* db, f
   float* part = work;
   float* bpart;
   bool bf16_part = false;
-  if (rag_wgrad_slab_ok(S, HI, HG, GC, COUTP, CINP, KS)) {
+  const bool slab = rag_wgrad_slab_ok(S, HI, HG, GC, COUTP, CINP, KS);
+  if (xcoef && !(slab && rag_wgrad_slab_bf16() && CINP == 128)) return -5;
+  if (slab) {
     bf16_part = rag_wgrad_slab_bf16();
     const int WP = S + 2 * HI;
     const int R = B * WP * WP;
@@ -786,7 +837,7 @@ static int conv_wgrad_impl(const void* G, const void* X, float* dW, float* db, f
     nchunks = rag_wgrad_slab_nchunks(R, CINP, &spc);
     bpart = db ? work + (size_t)nchunks * taps * COUTP * CINP : nullptr;
     const int rc = rag_launch_wgrad_slab(g, x, part, bpart, R, WP, GC, CINP, spc, CINP, nchunks,
-                                         stream);
+                                         stream, xcoef, S);
     if (rc) return rc;
   } else if (tp.ok) {
     nchunks = tp.nchunks;
@@ -876,6 +927,17 @@ RAG_API int rag_conv_wgrad_deferred(const void* G, const void* X, float* dW, flo
   if (!pending) return -4;
   return conv_wgrad_impl(G, X, dW, db, work, B, S, HI, HG, GC, COUT, COUTP, CIN, CINP, KS,
                          accumulate, stream, nullptr, pending);
+}
+
+// As rag_conv_wgrad_deferred with the BN prologue: X is the BN input x and the layer input is
+// U = ReLU(xcoef[0][col] * x + xcoef[2][col]) (-5 if the shape has no fused kernel).
+RAG_API int rag_conv_wgrad_deferred_bn(const void* G, const void* X, float* dW, float* db,
+                                       float* work, int B, int S, int HI, int HG, int GC, int COUT,
+                                       int COUTP, int CIN, int CINP, int KS, int accumulate,
+                                       hipStream_t stream, void* pending, const float* xcoef) {
+  if (!xcoef) return -5;
+  return conv_wgrad_impl(G, X, dW, db, work, B, S, HI, HG, GC, COUT, COUTP, CIN, CINP, KS,
+                         accumulate, stream, nullptr, pending, xcoef);
 }
 
 RAG_API int rag_pack_weights(const float* W, void* Wf, void* Wb, int COUT, int CIN, int KS,

@@ -105,16 +105,18 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NT][kMT], int mw, in
 // 192 channels (384 contiguous bytes in the channels-last activation) with 16-byte lane chunks,
 // applying the dgrad ReLU mask from equally coalesced reads. The register epilogue above writes
 // 16 pixels x 32 bytes per store instruction; this one writes whole rows.
-constexpr int kEpRow = kBN + 8;  // bf16 per LDS image row
-template <int BM>
-__device__ __forceinline__ void epilogue_lds(const f32x4 (&acc)[kNT][kMT], bf16* __restrict__ img,
+constexpr int kEpRow = kBN + 8;  // bf16 per LDS image row (192 channels; NT = 4: 136)
+template <int BM, int NT = kNT>
+__device__ __forceinline__ void epilogue_lds(const f32x4 (&acc)[NT][kMT], bf16* __restrict__ img,
                                              int mwl, int nwl, int m0, int n0, int M, int S,
                                              int WO, int HO, int YC, int HM,
                                              const float* __restrict__ bias, int relu,
                                              const bf16* __restrict__ mask,
-                                             bf16* __restrict__ Y, int frow, int fq) {
+                                             bf16* __restrict__ Y, int frow, int fq,
+                                             const float* __restrict__ mcoef = nullptr) {
+  constexpr int EpRow = 32 * NT + 8;
 #pragma unroll
-  for (int j = 0; j < kNT; ++j) {
+  for (int j = 0; j < NT; ++j) {
     const int n = nwl + j * 16 + fq * 4;
     float4 bb = {0.f, 0.f, 0.f, 0.f};
     if (bias) bb = *reinterpret_cast<const float4*>(bias + n0 + n);
@@ -125,12 +127,12 @@ __device__ __forceinline__ void epilogue_lds(const f32x4 (&acc)[kNT][kMT], bf16*
       bf16x4 o;
 #pragma unroll
       for (int r = 0; r < 4; ++r) o[r] = (bf16)(relu ? fmaxf(v[r], 0.f) : v[r]);
-      *reinterpret_cast<bf16x4*>(img + (mwl + i * 16 + frow) * kEpRow + n) = o;
+      *reinterpret_cast<bf16x4*>(img + (mwl + i * 16 + frow) * EpRow + n) = o;
     }
   }
   __syncthreads();
   const int S2 = S * S, WMK = S + 2 * HM;
-  constexpr int kChunks = kBN / 8;  // 16-byte chunks per pixel row
+  constexpr int kChunks = 32 * NT / 8;  // 16-byte chunks per pixel row
   for (int c = threadIdx.x; c < BM * kChunks; c += blockDim.x) {
     const int row = c / kChunks, k8 = (c - row * kChunks) * 8;
     const int m = m0 + row;
@@ -138,12 +140,20 @@ __device__ __forceinline__ void epilogue_lds(const f32x4 (&acc)[kNT][kMT], bf16*
     const int b = m / S2;
     const int rem = m - b * S2;
     const int pi = rem / S, pj = rem - pi * S;
-    bf16x8 v = *reinterpret_cast<const bf16x8*>(img + row * kEpRow + k8);
+    bf16x8 v = *reinterpret_cast<const bf16x8*>(img + row * EpRow + k8);
     if (mask) {
       const bf16x8 mk = *reinterpret_cast<const bf16x8*>(
           mask + (size_t)((b * WMK + pi + HM) * WMK + pj + HM) * YC + n0 + k8);
+      if (mcoef) {
+        // the layer input U = ReLU(cx[col] * x + cc[col]) was never stored (BN prologue): the
+        // mask is recomputed from the BN input x and the column coefficients
+        const float cx = mcoef[pj], cc = mcoef[2 * S + pj];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = ((float)mk[e] > 0.f) ? v[e] : (bf16)0.f;
+        for (int e = 0; e < 8; ++e) v[e] = fmaf(cx, (float)mk[e], cc) > 0.f ? v[e] : (bf16)0.f;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = ((float)mk[e] > 0.f) ? v[e] : (bf16)0.f;
+      }
     }
     *reinterpret_cast<bf16x8*>(Y + (size_t)((b * WO + pi + HO) * WO + pj + HO) * YC + n0 + k8) =
         v;
@@ -631,20 +641,26 @@ constexpr int kPPBM = 384;
 constexpr int kPPSlabRows = 640;
 constexpr int kPPSlab = kPPSlabRows * kBK;
 constexpr int kPPAL = kPPSlabRows / 64;  // slab glds per loader wave (4 loader waves x 16 rows)
-constexpr int kPPBL = kBN / 64;          // weight glds per loader wave per step
 
 // DIAG (diagnostic builds only, wrong results): bit 0 = no staging inside the loop, bit 1 = no
 // fragment reads (MFMAs on stale registers), bit 2 = clock stamps (s_memtime / s_memrealtime of
 // wave 0 around the main loop into `stamps`).
-template <int NB, int DIAG = 0, int ISSUE = 0>
+// BNP (ResnetPolicy, K13): the input slab is X = the BN input x, and the loader waves turn each
+// staged slab into U = ReLU(cx[col] * x + cc[col]) in place (zero on halo rows) before the barrier
+// that publishes it, with bnc = the BN's [3][S] column coefficients; U is never written to HBM.
+// mcoef: the dgrad form of the same fusion (mask = U > 0 recomputed from x, see epilogue_lds).
+template <int NB, int DIAG = 0, int ISSUE = 0, int NT = kNT, bool BNP = false>
 __global__ void __launch_bounds__(512)
 conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                    const float* __restrict__ bias, bf16* __restrict__ Y,
                    const bf16* __restrict__ mask, const bf16* __restrict__ res, int M, int S,
                    int WI, int shift, int WO, int HO, int CIN, int WROWS, int YC, int relu, int HM,
-                   long total_rows, int nconv, WgradRed red, long long* stamps = nullptr) {
-  constexpr int kLoop = 2 * kPPSlab + NB * kBTile;
-  constexpr int kL = kLoop > kPPBM * kEpRow ? kLoop : kPPBM * kEpRow;  // loop ring | epilogue image
+                   long total_rows, int nconv, WgradRed red, const float* __restrict__ bnc = nullptr,
+                   const float* __restrict__ mcoef = nullptr, long long* stamps = nullptr) {
+  constexpr int BN = 32 * NT, BTile = BN * kBK, PPBL = BN / 64, EpRow = BN + 8;
+  static_assert(BN % 64 == 0, "the loader waves stage 64-row weight slices");
+  constexpr int kLoop = 2 * kPPSlab + NB * BTile;
+  constexpr int kL = kLoop > kPPBM * EpRow ? kLoop : kPPBM * EpRow;  // loop ring | epilogue image
   // weight tiles staged ahead of the current step (issued in the MFMA segment, the slot's last
   // reader is one phase further back: NB tiles ahead are safe)
   constexpr int D = ISSUE ? NB : NB - 1;
@@ -664,7 +680,7 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
   const int bid = xcd_remap(blockIdx.x, nconv);
   const int bm = bid % nblk_m, bn = bid / nblk_m;
   const int m0 = bm * kPPBM;
-  const int n0 = bn * kBN;
+  const int n0 = bn * BN;
   const int S2 = S * S;
   auto prow = [&](int m) {
     const int b = m / S2;
@@ -678,9 +694,44 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
   const int lrow = lane >> 2, lcol = lane & 3;
 
   // group 0's weight sources (row (wl + 4k)*16 + lane/4 of the 192-row tile)
-  const bf16* bsrc[kPPBL];
+  // BNP: per staged slab row of this lane (fixed across chunks: column BN), the coefficients of
+  // U = ReLU(cx * x + cc); zero on halo / past-the-end rows, so U = 0 there
+  float pcx[BNP ? kPPAL : 1], pcc[BNP ? kPPAL : 1];
+  if constexpr (BNP) {
+    const long WI2 = (long)WI * WI;
+    const int hi = shift + 1;  // 3x3: the input halo
 #pragma unroll
-  for (int k = 0; k < kPPBL; ++k) {
+    for (int k = 0; k < kPPAL; ++k) {
+      const long g = base + (wl + 4 * k) * 16 + lrow;
+      const long b = g / WI2;
+      const int rem = (int)(g - b * WI2);
+      const int ii = rem / WI, jj = rem - (rem / WI) * WI;
+      const bool in = g < total_rows && ii >= hi && ii < hi + S && jj >= hi && jj < hi + S;
+      pcx[k] = in ? bnc[jj - hi] : 0.f;
+      pcc[k] = in ? bnc[2 * S + jj - hi] : 0.f;
+    }
+  }
+  // after this wave's own slab(q) loads completed: its 16 bytes of staged rows k0 .. k1-1 -> U.
+  // The next chunk's slab is transformed two rows per step over taps 4..8 of the current chunk
+  // (its loads, issued at tap 0, have landed by tap 4), behind group 0's MFMA issue, so the LDS
+  // round trips never sit in front of a barrier (all ten at tap 8 cost +10 % kernel time).
+  auto bn_slab = [&](int q, int k0, int k1) {
+    if constexpr (BNP) {
+      bf16* dst = lds + (q & 1) * kPPSlab;
+#pragma unroll
+      for (int k = 0; k < kPPAL; ++k) {
+        if (k < k0 || k >= k1) continue;
+        bf16x8* p = reinterpret_cast<bf16x8*>(dst + (wl + 4 * k) * 16 * kBK + lane * 8);
+        bf16x8 v = *p;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (bf16)fmaxf(fmaf(pcx[k], (float)v[e], pcc[k]), 0.f);
+        *p = v;
+      }
+    }
+  };
+  const bf16* bsrc[PPBL];
+#pragma unroll
+  for (int k = 0; k < PPBL; ++k) {
     const int r = (wl + 4 * k) * 16 + lrow;
     bsrc[k] = Wt + (long)(n0 + r) * CIN + ((lcol ^ swz4(r)) * 8);
   }
@@ -696,10 +747,10 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
   };
   auto stage_b = [&](int s) {  // step s = chunk * 9 + tap
     const int q = s / 9, t = s - q * 9;
-    bf16* dst = lds + 2 * kPPSlab + (s % NB) * kBTile;
+    bf16* dst = lds + 2 * kPPSlab + (s % NB) * BTile;
     const long off = t * tap_stride + q * kBK;
 #pragma unroll
-    for (int k = 0; k < kPPBL; ++k) glds16(bsrc[k] + off, dst + (wl + 4 * k) * 16 * kBK);
+    for (int k = 0; k < PPBL; ++k) glds16(bsrc[k] + off, dst + (wl + 4 * k) * 16 * kBK);
   };
 
   const int frow = lane & 15;
@@ -711,22 +762,22 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
     m = m < M ? m : M - 1;
     prel[i] = (int)(prow(m) - base);
   }
-  int boffs[kNT];
+  int boffs[NT];
 #pragma unroll
-  for (int j = 0; j < kNT; ++j) {
-    const int row = wn * (16 * kNT) + j * 16 + frow;
+  for (int j = 0; j < NT; ++j) {
+    const int row = wn * (16 * NT) + j * 16 + frow;
     boffs[j] = row * kBK + ((fq ^ swz4(row)) * 8);
   }
 
-  f32x4 acc[kNT][kMT];
+  f32x4 acc[NT][kMT];
 #pragma unroll
-  for (int j = 0; j < kNT; ++j)
+  for (int j = 0; j < NT; ++j)
 #pragma unroll
     for (int i = 0; i < kMT; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int cchunks = CIN / kBK;
   const int nsteps = 9 * cchunks;
-  bf16x8 xa[kMT], wb[kNT];
+  bf16x8 xa[kMT], wb[NT];
   auto read_frags = [&](int s) {
     if constexpr (DIAG & 2) {
       asm volatile("" : "+v"(xa[0]), "+v"(wb[0]));
@@ -734,7 +785,7 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
     }
     const int q = s / 9, t = s - q * 9;
     const bf16* slab = lds + (q & 1) * kPPSlab;
-    const bf16* bt = lds + 2 * kPPSlab + (s % NB) * kBTile;
+    const bf16* bt = lds + 2 * kPPSlab + (s % NB) * BTile;
     const int ky = t / 3, kx = t - ky * 3;
     const int toff = ky * WI + kx;
 #pragma unroll
@@ -743,13 +794,13 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
       xa[i] = *reinterpret_cast<const bf16x8*>(slab + r * kBK + ((fq ^ swz4(r)) * 8));
     }
 #pragma unroll
-    for (int j = 0; j < kNT; ++j) wb[j] = *reinterpret_cast<const bf16x8*>(bt + boffs[j]);
+    for (int j = 0; j < NT; ++j) wb[j] = *reinterpret_cast<const bf16x8*>(bt + boffs[j]);
     lds_reads_done();  // retire this burst before the wave's next barrier (WAR on the LDS)
   };
   auto mfmas = [&]() {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int j = 0; j < kNT; ++j)
+    for (int j = 0; j < NT; ++j)
 #pragma unroll
       for (int i = 0; i < kMT; ++i) acc[j][i] = mfma16(wb[j], xa[i], acc[j][i]);
     __builtin_amdgcn_s_setprio(0);
@@ -758,12 +809,12 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
   auto mfmas_staged = [&](int sb) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int j = 0; j < kNT; ++j) {
+    for (int j = 0; j < NT; ++j) {
 #pragma unroll
       for (int i = 0; i < kMT; ++i) acc[j][i] = mfma16(wb[j], xa[i], acc[j][i]);
-      if (j < kPPBL && sb >= 0) {
+      if (j < PPBL && sb >= 0) {
         const int q = sb / 9, t = sb - q * 9;
-        bf16* dst = lds + 2 * kPPSlab + (sb % NB) * kBTile;
+        bf16* dst = lds + 2 * kPPSlab + (sb % NB) * BTile;
         glds16(bsrc[j] + t * tap_stride + q * kBK, dst + (wl + 4 * j) * 16 * kBK);
       }
     }
@@ -781,7 +832,7 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
 #pragma unroll
       for (int e = 0; e < 8; ++e) xa[i][e] = (bf16)(((lane * 37 + i * 11 + e * 5) % 29) * 0.07f - 1.f);
 #pragma unroll
-    for (int j = 0; j < kNT; ++j)
+    for (int j = 0; j < NT; ++j)
 #pragma unroll
       for (int e = 0; e < 8; ++e) wb[j][e] = (bf16)(((lane * 13 + j * 7 + e * 3) % 31) * 0.06f - 0.9f);
   }
@@ -798,6 +849,7 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
   if (grp == 0) {
     stage_a(0);
     wait_vm<0>();
+    bn_slab(0, 0, kPPAL);
 #pragma unroll 1
     for (int s = 0; s < nsteps; ++s) {
       const int q = s / 9, t = s - q * 9;
@@ -816,7 +868,16 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
       const long long c4 = now();
       mfmas();
       const long long c5 = now();
-      if (t == 8 && more) wait_vm<0>();  // slab(q+1) complete before X of the next chunk
+      if constexpr (BNP) {
+        // slab(q+1) complete at tap 4, transformed over taps 4..8 (this wave's reads of step s+1
+        // drain the writes before the next chunk's X barrier)
+        if (t >= 4 && more) {
+          if (t == 4) wait_vm<0>();
+          bn_slab(q + 1, 2 * (t - 4), 2 * (t - 4) + 2);
+        }
+      } else {
+        if (t == 8 && more) wait_vm<0>();  // slab(q+1) complete before X of the next chunk
+      }
       const long long c6 = now();
       if constexpr (DIAG & 8) {  // X wait, stage+read, Y wait, MFMA issue, vm wait
         acc_t[0] += c2 - c1;
@@ -830,7 +891,7 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
 #pragma unroll
     for (int k = 0; k < D; ++k)
       if (k < nsteps) stage_b(k);
-    wait_vm_rt((nsteps - 1 < D - 1 ? nsteps - 1 : D - 1) * kPPBL);  // B(0) complete
+    wait_vm_rt((nsteps - 1 < D - 1 ? nsteps - 1 : D - 1) * PPBL);  // B(0) complete
 #pragma unroll 1
     for (int s = 0; s < nsteps; ++s) {
       const long long c0 = now();
@@ -854,13 +915,13 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
           // B(s+1) complete before X_{s+1}: issued so far are B(.. min(s-1+D, nsteps-1))
           int last = s - 1 + D < nsteps - 1 ? s - 1 + D : nsteps - 1;
           const int yb = last - (s + 1);
-          wait_vm_rt(yb > 0 ? yb * kPPBL : 0);
+          wait_vm_rt(yb > 0 ? yb * PPBL : 0);
         } else {
           if (s + D < nsteps) stage_b(s + D);
           // B(s+1) complete before X_{s+1}: younger are B(s+2 .. min(s+D, nsteps-1))
           int yb = nsteps - 2 - s;
           yb = yb < D - 1 ? yb : D - 1;
-          wait_vm_rt(yb > 0 ? yb * kPPBL : 0);
+          wait_vm_rt(yb > 0 ? yb * PPBL : 0);
         }
       }
       const long long c5 = now();
@@ -887,12 +948,12 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
     r1 = __builtin_amdgcn_s_memrealtime();
   }
   if (res) {
-    epilogue(acc, m0 + wm * (16 * kMT), n0 + wn * (16 * kNT), M, S, WO, HO, YC, HM, bias, res,
+    epilogue(acc, m0 + wm * (16 * kMT), n0 + wn * (16 * NT), M, S, WO, HO, YC, HM, bias, res,
              relu, mask, Y, frow, fq);
   } else {
     __syncthreads();  // every wave is past its last LDS read: the ring becomes the output image
-    epilogue_lds<kPPBM>(acc, lds, wm * (16 * kMT), wn * (16 * kNT), m0, n0, M, S, WO, HO, YC, HM,
-                        bias, relu, mask, Y, frow, fq);
+    epilogue_lds<kPPBM, NT>(acc, lds, wm * (16 * kMT), wn * (16 * NT), m0, n0, M, S, WO, HO, YC, HM,
+                        bias, relu, mask, Y, frow, fq, mcoef);
   }
   if constexpr (DIAG & 4) {
     // per block: loop cycles, loop ticks, then absolute ticks at entry / loop start / loop end /
@@ -947,7 +1008,8 @@ RAG_API int rag_conv_pp_diag(int diag, const void* X, const void* W, const float
 #define RAG_PPD(D)                                                                               \
   conv_tap_pp_kernel<4, D><<<nconv, 512, 0, stream>>>(x, w, bias, y, mk, nullptr, M, S, WI,      \
                                                       shift, WO, HO, CIN, COUTP, YC, relu, HM,  \
-                                                      total, nconv, r, g_stamps)
+                                                      total, nconv, r, nullptr, nullptr, \
+                                                      g_stamps)
   switch (diag & 11) {
     case 0: RAG_PPD(4); break;
     case 1: RAG_PPD(5); break;
@@ -995,15 +1057,25 @@ RAG_API int rag_conv_tap_mode(int mode) {
 // 8 / 9 = the same with the weight loads issued inside the MFMA segment (measured slower).
 int rag_launch_wgrad_slab_reduce(const WgradRed& r, hipStream_t stream);  // wgrad_slab.hip
 
+// bnc / mcoef (BN prologue / mask coefficients, conv_tap_pp_kernel BNP): only the 128-channel
+// ping-pong path takes them; with either set, any other shape returns false.
+bool rag_conv_tap_bn_ok(int M, int S, int WI, int shift, int CIN, int COUTP, int KS);
+
 bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* y,
                          const bf16* mk, const bf16* res, int M, int S, int WI, int shift, int WO,
                          int HO, int CIN, int COUTP, int YC, int KS, int relu, int HM, long total_rows,
-                         hipStream_t stream, const WgradRed* red) {
+                         hipStream_t stream, const WgradRed* red, const float* bnc,
+                         const float* mcoef) {
+  if ((bnc || mcoef) && ((mcoef && res) || !rag_conv_tap_bn_ok(M, S, WI, shift, CIN, COUTP, KS)))
+    return false;
   if (g_tap_mode < 0) {
     const char* e = getenv("RAG_CONV_TAP");
     g_tap_mode = e ? atoi(e) : 6;  // ping-pong, 3-deep ring: profiles/conv_pp_r3.txt
   }
-  if (!g_tap_mode || KS != 3 || COUTP % kBN || CIN % kBK || CIN < kBK) return false;
+  // 192-multiple widths: 96 x 96 wave tiles (NT = 6); 128-multiple widths (ResnetPolicy's and
+  // the reference CNNPolicy's default 128 filters) only on the ping-pong kernel, 96 x 64 (NT = 4)
+  const bool w192 = COUTP % kBN == 0, w128 = !w192 && COUTP % 128 == 0;
+  if (!g_tap_mode || KS != 3 || !(w192 || w128) || CIN % kBK || CIN < kBK) return false;
   static int cached_key = -1, cached_rows = 0, cached_rows8 = 0;
   const int key = S * 4096 + WI * 8 + shift;
   if (key != cached_key) {
@@ -1011,7 +1083,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
     cached_rows8 = max_slab_rows(S, WI, shift, k8BM);
     cached_key = key;
   }
-  if ((g_tap_mode == 2 || g_tap_mode == 3) && cached_rows8 <= k8SlabRows) {
+  if ((g_tap_mode == 2 || g_tap_mode == 3) && w192 && cached_rows8 <= k8SlabRows) {
     if (red) rag_launch_wgrad_slab_reduce(*red, stream);
     const int nblk_m = (M + k8BM - 1) / k8BM;
     dim3 grid(nblk_m * (COUTP / kBN));
@@ -1029,6 +1101,26 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
     const char* e = getenv("RAG_PP_MIN_BLOCKS");
     return e ? atoi(e) : 200;  // B = 256 at 19x19 is 241 blocks: stays on the ping-pong kernel
   }();
+  if (w128) {
+    const int nconv = ((M + kPPBM - 1) / kPPBM) * (COUTP / 128);
+    if (g_tap_mode < 5 || g_tap_mode > 9 || cached_rows8 > kPPSlabRows || nconv < pp_min)
+      return false;  // small batches: conv_pipe
+    int nred = 0;
+    WgradRed r{};
+    if (red) {
+      r = *red;
+      nred = std::max(8, (256 - nconv % 256) % 256);
+    }
+    if (bnc)
+      conv_tap_pp_kernel<3, 0, 0, 4, true><<<nconv + nred, 512, 0, stream>>>(
+          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
+          nconv, r, bnc, mcoef);
+    else
+      conv_tap_pp_kernel<3, 0, 0, 4><<<nconv + nred, 512, 0, stream>>>(
+          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
+          nconv, r, nullptr, mcoef);
+    return true;
+  }
   const bool pp_fills = ((M + kPPBM - 1) / kPPBM) * (COUTP / kBN) >= pp_min;
   if ((g_tap_mode >= 5 && g_tap_mode <= 9) && cached_rows8 <= kPPSlabRows && pp_fills) {
     // ping-pong kernel: one block per CU; reduce blocks fill the CUs its last round leaves free
@@ -1087,4 +1179,17 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
                                                     nconv, r, g_ep_lds_override >= 0
                                                                   ? g_ep_lds_override : ep_lds);
   return true;
+}
+
+bool rag_conv_tap_bn_ok(int M, int S, int WI, int shift, int CIN, int COUTP, int KS) {
+  if (g_tap_mode < 0) {
+    const char* e = getenv("RAG_CONV_TAP");
+    g_tap_mode = e ? atoi(e) : 6;
+  }
+  const char* e = getenv("RAG_PP_MIN_BLOCKS");
+  const int pp_min = e ? atoi(e) : 200;
+  const int nconv = ((M + kPPBM - 1) / kPPBM) * (COUTP / 128);
+  return g_tap_mode >= 5 && g_tap_mode <= 9 && KS == 3 && COUTP % kBN != 0 && COUTP % 128 == 0 &&
+         CIN % kBK == 0 && CIN >= kBK && nconv >= pp_min &&
+         max_slab_rows(S, WI, shift, kPPBM) <= kPPSlabRows;
 }

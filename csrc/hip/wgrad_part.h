@@ -13,10 +13,10 @@
 
 namespace rag {
 
-constexpr int kWsN = 192;                   // output channels (all of them per block)
+// A block owns all N output channels (N = 192: 12 waves, N = 128: 8 waves, one wave per 16 of
+// them) x one 32-channel c-tile x 9 taps.
 constexpr int kWsC = 32;                    // input channels per block (c-tile)
-constexpr int kWsWaves = 12;                // waves per wgrad_slab block
-constexpr int kWsBlk = 9 * kWsN * kWsC;     // accumulators per block
+__host__ __device__ constexpr int ws_blk(int n) { return 9 * n * kWsC; }  // accumulators / block
 
 // Everything a chunk reduction needs (passed by value into kernels).
 typedef _Float16 f16;
@@ -24,12 +24,13 @@ typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
 struct WgradRed {
-  const f16* part;     // [nchunks][ntc * kWsBlk] scaled fp16 partials
+  const f16* part;     // [nchunks][ntc * blk] scaled fp16 partials
   const float* scale;  // [nchunks * ntc] inverse block scales
-  const float* bpart;  // [nchunks][kWsN] fp32 bias partials (or null)
+  const float* bpart;  // [nchunks][n] fp32 bias partials (or null)
   float* dW;           // OIHW [COUT][CIN][3][3]
   float* db;           // [COUT] (or null)
   int nchunks, ntc, COUT, CIN, accumulate, map;
+  int n, waves, blk;   // block channels (192 | 128), waves (n / 16), ws_blk(n)
 };
 
 __device__ __forceinline__ void wslab_add8(float (&s)[8], const uint4& v, float sc) {
@@ -45,22 +46,22 @@ __device__ __forceinline__ void wslab_add8(float (&s)[8], const uint4& v, float 
 // Scatter the chunk sum of oct q to OIHW dW.
 __device__ __forceinline__ void wslab_store_oct(const WgradRed& r, int q, const float (&s)[8]) {
   const int e = q * 8;
-  const int ctile = e / kWsBlk;
-  const int loc = e - ctile * kWsBlk;
+  const int ctile = e / r.blk;
+  const int loc = e - ctile * r.blk;
   const int lane0 = (loc >> 2) & 63;
-  const int wv = (loc >> 8) % kWsWaves;
-  const int slot = (loc >> 8) / kWsWaves;  // i * NA + a
+  const int wv = (loc >> 8) % r.waves;
+  const int slot = (loc >> 8) / r.waves;  // i * NA + a
   int nb, cb, t;
   if (r.map) {
     const int a = slot % 6, i = slot / 6;
     t = (wv >> 2) * 3 + i;
     nb = ((wv & 1) * 6 + a) * 16;
     cb = ctile * kWsC + ((wv >> 1) & 1) * 16;
-  } else {
-    const int a = slot & 1;
+  } else {  // map 0: wave wv owns n-frags 2 (wv % g), +1 and c-frag wv / g, g = n / 32
+    const int a = slot & 1, g = r.n >> 5;
     t = slot >> 1;
-    nb = ((wv % 6) * 2 + a) * 16;
-    cb = ctile * kWsC + (wv / 6) * 16;
+    nb = ((wv % g) * 2 + a) * 16;
+    cb = ctile * kWsC + (wv / g) * 16;
   }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -82,15 +83,15 @@ __device__ __forceinline__ void wslab_store_oct(const WgradRed& r, int q, const 
 template <int U>
 __device__ __forceinline__ void wslab_reduce_blocks(const WgradRed& r, int b, int nb) {
   const int T = blockDim.x, tid = threadIdx.x;
-  const int octs = r.ntc * kWsBlk / 8;
-  const size_t st = (size_t)r.ntc * kWsBlk / 8;  // uint4 stride between chunks
+  const int octs = r.ntc * r.blk / 8;
+  const size_t st = (size_t)r.ntc * r.blk / 8;  // uint4 stride between chunks
   const uint4* base = reinterpret_cast<const uint4*>(r.part);
   for (int q = b * T + tid; q < octs; q += nb * T) {
     float s[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) s[j] = 0.f;
     const uint4* p = base + q;
-    const float* sc = r.scale + (q * 8) / kWsBlk;  // + chunk * ntc
+    const float* sc = r.scale + (q * 8) / r.blk;  // + chunk * ntc
     int k = 0;
     for (; k + U <= r.nchunks; k += U) {
       uint4 a[U];
@@ -105,7 +106,7 @@ __device__ __forceinline__ void wslab_reduce_blocks(const WgradRed& r, int b, in
   if (b == 0 && r.db && r.bpart) {
     for (int n = tid; n < r.COUT; n += T) {
       float v = 0.f;
-      for (int k = 0; k < r.nchunks; ++k) v += r.bpart[(size_t)k * kWsN + n];
+      for (int k = 0; k < r.nchunks; ++k) v += r.bpart[(size_t)k * r.n + n];
       r.db[n] = r.accumulate ? r.db[n] + v : v;
     }
   }

@@ -39,18 +39,30 @@ using namespace rag;
 namespace {
 
 constexpr int kRows = 64;                       // padded rows per stage (two MFMA k-steps)
-constexpr int kN = 192;                         // output channels (all of them)
+constexpr int kN = 192;                         // output channels (all of them) of the default
 constexpr int kC = 32;                          // input channels per block
-constexpr int kGChunks = kN / 8;                // 16-byte chunks per G row
 constexpr int kXRows = 112;                     // X slab rows (7 glds x 16 rows)
 constexpr int kXWaves = kXRows / 16;            // waves that stage X
-constexpr int kGElems = kRows * kN;
-constexpr int kStage = kGElems + kXRows * kC;
-constexpr int kWaves = 12;
-static_assert(kRows * kGChunks == kWaves * 2 * 64, "two G glds per wave");
+
+// Per-width layout: a block owns all N (192 | 128) output channels with N / 16 waves.
+template <int N>
+struct WS {
+  static constexpr int GChunks = N / 8;         // 16-byte chunks per G row
+  static constexpr int GElems = kRows * N;
+  static constexpr int Stage = GElems + kXRows * kC;
+  static constexpr int Waves = N / 16;
+  static constexpr int Blk = 9 * N * kC;        // accumulators per block (fp16 partial slab)
+  static_assert(kRows * GChunks == Waves * 2 * 64, "two G glds per wave");
+  static_assert(Waves >= kXWaves, "seven waves stage the X slab");
+  // G rows of 384 B (N = 192) are 32 words mod 64 banks: XOR the 32-byte unit with row bits 1..2;
+  // rows of 256 B (N = 128) all start at bank 0: XOR it with row bits 0..2. Either way the 8 rows
+  // of a transposed-read half hit 8 distinct 8-word bank windows.
+  __device__ static int swz_g(int row) {
+    return N == 192 ? ((row >> 1) & 3) << 1 : (row & 7) << 1;
+  }
+};
 
 __device__ __forceinline__ int swz_x(int row) { return ((row >> 2) & 1) << 1; }
-__device__ __forceinline__ int swz_g(int row) { return ((row >> 1) & 3) << 1; }
 __device__ __forceinline__ int krow(int g, int q) { return (g & 1) * 4 + q + (g >> 1) * 8; }
 
 // vmcnt(N) with N = `young` stages of this wave's loads (PER glds each) left in flight
@@ -68,31 +80,49 @@ __device__ __forceinline__ void wait_young(int young) {
 // in the one __shared__ array: a second __shared__ object made hipcc drain every in-flight
 // global_load_lds (s_waitcnt vmcnt(0)) before the first ds_read of each stage (guide §5,
 // "Projection GEMM" item 4(a); seen in this kernel's .s).
-constexpr int kBlkElems = 9 * kN * kC;  // accumulators per block (fp16 partial slab)
+constexpr int kBlkElems = 9 * kN * kC;  // accumulators per block at the default width
 
 // inverse block scales follow the fp16 partials of all nblk blocks in the workspace
-__host__ __device__ inline float* part_scale(float* part, int nblk) {
+__host__ __device__ inline float* part_scale(float* part, int nblk, int blk = kBlkElems) {
   return reinterpret_cast<float*>(reinterpret_cast<char*>(part) +
-                                  (size_t)nblk * kBlkElems * sizeof(_Float16));
+                                  (size_t)nblk * blk * sizeof(_Float16));
 }
 
 // Wave -> tile map (kMAP): the block's 12 n-frags x 2 c-frags x 9 taps = 216 MFMA tiles, 18 per
 // wave. kMAP 0: 2 n-frags x 1 c-frag x 9 taps per wave (11 transposed fragment reads per k-step);
 // kMAP 1: 6 n-frags x 1 c-frag x 3 taps (one kernel row; 9 reads per k-step, -18 % LDS reads).
-template <int kMAP> struct WMap {
+template <int kMAP, int N = kN> struct WMap {
+  static_assert(kMAP == 0 || N == 192, "map 1 is the 192-channel layout");
   static constexpr int NA = kMAP ? 6 : 2;  // n-frags per wave
   static constexpr int NT = kMAP ? 3 : 9;  // taps per wave
-  __device__ static int nf0(int w) { return kMAP ? (w & 1) * 6 : (w % 6) * 2; }
-  __device__ static int cf(int w) { return kMAP ? (w >> 1) & 1 : w / 6; }
+  static constexpr int G = N / 32;         // map 0: wave groups along n
+  __device__ static int nf0(int w) { return kMAP ? (w & 1) * 6 : (w % G) * 2; }
+  __device__ static int cf(int w) { return kMAP ? (w >> 1) & 1 : w / G; }
   __device__ static int tap(int w, int i) { return kMAP ? (w >> 2) * 3 + i : i; }
 };
 
-template <int kNBUF, bool kBF, int kMAP>
-__global__ void __launch_bounds__(768)
+// BNX (ResnetPolicy BN prologue, K13): X is the BN input x and the layer input is
+// U = ReLU(xcoef[0][col] * x + xcoef[2][col]) (zero on halo rows). Each X-staging wave turns its
+// own 16-byte chunk of every staged X slab into U in place, software-pipelined over a 4-stage ring
+// so that no LDS latency sits in front of a barrier: at the end of step s it waits for stage s+2's
+// loads (stage s+3 stays in flight) and issues the ds_read of its chunk; in step s+1, once the
+// first k-step's fragment reads have drained (that wait covers the chunk too), it applies the BN +
+// ReLU and ds_writes it back -- the slot is next read in step s+2. U is never stored in HBM.
+// (Transforming stage s+1 right before barrier s+1 cost +14 %; loading the chunk to registers
+// instead of LDS-DMA made the compiler drain all loads: +60 %.)
+template <int kNBUF, bool kBF, int kMAP, int N = kN, bool BNX = false>
+__global__ void __launch_bounds__(64 * WS<N>::Waves)
 wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
                   float* __restrict__ part, float* __restrict__ bpart, int R, int WP, int GC,
-                  int CIN, int spc, int CINP) {
-  __shared__ __attribute__((aligned(16))) bf16 lds[kNBUF * kStage];
+                  int CIN, int spc, int CINP, const float* __restrict__ xcoef = nullptr,
+                  int S = 0) {
+  using L = WS<N>;
+  constexpr int kStage = L::Stage, kGElems = L::GElems, kGChunks = L::GChunks;
+  constexpr int kWaves = L::Waves, kBlk = L::Blk, kThreads = 64 * kWaves;
+  static_assert(!BNX || kNBUF == 4, "the BN prologue pipeline assumes a 4-stage ring");
+  // BNX: a [2][64] float table of the column coefficients follows the staging ring (one
+  // __shared__ object: see above)
+  __shared__ __attribute__((aligned(16))) bf16 lds[kNBUF * kStage + (BNX ? 256 : 0)];
   static_assert(kNBUF * kStage * 2 >= kWaves * 64 * 4, "bias scratch fits the staging array");
 
   const int lane = lane_id();
@@ -119,12 +149,20 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
     const int row = slot / kGChunks;
     const int pc = slot - row * kGChunks;
     grow[k] = row;
-    gcol[k] = (pc ^ swz_g(row)) * 8;
+    gcol[k] = (pc ^ L::swz_g(row)) * 8;
   }
   const int xrow = w * 16 + (lane >> 2);
   const int xcol = c0 + (((lane & 3) ^ swz_x(xrow)) * 8);
   const bool xw = w < kXWaves;
 
+  float* tab = reinterpret_cast<float*>(lds + kNBUF * kStage);
+  if constexpr (BNX) {
+    if (tid < S) {
+      tab[tid] = xcoef[tid];
+      tab[64 + tid] = xcoef[2 * S + tid];
+    }
+    __syncthreads();
+  }
   auto stage = [&](int s, int buf) {
     const int r0 = (sbeg + s) * kRows;
     bf16* lg = lds + buf * kStage;
@@ -140,17 +178,44 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
       glds16(X + (size_t)r * CIN + xcol, lg + kGElems + w * 512);
     }
   };
+  // BNX: this lane's chunk of stage s's X slab (landed): xfetch issues the LDS reads (chunk and
+  // column coefficients), xstore applies U = ReLU(cx x + cc) and writes it back in place
+  const int WP2 = WP * WP;
+  bf16x8 xv;
+  float xcx = 0.f, xcc = 0.f;
+  auto xslot = [&](int s) {
+    return reinterpret_cast<bf16x8*>(lds + (s % kNBUF) * kStage + kGElems + w * 512 + lane * 8);
+  };
+  auto xfetch = [&](int s) {
+    const int r = (sbeg + s) * kRows + xshift + xrow;
+    xcx = 0.f;
+    xcc = 0.f;
+    if (r >= 0 && r < R) {
+      const int rem = r % WP2, ii = rem / WP, jj = rem - (rem / WP) * WP;
+      if (ii >= 1 && ii <= S && jj >= 1 && jj <= S) {
+        xcx = tab[jj - 1];
+        xcc = tab[64 + jj - 1];
+      }
+    }
+    xv = *xslot(s);
+  };
+  auto xstore = [&](int s) {
+    bf16x8 v = xv;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (bf16)fmaxf(fmaf(xcx, (float)v[e], xcc), 0.f);
+    *xslot(s) = v;
+  };
 
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
   const int kr = krow(g, q);
-  using M = WMap<kMAP>;
+  using M = WMap<kMAP, N>;
   constexpr int NA = M::NA, NT = M::NT;
   const int nf0 = M::nf0(w);  // this wave's NA 16-channel n fragments
   const int cf = M::cf(w);    // its 16-channel c fragment
   int goff[NA];
 #pragma unroll
   for (int a = 0; a < NA; ++a)
-    goff[a] = kr * kN + ((((nf0 + a) * 2 + (p >> 1)) ^ swz_g(kr)) * 8) + 4 * (p & 1);
+    goff[a] = kr * N + ((((nf0 + a) * 2 + (p >> 1)) ^ L::swz_g(kr)) * 8) + 4 * (p & 1);
   int xoff[NT];
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
@@ -165,13 +230,24 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
 #pragma unroll
     for (int a = 0; a < NA; ++a) acc[i][a] = f32x4{0.f, 0.f, 0.f, 0.f};
   const bool do_bias = bpart != nullptr;
-  const int bcol = ctile * 32 + (tid & 31);  // bias columns: this c-tile's 32 of the 192
-  const int brow = tid >> 5;                 // rows brow, brow + 24, brow + 48
+  const int bcol = ctile * 32 + (tid & 31);  // bias columns: this c-tile's 32 of the N
+  const int brow = tid >> 5;                 // rows brow, brow + kThreads / 32, ...
   float bsum = 0.f;
 
 #pragma unroll
   for (int k = 0; k < kNBUF - 1; ++k)
     if (k < nsteps) stage(k, k);
+  if constexpr (BNX) {
+    if (xw && nsteps > 0) {  // stage 0 before the first barrier, stage 1's chunk fetched
+      wait_young<3>(nsteps - 1 < 2 ? nsteps - 1 : 2);
+      xfetch(0);
+      xstore(0);
+      if (nsteps > 1) {
+        wait_young<3>(nsteps - 2 < 1 ? nsteps - 2 : 1);
+        xfetch(1);
+      }
+    }
+  }
   for (int s = 0; s < nsteps; ++s) {
     // retire stage s; up to kNBUF-2 younger stages (2 or 3 glds of this wave each) stay in flight
     int young = nsteps - 1 - s;
@@ -190,11 +266,14 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
       bf16x8 fa[NA], fb[NT];
 #pragma unroll
       for (int a = 0; a < NA; ++a)
-        fa[a] = tr_frag(lb + goff[a] + ro * kN, lb + goff[a] + (ro + 16) * kN);
+        fa[a] = tr_frag(lb + goff[a] + ro * N, lb + goff[a] + (ro + 16) * N);
 #pragma unroll
       for (int i = 0; i < NT; ++i)
         fb[i] = tr_frag(lb + xoff[i] + ro * kC, lb + xoff[i] + (ro + 16) * kC);
       lds_reads_done();
+      if constexpr (BNX) {
+        if (kk == 0 && xw && s + 1 < nsteps) xstore(s + 1);  // fetched at the end of step s-1
+      }
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < NT; ++i)
@@ -202,9 +281,16 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
         for (int a = 0; a < NA; ++a) acc[i][a] = mfma16(fa[a], fb[i], acc[i][a]);
       __builtin_amdgcn_s_setprio(0);
     }
-    if (do_bias && bcol < kN) {
-      for (int r = brow; r < kRows; r += 24)
-        bsum += (float)lb[r * kN + (((bcol >> 3) ^ swz_g(r)) << 3) + (bcol & 7)];
+    if constexpr (BNX) {
+      // stage s+2 landed (s+3 stays in flight): fetch this lane's chunk for step s+1's xstore
+      if (xw && s + 2 < nsteps) {
+        wait_young<3>(s + 3 < nsteps ? 1 : 0);
+        xfetch(s + 2);
+      }
+    }
+    if (do_bias && bcol < N) {
+      for (int r = brow; r < kRows; r += kThreads / 32)
+        bsum += (float)lb[r * N + (((bcol >> 3) ^ L::swz_g(r)) << 3) + (bcol & 7)];
     }
   }
 
@@ -230,8 +316,8 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
     // float range (inf * value, NaN * 0); below 2^-100 its fp16 values are 0 anyway
     const int e = mx > 0.f ? max(ilogbf(mx), -100) : 0;
     const float up = ldexpf(1.f, 14 - e);
-    if (tid == 0) part_scale(part, gridDim.x)[wid] = ldexpf(1.f, e - 14);
-    f16* dst = reinterpret_cast<f16*>(part) + (size_t)wid * kBlkElems + (w * 64 + lane) * 4;
+    if (tid == 0) part_scale(part, gridDim.x, kBlk)[wid] = ldexpf(1.f, e - 14);
+    f16* dst = reinterpret_cast<f16*>(part) + (size_t)wid * kBlk + (w * 64 + lane) * 4;
 #pragma unroll
     for (int i = 0; i < NT; ++i)
 #pragma unroll
@@ -245,7 +331,7 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
   // partial slab part[chunk][tap][n][c]; C layout: col = lane&15, row = 4*(lane>>4) + r
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
-    float* dst = part + ((size_t)(chunk * 9 + M::tap(w, i)) * kN) * CINP;
+    float* dst = part + ((size_t)(chunk * 9 + M::tap(w, i)) * N) * CINP;
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
       const int n = (nf0 + a) * 16 + g * 4;
@@ -260,10 +346,10 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
     __syncthreads();  // every wave is done reading the staging ring
     bred[tid] = bsum;
     __syncthreads();
-    if (tid < 32 && bcol < kN) {
+    if (tid < 32 && bcol < N) {
       float v = 0.f;
-      for (int k = 0; k < 24; ++k) v += bred[k * 32 + tid];
-      bpart[(size_t)chunk * kN + bcol] = v;
+      for (int k = 0; k < kThreads / 32; ++k) v += bred[k * 32 + tid];
+      bpart[(size_t)chunk * N + bcol] = v;
     }
   }
 }
@@ -274,13 +360,12 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
 // (wave s sums chunks s, s+4, ...: a 16-byte load per chunk, U in flight) and combine through
 // LDS. 4x the threads of one-thread-per-oct, so the ~28 MB of partials stream at HBM rate.
 constexpr int kRedSplit = 4;
-static_assert(kBlkElems == kWsBlk && kWaves == kWsWaves && kN == kWsN && kC == kWsC,
-              "wgrad_part.h layout constants");
+static_assert(kBlkElems == ws_blk(kN) && kC == kWsC, "wgrad_part.h layout constants");
 template <int U>
 __global__ void __launch_bounds__(256)
 wgrad_slab_reduce_kernel(WgradRed red) {
   __shared__ float part_sums[kRedSplit - 1][64][9];  // 9: odd stride, conflict-free
-  const size_t slab = (size_t)red.ntc * kBlkElems;  // elements per chunk
+  const size_t slab = (size_t)red.ntc * red.blk;  // elements per chunk
   const int octs = (int)(slab / 8);
   const int oblocks = (octs + 63) / 64;
   const int tid = threadIdx.x;
@@ -288,7 +373,7 @@ wgrad_slab_reduce_kernel(WgradRed red) {
     const int n = ((int)blockIdx.x - oblocks) * 256 + tid;
     if (!red.db || !red.bpart || n >= red.COUT) return;
     float v = 0.f;
-    for (int k = 0; k < red.nchunks; ++k) v += red.bpart[(size_t)k * kN + n];
+    for (int k = 0; k < red.nchunks; ++k) v += red.bpart[(size_t)k * red.n + n];
     red.db[n] = red.accumulate ? red.db[n] + v : v;
     return;
   }
@@ -297,7 +382,7 @@ wgrad_slab_reduce_kernel(WgradRed red) {
   const bool live = q < octs;
   q = live ? q : octs - 1;
   const uint4* p = reinterpret_cast<const uint4*>(red.part) + q;
-  const float* sc = red.scale + (q * 8) / kBlkElems;  // + chunk * ntc
+  const float* sc = red.scale + (q * 8) / red.blk;  // + chunk * ntc
   const size_t st = slab / 8;
   float s[8];
 #pragma unroll
@@ -335,8 +420,8 @@ bool rag_wgrad_slab_ok(int S, int H, int HG, int GC, int COUTP, int CINP, int KS
     return !(e && e[0] == '0');
   }();
   const int WP = S + 2 * H;
-  return on && KS == 3 && H == 1 && HG == 1 && COUTP == kN && CINP == kN && GC % 8 == 0 &&
-         GC >= kN && kRows + 2 * WP + 2 <= kXRows;
+  return on && KS == 3 && H == 1 && HG == 1 && (COUTP == 192 || COUTP == 128) &&
+         CINP == COUTP && GC % 8 == 0 && GC >= COUTP && kRows + 2 * WP + 2 <= kXRows;
 }
 
 // Chunks of 64-row stages: one resident block per CU (256) over all c-tiles.
@@ -386,7 +471,6 @@ WgradRed rag_wgrad_slab_red(const void* part, const float* bpart, float* dW, flo
                             int nchunks, int CINP, int COUT, int CIN, int accumulate) {
   WgradRed r;
   r.part = (const f16*)part;
-  r.scale = part_scale((float*)part, nchunks * (CINP / kC));
   r.bpart = bpart;
   r.dW = dW;
   r.db = db;
@@ -395,13 +479,17 @@ WgradRed rag_wgrad_slab_red(const void* part, const float* bpart, float* dW, flo
   r.COUT = COUT;
   r.CIN = CIN;
   r.accumulate = accumulate;
-  r.map = wslab_map();
+  r.n = CINP;  // square: the block's c-tiles also split the N bias columns
+  r.waves = CINP / 16;
+  r.blk = ws_blk(CINP);
+  r.scale = part_scale((float*)part, nchunks * (CINP / kC), r.blk);
+  r.map = CINP == kN ? wslab_map() : 0;
   return r;
 }
 
 int rag_launch_wgrad_slab_reduce(const WgradRed& r, hipStream_t stream) {
-  const int octs = (int)((size_t)r.ntc * kBlkElems / 8);
-  const int blocks = (octs + 63) / 64 + (kN + 255) / 256;
+  const int octs = (int)((size_t)r.ntc * r.blk / 8);
+  const int blocks = (octs + 63) / 64 + (r.n + 255) / 256;
   wgrad_slab_reduce_kernel<4><<<blocks, 256, 0, stream>>>(r);
   return (int)hipGetLastError();
 }
@@ -413,18 +501,35 @@ RAG_API int rag_wgrad_slab_nbuf(int n) {
 }
 
 int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpart, int R, int WP,
-                          int GC, int CIN, int spc, int CINP, int nchunks, hipStream_t stream) {
+                          int GC, int CIN, int spc, int CINP, int nchunks, hipStream_t stream,
+                          const float* xcoef, int S) {
   if (g_wslab_nbuf < 0) {
     const char* e = getenv("RAG_WGRAD_NBUF");
     g_wslab_nbuf = e ? atoi(e) : 3;
   }
   const dim3 grid(nchunks * (CINP / kC));
+  const bool bf = rag_wgrad_slab_bf16();
+  if (xcoef) {  // BN prologue: 128 channels, fp16 partials
+    if (CINP != 128 || !bf || S > 64) return -5;
+    wgrad_slab_kernel<4, true, 0, 128, true><<<grid, 512, 0, stream>>>(G, X, part, bpart, R, WP,
+                                                                       GC, CIN, spc, CINP, xcoef,
+                                                                       S);
+    return (int)hipGetLastError();
+  }
+  if (CINP == 128) {  // 8 waves, map 0
+    if (bf)
+      wgrad_slab_kernel<3, true, 0, 128><<<grid, 512, 0, stream>>>(G, X, part, bpart, R, WP, GC,
+                                                                   CIN, spc, CINP);
+    else
+      wgrad_slab_kernel<3, false, 0, 128><<<grid, 512, 0, stream>>>(G, X, part, bpart, R, WP, GC,
+                                                                    CIN, spc, CINP);
+    return (int)hipGetLastError();
+  }
 #define RAG_WSLAB2(NB, BF, MP)                                                                 \
-  wgrad_slab_kernel<NB, BF, MP><<<grid, 64 * kWaves, 0, stream>>>(G, X, part, bpart, R, WP, GC, \
-                                                                  CIN, spc, CINP)
+  wgrad_slab_kernel<NB, BF, MP><<<grid, 64 * WS<kN>::Waves, 0, stream>>>(G, X, part, bpart, R, \
+                                                                        WP, GC, CIN, spc, CINP)
 #define RAG_WSLAB(NB, BF) \
   if (mp) RAG_WSLAB2(NB, BF, 1); else RAG_WSLAB2(NB, BF, 0)
-  const bool bf = rag_wgrad_slab_bf16();
   const int mp = wslab_map();
   switch (g_wslab_nbuf) {
     case 4:

@@ -240,10 +240,13 @@ class ResTrunk(_PackedConvs):
         unit u: X = A_u; n_skip x [U = ReLU(BN(X)); X = conv(U)]; A_{u+1} = A_u + X
         H = ReLU(A_U)                                        (read by the policy head)
 
-    Forward: the column BN statistics (bn.hip) + one fused BN+ReLU pass per BN, the MFMA conv
-    with the residual sum in its epilogue (conv.hip ``res``). Backward, per conv: all-taps wgrad,
-    dgrad with the ReLU mask of its input U in the epilogue, then the BN backward (reduction +
-    one elementwise pass that also adds the skip gradient, in place when the halos agree).
+    Forward: the column BN statistics (bn.hip, one launch), then BN+ReLU fused into the next
+    conv's prologue (the ping-pong kernel stages the BN input x and turns it into U while
+    staging; ``_prologue_ok``) or, for shapes without that kernel (5x5, small batches), one BN+ReLU
+    pass; the MFMA conv adds the residual in its epilogue (conv.hip ``res``). Backward, per conv:
+    wgrad (fused layers rebuild U from x while staging), dgrad with the ReLU mask of U in the
+    epilogue (fused: recomputed from x), then the BN backward (reduction + one elementwise pass
+    that also adds the skip gradient, in place when the halos agree).
 
     Halos: A_u / X / H use halo 1. U_j (conv l = j+1's input) and every gradient consumed by
     conv l use halo hin[l] = max(1, ks_l // 2), so wgrad always runs the all-taps kernel and the
@@ -272,6 +275,11 @@ class ResTrunk(_PackedConvs):
             ends.append(j)
         self._unit_last = ends
         self._work = None
+        # 3x3 wgrad slab reductions ride along the dgrad launch that follows them (as HipTrunk)
+        self.defer_reduce = os.environ.get("RAG_WGRAD_DEFER", "1") != "0"
+        self._pending = ops.PendingReduction() if device.type == "cuda" else None
+        self.bn_prologue = os.environ.get("RAG_BN_PROLOGUE", "1") != "0"
+        self._fused = []  # per BN: fused into the next conv on the last forward
 
     # ------------------------------------------------------------------ buffers
     def ensure_batch(self, B):
@@ -321,6 +329,16 @@ class ResTrunk(_PackedConvs):
     def _bn_input(self, j, u, B):
         return self.A[u][:B] if self.Xin[j] is None else self.Xin[j][:B]
 
+    def _prologue_ok(self, j, B):
+        """BN j + ReLU fused into conv j+1 (conv prologue): that conv stages the BN
+        input x and applies U = ReLU(cx[col] x + cc[col]) while staging, its wgrad does the same,
+        and its dgrad recomputes the ReLU mask from x; U is never materialised. Needs the
+        128-channel ping-pong / slab kernels (3x3, unpadded width, a grid that fills the chip);
+        other layers keep the bn_apply pass. RAG_BN_PROLOGUE=0 disables it."""
+        sp = self.specs[j + 1]
+        return (self.bn_prologue and sp.ks == 3 and self.hin[j + 1] == 1 and self.K == self.KP
+                and ops.conv_bn_fusable(B, self.S, 1, sp.cinp, sp.coutp, sp.ks))
+
     # ------------------------------------------------------------------ compute
     def forward(self, B, training=False):
         S, K = self.S, self.K
@@ -328,6 +346,7 @@ class ResTrunk(_PackedConvs):
         ops.conv_igemm(self.xin[:B], self._wf[0], self._bias[0], self.A[0][:B], B, S,
                        self.hin[0], 1, s0.cinp, s0.coutp, s0.ks, False)
         j = 0
+        self._fused = [self._prologue_ok(jj, B) for jj in range(len(self.bns))]
         for u, n in enumerate(self.units):
             for i in range(n):
                 bn, x, U = self.bns[j], self._bn_input(j, u, B), self.U[j][:B]
@@ -337,13 +356,17 @@ class ResTrunk(_PackedConvs):
                 else:
                     ops.bn_infer_coef(bn.gamma, bn.beta, bn.rmean, bn.rvar, bn.eps, S,
                                       self.coef[j])
-                ops.bn_apply(x, U, B, S, K, coef=self.coef[j], relu=True)
                 l, sp = j + 1, self.specs[j + 1]
                 last = i == n - 1
                 y = self.A[u + 1][:B] if last else self.Xin[j + 1][:B]
-                ops.conv_igemm(U, self._wf[l], self._bias[l], y, B, S, self.hin[l], 1, sp.cinp,
-                               sp.coutp, sp.ks, False,
-                               residual=self.A[u][:B] if last else None)
+                res = self.A[u][:B] if last else None
+                if self._fused[j]:
+                    ops.conv_igemm_bn(x, self._wf[l], self._bias[l], y, B, S, sp.cinp, sp.coutp,
+                                      False, bn_coef=self.coef[j], residual=res)
+                else:
+                    ops.bn_apply(x, U, B, S, K, coef=self.coef[j], relu=True)
+                    ops.conv_igemm(U, self._wf[l], self._bias[l], y, B, S, self.hin[l], 1,
+                                   sp.cinp, sp.coutp, sp.ks, False, residual=res)
                 j += 1
         ops.bn_apply(self.A[-1][:B], self.H[:B], B, S, K, coef=None, relu=True)
         return self.H[:B]
@@ -367,14 +390,29 @@ class ResTrunk(_PackedConvs):
                 j = jend - n + i
                 l, sp, bn = j + 1, self.specs[j + 1], self.bns[j]
                 U, x = self.U[j][:B], self._bn_input(j, u, B)
-                ops.conv_wgrad(gx, U, dws[l], dbs[l], B, S, self.hin[l], sp.cout, sp.coutp,
-                               sp.cin, sp.cinp, sp.ks, accumulate=accumulate, work=self._work,
-                               hg=self.hin[l])
+                defer = self._pending is not None and self.defer_reduce
+                fused = self._fused[j] if j < len(self._fused) else False
+                dU = self.dU[:B]
+                if fused:  # U never stored: both kernels rebuild it from x and BN j's coefs
+                    ops.conv_wgrad(gx, x, dws[l], dbs[l], B, S, 1, sp.cout, sp.coutp, sp.cin,
+                                   sp.cinp, sp.ks, accumulate=accumulate, work=self._work, hg=1,
+                                   defer=defer, pending=self._pending if defer else None,
+                                   xcoef=self.coef[j])
+                    ops.conv_igemm_bn(gx, self._wb[l], None, dU, B, S, sp.coutp, sp.cinp, False,
+                                      mask=x, mask_coef=self.coef[j],
+                                      pending=self._pending if defer else None)
+                else:
+                    ops.conv_wgrad(gx, U, dws[l], dbs[l], B, S, self.hin[l], sp.cout, sp.coutp,
+                                   sp.cin, sp.cinp, sp.ks, accumulate=accumulate,
+                                   work=self._work, hg=self.hin[l], defer=defer,
+                                   pending=self._pending if defer else None)
+                    # the dgrad runs the pending slab reduction in its free block slots: dW[l]
+                    # is final after it
+                    ops.conv_igemm(gx, self._wb[l], None, dU, B, S, self.hin[l], 1, sp.coutp,
+                                   sp.cinp, sp.ks, False, mask=U, mask_halo=self.hin[l],
+                                   pending=self._pending if defer else None)
                 if on_layer_done is not None:
                     on_layer_done(l)
-                dU = self.dU[:B]
-                ops.conv_igemm(gx, self._wb[l], None, dU, B, S, self.hin[l], 1, sp.coutp,
-                               sp.cinp, sp.ks, False, mask=U, mask_halo=self.hin[l])
                 ops.bn_bwd_coef(x, dU, B, S, K, bn.gamma, self.stats[j], bn.dgamma, bn.dbeta,
                                 self.bcoef)
                 if i > 0:  # gradient of the inner conv output Xin[j] = conv j's gx
@@ -390,6 +428,8 @@ class ResTrunk(_PackedConvs):
         ops.conv_wgrad(cur, self.xin[:B], dws[0], dbs[0], B, S, self.hin[0], s0.cout,
                        s0.coutp, s0.cin, s0.cinp, s0.ks, accumulate=accumulate, work=self._work,
                        hg=self.hin[0])
+        if self._pending is not None:
+            ops.wgrad_flush(self._pending)
         if on_layer_done is not None:
             on_layer_done(0)
 

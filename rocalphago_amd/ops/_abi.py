@@ -13,6 +13,9 @@ SIGNATURES = {
     "rag_conv_wgrad_workspace": [I, I, I, I, I, P],
     "rag_conv_wgrad": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, P],
     "rag_conv_wgrad_deferred": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, P],
+    "rag_conv_igemm_bn": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P, P, P, P],
+    "rag_conv_bn_fusable": [I, I, I, I, I, I],
+    "rag_conv_wgrad_deferred_bn": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, P, P],
     "rag_wgrad_flush": [P, P],
     "rag_wgrad_pending_bytes": [],
     "rag_pack_weights": [P, P, P, I, I, I, I, I, P],

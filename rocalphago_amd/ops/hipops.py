@@ -113,6 +113,33 @@ def conv_igemm(x, wpack, bias, y, B, S, hi, ho, cinp, coutp, ks, relu, mask=None
     return y
 
 
+def conv_bn_fusable(B, S, hi, cinp, coutp, ks):
+    """True if a layer of this shape can take its input as BN input x + column coefficients
+    (conv_igemm_bn / conv_wgrad(xcoef=...)): 3x3, 128 channels, a grid that fills the chip."""
+    return bool(_lib().rag_conv_bn_fusable(B, S, hi, cinp, coutp, ks))
+
+
+def conv_igemm_bn(x, wpack, bias, y, B, S, cinp, coutp, relu, bn_coef=None, mask=None,
+                  mask_coef=None, residual=None, pending=None):
+    """3x3 conv whose input is U = ReLU(bn_coef[0][col] * x + bn_coef[2][col]) computed while
+    staging (x = the BN input, halo 1; U is never stored), and/or the dgrad form whose ReLU mask
+    U > 0 is recomputed from ``mask`` = x and ``mask_coef``. Only shapes with
+    conv_bn_fusable(...) have a kernel. ``residual``: as conv_igemm (forward form only)."""
+    _index_range_ok(x, y, mask, residual)
+    if residual is not None and residual.shape[1:] != y.shape[1:]:
+        raise ValueError("residual layout does not match the output")
+    if mask is not None and (mask.shape[1] != S + 2 or mask.shape[-1] != y.shape[-1]):
+        raise ValueError("mask layout does not match (halo 1, %d channels)" % y.shape[-1])
+    if (mask is None) != (mask_coef is None):
+        raise ValueError("mask and mask_coef go together")
+    _check(_lib().rag_conv_igemm_bn(_ptr(x), _ptr(wpack), _ptr(bias), _ptr(y), _ptr(mask),
+                                    _ptr(residual), B, S, 1, 1, cinp, coutp, y.shape[-1],
+                                    int(relu), 1, _stream(),
+                                    _hptr(pending), _ptr(bn_coef), _ptr(mask_coef)),
+           "conv_igemm_bn")
+    return y
+
+
 # ---- column BatchNorm (bn.hip; ResnetPolicy). Activations use the padded layout above; every
 # per-column vector (gamma, beta, running mean / var, stats [2, S], coef [3, S]) is fp32.
 
@@ -178,7 +205,7 @@ def wgrad_workspace(B, S, coutp, cinp, ks, device):
 
 
 def conv_wgrad(g, x, dw, db, B, S, hi, cout, coutp, cin, cinp, ks, accumulate=False, work=None,
-               hg=None, reduce_stream=None, defer=False, pending=None):
+               hg=None, reduce_stream=None, defer=False, pending=None, xcoef=None):
     """dW (OIHW fp32) and db from dL/dpre g [pad hg] and the layer input x [pad hi].
     ``reduce_stream`` (a torch stream): run the partial-slab reduction there, ordered after the
     wgrad kernel by an event, so it overlaps the following kernels of the current stream; the
@@ -186,12 +213,22 @@ def conv_wgrad(g, x, dw, db, B, S, hi, cout, coutp, cin, cinp, ks, accumulate=Fa
     ``defer``: leave an fp16 partial-slab reduction pending in ``pending`` (a PendingReduction,
     required); the next ``conv_igemm(..., pending=pending)`` on this stream runs it in its free
     block slots (or ``wgrad_flush(pending)`` launches it). ``dw``/``db`` are final only after
-    that."""
+    that. ``xcoef`` (BN prologue, conv_bn_fusable shapes): x is the BN input and the layer input
+    is U = ReLU(xcoef[0][col] * x + xcoef[2][col]), applied while staging."""
     _index_range_ok(g, x)
     if work is None:
         work = wgrad_workspace(B, S, coutp, cinp, ks, g.device)
     if hg is None:
         hg = (g.shape[1] - S) // 2
+    if xcoef is not None:
+        if reduce_stream is not None:
+            raise ValueError("conv_wgrad(xcoef=...) has no reduce-stream form")
+        _check(_lib().rag_conv_wgrad_deferred_bn(_ptr(g), _ptr(x), _ptr(dw), _ptr(db), _ptr(work),
+                                                 B, S, hi, hg, g.shape[-1], cout, coutp, cin,
+                                                 cinp, ks, int(accumulate), _stream(),
+                                                 _hptr(pending) if defer else None, _ptr(xcoef)),
+               "conv_wgrad_bn")
+        return
     if defer and reduce_stream is None:
         if pending is None:
             raise ValueError("conv_wgrad(defer=True) needs a PendingReduction handle")

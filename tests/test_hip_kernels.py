@@ -484,3 +484,41 @@ def test_wgrad_denormal_scale_gradients_stay_finite(ops):
     torch.cuda.synchronize()
     assert torch.isfinite(dw).all() and torch.isfinite(db).all()
     assert rel_err(dw / tiny, ref_dw) < 5e-2
+
+
+@pytest.mark.gpu
+def test_width128_pingpong_conv_and_wgrad_slab(ops):
+    """128-channel 3x3 layers (ResnetPolicy / the reference CNNPolicy default width) at B = 256:
+    the ping-pong tap kernel with 96 x 64 wave tiles (forward with bias + ReLU, residual
+    sum-merge, dgrad with the ReLU mask) and the 8-wave wgrad slab kernel with its reduction
+    deferred into that dgrad, each against fp32 PyTorch on bf16-rounded operands."""
+    dev = torch.device("cuda")
+    torch.manual_seed(11)
+    B, C, S = 256, 128, 19
+    x = F.relu(torch.randn(B, C, S, S, device=dev))
+    w = torch.randn(C, C, 3, 3, device=dev) * 0.05
+    b = torch.randn(C, device=dev) * 0.1
+    r = torch.randn(B, C, S, S, device=dev)
+    g = torch.randn(B, C, S, S, device=dev)
+    xp, gp = ops.pack_nchw(x, 1, C), ops.pack_nchw(g, 1, C)
+    wf, wb = ops.pack_weights(w, C, C, wb=torch.empty(9, C, C, dtype=torch.bfloat16, device=dev))
+    y = ops.alloc_padded(B, S, 1, C, dev)
+    ops.conv_igemm(xp, wf, b, y, B, S, 1, 1, C, C, 3, relu=True)
+    assert rel_err(ops.unpack(y, C, 1), F.relu(F.conv2d(bf(x), bf(w), b, padding=1))) < 2e-2
+    assert y[:, 0].abs().max().item() == 0 and y[:, :, -1].abs().max().item() == 0
+    rp = ops.pack_nchw(r, 1, C)
+    yr = ops.alloc_padded(B, S, 1, C, dev)
+    ops.conv_igemm(xp, wf, None, yr, B, S, 1, 1, C, C, 3, relu=False, residual=rp)
+    assert rel_err(ops.unpack(yr, C, 1), F.conv2d(bf(x), bf(w), padding=1) + bf(r)) < 2e-2
+    # wgrad (deferred) + dgrad with the ReLU mask of the layer input
+    xr, wr = bf(x).requires_grad_(), bf(w).requires_grad_()
+    (F.conv2d(xr, wr, padding=1) * bf(g)).sum().backward()
+    h = ops.PendingReduction()
+    dw, db = torch.zeros(C, C, 3, 3, device=dev), torch.zeros(C, device=dev)
+    ops.conv_wgrad(gp, xp, dw, db, B, S, 1, C, C, C, C, 3, hg=1, defer=True, pending=h)
+    dx = ops.alloc_padded(B, S, 1, C, dev)
+    ops.conv_igemm(gp, wb, None, dx, B, S, 1, 1, C, C, 3, relu=False, mask=xp, pending=h)
+    torch.cuda.synchronize()
+    assert rel_err(ops.unpack(dx, C, 1), xr.grad * (x > 0)) < 2e-2
+    assert rel_err(dw, wr.grad) < 1e-2
+    assert rel_err(db, bf(g).sum((0, 2, 3))) < 1e-2

@@ -238,3 +238,76 @@ def test_resnet_plan_with_pass_logit_matches_generic(ops):
     for gc, gg in zip(net_c._gviews[-2:], net_g._gviews[-2:]):
         gc, gg = gc.detach().reshape(-1), gg.detach().cpu().reshape(-1)
         assert (gc - gg).abs().max().item() < 5e-2 * max(gc.abs().max().item(), 1e-3)
+
+
+def test_bn_prologue_kernels_match_torch(ops):
+    """K13: BN + ReLU fused into the 128-channel conv kernels. The layer input
+    U = ReLU(cx[col] * x + cc[col]) (zero on the halo) is built while staging from the BN input x:
+    forward with the residual epilogue, dgrad with the ReLU mask recomputed from x, and the slab
+    wgrad (reduction deferred into that dgrad) -- each against fp32 PyTorch on the materialised
+    U."""
+    dev = "cuda"
+    torch.manual_seed(7)
+    B, C, S = 256, 128, 19
+    assert ops.conv_bn_fusable(B, S, 1, C, C, 3)
+    x = bfr(torch.randn(B, C, S, S, device=dev) * 1.5)
+    coef = torch.zeros(3, S, device=dev)
+    coef[0] = torch.rand(S, device=dev) + 0.5
+    coef[2] = torch.randn(S, device=dev) * 0.3
+    U = bfr(F.relu(x * coef[0] + coef[2]))  # per column w (last axis)
+    w = torch.randn(C, C, 3, 3, device=dev) * 0.05
+    b = torch.randn(C, device=dev) * 0.1
+    r = bfr(torch.randn(B, C, S, S, device=dev))
+    g = bfr(torch.randn(B, C, S, S, device=dev))
+    xp, rp, gp = ops.pack_nchw(x, 1, C), ops.pack_nchw(r, 1, C), ops.pack_nchw(g, 1, C)
+    wf, wb = ops.pack_weights(w, C, C, wb=torch.empty(9, C, C, dtype=torch.bfloat16, device=dev))
+    y = ops.alloc_padded(B, S, 1, C, dev)
+    ops.conv_igemm_bn(xp, wf, b, y, B, S, C, C, False, bn_coef=coef, residual=rp)
+    ref = F.conv2d(U, bfr(w), b, padding=1) + r
+    assert (ops.unpack(y, C, 1) - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
+    assert y[:, 0].abs().max().item() == 0 and y[:, :, -1].abs().max().item() == 0
+    Ur, wr = U.clone().requires_grad_(), bfr(w).requires_grad_()
+    (F.conv2d(Ur, wr, padding=1) * g).sum().backward()
+    h = ops.PendingReduction()
+    dw, db = torch.zeros(C, C, 3, 3, device=dev), torch.zeros(C, device=dev)
+    ops.conv_wgrad(gp, xp, dw, db, B, S, 1, C, C, C, C, 3, hg=1, defer=True, pending=h,
+                   xcoef=coef)
+    dx = ops.alloc_padded(B, S, 1, C, dev)
+    ops.conv_igemm_bn(gp, wb, None, dx, B, S, C, C, False, mask=xp, mask_coef=coef, pending=h)
+    torch.cuda.synchronize()
+    ref_dx = Ur.grad * (U > 0)
+    err = (ops.unpack(dx, C, 1) - ref_dx).abs().max().item()
+    assert err < 2e-2 * ref_dx.abs().max().item()
+    assert (dw - wr.grad).abs().max().item() < 1e-2 * wr.grad.abs().max().item()
+    assert torch.allclose(db, g.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+
+
+def test_resnet_bn_prologue_train_step_matches_unfused(ops):
+    """A 128-filter ResnetPolicy train step at B = 256 with BN+ReLU fused into the conv
+    prologues gives the same loss and gradients as the bn_apply path (RAG_BN_PROLOGUE=0)."""
+    from rocalphago_amd.models import kerasish as KZ
+    _, fused = _pair(128, 5, 19, {})
+    _, plain = _pair(128, 5, 19, {})
+    plain.model._plan_for().trunk.bn_prologue = False
+    B = 256
+    X = _planes(B, 19, 5)
+    lab = np.random.RandomState(6).randint(0, 361, B)
+    Y = np.zeros((B, 361), np.float32)
+    Y[np.arange(B), lab] = 1
+    for m in (fused.model, plain.model):
+        m.compile(loss="categorical_crossentropy", optimizer=KZ.SGD(lr=0.0))
+    lf, lp = fused.model.train_on_batch(X, Y), plain.model.train_on_batch(X, Y)
+    assert any(fused.model._plan_for().trunk._fused)
+    assert not any(plain.model._plan_for().trunk._fused)
+    assert abs(lf - lp) < 1e-3 * abs(lp)
+    for (lname, wname, shape), gf, gp in zip(fused.model.net.weight_names,
+                                             fused.model.net._gviews, plain.model.net._gviews):
+        if "running" in wname:
+            continue
+        gf, gp = gf.detach().reshape(-1).float(), gp.detach().reshape(-1).float()
+        n = gp.norm().item()
+        if n < 1e-6:
+            continue
+        cos = torch.dot(gf, gp).item() / (n * gf.norm().item() + 1e-12)
+        assert cos > 0.999, (wname, cos)
+        assert abs(gf.norm().item() / n - 1) < 1e-2, (wname, gf.norm().item(), n)
