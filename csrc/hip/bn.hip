@@ -280,6 +280,30 @@ RAG_API int rag_bn_bwd_coef(const void* X, int hx, const void* DY, int hd, int B
   return (int)hipGetLastError();
 }
 
+// Finalize from per-block partials [nblk][2][S] that another kernel produced (the BN-fused conv
+// epilogues, conv_tap.hip `spart`): forward (sum x, sum x^2) -> stats / coef / running averages,
+// backward (sum dy, sum dy (x - mean)) -> dgamma / dbeta / the dL/dx coefficients.
+RAG_API int rag_bn_finalize_fwd(const float* part, int nblk, int B, int S, int C,
+                                const float* gamma, const float* beta, float* rmean, float* rvar,
+                                float eps, float momentum, float* stats, float* coef,
+                                hipStream_t stream) {
+  if (S > 64) return -1;
+  const BNArgs a{(double)B * S * C, eps, momentum, gamma, beta, rmean, rvar, stats, coef,
+                 nullptr, nullptr};
+  bn_finalize_kernel<0><<<S, kT, 0, stream>>>(part, nblk, S, a);
+  return (int)hipGetLastError();
+}
+
+RAG_API int rag_bn_finalize_bwd(const float* part, int nblk, int B, int S, int C,
+                                const float* gamma, const float* stats, float* dgamma,
+                                float* dbeta, float* coef, hipStream_t stream) {
+  if (S > 64) return -1;
+  const BNArgs a{(double)B * S * C, 0.f, 0.f, gamma, nullptr, nullptr, nullptr, (float*)stats,
+                 coef, dgamma, dbeta};
+  bn_finalize_kernel<1><<<S, kT, 0, stream>>>(part, nblk, S, a);
+  return (int)hipGetLastError();
+}
+
 RAG_API int rag_bn_apply(const void* X, int hx, const void* DY, int hd, const void* RES, int hr,
                          void* O, int ho, const float* coef, int relu, int B, int S, int C, int CP,
                          hipStream_t stream) {

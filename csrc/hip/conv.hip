@@ -574,7 +574,8 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
                          const bf16* mk, const bf16* res, int M, int S, int WI, int shift, int WO,
                          int HO, int CIN, int COUTP, int YC, int KS, int relu, int HM,
                          long total_rows, hipStream_t stream, const WgradRed* red,
-                         const float* bnc, const float* mcoef);  // conv_tap.hip
+                         const float* bnc, const float* mcoef, float* spart,
+                         const float* smean);  // conv_tap.hip
 bool rag_conv_tap_bn_ok(int M, int S, int WI, int shift, int CIN, int COUTP, int KS);
 bool rag_wgrad_slab_ok(int S, int H, int HG, int GC, int COUTP, int CINP, int KS);
 
@@ -633,7 +634,8 @@ static int conv_igemm_impl(const void* X, const void* W, const float* bias, void
                            const void* mask, const void* resid, int B, int S, int HI, int HO,
                            int CIN, int COUTP, int YC, int KS, int relu, int HM,
                            hipStream_t stream, void* pending, const float* bnc,
-                           const float* mcoef);
+                           const float* mcoef, float* spart = nullptr,
+                           const float* smean = nullptr);
 
 // `pending`: null, or the caller's deferred-reduction handle (see PendingRed above).
 RAG_API int rag_conv_igemm(const void* X, const void* W, const float* bias, void* Y,
@@ -648,20 +650,28 @@ RAG_API int rag_conv_igemm(const void* X, const void* W, const float* bias, void
 // U = ReLU(bnc[0][col] * x + bnc[2][col]) (forward), and/or the dgrad ReLU mask is recomputed
 // from `mask` = x and mcoef (no residual then). -5 if the shape has no fused kernel
 // (rag_conv_bn_fusable).
+// spart (optional): the output's BN column statistics as per-block partials [nblk][2][S] for
+// rag_bn_finalize (nblk = rag_conv_bn_stat_blocks); smean: the BN mean for the backward form.
 RAG_API int rag_conv_igemm_bn(const void* X, const void* W, const float* bias, void* Y,
                               const void* mask, const void* resid, int B, int S, int HI, int HO,
                               int CIN, int COUTP, int YC, int relu, int HM, hipStream_t stream,
-                              void* pending, const float* bnc, const float* mcoef) {
-  if ((!bnc && !mcoef) || (mcoef && resid)) return -5;
+                              void* pending, const float* bnc, const float* mcoef, float* spart,
+                              const float* smean) {
+  if ((!bnc && !mcoef && !spart) || (mcoef && resid) || (smean && !mcoef)) return -5;
   return conv_igemm_impl(X, W, bias, Y, mask, resid, B, S, HI, HO, CIN, COUTP, YC, 3, relu, HM,
-                         stream, pending, bnc, mcoef);
+                         stream, pending, bnc, mcoef, spart, smean);
+}
+
+// Partial rows rag_conv_igemm_bn writes to `spart` (one per convolution block).
+RAG_API int rag_conv_bn_stat_blocks(int B, int S, int COUTP) {
+  return ((B * S * S + 383) / 384) * (COUTP / 128);
 }
 
 static int conv_igemm_impl(const void* X, const void* W, const float* bias, void* Y,
                            const void* mask, const void* resid, int B, int S, int HI, int HO,
                            int CIN, int COUTP, int YC, int KS, int relu, int HM,
                            hipStream_t stream, void* pending, const float* bnc,
-                           const float* mcoef) {
+                           const float* mcoef, float* spart, const float* smean) {
   if (CIN % 32 || COUTP % 32 || YC < COUTP || HI < KS / 2) return -1;
   const int M = B * S * S;
   const int nt = pick_nt(COUTP);
@@ -687,9 +697,9 @@ static int conv_igemm_impl(const void* X, const void* W, const float* bias, void
       if (rc) return rc;
     }
   }
-  if (bnc || mcoef) {  // BN prologue: the 128-channel ping-pong kernel or nothing
+  if (bnc || mcoef || spart) {  // BN fusion: the 128-channel ping-pong kernel or nothing
     if (rag_conv_tap_launch(x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, KS,
-                            relu, HM, (long)B * WI * WI, stream, red, bnc, mcoef))
+                            relu, HM, (long)B * WI * WI, stream, red, bnc, mcoef, spart, smean))
       return (int)hipGetLastError();
     if (red) rag_launch_wgrad_slab_reduce(*red, stream);
     return -5;
@@ -701,7 +711,7 @@ static int conv_igemm_impl(const void* X, const void* W, const float* bias, void
   }
   if (use_pipe && rag_conv_tap_launch(x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN,
                                       COUTP, YC, KS, relu, HM, (long)B * WI * WI, stream, red,
-                                      nullptr, nullptr))
+                                      nullptr, nullptr, nullptr, nullptr))
     return (int)hipGetLastError();
   if (red) {  // not a tap-slab launch: the reduction goes out on its own first
     const int rc = rag_launch_wgrad_slab_reduce(*red, stream);

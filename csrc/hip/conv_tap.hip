@@ -45,17 +45,71 @@ __device__ __forceinline__ void wait_vm() {
 }
 
 // epilogue (as conv_pipe): lane owns channels n..n+3 of pixel m for every (j, i) tile
+// BN column statistics of a conv output (BN fusion, ResnetPolicy): `sred` is an LDS [2][64] float
+// accumulator of this block (sum, sum of squares per board column of the stored bf16 values).
+// The four lanes of a pixel (fq) are combined by shuffles, then one lane per pixel adds to LDS.
+__device__ __forceinline__ void stats_add_pixel(float* sred, int valid, int col, float s0,
+                                                float s1, int fq) {
+  s0 += __shfl_xor(s0, 16, 64);
+  s1 += __shfl_xor(s1, 16, 64);
+  s0 += __shfl_xor(s0, 32, 64);
+  s1 += __shfl_xor(s1, 32, 64);
+  if (fq == 0 && valid) {
+    atomicAdd(sred + col, s0);
+    atomicAdd(sred + 64 + col, s1);
+  }
+}
+
 template <int NT = kNT>
 __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NT][kMT], int mw, int nw, int M,
                                          int S, int WO, int HO, int YC, int HM,
                                          const float* __restrict__ bias,
                                          const bf16* __restrict__ res, int relu,
                                          const bf16* __restrict__ mask, bf16* __restrict__ Y,
-                                         int frow, int fq) {
+                                         int frow, int fq, float* sred = nullptr) {
   const int S2 = S * S;
 #pragma unroll
   for (int i = 0; i < kMT; ++i) {
     const int m = mw + i * 16 + frow;
+    if (sred) {  // uniform: every lane takes part in the shuffles
+      float s0 = 0.f, s1 = 0.f;
+      int col = 0;
+      if (m < M) {
+        const int rem = m % S2;
+        col = rem % S;
+        const size_t orow = (size_t)(((m / S2) * WO + rem / S + HO) * WO + col + HO) * YC;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const int n = nw + j * 16 + fq * 4;
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = acc[j][i][r];
+          if (bias) {
+            const float4 bb = *reinterpret_cast<const float4*>(bias + n);
+            v[0] += bb.x;
+            v[1] += bb.y;
+            v[2] += bb.z;
+            v[3] += bb.w;
+          }
+          if (res) {
+            const bf16x4 rv = *reinterpret_cast<const bf16x4*>(res + orow + n);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += (float)rv[r];
+          }
+          bf16x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            o[r] = (bf16)(relu ? fmaxf(v[r], 0.f) : v[r]);
+            const float q = (float)o[r];
+            s0 += q;
+            s1 = fmaf(q, q, s1);
+          }
+          *reinterpret_cast<bf16x4*>(Y + orow + n) = o;
+        }
+      }
+      stats_add_pixel(sred, m < M, col, s0, s1, fq);
+      continue;
+    }
     if (m >= M) continue;
     const int b = m / S2;
     const int rem = m - b * S2;
@@ -113,7 +167,9 @@ __device__ __forceinline__ void epilogue_lds(const f32x4 (&acc)[NT][kMT], bf16* 
                                              const float* __restrict__ bias, int relu,
                                              const bf16* __restrict__ mask,
                                              bf16* __restrict__ Y, int frow, int fq,
-                                             const float* __restrict__ mcoef = nullptr) {
+                                             const float* __restrict__ mcoef = nullptr,
+                                             float* sred = nullptr,
+                                             const float* __restrict__ smean = nullptr) {
   constexpr int EpRow = 32 * NT + 8;
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
@@ -133,6 +189,58 @@ __device__ __forceinline__ void epilogue_lds(const f32x4 (&acc)[NT][kMT], bf16* 
   __syncthreads();
   const int S2 = S * S, WMK = S + 2 * HM;
   constexpr int kChunks = 32 * NT / 8;  // 16-byte chunks per pixel row
+  // with statistics (128-channel tiles only): kChunks consecutive threads own one pixel row
+  // (kChunks | 64, and BM * kChunks a multiple of the block size, so every thread runs the same
+  // iterations)
+  if constexpr (64 % kChunks == 0) if (sred) {
+    for (int c = threadIdx.x; c < BM * kChunks; c += blockDim.x) {
+      const int row = c / kChunks, k8 = (c - row * kChunks) * 8;
+      const int m = m0 + row;
+      float s0 = 0.f, s1 = 0.f;
+      int pj = 0;
+      if (m < M) {
+        const int b = m / S2;
+        const int rem = m - b * S2;
+        const int pi = rem / S;
+        pj = rem - pi * S;
+        bf16x8 v = *reinterpret_cast<const bf16x8*>(img + row * EpRow + k8);
+        if (mask) {
+          const bf16x8 mk = *reinterpret_cast<const bf16x8*>(
+              mask + (size_t)((b * WMK + pi + HM) * WMK + pj + HM) * YC + n0 + k8);
+          const float cx = mcoef ? mcoef[pj] : 0.f, cc = mcoef ? mcoef[2 * S + pj] : 0.f;
+          const float mu = smean ? smean[pj] : 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float xm = (float)mk[e];
+            const bool on = mcoef ? fmaf(cx, xm, cc) > 0.f : xm > 0.f;
+            v[e] = on ? v[e] : (bf16)0.f;
+            const float d = (float)v[e];
+            s0 += d;
+            s1 = fmaf(d, xm - mu, s1);  // backward: sum dy * (x - mean)
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float q = (float)v[e];
+            s0 += q;
+            s1 = fmaf(q, q, s1);  // forward: sum x^2
+          }
+        }
+        *reinterpret_cast<bf16x8*>(Y + (size_t)((b * WO + pi + HO) * WO + pj + HO) * YC + n0 +
+                                   k8) = v;
+      }
+#pragma unroll
+      for (int o = kChunks / 2; o > 0; o >>= 1) {
+        s0 += __shfl_xor(s0, o, 64);
+        s1 += __shfl_xor(s1, o, 64);
+      }
+      if ((threadIdx.x & (kChunks - 1)) == 0 && m < M) {
+        atomicAdd(sred + pj, s0);
+        atomicAdd(sred + 64 + pj, s1);
+      }
+    }
+    return;
+  }  // if (sred)
   for (int c = threadIdx.x; c < BM * kChunks; c += blockDim.x) {
     const int row = c / kChunks, k8 = (c - row * kChunks) * 8;
     const int m = m0 + row;
@@ -649,6 +757,10 @@ constexpr int kPPAL = kPPSlabRows / 64;  // slab glds per loader wave (4 loader 
 // staged slab into U = ReLU(cx[col] * x + cc[col]) in place (zero on halo rows) before the barrier
 // that publishes it, with bnc = the BN's [3][S] column coefficients; U is never written to HBM.
 // mcoef: the dgrad form of the same fusion (mask = U > 0 recomputed from x, see epilogue_lds).
+// spart: this block's BN column statistics of the output ([blockIdx][2][S] partials for
+// bn.hip's finalize): (sum, sum of squares) of the stored output in the forward, or with smean
+// (the BN's mean) (sum dU, sum dU * (x - mean)) of the masked dgrad output, x = `mask`. They
+// replace the separate statistics passes over the activation.
 template <int NB, int DIAG = 0, int ISSUE = 0, int NT = kNT, bool BNP = false>
 __global__ void __launch_bounds__(512)
 conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
@@ -656,7 +768,8 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                    const bf16* __restrict__ mask, const bf16* __restrict__ res, int M, int S,
                    int WI, int shift, int WO, int HO, int CIN, int WROWS, int YC, int relu, int HM,
                    long total_rows, int nconv, WgradRed red, const float* __restrict__ bnc = nullptr,
-                   const float* __restrict__ mcoef = nullptr, long long* stamps = nullptr) {
+                   const float* __restrict__ mcoef = nullptr, float* __restrict__ spart = nullptr,
+                   const float* __restrict__ smean = nullptr, long long* stamps = nullptr) {
   constexpr int BN = 32 * NT, BTile = BN * kBK, PPBL = BN / 64, EpRow = BN + 8;
   static_assert(BN % 64 == 0, "the loader waves stage 64-row weight slices");
   constexpr int kLoop = 2 * kPPSlab + NB * BTile;
@@ -664,10 +777,16 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
   // weight tiles staged ahead of the current step (issued in the MFMA segment, the slot's last
   // reader is one phase further back: NB tiles ahead are safe)
   constexpr int D = ISSUE ? NB : NB - 1;
-  __shared__ __attribute__((aligned(16))) bf16 lds[kL];
+  // + a [2][64] float BN-statistics accumulator past the ring / epilogue image
+  __shared__ __attribute__((aligned(16))) bf16 lds[kL + 256];
   if ((int)blockIdx.x >= nconv) {
     wslab_reduce_blocks<kRedU>(red, (int)blockIdx.x - nconv, (int)gridDim.x - nconv);
     return;
+  }
+  float* sred = spart ? reinterpret_cast<float*>(lds + kL) : nullptr;
+  if (spart) {
+    if (threadIdx.x < 128) sred[threadIdx.x] = 0.f;
+    __syncthreads();
   }
   long long r_entry = 0;
   if constexpr (DIAG & 4) r_entry = __builtin_amdgcn_s_memrealtime();
@@ -949,11 +1068,18 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
   }
   if (res) {
     epilogue(acc, m0 + wm * (16 * kMT), n0 + wn * (16 * NT), M, S, WO, HO, YC, HM, bias, res,
-             relu, mask, Y, frow, fq);
+             relu, mask, Y, frow, fq, sred);
   } else {
     __syncthreads();  // every wave is past its last LDS read: the ring becomes the output image
     epilogue_lds<kPPBM, NT>(acc, lds, wm * (16 * kMT), wn * (16 * NT), m0, n0, M, S, WO, HO, YC, HM,
-                        bias, relu, mask, Y, frow, fq, mcoef);
+                        bias, relu, mask, Y, frow, fq, mcoef, sred, smean);
+  }
+  if (spart) {  // the block's column partials
+    __syncthreads();
+    if ((int)threadIdx.x < 2 * S) {
+      const int q = threadIdx.x / S, wc = threadIdx.x - q * S;
+      spart[((size_t)blockIdx.x * 2 + q) * S + wc] = sred[q * 64 + wc];
+    }
   }
   if constexpr (DIAG & 4) {
     // per block: loop cycles, loop ticks, then absolute ticks at entry / loop start / loop end /
@@ -1009,7 +1135,7 @@ RAG_API int rag_conv_pp_diag(int diag, const void* X, const void* W, const float
   conv_tap_pp_kernel<4, D><<<nconv, 512, 0, stream>>>(x, w, bias, y, mk, nullptr, M, S, WI,      \
                                                       shift, WO, HO, CIN, COUTP, YC, relu, HM,  \
                                                       total, nconv, r, nullptr, nullptr, \
-                                                      g_stamps)
+                                                      nullptr, nullptr, g_stamps)
   switch (diag & 11) {
     case 0: RAG_PPD(4); break;
     case 1: RAG_PPD(5); break;
@@ -1065,8 +1191,9 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
                          const bf16* mk, const bf16* res, int M, int S, int WI, int shift, int WO,
                          int HO, int CIN, int COUTP, int YC, int KS, int relu, int HM, long total_rows,
                          hipStream_t stream, const WgradRed* red, const float* bnc,
-                         const float* mcoef) {
-  if ((bnc || mcoef) && ((mcoef && res) || !rag_conv_tap_bn_ok(M, S, WI, shift, CIN, COUTP, KS)))
+                         const float* mcoef, float* spart, const float* smean) {
+  if ((bnc || mcoef || spart) &&
+      ((mcoef && res) || !rag_conv_tap_bn_ok(M, S, WI, shift, CIN, COUTP, KS)))
     return false;
   if (g_tap_mode < 0) {
     const char* e = getenv("RAG_CONV_TAP");
@@ -1114,11 +1241,11 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
     if (bnc)
       conv_tap_pp_kernel<3, 0, 0, 4, true><<<nconv + nred, 512, 0, stream>>>(
           x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
-          nconv, r, bnc, mcoef);
+          nconv, r, bnc, mcoef, spart, smean);
     else
       conv_tap_pp_kernel<3, 0, 0, 4><<<nconv + nred, 512, 0, stream>>>(
           x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
-          nconv, r, nullptr, mcoef);
+          nconv, r, nullptr, mcoef, spart, smean);
     return true;
   }
   const bool pp_fills = ((M + kPPBM - 1) / kPPBM) * (COUTP / kBN) >= pp_min;

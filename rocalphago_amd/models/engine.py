@@ -240,13 +240,15 @@ class ResTrunk(_PackedConvs):
         unit u: X = A_u; n_skip x [U = ReLU(BN(X)); X = conv(U)]; A_{u+1} = A_u + X
         H = ReLU(A_U)                                        (read by the policy head)
 
-    Forward: the column BN statistics (bn.hip, one launch), then BN+ReLU fused into the next
+    Forward: the column BN statistics (summed in the epilogue of the fused conv that produced
+    the BN input, else a bn.hip pass) + a finalize launch, then BN+ReLU fused into the next
     conv's prologue (the ping-pong kernel stages the BN input x and turns it into U while
     staging; ``_prologue_ok``) or, for shapes without that kernel (5x5, small batches), one BN+ReLU
     pass; the MFMA conv adds the residual in its epilogue (conv.hip ``res``). Backward, per conv:
     wgrad (fused layers rebuild U from x while staging), dgrad with the ReLU mask of U in the
-    epilogue (fused: recomputed from x), then the BN backward (reduction + one elementwise pass
-    that also adds the skip gradient, in place when the halos agree).
+    epilogue (fused: recomputed from x, and the BN backward sums taken in the same epilogue),
+    then the BN backward (reduction unless fused + one elementwise pass that also adds the skip
+    gradient, in place when the halos agree).
 
     Halos: A_u / X / H use halo 1. U_j (conv l = j+1's input) and every gradient consumed by
     conv l use halo hin[l] = max(1, ks_l // 2), so wgrad always runs the all-taps kernel and the
@@ -309,6 +311,11 @@ class ResTrunk(_PackedConvs):
         self.stats = torch.zeros((nb, 2, S), dtype=torch.float32, device=dev)
         self.coef = torch.zeros((nb, 3, S), dtype=torch.float32, device=dev)
         self.bcoef = torch.zeros((3, S), dtype=torch.float32, device=dev)
+        # BN column-statistics partials written by the fused conv epilogues (forward: one per
+        # BN, whose input that conv produced; backward: one, reused layer by layer)
+        nblk = ops.conv_bn_stat_blocks(B, S, KP) if KP % 128 == 0 and KP % 192 else 1
+        self.spart = torch.zeros((nb, nblk, 2, S), dtype=torch.float32, device=dev)
+        self.bpart = torch.zeros((nblk, 2, S), dtype=torch.float32, device=dev)
         need = max(ops._lib().rag_conv_wgrad_workspace(B, S, s.coutp, s.cinp, s.ks, None)
                    for s in self.specs)
         self._work = torch.empty(need + 1024, dtype=torch.float32, device=dev)
@@ -346,11 +353,18 @@ class ResTrunk(_PackedConvs):
         ops.conv_igemm(self.xin[:B], self._wf[0], self._bias[0], self.A[0][:B], B, S,
                        self.hin[0], 1, s0.cinp, s0.coutp, s0.ks, False)
         j = 0
-        self._fused = [self._prologue_ok(jj, B) for jj in range(len(self.bns))]
+        nb = len(self.bns)
+        self._fused = [self._prologue_ok(jj, B) for jj in range(nb)]
+        nblk = ops.conv_bn_stat_blocks(B, S, self.KP) if any(self._fused) else 0
+        stat_ready = [False] * nb  # BN j's input statistics came out of the conv producing it
         for u, n in enumerate(self.units):
             for i in range(n):
                 bn, x, U = self.bns[j], self._bn_input(j, u, B), self.U[j][:B]
-                if training:
+                if training and stat_ready[j]:
+                    ops.bn_finalize_fwd(self.spart[j], nblk, B, S, K, bn.gamma, bn.beta,
+                                        bn.rmean, bn.rvar, bn.eps, bn.momentum, self.stats[j],
+                                        self.coef[j])
+                elif training:
                     ops.bn_train_fwd(x, B, S, K, bn.gamma, bn.beta, bn.rmean, bn.rvar, bn.eps,
                                      bn.momentum, self.stats[j], self.coef[j])
                 else:
@@ -361,8 +375,13 @@ class ResTrunk(_PackedConvs):
                 y = self.A[u + 1][:B] if last else self.Xin[j + 1][:B]
                 res = self.A[u][:B] if last else None
                 if self._fused[j]:
+                    # this conv's output is BN l's input: its epilogue also sums BN l's stats
+                    sp_out = self.spart[l] if training and l < nb else None
                     ops.conv_igemm_bn(x, self._wf[l], self._bias[l], y, B, S, sp.cinp, sp.coutp,
-                                      False, bn_coef=self.coef[j], residual=res)
+                                      False, bn_coef=self.coef[j], residual=res,
+                                      stat_part=sp_out)
+                    if sp_out is not None:
+                        stat_ready[l] = True
                 else:
                     ops.bn_apply(x, U, B, S, K, coef=self.coef[j], relu=True)
                     ops.conv_igemm(U, self._wf[l], self._bias[l], y, B, S, self.hin[l], 1,
@@ -398,9 +417,11 @@ class ResTrunk(_PackedConvs):
                                    sp.cinp, sp.ks, accumulate=accumulate, work=self._work, hg=1,
                                    defer=defer, pending=self._pending if defer else None,
                                    xcoef=self.coef[j])
+                    # its epilogue also sums BN j's backward statistics (dU, dU (x - mean))
                     ops.conv_igemm_bn(gx, self._wb[l], None, dU, B, S, sp.coutp, sp.cinp, False,
                                       mask=x, mask_coef=self.coef[j],
-                                      pending=self._pending if defer else None)
+                                      pending=self._pending if defer else None,
+                                      stat_part=self.bpart, stat_mean=self.stats[j])
                 else:
                     ops.conv_wgrad(gx, U, dws[l], dbs[l], B, S, self.hin[l], sp.cout, sp.coutp,
                                    sp.cin, sp.cinp, sp.ks, accumulate=accumulate,
@@ -413,8 +434,13 @@ class ResTrunk(_PackedConvs):
                                    pending=self._pending if defer else None)
                 if on_layer_done is not None:
                     on_layer_done(l)
-                ops.bn_bwd_coef(x, dU, B, S, K, bn.gamma, self.stats[j], bn.dgamma, bn.dbeta,
-                                self.bcoef)
+                if fused:
+                    ops.bn_finalize_bwd(self.bpart, ops.conv_bn_stat_blocks(B, S, self.KP), B, S,
+                                        K, bn.gamma, self.stats[j], bn.dgamma, bn.dbeta,
+                                        self.bcoef)
+                else:
+                    ops.bn_bwd_coef(x, dU, B, S, K, bn.gamma, self.stats[j], bn.dgamma,
+                                    bn.dbeta, self.bcoef)
                 if i > 0:  # gradient of the inner conv output Xin[j] = conv j's gx
                     gx = self.gI[self.hin[j]][:B]
                     ops.bn_apply(x, gx, B, S, K, coef=self.bcoef, relu=False, dy=dU)

@@ -13,7 +13,8 @@ SIGNATURES = {
     "rag_conv_wgrad_workspace": [I, I, I, I, I, P],
     "rag_conv_wgrad": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, P],
     "rag_conv_wgrad_deferred": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, P],
-    "rag_conv_igemm_bn": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P, P, P, P],
+    "rag_conv_igemm_bn": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P, P, P, P, P, P],
+    "rag_conv_bn_stat_blocks": [I, I, I],
     "rag_conv_bn_fusable": [I, I, I, I, I, I],
     "rag_conv_wgrad_deferred_bn": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, P, P],
     "rag_wgrad_flush": [P, P],
@@ -47,6 +48,8 @@ SIGNATURES = {
     "rag_bn_infer_coef": [P, P, P, P, F, I, P, P],
     "rag_bn_bwd_coef": [P, I, P, I, I, I, I, I, P, P, P, P, P, P, P],
     "rag_bn_apply": [P, I, P, I, P, I, P, I, P, I, I, I, I, I, P],
+    "rag_bn_finalize_fwd": [P, I, I, I, I, P, P, P, P, F, F, P, P, P],
+    "rag_bn_finalize_bwd": [P, I, I, I, I, P, P, P, P, P, P],
     # sample.hip
     "rag_sample_moves": [P, P, I, P, I, I, F, C.c_uint64, P, P],
     # features.hip

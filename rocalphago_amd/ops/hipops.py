@@ -119,12 +119,20 @@ def conv_bn_fusable(B, S, hi, cinp, coutp, ks):
     return bool(_lib().rag_conv_bn_fusable(B, S, hi, cinp, coutp, ks))
 
 
+def conv_bn_stat_blocks(B, S, coutp):
+    """Partial rows [n][2][S] a statistics-producing conv_igemm_bn writes (its block count)."""
+    return int(_lib().rag_conv_bn_stat_blocks(B, S, coutp))
+
+
 def conv_igemm_bn(x, wpack, bias, y, B, S, cinp, coutp, relu, bn_coef=None, mask=None,
-                  mask_coef=None, residual=None, pending=None):
+                  mask_coef=None, residual=None, pending=None, stat_part=None, stat_mean=None):
     """3x3 conv whose input is U = ReLU(bn_coef[0][col] * x + bn_coef[2][col]) computed while
     staging (x = the BN input, halo 1; U is never stored), and/or the dgrad form whose ReLU mask
     U > 0 is recomputed from ``mask`` = x and ``mask_coef``. Only shapes with
-    conv_bn_fusable(...) have a kernel. ``residual``: as conv_igemm (forward form only)."""
+    conv_bn_fusable(...) have a kernel. ``residual``: as conv_igemm (forward form only).
+    ``stat_part`` [conv_bn_stat_blocks, 2, S] fp32: the output's BN column statistics as per-block
+    partials for bn_finalize_fwd (sum, sum of squares), or, with ``stat_mean`` (the BN mean) in the
+    dgrad form, for bn_finalize_bwd (sum dU, sum dU (x - mean))."""
     _index_range_ok(x, y, mask, residual)
     if residual is not None and residual.shape[1:] != y.shape[1:]:
         raise ValueError("residual layout does not match the output")
@@ -135,7 +143,8 @@ def conv_igemm_bn(x, wpack, bias, y, B, S, cinp, coutp, relu, bn_coef=None, mask
     _check(_lib().rag_conv_igemm_bn(_ptr(x), _ptr(wpack), _ptr(bias), _ptr(y), _ptr(mask),
                                     _ptr(residual), B, S, 1, 1, cinp, coutp, y.shape[-1],
                                     int(relu), 1, _stream(),
-                                    _hptr(pending), _ptr(bn_coef), _ptr(mask_coef)),
+                                    _hptr(pending), _ptr(bn_coef), _ptr(mask_coef),
+                                    _ptr(stat_part), _ptr(stat_mean)),
            "conv_igemm_bn")
     return y
 
@@ -169,6 +178,22 @@ def bn_train_fwd(x, B, S, C, gamma, beta, rmean, rvar, eps, momentum, stats, coe
 def bn_infer_coef(gamma, beta, rmean, rvar, eps, S, coef):
     _check(_lib().rag_bn_infer_coef(_ptr(gamma), _ptr(beta), _ptr(rmean), _ptr(rvar),
                                     float(eps), S, _ptr(coef), _stream()), "bn_infer_coef")
+
+
+def bn_finalize_fwd(part, nblk, B, S, C, gamma, beta, rmean, rvar, eps, momentum, stats, coef):
+    """bn_train_fwd from per-block partials a fused conv epilogue wrote (conv_igemm_bn
+    ``stat_part``)."""
+    _check(_lib().rag_bn_finalize_fwd(_ptr(part), nblk, B, S, C, _ptr(gamma), _ptr(beta),
+                                      _ptr(rmean), _ptr(rvar), float(eps), float(momentum),
+                                      _ptr(stats), _ptr(coef), _stream()), "bn_finalize_fwd")
+
+
+def bn_finalize_bwd(part, nblk, B, S, C, gamma, stats, dgamma, dbeta, coef):
+    """bn_bwd_coef from per-block partials of a fused dgrad epilogue (conv_igemm_bn
+    ``stat_part`` + ``stat_mean``)."""
+    _check(_lib().rag_bn_finalize_bwd(_ptr(part), nblk, B, S, C, _ptr(gamma), _ptr(stats),
+                                      _ptr(dgamma), _ptr(dbeta), _ptr(coef), _stream()),
+           "bn_finalize_bwd")
 
 
 def bn_bwd_coef(x, dy, B, S, C, gamma, stats, dgamma, dbeta, coef):

@@ -262,9 +262,16 @@ def test_bn_prologue_kernels_match_torch(ops):
     xp, rp, gp = ops.pack_nchw(x, 1, C), ops.pack_nchw(r, 1, C), ops.pack_nchw(g, 1, C)
     wf, wb = ops.pack_weights(w, C, C, wb=torch.empty(9, C, C, dtype=torch.bfloat16, device=dev))
     y = ops.alloc_padded(B, S, 1, C, dev)
-    ops.conv_igemm_bn(xp, wf, b, y, B, S, C, C, False, bn_coef=coef, residual=rp)
+    nblk = ops.conv_bn_stat_blocks(B, S, C)
+    part = torch.full((nblk, 2, S), 7.0, device=dev)
+    ops.conv_igemm_bn(xp, wf, b, y, B, S, C, C, False, bn_coef=coef, residual=rp, stat_part=part)
     ref = F.conv2d(U, bfr(w), b, padding=1) + r
-    assert (ops.unpack(y, C, 1) - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
+    got = ops.unpack(y, C, 1)
+    assert (got - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
+    # the epilogue's column statistics are those of the stored output
+    sums = part.double().sum(0)
+    assert torch.allclose(sums[0], got.double().sum((0, 1, 2)), rtol=1e-4, atol=1e-1)
+    assert torch.allclose(sums[1], (got.double() ** 2).sum((0, 1, 2)), rtol=1e-4, atol=1e-1)
     assert y[:, 0].abs().max().item() == 0 and y[:, :, -1].abs().max().item() == 0
     Ur, wr = U.clone().requires_grad_(), bfr(w).requires_grad_()
     (F.conv2d(Ur, wr, padding=1) * g).sum().backward()
@@ -273,9 +280,16 @@ def test_bn_prologue_kernels_match_torch(ops):
     ops.conv_wgrad(gp, xp, dw, db, B, S, 1, C, C, C, C, 3, hg=1, defer=True, pending=h,
                    xcoef=coef)
     dx = ops.alloc_padded(B, S, 1, C, dev)
-    ops.conv_igemm_bn(gp, wb, None, dx, B, S, C, C, False, mask=xp, mask_coef=coef, pending=h)
+    mean = torch.randn(S, device=dev) * 0.1
+    ops.conv_igemm_bn(gp, wb, None, dx, B, S, C, C, False, mask=xp, mask_coef=coef, pending=h,
+                      stat_part=part, stat_mean=mean)
     torch.cuda.synchronize()
     ref_dx = Ur.grad * (U > 0)
+    d = ops.unpack(dx, C, 1).double()
+    sums = part.double().sum(0)
+    assert torch.allclose(sums[0], d.sum((0, 1, 2)), rtol=1e-4, atol=1e-1)
+    assert torch.allclose(sums[1], (d * (x.double() - mean.double())).sum((0, 1, 2)), rtol=1e-4,
+                          atol=1e-1)
     err = (ops.unpack(dx, C, 1) - ref_dx).abs().max().item()
     assert err < 2e-2 * ref_dx.abs().max().item()
     assert (dw - wr.grad).abs().max().item() < 1e-2 * wr.grad.abs().max().item()
