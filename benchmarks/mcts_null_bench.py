@@ -4,12 +4,14 @@ measured simulations/s is what the host-side tree work alone (selection with vir
 board construction, leaf packing, expansion and backup) can sustain. No GPU is used.
 
   python benchmarks/mcts_null_bench.py [--playouts 65536] [--batch 512] [--threads 16]
-  python -m torch.distributed.run --nproc-per-node 2 benchmarks/mcts_null_bench.py --distributed
+  python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \
+      benchmarks/mcts_null_bench.py --distributed --threads 4
 
 Single process: one JSON line with sims/s and the per-phase split (select, pack, eval = the
-null evaluator itself, backup). ``--distributed`` (gloo, CPU): the multi-rank search of
-search/distributed.py with the null evaluator on every rank — the rate the rank-0 master can
-feed, i.e. the ceiling of the N-GPU search.
+null evaluator itself, backup). ``--distributed`` (gloo, CPU): the shared-root multi-rank search
+of search/distributed.py with the null evaluator on every rank and no rollouts — the aggregate
+rate the ranks' host work plus the per-wave root all-reduce sustain, i.e. the host ceiling of
+the N-GPU search.
 """
 import argparse
 import json
@@ -109,6 +111,45 @@ def run_single(args):
     _ = P
 
 
+def run_distributed(args):
+    """Shared-root search (search/distributed.SharedRootMCTS) on every torchrun rank with the
+    null evaluator and no rollouts (lambda 0): what N ranks' host tree work plus the per-wave root
+    all-reduce can sustain together, i.e. the host ceiling of the N-GPU search. gloo on CPU."""
+    import torch
+    import torch.distributed as dist
+    from rocalphago_amd.engine.gamestate import GameState
+    from rocalphago_amd.parallel.dp import DPContext
+    from rocalphago_amd.search.distributed import SharedRootMCTS
+    dp = DPContext(device="cpu", backend="gloo")
+    ev = NullEvaluator(nthreads=args.threads, seed=dp.rank)
+    mc = SharedRootMCTS(None, value=True, evaluator=ev, dp=dp, lmbda=0.0, batch=args.batch,
+                        nthreads=args.threads, pipeline=1, n_playout=args.playouts)
+    st = GameState()
+    mc.search(st, 4 * args.batch * dp.world)  # warm-up; a fresh tree below
+    mc._search = None
+    dp.barrier()
+    t0 = time.perf_counter()
+    s = mc.search(st, args.playouts)
+    dt = time.perf_counter() - t0
+    t = torch.tensor([float(s.sims), dt, float(mc.exchanges)], dtype=torch.float64)
+    per = [torch.zeros_like(t) for _ in range(dp.world)]
+    if dp.enabled:
+        dist.all_gather(per, t)
+    else:
+        per = [t]
+    if dp.rank == 0:
+        sims = sum(int(p[0]) for p in per)
+        wall = max(float(p[1]) for p in per)
+        print(json.dumps({
+            "metric": "MCTS host ceiling, shared-root N-rank search (null evaluator, gloo), 19x19",
+            "ranks": dp.world, "threads_per_rank": args.threads, "batch": args.batch,
+            "sims": sims, "seconds": round(wall, 3), "sims_per_s": round(sims / wall, 1),
+            "sims_per_s_per_rank": round(sims / wall / dp.world, 1),
+            "exchanges_rank0": int(per[0][2]), "playouts_per_move": args.playouts}), flush=True)
+    if dp.enabled:
+        dp.shutdown()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--playouts", type=int, default=65536)
@@ -119,7 +160,8 @@ def main():
     ap.add_argument("--distributed", action="store_true")
     args = ap.parse_args()
     if args.distributed:
-        raise SystemExit("--distributed: see run_distributed")
+        run_distributed(args)
+        return
     run_single(args)
 
 
