@@ -22,12 +22,22 @@ def _lib():
     return _hip_lib(required=True)
 
 
+# ctypes converts plain ints / None for c_void_p arguments: no per-argument wrapper objects
 def _ptr(t):
-    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+    return None if t is None else t.data_ptr()
+
+
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_cur_device = getattr(torch._C, "_cuda_getDevice", None)
 
 
 def _stream():
-    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    """The current HIP stream of the current device as a raw handle. The C-level getters cost
+    ~1 us; torch.cuda.current_stream() builds a Stream object (~8 us, a third of a self-play
+    ply's host time went there: profiles/selfplay_host_r3.txt)."""
+    if _raw_stream is not None:
+        return _raw_stream(_cur_device())
+    return torch.cuda.current_stream().cuda_stream
 
 
 def _check(rc, name):
@@ -399,7 +409,7 @@ def value_mlp_fwd(z, W1, b1, W2, b2, act="linear", out=None, hout=None):
         out = torch.empty((B, 1), dtype=torch.float32, device=z.device)
     need = _lib().rag_value_mlp_workspace(B, H)
     stream = _stream()
-    key = (z.device, stream.value)  # per stream: pipelined evaluations may run concurrently
+    key = (z.device, stream)  # per stream: pipelined evaluations may run concurrently
     work = _mlp_ws.get(key)
     if work is None or work.numel() < need:
         work = torch.empty(need, dtype=torch.float32, device=z.device)
@@ -452,7 +462,7 @@ def value_mlp_train(z, W1, b1, W2, b2, y, sw, act, dW1, db1, dW2, db2, dz=None, 
         raise ValueError("value_mlp_train: bad gradient shapes")
     lib = _lib()
     stream = _stream()
-    key = (z.device, stream.value)
+    key = (z.device, stream)
     ws = _mlp_train_ws.get(key)
     npart, nbwd = lib.rag_value_mlp_workspace(B, H), lib.rag_value_mlp_bwd_workspace(B, H)
     if ws is None or ws[0].numel() < npart or ws[1].numel() < B * H or ws[2].numel() < nbwd \
