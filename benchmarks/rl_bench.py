@@ -130,6 +130,11 @@ def main():
         r["learner_positions_per_s"] = sp["positions"] / r["seconds"] / 2.0
         r["selfplay_plies"] = sp["plies"]
         r["selfplay_host_share"] = round(sp["host_s"] / tot, 3) if tot else None
+        # where a ply's host time goes (s over the run): native pack / GPU launch (graph
+        # replay) / native play, and the time waiting on the GPU
+        r["selfplay_split_s"] = {k: round(sp[k], 3) for k in ("pack_s", "launch_s", "play_s",
+                                                              "host_s", "gpu_wait_s")
+                                 if k in sp}
     print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}))
 
 

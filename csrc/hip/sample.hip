@@ -38,7 +38,9 @@ __global__ void __launch_bounds__(256) sample_moves_kernel(const float* __restri
                                                            const uint8_t* __restrict__ mask,
                                                            int ms, const uint8_t* __restrict__ greedy,
                                                            int B, int P, float beta, uint64_t seed,
+                                                           const uint64_t* __restrict__ seed_dev,
                                                            int* __restrict__ moves) {
+  if (seed_dev) seed ^= seed_dev[0];  // a captured graph's per-replay seed (self-play plies)
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= B) return;
@@ -76,12 +78,14 @@ __global__ void __launch_bounds__(256) sample_moves_kernel(const float* __restri
 
 }  // namespace
 
+// seed_dev: null, or a device uint64 XORed into `seed` at run time (so a captured HIP graph can
+// draw fresh moves on every replay from a host-written pinned copy).
 RAG_API int rag_sample_moves(const float* probs, const uint8_t* mask, int ms,
                              const uint8_t* greedy, int B, int P, float beta, uint64_t seed,
-                             int* moves, hipStream_t stream) {
+                             const uint64_t* seed_dev, int* moves, hipStream_t stream) {
   if (B <= 0) return 0;
   if (ms < P || P <= 0) return -1;
   sample_moves_kernel<<<(B + 3) / 4, 256, 0, stream>>>(probs, mask, ms, greedy, B, P, beta, seed,
-                                                       moves);
+                                                       seed_dev, moves);
   return (int)hipGetLastError();
 }

@@ -51,7 +51,7 @@ SIGNATURES = {
     "rag_bn_finalize_fwd": [P, I, I, I, I, P, P, P, P, F, F, P, P, P],
     "rag_bn_finalize_bwd": [P, I, I, I, I, P, P, P, P, P, P],
     # sample.hip
-    "rag_sample_moves": [P, P, I, P, I, I, F, C.c_uint64, P, P],
+    "rag_sample_moves": [P, P, I, P, I, I, F, C.c_uint64, P, P, P],
     # features.hip
     "rag_pass_grads": [P, P, P, P, I, I, P],
     "rag_features": [P, P, P, P, P, I, I, P, I, I, P, P, P],

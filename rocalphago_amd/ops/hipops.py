@@ -481,10 +481,11 @@ def value_mlp_train(z, W1, b1, W2, b2, y, sw, act, dW1, db1, dW2, db2, dz=None, 
     return loss[:B]
 
 
-def sample_moves(probs, mask, beta=1.0, greedy=None, seed=0, out=None):
+def sample_moves(probs, mask, beta=1.0, greedy=None, seed=0, out=None, seed_dev=None):
     """Per row: a move drawn from probs^beta restricted to ``mask`` (uint8 [B, >=P]), or the
     masked argmax where ``greedy`` (uint8 [B]) is set; -1 for rows without candidates
-    (sample.hip, Gumbel-max). Returns int32 [B] on the device."""
+    (sample.hip, Gumbel-max). Returns int32 [B] on the device. ``seed_dev`` (int64 [1] on the
+    device, optional) is XORed into the seed when the kernel runs (captured graphs)."""
     B, P = probs.shape
     probs = probs.contiguous().float()
     mask = mask.reshape(B, -1)
@@ -494,8 +495,8 @@ def sample_moves(probs, mask, beta=1.0, greedy=None, seed=0, out=None):
     if out is None:
         out = torch.empty(B, dtype=torch.int32, device=probs.device)
     _check(_lib().rag_sample_moves(_ptr(probs), _ptr(mask), mask.shape[1], _ptr(greedy), B, P,
-                                   float(beta), int(seed) & ((1 << 64) - 1), _ptr(out),
-                                   _stream()), "sample_moves")
+                                   float(beta), int(seed) & ((1 << 64) - 1), _ptr(seed_dev),
+                                   _ptr(out), _stream()), "sample_moves")
     return out
 
 

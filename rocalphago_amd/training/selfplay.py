@@ -76,84 +76,162 @@ class NativeSelfPlay(object):
         gf = self._gf.get(key)
         if gf is None:
             from ..ops.features import GpuFeatures
+            # host ladder reads (the pack): RAG_LADDERS=gpu faulted the GPU once in 19x19
+            # self-play (256 games to the 500-move limit; open item in docs/KERNELS.md), so the
+            # self-play engine does not take the GPU ladder kernel
             gf = self._gf[key] = GpuFeatures(policy.preprocessor.feature_list, self.device,
-                                             self.nthreads)
+                                             self.nthreads, ladders="host")
         return gf
 
-    def _buf(self, name, shape, dtype):
-        t = self._pinned.get(name)
-        if t is None or t.shape[0] < shape[0] or tuple(t.shape[1:]) != tuple(shape[1:]):
-            t = torch.empty(shape, dtype=dtype, pin_memory=True)
-            self._pinned[name] = t
-        return t
-
     # ------------------------------------------------------------------ one ply
-    def _launch(self, batch, player, idx, S, slot=0, limit=None):
+    def _launch(self, batch, player, idx, S, slot=0, limit=None, group=None):
         """Queue one ply of games ``idx`` (pack -> copies in -> features -> policy -> sampling
-        -> chosen points copied back into pinned memory) without waiting for the GPU."""
+        -> chosen points copied back into pinned memory) without waiting for the GPU.
+
+        ``group`` (the fixed game list of a pipeline group, idx a subset of it): every game of
+        the group is packed and evaluated, so the GPU pass has one shape per (group, player) and
+        replays as a captured HIP graph after its first eager run -- one host call instead of ~25
+        Python kernel launches (the launch sequence was the self-play's host bound,
+        profiles/selfplay_host_r3.txt). Finished games ride along; their moves are ignored.
+        RAG_SELFPLAY_GRAPH=0: eager launches of the active games only."""
+        import os
         import time
-        from ..ops import hipops as ops
         t0 = time.perf_counter()
-        n = len(idx)
+        if group is None or os.environ.get("RAG_SELFPLAY_GRAPH", "1") == "0":
+            group = None
+            packed = idx
+            pos = np.arange(len(idx))
+        else:
+            packed = group
+            pos = np.searchsorted(group, idx)
+        n = len(packed)
         P = S * S
         policy = player.policy
         gf = self._features(policy)
         host_lad = gf.ladders and gf.ladder_device == "host"
-        h = {"colors": self._buf("colors%d" % slot, (n, P), torch.int8),
-             "ages": self._buf("ages%d" % slot, (n, P), torch.int16),
-             "meta4": self._buf("meta4%d" % slot, (n, 4), torch.int32)}
-        if host_lad:
-            h["ladders"] = self._buf("ladders%d" % slot, (n, 2, P), torch.uint8)
-        hv = {k: v[:n].numpy() for k, v in h.items()}
-        batch.pack(idx, hv["colors"], hv["ages"], hv["meta4"], hv.get("ladders"))
-        d = {k: v[:n].to(self.device, non_blocking=True) for k, v in h.items()}
-        sens = torch.empty((n, P), dtype=torch.uint8, device=self.device)
-        planes = gf.run(d["colors"], d["ages"], d["meta4"], None, d.get("ladders"), n, S,
-                        sens_out=sens)
-        probs = policy.forward_device(planes)
-        if probs.shape[1] == P + 1:  # pass-logit network: pass is always a candidate
-            sens = torch.cat([sens, torch.ones((n, 1), dtype=torch.uint8, device=self.device)],
-                             1)
-        greedy = None
+        b = self._slot(slot, n, S, gf, host_lad, persistent=group is not None)
+        t1 = time.perf_counter()
+        batch.pack(packed, b["hv"]["colors"], b["hv"]["ages"], b["hv"]["meta4"],
+                   b["hv"].get("ladders"))
+        t2 = time.perf_counter()
+        self.stats["pack_s"] = self.stats.get("pack_s", 0.0) + t2 - t1
         kind = _player_kind(player)
-        beta = getattr(player, "beta", 1.0)
+        beta = float(getattr(player, "beta", 1.0))
         gs = getattr(player, "greedy_start", None)
+        g = b["hv"]["greedy"]
         if kind == "greedy":
-            greedy = torch.ones(n, dtype=torch.uint8, device=self.device)
+            g[:] = 1
         elif gs is not None:
-            g = np.array([batch.board(int(i)).move_count >= gs for i in idx], np.uint8)
-            if g.any():
-                greedy = torch.from_numpy(g).to(self.device)
+            g[:] = [batch.board(int(i)).move_count >= gs for i in packed]
+        else:
+            g[:] = 0
         rng = getattr(player, "rng", np.random)
         seed = (int(rng.randint(0, 2 ** 31 - 1)) << 31) | int(rng.randint(0, 2 ** 31 - 1))
-        mv = ops.sample_moves(probs, sens, beta, greedy, seed)
-        hm = self._buf("moves%d" % slot, (n,), mv.dtype)[:n]
-        hm.copy_(mv, non_blocking=True)
+        b["hv"]["seed"][0] = seed
+        t3 = time.perf_counter()
+        if group is None:
+            self._gpu_pass(b, policy, gf, n, S, P, beta)
+        else:
+            self._replay(b, policy, gf, n, S, P, beta, slot)
         ev = torch.cuda.Event()
         ev.record()
+        self.stats["launch_s"] = self.stats.get("launch_s", 0.0) + time.perf_counter() - t3
         if limit is None:
             limit = player.move_limit if player.move_limit is not None else -1
         self.stats["host_s"] += time.perf_counter() - t0
-        return {"idx": idx, "planes": planes, "moves": hm, "event": ev, "limit": limit,
-                "player": player}
+        return {"idx": idx, "pos": pos, "planes": b["planes"][:n], "moves": b["h"]["moves"][:n],
+                "event": ev, "limit": limit, "player": player}
+
+    def _slot(self, slot, n, S, gf, host_lad, persistent):
+        """Pinned host staging and device buffers of one pipeline slot, for n games: fixed
+        addresses (a captured graph reads and writes them)."""
+        P = S * S
+        key = (slot, n, S, host_lad, gf.F) if persistent else ("eager", slot)
+        b = self._pinned.get(key)
+        if b is not None and (persistent or b["n"] >= n):
+            return b
+        specs = {"colors": ((n, P), torch.int8), "ages": ((n, P), torch.int16),
+                 "meta4": ((n, 4), torch.int32), "greedy": ((n,), torch.uint8),
+                 "seed": ((1,), torch.int64)}
+        if host_lad:
+            specs["ladders"] = ((n, 2, P), torch.uint8)
+        h = {k: torch.zeros(shp, dtype=dt, pin_memory=True) for k, (shp, dt) in specs.items()}
+        h["moves"] = torch.zeros((n,), dtype=torch.int32, pin_memory=True)
+        d = {k: torch.zeros(shp, dtype=dt, device=self.device) for k, (shp, dt) in specs.items()}
+        b = {"n": n, "h": h, "d": d, "hv": {k: v.numpy() for k, v in h.items()},
+             "planes": torch.empty((n, gf.F, S, S), dtype=torch.uint8, device=self.device),
+             "sens": torch.empty((n, P), dtype=torch.uint8, device=self.device),
+             "mv": torch.empty((n,), dtype=torch.int32, device=self.device), "graphs": {}}
+        self._pinned[key] = b
+        return b
+
+    def _gpu_pass(self, b, policy, gf, n, S, P, beta):
+        from ..ops import hipops as ops
+        h, d = b["h"], b["d"]
+        for k in d:
+            d[k][:n].copy_(h[k][:n], non_blocking=True)
+        planes = gf.run(d["colors"][:n], d["ages"][:n], d["meta4"][:n], None,
+                        d["ladders"][:n] if "ladders" in d else None, n, S,
+                        out=b["planes"][:n], sens_out=b["sens"][:n])
+        plan = policy.model._plan_for()
+        with torch.no_grad():
+            probs = plan.forward(planes, clone=False) if plan is not None else \
+                policy.forward_device(planes)
+        sens = b["sens"][:n]
+        if probs.shape[1] == P + 1:  # pass-logit network: pass is always a candidate
+            sens = torch.cat([sens, torch.ones((n, 1), dtype=torch.uint8, device=self.device)],
+                             1)
+        mv = ops.sample_moves(probs, sens, beta, d["greedy"][:n], 0, out=b["mv"][:n],
+                              seed_dev=d["seed"])
+        h["moves"][:n].copy_(mv, non_blocking=True)
+
+    def _replay(self, b, policy, gf, n, S, P, beta, slot):
+        """The slot's GPU pass as a captured HIP graph (captured after one eager run of this
+        shape; recaptured when the plan's buffers moved)."""
+        plan = policy.model._plan_for()
+        if plan is None:
+            return self._gpu_pass(b, policy, gf, n, S, P, beta)
+        gens = tuple(getattr(o, "gen", 0) for o in (plan.trunk, plan.head))
+        key = (id(policy), beta)
+        ent = b["graphs"].get(key)
+        if ent is None or ent[1] != gens:
+            if ent is None and key not in b.setdefault("seen", set()):
+                b["seen"].add(key)
+                return self._gpu_pass(b, policy, gf, n, S, P, beta)  # warm-up, eager
+            graph = torch.cuda.CUDAGraph()
+            side = self.__dict__.get("_cap_stream")
+            if side is None:
+                side = self._cap_stream = torch.cuda.Stream(self.device)
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                with torch.cuda.graph(graph, stream=side, capture_error_mode="thread_local"):
+                    self._gpu_pass(b, policy, gf, n, S, P, beta)
+            torch.cuda.current_stream().wait_stream(side)
+            ent = b["graphs"][key] = (graph, gens)
+        plan.sync_weights()  # the graph reads the packed bf16 weights at fixed addresses
+        ent[0].replay()
 
     def _finish(self, batch, job, S):
-        """Wait for a queued ply and apply it natively; returns (planes, played)."""
+        """Wait for a queued ply and apply it natively; returns (planes, played, pos): the
+        planes rows of the ply's games are ``planes[pos]`` (valid until the slot's next
+        launch)."""
         import time
         t0 = time.perf_counter()
         job["event"].synchronize()
         t1 = time.perf_counter()
-        mv = job["moves"].numpy().astype(np.int32)
+        mv = job["moves"].numpy()[job["pos"]].astype(np.int32)
         mv[(mv < 0) | (mv >= S * S)] = -1
+        t2 = time.perf_counter()
         _, played = batch.play(job["idx"], mv, job["limit"])
+        self.stats["play_s"] = self.stats.get("play_s", 0.0) + time.perf_counter() - t2
         self.stats["plies"] += 1
         self.stats["positions"] += len(job["idx"])
         self.stats["gpu_wait_s"] += t1 - t0
         self.stats["host_s"] += time.perf_counter() - t1
-        return job["planes"], played
+        return job["planes"], played, job["pos"]
 
     def _ply(self, batch, player, idx, S, limit=None):
-        return self._finish(batch, self._launch(batch, player, idx, S, limit=limit), S)
+        return self._finish(batch, self._launch(batch, player, idx, S, limit=limit), S)[:2]
 
     def _groups(self, num_games):
         """Games split into independent groups whose plies alternate on the GPU: while one
@@ -185,13 +263,15 @@ class NativeSelfPlay(object):
         if len(odd):
             self._ply(batch, self.opponent, odd, size)
         K, grp = self._groups(num_games)
+        groups = [np.nonzero(grp == k)[0].astype(np.int32) for k in range(K)]
         current = [self.learner] * K
         jobs = [None] * K
-        recs = []  # (planes, rows of the ply the learner learns from, their games, moves)
+        recs = []  # (learner plane rows of a ply, their games, moves)
 
         def start(k):
             idx = self._active(batch, grp, k)
-            return self._launch(batch, current[k], idx, size, slot=k) if len(idx) else None
+            return self._launch(batch, current[k], idx, size, slot=k,
+                                group=groups[k]) if len(idx) else None
         for k in range(K):
             jobs[k] = start(k)
         while any(j is not None for j in jobs):
@@ -199,11 +279,13 @@ class NativeSelfPlay(object):
                 if jobs[k] is None:
                     continue
                 idx = jobs[k]["idx"]
-                planes, played = self._finish(batch, jobs[k], size)
+                planes, played, pos = self._finish(batch, jobs[k], size)
                 if current[k] is self.learner:
                     r = np.nonzero(played >= 0)[0]
                     if len(r):
-                        recs.append((planes, r, idx[r], played[r]))
+                        # copied out now: the slot's planes buffer is refilled by its next ply
+                        rows = torch.from_numpy(pos[r].astype(np.int64)).to(self.device)
+                        recs.append((planes.index_select(0, rows), idx[r], played[r]))
                 current[k] = self.opponent if current[k] is self.learner else self.learner
                 jobs[k] = start(k)
         self.illegal = batch.illegal
@@ -214,10 +296,9 @@ class NativeSelfPlay(object):
         if not recs:
             return [[] for _ in range(num_games)], [[] for _ in range(num_games)]
         dev = self.device
-        rows = torch.cat([pl[torch.from_numpy(r.astype(np.int64)).to(dev)]
-                          for pl, r, _, _ in recs])
-        gid = np.concatenate([g for _, _, g, _ in recs]).astype(np.int64)
-        mv = np.concatenate([m for _, _, _, m in recs]).astype(np.int64)
+        rows = torch.cat([pl for pl, _, _ in recs])
+        gid = np.concatenate([g for _, g, _ in recs]).astype(np.int64)
+        mv = np.concatenate([m for _, _, m in recs]).astype(np.int64)
         order = np.argsort(gid, kind="stable")  # plies were recorded in move order
         counts = np.bincount(gid, minlength=num_games)
         rows = rows[torch.from_numpy(order).to(dev)]
@@ -243,6 +324,7 @@ class NativeSelfPlay(object):
         # play() passes once move_count > limit: no real move at move_limit moves or later
         limit = move_limit - 1 if own is None else min(move_limit - 1, own)
         K, grp = self._groups(num_games)
+        groups = [np.nonzero(grp == k)[0].astype(np.int32) for k in range(K)]
         jobs = [None] * K
 
         def start(k):
@@ -253,7 +335,8 @@ class NativeSelfPlay(object):
             for g in due:
                 snaps[int(g)] = batch.board(int(g)).copy()
             pending[due] = False
-            return self._launch(batch, self.learner, idx, size, slot=k, limit=limit)
+            return self._launch(batch, self.learner, idx, size, slot=k, limit=limit,
+                                group=groups[k])
         for k in range(K):
             jobs[k] = start(k)
         while any(j is not None for j in jobs):

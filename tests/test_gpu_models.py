@@ -159,6 +159,34 @@ def test_native_selfplay_matches_python_loop(cuda, monkeypatch):
     assert sp.stats["plies"] > 0 and sp.illegal == 0
 
 
+def test_native_selfplay_graph_replay_matches_eager(cuda, monkeypatch):
+    """Self-play plies replayed as captured HIP graphs (two pipeline groups, every game of a
+    group packed each ply, fresh sampling seeds through the pinned seed buffer) play exactly the
+    games of the eager launches, for sampling (probabilistic) players with the same RNG seeds."""
+    import torch
+    from rocalphago_amd.players.ai import ProbabilisticPolicyPlayer
+    from rocalphago_amd.training.selfplay import NativeSelfPlay
+    feats = ["board", "ones", "turns_since", "liberties", "sensibleness"]
+    a = CNNPolicy(feats, board=9, layers=2, filters_per_layer=32, device=cuda, seed=31)
+    b = CNNPolicy(feats, board=9, layers=2, filters_per_layer=32, device=cuda, seed=32)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("RAG_SELFPLAY_GRAPH", mode)
+        la = ProbabilisticPolicyPlayer(a, move_limit=50, rng=np.random.RandomState(7))
+        lb = ProbabilisticPolicyPlayer(b, move_limit=50, rng=np.random.RandomState(8))
+        sp = NativeSelfPlay(la, lb)
+        out[mode] = sp.play(130, 9)
+        if mode == "1":
+            assert any(len(v["graphs"]) for k, v in sp._pinned.items() if k[0] != "eager")
+    f1, m1, c1, w1 = out["1"]
+    f0, m0, c0, w0 = out["0"]
+    assert m1 == m0 and c1 == c0 and np.array_equal(w1, w0)
+    for g in range(130):
+        assert len(f1[g]) == len(f0[g])
+        if len(f1[g]):
+            assert torch.equal(f1[g], f0[g])
+
+
 def test_native_value_generation_matches_python_loop(cuda):
     """generate_value_dataset's native path (all games of a ply in one GameBatch call + one
     GPU pass) samples the same positions and labels as the Python get_moves loop for a greedy
