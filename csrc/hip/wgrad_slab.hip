@@ -354,6 +354,220 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Ping-pong wgrad (192 channels, fp16 partials; RAG_WGRAD_PP=1, opt-in): the same block tile
+// (192 n x one 32-channel c-tile x 9 taps over a chunk of 64-row stages, 3-stage ring) run by 8
+// waves in two groups that alternate roles at every barrier, as conv_tap_pp_kernel does for the
+// forward: per MFMA k-step t (two per stage)
+//
+//   X(t): group 0 reads step t's fragments        group 1 runs the MFMAs of step t-1
+//   ---- s_barrier ----
+//   Y(t): group 0 runs the MFMAs of step t         group 1 reads step t's fragments
+//   ---- s_barrier ----
+//
+// so the two waves of a SIMD (w, w+4) never want the matrix pipe at the same time and no wave
+// needs a second fragment register set. Wave (g, wl): c-fragment g, n-fragments 3 wl .. 3 wl + 2,
+// all 9 taps (27 MFMAs per k-step from 3 + 9 transposed fragment reads). Every wave stages three
+// of the 24 G glds of a stage and waves 0-6 one X glds each; stage s+2 is issued at X(2s) and a
+// wave retires its stage s+1 loads (counted vmcnt, stage s+2 stays in flight) before the barrier
+// into X(2s+2), the first read of stage s+1. Group 1 also sums the bias columns of each stage in
+// its MFMA phase. Partials: the kBF layout of wgrad_slab_kernel with NA = 3, NT = 9, 8 waves
+// (WgradRed.map = 2). Measured SLOWER than the 12-wave slab kernel (B = 256: 97 vs 83 us alone,
+// 148 vs 135 us with the deferred dgrad; SL 99.6k vs 107.2k positions/s,
+// profiles/wgrad_pp_ab_r3.txt): three waves per SIMD already overlap one wave's fragment reads
+// with the others' MFMAs, and four barriers per stage instead of one cost more than the
+// ping-pong saves. Kept opt-in, with its test, as the measured alternative.
+constexpr int kPPWaves = 8;
+template <int NB>
+__global__ void __launch_bounds__(512)
+wgrad_pp_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X, float* __restrict__ part,
+                float* __restrict__ bpart, int R, int WP, int GC, int CIN, int spc, int CINP) {
+  using L = WS<kN>;
+  constexpr int kStage = L::Stage, kGElems = L::GElems, kGChunks = L::GChunks;
+  constexpr int kBlk = L::Blk;
+  constexpr int NA = 3, NT = 9;
+  static_assert(kRows * kGChunks == kPPWaves * 3 * 64, "three G glds per wave");
+  static_assert(NA * NT * kPPWaves == 9 * (kN / 16) * (kC / 16), "the waves cover the tile");
+  __shared__ __attribute__((aligned(16))) bf16 lds[NB * kStage];
+
+  const int lane = lane_id();
+  const int w = wave_id();
+  const int grp = w >> 2, wl = w & 3;  // waves w and w + 4 share a SIMD
+  const int tid = threadIdx.x;
+  const int ntc = CINP / kC;
+  const int wid = xcd_remap(blockIdx.x, gridDim.x);  // the c-tiles of a chunk share one XCD
+  const int chunk = wid / ntc;
+  const int ctile = wid - chunk * ntc;
+  const int c0 = ctile * kC;
+  const int steps = (R + kRows - 1) / kRows;
+  const int sbeg = chunk * spc;
+  int nsteps = steps - sbeg;
+  nsteps = nsteps < spc ? nsteps : spc;
+  nsteps = nsteps > 0 ? nsteps : 0;
+  const int xshift = -(WP + 1);
+
+  int grow[3], gcol[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int slot = (3 * w + k) * 64 + lane;
+    const int row = slot / kGChunks;
+    const int pc = slot - row * kGChunks;
+    grow[k] = row;
+    gcol[k] = (pc ^ L::swz_g(row)) * 8;
+  }
+  const bool xw = w < kXWaves;
+  const int xrow = w * 16 + (lane >> 2);
+  const int xcol = c0 + (((lane & 3) ^ swz_x(xrow)) * 8);
+  const int nl = xw ? 4 : 3;  // this wave's loads per stage
+  auto stage = [&](int s) {
+    const int r0 = (sbeg + s) * kRows;
+    bf16* lg = lds + (s % NB) * kStage;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      int r = r0 + grow[k];
+      r = r < R ? r : R - 1;
+      glds16(G + (size_t)r * GC + gcol[k], lg + (3 * w + k) * 512);
+    }
+    if (xw) {
+      int r = r0 + xshift + xrow;
+      r = r < 0 ? 0 : (r < R ? r : R - 1);
+      glds16(X + (size_t)r * CIN + xcol, lg + kGElems + w * 512);
+    }
+  };
+  auto wait_stage = [&](int young) {  // own loads: `young` younger stages stay in flight
+    if (young <= 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (nl == 4) {
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    }
+  };
+
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int kr = krow(g, q);
+  int goff[NA];
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+    goff[a] = kr * kN + ((((wl * NA + a) * 2 + (p >> 1)) ^ L::swz_g(kr)) * 8) + 4 * (p & 1);
+  int xoff[NT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    const int xr = kr + (i / 3) * WP + (i % 3);
+    xoff[i] = kGElems + xr * kC + (((grp * 2 + (p >> 1)) ^ swz_x(xr)) * 8) + 4 * (p & 1);
+  }
+  f32x4 acc[NT][NA];
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+#pragma unroll
+    for (int a = 0; a < NA; ++a) acc[i][a] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 fa[NA], fb[NT];
+  auto read_frags = [&](int t) {
+    const bf16* lb = lds + ((t >> 1) % NB) * kStage;
+    const int ro = (t & 1) * 32;
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+      fa[a] = tr_frag(lb + goff[a] + ro * kN, lb + goff[a] + (ro + 16) * kN);
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+      fb[i] = tr_frag(lb + xoff[i] + ro * kC, lb + xoff[i] + (ro + 16) * kC);
+    lds_reads_done();
+  };
+  auto mfmas = [&]() {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+      for (int a = 0; a < NA; ++a) acc[i][a] = mfma16(fa[a], fb[i], acc[i][a]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  const bool do_bias = bpart != nullptr;
+  const int bt = tid - 256;  // group 1's threads sum the bias columns
+  const int bcol = ctile * 32 + (bt & 31);
+  float bsum = 0.f;
+
+  const int T = 2 * nsteps;
+  if (nsteps > 0) stage(0);
+  if (nsteps > 1) stage(1);
+  if (nsteps > 0) wait_stage(nsteps > 1 ? 1 : 0);
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (grp == 0) {
+#pragma unroll 1
+    for (int t = 0; t < T; ++t) {
+      const int s = t >> 1;
+      if (!(t & 1) && s + 2 < nsteps) stage(s + 2);
+      read_frags(t);
+      __builtin_amdgcn_s_barrier();  // X -> Y
+      asm volatile("" ::: "memory");
+      mfmas();
+      if ((t & 1) && s + 1 < nsteps) wait_stage(s + 2 < nsteps ? 1 : 0);
+      __builtin_amdgcn_s_barrier();  // Y -> X(t+1)
+      asm volatile("" ::: "memory");
+    }
+  } else {
+#pragma unroll 1
+    for (int t = 0; t < T; ++t) {
+      const int s = t >> 1;
+      if (!(t & 1) && s + 2 < nsteps) stage(s + 2);
+      if (t > 0) mfmas();  // step t-1, beside group 0's reads of step t
+      if (!(t & 1) && do_bias && bcol < kN) {
+        const bf16* lb = lds + (s % NB) * kStage;
+#pragma unroll
+        for (int r = bt >> 5; r < kRows; r += 8)
+          bsum += (float)lb[r * kN + (((bcol >> 3) ^ L::swz_g(r)) << 3) + (bcol & 7)];
+      }
+      __builtin_amdgcn_s_barrier();  // X -> Y
+      asm volatile("" ::: "memory");
+      read_frags(t);                 // beside group 0's MFMAs of step t
+      if ((t & 1) && s + 1 < nsteps) wait_stage(s + 2 < nsteps ? 1 : 0);
+      __builtin_amdgcn_s_barrier();  // Y -> X(t+1)
+      asm volatile("" ::: "memory");
+    }
+    if (T > 0) mfmas();
+  }
+
+  // scaled fp16 partials in the MFMA C layout: [chunk][ctile][i * NA + a][wave][lane][4]
+  float mx = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) mx = fmaxf(mx, fabsf(acc[i][a][r]));
+  mx = warp_max(mx);
+  float* red = reinterpret_cast<float*>(lds);
+  __syncthreads();  // every wave is done with the staging ring
+  if (lane == 0) red[w] = mx;
+  __syncthreads();
+  mx = red[0];
+#pragma unroll
+  for (int k = 1; k < kPPWaves; ++k) mx = fmaxf(mx, red[k]);
+  const int e = mx > 0.f ? max(ilogbf(mx), -100) : 0;
+  const float up = ldexpf(1.f, 14 - e);
+  if (tid == 0) part_scale(part, gridDim.x, kBlk)[wid] = ldexpf(1.f, e - 14);
+  f16* dst = reinterpret_cast<f16*>(part) + (size_t)wid * kBlk + (w * 64 + lane) * 4;
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+      f16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (f16)(acc[i][a][r] * up);
+      *reinterpret_cast<f16x4*>(dst + (i * NA + a) * (kPPWaves * 256)) = o;
+    }
+  if (do_bias) {
+    float* bred = reinterpret_cast<float*>(lds) + 64;
+    if (tid >= 256) bred[bt] = bsum;
+    __syncthreads();
+    if (tid < 32 && ctile * 32 + tid < kN) {
+      float v = 0.f;
+      for (int k = 0; k < 8; ++k) v += bred[k * 32 + tid];
+      bpart[(size_t)chunk * kN + ctile * 32 + tid] = v;
+    }
+  }
+}
+
 // Sums the fp16 partial slabs of wgrad_slab_kernel<.., true> over chunks in fp32 and scatters
 // to OIHW dW [COUT][CIN][3][3] (+ the fp32 bias partials). A 256-thread block owns 64 "octs"
 // (8 consecutive partial elements = two lanes' 4-value C fragments); its 4 waves split the chunks
@@ -435,6 +649,20 @@ int rag_wgrad_slab_nchunks(int R, int CINP, int* spc) {
   return (steps + s - 1) / s;
 }
 
+// ping-pong 192-channel kernel (RAG_WGRAD_PP=1, opt-in: measured slower, see wgrad_pp_kernel)
+static int g_wslab_pp = -1;
+static bool wslab_pp() {
+  if (g_wslab_pp < 0) {
+    const char* e = getenv("RAG_WGRAD_PP");
+    g_wslab_pp = e ? (atoi(e) != 0) : 0;
+  }
+  return g_wslab_pp != 0;
+}
+RAG_API int rag_wgrad_slab_pp(int on) {
+  const int old = g_wslab_pp;
+  g_wslab_pp = on;
+  return old;
+}
 static int g_wslab_nbuf = -1;  // RAG_WGRAD_NBUF (3..5), read on first use
 static int g_wslab_bf = -1;    // block-scaled fp16 partial slabs unless RAG_WGRAD_PART=fp32
 static int g_wslab_map = -1;   // wave -> tile map (WMap), RAG_WGRAD_MAP
@@ -484,6 +712,10 @@ WgradRed rag_wgrad_slab_red(const void* part, const float* bpart, float* dW, flo
   r.blk = ws_blk(CINP);
   r.scale = part_scale((float*)part, nchunks * (CINP / kC), r.blk);
   r.map = CINP == kN ? wslab_map() : 0;
+  if (CINP == kN && wslab_pp()) {  // wgrad_pp_kernel's layout
+    r.map = 2;
+    r.waves = kPPWaves;
+  }
   return r;
 }
 
@@ -514,6 +746,10 @@ int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpar
     wgrad_slab_kernel<4, true, 0, 128, true><<<grid, 512, 0, stream>>>(G, X, part, bpart, R, WP,
                                                                        GC, CIN, spc, CINP, xcoef,
                                                                        S);
+    return (int)hipGetLastError();
+  }
+  if (CINP == kN && bf && wslab_pp()) {
+    wgrad_pp_kernel<3><<<grid, 512, 0, stream>>>(G, X, part, bpart, R, WP, GC, CIN, spc, CINP);
     return (int)hipGetLastError();
   }
   if (CINP == 128) {  // 8 waves, map 0

@@ -66,6 +66,7 @@ SIGNATURES = {
     "rag_wgrad_slab_nbuf": [I],
     "rag_wgrad_slab_part_bf16": [I],
     "rag_wgrad_slab_map": [I],
+    "rag_wgrad_slab_pp": [I],
 }
 
 RESTYPES = {"rag_conv_wgrad_workspace": SZ, "rag_head_bwd_workspace": SZ,

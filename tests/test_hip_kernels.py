@@ -522,3 +522,41 @@ def test_width128_pingpong_conv_and_wgrad_slab(ops):
     assert rel_err(ops.unpack(dx, C, 1), xr.grad * (x > 0)) < 2e-2
     assert rel_err(dw, wr.grad) < 1e-2
     assert rel_err(db, bf(g).sum((0, 2, 3))) < 1e-2
+
+
+@pytest.mark.gpu
+def test_wgrad_pingpong_matches_slab_kernel(ops):
+    """The ping-pong 192-channel wgrad (two wave groups alternating MFMA / fragment-read phases,
+    partial layout map 2) against the 12-wave slab kernel and fp32 PyTorch, deferred into a dgrad
+    and standalone, accumulating, at the bench shape (B = 256)."""
+    dev = torch.device("cuda")
+    torch.manual_seed(13)
+    B, C, S = 256, 192, 19
+    x = F.relu(torch.randn(B, C, S, S, device=dev))
+    g = torch.randn(B, C, S, S, device=dev)
+    w = torch.randn(C, C, 3, 3, device=dev) * 0.05
+    ref = torch.nn.grad.conv2d_weight(bf(x), (C, C, 3, 3), bf(g), padding=1)
+    xp, gp = ops.pack_nchw(x, 1, C), ops.pack_nchw(g, 1, C)
+    _, wb = ops.pack_weights(w, C, C, wb=torch.empty(9, C, C, dtype=torch.bfloat16, device=dev))
+    lib = ops._lib()
+    out = {}
+    for pp in (1, 0):
+        prev = lib.rag_wgrad_slab_pp(pp)
+        try:
+            dw = torch.full((C, C, 3, 3), 0.5, device=dev)
+            db = torch.full((C,), 0.5, device=dev)
+            ops.conv_wgrad(gp, xp, dw, db, B, S, 1, C, C, C, C, 3, accumulate=True, hg=1)
+            h = ops.PendingReduction()
+            ops.conv_wgrad(gp, xp, dw, db, B, S, 1, C, C, C, C, 3, accumulate=True, hg=1,
+                           defer=True, pending=h)
+            dx = ops.alloc_padded(B, S, 1, C, dev)
+            ops.conv_igemm(gp, wb, None, dx, B, S, 1, 1, C, C, 3, False, mask=xp, pending=h)
+            torch.cuda.synchronize()
+            out[pp] = (dw - 0.5, db - 0.5)
+        finally:
+            lib.rag_wgrad_slab_pp(prev)
+    for pp in (1, 0):
+        assert rel_err(out[pp][0], 2 * ref) < 1e-2
+        assert rel_err(out[pp][1], 2 * bf(g).sum((0, 2, 3))) < 1e-2
+    assert rel_err(out[1][0], out[0][0]) < 1e-3
+    assert rel_err(out[1][1], out[0][1]) < 1e-5
