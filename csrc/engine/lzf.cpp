@@ -38,9 +38,16 @@ size_t lzf_decompress(const uint8_t* in, size_t n, uint8_t* out, size_t cap) {
   return op;
 }
 
+// The hash table lives per thread and is never cleared: entries carry a per-call base offset, so
+// an entry below the current call's base is stale (no 128 KB reset per 1.1 MB chunk). Matches are
+// extended 8 bytes at a time (the converter's feature planes are long zero / one runs, matched at
+// up to 264 bytes per back reference).
 size_t lzf_compress(const uint8_t* in, size_t n, uint8_t* out, size_t cap) {
   constexpr int HLOG = 14;
-  std::vector<int64_t> htab(1u << HLOG, -1);
+  thread_local std::vector<uint64_t> htab(1u << HLOG, 0);
+  thread_local uint64_t next_base = 1;
+  const uint64_t base = next_base;
+  next_base += n + 1;
   size_t op = 0, ip = 0, lit = 0;
   auto flush = [&](size_t upto) -> bool {
     while (lit < upto) {
@@ -57,31 +64,47 @@ size_t lzf_compress(const uint8_t* in, size_t n, uint8_t* out, size_t cap) {
   while (ip + 2 < n) {
     uint32_t v = ((uint32_t)in[ip] << 16) | ((uint32_t)in[ip + 1] << 8) | in[ip + 2];
     uint32_t h = (v * 2654435761u) >> (32 - HLOG);
-    int64_t ref = htab[h];
-    htab[h] = (int64_t)ip;
-    if (ref >= 0 && ip - (size_t)ref <= 8192 && in[ref] == in[ip] && in[ref + 1] == in[ip + 1] &&
-        in[ref + 2] == in[ip + 2]) {
-      size_t maxlen = n - ip;
-      if (maxlen > 264) maxlen = 264;
-      size_t len = 3;
-      while (len < maxlen && in[ref + len] == in[ip + len]) ++len;
-      if (!flush(ip)) return 0;
-      size_t off = ip - (size_t)ref - 1;
-      size_t l2 = len - 2;
-      if (l2 < 7) {
-        if (op + 2 > cap) return 0;
-        out[op++] = (uint8_t)((l2 << 5) | (off >> 8));
-      } else {
-        if (op + 3 > cap) return 0;
-        out[op++] = (uint8_t)((7 << 5) | (off >> 8));
-        out[op++] = (uint8_t)(l2 - 7);
+    const uint64_t e = htab[h];
+    htab[h] = base + ip;
+    if (e >= base && ip - (size_t)(e - base) <= 8192) {
+      const size_t ref = (size_t)(e - base);
+      if (in[ref] == in[ip] && in[ref + 1] == in[ip + 1] && in[ref + 2] == in[ip + 2]) {
+        size_t maxlen = n - ip;
+        if (maxlen > 264) maxlen = 264;
+        size_t len = 3;
+        bool done = false;
+        while (len + 8 <= maxlen) {
+          uint64_t a, b;
+          std::memcpy(&a, in + ref + len, 8);
+          std::memcpy(&b, in + ip + len, 8);
+          const uint64_t d = a ^ b;
+          if (d) {
+            len += (size_t)(__builtin_ctzll(d) >> 3);
+            done = true;
+            break;
+          }
+          len += 8;
+        }
+        if (!done)
+          while (len < maxlen && in[ref + len] == in[ip + len]) ++len;
+        if (!flush(ip)) return 0;
+        size_t off = ip - ref - 1;
+        size_t l2 = len - 2;
+        if (l2 < 7) {
+          if (op + 2 > cap) return 0;
+          out[op++] = (uint8_t)((l2 << 5) | (off >> 8));
+        } else {
+          if (op + 3 > cap) return 0;
+          out[op++] = (uint8_t)((7 << 5) | (off >> 8));
+          out[op++] = (uint8_t)(l2 - 7);
+        }
+        out[op++] = (uint8_t)(off & 0xff);
+        ip += len;
+        lit = ip;
+        continue;
       }
-      out[op++] = (uint8_t)(off & 0xff);
-      ip += len;
-      lit = ip;
-    } else {
-      ++ip;
     }
+    ++ip;
   }
   if (!flush(n)) return 0;
   return op;
