@@ -737,14 +737,15 @@ int rag_launch_wgrad_taps(const bf16* G, const bf16* X, float* part, float* bpar
 bool rag_wgrad_taps_fits(int WP, int KS, int RG);  // wgrad.hip
 int rag_wgrad_taps_target_blocks();  // wgrad.hip
 bool rag_wgrad_slab_ok(int S, int H, int HG, int GC, int COUTP, int CINP, int KS);  // wgrad_slab.hip
-int rag_wgrad_slab_nchunks(int R, int CINP, int* spc);                            // wgrad_slab.hip
+int rag_wgrad_slab_nchunks(int R, int CINP, int* spc, int KS);                    // wgrad_slab.hip
 bool rag_wgrad_slab_bf16();                                                        // wgrad_slab.hip
 WgradRed rag_wgrad_slab_red(const void* part, const float* bpart, float* dW, float* db,
-                            int nchunks, int CINP, int COUT, int CIN, int accumulate);
+                            int nchunks, int CINP, int COUTP, int COUT, int CIN, int accumulate,
+                            int KS);
 int rag_launch_wgrad_slab_reduce(const WgradRed& r, hipStream_t stream);        // wgrad_slab.hip
 int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpart, int R, int WP,
                           int GC, int CIN, int spc, int CINP, int nchunks, hipStream_t stream,
-                          const float* xcoef, int S);
+                          const float* xcoef, int S, int KS, int COUTP);
 
 namespace {
 // all-taps variant applicability and plan (see wgrad.hip)
@@ -792,9 +793,11 @@ RAG_API size_t rag_conv_wgrad_workspace(int B, int S, int COUTP, int CINP, int K
     TapsPlan tp = taps_plan(B, S, H, H, COUTP, CINP, KS);
     if (tp.ok && tp.nchunks > nc) nc = tp.nchunks;
   }
-  if (rag_wgrad_slab_ok(S, 1, 1, COUTP, COUTP, CINP, KS)) {
-    const int sn = rag_wgrad_slab_nchunks(B * (S + 2) * (S + 2), CINP, nullptr);
-    if (sn > nc) nc = sn;
+  for (int H = 1; H <= 2; ++H) {
+    if (rag_wgrad_slab_ok(S, H, H, COUTP, COUTP, CINP, KS)) {
+      const int sn = rag_wgrad_slab_nchunks(B * (S + 2 * H) * (S + 2 * H), CINP, nullptr, KS);
+      if (sn > nc) nc = sn;
+    }
   }
   if (nchunks) *nchunks = nc;
   return (size_t)nc * taps * COUTP * CINP + (size_t)nc * COUTP;
@@ -838,16 +841,16 @@ static int conv_wgrad_impl(const void* G, const void* X, float* dW, float* db, f
   float* bpart;
   bool bf16_part = false;
   const bool slab = rag_wgrad_slab_ok(S, HI, HG, GC, COUTP, CINP, KS);
-  if (xcoef && !(slab && rag_wgrad_slab_bf16() && CINP == 128)) return -5;
+  if (xcoef && !(slab && KS == 3 && rag_wgrad_slab_bf16() && CINP == 128)) return -5;
   if (slab) {
     bf16_part = rag_wgrad_slab_bf16();
     const int WP = S + 2 * HI;
     const int R = B * WP * WP;
     int spc = 1;
-    nchunks = rag_wgrad_slab_nchunks(R, CINP, &spc);
+    nchunks = rag_wgrad_slab_nchunks(R, CINP, &spc, KS);
     bpart = db ? work + (size_t)nchunks * taps * COUTP * CINP : nullptr;
     const int rc = rag_launch_wgrad_slab(g, x, part, bpart, R, WP, GC, CINP, spc, CINP, nchunks,
-                                         stream, xcoef, S);
+                                         stream, xcoef, S, KS, COUTP);
     if (rc) return rc;
   } else if (tp.ok) {
     nchunks = tp.nchunks;
@@ -889,8 +892,8 @@ static int conv_wgrad_impl(const void* G, const void* X, float* dW, float* db, f
     rs = reduce_stream;
   }
   if (bf16_part) {
-    const WgradRed r = rag_wgrad_slab_red(part, bpart, dW, db, nchunks, CINP, COUT, CIN,
-                                          accumulate);
+    const WgradRed r = rag_wgrad_slab_red(part, bpart, dW, db, nchunks, CINP, COUTP, COUT, CIN,
+                                          accumulate, KS);
     if (defer && rs == stream) {
       PendingRed* p = static_cast<PendingRed*>(pending);
       p->r = r;

@@ -30,7 +30,8 @@ struct WgradRed {
   float* dW;           // OIHW [COUT][CIN][3][3]
   float* db;           // [COUT] (or null)
   int nchunks, ntc, COUT, CIN, accumulate, map;
-  int n, waves, blk;   // block channels (192 | 128), waves (n / 16), ws_blk(n)
+  int n, waves, blk;   // block channels (192 | 128), waves (n / 16), accumulators per block
+  int taps, kgrp;      // KS * KS; blocks per c-tile (5x5: one kernel row each, else 1)
 };
 
 __device__ __forceinline__ void wslab_add8(float (&s)[8], const uint4& v, float sc) {
@@ -46,8 +47,9 @@ __device__ __forceinline__ void wslab_add8(float (&s)[8], const uint4& v, float 
 // Scatter the chunk sum of oct q to OIHW dW.
 __device__ __forceinline__ void wslab_store_oct(const WgradRed& r, int q, const float (&s)[8]) {
   const int e = q * 8;
-  const int ctile = e / r.blk;
-  const int loc = e - ctile * r.blk;
+  const int pct = e / r.blk;  // (pseudo) c-tile: c-tile * kgrp + kernel row
+  const int loc = e - pct * r.blk;
+  const int ctile = pct / r.kgrp, ky = pct - ctile * r.kgrp;
   const int lane0 = (loc >> 2) & 63;
   const int wv = (loc >> 8) % r.waves;
   const int slot = (loc >> 8) / r.waves;  // i * NA + a
@@ -64,7 +66,7 @@ __device__ __forceinline__ void wslab_store_oct(const WgradRed& r, int q, const 
     cb = ctile * kWsC + ((wv >> 1) & 1) * 16;
   } else {  // map 0: wave wv owns n-frags 2 (wv % g), +1 and c-frag wv / g, g = n / 32
     const int a = slot & 1, g = r.n >> 5;
-    t = slot >> 1;
+    t = ky * 5 + (slot >> 1);  // 3x3: ky = 0, slot >> 1 = tap; 5x5: the block's row ky, kx
     nb = ((wv % g) * 2 + a) * 16;
     cb = ctile * kWsC + (wv / g) * 16;
   }
@@ -77,7 +79,7 @@ __device__ __forceinline__ void wslab_store_oct(const WgradRed& r, int q, const 
     for (int k = 0; k < 4; ++k) {
       const int n = nb + (lane >> 4) * 4 + k;
       if (n >= r.COUT) continue;
-      const size_t o = ((size_t)n * r.CIN + c) * 9 + t;
+      const size_t o = ((size_t)n * r.CIN + c) * r.taps + t;
       r.dW[o] = r.accumulate ? r.dW[o] + s[h * 4 + k] : s[h * 4 + k];
     }
   }

@@ -91,10 +91,10 @@ __host__ __device__ inline float* part_scale(float* part, int nblk, int blk = kB
 // Wave -> tile map (kMAP): the block's 12 n-frags x 2 c-frags x 9 taps = 216 MFMA tiles, 18 per
 // wave. kMAP 0: 2 n-frags x 1 c-frag x 9 taps per wave (11 transposed fragment reads per k-step);
 // kMAP 1: 6 n-frags x 1 c-frag x 3 taps (one kernel row; 9 reads per k-step, -18 % LDS reads).
-template <int kMAP, int N = kN> struct WMap {
-  static_assert(kMAP == 0 || N == 192, "map 1 is the 192-channel layout");
+template <int kMAP, int N = kN, int KS = 3> struct WMap {
+  static_assert(kMAP == 0 || (N == 192 && KS == 3), "map 1 is the 192-channel 3x3 layout");
   static constexpr int NA = kMAP ? 6 : 2;  // n-frags per wave
-  static constexpr int NT = kMAP ? 3 : 9;  // taps per wave
+  static constexpr int NT = kMAP ? 3 : (KS == 3 ? 9 : KS);  // taps per wave (5x5: one row)
   static constexpr int G = N / 32;         // map 0: wave groups along n
   __device__ static int nf0(int w) { return kMAP ? (w & 1) * 6 : (w % G) * 2; }
   __device__ static int cf(int w) { return kMAP ? (w >> 1) & 1 : w / G; }
@@ -110,15 +110,23 @@ template <int kMAP, int N = kN> struct WMap {
 // ReLU and ds_writes it back -- the slot is next read in step s+2. U is never stored in HBM.
 // (Transforming stage s+1 right before barrier s+1 cost +14 %; loading the chunk to registers
 // instead of LDS-DMA made the compiler drain all loads: +60 %.)
-template <int kNBUF, bool kBF, int kMAP, int N = kN, bool BNX = false>
+// KS = 5 (the 5x5 input layer / ResnetPolicy's first unit, halo 2): a block owns ONE kernel row
+// ky (5 taps) of its c-tile, blocks ordered (chunk, c-tile, ky) so the G stages of a chunk are
+// re-read from one XCD's L2; its X slab starts ky rows down (64 + 4 rows of the 112 staged).
+// Partials per block: 5 x N x 32 in the map-0 C layout ("c-tile" = c-tile * 5 + ky for the
+// reduction); the N bias columns are split over those 5 * ntc pseudo c-tiles. fp16 partials only.
+template <int kNBUF, bool kBF, int kMAP, int N = kN, bool BNX = false, int KS = 3>
 __global__ void __launch_bounds__(64 * WS<N>::Waves)
 wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
                   float* __restrict__ part, float* __restrict__ bpart, int R, int WP, int GC,
                   int CIN, int spc, int CINP, const float* __restrict__ xcoef = nullptr,
                   int S = 0) {
   using L = WS<N>;
+  static_assert(KS == 3 || (KS == 5 && kBF && kMAP == 0 && !BNX), "5x5: fp16 map-0 partials");
+  constexpr int kGrp = KS == 3 ? 1 : KS;  // blocks per (chunk, c-tile): kernel rows
   constexpr int kStage = L::Stage, kGElems = L::GElems, kGChunks = L::GChunks;
-  constexpr int kWaves = L::Waves, kBlk = L::Blk, kThreads = 64 * kWaves;
+  constexpr int kWaves = L::Waves, kBlk = KS == 3 ? L::Blk : L::Blk / 9 * KS,
+                kThreads = 64 * kWaves;
   static_assert(!BNX || kNBUF == 4, "the BN prologue pipeline assumes a 4-stage ring");
   // BNX: a [2][64] float table of the column coefficients follows the staging ring (one
   // __shared__ object: see above)
@@ -130,15 +138,17 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
   const int tid = threadIdx.x;
   const int ntc = CINP / kC;
   const int wid = xcd_remap(blockIdx.x, gridDim.x);  // the c-tiles of a chunk share one XCD
-  const int chunk = wid / ntc;
-  const int ctile = wid - chunk * ntc;
+  const int chunk = wid / (ntc * kGrp);
+  const int pct = wid - chunk * ntc * kGrp;  // pseudo c-tile: c-tile * kGrp + ky
+  const int ctile = pct / kGrp, ky = pct - ctile * kGrp;
   const int c0 = ctile * kC;
   const int steps = (R + kRows - 1) / kRows;
   const int sbeg = chunk * spc;
   int nsteps = steps - sbeg;
   nsteps = nsteps < spc ? nsteps : spc;
   nsteps = nsteps > 0 ? nsteps : 0;
-  const int xshift = -(WP + 1);  // X slab row 0 <-> stage row 0 shifted by tap (0, 0)
+  // X slab row 0 <-> stage row 0 shifted by tap (0, 0) (5x5: by tap (ky, 0))
+  const int xshift = KS == 3 ? -(WP + 1) : (ky - 2) * WP - 2;
 
   // staging: G instruction i = 2w + k covers chunk slots [64 i, 64 i + 64) of the [64][24] tile;
   // X instruction w (< 7) covers slab rows [16 w, 16 w + 16)
@@ -208,7 +218,7 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
 
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
   const int kr = krow(g, q);
-  using M = WMap<kMAP, N>;
+  using M = WMap<kMAP, N, KS>;
   constexpr int NA = M::NA, NT = M::NT;
   const int nf0 = M::nf0(w);  // this wave's NA 16-channel n fragments
   const int cf = M::cf(w);    // its 16-channel c fragment
@@ -220,7 +230,7 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
     const int t = M::tap(w, i);
-    const int xr = kr + (t / 3) * WP + (t % 3);
+    const int xr = KS == 3 ? kr + (t / 3) * WP + (t % 3) : kr + t;  // 5x5: t = kx
     xoff[i] = kGElems + xr * kC + (((cf * 2 + (p >> 1)) ^ swz_x(xr)) * 8) + 4 * (p & 1);
   }
 
@@ -230,7 +240,7 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
 #pragma unroll
     for (int a = 0; a < NA; ++a) acc[i][a] = f32x4{0.f, 0.f, 0.f, 0.f};
   const bool do_bias = bpart != nullptr;
-  const int bcol = ctile * 32 + (tid & 31);  // bias columns: this c-tile's 32 of the N
+  const int bcol = pct * 32 + (tid & 31);  // bias columns: this (pseudo) c-tile's 32 of the N
   const int brow = tid >> 5;                 // rows brow, brow + kThreads / 32, ...
   float bsum = 0.f;
 
@@ -385,7 +395,7 @@ wgrad_pp_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X, float* _
   using L = WS<kN>;
   constexpr int kStage = L::Stage, kGElems = L::GElems, kGChunks = L::GChunks;
   constexpr int kBlk = L::Blk;
-  constexpr int NA = 3, NT = 9;
+  constexpr int NA = 3, NT = 9, kGrp = 1;
   static_assert(kRows * kGChunks == kPPWaves * 3 * 64, "three G glds per wave");
   static_assert(NA * NT * kPPWaves == 9 * (kN / 16) * (kC / 16), "the waves cover the tile");
   __shared__ __attribute__((aligned(16))) bf16 lds[NB * kStage];
@@ -396,8 +406,9 @@ wgrad_pp_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X, float* _
   const int tid = threadIdx.x;
   const int ntc = CINP / kC;
   const int wid = xcd_remap(blockIdx.x, gridDim.x);  // the c-tiles of a chunk share one XCD
-  const int chunk = wid / ntc;
-  const int ctile = wid - chunk * ntc;
+  const int chunk = wid / (ntc * kGrp);
+  const int pct = wid - chunk * ntc * kGrp;  // pseudo c-tile: c-tile * kGrp + ky
+  const int ctile = pct / kGrp, ky = pct - ctile * kGrp;
   const int c0 = ctile * kC;
   const int steps = (R + kRows - 1) / kRows;
   const int sbeg = chunk * spc;
@@ -628,20 +639,29 @@ wgrad_slab_reduce_kernel(WgradRed red) {
 // Applicability: 3x3, G and X both halo 1, 192 output channels, CINP == 192 (its six 32-channel
 // c-tiles also split the 192 bias columns), and the X slab covering every tap window of a stage
 // (64 + 2*WP + 2 <= 112). RAG_WGRAD_SLAB=0 disables it.
+bool rag_wgrad_slab_bf16();
 bool rag_wgrad_slab_ok(int S, int H, int HG, int GC, int COUTP, int CINP, int KS) {
   static const bool on = [] {
     const char* e = getenv("RAG_WGRAD_SLAB");
     return !(e && e[0] == '0');
   }();
+  static const bool on5 = [] {  // RAG_WGRAD_SLAB5=0: the 5x5 layers keep wgrad_taps
+    const char* e = getenv("RAG_WGRAD_SLAB5");
+    return !(e && e[0] == '0');
+  }();
   const int WP = S + 2 * H;
-  return on && KS == 3 && H == 1 && HG == 1 && (COUTP == 192 || COUTP == 128) &&
-         CINP == COUTP && GC % 8 == 0 && GC >= COUTP && kRows + 2 * WP + 2 <= kXRows;
+  if (!on || (COUTP != 192 && COUTP != 128) || GC % 8 || GC < COUTP || CINP % kC) return false;
+  if (KS == 3)
+    return H == 1 && HG == 1 && CINP == COUTP && kRows + 2 * WP + 2 <= kXRows;
+  // 5x5: per-row blocks; the 5 * CINP / 32 pseudo c-tiles must cover the COUTP bias columns
+  return KS == 5 && on5 && rag_wgrad_slab_bf16() && H == 2 && HG == 2 &&
+         5 * CINP >= COUTP && kRows + 4 <= kXRows;
 }
 
 // Chunks of 64-row stages: one resident block per CU (256) over all c-tiles.
-int rag_wgrad_slab_nchunks(int R, int CINP, int* spc) {
+int rag_wgrad_slab_nchunks(int R, int CINP, int* spc, int KS) {
   const int steps = (R + kRows - 1) / kRows;
-  int nc = 256 / (CINP / kC);
+  int nc = 256 / (CINP / kC * (KS == 5 ? 5 : 1));
   nc = nc < steps ? nc : steps;
   nc = nc > 0 ? nc : 1;
   const int s = (steps + nc - 1) / nc;
@@ -696,23 +716,26 @@ bool rag_wgrad_slab_bf16() {
 }
 
 WgradRed rag_wgrad_slab_red(const void* part, const float* bpart, float* dW, float* db,
-                            int nchunks, int CINP, int COUT, int CIN, int accumulate) {
+                            int nchunks, int CINP, int COUTP, int COUT, int CIN, int accumulate,
+                            int KS) {
   WgradRed r;
   r.part = (const f16*)part;
   r.bpart = bpart;
   r.dW = dW;
   r.db = db;
   r.nchunks = nchunks;
-  r.ntc = CINP / kC;
+  r.kgrp = KS == 5 ? 5 : 1;
+  r.taps = KS * KS;
+  r.ntc = CINP / kC * r.kgrp;  // (pseudo) c-tiles per chunk
   r.COUT = COUT;
   r.CIN = CIN;
   r.accumulate = accumulate;
-  r.n = CINP;  // square: the block's c-tiles also split the N bias columns
-  r.waves = CINP / 16;
-  r.blk = ws_blk(CINP);
-  r.scale = part_scale((float*)part, nchunks * (CINP / kC), r.blk);
-  r.map = CINP == kN ? wslab_map() : 0;
-  if (CINP == kN && wslab_pp()) {  // wgrad_pp_kernel's layout
+  r.n = COUTP;  // the block's (pseudo) c-tiles also split the N bias columns
+  r.waves = COUTP / 16;
+  r.blk = KS == 5 ? 5 * COUTP * kC : ws_blk(COUTP);
+  r.scale = part_scale((float*)part, nchunks * r.ntc, r.blk);
+  r.map = (COUTP == kN && KS == 3) ? wslab_map() : 0;
+  if (COUTP == kN && KS == 3 && wslab_pp()) {  // wgrad_pp_kernel's layout
     r.map = 2;
     r.waves = kPPWaves;
   }
@@ -734,13 +757,26 @@ RAG_API int rag_wgrad_slab_nbuf(int n) {
 
 int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpart, int R, int WP,
                           int GC, int CIN, int spc, int CINP, int nchunks, hipStream_t stream,
-                          const float* xcoef, int S) {
+                          const float* xcoef, int S, int KS, int COUTP) {
   if (g_wslab_nbuf < 0) {
     const char* e = getenv("RAG_WGRAD_NBUF");
     g_wslab_nbuf = e ? atoi(e) : 3;
   }
-  const dim3 grid(nchunks * (CINP / kC));
   const bool bf = rag_wgrad_slab_bf16();
+  if (KS == 5) {  // per-row blocks, fp16 partials, map 0
+    if (!bf || xcoef) return -5;
+    const dim3 g5(nchunks * (CINP / kC) * 5);
+    if (COUTP == 192)
+      wgrad_slab_kernel<3, true, 0, 192, false, 5><<<g5, 768, 0, stream>>>(G, X, part, bpart, R,
+                                                                          WP, GC, CIN, spc, CINP);
+    else if (COUTP == 128)
+      wgrad_slab_kernel<3, true, 0, 128, false, 5><<<g5, 512, 0, stream>>>(G, X, part, bpart, R,
+                                                                          WP, GC, CIN, spc, CINP);
+    else
+      return -5;
+    return (int)hipGetLastError();
+  }
+  const dim3 grid(nchunks * (CINP / kC));
   if (xcoef) {  // BN prologue: 128 channels, fp16 partials
     if (CINP != 128 || !bf || S > 64) return -5;
     wgrad_slab_kernel<4, true, 0, 128, true><<<grid, 512, 0, stream>>>(G, X, part, bpart, R, WP,

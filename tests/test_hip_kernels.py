@@ -560,3 +560,29 @@ def test_wgrad_pingpong_matches_slab_kernel(ops):
         assert rel_err(out[pp][1], 2 * bf(g).sum((0, 2, 3))) < 1e-2
     assert rel_err(out[1][0], out[0][0]) < 1e-3
     assert rel_err(out[1][1], out[0][1]) < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,cin,cout", [(256, 48, 192), (256, 128, 128), (7, 48, 192)])
+def test_wgrad_slab_5x5_rows(ops, B, cin, cout):
+    """5x5 weight gradients on the slab kernel (one kernel row per block, fp16 partials; the
+    SL input layer 48->192 and ResnetPolicy's first unit 128->128) against fp32 PyTorch and the
+    all-taps kernel (RAG_WGRAD_SLAB5 path off), standalone and deferred into a dgrad."""
+    dev = torch.device("cuda")
+    torch.manual_seed(17)
+    S = 19
+    cinp, coutp = ops.pad_channels(cin), ops.pad_channels(cout)
+    x = F.relu(torch.randn(B, cin, S, S, device=dev))
+    g = torch.randn(B, cout, S, S, device=dev)
+    ref = torch.nn.grad.conv2d_weight(bf(x), (cout, cin, 5, 5), bf(g), padding=2)
+    xp, gp = ops.pack_nchw(x, 2, cinp), ops.pack_nchw(g, 2, coutp)
+    dw = torch.full((cout, cin, 5, 5), 0.25, device=dev)
+    db = torch.full((cout,), 0.25, device=dev)
+    ops.conv_wgrad(gp, xp, dw, db, B, S, 2, cout, coutp, cin, cinp, 5, accumulate=True, hg=2)
+    h = ops.PendingReduction()
+    ops.conv_wgrad(gp, xp, dw, db, B, S, 2, cout, coutp, cin, cinp, 5, accumulate=True, hg=2,
+                   defer=True, pending=h)
+    ops.wgrad_flush(h)
+    torch.cuda.synchronize()
+    assert rel_err(dw - 0.25, 2 * ref) < 1e-2
+    assert rel_err(db - 0.25, 2 * bf(g).sum((0, 2, 3))) < 1e-2
