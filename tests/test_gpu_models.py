@@ -96,6 +96,57 @@ def test_value_train_step_matches_cpu(cuda, dense_act):
     assert max(errs[-4:]) < (2e-2 if dense_act != "relu" else 0.15), errs
     assert max(errs) < 0.25, errs
 
+@pytest.mark.parametrize("dense_act", ["relu", "linear", "tanh"])
+def test_value_head_gradients_match_fp32_on_same_trunk(cuda, dense_act):
+    """The value head's HIP training tail (1x1 conv, value_mlp forward, MSE, value_bwd.hip
+    gradients, the ReLU-masked trunk-top gradient) against fp32 torch autograd applied to the
+    SAME bf16 trunk output, so the bounds measure the head kernels alone (the whole-network
+    comparison above also carries the bf16 trunk's error)."""
+    import torch
+    from rocalphago_amd.features.preprocessing import VALUE_FEATURES
+    from rocalphago_amd.ops import hipops as ops
+    g, _ = _pair(CNNValue, VALUE_FEATURES, filters_per_layer=32, layers=3,
+                 dense_activation=dense_act)
+    plan = g.model._plan_for()
+    net = g.model.net
+    rng = np.random.RandomState(4)
+    B, S = 16, 19
+    X = torch.from_numpy((rng.rand(B, g.preprocessor.output_dim, S, S) > 0.6)
+                         .astype(np.float32)).cuda()
+    Y = torch.from_numpy(rng.uniform(-1, 1, (B, 1)).astype(np.float32)).cuda()
+    net.flat_grad.zero_()
+    Bp = plan.prepare(X)
+    lossv = float(plan.fwd_bwd(Bp, Y.reshape(B, -1)))
+    torch.cuda.synchronize()
+    K = plan.K
+    H = ops.unpack(plan.trunk.output(B), K, 1).detach().clone().requires_grad_()
+    w, b0 = [t.detach().clone().requires_grad_() for t in plan.head_params()]
+    W1, b1, W2, b2 = [t.detach().clone().requires_grad_() for t in plan._dense_params()]
+    z = (H * w.reshape(1, K, 1, 1)).sum(1).reshape(B, -1) + b0
+    h = z @ W1 + b1
+    h = torch.relu(h) if dense_act == "relu" else torch.tanh(h) if dense_act == "tanh" else h
+    v = torch.tanh(h @ W2 + b2)
+    loss = ((v - Y) ** 2).mean()
+    loss.backward()
+    assert abs(lossv - loss.item()) < 1e-4 * max(1.0, abs(loss.item()))
+
+    def rel(a, b):
+        return float((a - b).norm() / max(float(b.norm()), 1e-12))
+    gW1, gb1, gW2, gb2 = net.grads_of(plan.d1) + net.grads_of(plan.d2)
+    hw, hb = net.grads_of(plan.head_name)
+    errs = {"W1": rel(gW1, W1.grad), "b1": rel(gb1, b1.grad), "W2": rel(gW2, W2.grad),
+            "b2": rel(gb2, b2.grad), "head_w": rel(hw.reshape(-1), w.grad.reshape(-1)),
+            "head_b": rel(hb.reshape(-1), b0.grad.reshape(-1))}
+    top = ops.unpack(plan.trunk.top_grad(B), K, 1)
+    ref_top = H.grad * (H > 0) if plan.trunk.top_relu else H.grad
+    errs["dH"] = rel(top, ref_top)
+    print(dense_act, errs)
+    # measured on MI355X: ~1e-7 for every fp32 head gradient, 1.6e-3 for dH (bf16 storage)
+    for k in ("W1", "b1", "W2", "b2", "head_w", "head_b"):
+        assert errs[k] < 1e-5, (k, errs)
+    assert errs["dH"] < 5e-3, errs
+
+
 def test_resnet_uses_hip_convs(cuda):
     g, c = _pair(ResnetPolicy, ["board", "ones"], filters_per_layer=32, layers=3)
     x = g.preprocessor.state_to_tensor(GameState())
