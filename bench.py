@@ -255,10 +255,15 @@ def main():
                 # untimed warmup: 8 waves (allocations, a full 6-wave rollout group); 4 moves timed
                 r = measure(dev, playouts=args.mcts_playouts, warmup=4096, moves=4)
         except Exception as e:  # the SL metric stands on its own
-            err = str(e)[:200]
-        tot = torch.tensor([r["sims_per_s"] if r else 0.0,
-                            r.get("rollouts_per_s", 0.0) if r else 0.0,
-                            1.0 if r else 0.0], device=dev)
+            import traceback
+            traceback.print_exc()  # on stderr, per rank: the cause of a failed measurement
+            err = "rank %d: %s" % (dp.rank, str(e)[:200])
+        # explicit dtype: rank 0's numbers are numpy float64 and the others' Python floats, and
+        # torch.tensor would infer float64 on one rank and float32 on the rest (a collective
+        # mismatch: gloo aborts, RCCL would hang until the guard fired)
+        tot = torch.tensor([float(r["sims_per_s"]) if r else 0.0,
+                            float(r.get("rollouts_per_s", 0.0)) if r else 0.0,
+                            1.0 if r else 0.0], dtype=torch.float64, device=dev)
         dp.allreduce_sum_(tot)
         if guard is not None:
             guard.cancel()

@@ -290,7 +290,8 @@ def run_training(cmd_line_args=None):
             print("Batch {}\tsampled opponent is {}".format(i_iter, opp_weights))
         win_ratio = run_n_games(optimizer, player, opponent, args.game_batch, mode=mode, dp=dp)
         if dp.enabled:
-            win_ratio = dp.allreduce_mean_(torch.tensor([win_ratio], device=dp.device)).item()
+            win_ratio = dp.allreduce_mean_(torch.tensor([float(win_ratio)], dtype=torch.float32,
+                                                        device=dp.device)).item()
         metadata["win_ratio"][player_weights] = (opp_weights, win_ratio)
         player_weights = "weights.%05d.hdf5" % i_iter
         if dp.is_root:
