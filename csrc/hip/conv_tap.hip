@@ -749,6 +749,7 @@ constexpr int kPPBM = 384;
 constexpr int kPPSlabRows = 640;
 constexpr int kPPSlab = kPPSlabRows * kBK;
 constexpr int kPPAL = kPPSlabRows / 64;  // slab glds per loader wave (4 loader waves x 16 rows)
+constexpr int kPPSlabRows5 = 768;        // 5x5 taps (12 glds per loader wave)
 
 // DIAG (diagnostic builds only, wrong results): bit 0 = no staging inside the loop, bit 1 = no
 // fragment reads (MFMAs on stale registers), bit 2 = clock stamps (s_memtime / s_memrealtime of
@@ -761,7 +762,7 @@ constexpr int kPPAL = kPPSlabRows / 64;  // slab glds per loader wave (4 loader 
 // bn.hip's finalize): (sum, sum of squares) of the stored output in the forward, or with smean
 // (the BN's mean) (sum dU, sum dU * (x - mean)) of the masked dgrad output, x = `mask`. They
 // replace the separate statistics passes over the activation.
-template <int NB, int DIAG = 0, int ISSUE = 0, int NT = kNT, bool BNP = false>
+template <int NB, int DIAG = 0, int ISSUE = 0, int NT = kNT, bool BNP = false, int KS = 3>
 __global__ void __launch_bounds__(512)
 conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                    const float* __restrict__ bias, bf16* __restrict__ Y,
@@ -771,8 +772,13 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                    const float* __restrict__ mcoef = nullptr, float* __restrict__ spart = nullptr,
                    const float* __restrict__ smean = nullptr, long long* stamps = nullptr) {
   constexpr int BN = 32 * NT, BTile = BN * kBK, PPBL = BN / 64, EpRow = BN + 8;
+  constexpr int TAPS = KS * KS;  // 9 (3x3) or 25 (the 5x5 layers: SL input, ResNet unit 0)
+  // slab rows: 640 cover any 384-pixel run's 9-tap window (554), 768 its 25-tap one (748)
+  constexpr int SR = KS == 3 ? kPPSlabRows : kPPSlabRows5;
+  constexpr int SLAB = SR * kBK, AL = SR / 64;
+  static_assert(!BNP || KS == 3, "the BN prologue is a 3x3 path");
   static_assert(BN % 64 == 0, "the loader waves stage 64-row weight slices");
-  constexpr int kLoop = 2 * kPPSlab + NB * BTile;
+  constexpr int kLoop = 2 * SLAB + NB * BTile;
   constexpr int kL = kLoop > kPPBM * EpRow ? kLoop : kPPBM * EpRow;  // loop ring | epilogue image
   // weight tiles staged ahead of the current step (issued in the MFMA segment, the slot's last
   // reader is one phase further back: NB tiles ahead are safe)
@@ -815,12 +821,12 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
   // group 0's weight sources (row (wl + 4k)*16 + lane/4 of the 192-row tile)
   // BNP: per staged slab row of this lane (fixed across chunks: column BN), the coefficients of
   // U = ReLU(cx * x + cc); zero on halo / past-the-end rows, so U = 0 there
-  float pcx[BNP ? kPPAL : 1], pcc[BNP ? kPPAL : 1];
+  float pcx[BNP ? AL : 1], pcc[BNP ? AL : 1];
   if constexpr (BNP) {
     const long WI2 = (long)WI * WI;
     const int hi = shift + 1;  // 3x3: the input halo
 #pragma unroll
-    for (int k = 0; k < kPPAL; ++k) {
+    for (int k = 0; k < AL; ++k) {
       const long g = base + (wl + 4 * k) * 16 + lrow;
       const long b = g / WI2;
       const int rem = (int)(g - b * WI2);
@@ -836,9 +842,9 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
   // round trips never sit in front of a barrier (all ten at tap 8 cost +10 % kernel time).
   auto bn_slab = [&](int q, int k0, int k1) {
     if constexpr (BNP) {
-      bf16* dst = lds + (q & 1) * kPPSlab;
+      bf16* dst = lds + (q & 1) * SLAB;
 #pragma unroll
-      for (int k = 0; k < kPPAL; ++k) {
+      for (int k = 0; k < AL; ++k) {
         if (k < k0 || k >= k1) continue;
         bf16x8* p = reinterpret_cast<bf16x8*>(dst + (wl + 4 * k) * 16 * kBK + lane * 8);
         bf16x8 v = *p;
@@ -855,9 +861,9 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
     bsrc[k] = Wt + (long)(n0 + r) * CIN + ((lcol ^ swz4(r)) * 8);
   }
   auto stage_a = [&](int q) {  // slab of chunk q: rows (wl + 4k)*16 .. +15 per glds
-    bf16* dst = lds + (q & 1) * kPPSlab;
+    bf16* dst = lds + (q & 1) * SLAB;
 #pragma unroll
-    for (int k = 0; k < kPPAL; ++k) {
+    for (int k = 0; k < AL; ++k) {
       const int r = (wl + 4 * k) * 16 + lrow;
       long g = base + r;
       g = g < total_rows ? g : total_rows - 1;
@@ -865,8 +871,8 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
     }
   };
   auto stage_b = [&](int s) {  // step s = chunk * 9 + tap
-    const int q = s / 9, t = s - q * 9;
-    bf16* dst = lds + 2 * kPPSlab + (s % NB) * BTile;
+    const int q = s / TAPS, t = s - q * TAPS;
+    bf16* dst = lds + 2 * SLAB + (s % NB) * BTile;
     const long off = t * tap_stride + q * kBK;
 #pragma unroll
     for (int k = 0; k < PPBL; ++k) glds16(bsrc[k] + off, dst + (wl + 4 * k) * 16 * kBK);
@@ -895,17 +901,17 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
     for (int i = 0; i < kMT; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int cchunks = CIN / kBK;
-  const int nsteps = 9 * cchunks;
+  const int nsteps = TAPS * cchunks;
   bf16x8 xa[kMT], wb[NT];
   auto read_frags = [&](int s) {
     if constexpr (DIAG & 2) {
       asm volatile("" : "+v"(xa[0]), "+v"(wb[0]));
       return;
     }
-    const int q = s / 9, t = s - q * 9;
-    const bf16* slab = lds + (q & 1) * kPPSlab;
-    const bf16* bt = lds + 2 * kPPSlab + (s % NB) * BTile;
-    const int ky = t / 3, kx = t - ky * 3;
+    const int q = s / TAPS, t = s - q * TAPS;
+    const bf16* slab = lds + (q & 1) * SLAB;
+    const bf16* bt = lds + 2 * SLAB + (s % NB) * BTile;
+    const int ky = t / KS, kx = t - ky * KS;
     const int toff = ky * WI + kx;
 #pragma unroll
     for (int i = 0; i < kMT; ++i) {
@@ -932,8 +938,8 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
 #pragma unroll
       for (int i = 0; i < kMT; ++i) acc[j][i] = mfma16(wb[j], xa[i], acc[j][i]);
       if (j < PPBL && sb >= 0) {
-        const int q = sb / 9, t = sb - q * 9;
-        bf16* dst = lds + 2 * kPPSlab + (sb % NB) * BTile;
+        const int q = sb / TAPS, t = sb - q * TAPS;
+        bf16* dst = lds + 2 * SLAB + (sb % NB) * BTile;
         glds16(bsrc[j] + t * tap_stride + q * kBK, dst + (wl + 4 * j) * 16 * kBK);
       }
     }
@@ -968,10 +974,10 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
   if (grp == 0) {
     stage_a(0);
     wait_vm<0>();
-    bn_slab(0, 0, kPPAL);
+    bn_slab(0, 0, AL);
 #pragma unroll 1
     for (int s = 0; s < nsteps; ++s) {
-      const int q = s / 9, t = s - q * 9;
+      const int q = s / TAPS, t = s - q * TAPS;
       const bool more = q + 1 < cchunks;
       const long long c1 = now();
       __builtin_amdgcn_s_barrier();  // X_s
@@ -995,7 +1001,7 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
           bn_slab(q + 1, 2 * (t - 4), 2 * (t - 4) + 2);
         }
       } else {
-        if (t == 8 && more) wait_vm<0>();  // slab(q+1) complete before X of the next chunk
+        if (t == TAPS - 1 && more) wait_vm<0>();  // slab(q+1) complete before the next chunk
       }
       const long long c6 = now();
       if constexpr (DIAG & 8) {  // X wait, stage+read, Y wait, MFMA issue, vm wait
@@ -1102,7 +1108,7 @@ int g_tap_mode = -1;  // -1: read RAG_CONV_TAP on first use (default on)
 int g_ep_lds_override = -1;  // rag_conv_ep_lds(): A/B switch of conv_tap_kernel's epilogue
 
 // Worst-case slab extent of a bm-pixel run (host check of the kernels' slab-row assumptions).
-int max_slab_rows(int S, int WI, int shift, int bm) {
+int max_slab_rows(int S, int WI, int shift, int bm, int KS = 3) {
   const int S2 = S * S;
   auto prow = [&](long m) {
     const long b = m / S2, rem = m - b * S2, i = rem / S, j = rem - i * S;
@@ -1110,7 +1116,7 @@ int max_slab_rows(int S, int WI, int shift, int bm) {
   };
   long mx = 0;
   for (long m0 = 0; m0 < (long)S2 * bm + bm; m0 += bm)
-    mx = std::max(mx, prow(m0 + bm - 1) + 2 * WI + 2 - prow(m0) + 1);
+    mx = std::max(mx, prow(m0 + bm - 1) + (KS - 1) * (WI + 1) - prow(m0) + 1);
   return (int)mx;
 }
 
@@ -1202,7 +1208,43 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
   // 192-multiple widths: 96 x 96 wave tiles (NT = 6); 128-multiple widths (ResnetPolicy's and
   // the reference CNNPolicy's default 128 filters) only on the ping-pong kernel, 96 x 64 (NT = 4)
   const bool w192 = COUTP % kBN == 0, w128 = !w192 && COUTP % 128 == 0;
-  if (!g_tap_mode || KS != 3 || !(w192 || w128) || CIN % kBK || CIN < kBK) return false;
+  if (!g_tap_mode || !(KS == 3 || KS == 5) || !(w192 || w128) || CIN % kBK || CIN < kBK)
+    return false;
+  if (KS == 5) {
+    // 5x5 (the SL input layer, ResnetPolicy's first unit): the ping-pong kernel over 25 taps,
+    // when the grid fills the chip and every 384-pixel run's 25-tap slab fits 640 rows
+    static int key5 = -1, rows5 = 0;
+    const int k5 = S * 4096 + WI * 8 + shift;
+    if (k5 != key5) {
+      rows5 = max_slab_rows(S, WI, shift, kPPBM, KS);
+      key5 = k5;
+    }
+    const char* e = getenv("RAG_PP_MIN_BLOCKS");
+    const int pmin = e ? atoi(e) : 200;
+    const int nconv = ((M + kPPBM - 1) / kPPBM) * (COUTP / (w192 ? kBN : 128));
+    static const bool pp5 = [] {  // RAG_CONV_PP5=0: the 5x5 layers stay on conv_pipe
+      const char* v = getenv("RAG_CONV_PP5");
+      return !(v && v[0] == '0');
+    }();
+    if (!pp5 || bnc || mcoef || spart || g_tap_mode < 5 || g_tap_mode > 9 ||
+        rows5 > kPPSlabRows5 || nconv < pmin)
+      return false;
+    int nred = 0;
+    WgradRed r{};
+    if (red) {
+      r = *red;
+      nred = std::max(8, (256 - nconv % 256) % 256);
+    }
+    if (w192)
+      conv_tap_pp_kernel<3, 0, 0, 6, false, 5><<<nconv + nred, 512, 0, stream>>>(
+          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
+          nconv, r);
+    else
+      conv_tap_pp_kernel<3, 0, 0, 4, false, 5><<<nconv + nred, 512, 0, stream>>>(
+          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
+          nconv, r);
+    return true;
+  }
   static int cached_key = -1, cached_rows = 0, cached_rows8 = 0;
   const int key = S * 4096 + WI * 8 + shift;
   if (key != cached_key) {

@@ -586,3 +586,42 @@ def test_wgrad_slab_5x5_rows(ops, B, cin, cout):
     torch.cuda.synchronize()
     assert rel_err(dw - 0.25, 2 * ref) < 1e-2
     assert rel_err(db - 0.25, 2 * bf(g).sum((0, 2, 3))) < 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout", [(48, 192), (128, 128)])
+def test_pingpong_conv_5x5(ops, cin, cout):
+    """5x5 layers at B = 256 on the ping-pong kernel (25 taps per channel chunk): the SL input
+    layer 48->192 (bias + ReLU) and ResnetPolicy's first unit 128->128 (residual forward, dgrad
+    with the ReLU mask), against fp32 PyTorch on bf16-rounded operands."""
+    dev = torch.device("cuda")
+    torch.manual_seed(19)
+    B, S = 256, 19
+    cinp, coutp = ops.pad_channels(cin), ops.pad_channels(cout)
+    x = F.relu(torch.randn(B, cin, S, S, device=dev))
+    w = torch.randn(cout, cin, 5, 5, device=dev) * 0.03
+    b = torch.randn(cout, device=dev) * 0.1
+    xp = ops.pack_nchw(x, 2, cinp)
+    wf, wb = ops.pack_weights(w, coutp, cinp, wb=torch.empty(25, cinp, coutp,
+                                                              dtype=torch.bfloat16, device=dev))
+    bias = torch.zeros(coutp, device=dev)
+    bias[:cout] = b
+    y = ops.alloc_padded(B, S, 1, coutp, dev)
+    ops.conv_igemm(xp, wf, bias, y, B, S, 2, 1, cinp, coutp, 5, relu=True)
+    ref = F.relu(F.conv2d(bf(x), bf(w), b, padding=2))
+    assert rel_err(ops.unpack(y, cout, 1), ref) < 2e-2
+    assert y[:, 0].abs().max().item() == 0 and y[:, :, -1].abs().max().item() == 0
+    if cin == cout:
+        r = torch.randn(B, cout, S, S, device=dev)
+        rp = ops.pack_nchw(r, 1, coutp)
+        yr = ops.alloc_padded(B, S, 1, coutp, dev)
+        ops.conv_igemm(xp, wf, None, yr, B, S, 2, 1, cinp, coutp, 5, relu=False, residual=rp)
+        assert rel_err(ops.unpack(yr, cout, 1), F.conv2d(bf(x), bf(w), padding=2) + bf(r)) < 2e-2
+        g = torch.randn(B, cout, S, S, device=dev)
+        xr = bf(x).requires_grad_()
+        (F.conv2d(xr, bf(w), padding=2) * bf(g)).sum().backward()
+        gp = ops.pack_nchw(g, 2, coutp)
+        dx = ops.alloc_padded(B, S, 1, cinp, dev)
+        xm = ops.pack_nchw(x, 1, cinp)
+        ops.conv_igemm(gp, wb, None, dx, B, S, 2, 1, coutp, cinp, 5, relu=False, mask=xm)
+        assert rel_err(ops.unpack(dx, cin, 1), xr.grad * (x > 0)) < 2e-2
