@@ -21,7 +21,8 @@ def _port():
 def _launch(env_extra, timeout):
     env = dict(os.environ)
     env.update(env_extra)
-    env.update(RAG_TEST_STALL_LIMIT="6", OMP_NUM_THREADS="1")
+    # 12 s: above the start-up skew of two ranks on a loaded CI host (pytest -n 4 saw >6 s)
+    env.update(RAG_TEST_STALL_LIMIT="12", OMP_NUM_THREADS="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()),
            os.path.join(ROOT, "tests", "stall_job.py")]
