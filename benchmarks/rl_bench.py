@@ -133,8 +133,14 @@ def main():
         # where a ply's host time goes (s over the run): native pack / GPU launch (graph
         # replay) / native play, and the time waiting on the GPU
         r["selfplay_split_s"] = {k: round(sp[k], 3) for k in ("pack_s", "launch_s", "play_s",
-                                                              "host_s", "gpu_wait_s")
+                                                              "host_s", "gpu_wait_s",
+                                                              "gpu_pass_s", "wall_s")
                                  if k in sp}
+        # share of the self-play wall time the GPU spends in ply passes: with the two pipelined
+        # groups a busy host overlaps the other group's GPU pass, so this, not the host share,
+        # says which side bounds the loop
+        if sp.get("wall_s") and "gpu_pass_s" in sp:
+            r["selfplay_gpu_busy"] = round(sp["gpu_pass_s"] / sp["wall_s"], 3)
     print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}))
 
 

@@ -129,18 +129,20 @@ class NativeSelfPlay(object):
         seed = (int(rng.randint(0, 2 ** 31 - 1)) << 31) | int(rng.randint(0, 2 ** 31 - 1))
         b["hv"]["seed"][0] = seed
         t3 = time.perf_counter()
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
         if group is None:
             self._gpu_pass(b, policy, gf, n, S, P, beta)
         else:
             self._replay(b, policy, gf, n, S, P, beta, slot)
-        ev = torch.cuda.Event()
+        ev = torch.cuda.Event(enable_timing=True)
         ev.record()
         self.stats["launch_s"] = self.stats.get("launch_s", 0.0) + time.perf_counter() - t3
         if limit is None:
             limit = player.move_limit if player.move_limit is not None else -1
         self.stats["host_s"] += time.perf_counter() - t0
         return {"idx": idx, "pos": pos, "planes": b["planes"][:n], "moves": b["h"]["moves"][:n],
-                "event": ev, "limit": limit, "player": player}
+                "event": ev, "event0": ev0, "limit": limit, "player": player}
 
     def _slot(self, slot, n, S, gf, host_lad, persistent):
         """Pinned host staging and device buffers of one pipeline slot, for n games: fixed
@@ -219,6 +221,11 @@ class NativeSelfPlay(object):
         t0 = time.perf_counter()
         job["event"].synchronize()
         t1 = time.perf_counter()
+        # GPU time of the pass (ev0 fires once the stream reaches it, i.e. after the other
+        # group's pass): summed against the self-play wall time it says whether the pipelined
+        # loop keeps the GPU busy, which the host share alone cannot
+        self.stats["gpu_pass_s"] = self.stats.get("gpu_pass_s", 0.0) + \
+            job["event0"].elapsed_time(job["event"]) * 1e-3
         mv = job["moves"].numpy()[job["pos"]].astype(np.int32)
         mv[(mv < 0) | (mv >= S * S)] = -1
         t2 = time.perf_counter()
@@ -255,6 +262,8 @@ class NativeSelfPlay(object):
         order, or [] if it never moved; per game: its flat moves; learner colours; winners int8
         [num_games]). The rows are gathered once at the end (one index per ply, one sort by
         game), not as per-position tensor views."""
+        import time
+        t_start = time.perf_counter()
         zw, zb, _ = go._zobrist(size)
         batch = _rg.GameBatch(num_games, size, komi, False, zw.ravel().copy(),
                               zb.ravel().copy(), self.nthreads)
@@ -290,6 +299,7 @@ class NativeSelfPlay(object):
                 jobs[k] = start(k)
         self.illegal = batch.illegal
         feats, moves = self._per_game(recs, num_games)
+        self.stats["wall_s"] = self.stats.get("wall_s", 0.0) + time.perf_counter() - t_start
         return feats, moves, colors, batch.winners()
 
     def _per_game(self, recs, num_games):
@@ -313,6 +323,8 @@ class NativeSelfPlay(object):
         earlier) and the winners int8 [num_games]. A game that reaches ``move_limit`` moves
         passes out (the winner is that of the limit position, as the Python loop that stops
         there)."""
+        import time
+        t_start = time.perf_counter()
         zw, zb, _ = go._zobrist(size)
         batch = _rg.GameBatch(num_games, size, komi, False, zw.ravel().copy(),
                               zb.ravel().copy(), self.nthreads)
@@ -350,4 +362,5 @@ class NativeSelfPlay(object):
         for g in np.nonzero(pending)[0]:
             snaps[int(g)] = batch.board(int(g)).copy()
         self.illegal = batch.illegal
+        self.stats["wall_s"] = self.stats.get("wall_s", 0.0) + time.perf_counter() - t_start
         return snaps, batch.winners()

@@ -17,7 +17,7 @@ def load(path):
                   for r in rows)
 
 
-def main(path, marker="pack_input_kernel"):
+def main(path, marker="pack_input"):
     ks = load(path)
     starts = [s for s, e, n in ks if marker in n]
     steps = list(zip(starts, starts[1:]))[-8:]
