@@ -60,8 +60,8 @@ __device__ __forceinline__ void stats_add_pixel(float* sred, int valid, int col,
   }
 }
 
-template <int NT = kNT>
-__device__ __forceinline__ void epilogue(const f32x4 (&acc)[NT][kMT], int mw, int nw, int M,
+template <int NT = kNT, int MT = kMT>
+__device__ __forceinline__ void epilogue(const f32x4 (&acc)[NT][MT], int mw, int nw, int M,
                                          int S, int WO, int HO, int YC, int HM,
                                          const float* __restrict__ bias,
                                          const bf16* __restrict__ res, int relu,
@@ -69,7 +69,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NT][kMT], int mw, in
                                          int frow, int fq, float* sred = nullptr) {
   const int S2 = S * S;
 #pragma unroll
-  for (int i = 0; i < kMT; ++i) {
+  for (int i = 0; i < MT; ++i) {
     const int m = mw + i * 16 + frow;
     if (sred) {  // uniform: every lane takes part in the shuffles
       float s0 = 0.f, s1 = 0.f;
@@ -160,8 +160,8 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NT][kMT], int mw, in
 // applying the dgrad ReLU mask from equally coalesced reads. The register epilogue above writes
 // 16 pixels x 32 bytes per store instruction; this one writes whole rows.
 constexpr int kEpRow = kBN + 8;  // bf16 per LDS image row (192 channels; NT = 4: 136)
-template <int BM, int NT = kNT>
-__device__ __forceinline__ void epilogue_lds(const f32x4 (&acc)[NT][kMT], bf16* __restrict__ img,
+template <int BM, int NT = kNT, int MT = kMT>
+__device__ __forceinline__ void epilogue_lds(const f32x4 (&acc)[NT][MT], bf16* __restrict__ img,
                                              int mwl, int nwl, int m0, int n0, int M, int S,
                                              int WO, int HO, int YC, int HM,
                                              const float* __restrict__ bias, int relu,
@@ -177,7 +177,7 @@ __device__ __forceinline__ void epilogue_lds(const f32x4 (&acc)[NT][kMT], bf16* 
     float4 bb = {0.f, 0.f, 0.f, 0.f};
     if (bias) bb = *reinterpret_cast<const float4*>(bias + n0 + n);
 #pragma unroll
-    for (int i = 0; i < kMT; ++i) {
+    for (int i = 0; i < MT; ++i) {
       float v[4] = {acc[j][i][0] + bb.x, acc[j][i][1] + bb.y, acc[j][i][2] + bb.z,
                     acc[j][i][3] + bb.w};
       bf16x4 o;
@@ -750,6 +750,7 @@ constexpr int kPPSlabRows = 640;
 constexpr int kPPSlab = kPPSlabRows * kBK;
 constexpr int kPPAL = kPPSlabRows / 64;  // slab glds per loader wave (4 loader waves x 16 rows)
 constexpr int kPPSlabRows5 = 768;        // 5x5 taps (12 glds per loader wave)
+constexpr int kPPSlabRows192 = 320;      // 192-pixel blocks (MT = 3, 5 glds per loader wave)
 
 // DIAG (diagnostic builds only, wrong results): bit 0 = no staging inside the loop, bit 1 = no
 // fragment reads (MFMAs on stale registers), bit 2 = clock stamps (s_memtime / s_memrealtime of
@@ -762,7 +763,8 @@ constexpr int kPPSlabRows5 = 768;        // 5x5 taps (12 glds per loader wave)
 // bn.hip's finalize): (sum, sum of squares) of the stored output in the forward, or with smean
 // (the BN's mean) (sum dU, sum dU * (x - mean)) of the masked dgrad output, x = `mask`. They
 // replace the separate statistics passes over the activation.
-template <int NB, int DIAG = 0, int ISSUE = 0, int NT = kNT, bool BNP = false, int KS = 3>
+template <int NB, int DIAG = 0, int ISSUE = 0, int NT = kNT, bool BNP = false, int KS = 3,
+          int MT = kMT>
 __global__ void __launch_bounds__(512)
 conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                    const float* __restrict__ bias, bf16* __restrict__ Y,
@@ -774,12 +776,15 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
   constexpr int BN = 32 * NT, BTile = BN * kBK, PPBL = BN / 64, EpRow = BN + 8;
   constexpr int TAPS = KS * KS;  // 9 (3x3) or 25 (the 5x5 layers: SL input, ResNet unit 0)
   // slab rows: 640 cover any 384-pixel run's 9-tap window (554), 768 its 25-tap one (748)
-  constexpr int SR = KS == 3 ? kPPSlabRows : kPPSlabRows5;
+  // MT = 3: 192-pixel blocks (sub-chip grids, e.g. 128-game self-play passes): <= 298 rows
+  constexpr int SR = KS == 3 ? (MT == kMT ? kPPSlabRows : kPPSlabRows192) : kPPSlabRows5;
+  constexpr int BM = 64 * MT;  // 4 wave rows of MT fragments
+  static_assert(MT == kMT || (MT == 3 && KS == 3 && !BNP), "192-pixel blocks: plain 3x3");
   constexpr int SLAB = SR * kBK, AL = SR / 64;
   static_assert(!BNP || KS == 3, "the BN prologue is a 3x3 path");
   static_assert(BN % 64 == 0, "the loader waves stage 64-row weight slices");
   constexpr int kLoop = 2 * SLAB + NB * BTile;
-  constexpr int kL = kLoop > kPPBM * EpRow ? kLoop : kPPBM * EpRow;  // loop ring | epilogue image
+  constexpr int kL = kLoop > BM * EpRow ? kLoop : BM * EpRow;  // loop ring | epilogue image
   // weight tiles staged ahead of the current step (issued in the MFMA segment, the slot's last
   // reader is one phase further back: NB tiles ahead are safe)
   constexpr int D = ISSUE ? NB : NB - 1;
@@ -801,10 +806,10 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
   const int grp = w >> 2;  // wave-uniform: waves w and w + 4 share a SIMD
   const int wl = w & 3;
   const int wm = grp * 2 + (wl & 1), wn = wl >> 1;
-  const int nblk_m = (M + kPPBM - 1) / kPPBM;
+  const int nblk_m = (M + BM - 1) / BM;
   const int bid = xcd_remap(blockIdx.x, nconv);
   const int bm = bid % nblk_m, bn = bid / nblk_m;
-  const int m0 = bm * kPPBM;
+  const int m0 = bm * BM;
   const int n0 = bn * BN;
   const int S2 = S * S;
   auto prow = [&](int m) {
@@ -880,10 +885,10 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
 
   const int frow = lane & 15;
   const int fq = lane >> 4;
-  int prel[kMT];
+  int prel[MT];
 #pragma unroll
-  for (int i = 0; i < kMT; ++i) {
-    int m = m0 + wm * (16 * kMT) + i * 16 + frow;
+  for (int i = 0; i < MT; ++i) {
+    int m = m0 + wm * (16 * MT) + i * 16 + frow;
     m = m < M ? m : M - 1;
     prel[i] = (int)(prow(m) - base);
   }
@@ -894,15 +899,15 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
     boffs[j] = row * kBK + ((fq ^ swz4(row)) * 8);
   }
 
-  f32x4 acc[NT][kMT];
+  f32x4 acc[NT][MT];
 #pragma unroll
   for (int j = 0; j < NT; ++j)
 #pragma unroll
-    for (int i = 0; i < kMT; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < MT; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int cchunks = CIN / kBK;
   const int nsteps = TAPS * cchunks;
-  bf16x8 xa[kMT], wb[NT];
+  bf16x8 xa[MT], wb[NT];
   auto read_frags = [&](int s) {
     if constexpr (DIAG & 2) {
       asm volatile("" : "+v"(xa[0]), "+v"(wb[0]));
@@ -914,7 +919,7 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
     const int ky = t / KS, kx = t - ky * KS;
     const int toff = ky * WI + kx;
 #pragma unroll
-    for (int i = 0; i < kMT; ++i) {
+    for (int i = 0; i < MT; ++i) {
       const int r = prel[i] + toff;
       xa[i] = *reinterpret_cast<const bf16x8*>(slab + r * kBK + ((fq ^ swz4(r)) * 8));
     }
@@ -927,7 +932,7 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
 #pragma unroll
     for (int j = 0; j < NT; ++j)
 #pragma unroll
-      for (int i = 0; i < kMT; ++i) acc[j][i] = mfma16(wb[j], xa[i], acc[j][i]);
+      for (int i = 0; i < MT; ++i) acc[j][i] = mfma16(wb[j], xa[i], acc[j][i]);
     __builtin_amdgcn_s_setprio(0);
   };
   // MFMA segment with staging loads issued between its MFMA rows (ISSUE = 1)
@@ -936,7 +941,7 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
 #pragma unroll
-      for (int i = 0; i < kMT; ++i) acc[j][i] = mfma16(wb[j], xa[i], acc[j][i]);
+      for (int i = 0; i < MT; ++i) acc[j][i] = mfma16(wb[j], xa[i], acc[j][i]);
       if (j < PPBL && sb >= 0) {
         const int q = sb / TAPS, t = sb - q * TAPS;
         bf16* dst = lds + 2 * SLAB + (sb % NB) * BTile;
@@ -953,7 +958,7 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
   }
   if constexpr (DIAG & 2) {  // random-looking operands (zeros would let the clock rise)
 #pragma unroll
-    for (int i = 0; i < kMT; ++i)
+    for (int i = 0; i < MT; ++i)
 #pragma unroll
       for (int e = 0; e < 8; ++e) xa[i][e] = (bf16)(((lane * 37 + i * 11 + e * 5) % 29) * 0.07f - 1.f);
 #pragma unroll
@@ -1073,11 +1078,11 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
     r1 = __builtin_amdgcn_s_memrealtime();
   }
   if (res) {
-    epilogue(acc, m0 + wm * (16 * kMT), n0 + wn * (16 * NT), M, S, WO, HO, YC, HM, bias, res,
+    epilogue(acc, m0 + wm * (16 * MT), n0 + wn * (16 * NT), M, S, WO, HO, YC, HM, bias, res,
              relu, mask, Y, frow, fq, sred);
   } else {
     __syncthreads();  // every wave is past its last LDS read: the ring becomes the output image
-    epilogue_lds<kPPBM, NT>(acc, lds, wm * (16 * kMT), wn * (16 * NT), m0, n0, M, S, WO, HO, YC, HM,
+    epilogue_lds<BM, NT>(acc, lds, wm * (16 * MT), wn * (16 * NT), m0, n0, M, S, WO, HO, YC, HM,
                         bias, relu, mask, Y, frow, fq, mcoef, sred, smean);
   }
   if (spart) {  // the block's column partials
@@ -1320,6 +1325,28 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
       conv_tap_pp_kernel<3><<<nconv + nred, 512, 0, stream>>>(
           x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
           nconv, r);
+    return true;
+  }
+  // Grids too small for 384-pixel blocks (the 128-game passes of self-play: 121 blocks) but that
+  // fill the chip with 192-pixel ones: the ping-pong kernel with 48 x 96 wave tiles (MT = 3) -- two
+  // waves per SIMD, where conv_tap_kernel below runs ONE 4-wave block per CU, one wave per SIMD,
+  // with nothing to hide its LDS reads behind. RAG_CONV_PP192=0: conv_tap_kernel.
+  static const bool pp192 = [] {
+    const char* v = getenv("RAG_CONV_PP192");
+    return !(v && v[0] == '0');
+  }();
+  const int n192 = ((M + kBM - 1) / kBM) * (COUTP / kBN);
+  if (pp192 && g_tap_mode >= 5 && g_tap_mode <= 9 && n192 >= pp_min &&
+      cached_rows <= kPPSlabRows192) {
+    int nred = 0;
+    WgradRed r{};
+    if (red) {
+      r = *red;
+      nred = std::max(8, (256 - n192 % 256) % 256);
+    }
+    conv_tap_pp_kernel<3, 0, 0, kNT, false, 3, 3><<<n192 + nred, 512, 0, stream>>>(
+        x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
+        n192, r);
     return true;
   }
   if (cached_rows > kSlabRows) return false;
