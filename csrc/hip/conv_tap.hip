@@ -765,7 +765,7 @@ constexpr int kPPSlabRows192 = 320;      // 192-pixel blocks (MT = 3, 5 glds per
 // replace the separate statistics passes over the activation.
 template <int NB, int DIAG = 0, int ISSUE = 0, int NT = kNT, bool BNP = false, int KS = 3,
           int MT = kMT>
-__global__ void __launch_bounds__(512)
+__global__ void __launch_bounds__(512, MT == kMT ? 1 : 4)
 conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                    const float* __restrict__ bias, bf16* __restrict__ Y,
                    const bf16* __restrict__ mask, const bf16* __restrict__ res, int M, int S,
@@ -1296,7 +1296,12 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
     return true;
   }
   const bool pp_fills = ((M + kPPBM - 1) / kPPBM) * (COUTP / kBN) >= pp_min;
-  if ((g_tap_mode >= 5 && g_tap_mode <= 9) && cached_rows8 <= kPPSlabRows && pp_fills) {
+  static const bool pp192_all = [] {  // RAG_CONV_PP192=2: 192-pixel blocks everywhere (A/B)
+    const char* v = getenv("RAG_CONV_PP192");
+    return v && v[0] == '2';
+  }();
+  if ((g_tap_mode >= 5 && g_tap_mode <= 9) && cached_rows8 <= kPPSlabRows && pp_fills &&
+      !pp192_all) {
     // ping-pong kernel: one block per CU; reduce blocks fill the CUs its last round leaves free
     const int nconv = ((M + kPPBM - 1) / kPPBM) * (COUTP / kBN);
     int nred = 0;
