@@ -751,6 +751,7 @@ constexpr int kPPSlab = kPPSlabRows * kBK;
 constexpr int kPPAL = kPPSlabRows / 64;  // slab glds per loader wave (4 loader waves x 16 rows)
 constexpr int kPPSlabRows5 = 768;        // 5x5 taps (12 glds per loader wave)
 constexpr int kPPSlabRows192 = 320;      // 192-pixel blocks (MT = 3, 5 glds per loader wave)
+constexpr int kPPSlabRows192x5 = 448;    // 192-pixel blocks, 5x5 taps (<= 424 rows at 19x19)
 
 // DIAG (diagnostic builds only, wrong results): bit 0 = no staging inside the loop, bit 1 = no
 // fragment reads (MFMAs on stale registers), bit 2 = clock stamps (s_memtime / s_memrealtime of
@@ -777,9 +778,10 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
   constexpr int TAPS = KS * KS;  // 9 (3x3) or 25 (the 5x5 layers: SL input, ResNet unit 0)
   // slab rows: 640 cover any 384-pixel run's 9-tap window (554), 768 its 25-tap one (748)
   // MT = 3: 192-pixel blocks (sub-chip grids, e.g. 128-game self-play passes): <= 298 rows
-  constexpr int SR = KS == 3 ? (MT == kMT ? kPPSlabRows : kPPSlabRows192) : kPPSlabRows5;
+  constexpr int SR = KS == 3 ? (MT == kMT ? kPPSlabRows : kPPSlabRows192)
+                             : (MT == kMT ? kPPSlabRows5 : kPPSlabRows192x5);
   constexpr int BM = 64 * MT;  // 4 wave rows of MT fragments
-  static_assert(MT == kMT || (MT == 3 && KS == 3 && !BNP), "192-pixel blocks: plain 3x3");
+  static_assert(MT == kMT || (MT == 3 && !BNP), "192-pixel blocks: no BN prologue");
   constexpr int SLAB = SR * kBK, AL = SR / 64;
   static_assert(!BNP || KS == 3, "the BN prologue is a 3x3 path");
   static_assert(BN % 64 == 0, "the loader waves stage 64-row weight slices");
@@ -1231,9 +1233,28 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
       const char* v = getenv("RAG_CONV_PP5");
       return !(v && v[0] == '0');
     }();
-    if (!pp5 || bnc || mcoef || spart || g_tap_mode < 5 || g_tap_mode > 9 ||
-        rows5 > kPPSlabRows5 || nconv < pmin)
-      return false;
+    if (!pp5 || bnc || mcoef || spart || g_tap_mode < 5 || g_tap_mode > 9) return false;
+    if (nconv < pmin) {
+      // sub-chip grids (128-game self-play passes): 192-pixel blocks, as the 3x3 layers
+      static int key5b = -1, rows5b = 0;
+      if (k5 != key5b) {
+        rows5b = max_slab_rows(S, WI, shift, kBM, KS);
+        key5b = k5;
+      }
+      const int n192 = ((M + kBM - 1) / kBM) * (COUTP / kBN);
+      if (!w192 || n192 < pmin || rows5b > kPPSlabRows192x5) return false;
+      int nred = 0;
+      WgradRed r{};
+      if (red) {
+        r = *red;
+        nred = std::max(8, (256 - n192 % 256) % 256);
+      }
+      conv_tap_pp_kernel<3, 0, 0, 6, false, 5, 3><<<n192 + nred, 512, 0, stream>>>(
+          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
+          n192, r);
+      return true;
+    }
+    if (rows5 > kPPSlabRows5) return false;
     int nred = 0;
     WgradRed r{};
     if (red) {

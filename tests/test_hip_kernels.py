@@ -26,7 +26,8 @@ def ops():
 @pytest.mark.parametrize("B,cin,cout,ks,S", [(3, 192, 192, 3, 19), (5, 48, 192, 5, 19),
                                              (2, 16, 16, 3, 19), (7, 128, 128, 3, 13),
                                              (4, 192, 32, 1, 19), (1, 12, 16, 5, 9),
-                                             (2, 64, 96, 3, 7), (130, 192, 192, 3, 19)])
+                                             (2, 64, 96, 3, 7), (130, 192, 192, 3, 19),
+                                             (128, 48, 192, 5, 19)])
 def test_conv_forward(ops, B, cin, cout, ks, S):
     dev = torch.device("cuda")
     torch.manual_seed(0)
