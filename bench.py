@@ -252,8 +252,9 @@ def main():
                 r = r or {"sims_per_s": 0.0, "rollouts_per_s": 0.0}
             else:
                 from benchmarks.mcts_bench import measure
-                # untimed warmup: 8 waves (allocations, a full 6-wave rollout group); 4 moves timed
-                r = measure(dev, playouts=args.mcts_playouts, warmup=4096, moves=4)
+                # untimed warmup: 8 waves (allocations, a full 6-wave rollout group); 12 moves timed
+                # (~1 s: 4 moves (0.3 s) varied by +-4 % run to run)
+                r = measure(dev, playouts=args.mcts_playouts, warmup=4096, moves=12)
         except Exception as e:  # the SL metric stands on its own
             import traceback
             traceback.print_exc()  # on stderr, per rank: the cause of a failed measurement
