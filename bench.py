@@ -129,6 +129,9 @@ def main():
         raise SystemExit("HIP fused plan not active for the %s network" % args.model)
 
     counter = [0]
+    # epoch-shuffled sampling, as the trainers' samplers: one device permutation per pass over the
+    # synthetic set, each step a contiguous slice of it (no per-step RNG launch)
+    order = {"perm": None, "pos": N}
 
     def step():
         # heartbeat 2k: step k started; 2k+1: its gradients reached the all-reduce
@@ -137,7 +140,11 @@ def main():
         inject_stall(dp.rank, k)  # RAG_STALL_RANK / RAG_STALL_STEP rehearsal of a hung rank
         if wd is not None:
             wd.beat(2 * k)
-        idx = torch.randint(0, N, (args.batch,), generator=gen, device=dev)
+        if order["pos"] + args.batch > N:
+            order["perm"] = torch.randperm(N, generator=gen, device=dev)
+            order["pos"] = 0
+        idx = order["perm"][order["pos"]:order["pos"] + args.batch]
+        order["pos"] += args.batch
         trainer.step(idx)
         if wd is not None:
             wd.beat(2 * k + 1)
