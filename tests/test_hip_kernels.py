@@ -626,3 +626,30 @@ def test_pingpong_conv_5x5(ops, cin, cout):
         xm = ops.pack_nchw(x, 1, cinp)
         ops.conv_igemm(gp, wb, None, dx, B, S, 2, 1, coutp, cinp, 5, relu=False, mask=xm)
         assert rel_err(ops.unpack(dx, cin, 1), xr.grad * (x > 0)) < 2e-2
+
+
+@pytest.mark.gpu
+def test_pingpong_conv_192px_blocks_residual_and_dgrad(ops):
+    """B = 128 (a self-play pipeline group): 121 blocks of 384 pixels would leave half the chip
+    idle, so the 3x3 layers run the ping-pong kernel on 192-pixel blocks (MT = 3). Forward with
+    the residual sum-merge (register epilogue) and the masked dgrad (LDS epilogue) vs fp32."""
+    dev = torch.device("cuda")
+    torch.manual_seed(21)
+    B, C, S = 128, 192, 19
+    x = F.relu(torch.randn(B, C, S, S, device=dev))
+    w = torch.randn(C, C, 3, 3, device=dev) * 0.05
+    b = torch.randn(C, device=dev) * 0.1
+    r = torch.randn(B, C, S, S, device=dev)
+    xp = ops.pack_nchw(x, 1, C)
+    wf, wb = ops.pack_weights(w, C, C, wb=torch.empty(9, C, C, dtype=torch.bfloat16, device=dev))
+    y = ops.pack_nchw(r, 1, C)  # residual in place
+    ops.conv_igemm(xp, wf, b.contiguous(), y, B, S, 1, 1, C, C, 3, relu=True, residual=y)
+    ref = F.relu(F.conv2d(bf(x), bf(w), b, padding=1) + bf(r))
+    assert rel_err(ops.unpack(y, C, 1), ref) < 2e-2
+    g = torch.randn(B, C, S, S, device=dev)
+    gp = ops.pack_nchw(g, 1, C)
+    dx = ops.alloc_padded(B, S, 1, C, dev)
+    ops.conv_igemm(gp, wb, None, dx, B, S, 1, 1, C, C, 3, relu=False, mask=xp)
+    xr = bf(x).requires_grad_()
+    (F.conv2d(xr, bf(w), padding=1) * bf(g)).sum().backward()
+    assert rel_err(ops.unpack(dx, C, 1), xr.grad * (x > 0)) < 2e-2
