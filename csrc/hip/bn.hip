@@ -186,10 +186,11 @@ __global__ void bn_infer_kernel(BNArgs a, int S) {
   if (w < S) bn_finish_col<2>(a, S, w, 0.0, 0.0);
 }
 
-__global__ void __launch_bounds__(kT) bn_apply_kernel(
-    const bf16* __restrict__ X, int hx, const bf16* __restrict__ DY, int hd,
-    const bf16* RES, int hr, bf16* O, int ho,  // RES may alias O (in-place skip gradient)
-    const float* __restrict__ coef, int relu, int B, int S, int C, int CP) {
+// out = act(c0[w]*x + c1[w]*dy + c2[w] + res) over the interior, grid-stride (coef may be LDS)
+__device__ __forceinline__ void bn_apply_body(const bf16* __restrict__ X, int hx,
+                                              const bf16* __restrict__ DY, int hd, const bf16* RES,
+                                              int hr, bf16* O, int ho, const float* coef, int relu,
+                                              int B, int S, int C, int CP) {
   const int CPV = CP / 8;
   const int total = B * S * S * CPV;  // < 2^31 (checked by the launcher)
   const int WX = S + 2 * hx, WD = S + 2 * hd, WR = S + 2 * hr, WO = S + 2 * ho;
@@ -234,6 +235,56 @@ __global__ void __launch_bounds__(kT) bn_apply_kernel(
     }
     *reinterpret_cast<bf16x8*>(O + ((size_t)(b * WO + h + ho) * WO + w + ho) * CP + c0) = o;
   }
+}
+
+__global__ void __launch_bounds__(kT) bn_apply_kernel(
+    const bf16* __restrict__ X, int hx, const bf16* __restrict__ DY, int hd,
+    const bf16* RES, int hr, bf16* O, int ho,  // RES may alias O (in-place skip gradient)
+    const float* __restrict__ coef, int relu, int B, int S, int C, int CP) {
+  bn_apply_body(X, hx, DY, hd, RES, hr, O, ho, coef, relu, B, S, C, CP);
+}
+
+// The backward BN apply with its finalize folded in: every block sums the nblk backward partials
+// [nblk][2][S] (the dgrad epilogues' (sum dU, sum dU (x - mean))) itself -- 8 slices of 32
+// column lanes, double, the same order in every block, so all blocks derive bit-identical
+// coefficients -- into LDS; block 0 also writes dgamma / dbeta. Saves the finalize launch per BN
+// (19 per ResnetPolicy step); the grid is capped so the partial reads stay a few MB of L2.
+constexpr int kApplyPartBlocks = 1024;
+__global__ void __launch_bounds__(kT) bn_apply_part_kernel(
+    const float* __restrict__ part, int nblk, BNArgs a, const bf16* __restrict__ X, int hx,
+    const bf16* __restrict__ DY, int hd, const bf16* RES, int hr, bf16* O, int ho, int B, int S,
+    int C, int CP) {
+  __shared__ double red[2][8][32];
+  __shared__ float cf[3 * 64];
+  const int t = threadIdx.x, w = t & 31, sl = t >> 5;
+  double s0 = 0.0, s1 = 0.0;
+  if (w < S) {
+#pragma unroll 4
+    for (int i = sl; i < nblk; i += 8) {
+      s0 += part[((size_t)i * 2) * S + w];
+      s1 += part[((size_t)i * 2 + 1) * S + w];
+    }
+  }
+  red[0][sl][w] = s0;
+  red[1][sl][w] = s1;
+  __syncthreads();
+  if (t < S) {
+    double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      a0 += red[0][k][t];
+      a1 += red[1][k][t];
+    }
+    BNArgs b = a;
+    b.coef = cf;
+    if (blockIdx.x != 0) {
+      b.dgamma = nullptr;
+      b.dbeta = nullptr;
+    }
+    bn_finish_col<1>(b, S, t, a0, a1);
+  }
+  __syncthreads();
+  bn_apply_body(X, hx, DY, hd, RES, hr, O, ho, cf, 0, B, S, C, CP);
 }
 
 int reduce_blocks(int R) { return R < 1024 ? R : 1024; }
@@ -314,5 +365,25 @@ RAG_API int rag_bn_apply(const void* X, int hx, const void* DY, int hd, const vo
   bn_apply_kernel<<<(int)nb, kT, 0, stream>>>((const bf16*)X, hx, (const bf16*)DY, hd,
                                               (const bf16*)RES, hr, (bf16*)O, ho, coef, relu, B,
                                               S, C, CP);
+  return (int)hipGetLastError();
+}
+
+// rag_bn_finalize_bwd + rag_bn_apply(dy, coef) in one launch: out = dL/dx (+ RES) of a BN whose
+// backward statistics are the per-block partials `part` [nblk][2][S]; dgamma / dbeta as the
+// finalize. S <= 32.
+RAG_API int rag_bn_apply_bwd_part(const float* part, int nblk, const float* gamma,
+                                  const float* stats, float* dgamma, float* dbeta, const void* X,
+                                  int hx, const void* DY, int hd, const void* RES, int hr, void* O,
+                                  int ho, int B, int S, int C, int CP, hipStream_t stream) {
+  if (S > 32 || CP % 8 || C > CP || (size_t)B * S * S * (CP / 8) >= (1u << 31) || !DY)
+    return -1;
+  const BNArgs a{(double)B * S * C, 0.f, 0.f, gamma, nullptr, nullptr, nullptr, (float*)stats,
+                 nullptr, dgamma, dbeta};
+  const size_t total = (size_t)B * S * S * (CP / 8);
+  size_t nb = (total + kT - 1) / kT;
+  if (nb > kApplyPartBlocks) nb = kApplyPartBlocks;
+  bn_apply_part_kernel<<<(int)nb, kT, 0, stream>>>(part, nblk, a, (const bf16*)X, hx,
+                                                   (const bf16*)DY, hd, (const bf16*)RES, hr,
+                                                   (bf16*)O, ho, B, S, C, CP);
   return (int)hipGetLastError();
 }

@@ -281,6 +281,8 @@ class ResTrunk(_PackedConvs):
         self.defer_reduce = os.environ.get("RAG_WGRAD_DEFER", "1") != "0"
         self._pending = ops.PendingReduction() if device.type == "cuda" else None
         self.bn_prologue = os.environ.get("RAG_BN_PROLOGUE", "1") != "0"
+        # fused BNs: the backward finalize folded into the apply (RAG_BN_FOLD=0: two launches)
+        self.fold_bwd_finalize = os.environ.get("RAG_BN_FOLD", "1") != "0" and self.S <= 32
         self._fused = []  # per BN: fused into the next conv on the last forward
 
     # ------------------------------------------------------------------ buffers
@@ -434,21 +436,31 @@ class ResTrunk(_PackedConvs):
                                    pending=self._pending if defer else None)
                 if on_layer_done is not None:
                     on_layer_done(l)
-                if fused:
-                    ops.bn_finalize_bwd(self.bpart, ops.conv_bn_stat_blocks(B, S, self.KP), B, S,
-                                        K, bn.gamma, self.stats[j], bn.dgamma, bn.dbeta,
-                                        self.bcoef)
+                # i > 0: gradient of the inner conv output Xin[j] = conv j's gx; i == 0:
+                # dL/dA_u = BN'(dU) + skip gradient (in place when halos agree)
+                if i > 0:
+                    out, res = self.gI[self.hin[j]][:B], None
                 else:
-                    ops.bn_bwd_coef(x, dU, B, S, K, bn.gamma, self.stats[j], bn.dgamma,
-                                    bn.dbeta, self.bcoef)
-                if i > 0:  # gradient of the inner conv output Xin[j] = conv j's gx
-                    gx = self.gI[self.hin[j]][:B]
-                    ops.bn_apply(x, gx, B, S, K, coef=self.bcoef, relu=False, dy=dU)
-                else:      # dL/dA_u = BN'(dU) + skip gradient (in place when halos agree)
                     hn = self.hin[self._unit_last[u - 1]] if u > 0 else self.hin[0]
-                    out = self.G[hn][:B]
+                    out, res = self.G[hn][:B], cur
+                if fused and self.fold_bwd_finalize:
+                    # the finalize folded into the apply (each block sums the dgrad's partials)
+                    ops.bn_apply_bwd_part(self.bpart, ops.conv_bn_stat_blocks(B, S, self.KP), x,
+                                          out, B, S, K, bn.gamma, self.stats[j], bn.dgamma,
+                                          bn.dbeta, dU, residual=res)
+                else:
+                    if fused:
+                        ops.bn_finalize_bwd(self.bpart, ops.conv_bn_stat_blocks(B, S, self.KP),
+                                            B, S, K, bn.gamma, self.stats[j], bn.dgamma,
+                                            bn.dbeta, self.bcoef)
+                    else:
+                        ops.bn_bwd_coef(x, dU, B, S, K, bn.gamma, self.stats[j], bn.dgamma,
+                                        bn.dbeta, self.bcoef)
                     ops.bn_apply(x, out, B, S, K, coef=self.bcoef, relu=False, dy=dU,
-                                 residual=cur)
+                                 residual=res)
+                if i > 0:
+                    gx = out
+                else:
                     cur, hcur = out, hn
         s0 = self.specs[0]
         ops.conv_wgrad(cur, self.xin[:B], dws[0], dbs[0], B, S, self.hin[0], s0.cout,

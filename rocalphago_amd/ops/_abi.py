@@ -48,6 +48,7 @@ SIGNATURES = {
     "rag_bn_infer_coef": [P, P, P, P, F, I, P, P],
     "rag_bn_bwd_coef": [P, I, P, I, I, I, I, I, P, P, P, P, P, P, P],
     "rag_bn_apply": [P, I, P, I, P, I, P, I, P, I, I, I, I, I, P],
+    "rag_bn_apply_bwd_part": [P, I, P, P, P, P, P, I, P, I, P, I, P, I, I, I, I, I, P],
     "rag_bn_finalize_fwd": [P, I, I, I, I, P, P, P, P, F, F, P, P, P],
     "rag_bn_finalize_bwd": [P, I, I, I, I, P, P, P, P, P, P],
     # sample.hip

@@ -62,6 +62,7 @@ class GpuFeatures(object):
         self.ladders = any(f in _LADDERS for f in self.fids)
         self.nthreads = nthreads
         self._work = None
+        self._retired = []
         self.ladder_device = ladders or _DEFAULT_LADDERS
         if self.ladder_device not in ("host", "gpu"):
             raise ValueError("ladders must be 'host' or 'gpu'")
@@ -83,7 +84,12 @@ class GpuFeatures(object):
         superko-illegal mask or None, ladder planes [n, 2, S*S] or None: read on the GPU);
         with ``sens_out`` (uint8, n*S*S elements) also the sensibleness mask."""
         if self.ladders and ld is None:
+            old = self._work
             ld, self._work = gpu_ladders(c, m, S, work=self._work)
+            if old is not None and self._work is not old:
+                # a grown workspace never frees the old one: a captured HIP graph (self-play
+                # plies replay as graphs) may still address it
+                self._retired.append(old)
         if out is None:
             out = torch.empty((n, self.F, S, S), dtype=torch.uint8, device=self.device)
         if sens_out is not None and (sens_out.numel() != n * S * S or

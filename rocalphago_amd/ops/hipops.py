@@ -226,6 +226,23 @@ def bn_apply(x, out, B, S, C, coef=None, relu=True, dy=None, residual=None):
     return out
 
 
+def bn_apply_bwd_part(part, nblk, x, out, B, S, C, gamma, stats, dgamma, dbeta, dy,
+                      residual=None):
+    """bn_finalize_bwd + bn_apply(dy, coef) in one launch: out = dL/dx [+ residual] of a BN
+    whose backward statistics are the per-block partials ``part`` [nblk, 2, S] (each block of
+    the apply derives the column coefficients itself); dgamma / dbeta as bn_finalize_bwd."""
+    CP = x.shape[-1]
+    for t in (out, dy, residual):
+        if t is not None and t.shape[-1] != CP:
+            raise ValueError("bn_apply channel mismatch")
+    _check(_lib().rag_bn_apply_bwd_part(
+        _ptr(part), int(nblk), _ptr(gamma), _ptr(stats), _ptr(dgamma), _ptr(dbeta), _ptr(x),
+        _halo(x, S), _ptr(dy), _halo(dy, S), _ptr(residual),
+        0 if residual is None else _halo(residual, S), _ptr(out), _halo(out, S), B, S, C, CP,
+        _stream()), "bn_apply_bwd_part")
+    return out
+
+
 _ws_cache = {}
 
 

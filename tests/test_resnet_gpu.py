@@ -325,3 +325,33 @@ def test_resnet_bn_prologue_train_step_matches_unfused(ops):
         cos = torch.dot(gf, gp).item() / (n * gf.norm().item() + 1e-12)
         assert cos > 0.999, (wname, cos)
         assert abs(gf.norm().item() / n - 1) < 1e-2, (wname, gf.norm().item(), n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("residual", [False, True])
+def test_bn_apply_with_folded_finalize_matches_two_launches(ops, residual):
+    """bn_apply_bwd_part (every block derives the column coefficients from the dgrad partials)
+    equals bn_finalize_bwd + bn_apply: dgamma / dbeta and dL/dx (+ the skip gradient)."""
+    dev = torch.device("cuda")
+    torch.manual_seed(8)
+    B, C, S, nblk = 64, 128, 19, 61
+    part = torch.randn(nblk, 2, S, device=dev) * 3.0
+    gamma = torch.rand(S, device=dev) + 0.5
+    stats = torch.stack([torch.randn(S, device=dev) * 0.1, torch.rand(S, device=dev) + 0.5])
+    x = ops.pack_nchw(torch.randn(B, C, S, S, device=dev), 1, C)
+    dy = ops.pack_nchw(torch.randn(B, C, S, S, device=dev), 1, C)
+    res = ops.pack_nchw(torch.randn(B, C, S, S, device=dev), 1, C) if residual else None
+    dg0, db0 = torch.zeros(S, device=dev), torch.zeros(S, device=dev)
+    coef = torch.zeros(3, S, device=dev)
+    ops.bn_finalize_bwd(part, nblk, B, S, C, gamma, stats, dg0, db0, coef)
+    ref = ops.alloc_padded(B, S, 1, C, dev)
+    ops.bn_apply(x, ref, B, S, C, coef=coef, relu=False, dy=dy, residual=res)
+    dg1, db1 = torch.zeros(S, device=dev), torch.zeros(S, device=dev)
+    out = ops.alloc_padded(B, S, 1, C, dev)
+    ops.bn_apply_bwd_part(part, nblk, x, out, B, S, C, gamma, stats, dg1, db1, dy, residual=res)
+    torch.cuda.synchronize()
+    assert torch.allclose(dg1, dg0, rtol=1e-6, atol=1e-6)
+    assert torch.allclose(db1, db0, rtol=1e-6, atol=1e-6)
+    d = (out.float() - ref.float()).abs()
+    assert d.max().item() <= 1e-2 * ref.float().abs().max().item()
+    assert out[:, 0].abs().max().item() == 0 and out[:, :, -1].abs().max().item() == 0
