@@ -15,6 +15,9 @@ using namespace rag;
 namespace {
 
 constexpr int kHeadThreads = 256;
+// policy_head_fwd: 384 threads, so a 19x19 board's 361 pixel dot products take one pass (with
+// 256 threads 105 of them took two serial 384-byte row walks: the kernel is latency-bound)
+constexpr int kHeadFwdThreads = 384;
 
 __device__ __forceinline__ float block_reduce(float v, float* sh, bool is_max) {
   v = is_max ? warp_max(v) : warp_sum(v);
@@ -28,7 +31,7 @@ __device__ __forceinline__ float block_reduce(float v, float* sh, bool is_max) {
   return r;
 }
 
-__global__ void __launch_bounds__(kHeadThreads)
+__global__ void __launch_bounds__(kHeadFwdThreads)
 policy_head_fwd_kernel(const bf16* __restrict__ H, const float* __restrict__ w, const float* b0,
                        const float* __restrict__ pbias, float* __restrict__ probs,
                        const int64_t* __restrict__ labels, const float* __restrict__ sweight,
@@ -414,7 +417,7 @@ RAG_API int rag_policy_head_fwd(const void* H, const float* w, const float* b0,
                                 hipStream_t stream) {
   // acc (optional, float[2]): += sum of the batch's losses, += number of top-1 hits
   const size_t sm = (size_t)(((S * S + 4) & ~3) + KP) * sizeof(float);
-  policy_head_fwd_kernel<<<B, kHeadThreads, sm, stream>>>((const bf16*)H, w, b0, pbias, probs,
+  policy_head_fwd_kernel<<<B, kHeadFwdThreads, sm, stream>>>((const bf16*)H, w, b0, pbias, probs,
                                                           labels, sweight, loss, dz, hit, nullptr,
                                                           nullptr, nullptr, nullptr, acc, S, KP,
                                                           K, mode, gscale);
@@ -432,7 +435,7 @@ RAG_API int rag_policy_head_pass_fwd(const void* H, const float* w, const float*
                                      int K, int mode, float gscale, hipStream_t stream) {
   if (!pass_w || !pass_b) return -1;
   const size_t sm = (size_t)(((S * S + 4) & ~3) + KP) * sizeof(float);
-  policy_head_fwd_kernel<<<B, kHeadThreads, sm, stream>>>((const bf16*)H, w, b0, pbias, probs,
+  policy_head_fwd_kernel<<<B, kHeadFwdThreads, sm, stream>>>((const bf16*)H, w, b0, pbias, probs,
                                                           labels, sweight, loss, dz, hit, pass_w,
                                                           pass_b, zout, dpass, acc, S, KP, K,
                                                           mode, gscale);
