@@ -476,8 +476,9 @@ __global__ void pack_input_kernel(const T* __restrict__ F, const int64_t* __rest
 // (pixel, 8-channel) stores from LDS. The per-thread gather of pack_input_kernel reads 8 bytes
 // at a 361-byte stride per store (14.7 us for B = 256, 48 planes); this reads F once, in order.
 constexpr int kPackInMaxC = 64, kPackInMaxS2 = 361;
+constexpr int kPackInThreads = 512;  // one block per position: short per-thread load chains
 template <typename T>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(kPackInThreads)
 pack_input_lds_kernel(const T* __restrict__ F, const int64_t* __restrict__ index,
                       const int* __restrict__ tf, bf16* __restrict__ X, int NF, int FS, int S,
                       int H, int CP) {
@@ -492,20 +493,20 @@ pack_input_lds_kernel(const T* __restrict__ F, const int64_t* __restrict__ index
     const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
     const int n4 = n >> 2;
 #pragma unroll 4
-    for (int e = threadIdx.x; e < n4; e += 256) {
+    for (int e = threadIdx.x; e < n4; e += kPackInThreads) {
       const uint32_t w = s4[e];
 #pragma unroll
       for (int k = 0; k < 4; ++k) st[4 * e + k] = (bf16)(float)((w >> (8 * k)) & 0xff);
     }
-    for (int e = 4 * n4 + threadIdx.x; e < n; e += 256) st[e] = (bf16)(float)src[e];
+    for (int e = 4 * n4 + threadIdx.x; e < n; e += kPackInThreads) st[e] = (bf16)(float)src[e];
   } else {
 #pragma unroll 4
-    for (int e = threadIdx.x; e < n; e += 256) st[e] = (bf16)(float)src[e];
+    for (int e = threadIdx.x; e < n; e += kPackInThreads) st[e] = (bf16)(float)src[e];
   }
   __syncthreads();
   const int G = CP / 8, WP = S + 2 * H;
   const int t = tf ? tf[b] : 0;
-  for (int e = threadIdx.x; e < S2 * G; e += 256) {
+  for (int e = threadIdx.x; e < S2 * G; e += kPackInThreads) {
     const int p = e / G, c8 = (e - p * G) * 8;
     const int i = p / S, j = p - i * S;
     int si = i, sj = j;
@@ -1073,7 +1074,8 @@ RAG_API int rag_pack_input_u8(const uint8_t* F, const int64_t* index, const int*
                               int B, int NF, int FS, int S, int H, int CP, hipStream_t stream) {
   if (FS < NF) return -1;
   if (NF <= kPackInMaxC && S * S <= kPackInMaxS2 && CP <= kPackInMaxC && B > 0) {
-    pack_input_lds_kernel<uint8_t><<<B, 256, 0, stream>>>(F, index, tf, (bf16*)X, NF, FS, S, H, CP);
+    pack_input_lds_kernel<uint8_t><<<B, kPackInThreads, 0, stream>>>(F, index, tf, (bf16*)X, NF, FS,
+                                                                     S, H, CP);
     return (int)hipGetLastError();
   }
   const int total = B * S * S * (CP / 8);
@@ -1096,7 +1098,8 @@ RAG_API int rag_pack_input_f32(const float* F, const int64_t* index, const int* 
                                int B, int NF, int FS, int S, int H, int CP, hipStream_t stream) {
   if (FS < NF) return -1;
   if (NF <= kPackInMaxC && S * S <= kPackInMaxS2 && CP <= kPackInMaxC && B > 0) {
-    pack_input_lds_kernel<float><<<B, 256, 0, stream>>>(F, index, tf, (bf16*)X, NF, FS, S, H, CP);
+    pack_input_lds_kernel<float><<<B, kPackInThreads, 0, stream>>>(F, index, tf, (bf16*)X, NF, FS,
+                                                                   S, H, CP);
     return (int)hipGetLastError();
   }
   const int total = B * S * S * (CP / 8);
