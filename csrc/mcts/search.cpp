@@ -16,6 +16,9 @@ using FArr = py::array_t<float, py::array::c_style | py::array::forcecast>;
 }  // namespace
 
 void register_search(py::module_& m) {
+  m.def("trim_tree_cache", [] { return rag::mcts_detail::MapCache::get().trim(); },
+        "unmap the cached (warm) tree arenas kept for the next Search; returns the bytes freed");
+  m.def("tree_cache_bytes", [] { return rag::mcts_detail::MapCache::get().cached_bytes(); });
   py::class_<Search>(m, "Search")
       .def(py::init<const Board&, int>(), py::arg("root"), py::arg("nthreads") = 8)
       .def("reset", &Search::reset)

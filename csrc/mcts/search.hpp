@@ -41,6 +41,7 @@
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <map>
@@ -122,13 +123,38 @@ class MapCache {
   }
   void give(void* p, size_t bytes, size_t warm) {
     std::lock_guard<std::mutex> g(mu_);
-    // keep a bounded amount of resident memory; beyond it the range is unmapped
-    if (free_.size() < 8 && warm_total_ + warm <= (size_t(6) << 30)) {
+    // keep a bounded amount of resident (warm) memory for the next Search's arenas: one node +
+    // one edge arena by default (RAG_TREE_CACHE_MB, 0 = keep nothing); beyond it the range is
+    // unmapped and its pages go back to the OS
+    if (free_.size() < 4 && warm_total_ + warm <= budget()) {
       free_.push_back(Entry{p, bytes, warm});
       warm_total_ += warm;
     } else {
       munmap(p, bytes);
     }
+  }
+  // Unmap every cached range (callers that have finished searching).
+  size_t trim() {
+    std::lock_guard<std::mutex> g(mu_);
+    size_t freed = 0;
+    for (const Entry& e : free_) {
+      munmap(e.p, e.bytes);
+      freed += e.warm;
+    }
+    free_.clear();
+    warm_total_ = 0;
+    return freed;
+  }
+  size_t cached_bytes() {
+    std::lock_guard<std::mutex> g(mu_);
+    return warm_total_;
+  }
+  static size_t budget() {
+    static const size_t b = [] {
+      const char* e = getenv("RAG_TREE_CACHE_MB");
+      return (e && *e ? size_t(atoll(e)) : size_t(2560)) << 20;
+    }();
+    return b;
   }
 
  private:

@@ -41,22 +41,25 @@ class NeuralNetBase(object):
 
     @staticmethod
     def load_model(json_file, device=None):
+        """Rebuild a network from its JSON spec (class name, Keras-1 model JSON,
+        feature list, optional weights file); reference contract
+        /root/reference/AlphaGo/models/nn_util.py:60-83."""
         with open(json_file, 'r') as f:
-            object_specs = json.load(f)
-        class_name = object_specs.get('class', 'CNNPolicy')
-        try:
-            network_class = NeuralNetBase.subclasses[class_name]
-        except KeyError:
-            raise ValueError("Unknown neural network type in json file: {}\n"
-                             "(was it registered with the @neuralnet decorator?)"
-                             .format(class_name))
-        new_net = network_class(object_specs['feature_list'], init_network=False)
-        new_net.model = kerasish.model_from_json(object_specs['keras_model'],
-                                                 custom_objects={'Bias': Bias}, device=device)
-        if 'weights_file' in object_specs:
-            new_net.model.load_weights(_resolve(object_specs['weights_file'], json_file))
-        new_net.forward = new_net._model_forward()
-        return new_net
+            spec = json.load(f)
+        name = spec.get('class', 'CNNPolicy')
+        cls = NeuralNetBase.subclasses.get(name)
+        if cls is None:
+            known = ", ".join(sorted(NeuralNetBase.subclasses))
+            raise ValueError("%s names network class %r, which is not registered (known: %s); "
+                             "decorate the class with @neuralnet" % (json_file, name, known))
+        net = cls(spec['feature_list'], init_network=False)
+        net.model = kerasish.model_from_json(spec['keras_model'], custom_objects={'Bias': Bias},
+                                             device=device)
+        weights = spec.get('weights_file')
+        if weights:
+            net.model.load_weights(_resolve(weights, json_file))
+        net.forward = net._model_forward()
+        return net
 
     def set_dtype(self, dtype):
         """GPU compute precision: ``"bf16"`` (fused HIP kernels, default) or ``"fp32"``
@@ -65,16 +68,14 @@ class NeuralNetBase(object):
         return self
 
     def save_model(self, json_file, weights_file=None):
-        object_specs = {
-            'class': self.__class__.__name__,
-            'keras_model': self.model.to_json(),
-            'feature_list': self.preprocessor.feature_list
-        }
+        """Write the JSON spec (and the weights, when a file is given) that load_model reads."""
+        spec = {'class': type(self).__name__, 'keras_model': self.model.to_json(),
+                'feature_list': self.preprocessor.feature_list}
         if weights_file is not None:
             self.model.save_weights(weights_file)
-            object_specs['weights_file'] = weights_file
+            spec['weights_file'] = weights_file
         with open(json_file, 'w') as f:
-            json.dump(object_specs, f)
+            json.dump(spec, f)
 
 
 def _resolve(path, json_file):

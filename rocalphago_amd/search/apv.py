@@ -54,7 +54,10 @@ class _Slots(object):
                           self.pool[0].planes.shape[1] != F or
                           self.pool[0].o_pri.shape[1] != PW or
                           ("ladders" in self.pool[0].h) != host_ladders):
+            # restart the rotation with the pool: once it refills, the slot handed out next is
+            # pool[0], the oldest wave's (a stale odd ``next`` would return a slot still in flight)
             self.pool = []
+            self.next = 0
         if len(self.pool) < self.depth:
             self.pool.append(_Slot(max(n, cap, 64), S, F, PW, self.device, host_ladders))
             return self.pool[-1]

@@ -65,14 +65,34 @@ class MetadataWriterCallback(K.Callback):
         self.metadata = {"epochs": [], "best_epoch": 0}
 
     def on_epoch_end(self, epoch, logs={}):
-        epoch = len(self.metadata["epochs"])
-        self.metadata["epochs"].append(logs)
-        key = "val_loss" if "val_loss" in logs else "loss"
-        best_loss = self.metadata["epochs"][self.metadata["best_epoch"]][key]
-        if logs.get(key) < best_loss:
-            self.metadata["best_epoch"] = epoch
+        # Keras numbers the epochs of every fit call from 0: append (the reference's behaviour)
+        self.record(len(self.metadata["epochs"]), logs)
+
+    def record(self, epoch, logs):
+        """Log ``logs`` as global epoch ``epoch`` (0-based, the weights file's number): the list
+        is cut or padded so that entry i always describes ``weights.<i>.hdf5``, and
+        ``best_epoch`` is recomputed from the entries kept."""
+        eps = self.metadata["epochs"]
+        del eps[epoch:]
+        while len(eps) < epoch:
+            eps.append({})  # an epoch whose log was lost (never written before a kill)
+        eps.append(logs)
+        self.metadata["best_epoch"] = best_epoch(eps)
         if K._is_rank0():
             _atomic_json(self.file, self.metadata, indent=2)
+
+
+def best_epoch(epochs):
+    """Index of the lowest val_loss (loss without a validation split) among the logged epochs;
+    the earliest on ties, 0 when nothing is logged."""
+    best, key = 0, None
+    for i, logs in enumerate(epochs):
+        k = "val_loss" if "val_loss" in logs else "loss"
+        if k not in logs:
+            continue
+        if key is None or logs[k] < epochs[best].get(key, float("inf")):
+            best, key = i, k
+    return best
 
 
 class SupervisedTrainer(object):
@@ -368,7 +388,7 @@ def run_training(cmd_line_args=None):
         save_checkpoint(checkpointer, gepoch, logs,
                         {"iterations": int(sgd.iterations), "cursor": int(cursor),
                          "lr": args.learning_rate, "decay": args.decay})
-        meta_writer.on_epoch_end(gepoch, logs)
+        meta_writer.record(gepoch, logs)
         if dp.is_root:
             with open(metrics_file, "a") as f:
                 f.write(json.dumps(dict(logs, epoch=gepoch, seconds=round(dt, 3),
@@ -405,7 +425,10 @@ def save_checkpoint(checkpointer, epoch, logs, opt_state):
         checkpointer.on_epoch_end(epoch, logs)  # no-op off rank 0
         return
     path = checkpointer.filepath.format(epoch=epoch, **logs)
-    _atomic_json(os.path.splitext(path)[0] + ".opt.json", dict(opt_state, epoch=epoch))
+    # the epoch's logs ride in the sidecar: a kill between the checkpoint and metadata.json
+    # leaves the metadata one entry short, and resume restores that entry from here
+    _atomic_json(os.path.splitext(path)[0] + ".opt.json", dict(opt_state, epoch=epoch,
+                                                               logs=logs))
     checkpointer.on_epoch_end(epoch, logs)
 
 
@@ -439,8 +462,12 @@ def resume_epoch_base(metadata, opt_state):
         return len(epochs)
     base = int(opt_state["epoch"]) + 1
     del epochs[base:]
-    if metadata.get("best_epoch", 0) >= max(1, len(epochs)):
-        metadata["best_epoch"] = 0
+    if len(epochs) < base:
+        # killed after the checkpoint, before metadata.json recorded its epoch
+        while len(epochs) < base - 1:
+            epochs.append({})
+        epochs.append(dict(opt_state.get("logs") or {}))
+    metadata["best_epoch"] = best_epoch(epochs)
     return base
 
 

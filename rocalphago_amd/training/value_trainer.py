@@ -74,7 +74,12 @@ def generate_value_dataset(player, n_games, out_file=None, board=19, features=VA
     GPU pass (training/selfplay.py) instead of the per-game Python loop."""
     rng = rng or np.random.RandomState(0)
     if world > 1:
+        shared = getattr(player, "rng", None) is rng
         rng = np.random.RandomState(rng.randint(0, 2 ** 31 - 1) + 7919 * rank)
+        if shared:
+            # the player draws its moves (and the native self-play seeds) from its own rng: a
+            # player built on the caller's stream would play the same games on every rank
+            player.rng = np.random.RandomState(rng.randint(0, 2 ** 31 - 1))
     mine = len(range(rank, n_games, world))
     pp = Preprocess(features)
     use_native = _use_native(player, native)
@@ -164,9 +169,12 @@ def run_generate(cmd_line_args=None):
     dp = DPContext()
     pol = CNNPolicy.load_model(args.model, device=dp.device)
     pol.model.load_weights(args.weights)
+    # one random stream per rank for the player's moves (the same seed everywhere would give
+    # every rank the same game trajectories); the snapshot targets draw from ``rng``
     rng = np.random.RandomState(args.seed)
     player = ProbabilisticPolicyPlayer(pol, temperature=args.temperature,
-                                       move_limit=args.move_limit, rng=rng)
+                                       move_limit=args.move_limit,
+                                       rng=np.random.RandomState(args.seed + 7919 * dp.rank))
     board = pol.model.input_shape[-1]
     features = list(pol.preprocessor.feature_list) + ["color"]
     t0 = time.time()
@@ -386,7 +394,7 @@ def run_training(cmd_line_args=None):
         save_checkpoint(ckpt, gepoch, logs,
                         {"iterations": int(sgd.iterations), "cursor": int(cursor),
                          "lr": args.learning_rate, "decay": args.decay})
-        meta.on_epoch_end(gepoch, logs)
+        meta.record(gepoch, logs)
         if dp.is_root:
             with open(os.path.join(args.out_directory, "metrics.jsonl"), "a") as f:
                 f.write(json.dumps(dict(logs, epoch=gepoch, seconds=round(dt, 3),

@@ -259,3 +259,36 @@ def test_parallel_select_claims_distinct_leaves():
     assert s.root_visits == total > 600
     mv, vis, _, _ = s.root_stats()
     assert vis.sum() == total - 1
+
+
+def test_slot_pool_restarts_rotation_when_reallocated(monkeypatch):
+    """After a shape change empties the pool, the rotation restarts at the oldest slot: with
+    two waves in flight a stale odd counter would hand out the slot of the wave still in flight
+    (_Slots.take)."""
+    from types import SimpleNamespace
+
+    from rocalphago_amd.search import apv
+
+    def fake_slot(B, S, F, PW, device, host_ladders):
+        return SimpleNamespace(B=B, S=S, planes=np.zeros((1, F)), o_pri=np.zeros((1, PW)),
+                               h={"ladders": 1} if host_ladders else {})
+    monkeypatch.setattr(apv, "_Slot", fake_slot)
+    slots = apv._Slots("cpu", 2)
+    a, b = slots.take(64, 19, 48, 362, False), slots.take(64, 19, 48, 362, False)
+    assert slots.take(64, 19, 48, 362, False) is a  # next = 1 (odd) now
+    c = slots.take(64, 9, 48, 82, False)  # new board size: pool reallocated
+    d = slots.take(64, 9, 48, 82, False)
+    assert c is not d
+    assert slots.take(64, 9, 48, 82, False) is c  # the oldest wave's slot, not d (in flight)
+    assert slots.take(64, 9, 48, 82, False) is d
+
+
+def test_tree_arena_cache_is_bounded_and_trimmable():
+    """The warm tree arenas a finished Search leaves for the next one are capped and can be
+    released (MapCache kept up to 6 GiB resident for the life of the process)."""
+    s = rg.Search(GameState().native, 2)
+    s.select(8)
+    del s
+    assert 0 < rg.tree_cache_bytes() <= (2560 << 20)
+    assert rg.trim_tree_cache() > 0
+    assert rg.tree_cache_bytes() == 0

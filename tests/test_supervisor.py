@@ -81,7 +81,13 @@ def test_resume_skips_incomplete_checkpoints(tmp_path):
     assert latest_checkpoint(str(d)) == (1, "weights.00001.hdf5")
     meta = {"epochs": [{"loss": 3.0}, {"loss": 2.0}, {"loss": 1.0}], "best_epoch": 2}
     assert resume_epoch_base(meta, {"epoch": 1, "iterations": 5}) == 2
-    assert len(meta["epochs"]) == 2 and meta["best_epoch"] == 0
+    # best_epoch is recomputed from the entries kept (epoch 1's loss 2.0 beats epoch 0's 3.0)
+    assert len(meta["epochs"]) == 2 and meta["best_epoch"] == 1
+    # killed between the checkpoint of epoch 2 and metadata.json: the sidecar's logs restore
+    # the missing entry, so entry i keeps describing weights.<i>.hdf5
+    meta = {"epochs": [{"loss": 3.0}, {"loss": 2.0}], "best_epoch": 1}
+    assert resume_epoch_base(meta, {"epoch": 2, "logs": {"loss": 0.5}}) == 3
+    assert meta["epochs"][2] == {"loss": 0.5} and meta["best_epoch"] == 2
     # RL-style directories (no sidecars at all): newest weights file
     rl = tmp_path / "rl"
     rl.mkdir()

@@ -60,6 +60,31 @@ def test_sharded_generation_merges_rank_slices(tmp_path):
         assert np.array_equal(f["values"][()], np.concatenate([y for _, y in parts]))
 
 
+def test_ranks_sharing_one_seeded_player_rng_play_different_games():
+    """A player built on the caller's seeded stream (as every rank of a torchrun job would build
+    it from the same --seed) must not replay the same games on every rank."""
+    pol = CNNPolicy(["board", "ones", "sensibleness"], board=7, filters_per_layer=8, layers=2,
+                    device="cpu", seed=1)
+    played = []
+    for r in range(2):
+        rng = np.random.RandomState(0)
+        player = ProbabilisticPolicyPlayer(pol, move_limit=40, rng=rng)
+        moves = []
+        get_moves = player.get_moves
+
+        def spy(states, _g=get_moves, _m=moves):
+            out = _g(states)
+            _m.append(list(out))
+            return out
+        player.get_moves = spy
+        X, _ = vt.generate_value_dataset(player, 12, board=7, move_limit=40, rng=rng,
+                                         batch_games=6, rank=r, world=2, native=False)
+        assert X.shape == (6, 49, 7, 7)
+        played.append(moves)
+    assert played[0] and played[1]
+    assert played[0] != played[1]  # the trajectories, not only the sampled snapshots, differ
+
+
 def test_generate_cli_two_ranks(tmp_path):
     """``value_trainer generate`` under torchrun (2 gloo ranks): shards merged by rank 0."""
     import subprocess
@@ -83,3 +108,6 @@ def test_generate_cli_two_ranks(tmp_path):
     with h5lite.File(out) as f:
         assert f["states"].shape == (6, 6, 7, 7)  # board 3 + ones + sensibleness + color
         assert f["values"].shape == (6, 1)
+        X = f["states"][()]
+    # rank 0 holds rows 0-2, rank 1 rows 3-5: per-rank player streams give different games
+    assert not np.array_equal(X[:3], X[3:])
