@@ -34,6 +34,31 @@ def _free_port():
     return p
 
 
+def allreduce_probe(dp, dev, nbytes=15531176, reps=10):
+    """One timed all-reduce of the north-star gradient size (3,882,794 fp32 = 15.5 MB) over the
+    job's process group before the SL phase: the RCCL bandwidth the bucketed gradient all-reduce
+    can get (busbw = 2 (N-1)/N x bytes / time, the ring's per-rank traffic rate)."""
+    import torch
+    import torch.distributed as dist
+    buf = torch.ones(nbytes // 4, dtype=torch.float32, device=dev)
+    for _ in range(2):
+        dist.all_reduce(buf)
+    torch.cuda.synchronize()
+    dp.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dist.all_reduce(buf)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    ok = bool(torch.all(buf == float(dp.world) ** (reps + 2)).item())
+    n = dp.world
+    return {"rccl_ranks": n, "comm_backend": dp.backend,
+            "allreduce_bytes": nbytes, "allreduce_us": round(dt * 1e6, 1),
+            "allreduce_algbw_GBps": round(nbytes / dt / 1e9, 2),
+            "allreduce_busbw_GBps": round(2.0 * (n - 1) / n * nbytes / dt / 1e9, 2),
+            "allreduce_ok": ok}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -88,9 +113,10 @@ def main():
     dp = DPContext(timeout_s=int(args.stall_timeout) + 60)
     dev = dp.device
     wd = RankWatchdog(dp.rank, dp.world, args.stall_timeout, phase="setup") \
-        if dp.world > 1 else None
+        if dp.enabled else None
     if dev.type != "cuda":
         raise SystemExit("bench.py needs a GPU")
+    comm = allreduce_probe(dp, dev) if dp.enabled else None
     torch.manual_seed(1234)
     gen = torch.Generator(device=dev)
     gen.manual_seed(99 + dp.rank)
@@ -229,6 +255,8 @@ def main():
                                     "column BN + ReLU + residual units), %d params" % (
                                         args.filters, args.layers, nparams)
         result["baseline_note"] = "no published baseline for the residual policy"
+    if comm is not None:
+        result.update(comm)
     if wd is not None:
         wd.set_phase("mcts", limit_s=max(args.stall_timeout, args.mcts_guard_s + 30))
     if not args.no_mcts and args.model == "policy":

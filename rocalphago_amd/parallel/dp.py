@@ -12,9 +12,16 @@ as its lowest layer's wgrad has been launched, overlapping communication with th
 backward kernels. Buckets are sized for xGMI ring throughput (a few MB each), not NVSwitch.
 
 CPU runs (tests) use the gloo backend with the same code path.
+
+``RAG_FORCE_PG=1`` initialises the process group even for a single process (WORLD_SIZE = 1, an
+RCCL communicator of one rank on a GPU): every collective of the DP path (bucketed gradient
+all-reduce in fp32 or bf16, broadcasts, barriers, the search's RootExchange, the watchdog's
+c10d store) then runs through the real library on a one-GPU box, where a one-rank all-reduce
+must leave every value unchanged.
 """
 import datetime
 import os
+import socket
 
 import torch
 import torch.distributed as dist
@@ -25,11 +32,30 @@ def env_world():
         int(os.environ.get("LOCAL_RANK", "0"))
 
 
+def force_pg():
+    return os.environ.get("RAG_FORCE_PG", "0") not in ("", "0")
+
+
+def _single_rank_env():
+    """Rendezvous variables for a one-process group (env:// needs them)."""
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if "MASTER_PORT" not in os.environ:
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        os.environ["MASTER_PORT"] = str(s.getsockname()[1])
+        s.close()
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", "1")
+    os.environ.setdefault("LOCAL_RANK", "0")
+
+
 class DPContext(object):
     def __init__(self, device=None, backend=None, timeout_s=600):
         world, rank, local = env_world()
         self.world, self.rank, self.local_rank = world, rank, local
-        self.enabled = world > 1
+        self.enabled = world > 1 or force_pg() or (dist.is_available() and dist.is_initialized())
+        if self.enabled and world == 1 and not dist.is_initialized():
+            _single_rank_env()
         if device is None:
             device = torch.device("cuda", local % max(1, torch.cuda.device_count())) \
                 if torch.cuda.is_available() else torch.device("cpu")
@@ -47,6 +73,10 @@ class DPContext(object):
                                     timeout=datetime.timedelta(seconds=timeout_s), **kw)
         self.is_root = self.rank == 0
         self.backend = dist.get_backend() if self.enabled else None
+        if self.enabled:
+            self.world = dist.get_world_size()
+            self.rank = dist.get_rank()
+            self.is_root = self.rank == 0
 
     def broadcast_(self, t, src=0):
         if self.enabled:

@@ -44,7 +44,7 @@ class RankWatchdog(object):
         self.publish_s = float(publish_s)
         self.phase = phase
         self.step = -1
-        self.store = store if store is not None else (_default_store() if world > 1 else None)
+        self.store = store if store is not None else _default_store()
         self.stream = stream or sys.stderr
         self.on_stall = on_stall  # tests: called with the message instead of exiting
         self.t0 = time.time()

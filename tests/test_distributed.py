@@ -350,3 +350,104 @@ def _rl_pergame_worker(rank, world, port, outdir):
 def test_dp_rl_per_game_rejected(tmp_path):
     _spawn(_rl_pergame_worker, (str(tmp_path),))
     assert np.load(tmp_path / "pg0.npy")[0] == 1 and np.load(tmp_path / "pg1.npy")[0] == 1
+
+
+def test_forced_single_rank_group_cpu(monkeypatch):
+    """RAG_FORCE_PG=1 at WORLD_SIZE=1 (gloo here, RCCL on a GPU box: tests/test_gpu_rccl.py):
+    the DP code paths run real collectives of one rank, which leave values unchanged."""
+    import torch.distributed as dist
+
+    from rocalphago_amd.parallel.dp import BucketedAllReduce, DPContext
+    from rocalphago_amd.parallel.watchdog import RankWatchdog
+    from rocalphago_amd.search.distributed import RootExchange
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("RAG_FORCE_PG", "1")
+    dp = DPContext(device="cpu")
+    try:
+        assert dp.enabled and dp.world == 1 and dp.backend == "gloo"
+        g = torch.randn(1000)
+        ref = g.clone()
+        b = BucketedAllReduce(dp, g, [0, 300, 700], bucket_bytes=256)
+        for layer in (2, 1, 0):
+            b.layer_done(layer)
+        b.finish()
+        assert torch.equal(g, ref)
+        dp.barrier()
+        rx = RootExchange(8, torch.device("cpu"))
+        v = np.arange(8, dtype=np.float32)
+        assert rx.exchange(v) is None
+        tot, own = rx.wait()
+        assert np.array_equal(tot, v) and np.array_equal(own, v)
+        wd = RankWatchdog(0, 1, 60.0, phase="forced", on_stall=lambda m: None)
+        wd.beat(3)
+        wd._publish(force=True)
+        assert wd.heartbeats()[0][:2] == ("forced", 3)
+        wd.stop()
+    finally:
+        dp.shutdown()
+    assert not dist.is_initialized()
+
+
+def _rl_games(n_games=6, board=7, planes=12, seed=0):
+    """Fixed synthetic REINFORCE batch: per game a few positions, moves and an outcome."""
+    rng = np.random.RandomState(seed)
+    feats, moves, won = [], [], []
+    for g in range(n_games):
+        n = 3 + g % 4
+        feats.append([(rng.rand(planes, board, board) < 0.3).astype(np.float32)
+                      for _ in range(n)])
+        moves.append([int(m) for m in rng.randint(0, board * board, n)])
+        won.append(bool(g % 3 != 1))
+    return feats, moves, won
+
+
+def _rl_policy():
+    from rocalphago_amd.models import kerasish as K
+    from rocalphago_amd.models.policy import CNNPolicy
+    from rocalphago_amd.training import reinforcement as rl
+    pol = CNNPolicy(FEATS, board=7, filters_per_layer=8, layers=3, device="cpu", seed=3)
+    opt = K.SGD(lr=0.05)
+    pol.model.compile(loss=rl.log_loss, optimizer=opt)
+    return pol.model, opt
+
+
+def _rl_sym_worker(rank, world, port, outdir):
+    """Each rank updates on its shard (games rank::world) of the fixed batch, once with the
+    outcomes as given and once with every outcome flipped, from the same initial weights."""
+    _setup(rank, world, port)
+    from rocalphago_amd.parallel.dp import DPContext
+    from rocalphago_amd.training import reinforcement as rl
+    dp = DPContext(device="cpu")
+    feats, moves, won = _rl_games()
+    mine = list(range(rank, len(won), world))
+    for tag, flip in (("w", False), ("l", True)):
+        model, opt = _rl_policy()
+        init = model.net.flat.detach().clone()
+        rl._batched_update(model, opt, [feats[i] for i in mine], [moves[i] for i in mine],
+                           [won[i] != flip for i in mine], 49, dp)
+        np.save(os.path.join(outdir, "d%s%d.npy" % (tag, rank)),
+                (model.net.flat.detach() - init).numpy())
+    dp.shutdown()
+
+
+@pytest.mark.timeout(300)
+def test_dp_rl_update_symmetry_and_union(tmp_path):
+    """Cross-rank version of the reference's gradient-symmetry check
+    (/root/reference/tests/test_reinforcement_policy_trainer.py:82-126):
+    the all-reduced batched REINFORCE update over 2 ranks equals the single-process batched
+    update on the union of the games, and flipping every win/loss gives the equal and opposite
+    weight change."""
+    from rocalphago_amd.training import reinforcement as rl
+    _spawn(_rl_sym_worker, (str(tmp_path),))
+    dw0, dw1 = np.load(tmp_path / "dw0.npy"), np.load(tmp_path / "dw1.npy")
+    dl0, dl1 = np.load(tmp_path / "dl0.npy"), np.load(tmp_path / "dl1.npy")
+    assert np.array_equal(dw0, dw1) and np.array_equal(dl0, dl1), "replicas diverged"
+    feats, moves, won = _rl_games()
+    model, opt = _rl_policy()
+    init = model.net.flat.detach().clone()
+    rl._batched_update(model, opt, feats, moves, won, 49, None)
+    single = (model.net.flat.detach() - init).numpy()
+    assert np.abs(single).max() > 0
+    assert np.linalg.norm(dw0 - single) <= 1e-5 * np.linalg.norm(single)
+    np.testing.assert_allclose(dl0, -dw0, rtol=1e-3, atol=1e-7 * np.abs(dw0).max())
