@@ -76,6 +76,10 @@ def main():
     ap.add_argument("--no-mcts", action="store_true",
                     help="skip the APV-MCTS sims/s measurement (run after the timed SL steps)")
     ap.add_argument("--mcts-playouts", type=int, default=8192)
+    ap.add_argument("--mcts-mode", default="master", choices=["master", "shared"],
+                    help="N>1 search: one tree on rank 0 with leaf waves on every GPU (master), "
+                         "or N trees with shared root statistics (shared; measured 1/N budget "
+                         "efficiency, kept for comparison)")
     ap.add_argument("--mcts-guard-s", type=int, default=180,
                     help="N>1: wall-clock limit of the multi-GPU search measurement")
     ap.add_argument("--trace", default=None,
@@ -282,8 +286,14 @@ def main():
             guard.start()
         try:
             if dp.world > 1:
-                from benchmarks.mcts_bench import measure_distributed
-                r = measure_distributed(dp, dev, playouts=args.mcts_playouts * dp.world)
+                # ONE tree (rank 0) whose rounds keep the one-GPU search's leaves in flight,
+                # evaluated on all N GPUs: every simulation is a distinct node of one search
+                # (search/efficiency.py: budget efficiency 1.0 at N = 2, 4, 8, where N trees with
+                # shared root statistics measured 1/N; profiles/search_efficiency_r4.json)
+                from benchmarks.mcts_bench import distributed_wave, measure_distributed
+                r = measure_distributed(dp, dev, playouts=args.mcts_playouts * dp.world,
+                                        mode=args.mcts_mode,
+                                        batch=distributed_wave(dp.world, args.mcts_mode))
                 r = r or {"sims_per_s": 0.0, "rollouts_per_s": 0.0}
             else:
                 from benchmarks.mcts_bench import measure
@@ -312,10 +322,17 @@ def main():
                                         r["rollouts_per_leaf"] if "rollouts_per_leaf" in r
                                         else 1, r.get("batch", 512),
                                         args.mcts_playouts * dp.world,
-                                        "one search over %d GPUs" % dp.world if dp.world > 1
+                                        "one tree over %d GPUs" % dp.world if dp.world > 1
                                         else "1 GPU")
             if dp.is_root and "leaves_per_rank" in r:
                 result["mcts_leaves_per_rank"] = r["leaves_per_rank"]
+            if dp.is_root and dp.world > 1:
+                # over-crediting guard: simulations of one tree are all distinct; with N
+                # independent trees (mode shared) the duplicated expansions are measured live
+                dup = float(r.get("duplication", 1.0))
+                result["mcts_mode"] = r.get("mode", args.mcts_mode)
+                result["mcts_tree_duplication"] = round(dup, 3)
+                result["mcts_unique_sims_per_s"] = round(float(tot[0]) / max(dup, 1.0), 1)
         else:
             result["mcts_error"] = err or "MCTS measurement failed on %d rank(s)" % (
                 dp.world - int(tot[2]))

@@ -62,12 +62,24 @@ def measure(device, playouts=8192, warmup=512, moves=1, **kw):
     return out
 
 
+def distributed_wave(world, mode="master"):
+    """Leaves per rank and round of the N-GPU search. master: the round (N waves) keeps about
+    the one-GPU search's leaves in flight (512-leaf waves) -- N x 512 per round would search
+    like one tree with N-times-wider waves (budget efficiency 0.24 at N = 8 in
+    search/efficiency.py's study, 1.0 with the split) -- but at least 128 leaves per GPU pass.
+    shared: every rank runs the one-GPU search."""
+    if mode != "master" or world <= 1:
+        return 512
+    return max(128, 512 // world)
+
+
 def measure_distributed(dp, device, playouts=8192, warmup=512, moves=1, filters=192,
                         layers=12, batch=512, rollouts_per_leaf=1, lmbda=0.5, nthreads=16,
-                        seed=1, rollout_delay=6, mode="shared"):
-    """One search over all ranks (search/distributed.py). mode "shared" (default): every rank
-    runs the pipelined single-GPU search with shared root statistics (SharedRootMCTS);
-    "master": one tree on rank 0 with leaf waves dealt to all ranks (DistributedMCTS).
+                        seed=1, rollout_delay=6, mode="master"):
+    """Search over all ranks (search/distributed.py). mode "master" (default): one tree on rank 0
+    with leaf waves dealt to all ranks (DistributedMCTS); "shared": every rank runs the pipelined
+    single-GPU search with shared root statistics (SharedRootMCTS; its duplicated expansions
+    are measured and reported).
     Collective: every rank calls it; rank 0's dict has the job's sims/s, the others None."""
     if mode == "shared":
         return _measure_shared(dp, device, playouts, warmup, moves, filters, layers, batch,
@@ -106,7 +118,8 @@ def measure_distributed(dp, device, playouts=8192, warmup=512, moves=1, filters=
     s = mc.stats
     out = {"sims_per_s": s["sims"] / dt, "sims": s["sims"], "seconds": dt, "waves": s["waves"],
            "batch": batch, "rollouts_per_leaf": rollouts_per_leaf, "rollout_device": "gpu",
-           "gpus": dp.world, "leaves_per_rank": [int(c) for c in counts]}
+           "gpus": dp.world, "leaves_per_rank": [int(c) for c in counts],
+           "mode": "master", "duplication": 1.0, "leaves_per_round": batch * dp.world}
     if lmbda > 0:
         out["rollouts_per_s"] = s["sims"] * rollouts_per_leaf / dt
     for k in ("t_select", "t_eval", "t_backup"):
@@ -147,6 +160,16 @@ def _measure_shared(dp, device, playouts, warmup, moves, filters, layers, batch,
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     s = mc.stats
+    # duplication of the ranks' trees (same move-path = same node): all expanded nodes over the
+    # distinct ones, on the trees of the last move's search
+    keys = mc._search.expanded_keys() if mc._search is not None else []
+    dup = 1.0
+    if dp.world > 1:
+        import torch.distributed as dist
+        allk = [None] * dp.world
+        dist.all_gather_object(allk, [int(k) for k in keys])
+        flat = [k for ks in allk for k in ks]
+        dup = len(flat) / max(1, len(set(flat)))
     t = torch.tensor([float(s["sims"]), dt, float(mc.exchanges)], dtype=torch.float64,
                      device=device if dp.backend != "gloo" else "cpu")
     if dp.world > 1:
@@ -162,7 +185,8 @@ def _measure_shared(dp, device, playouts, warmup, moves, filters, layers, batch,
     dtm = max(p[1] for p in per)
     out = {"sims_per_s": tot / dtm, "sims": int(tot), "seconds": dtm, "batch": batch,
            "rollouts_per_leaf": rollouts_per_leaf, "rollout_device": mc.rollout_device,
-           "gpus": dp.world, "mode": "shared-root", "leaves_per_rank": [int(p[0]) for p in per],
+           "gpus": dp.world, "mode": "shared", "duplication": round(dup, 3),
+           "leaves_per_rank": [int(p[0]) for p in per],
            "root_exchanges_per_rank": [int(p[2]) for p in per]}
     if lmbda > 0:
         out["rollouts_per_s"] = tot * rollouts_per_leaf / dtm
@@ -195,14 +219,16 @@ def main():
                     help="--distributed: rounds a wave's rollouts may stay in flight")
     ap.add_argument("--distributed", action="store_true",
                     help="one search over all torchrun ranks (search/distributed.py)")
-    ap.add_argument("--mode", default="shared", choices=["shared", "master"],
-                    help="--distributed: shared root statistics (default) or rank-0 master")
+    ap.add_argument("--mode", default="master", choices=["shared", "master"],
+                    help="--distributed: one tree on rank 0 (default) or shared root statistics")
     args = ap.parse_args()
     import torch
     if args.distributed:
         from rocalphago_amd.parallel.dp import DPContext
         dp = DPContext()
-        r = measure_distributed(dp, dp.device, playouts=args.playouts, batch=args.batch,
+        r = measure_distributed(dp, dp.device, playouts=args.playouts,
+                                batch=distributed_wave(dp.world, args.mode)
+                                if args.batch == 512 else args.batch,
                                 moves=args.moves, rollouts_per_leaf=args.rollouts_per_leaf,
                                 lmbda=args.lmbda, filters=args.filters, nthreads=args.threads,
                                 rollout_delay=args.rollout_delay, mode=args.mode)

@@ -764,8 +764,11 @@ constexpr int kPPSlabRows192x5 = 448;    // 192-pixel blocks, 5x5 taps (<= 424 r
 // bn.hip's finalize): (sum, sum of squares) of the stored output in the forward, or with smean
 // (the BN's mean) (sum dU, sum dU * (x - mean)) of the masked dgrad output, x = `mask`. They
 // replace the separate statistics passes over the activation.
+// SPREAD: the loader group issues the next chunk's slab loads a few per step over taps
+// 0 .. TAPS-2 instead of all of them at tap 0 (the tap-0 read phase otherwise carries ~10 DMA
+// issues and holds the partner group at the next barrier).
 template <int NB, int DIAG = 0, int ISSUE = 0, int NT = kNT, bool BNP = false, int KS = 3,
-          int MT = kMT>
+          int MT = kMT, int SPREAD = 0>
 __global__ void __launch_bounds__(512, MT == kMT ? 1 : 4)
 conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                    const float* __restrict__ bias, bf16* __restrict__ Y,
@@ -867,10 +870,11 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
     const int r = (wl + 4 * k) * 16 + lrow;
     bsrc[k] = Wt + (long)(n0 + r) * CIN + ((lcol ^ swz4(r)) * 8);
   }
-  auto stage_a = [&](int q) {  // slab of chunk q: rows (wl + 4k)*16 .. +15 per glds
+  auto stage_a = [&](int q, int k0 = 0, int k1 = 1 << 20) {  // chunk q, pieces k0 .. k1-1
     bf16* dst = lds + (q & 1) * SLAB;
 #pragma unroll
     for (int k = 0; k < AL; ++k) {
+      if (k < k0 || k >= k1) continue;
       const int r = (wl + 4 * k) * 16 + lrow;
       long g = base + r;
       g = g < total_rows ? g : total_rows - 1;
@@ -991,7 +995,13 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
       asm volatile("" ::: "memory");
       const long long c2 = now();
       if constexpr (!(DIAG & 1)) {
-        if (t == 0 && more) stage_a(q + 1);
+        if constexpr (SPREAD && !BNP) {
+          // pieces [t*AL/(TAPS-1), (t+1)*AL/(TAPS-1)) at taps 0 .. TAPS-2; all retired by the
+          // wait after the last tap's MFMAs, as before
+          if (t < TAPS - 1 && more) stage_a(q + 1, t * AL / (TAPS - 1), (t + 1) * AL / (TAPS - 1));
+        } else {
+          if (t == 0 && more) stage_a(q + 1);
+        }
       }
       read_frags(s);
       const long long c3 = now();
@@ -1233,7 +1243,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
       const char* v = getenv("RAG_CONV_PP5");
       return !(v && v[0] == '0');
     }();
-    if (!pp5 || bnc || mcoef || spart || g_tap_mode < 5 || g_tap_mode > 9) return false;
+    if (!pp5 || bnc || mcoef || spart || g_tap_mode < 5 || g_tap_mode > 10) return false;
     if (nconv < pmin) {
       // sub-chip grids (128-game self-play passes): 192-pixel blocks, as the 3x3 layers
       static int key5b = -1, rows5b = 0;
@@ -1261,7 +1271,11 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
       r = *red;
       nred = std::max(8, (256 - nconv % 256) % 256);
     }
-    if (w192)
+    if (w192 && g_tap_mode == 10)
+      conv_tap_pp_kernel<3, 0, 0, 6, false, 5, kMT, 1><<<nconv + nred, 512, 0, stream>>>(
+          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
+          nconv, r);
+    else if (w192)
       conv_tap_pp_kernel<3, 0, 0, 6, false, 5><<<nconv + nred, 512, 0, stream>>>(
           x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
           nconv, r);
@@ -1298,7 +1312,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
   }();
   if (w128) {
     const int nconv = ((M + kPPBM - 1) / kPPBM) * (COUTP / 128);
-    if (g_tap_mode < 5 || g_tap_mode > 9 || cached_rows8 > kPPSlabRows || nconv < pp_min)
+    if (g_tap_mode < 5 || g_tap_mode > 10 || cached_rows8 > kPPSlabRows || nconv < pp_min)
       return false;  // small batches: conv_pipe
     int nred = 0;
     WgradRed r{};
@@ -1321,7 +1335,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
     const char* v = getenv("RAG_CONV_PP192");
     return v && v[0] == '2';
   }();
-  if ((g_tap_mode >= 5 && g_tap_mode <= 9) && cached_rows8 <= kPPSlabRows && pp_fills &&
+  if ((g_tap_mode >= 5 && g_tap_mode <= 10) && cached_rows8 <= kPPSlabRows && pp_fills &&
       !pp192_all) {
     // ping-pong kernel: one block per CU; reduce blocks fill the CUs its last round leaves free
     const int nconv = ((M + kPPBM - 1) / kPPBM) * (COUTP / kBN);
@@ -1347,6 +1361,10 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
       conv_tap_pp_kernel<4, 0, 1><<<nconv + nred, 512, 0, stream>>>(
           x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
           nconv, r);
+    else if (g_tap_mode == 10)
+      conv_tap_pp_kernel<3, 0, 0, kNT, false, 3, kMT, 1><<<nconv + nred, 512, 0, stream>>>(
+          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
+          nconv, r);
     else
       conv_tap_pp_kernel<3><<<nconv + nred, 512, 0, stream>>>(
           x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
@@ -1362,7 +1380,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
     return !(v && v[0] == '0');
   }();
   const int n192 = ((M + kBM - 1) / kBM) * (COUTP / kBN);
-  if (pp192 && g_tap_mode >= 5 && g_tap_mode <= 9 && n192 >= pp_min &&
+  if (pp192 && g_tap_mode >= 5 && g_tap_mode <= 10 && n192 >= pp_min &&
       cached_rows <= kPPSlabRows192) {
     int nred = 0;
     WgradRed r{};
@@ -1411,7 +1429,7 @@ bool rag_conv_tap_bn_ok(int M, int S, int WI, int shift, int CIN, int COUTP, int
   const char* e = getenv("RAG_PP_MIN_BLOCKS");
   const int pp_min = e ? atoi(e) : 200;
   const int nconv = ((M + kPPBM - 1) / kPPBM) * (COUTP / 128);
-  return g_tap_mode >= 5 && g_tap_mode <= 9 && KS == 3 && COUTP % kBN != 0 && COUTP % 128 == 0 &&
+  return g_tap_mode >= 5 && g_tap_mode <= 10 && KS == 3 && COUTP % kBN != 0 && COUTP % 128 == 0 &&
          CIN % kBK == 0 && CIN >= kBK && nconv >= pp_min &&
          max_slab_rows(S, WI, shift, kPPBM) <= kPPSlabRows;
 }

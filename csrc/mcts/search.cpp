@@ -113,6 +113,13 @@ void register_search(py::module_& m) {
       .def("finish_rollouts", &Search::finish_rollouts, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("pending_waves", &Search::pending_waves)
       .def("best_move", &Search::best_move)
+      .def("expanded_keys",
+           [](const Search& s) {
+             const auto k = s.expanded_keys();
+             py::array_t<uint64_t> a(k.size());
+             std::copy(k.begin(), k.end(), a.mutable_data());
+             return a;
+           })
       .def("root_stats",
            [](const Search& s) {
              std::vector<int32_t> mv, vis;

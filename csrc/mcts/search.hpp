@@ -808,6 +808,30 @@ class Search {
     return E[best].move;
   }
 
+  // One 64-bit key per expanded node: a hash of its move path from the root (the same node of
+  // two trees of the same root gets the same key). Used to measure how much of the work of
+  // several ranks' trees is the same tree expanded twice (search/efficiency.py).
+  std::vector<uint64_t> expanded_keys() const {
+    std::vector<uint64_t> out;
+    std::vector<std::pair<int32_t, uint64_t>> st{{root_, 0x243F6A8885A308D3ull}};
+    while (!st.empty()) {
+      const auto [i, h] = st.back();
+      st.pop_back();
+      const Node& nd = (*nodes_)[i];
+      if (nd.state != N_EXPANDED) continue;
+      out.push_back(h);
+      const Edge* E = &(*edges_)[nd.edges];
+      for (int k = 0; k < nd.nedge; ++k) {
+        if (E[k].child < 0) continue;
+        uint64_t x = h ^ (uint64_t(uint16_t(E[k].move)) + 0x9E3779B97F4A7C15ull);
+        x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+        x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+        st.push_back({E[k].child, x ^ (x >> 31)});
+      }
+    }
+    return out;
+  }
+
   // (moves, visits, Q, prior) of the root's children, in increasing point order (pass last)
   void root_stats(std::vector<int32_t>& mv, std::vector<int32_t>& vis, std::vector<float>& q,
                   std::vector<float>& pr) const {

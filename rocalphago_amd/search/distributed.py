@@ -1,17 +1,22 @@
 """APV-MCTS on several GPUs (the reference's ParallelMCTS is an empty stub,
 AlphaGo/mcts.py:219-220). One process per GPU, torch.distributed "nccl" = RCCL between them
-(gloo in the CPU tests). Two designs:
+(gloo in the CPU tests). Two designs, compared by search/efficiency.py (one tree with the same
+total budget as the yardstick; profiles/search_efficiency_r4.json):
 
-SharedRootMCTS (default; ``benchmarks/mcts_bench.py --distributed``) — every rank runs the full
-single-GPU pipelined search (its own native tree, its own host threads, its own GPU) on the same
-position, and after every wave the ranks all-reduce the statistics their trees added at the
-root's children (4 x 362 floats, asynchronous, one wave of lag). Each rank mixes the other ranks'
-totals into its root selection (Search.set_root_external), so the job explores the root as one
-search — the "root parallelisation with shared root statistics" family of parallel MCTS — while
-everything below the root stays rank-local. No host funnels the job: the r2 master design below
-needs rank 0 to select, pack and back up every leaf of every GPU, whose null-evaluator ceiling
-(benchmarks/mcts_null_bench.py) is below 8x one GPU's rate. The move is the most visited root
-child over all ranks (one final all-reduce of visit counts), identical on every rank.
+DistributedMCTS (default since round 4: ``bench.py --gpus N``, ``benchmarks/mcts_bench.py
+--distributed``) is ONE search: one tree on rank 0, each round's leaves evaluated on all GPUs
+(below). With the one-GPU search's leaves in flight per round (N waves of 512 / N, at least 128)
+its budget efficiency is 1.0 at N = 2, 4, 8 and no node is expanded twice; its rate is bounded by
+rank 0's host tree work (select + pack + backup, ~2.2 us per simulation:
+benchmarks/mcts_null_bench.py), not by N.
+
+SharedRootMCTS (``mode="shared"``) — every rank runs the full single-GPU pipelined search on the
+same position and the ranks all-reduce the statistics their trees added at the root's children
+after every wave (4 x 362 floats, one wave of lag), mixed into each rank's root selection
+(Search.set_root_external). Measured: the N trees expand the same nodes (duplication N with a
+deterministic evaluator) and the job searches like ONE rank (efficiency 1/N), so its N-fold
+simulations/s over-credit the search; the bench reports its live duplication. Kept for
+comparison.
 
 DistributedMCTS (``mode="master"``) — one tree on rank 0, leaf evaluation spread over all ranks:
 
@@ -58,19 +63,24 @@ class LeafCodec(object):
     superko-illegal [P] uint8 | ladder planes [2, P] uint8 (the last two only meaningful when the
     wave's boards enforce superko)."""
 
-    def __init__(self, S):
+    def __init__(self, S, superko=True):
         self.S = S
         P = self.P = S * S
         self.o_age = P
         self.o_meta = 3 * P
         self.o_ill = 3 * P + 32
         self.o_lad = 4 * P + 32
-        self.L = (6 * P + 32 + 7) // 8 * 8
+        # without positional superko the leaves' ladder planes are read by the evaluating rank
+        # and there is no illegal mask: the record stops after the meta words (half the bytes)
+        self.superko = bool(superko)
+        self.L = (6 * P + 32 + 7) // 8 * 8 if superko else (3 * P + 32 + 7) // 8 * 8
 
     def pack(self, search, wid, nthreads):
         boards = search.leaf_boards(wid)
         _, meta8 = search.rollout_inputs(wid)
         superko = boards[0].enforce_superko
+        if superko and not self.superko:
+            raise ValueError("a superko wave needs LeafCodec(S, superko=True)")
         colors, ages, _, illegal, lad = _rg.gpu_feature_inputs(boards, superko, nthreads)
         n, P = len(boards), self.P
         rec = np.zeros((n, self.L), np.uint8)
@@ -88,6 +98,8 @@ class LeafCodec(object):
         colors = np.ascontiguousarray(rec[:, :P]).view(np.int8)
         ages = np.ascontiguousarray(rec[:, self.o_age:self.o_meta]).view(np.int16)
         meta8 = np.ascontiguousarray(rec[:, self.o_meta:self.o_ill]).view(np.int32)
+        if not self.superko:
+            return colors, ages, meta8, None, None
         illegal = np.ascontiguousarray(rec[:, self.o_ill:self.o_lad])
         lad = np.ascontiguousarray(rec[:, self.o_lad:self.o_lad + 2 * P]).reshape(-1, 2, P)
         return colors, ages, meta8, illegal, lad
@@ -251,17 +263,25 @@ class DistributedMCTS(ParallelMCTS):
         n = int(counts[self.rank])
         if int(np.sum(counts)) == 0:  # an empty round only carries rollout results back
             return (rnd, 0, None, codec)
+        mine = None
         if self.world > 1:
-            payload = torch.zeros((self.world, B, codec.L), dtype=torch.uint8,
-                                  device=self.device)
+            # each rank receives only its own wave's records (scatter, not a broadcast of all)
+            buf = torch.zeros((B, codec.L), dtype=torch.uint8, device=self.device)
             if self.rank == 0:
+                parts = []
                 for r, rec in enumerate(recs):
+                    t = torch.zeros((B, codec.L), dtype=torch.uint8)
                     if rec is not None and len(rec):
-                        payload[r, :len(rec)] = torch.from_numpy(rec).to(self.device)
-            self._bcast(payload)
+                        t[:len(rec)] = torch.from_numpy(rec)
+                    parts.append(t.to(self.device, non_blocking=False))
+                dist.scatter(buf, scatter_list=parts, src=0)
+            else:
+                dist.scatter(buf, src=0)
+            if n:
+                mine = recs[0] if self.rank == 0 else buf[:n].cpu().numpy()
         handle = None
         if n:
-            mine = payload[self.rank, :n].cpu().numpy() if self.world > 1 else recs[0]
+            mine = mine if mine is not None else recs[0]
             seed = (self.seed * 7919 + rnd * 131 + self.rank) & 0x7FFFFFFF
             handle, pend = self.leaf_eval.submit(codec, mine, superko, komi, seed)
             if pend is not None:
@@ -327,7 +347,7 @@ class DistributedMCTS(ParallelMCTS):
         evaluates round k, then collects and backs up round k (virtual loss keeps the two rounds'
         leaves apart, as in the single-GPU pipeline)."""
         s = self._sync_root(state)
-        codec = LeafCodec(state.size)
+        codec = LeafCodec(state.size, bool(s.root_board.enforce_superko))
         target = s.root_visits + (n_playout or self.n_playout)
         waves = {}  # (round, rank) -> wave id still waiting for its rollout results
         inflight = None  # (shipped, counts, wids) of the round not collected yet
@@ -439,7 +459,8 @@ class DistributedMCTS(ParallelMCTS):
                 self._collect(inflight)
                 inflight = None
                 continue
-            shipped = self._ship(LeafCodec(int(h[5])), None, h[HDR:], int(h[3]), h[4] / 2.0)
+            shipped = self._ship(LeafCodec(int(h[5]), bool(h[3])), None, h[HDR:], int(h[3]),
+                                 h[4] / 2.0)
             if int(h[6]):
                 self._collect(inflight)
             inflight = shipped
