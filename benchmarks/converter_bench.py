@@ -42,7 +42,7 @@ def _synthetic_games(d, n):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--copies", type=int, default=40)
-    ap.add_argument("--threads", default="1,4,16")
+    ap.add_argument("--threads", default="1,4,8,16")
     ap.add_argument("--sgf-dir", default=REF)
     args = ap.parse_args()
     d = tempfile.mkdtemp()

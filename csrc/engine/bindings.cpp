@@ -302,7 +302,7 @@ PYBIND11_MODULE(_rocgo, m) {
       "convert_games",
       [](const std::vector<py::bytes>& texts, const std::vector<int>& fids, int bd_size,
          py::array_t<uint64_t, py::array::c_style> zw, py::array_t<uint64_t, py::array::c_style> zb,
-         int nthreads) {
+         int nthreads, int chunk_rows, int lead) -> py::tuple {
         auto zob = make_zobrist(zw, zb);
         const int n = (int)texts.size();
         std::vector<std::string> buf(n);
@@ -325,12 +325,21 @@ PYBIND11_MODULE(_rocgo, m) {
           });
         }
         const int F = total_planes(fids), P = bd_size * bd_size;
+        const size_t row_bytes = (size_t)F * P;
         std::vector<int64_t> off(n + 1, 0);
         for (int i = 0; i < n; ++i) off[i + 1] = off[i] + rp[i];
-        const py::ssize_t total = (py::ssize_t)off[n];
-        py::array_t<uint8_t> sa({total, (py::ssize_t)F, (py::ssize_t)bd_size,
+        const int64_t total = off[n];
+        // chunk_rows > 0 (the HDF5 writer's fused path): rows [lead, lead + k * chunk_rows) are
+        // never materialised -- each whole chunk is extracted into a thread-local buffer and
+        // LZF-compressed while it is cache-hot; only the `lead` rows that complete the writer's
+        // pending chunk and the tail after the last whole chunk come back as planes
+        const int64_t L = chunk_rows > 0 ? std::min<int64_t>(std::max(lead, 0), total) : total;
+        const int64_t nfull = chunk_rows > 0 ? (total - L) / chunk_rows : 0;
+        const int64_t T = total - L - nfull * (int64_t)std::max(chunk_rows, 0);
+        const int64_t kept = L + T;
+        py::array_t<uint8_t> sa({(py::ssize_t)kept, (py::ssize_t)F, (py::ssize_t)bd_size,
                                  (py::ssize_t)bd_size});
-        py::array_t<uint8_t> aa({total, (py::ssize_t)2});
+        py::array_t<uint8_t> aa({(py::ssize_t)total, (py::ssize_t)2});
         uint8_t* sd = sa.mutable_data();
         uint8_t* ad = aa.mutable_data();
         for (int i = 0; i < n; ++i)
@@ -338,19 +347,47 @@ PYBIND11_MODULE(_rocgo, m) {
         std::vector<int> game_of((size_t)total);
         for (int i = 0; i < n; ++i)
           for (int64_t r = off[i]; r < off[i + 1]; ++r) game_of[(size_t)r] = i;
-        {  // 2: the planes of every position of the batch, straight into the output block
+        const int nf = (int)fids.size();
+        auto extract_row = [&](int64_t r, uint8_t* dst) {
+          const int g = game_of[(size_t)r];
+          extract_features(bd[g][(size_t)(r - off[g])], fids.data(), nf, dst);
+        };
+        std::vector<std::string> comp((size_t)nfull);
+        std::vector<uint8_t> ok((size_t)nfull, 0);
+        {  // 2: planes of every position (compressed whole chunks first: the larger tasks)
           py::gil_scoped_release nogil;
-          const int nf = (int)fids.size();
-          parallel_for((int)total, nthreads, [&](int r) {
-            const int g = game_of[(size_t)r];
-            extract_features(bd[g][(size_t)(r - off[g])], fids.data(), nf,
-                             sd + (size_t)r * F * P);
+          const size_t cbytes = (size_t)std::max(chunk_rows, 0) * row_bytes;
+          parallel_for((int)(nfull + kept), nthreads, [&](int t) {
+            if (t < nfull) {
+              thread_local std::vector<uint8_t> tmp;
+              tmp.resize(cbytes);
+              const int64_t r0 = L + (int64_t)t * chunk_rows;
+              for (int k = 0; k < chunk_rows; ++k) extract_row(r0 + k, tmp.data() + k * row_bytes);
+              std::string& o = comp[(size_t)t];
+              o.resize(cbytes + 64);
+              size_t len = lzf_compress(tmp.data(), cbytes, (uint8_t*)&o[0], cbytes);
+              if (len) {
+                o.resize(len);
+                ok[(size_t)t] = 1;
+              } else {  // incompressible: the raw chunk (stored with the filter skipped)
+                o.assign((const char*)tmp.data(), cbytes);
+              }
+              return;
+            }
+            const int64_t k = t - nfull;  // kept row: lead rows, then the tail
+            const int64_t r = k < L ? k : L + nfull * chunk_rows + (k - L);
+            extract_row(r, sd + (size_t)k * row_bytes);
           });
         }
-        return py::make_tuple(status, rows, sa, aa);
+        if (chunk_rows <= 0) return py::make_tuple(status, rows, sa, aa);
+        py::list chunks;
+        for (int64_t t = 0; t < nfull; ++t)
+          chunks.append(py::make_tuple(py::bytes(comp[(size_t)t]), (bool)ok[(size_t)t]));
+        return py::make_tuple(status, rows, sa, aa, chunks, (py::ssize_t)L);
       },
       py::arg("texts"), py::arg("fids"), py::arg("bd_size"), py::arg("zobrist_white"),
-      py::arg("zobrist_black"), py::arg("nthreads") = 8);
+      py::arg("zobrist_black"), py::arg("nthreads") = 8, py::arg("chunk_rows") = 0,
+      py::arg("lead") = 0);
 
   // Leaf boards rebuilt from shipped arrays (distributed search workers; Board::from_arrays).
   m.def(

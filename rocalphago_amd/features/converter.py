@@ -31,6 +31,7 @@ from .preprocessing import DEFAULT_FEATURES, Preprocess
 
 _rg = _engine()
 _NATIVE_OK, _NATIVE_ILLEGAL = 0, 1
+_CHUNK = 64  # rows per states chunk (the layout contract)
 
 
 class SizeMismatchError(Exception):
@@ -71,7 +72,7 @@ class _Sink(object):
         shp = (n_planes, size, size)
         self.states = self.f.require_dataset(
             "states", dtype=np.uint8, shape=(0,) + shp, maxshape=(None,) + shp, exact=False,
-            chunks=(64,) + shp, compression="lzf")
+            chunks=(_CHUNK,) + shp, compression="lzf")
         self.actions = self.f.require_dataset(
             "actions", dtype=np.uint8, shape=(0, 2), maxshape=(None, 2), exact=False,
             chunks=(1024, 2), compression="lzf")
@@ -80,16 +81,25 @@ class _Sink(object):
         self.rows = 0
         self._queue = []
 
-    def add(self, file_name, states, actions):
-        """Queue one game's rows (written by flush(), in order)."""
+    def add(self, file_name, states, actions, rows_only=False):
+        """Queue one game's rows (written by flush(), in order). rows_only: the states come
+        with the batch's fused chunks (flush_fused); only the actions are queued."""
         n = len(actions)
         if n == 0:
             return 0
-        self._queue.append((np.asarray(states, dtype=np.uint8),
-                            np.asarray(actions, dtype=np.uint8).reshape(n, 2)))
+        st = None if rows_only else np.asarray(states, dtype=np.uint8)
+        self._queue.append((st, np.asarray(actions, dtype=np.uint8).reshape(n, 2)))
         self.offsets[file_name.replace("/", ":")] = np.array([self.rows, n], dtype=np.int64)
         self.rows += n
         return n
+
+    def flush_fused(self, lead, chunks, tail):
+        """Append a batch converted on the fused path: its actions, then its states as the
+        lead rows + precompressed whole chunks + tail rows."""
+        if self._queue:
+            self.actions.append(_join([q[1] for q in self._queue]))
+            self._queue = []
+        self.states.append_chunks(lead, chunks, tail)
 
     def flush(self):
         """Append the queued games as one block: whole 64-row chunks compress in parallel. Rows
@@ -142,11 +152,17 @@ class GameConverter(object):
         return planes, moves, None
 
     # ---- bulk conversion ----------------------------------------------------------------------
-    def _batch(self, names, bd_size, nthreads):
+    def _batch(self, names, bd_size, nthreads, lead=None):
         """Per game of a batch: (states array or list, actions, error or None). ``nthreads``
-        0 converts every game with the Python replay (the reference's path; benchmarks)."""
+        0 converts every game with the Python replay (the reference's path; benchmarks).
+
+        ``lead`` (the rows the writer's pending chunk still needs): the fused path -- the
+        native converter LZF-compresses every whole 64-row chunk of the batch while it is
+        cache-hot and returns only the lead and tail rows as planes. Returns (games, fused)
+        with fused = (lead rows, [(bytes, compressed)], tail rows) or None when a game of the
+        batch took the Python replay (its rows then go through the unfused path)."""
         if nthreads == 0:
-            return [self._python_game(name, bd_size) for name in names]
+            return [self._python_game(name, bd_size) for name in names], None
         texts, native_idx = [], []
         for i, name in enumerate(names):
             try:
@@ -157,15 +173,29 @@ class GameConverter(object):
                 continue
             texts.append(raw)
             native_idx.append(i)
+        fuse = lead is not None and len(native_idx) == len(names)
         done = [None] * len(names)
+        fused = None
         if texts:
             zw, zb, _ = go._zobrist(bd_size)
-            status, rows, block, acts = _rg.convert_games(
-                texts, list(self.feature_processor.feature_ids), bd_size,
-                np.ascontiguousarray(zw.ravel()), np.ascontiguousarray(zb.ravel()), nthreads)
+            args = (texts, list(self.feature_processor.feature_ids), bd_size,
+                    np.ascontiguousarray(zw.ravel()), np.ascontiguousarray(zb.ravel()),
+                    nthreads)
+            if fuse:
+                status, rows, block, acts, chunks, L = _rg.convert_games(
+                    *args, chunk_rows=_CHUNK, lead=int(lead))
+                if any(c not in (_NATIVE_OK, _NATIVE_ILLEGAL) and n
+                       for c, n in zip(status.tolist(), rows.tolist())):
+                    # rows of a game the writer will not keep sit inside the chunks: unfused
+                    return self._batch(names, bd_size, nthreads, None)
+                fused = (block[:L], chunks, block[L:])
+                block = None
+            else:
+                status, rows, block, acts = _rg.convert_games(*args)
             at = 0
             for i, code, n in zip(native_idx, status.tolist(), rows.tolist()):
-                st, ac = block[at:at + n], acts[at:at + n]
+                st = block[at:at + n] if block is not None else n
+                ac = acts[at:at + n]
                 at += n
                 if code == _NATIVE_OK:
                     done[i] = (st, ac, None)
@@ -174,43 +204,59 @@ class GameConverter(object):
         for i, name in enumerate(names):
             if done[i] is None:
                 done[i] = self._python_game(name, bd_size)
-        return done
+                if fused is not None and len(done[i][1]):
+                    # a game the native parser rejected but the replay converts: its rows
+                    # belong between the batch's native rows -- redo the batch unfused
+                    return self._batch(names, bd_size, nthreads, None)
+        return done, fused
 
     def sgfs_to_hdf5(self, sgf_files, hdf5_file, bd_size=19, ignore_errors=True, verbose=False,
-                     batch=256, nthreads=8):
+                     batch=32, nthreads=8):
         tmp = os.path.join(os.path.dirname(hdf5_file), ".tmp." + os.path.basename(hdf5_file))
         sink = _Sink(tmp, self.feature_processor.feature_list, self.n_features, bd_size)
         if verbose:
             print("created HDF5 dataset in {}".format(tmp))
         sink.states.nthreads = max(1, nthreads)
+        fuse = os.environ.get("RAG_CONVERT_FUSED", "1") != "0"
         t0, ngames = time.time(), 0
         files = iter(sgf_files)
         # the next batch converts on a helper thread (the native converter releases the GIL)
-        # while this one is compressed and written
+        # while this one is written; batches are small so that even a few hundred games overlap
         from concurrent.futures import ThreadPoolExecutor
         ex = ThreadPoolExecutor(1)
 
-        def submit():
+        def submit(lead):
             names = [n for _, n in zip(range(batch), files)]
-            return (names, ex.submit(self._batch, names, bd_size, nthreads)) if names else None
+            if not names:
+                return None
+            return names, ex.submit(self._batch, names, bd_size, nthreads,
+                                    lead if fuse else None)
         try:
-            nxt = submit()
+            nxt = submit(sink.states.lead_rows())
             while nxt is not None:
                 names, fut = nxt
-                results = fut.result()
-                nxt = submit()
+                results, fused = fut.result()
+                # rows of this batch that reach the file (unparsable / wrong-size games drop)
+                kept = 0
+                for states, moves, err in results:
+                    if not isinstance(err, (sgf.SGFParseError, SizeMismatchError)):
+                        kept += len(moves)
+                nxt = submit((sink.states.lead_rows() - kept) % _CHUNK)
                 for name, (states, moves, err) in zip(names, results):
                     ngames += 1
                     if verbose:
                         print(name)
                     if isinstance(err, (sgf.SGFParseError, SizeMismatchError)):
                         states, moves = [], []
-                    n = sink.add(name, states, moves)
+                    n = sink.add(name, states, moves, rows_only=fused is not None)
                     self._report(name, err, ignore_errors)
                     if verbose:
                         print("\t%d state/action pairs extracted" % n if n else
                               "\t-no usable data-")
-                sink.flush()
+                if fused is not None:
+                    sink.flush_fused(*fused)
+                else:
+                    sink.flush()
         except Exception:
             print("sgfs_to_hdf5 failed")
             ex.shutdown(wait=True)

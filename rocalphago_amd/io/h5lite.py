@@ -800,6 +800,42 @@ class WDataset(object):
             self._max_written = i + take
         return start
 
+    def lead_rows(self):
+        """Rows the pending (partial) chunk still needs before it is full (0 when empty)."""
+        if self.chunks is None:
+            return 0
+        used = self._max_written - self._pending_start
+        return (self.chunks[0] - used) % self.chunks[0]
+
+    def append_chunks(self, lead, chunks, tail):
+        """Append ``lead`` rows (exactly ``lead_rows()`` of them: they complete the pending
+        chunk), then whole chunks that arrive already LZF-compressed -- ``chunks`` is a list of
+        (bytes, compressed) pairs, raw bytes when the chunk did not compress (the native
+        converter's fused path) -- then the ``tail`` rows of a new partial chunk."""
+        lead = np.asarray(lead, dtype=self.dtype)
+        short = len(lead) < self.lead_rows() and not chunks and not len(tail)  # a small batch
+        if self.chunks is None or self.compression != "lzf" or \
+                (len(lead) != self.lead_rows() and not short):
+            raise ValueError("append_chunks: an LZF-chunked dataset and lead_rows() lead rows")
+        if len(lead):
+            self.append(lead)
+        c = self.chunks[0]
+        if chunks:
+            if self._max_written == self._pending_start + c:
+                self._flush_pending()
+            start = self._max_written
+            n = len(chunks) * c
+            if start + n > self.shape[0]:
+                self.resize((start + n,) + self._row_shape)
+            for data, comp in chunks:
+                if comp:
+                    self._store_chunk(None, data)
+                else:
+                    self._store_chunk(data, None)
+            self._max_written = start + n
+        if len(tail):
+            self.append(tail)
+
     def __getitem__(self, key):
         if self.chunks is None:
             return self._data[key]

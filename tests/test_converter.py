@@ -32,7 +32,7 @@ CASES = {
 
 
 def _compare(conv, files, size):
-    native = conv._batch(files, size, 4)
+    native, _ = conv._batch(files, size, 4)
     for f, (st, ac, err) in zip(files, native):
         pst, pac, perr = conv._python_game(f, size)
         assert type(err) is type(perr) or (isinstance(err, go.IllegalMove) and
@@ -85,3 +85,30 @@ def test_classification_helpers():
         GameConverter._report("x", ValueError("boom"), ignore_errors=False)
     assert issubclass(SizeMismatchError, Exception)
     assert issubclass(sgf.SGFParseError, Exception)
+
+
+def test_fused_chunk_compression_writes_the_same_file(tmp_path, ref_data, monkeypatch):
+    """The fused path (whole 64-row chunks extracted and LZF-compressed inside the native
+    converter, lead / tail rows through the writer) stores exactly the rows, actions and file
+    offsets of the unfused path, across batches whose rows straddle chunk boundaries."""
+    import glob
+    import shutil
+    src = sorted(glob.glob(os.path.join(ref_data, "sgf", "*.sgf")))
+    files = []
+    for k in range(3):
+        for f in src:
+            dst = str(tmp_path / ("%d_%s" % (k, os.path.basename(f))))
+            shutil.copy(f, dst)
+            files.append(dst)
+    out = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("RAG_CONVERT_FUSED", fused)
+        path = str(tmp_path / ("o%s.h5" % fused))
+        GameConverter(list(DEFAULT_FEATURES)).sgfs_to_hdf5(files, path, nthreads=3, batch=4)
+        with h5lite.File(path) as f:
+            out[fused] = (f["states"][()], f["actions"][()],
+                          {k: f["file_offsets"][k][()].tolist() for k in f["file_offsets"]})
+    assert out["1"][0].shape[0] > 3 * 64
+    assert np.array_equal(out["1"][0], out["0"][0])
+    assert np.array_equal(out["1"][1], out["0"][1])
+    assert out["1"][2] == out["0"][2]
