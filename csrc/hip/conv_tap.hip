@@ -767,8 +767,12 @@ constexpr int kPPSlabRows192x5 = 448;    // 192-pixel blocks, 5x5 taps (<= 424 r
 // SPREAD: the loader group issues the next chunk's slab loads a few per step over taps
 // 0 .. TAPS-2 instead of all of them at tap 0 (the tap-0 read phase otherwise carries ~10 DMA
 // issues and holds the partner group at the next barrier).
+// WG0: of the PPBL weight slices of a step, the last WG0 are staged by the loader group 0 right
+// after its MFMA segment (balancing the two groups' non-MFMA phases; group 1 stages the rest).
+// PRIO: one static s_setprio 1 for group 1 (the second-dispatched half) and no per-segment
+// priority flips (MI355X_MICROARCH.md, "Two waves per SIMD", item 4).
 template <int NB, int DIAG = 0, int ISSUE = 0, int NT = kNT, bool BNP = false, int KS = 3,
-          int MT = kMT, int SPREAD = 0>
+          int MT = kMT, int SPREAD = 0, int WG0 = 0, int PRIO = 0>
 __global__ void __launch_bounds__(512, MT == kMT ? 1 : 4)
 conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                    const float* __restrict__ bias, bf16* __restrict__ Y,
@@ -778,6 +782,8 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                    const float* __restrict__ mcoef = nullptr, float* __restrict__ spart = nullptr,
                    const float* __restrict__ smean = nullptr, long long* stamps = nullptr) {
   constexpr int BN = 32 * NT, BTile = BN * kBK, PPBL = BN / 64, EpRow = BN + 8;
+  constexpr int PB1 = PPBL - WG0;  // weight slices per step staged by group 1
+  static_assert(WG0 >= 0 && PB1 >= 1 && (WG0 == 0 || (!BNP && !ISSUE)), "WG0 split");
   constexpr int TAPS = KS * KS;  // 9 (3x3) or 25 (the 5x5 layers: SL input, ResNet unit 0)
   // slab rows: 640 cover any 384-pixel run's 9-tap window (554), 768 its 25-tap one (748)
   // MT = 3: 192-pixel blocks (sub-chip grids, e.g. 128-game self-play passes): <= 298 rows
@@ -881,12 +887,13 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
       glds16(X + g * CIN + ((lcol ^ swz4(r)) * 8) + q * kBK, dst + (wl + 4 * k) * 16 * kBK);
     }
   };
-  auto stage_b = [&](int s) {  // step s = chunk * 9 + tap
+  auto stage_b = [&](int s, int k0 = 0, int k1 = 1 << 20) {  // step s = chunk * 9 + tap
     const int q = s / TAPS, t = s - q * TAPS;
     bf16* dst = lds + 2 * SLAB + (s % NB) * BTile;
     const long off = t * tap_stride + q * kBK;
 #pragma unroll
-    for (int k = 0; k < PPBL; ++k) glds16(bsrc[k] + off, dst + (wl + 4 * k) * 16 * kBK);
+    for (int k = 0; k < PPBL; ++k)
+      if (k >= k0 && k < k1) glds16(bsrc[k] + off, dst + (wl + 4 * k) * 16 * kBK);
   };
 
   const int frow = lane & 15;
@@ -934,12 +941,12 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
     lds_reads_done();  // retire this burst before the wave's next barrier (WAR on the LDS)
   };
   auto mfmas = [&]() {
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr (!PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int j = 0; j < NT; ++j)
 #pragma unroll
       for (int i = 0; i < MT; ++i) acc[j][i] = mfma16(wb[j], xa[i], acc[j][i]);
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (!PRIO) __builtin_amdgcn_s_setprio(0);
   };
   // MFMA segment with staging loads issued between its MFMA rows (ISSUE = 1)
   auto mfmas_staged = [&](int sb) {
@@ -984,6 +991,11 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
   // the first read of that data (always group 0's, at the next X barrier).
   if (grp == 0) {
     stage_a(0);
+    if constexpr (WG0 > 0) {
+#pragma unroll
+      for (int k = 0; k < D; ++k)
+        if (k < nsteps) stage_b(k, PB1, PPBL);
+    }
     wait_vm<0>();
     bn_slab(0, 0, AL);
 #pragma unroll 1
@@ -994,13 +1006,21 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
       __builtin_amdgcn_s_barrier();  // X_s
       asm volatile("" ::: "memory");
       const long long c2 = now();
+      int slab_now = 0;  // slab pieces this wave issues in this step (younger than B(s+1)'s)
       if constexpr (!(DIAG & 1)) {
         if constexpr (SPREAD && !BNP) {
           // pieces [t*AL/(TAPS-1), (t+1)*AL/(TAPS-1)) at taps 0 .. TAPS-2; all retired by the
           // wait after the last tap's MFMAs, as before
-          if (t < TAPS - 1 && more) stage_a(q + 1, t * AL / (TAPS - 1), (t + 1) * AL / (TAPS - 1));
+          if (t < TAPS - 1 && more) {
+            const int k0 = t * AL / (TAPS - 1), k1 = (t + 1) * AL / (TAPS - 1);
+            stage_a(q + 1, k0, k1);
+            slab_now = k1 - k0;
+          }
         } else {
-          if (t == 0 && more) stage_a(q + 1);
+          if (t == 0 && more) {
+            stage_a(q + 1);
+            slab_now = AL;
+          }
         }
       }
       read_frags(s);
@@ -1018,6 +1038,16 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
           bn_slab(q + 1, 2 * (t - 4), 2 * (t - 4) + 2);
         }
       } else {
+        if constexpr (WG0 > 0 && !(DIAG & 1)) {
+          // this group's slices of B(s+D), then B(s+1)'s (issued a step ago) complete before
+          // X_{s+1}: younger are this step's slab pieces and the slices just issued
+          int young = slab_now;
+          if (s + D < nsteps) {
+            stage_b(s + D, PB1, PPBL);
+            young += WG0;
+          }
+          if (s + 1 < nsteps) wait_vm_rt(young);
+        }
         if (t == TAPS - 1 && more) wait_vm<0>();  // slab(q+1) complete before the next chunk
       }
       const long long c6 = now();
@@ -1030,10 +1060,11 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
       }
     }
   } else {
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);  // static: the younger half
 #pragma unroll
     for (int k = 0; k < D; ++k)
-      if (k < nsteps) stage_b(k);
-    wait_vm_rt((nsteps - 1 < D - 1 ? nsteps - 1 : D - 1) * PPBL);  // B(0) complete
+      if (k < nsteps) stage_b(k, 0, PB1);
+    wait_vm_rt((nsteps - 1 < D - 1 ? nsteps - 1 : D - 1) * PB1);  // B(0) complete
 #pragma unroll 1
     for (int s = 0; s < nsteps; ++s) {
       const long long c0 = now();
@@ -1059,11 +1090,11 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
           const int yb = last - (s + 1);
           wait_vm_rt(yb > 0 ? yb * PPBL : 0);
         } else {
-          if (s + D < nsteps) stage_b(s + D);
+          if (s + D < nsteps) stage_b(s + D, 0, PB1);
           // B(s+1) complete before X_{s+1}: younger are B(s+2 .. min(s+D, nsteps-1))
           int yb = nsteps - 2 - s;
           yb = yb < D - 1 ? yb : D - 1;
-          wait_vm_rt(yb > 0 ? yb * PPBL : 0);
+          wait_vm_rt(yb > 0 ? yb * PB1 : 0);
         }
       }
       const long long c5 = now();
@@ -1076,6 +1107,7 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
       }
     }
     mfmas();
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
   }
   if constexpr (DIAG & 8) {
     if (lane == 0 && (w == 0 || w == 4) && stamps) {
@@ -1243,7 +1275,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
       const char* v = getenv("RAG_CONV_PP5");
       return !(v && v[0] == '0');
     }();
-    if (!pp5 || bnc || mcoef || spart || g_tap_mode < 5 || g_tap_mode > 10) return false;
+    if (!pp5 || bnc || mcoef || spart || g_tap_mode < 5 || g_tap_mode > 13) return false;
     if (nconv < pmin) {
       // sub-chip grids (128-game self-play passes): 192-pixel blocks, as the 3x3 layers
       static int key5b = -1, rows5b = 0;
@@ -1312,7 +1344,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
   }();
   if (w128) {
     const int nconv = ((M + kPPBM - 1) / kPPBM) * (COUTP / 128);
-    if (g_tap_mode < 5 || g_tap_mode > 10 || cached_rows8 > kPPSlabRows || nconv < pp_min)
+    if (g_tap_mode < 5 || g_tap_mode > 13 || cached_rows8 > kPPSlabRows || nconv < pp_min)
       return false;  // small batches: conv_pipe
     int nred = 0;
     WgradRed r{};
@@ -1335,7 +1367,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
     const char* v = getenv("RAG_CONV_PP192");
     return v && v[0] == '2';
   }();
-  if ((g_tap_mode >= 5 && g_tap_mode <= 10) && cached_rows8 <= kPPSlabRows && pp_fills &&
+  if ((g_tap_mode >= 5 && g_tap_mode <= 13) && cached_rows8 <= kPPSlabRows && pp_fills &&
       !pp192_all) {
     // ping-pong kernel: one block per CU; reduce blocks fill the CUs its last round leaves free
     const int nconv = ((M + kPPBM - 1) / kPPBM) * (COUTP / kBN);
@@ -1365,6 +1397,18 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
       conv_tap_pp_kernel<3, 0, 0, kNT, false, 3, kMT, 1><<<nconv + nred, 512, 0, stream>>>(
           x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
           nconv, r);
+    else if (g_tap_mode == 11)
+      conv_tap_pp_kernel<3, 0, 0, kNT, false, 3, kMT, 1, 1><<<nconv + nred, 512, 0, stream>>>(
+          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
+          nconv, r);
+    else if (g_tap_mode == 12)
+      conv_tap_pp_kernel<3, 0, 0, kNT, false, 3, kMT, 1, 0, 1><<<nconv + nred, 512, 0, stream>>>(
+          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
+          nconv, r);
+    else if (g_tap_mode == 13)
+      conv_tap_pp_kernel<3, 0, 0, kNT, false, 3, kMT, 1, 1, 1><<<nconv + nred, 512, 0, stream>>>(
+          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
+          nconv, r);
     else
       conv_tap_pp_kernel<3><<<nconv + nred, 512, 0, stream>>>(
           x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
@@ -1380,7 +1424,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
     return !(v && v[0] == '0');
   }();
   const int n192 = ((M + kBM - 1) / kBM) * (COUTP / kBN);
-  if (pp192 && g_tap_mode >= 5 && g_tap_mode <= 10 && n192 >= pp_min &&
+  if (pp192 && g_tap_mode >= 5 && g_tap_mode <= 13 && n192 >= pp_min &&
       cached_rows <= kPPSlabRows192) {
     int nred = 0;
     WgradRed r{};
@@ -1429,7 +1473,7 @@ bool rag_conv_tap_bn_ok(int M, int S, int WI, int shift, int CIN, int COUTP, int
   const char* e = getenv("RAG_PP_MIN_BLOCKS");
   const int pp_min = e ? atoi(e) : 200;
   const int nconv = ((M + kPPBM - 1) / kPPBM) * (COUTP / 128);
-  return g_tap_mode >= 5 && g_tap_mode <= 10 && KS == 3 && COUTP % kBN != 0 && COUTP % 128 == 0 &&
+  return g_tap_mode >= 5 && g_tap_mode <= 13 && KS == 3 && COUTP % kBN != 0 && COUTP % 128 == 0 &&
          CIN % kBK == 0 && CIN >= kBK && nconv >= pp_min &&
          max_slab_rows(S, WI, shift, kPPBM) <= kPPSlabRows;
 }
