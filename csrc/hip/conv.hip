@@ -685,6 +685,12 @@ static int conv_igemm_impl(const void* X, const void* W, const float* bias, void
                            const float* mcoef, float* spart = nullptr,
                            const float* smean = nullptr);
 
+namespace {
+// Real input channels of the launch in progress (0 = unknown: the padded CIN is all real);
+// set by rag_conv_igemm_cin for the launch it makes, read by the tap kernels' dispatch.
+}  // namespace
+thread_local int g_conv_cin_real = 0;
+
 // `pending`: null, or the caller's deferred-reduction handle (see PendingRed above).
 RAG_API int rag_conv_igemm(const void* X, const void* W, const float* bias, void* Y,
                            const void* mask, const void* resid, int B, int S, int HI, int HO,
@@ -692,6 +698,19 @@ RAG_API int rag_conv_igemm(const void* X, const void* W, const float* bias, void
                            hipStream_t stream, void* pending) {
   return conv_igemm_impl(X, W, bias, Y, mask, resid, B, S, HI, HO, CIN, COUTP, YC, KS, relu, HM,
                          stream, pending, nullptr, nullptr);
+}
+
+// As rag_conv_igemm, telling the dispatch how many of the CIN (padded) input channels are real:
+// a 5x5 layer with <= 48 of 64 skips the zero channels' MFMAs (conv_tap.hip, PAIR).
+RAG_API int rag_conv_igemm_cin(const void* X, const void* W, const float* bias, void* Y,
+                               const void* mask, const void* resid, int B, int S, int HI, int HO,
+                               int CIN, int COUTP, int YC, int KS, int relu, int HM,
+                               hipStream_t stream, void* pending, int cin_real) {
+  g_conv_cin_real = cin_real;
+  const int rc = conv_igemm_impl(X, W, bias, Y, mask, resid, B, S, HI, HO, CIN, COUTP, YC, KS,
+                                 relu, HM, stream, pending, nullptr, nullptr);
+  g_conv_cin_real = 0;
+  return rc;
 }
 
 // As rag_conv_igemm with the BN prologue: X is the BN input x and the layer input is

@@ -771,8 +771,12 @@ constexpr int kPPSlabRows192x5 = 448;    // 192-pixel blocks, 5x5 taps (<= 424 r
 // after its MFMA segment (balancing the two groups' non-MFMA phases; group 1 stages the rest).
 // PRIO: one static s_setprio 1 for group 1 (the second-dispatched half) and no per-segment
 // priority flips (MI355X_MICROARCH.md, "Two waves per SIMD", item 4).
+// PAIR (5x5 input layer with <= 48 real input channels padded to 64): the second 32-channel
+// chunk holds only 16 real channels, so its steps pair two taps -- lanes of k-quads 0/1 read
+// channels 32..47 of tap t, quads 2/3 the same channels of tap t+1 (channels 48..63 of tap 24,
+// zero padding, for the last, unpaired tap) -- 25 + 13 = 38 K-steps instead of 50.
 template <int NB, int DIAG = 0, int ISSUE = 0, int NT = kNT, bool BNP = false, int KS = 3,
-          int MT = kMT, int SPREAD = 0, int WG0 = 0, int PRIO = 0>
+          int MT = kMT, int SPREAD = 0, int WG0 = 0, int PRIO = 0, int PAIR = 0>
 __global__ void __launch_bounds__(512, MT == kMT ? 1 : 4)
 conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                    const float* __restrict__ bias, bf16* __restrict__ Y,
@@ -783,6 +787,8 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                    const float* __restrict__ smean = nullptr, long long* stamps = nullptr) {
   constexpr int BN = 32 * NT, BTile = BN * kBK, PPBL = BN / 64, EpRow = BN + 8;
   constexpr int PB1 = PPBL - WG0;  // weight slices per step staged by group 1
+  constexpr bool PR = PAIR && KS == 5;
+  static_assert(!PAIR || (KS == 5 && !BNP && !ISSUE), "tap pairing: the 5x5 input layer");
   static_assert(WG0 >= 0 && PB1 >= 1 && (WG0 == 0 || (!BNP && !ISSUE)), "WG0 split");
   constexpr int TAPS = KS * KS;  // 9 (3x3) or 25 (the 5x5 layers: SL input, ResNet unit 0)
   // slab rows: 640 cover any 384-pixel run's 9-tap window (554), 768 its 25-tap one (748)
@@ -887,10 +893,26 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
       glds16(X + g * CIN + ((lcol ^ swz4(r)) * 8) + q * kBK, dst + (wl + 4 * k) * 16 * kBK);
     }
   };
+  // step s -> (chunk q, tap t); PR: steps TAPS.. are chunk 1's tap pairs (2p, 2p + 1)
+  auto decode = [&](int s, int& q, int& t) {
+    if (PR && s >= TAPS) {
+      q = 1;
+      t = 2 * (s - TAPS);
+    } else {
+      q = s / TAPS;
+      t = s - q * TAPS;
+    }
+  };
+  // PR: this lane's staged weight piece is virtual 16-byte chunk v = lcol ^ swz (the same for
+  // every slice: the slice rows differ by multiples of 16); v >= 2 of a paired step comes from
+  // the next tap's channels 32 + 8 (v - 2)
+  const bool vhi = ((lcol ^ swz4(lrow)) >= 2);
   auto stage_b = [&](int s, int k0 = 0, int k1 = 1 << 20) {  // step s = chunk * 9 + tap
-    const int q = s / TAPS, t = s - q * TAPS;
+    int q, t;
+    decode(s, q, t);
     bf16* dst = lds + 2 * SLAB + (s % NB) * BTile;
-    const long off = t * tap_stride + q * kBK;
+    long off = t * tap_stride + q * kBK;
+    if (PR && q == 1 && vhi && t + 1 < TAPS) off += tap_stride - 16;
 #pragma unroll
     for (int k = 0; k < PPBL; ++k)
       if (k >= k0 && k < k1) glds16(bsrc[k] + off, dst + (wl + 4 * k) * 16 * kBK);
@@ -919,22 +941,28 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
     for (int i = 0; i < MT; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int cchunks = CIN / kBK;
-  const int nsteps = TAPS * cchunks;
+  const int nsteps = PR ? TAPS + (TAPS + 1) / 2 : TAPS * cchunks;  // PR: cchunks == 2
   bf16x8 xa[MT], wb[NT];
   auto read_frags = [&](int s) {
     if constexpr (DIAG & 2) {
       asm volatile("" : "+v"(xa[0]), "+v"(wb[0]));
       return;
     }
-    const int q = s / TAPS, t = s - q * TAPS;
+    int q, t;
+    decode(s, q, t);
     const bf16* slab = lds + (q & 1) * SLAB;
     const bf16* bt = lds + 2 * SLAB + (s % NB) * BTile;
-    const int ky = t / KS, kx = t - ky * KS;
+    int tl = t, ch = fq;  // PR: k-quads 2/3 of a paired step read the next tap's chunks 0/1
+    if (PR && q == 1 && fq >= 2 && t + 1 < TAPS) {
+      tl = t + 1;
+      ch = fq & 1;
+    }
+    const int ky = tl / KS, kx = tl - ky * KS;
     const int toff = ky * WI + kx;
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
       const int r = prel[i] + toff;
-      xa[i] = *reinterpret_cast<const bf16x8*>(slab + r * kBK + ((fq ^ swz4(r)) * 8));
+      xa[i] = *reinterpret_cast<const bf16x8*>(slab + r * kBK + ((ch ^ swz4(r)) * 8));
     }
 #pragma unroll
     for (int j = 0; j < NT; ++j) wb[j] = *reinterpret_cast<const bf16x8*>(bt + boffs[j]);
@@ -956,7 +984,8 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
 #pragma unroll
       for (int i = 0; i < MT; ++i) acc[j][i] = mfma16(wb[j], xa[i], acc[j][i]);
       if (j < PPBL && sb >= 0) {
-        const int q = sb / TAPS, t = sb - q * TAPS;
+        int q, t;
+        decode(sb, q, t);
         bf16* dst = lds + 2 * SLAB + (sb % NB) * BTile;
         glds16(bsrc[j] + t * tap_stride + q * kBK, dst + (wl + 4 * j) * 16 * kBK);
       }
@@ -1000,7 +1029,8 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
     bn_slab(0, 0, AL);
 #pragma unroll 1
     for (int s = 0; s < nsteps; ++s) {
-      const int q = s / TAPS, t = s - q * TAPS;
+      int q, t;
+      decode(s, q, t);
       const bool more = q + 1 < cchunks;
       const long long c1 = now();
       __builtin_amdgcn_s_barrier();  // X_s
@@ -1154,6 +1184,7 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
 }
 
 int g_tap_mode = -1;  // -1: read RAG_CONV_TAP on first use (default on)
+extern thread_local int g_conv_cin_real;  // conv.hip: real input channels of this launch
 int g_ep_lds_override = -1;  // rag_conv_ep_lds(): A/B switch of conv_tap_kernel's epilogue
 
 // Worst-case slab extent of a bm-pixel run (host check of the kernels' slab-row assumptions).
@@ -1276,6 +1307,13 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
       return !(v && v[0] == '0');
     }();
     if (!pp5 || bnc || mcoef || spart || g_tap_mode < 5 || g_tap_mode > 13) return false;
+    // <= 48 real input channels in a 64-channel layout (the caller's hint, rag_conv_igemm_cin):
+    // chunk 1 steps pair two taps (PAIR; RAG_CONV_PAIR5=0 disables)
+    static const bool pair_on = [] {
+      const char* v = getenv("RAG_CONV_PAIR5");
+      return !(v && v[0] == '0');
+    }();
+    const bool pair5 = pair_on && CIN == 64 && g_conv_cin_real > 0 && g_conv_cin_real <= 48;
     if (nconv < pmin) {
       // sub-chip grids (128-game self-play passes): 192-pixel blocks, as the 3x3 layers
       static int key5b = -1, rows5b = 0;
@@ -1291,9 +1329,14 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
         r = *red;
         nred = std::max(8, (256 - n192 % 256) % 256);
       }
-      conv_tap_pp_kernel<3, 0, 0, 6, false, 5, 3><<<n192 + nred, 512, 0, stream>>>(
-          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
-          n192, r);
+      if (pair5)
+        conv_tap_pp_kernel<3, 0, 0, 6, false, 5, 3, 0, 0, 0, 1><<<n192 + nred, 512, 0, stream>>>(
+            x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM,
+            total_rows, n192, r);
+      else
+        conv_tap_pp_kernel<3, 0, 0, 6, false, 5, 3><<<n192 + nred, 512, 0, stream>>>(
+            x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM,
+            total_rows, n192, r);
       return true;
     }
     if (rows5 > kPPSlabRows5) return false;
@@ -1303,7 +1346,17 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
       r = *red;
       nred = std::max(8, (256 - nconv % 256) % 256);
     }
-    if (w192 && g_tap_mode == 10)
+    if (w192 && pair5 && g_tap_mode >= 10)
+      conv_tap_pp_kernel<3, 0, 0, 6, false, 5, kMT, 1, 0, 0, 1><<<nconv + nred, 512, 0,
+                                                                   stream>>>(
+          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
+          nconv, r);
+    else if (w192 && pair5)
+      conv_tap_pp_kernel<3, 0, 0, 6, false, 5, kMT, 0, 0, 0, 1><<<nconv + nred, 512, 0,
+                                                                   stream>>>(
+          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
+          nconv, r);
+    else if (w192 && g_tap_mode >= 10)
       conv_tap_pp_kernel<3, 0, 0, 6, false, 5, kMT, 1><<<nconv + nred, 512, 0, stream>>>(
           x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
           nconv, r);

@@ -170,7 +170,7 @@ class HipTrunk(_PackedConvs):
         for l, s in enumerate(self.specs):
             x, y = self.acts[l][:B], self.acts[l + 1][:B]
             ops.conv_igemm(x, self._wf[l], self._bias[l], y, B, S, self.halo[l],
-                           self.halo[l + 1], s.cinp, s.coutp, s.ks, s.relu)
+                           self.halo[l + 1], s.cinp, s.coutp, s.ks, s.relu, cin=s.cin)
         return self.acts[-1][:B]
 
     def backward(self, B, dws, dbs, top_which=0, accumulate=False, on_layer_done=None):

@@ -10,6 +10,7 @@ SZ = C.c_size_t
 SIGNATURES = {
     # conv.hip
     "rag_conv_igemm": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P, P],
+    "rag_conv_igemm_cin": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P, P, I],
     "rag_conv_wgrad_workspace": [I, I, I, I, I, P],
     "rag_conv_wgrad": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, P],
     "rag_conv_wgrad_deferred": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, P],

@@ -106,7 +106,7 @@ def max_rows(S, halo, channels):
 
 
 def conv_igemm(x, wpack, bias, y, B, S, hi, ho, cinp, coutp, ks, relu, mask=None,
-               mask_halo=None, residual=None, pending=None):
+               mask_halo=None, residual=None, pending=None, cin=None):
     """y[pad ho] = act(conv_ks(x[pad hi]) + bias [+ residual]), or the dgrad form with a ReLU
     mask (the layer input: y's channel count, its own halo ``mask_halo``, default ho).
     ``residual`` (ResNet sum-merge) has y's layout and may be y itself. ``pending``: a
@@ -117,6 +117,13 @@ def conv_igemm(x, wpack, bias, y, B, S, hi, ho, cinp, coutp, ks, relu, mask=None
         raise ValueError("mask layout does not match (halo %d, %d channels)" % (hm, y.shape[-1]))
     if residual is not None and residual.shape[1:] != y.shape[1:]:
         raise ValueError("residual layout does not match the output")
+    if cin is not None and cin < cinp:
+        # the real input channel count lets the 5x5 input layer skip its zero channels
+        _check(_lib().rag_conv_igemm_cin(_ptr(x), _ptr(wpack), _ptr(bias), _ptr(y), _ptr(mask),
+                                         _ptr(residual), B, S, hi, ho, cinp, coutp, y.shape[-1],
+                                         ks, int(relu), hm, _stream(), _hptr(pending), int(cin)),
+               "conv_igemm")
+        return y
     _check(_lib().rag_conv_igemm(_ptr(x), _ptr(wpack), _ptr(bias), _ptr(y), _ptr(mask),
                                  _ptr(residual), B, S, hi, ho, cinp, coutp, y.shape[-1], ks,
                                  int(relu), hm, _stream(), _hptr(pending)), "conv_igemm")

@@ -27,7 +27,8 @@ def ops():
                                              (2, 16, 16, 3, 19), (7, 128, 128, 3, 13),
                                              (4, 192, 32, 1, 19), (1, 12, 16, 5, 9),
                                              (2, 64, 96, 3, 7), (130, 192, 192, 3, 19),
-                                             (128, 48, 192, 5, 19)])
+                                             (128, 48, 192, 5, 19), (256, 48, 192, 5, 19),
+                                             (256, 40, 192, 5, 19)])
 def test_conv_forward(ops, B, cin, cout, ks, S):
     dev = torch.device("cuda")
     torch.manual_seed(0)
@@ -42,7 +43,7 @@ def test_conv_forward(ops, B, cin, cout, ks, S):
     bias = torch.zeros(coutp, device=dev)
     bias[:cout] = b
     y = ops.alloc_padded(B, S, 1, coutp, dev)
-    ops.conv_igemm(xp, wf, bias, y, B, S, hi, 1, cinp, coutp, ks, relu=True)
+    ops.conv_igemm(xp, wf, bias, y, B, S, hi, 1, cinp, coutp, ks, relu=True, cin=cin)
     out = ops.unpack(y, cout, 1)
     assert rel_err(out, ref) < 2e-2
     # halo stays zero
