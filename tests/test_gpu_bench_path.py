@@ -81,7 +81,8 @@ def _gpu_acts(plan, B):
     return out
 
 
-def test_north_star_sl_step_matches_fp32(cuda):
+@pytest.mark.parametrize("augment", [False, True])
+def test_north_star_sl_step_matches_fp32(cuda, augment):
     """Gradients of one bench-path step vs fp32 autograd, two references:
     (a) fp32 autograd at the kernels' own forward point (their stored bf16 activations injected
         as each layer's output, ReLU masks from them, dL/d(pre-activation) rounded to bf16 where
@@ -95,7 +96,10 @@ def test_north_star_sl_step_matches_fp32(cuda):
         trunk's activations are nearly constant over the board, so the gradient
         sum_p x(p) (p(p) - y(p)) cancels to a few % of its terms and amplifies that into ~12 %
         per tensor (3 layers: 1-4 %; identical with fp32 partial slabs and without deferred
-        reductions, i.e. not a kernel error)."""
+        reductions, i.e. not a kernel error).
+    ``augment``: the bench's random dihedral augmentation (all 8 transforms, drawn by the
+    sl_batch kernel and applied while packing the input) -- the reference applies the same
+    per-sample transforms to the planes and the targets with numpy."""
     torch.backends.cudnn.allow_tf32 = False
     torch.backends.cuda.matmul.allow_tf32 = False
     pol = CNNPolicy(DEFAULT_FEATURES, board=19, filters_per_layer=192, layers=12, device=cuda,
@@ -104,7 +108,10 @@ def test_north_star_sl_step_matches_fp32(cuda):
     model.compile(loss="categorical_crossentropy", optimizer=K.SGD(lr=0.003),
                   metrics=["accuracy"])
     ds = DeviceDataset.synthetic(1024, 48, 19, cuda, seed=17)
-    tr = SupervisedTrainer(model, ds, 256, ["noop"], None, seed=5)
+    from rocalphago_amd.ops import hipops as ops
+    from rocalphago_amd.training.data import TRANSFORM_NAMES, apply_transform_np
+    tr = SupervisedTrainer(model, ds, 256, TRANSFORM_NAMES if augment else ["noop"], None,
+                           seed=5)
     plan = tr.plan
     assert plan is not None and len(plan.conv_names) == 12
     net = model.net
@@ -113,11 +120,21 @@ def test_north_star_sl_step_matches_fp32(cuda):
     g = torch.Generator(device=cuda)
     g.manual_seed(3)
     idx = torch.randint(0, ds.N, (256,), generator=g, device=cuda)
+    # the transforms and transformed targets the step will draw (a pure function of the
+    # trainer seed and the optimizer iteration, batch.hip)
+    tf, labels = ops.sl_batch(idx.long().contiguous(), ds.labels, ds.tf_table, tr.sym, tr.seed,
+                              getattr(model.optimizer, "iterations", 0))
+    tf, labels = tf.clone(), labels.clone()
     tr.step(idx)
     torch.cuda.synchronize()
     got = {n: [t.detach().clone() for t in net.grads_of(n)] for n in params}
     acts = _gpu_acts(plan, 256)
-    x = ds.states[idx].float()
+    xs = ds.states[idx].cpu().numpy()
+    tfs = tf.cpu().numpy()
+    if augment:
+        assert len(set(tfs.tolist())) == 8  # every transform drawn in a batch of 256
+    x = torch.from_numpy(np.stack([apply_transform_np(xs[b], int(tfs[b]))
+                                   for b in range(256)]).astype(np.float32)).to(cuda)
     cases = (("kernels' forward point, bf16-stored grads", True, True, 2e-2),
              ("kernels' forward point, fp32 grads", True, False, 0.1),
              ("independent fp32", False, False, 0.25))
@@ -127,7 +144,7 @@ def test_north_star_sl_step_matches_fp32(cuda):
                        [leaf[n][1] for n in plan.conv_names], acts if inject else None, store)
         hw, hb = leaf[plan.head_name]
         z = F.conv2d(h, hw, hb).reshape(256, -1) + leaf[plan.bias_name][0]
-        loss = F.cross_entropy(z, ds.labels[idx])
+        loss = F.cross_entropy(z, labels)
         loss.backward()
         errs = {}
         for n in params:
