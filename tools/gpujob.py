@@ -26,6 +26,9 @@ PY = "python3 -u"
 PMC_SQ = ("SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES "
           "SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES GRBM_GUI_ACTIVE")
 
+PMC_LDS = ("SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS "
+           "SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY GRBM_GUI_ACTIVE GRBM_COUNT")
+
 # name -> (seconds, command, echo mode); {dir} = gpurun_out/OUT/<step tag> (profiler output)
 STEPS = {
     "tests": (900, PY + " -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread",
@@ -48,6 +51,8 @@ STEPS = {
                PY + " bench.py --no-mcts --steps 6 --warmup 2", "tail1"),
     "pmc-resnet": (150, "rocprofv3 --pmc " + PMC_SQ + " --output-format csv -d {dir} -- "
                    + PY + " bench.py --model resnet --no-mcts --steps 6 --warmup 2", "tail1"),
+    "pmc2-sl": (150, "rocprofv3 --pmc " + PMC_LDS + " --output-format csv -d {dir} -- " +
+                PY + " bench.py --no-mcts --steps 6 --warmup 2", "tail1"),
     "kernels": (600, PY + " -m pytest tests/test_hip_kernels.py tests/test_gpu_models.py "
                 "tests/test_gpu_bench_path.py -m gpu -x -q --timeout 200 "
                 "--timeout-method thread", "tail2"),
