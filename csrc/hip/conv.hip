@@ -804,15 +804,15 @@ int rag_launch_wgrad_taps(const bf16* G, const bf16* X, float* part, float* bpar
 bool rag_wgrad_taps_fits(int WP, int KS, int RG);  // wgrad.hip
 int rag_wgrad_taps_target_blocks();  // wgrad.hip
 bool rag_wgrad_slab_ok(int S, int H, int HG, int GC, int COUTP, int CINP, int KS);  // wgrad_slab.hip
-int rag_wgrad_slab_nchunks(int R, int CINP, int* spc, int KS);                    // wgrad_slab.hip
+int rag_wgrad_slab_nchunks(int R, int CINP, int* spc, int KS, int pair5 = 0);     // wgrad_slab.hip
 bool rag_wgrad_slab_bf16();                                                        // wgrad_slab.hip
 WgradRed rag_wgrad_slab_red(const void* part, const float* bpart, float* dW, float* db,
                             int nchunks, int CINP, int COUTP, int COUT, int CIN, int accumulate,
-                            int KS);
+                            int KS, int pair5);
 int rag_launch_wgrad_slab_reduce(const WgradRed& r, hipStream_t stream);        // wgrad_slab.hip
 int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpart, int R, int WP,
                           int GC, int CIN, int spc, int CINP, int nchunks, hipStream_t stream,
-                          const float* xcoef, int S, int KS, int COUTP);
+                          const float* xcoef, int S, int KS, int COUTP, int pair5);
 
 namespace {
 // all-taps variant applicability and plan (see wgrad.hip)
@@ -862,8 +862,11 @@ RAG_API size_t rag_conv_wgrad_workspace(int B, int S, int COUTP, int CINP, int K
   }
   for (int H = 1; H <= 2; ++H) {
     if (rag_wgrad_slab_ok(S, H, H, COUTP, COUTP, CINP, KS)) {
-      const int sn = rag_wgrad_slab_nchunks(B * (S + 2 * H) * (S + 2 * H), CINP, nullptr, KS);
-      if (sn > nc) nc = sn;
+      for (int pr = 0; pr <= 1; ++pr) {  // the 5x5 row-paired grid has more chunks
+        const int sn = rag_wgrad_slab_nchunks(B * (S + 2 * H) * (S + 2 * H), CINP, nullptr, KS,
+                                              pr);
+        if (sn > nc) nc = sn;
+      }
     }
   }
   if (nchunks) *nchunks = nc;
@@ -909,15 +912,22 @@ static int conv_wgrad_impl(const void* G, const void* X, float* dW, float* db, f
   bool bf16_part = false;
   const bool slab = rag_wgrad_slab_ok(S, HI, HG, GC, COUTP, CINP, KS);
   if (xcoef && !(slab && KS == 3 && rag_wgrad_slab_bf16() && CINP == 128)) return -5;
+  // 5x5 with <= 48 real of 64 input channels (the SL input layer): c-tile 1's blocks pair two
+  // kernel rows instead of computing a zero c-fragment (RAG_WGRAD_PAIR5=0 disables)
+  static const bool pair_on = [] {
+    const char* e = getenv("RAG_WGRAD_PAIR5");
+    return !(e && e[0] == '0');
+  }();
+  const int pair5 = pair_on && KS == 5 && CINP == 64 && CIN <= 48 && !xcoef ? 1 : 0;
   if (slab) {
     bf16_part = rag_wgrad_slab_bf16();
     const int WP = S + 2 * HI;
     const int R = B * WP * WP;
     int spc = 1;
-    nchunks = rag_wgrad_slab_nchunks(R, CINP, &spc, KS);
+    nchunks = rag_wgrad_slab_nchunks(R, CINP, &spc, KS, pair5);
     bpart = db ? work + (size_t)nchunks * taps * COUTP * CINP : nullptr;
     const int rc = rag_launch_wgrad_slab(g, x, part, bpart, R, WP, GC, CINP, spc, CINP, nchunks,
-                                         stream, xcoef, S, KS, COUTP);
+                                         stream, xcoef, S, KS, COUTP, pair5);
     if (rc) return rc;
   } else if (tp.ok) {
     nchunks = tp.nchunks;
@@ -960,7 +970,7 @@ static int conv_wgrad_impl(const void* G, const void* X, float* dW, float* db, f
   }
   if (bf16_part) {
     const WgradRed r = rag_wgrad_slab_red(part, bpart, dW, db, nchunks, CINP, COUTP, COUT, CIN,
-                                          accumulate, KS);
+                                          accumulate, KS, slab ? pair5 : 0);
     if (defer && rs == stream) {
       PendingRed* p = static_cast<PendingRed*>(pending);
       p->r = r;

@@ -32,6 +32,7 @@ struct WgradRed {
   int nchunks, ntc, COUT, CIN, accumulate, map;
   int n, waves, blk;   // block channels (192 | 128), waves (n / 16), accumulators per block
   int taps, kgrp;      // KS * KS; blocks per c-tile (5x5: one kernel row each, else 1)
+  int pair5;           // 5x5 with <= 48 of 64 channels: pseudo c-tiles 5..7 = c-tile 1, rows 2p, 2p+1
 };
 
 __device__ __forceinline__ void wslab_add8(float (&s)[8], const uint4& v, float sc) {
@@ -49,7 +50,9 @@ __device__ __forceinline__ void wslab_store_oct(const WgradRed& r, int q, const 
   const int e = q * 8;
   const int pct = e / r.blk;  // (pseudo) c-tile: c-tile * kgrp + kernel row
   const int loc = e - pct * r.blk;
-  const int ctile = pct / r.kgrp, ky = pct - ctile * r.kgrp;
+  const bool pblk = r.pair5 && pct >= 5;
+  const int ctile = pblk ? 1 : pct / r.kgrp;
+  int ky = pblk ? 2 * (pct - 5) : pct - ctile * r.kgrp;
   const int lane0 = (loc >> 2) & 63;
   const int wv = (loc >> 8) % r.waves;
   const int slot = (loc >> 8) / r.waves;  // i * NA + a
@@ -66,9 +69,15 @@ __device__ __forceinline__ void wslab_store_oct(const WgradRed& r, int q, const 
     cb = ctile * kWsC + ((wv >> 1) & 1) * 16;
   } else {  // map 0: wave wv owns n-frags 2 (wv % g), +1 and c-frag wv / g, g = n / 32
     const int a = slot & 1, g = r.n >> 5;
+    if (pblk) {  // the wave group picks the kernel row, the c-fragment is c-tile 1's first
+      ky += wv / g;
+      if (ky >= 5) return;
+      cb = kWsC;
+    } else {
+      cb = ctile * kWsC + (wv / g) * 16;
+    }
     t = ky * 5 + (slot >> 1);  // 3x3: ky = 0, slot >> 1 = tap; 5x5: the block's row ky, kx
     nb = ((wv % g) * 2 + a) * 16;
-    cb = ctile * kWsC + (wv / g) * 16;
   }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {

@@ -120,7 +120,7 @@ __global__ void __launch_bounds__(64 * WS<N>::Waves)
 wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
                   float* __restrict__ part, float* __restrict__ bpart, int R, int WP, int GC,
                   int CIN, int spc, int CINP, const float* __restrict__ xcoef = nullptr,
-                  int S = 0) {
+                  int S = 0, int pair5 = 0) {
   using L = WS<N>;
   static_assert(KS == 3 || (KS == 5 && kBF && kMAP == 0 && !BNX), "5x5: fp16 map-0 partials");
   constexpr int kGrp = KS == 3 ? 1 : KS;  // blocks per (chunk, c-tile): kernel rows
@@ -137,10 +137,18 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
   const int w = wave_id();
   const int tid = threadIdx.x;
   const int ntc = CINP / kC;
+  // pair5 (5x5, <= 48 real of 64 input channels): c-tile 1 has one real c-fragment, so its
+  // blocks take TWO kernel rows -- waves of c-fragment group 1 compute c-fragment 0 of row ky+1
+  // (its X window lies WP rows further down the same 112-row slab): 5 + 3 blocks per chunk
+  // instead of 10
+  const bool pr = KS == 5 && pair5;
+  const int ptc = pr ? 8 : ntc * kGrp;  // (pseudo) c-tiles per chunk
   const int wid = xcd_remap(blockIdx.x, gridDim.x);  // the c-tiles of a chunk share one XCD
-  const int chunk = wid / (ntc * kGrp);
-  const int pct = wid - chunk * ntc * kGrp;  // pseudo c-tile: c-tile * kGrp + ky
-  const int ctile = pct / kGrp, ky = pct - ctile * kGrp;
+  const int chunk = wid / ptc;
+  const int pct = wid - chunk * ptc;  // pseudo c-tile: c-tile * kGrp + ky (pr: see above)
+  const bool pblk = pr && pct >= 5;
+  const int ctile = pblk ? 1 : pct / kGrp;
+  const int ky = pblk ? 2 * (pct - 5) : pct - ctile * kGrp;  // the slab's kernel row
   const int c0 = ctile * kC;
   const int steps = (R + kRows - 1) / kRows;
   const int sbeg = chunk * spc;
@@ -221,7 +229,9 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
   using M = WMap<kMAP, N, KS>;
   constexpr int NA = M::NA, NT = M::NT;
   const int nf0 = M::nf0(w);  // this wave's NA 16-channel n fragments
-  const int cf = M::cf(w);    // its 16-channel c fragment
+  const int cf = pblk ? 0 : M::cf(w);    // its 16-channel c fragment
+  const int dky = pblk ? M::cf(w) : 0;   // pr: its kernel row is ky + dky
+  const bool idle = ky + dky >= KS;      // pr: the last pair block's second row does not exist
   int goff[NA];
 #pragma unroll
   for (int a = 0; a < NA; ++a)
@@ -230,7 +240,7 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
     const int t = M::tap(w, i);
-    const int xr = KS == 3 ? kr + (t / 3) * WP + (t % 3) : kr + t;  // 5x5: t = kx
+    const int xr = KS == 3 ? kr + (t / 3) * WP + (t % 3) : kr + t + dky * WP;  // 5x5: t = kx
     xoff[i] = kGElems + xr * kC + (((cf * 2 + (p >> 1)) ^ swz_x(xr)) * 8) + 4 * (p & 1);
   }
 
@@ -304,6 +314,12 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
     }
   }
 
+  if (idle) {  // nothing to report (the reduction skips these slots)
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+      for (int a = 0; a < NA; ++a) acc[i][a] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   if (kBF) {
     // scaled fp16 partials in the MFMA C layout: [chunk][ctile][i * NA + a][wave][lane][4];
     // the block's max |acc| picks a power-of-two scale into [2^14, 2^15) (wgrad_part.h)
@@ -659,9 +675,9 @@ bool rag_wgrad_slab_ok(int S, int H, int HG, int GC, int COUTP, int CINP, int KS
 }
 
 // Chunks of 64-row stages: one resident block per CU (256) over all c-tiles.
-int rag_wgrad_slab_nchunks(int R, int CINP, int* spc, int KS) {
+int rag_wgrad_slab_nchunks(int R, int CINP, int* spc, int KS, int pair5) {
   const int steps = (R + kRows - 1) / kRows;
-  int nc = 256 / (CINP / kC * (KS == 5 ? 5 : 1));
+  int nc = 256 / (KS == 5 && pair5 ? 8 : CINP / kC * (KS == 5 ? 5 : 1));
   nc = nc < steps ? nc : steps;
   nc = nc > 0 ? nc : 1;
   const int s = (steps + nc - 1) / nc;
@@ -717,7 +733,7 @@ bool rag_wgrad_slab_bf16() {
 
 WgradRed rag_wgrad_slab_red(const void* part, const float* bpart, float* dW, float* db,
                             int nchunks, int CINP, int COUTP, int COUT, int CIN, int accumulate,
-                            int KS) {
+                            int KS, int pair5) {
   WgradRed r;
   r.part = (const f16*)part;
   r.bpart = bpart;
@@ -726,7 +742,8 @@ WgradRed rag_wgrad_slab_red(const void* part, const float* bpart, float* dW, flo
   r.nchunks = nchunks;
   r.kgrp = KS == 5 ? 5 : 1;
   r.taps = KS * KS;
-  r.ntc = CINP / kC * r.kgrp;  // (pseudo) c-tiles per chunk
+  r.pair5 = KS == 5 && pair5;
+  r.ntc = r.pair5 ? 8 : CINP / kC * r.kgrp;  // (pseudo) c-tiles per chunk
   r.COUT = COUT;
   r.CIN = CIN;
   r.accumulate = accumulate;
@@ -757,7 +774,7 @@ RAG_API int rag_wgrad_slab_nbuf(int n) {
 
 int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpart, int R, int WP,
                           int GC, int CIN, int spc, int CINP, int nchunks, hipStream_t stream,
-                          const float* xcoef, int S, int KS, int COUTP) {
+                          const float* xcoef, int S, int KS, int COUTP, int pair5) {
   if (g_wslab_nbuf < 0) {
     const char* e = getenv("RAG_WGRAD_NBUF");
     g_wslab_nbuf = e ? atoi(e) : 3;
@@ -765,13 +782,14 @@ int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpar
   const bool bf = rag_wgrad_slab_bf16();
   if (KS == 5) {  // per-row blocks, fp16 partials, map 0
     if (!bf || xcoef) return -5;
-    const dim3 g5(nchunks * (CINP / kC) * 5);
+    if (pair5 && CINP != 2 * kC) return -5;
+    const dim3 g5(nchunks * (pair5 ? 8 : (CINP / kC) * 5));
     if (COUTP == 192)
-      wgrad_slab_kernel<3, true, 0, 192, false, 5><<<g5, 768, 0, stream>>>(G, X, part, bpart, R,
-                                                                          WP, GC, CIN, spc, CINP);
+      wgrad_slab_kernel<3, true, 0, 192, false, 5><<<g5, 768, 0, stream>>>(
+          G, X, part, bpart, R, WP, GC, CIN, spc, CINP, nullptr, 0, pair5);
     else if (COUTP == 128)
-      wgrad_slab_kernel<3, true, 0, 128, false, 5><<<g5, 512, 0, stream>>>(G, X, part, bpart, R,
-                                                                          WP, GC, CIN, spc, CINP);
+      wgrad_slab_kernel<3, true, 0, 128, false, 5><<<g5, 512, 0, stream>>>(
+          G, X, part, bpart, R, WP, GC, CIN, spc, CINP, nullptr, 0, pair5);
     else
       return -5;
     return (int)hipGetLastError();
