@@ -24,6 +24,8 @@
 
 using namespace rag;
 
+extern thread_local int g_conv_cin_real;  // conv.hip: real input channels of this launch
+
 namespace {
 
 constexpr int kBK = 32;
@@ -1184,7 +1186,6 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
 }
 
 int g_tap_mode = -1;  // -1: read RAG_CONV_TAP on first use (default on)
-extern thread_local int g_conv_cin_real;  // conv.hip: real input channels of this launch
 int g_ep_lds_override = -1;  // rag_conv_ep_lds(): A/B switch of conv_tap_kernel's epilogue
 
 // Worst-case slab extent of a bm-pixel run (host check of the kernels' slab-row assumptions).
