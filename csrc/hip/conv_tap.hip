@@ -1307,7 +1307,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
       const char* v = getenv("RAG_CONV_PP5");
       return !(v && v[0] == '0');
     }();
-    if (!pp5 || bnc || mcoef || spart || g_tap_mode < 5 || g_tap_mode > 13) return false;
+    if (!pp5 || bnc || mcoef || spart || g_tap_mode < 5 || g_tap_mode > 15) return false;
     // <= 48 real input channels in a 64-channel layout (the caller's hint, rag_conv_igemm_cin):
     // chunk 1 steps pair two taps (PAIR; RAG_CONV_PAIR5=0 disables)
     static const bool pair_on = [] {
@@ -1398,7 +1398,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
   }();
   if (w128) {
     const int nconv = ((M + kPPBM - 1) / kPPBM) * (COUTP / 128);
-    if (g_tap_mode < 5 || g_tap_mode > 13 || cached_rows8 > kPPSlabRows || nconv < pp_min)
+    if (g_tap_mode < 5 || g_tap_mode > 15 || cached_rows8 > kPPSlabRows || nconv < pp_min)
       return false;  // small batches: conv_pipe
     int nred = 0;
     WgradRed r{};
@@ -1421,7 +1421,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
     const char* v = getenv("RAG_CONV_PP192");
     return v && v[0] == '2';
   }();
-  if ((g_tap_mode >= 5 && g_tap_mode <= 13) && cached_rows8 <= kPPSlabRows && pp_fills &&
+  if ((g_tap_mode >= 5 && g_tap_mode <= 15) && cached_rows8 <= kPPSlabRows && pp_fills &&
       !pp192_all) {
     // ping-pong kernel: one block per CU; reduce blocks fill the CUs its last round leaves free
     const int nconv = ((M + kPPBM - 1) / kPPBM) * (COUTP / kBN);
@@ -1463,6 +1463,14 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
       conv_tap_pp_kernel<3, 0, 0, kNT, false, 3, kMT, 1, 1, 1><<<nconv + nred, 512, 0, stream>>>(
           x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
           nconv, r);
+    else if (g_tap_mode == 14)
+      conv_tap_pp_kernel<3, 0, 0, kNT, false, 3, kMT, 0, 0, 1><<<nconv + nred, 512, 0, stream>>>(
+          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
+          nconv, r);
+    else if (g_tap_mode == 15)
+      conv_tap_pp_kernel<4, 0, 0, kNT, false, 3, kMT, 1, 0, 1><<<nconv + nred, 512, 0, stream>>>(
+          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
+          nconv, r);
     else
       conv_tap_pp_kernel<3><<<nconv + nred, 512, 0, stream>>>(
           x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
@@ -1478,7 +1486,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
     return !(v && v[0] == '0');
   }();
   const int n192 = ((M + kBM - 1) / kBM) * (COUTP / kBN);
-  if (pp192 && g_tap_mode >= 5 && g_tap_mode <= 13 && n192 >= pp_min &&
+  if (pp192 && g_tap_mode >= 5 && g_tap_mode <= 15 && n192 >= pp_min &&
       cached_rows <= kPPSlabRows192) {
     int nred = 0;
     WgradRed r{};
@@ -1527,7 +1535,7 @@ bool rag_conv_tap_bn_ok(int M, int S, int WI, int shift, int CIN, int COUTP, int
   const char* e = getenv("RAG_PP_MIN_BLOCKS");
   const int pp_min = e ? atoi(e) : 200;
   const int nconv = ((M + kPPBM - 1) / kPPBM) * (COUTP / 128);
-  return g_tap_mode >= 5 && g_tap_mode <= 13 && KS == 3 && COUTP % kBN != 0 && COUTP % 128 == 0 &&
+  return g_tap_mode >= 5 && g_tap_mode <= 15 && KS == 3 && COUTP % kBN != 0 && COUTP % 128 == 0 &&
          CIN % kBK == 0 && CIN >= kBK && nconv >= pp_min &&
          max_slab_rows(S, WI, shift, kPPBM) <= kPPSlabRows;
 }

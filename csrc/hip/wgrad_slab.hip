@@ -120,7 +120,7 @@ __global__ void __launch_bounds__(64 * WS<N>::Waves)
 wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
                   float* __restrict__ part, float* __restrict__ bpart, int R, int WP, int GC,
                   int CIN, int spc, int CINP, const float* __restrict__ xcoef = nullptr,
-                  int S = 0, int pair5 = 0) {
+                  int S = 0, int pair5 = 0, int prio = 0) {
   using L = WS<N>;
   static_assert(KS == 3 || (KS == 5 && kBF && kMAP == 0 && !BNX), "5x5: fp16 map-0 partials");
   constexpr int kGrp = KS == 3 ? 1 : KS;  // blocks per (chunk, c-tile): kernel rows
@@ -268,6 +268,7 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
       }
     }
   }
+  if (prio == 2 && w >= kWaves - 4) __builtin_amdgcn_s_setprio(1);  // the last-dispatched waves
   for (int s = 0; s < nsteps; ++s) {
     // retire stage s; up to kNBUF-2 younger stages (2 or 3 glds of this wave each) stay in flight
     int young = nsteps - 1 - s;
@@ -294,12 +295,12 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
       if constexpr (BNX) {
         if (kk == 0 && xw && s + 1 < nsteps) xstore(s + 1);  // fetched at the end of step s-1
       }
-      __builtin_amdgcn_s_setprio(1);
+      if (prio == 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < NT; ++i)
 #pragma unroll
         for (int a = 0; a < NA; ++a) acc[i][a] = mfma16(fa[a], fb[i], acc[i][a]);
-      __builtin_amdgcn_s_setprio(0);
+      if (prio == 0) __builtin_amdgcn_s_setprio(0);
     }
     if constexpr (BNX) {
       // stage s+2 landed (s+3 stays in flight): fetch this lane's chunk for step s+1's xstore
@@ -815,9 +816,13 @@ int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpar
                                                                     CIN, spc, CINP);
     return (int)hipGetLastError();
   }
+  static const int wprio = [] {  // RAG_WGRAD_PRIO: 0 flips around MFMAs, 1 none, 2 static
+    const char* e = getenv("RAG_WGRAD_PRIO");
+    return e ? atoi(e) : 0;
+  }();
 #define RAG_WSLAB2(NB, BF, MP)                                                                 \
-  wgrad_slab_kernel<NB, BF, MP><<<grid, 64 * WS<kN>::Waves, 0, stream>>>(G, X, part, bpart, R, \
-                                                                        WP, GC, CIN, spc, CINP)
+  wgrad_slab_kernel<NB, BF, MP><<<grid, 64 * WS<kN>::Waves, 0, stream>>>(                      \
+      G, X, part, bpart, R, WP, GC, CIN, spc, CINP, nullptr, 0, 0, wprio)
 #define RAG_WSLAB(NB, BF) \
   if (mp) RAG_WSLAB2(NB, BF, 1); else RAG_WSLAB2(NB, BF, 0)
   const int mp = wslab_map();

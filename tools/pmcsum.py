@@ -49,13 +49,18 @@ def main(path, filters):
         m = {k: v / n for k, v in a.items() if not k.startswith("_")}
         out = ["%-70s n=%-4d dur_us=%.1f vgpr=%s agpr=%s lds=%s" % (
             short(name), n, m["dur"], a["_vgpr"], a["_agpr"], a["_lds"])]
-        if "GRBM_GUI_ACTIVE" in m and m["dur"] > 0:
-            clk = m["GRBM_GUI_ACTIVE"] / 8 / (m["dur"] * 1e-6) / 1e9
-            out.append("clk_GHz=%.2f" % clk)
+        if "SQ_BUSY_CYCLES" in m and m["dur"] > 0:
+            # SQ_BUSY_CYCLES is summed over the 32 shader engines' SQs (shader clock): kernel
+            # cycles = SQ_BUSY / 32 (the long elementwise kernels read 2.29-2.39 GHz this way, the
+            # GRBM-based quotient reads high below ~0.3 ms); MFMA busy cycles are summed over the
+            # 1024 SIMDs at 16 per v_mfma_f32_16x16x32_bf16 (checked against the conv's MFMA count)
+            cyc = m["SQ_BUSY_CYCLES"] / 32
+            out.append("clk_GHz=%.2f" % (cyc / (m["dur"] * 1e-6) / 1e9))
             if "SQ_VALU_MFMA_BUSY_CYCLES" in m:
-                # busy cycles are summed over all SIMDs (1024); kernel cycles = GUI_ACTIVE / 8
-                util = m["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / (m["GRBM_GUI_ACTIVE"] / 8)
-                out.append("mfma_busy=%.1f%%" % (100 * util))
+                out.append("mfma_busy=%.1f%%" % (100 * m["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / cyc))
+        elif "GRBM_GUI_ACTIVE" in m and m["dur"] > 0:
+            clk = m["GRBM_GUI_ACTIVE"] / 8 / (m["dur"] * 1e-6) / 1e9
+            out.append("clk_GHz(grbm)=%.2f" % clk)
         out.append(" ".join("%s=%.0f" % (k, v) for k, v in sorted(m.items()) if k != "dur"))
         print("  ".join(out))
 
