@@ -1266,8 +1266,12 @@ RAG_API int rag_conv_tap_mode(int mode) {
 // Mode (RAG_CONV_TAP / rag_conv_tap_mode): 0 off, 1 = 4-wave 192-pixel kernel (round-2 default),
 // 2 / 3 = 8-wave 384-pixel kernel with a 4- / 5-deep weight ring (measured slower: docs/KERNELS.md),
 // 4 = 8-wave 192-pixel kernel, four waves per SIMD (conv_tap16_kernel), 5 / 6 / 7 = ping-pong
-// 8-wave 384-pixel kernel with a 4- / 3- / 5-deep weight ring (conv_tap_pp_kernel; 6 = default),
-// 8 / 9 = the same with the weight loads issued inside the MFMA segment (measured slower).
+// 8-wave 384-pixel kernel with a 4- / 3- / 5-deep weight ring (conv_tap_pp_kernel; 6 = round 3),
+// 8 / 9 = the same with the weight loads issued inside the MFMA segment (measured slower),
+// 10 = mode 6 with the next chunk's slab loads spread over the taps, 11 = 10 + one weight slice
+// staged by the loader group, 12 = 10 + static priority for the second wave group (default),
+// 13 = 11 + 12, 14 = 6 + static priority, 15 = 12 with a 4-deep ring (3x3 192-channel layers;
+// the other shapes run the mode-6 kernels).
 int rag_launch_wgrad_slab_reduce(const WgradRed& r, hipStream_t stream);  // wgrad_slab.hip
 
 // bnc / mcoef (BN prologue / mask coefficients, conv_tap_pp_kernel BNP): only the 128-channel
@@ -1284,7 +1288,10 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
     return false;
   if (g_tap_mode < 0) {
     const char* e = getenv("RAG_CONV_TAP");
-    g_tap_mode = e ? atoi(e) : 6;  // ping-pong, 3-deep ring: profiles/conv_pp_r3.txt
+    // ping-pong, 3-deep ring, slab loads spread over the chunk's taps, static priority for the
+    // second wave group (mode 12): SL 111.7-111.9k -> 113.6-113.9k positions/s on one box
+    // (profiles/conv_variants_r4b.txt)
+    g_tap_mode = e ? atoi(e) : 12;
   }
   // 192-multiple widths: 96 x 96 wave tiles (NT = 6); 128-multiple widths (ResnetPolicy's and
   // the reference CNNPolicy's default 128 filters) only on the ping-pong kernel, 96 x 64 (NT = 4)
@@ -1347,18 +1354,11 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
       r = *red;
       nred = std::max(8, (256 - nconv % 256) % 256);
     }
-    if (w192 && pair5 && g_tap_mode >= 10)
-      conv_tap_pp_kernel<3, 0, 0, 6, false, 5, kMT, 1, 0, 0, 1><<<nconv + nred, 512, 0,
-                                                                   stream>>>(
-          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
-          nconv, r);
-    else if (w192 && pair5)
+    // (the spread / static-priority 3x3 variants measured slower on the 5x5 layer: 52.9-53.7
+    // vs 49.9 us, profiles/conv_variants_r4b.txt; every mode runs the plain ping-pong here)
+    if (w192 && pair5)
       conv_tap_pp_kernel<3, 0, 0, 6, false, 5, kMT, 0, 0, 0, 1><<<nconv + nred, 512, 0,
                                                                    stream>>>(
-          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
-          nconv, r);
-    else if (w192 && g_tap_mode >= 10)
-      conv_tap_pp_kernel<3, 0, 0, 6, false, 5, kMT, 1><<<nconv + nred, 512, 0, stream>>>(
           x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
           nconv, r);
     else if (w192)
@@ -1530,7 +1530,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
 bool rag_conv_tap_bn_ok(int M, int S, int WI, int shift, int CIN, int COUTP, int KS) {
   if (g_tap_mode < 0) {
     const char* e = getenv("RAG_CONV_TAP");
-    g_tap_mode = e ? atoi(e) : 6;
+    g_tap_mode = e ? atoi(e) : 12;
   }
   const char* e = getenv("RAG_PP_MIN_BLOCKS");
   const int pp_min = e ? atoi(e) : 200;
