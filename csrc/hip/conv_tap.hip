@@ -1365,6 +1365,11 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
       conv_tap_pp_kernel<3, 0, 0, 6, false, 5><<<nconv + nred, 512, 0, stream>>>(
           x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
           nconv, r);
+    else if (pair5)  // 128 filters (ResnetPolicy's input layer)
+      conv_tap_pp_kernel<3, 0, 0, 4, false, 5, kMT, 0, 0, 0, 1><<<nconv + nred, 512, 0,
+                                                                   stream>>>(
+          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
+          nconv, r);
     else
       conv_tap_pp_kernel<3, 0, 0, 4, false, 5><<<nconv + nred, 512, 0, stream>>>(
           x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,

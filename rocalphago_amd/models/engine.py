@@ -353,7 +353,7 @@ class ResTrunk(_PackedConvs):
         S, K = self.S, self.K
         s0 = self.specs[0]
         ops.conv_igemm(self.xin[:B], self._wf[0], self._bias[0], self.A[0][:B], B, S,
-                       self.hin[0], 1, s0.cinp, s0.coutp, s0.ks, False)
+                       self.hin[0], 1, s0.cinp, s0.coutp, s0.ks, False, cin=s0.cin)
         j = 0
         nb = len(self.bns)
         self._fused = [self._prologue_ok(jj, B) for jj in range(nb)]

@@ -28,7 +28,7 @@ def ops():
                                              (4, 192, 32, 1, 19), (1, 12, 16, 5, 9),
                                              (2, 64, 96, 3, 7), (130, 192, 192, 3, 19),
                                              (128, 48, 192, 5, 19), (256, 48, 192, 5, 19),
-                                             (256, 40, 192, 5, 19)])
+                                             (256, 40, 192, 5, 19), (256, 48, 128, 5, 19)])
 def test_conv_forward(ops, B, cin, cout, ks, S):
     dev = torch.device("cuda")
     torch.manual_seed(0)
