@@ -777,8 +777,15 @@ constexpr int kPPSlabRows192x5 = 448;    // 192-pixel blocks, 5x5 taps (<= 424 r
 // chunk holds only 16 real channels, so its steps pair two taps -- lanes of k-quads 0/1 read
 // channels 32..47 of tap t, quads 2/3 the same channels of tap t+1 (channels 48..63 of tap 24,
 // zero padding, for the last, unpaired tap) -- 25 + 13 = 38 K-steps instead of 50.
+// K2 (the 128-channel 3x3 layers, NT = 4): each barrier pair covers two K-steps. A wave's 24
+// MFMAs per step are shorter than its 10 fragment reads plus two barriers (the loop ran ~890
+// cycles per phase for 384 MFMA cycles), so both groups hold two steps' fragments (80 VGPRs
+// beside the 96 accumulators) and a phase is 48 MFMAs against 20 reads. The weight ring is
+// NB = 6 tiles (two being read, two landed, two in flight); the next chunk's slab is issued at
+// tap 1 (the super-step holding tap 0 may still read the chunk before, tap 8) and completes --
+// and, with BNP, is transformed over taps 4..7 -- before the super-step that reads its tap 0.
 template <int NB, int DIAG = 0, int ISSUE = 0, int NT = kNT, bool BNP = false, int KS = 3,
-          int MT = kMT, int SPREAD = 0, int WG0 = 0, int PRIO = 0, int PAIR = 0>
+          int MT = kMT, int SPREAD = 0, int WG0 = 0, int PRIO = 0, int PAIR = 0, int K2 = 0>
 __global__ void __launch_bounds__(512, MT == kMT ? 1 : 4)
 conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                    const float* __restrict__ bias, bf16* __restrict__ Y,
@@ -792,6 +799,8 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
   constexpr bool PR = PAIR && KS == 5;
   static_assert(!PAIR || (KS == 5 && !BNP && !ISSUE), "tap pairing: the 5x5 input layer");
   static_assert(WG0 >= 0 && PB1 >= 1 && (WG0 == 0 || (!BNP && !ISSUE)), "WG0 split");
+  static_assert(!K2 || (KS == 3 && MT == kMT && NB >= 6 && !DIAG && !ISSUE && !SPREAD && !WG0 &&
+                        !PAIR), "two K-steps per barrier pair: the plain 3x3 ping-pong");
   constexpr int TAPS = KS * KS;  // 9 (3x3) or 25 (the 5x5 layers: SL input, ResNet unit 0)
   // slab rows: 640 cover any 384-pixel run's 9-tap window (554), 768 its 25-tap one (748)
   // MT = 3: 192-pixel blocks (sub-chip grids, e.g. 128-game self-play passes): <= 298 rows
@@ -945,11 +954,8 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
   const int cchunks = CIN / kBK;
   const int nsteps = PR ? TAPS + (TAPS + 1) / 2 : TAPS * cchunks;  // PR: cchunks == 2
   bf16x8 xa[MT], wb[NT];
-  auto read_frags = [&](int s) {
-    if constexpr (DIAG & 2) {
-      asm volatile("" : "+v"(xa[0]), "+v"(wb[0]));
-      return;
-    }
+  bf16x8 xa2[K2 ? MT : 1], wb2[K2 ? NT : 1];  // K2: the second step's fragments
+  auto read_into = [&](int s, bf16x8* xa, bf16x8* wb) {
     int q, t;
     decode(s, q, t);
     const bf16* slab = lds + (q & 1) * SLAB;
@@ -968,7 +974,34 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
     }
 #pragma unroll
     for (int j = 0; j < NT; ++j) wb[j] = *reinterpret_cast<const bf16x8*>(bt + boffs[j]);
+  };
+  auto read_frags = [&](int s) {
+    if constexpr (DIAG & 2) {
+      asm volatile("" : "+v"(xa[0]), "+v"(wb[0]));
+      return;
+    }
+    read_into(s, xa, wb);
     lds_reads_done();  // retire this burst before the wave's next barrier (WAR on the LDS)
+  };
+  // K2: the fragments of steps s (and s + 1 when has1), one retire for both bursts
+  auto read_pair = [&](int s, bool has1) {
+    read_into(s, xa, wb);
+    if (has1) read_into(s + 1, xa2, wb2);
+    lds_reads_done();
+  };
+  auto mfmas_pair = [&](bool has1) {
+    if constexpr (!PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int i = 0; i < MT; ++i) acc[j][i] = mfma16(wb[j], xa[i], acc[j][i]);
+    if (has1) {
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int i = 0; i < MT; ++i) acc[j][i] = mfma16(wb2[j], xa2[i], acc[j][i]);
+    }
+    if constexpr (!PRIO) __builtin_amdgcn_s_setprio(0);
   };
   auto mfmas = [&]() {
     if constexpr (!PRIO) __builtin_amdgcn_s_setprio(1);
@@ -1020,7 +1053,82 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
   // per wave per chunk, at tap 0), group 1 the weight tiles (3 glds per wave per step, after its
   // fragment reads). Each group waits only for its own loads, before the barrier that precedes
   // the first read of that data (always group 0's, at the next X barrier).
-  if (grp == 0) {
+  if constexpr (K2) {
+    const int nsup = (nsteps + 1) / 2;
+    if (grp == 0) {
+      stage_a(0);
+      wait_vm<0>();
+      bn_slab(0, 0, AL);
+#pragma unroll 1
+      for (int u = 0; u < nsup; ++u) {
+        const int s0 = 2 * u;
+        const bool has1 = s0 + 1 < nsteps;
+        __builtin_amdgcn_s_barrier();  // X_u
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {  // slab(q+1) at tap 1: its buffer's last reader is tap 8
+          int q, t;
+          decode(s0 + h, q, t);
+          if ((h == 0 || has1) && t == 1 && q + 1 < cchunks) stage_a(q + 1);
+        }
+        read_pair(s0, has1);
+        __builtin_amdgcn_s_barrier();  // Y_u
+        asm volatile("" ::: "memory");
+        mfmas_pair(has1);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          if (h == 1 && !has1) break;
+          int q, t;
+          decode(s0 + h, q, t);
+          if (q + 1 >= cchunks) continue;
+          if constexpr (BNP) {
+            // slab(q+1), issued at tap 1, transformed over taps 4..7: done before the super-step
+            // holding tap 8 (which may also hold the next chunk's tap 0)
+            if (t >= 4 && t <= 7) {
+              if (t == 4) wait_vm<0>();
+              bn_slab(q + 1, (t - 4) * AL / 4, (t - 3) * AL / 4);
+              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            }
+          } else {
+            if (t == 7) wait_vm<0>();
+          }
+        }
+      }
+    } else {
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+      constexpr int DA = NB - 2;  // steps staged ahead of the super-step being read
+#pragma unroll
+      for (int k = 0; k < DA; ++k)
+        if (k < nsteps) stage_b(k, 0, PB1);
+      {  // B(0), B(1) complete
+        const int last = nsteps - 1 < DA - 1 ? nsteps - 1 : DA - 1;
+        const int need = nsteps - 1 < 1 ? nsteps - 1 : 1;
+        wait_vm_rt((last - need) * PB1);
+      }
+      bool had1 = false;
+#pragma unroll 1
+      for (int u = 0; u < nsup; ++u) {
+        const int s0 = 2 * u;
+        const bool has1 = s0 + 1 < nsteps;
+        __builtin_amdgcn_s_barrier();  // X_u
+        asm volatile("" ::: "memory");
+        if (u > 0) mfmas_pair(had1);  // super-step u - 1, beside group 0's reads of u
+        __builtin_amdgcn_s_barrier();  // Y_u
+        asm volatile("" ::: "memory");
+        read_pair(s0, has1);  // beside group 0's MFMAs of u
+        had1 = has1;
+        if (s0 + DA < nsteps) stage_b(s0 + DA, 0, PB1);
+        if (s0 + DA + 1 < nsteps) stage_b(s0 + DA + 1, 0, PB1);
+        // B(s0 + 2), B(s0 + 3) complete before X_{u+1}: younger are the steps up to s0 + DA + 1
+        const int lastc = s0 + DA + 1 < nsteps - 1 ? s0 + DA + 1 : nsteps - 1;
+        const int need = s0 + 3 < nsteps - 1 ? s0 + 3 : nsteps - 1;
+        const int yb = lastc - need;
+        wait_vm_rt(yb > 0 ? yb * PB1 : 0);
+      }
+      mfmas_pair(had1);
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+    }
+  } else if (grp == 0) {
     stage_a(0);
     if constexpr (WG0 > 0) {
 #pragma unroll
@@ -1186,6 +1294,7 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
 }
 
 int g_tap_mode = -1;  // -1: read RAG_CONV_TAP on first use (default on)
+int g_conv_k2 = -1;   // -1: read RAG_CONV_K2 on first use (128-channel 3x3 ping-pong variant)
 int g_ep_lds_override = -1;  // rag_conv_ep_lds(): A/B switch of conv_tap_kernel's epilogue
 
 // Worst-case slab extent of a bm-pixel run (host check of the kernels' slab-row assumptions).
@@ -1250,6 +1359,12 @@ RAG_API int rag_conv_diag_segments(long long* host, int nblocks) {
 RAG_API int rag_conv_ep_lds(int on) {
   const int old = g_ep_lds_override;
   g_ep_lds_override = on;
+  return old;
+}
+
+RAG_API int rag_conv_k2(int v) {
+  const int old = g_conv_k2;
+  g_conv_k2 = v;
   return old;
 }
 
@@ -1411,14 +1526,26 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
       r = *red;
       nred = std::max(8, (256 - nconv % 256) % 256);
     }
-    if (bnc)
-      conv_tap_pp_kernel<3, 0, 0, 4, true><<<nconv + nred, 512, 0, stream>>>(
-          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
-          nconv, r, bnc, mcoef, spart, smean);
-    else
-      conv_tap_pp_kernel<3, 0, 0, 4><<<nconv + nred, 512, 0, stream>>>(
-          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
-          nconv, r, nullptr, mcoef, spart, smean);
+    if (g_conv_k2 < 0) {
+      const char* e = getenv("RAG_CONV_K2");
+      g_conv_k2 = e ? atoi(e) : 0;
+    }
+    // K2 (two K-steps per barrier pair, rag_conv_k2): 1 = plain, 2 = + static group-1 priority
+#define RAG_PP128(BNPV, PRIOV, K2V, BNC)                                                          \
+  conv_tap_pp_kernel<K2V ? 6 : 3, 0, 0, 4, BNPV, 3, kMT, 0, 0, PRIOV, 0, K2V>                     \
+      <<<nconv + nred, 512, 0, stream>>>(x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN,   \
+                                         COUTP, YC, relu, HM, total_rows, nconv, r, BNC, mcoef,  \
+                                         spart, smean)
+    if (bnc) {
+      if (g_conv_k2 == 1) RAG_PP128(true, 0, 1, bnc);
+      else if (g_conv_k2 == 2) RAG_PP128(true, 1, 1, bnc);
+      else RAG_PP128(true, 0, 0, bnc);
+    } else {
+      if (g_conv_k2 == 1) RAG_PP128(false, 0, 1, nullptr);
+      else if (g_conv_k2 == 2) RAG_PP128(false, 1, 1, nullptr);
+      else RAG_PP128(false, 0, 0, nullptr);
+    }
+#undef RAG_PP128
     return true;
   }
   const bool pp_fills = ((M + kPPBM - 1) / kPPBM) * (COUTP / kBN) >= pp_min;

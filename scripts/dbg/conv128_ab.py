@@ -1,6 +1,7 @@
 """Per-kernel timing of the 3x3 conv forms at 128 and 192 channels, B=256: forward (bias+ReLU,
 LDS-staged epilogue), forward with residual (register epilogue), dgrad with ReLU mask, wgrad
-(slab, reduction standalone). Variants: tap mode 6 (ping-pong) vs 0 (conv_pipe)."""
+(slab, reduction standalone). Variants: tap mode 6 (ping-pong) vs 0 (conv_pipe); at 128
+channels also the two-K-steps-per-barrier-pair kernel (K2 env list, default "0,1,2")."""
 import json
 import os
 import sys
@@ -55,10 +56,20 @@ for C in (128, 192):
     if C == 128:  # BN prologue forms (ResnetPolicy)
         coef = torch.zeros(3, S, device=dev)
         coef[0] = 1.0
-        out["c128_bn_fwd_res_us"] = round(timeit(lambda: ops.conv_igemm_bn(
-            xp, wf, None, y, B, S, C, C, False, bn_coef=coef, residual=rp)), 2)
-        out["c128_bn_dgrad_us"] = round(timeit(lambda: ops.conv_igemm_bn(
-            g, wb, None, y, B, S, C, C, False, mask=xp, mask_coef=coef)), 2)
+        cases["bn_fwd_res"] = lambda: ops.conv_igemm_bn(
+            xp, wf, None, y, B, S, C, C, False, bn_coef=coef, residual=rp)
+        cases["bn_dgrad"] = lambda: ops.conv_igemm_bn(
+            g, wb, None, y, B, S, C, C, False, mask=xp, mask_coef=coef)
+        for rep in range(2):  # interleaved repeats
+            for k2 in [int(v) for v in os.environ.get("K2", "0,1,2").split(",")]:
+                _lib().rag_conv_k2(k2)
+                for k, fn in cases.items():
+                    key = "c128_%s_k2_%d_us" % (k, k2)
+                    t = round(timeit(fn), 2)
+                    out[key] = min(out.get(key, 1e9), t)
+        _lib().rag_conv_k2(0)
+        out["c128_bn_fwd_res_us"] = out["c128_bn_fwd_res_k2_0_us"]
+        out["c128_bn_dgrad_us"] = out["c128_bn_dgrad_k2_0_us"]
         out["c128_bn_wgrad_us"] = round(timeit(lambda: ops.conv_wgrad(
             g, xp, dw, db, B, S, 1, C, C, C, C, 3, work=work, hg=1, xcoef=coef)), 2)
         h = ops.PendingReduction()

@@ -355,3 +355,62 @@ def test_bn_apply_with_folded_finalize_matches_two_launches(ops, residual):
     d = (out.float() - ref.float()).abs()
     assert d.max().item() <= 1e-2 * ref.float().abs().max().item()
     assert out[:, 0].abs().max().item() == 0 and out[:, :, -1].abs().max().item() == 0
+
+
+@pytest.mark.parametrize("k2", [1, 2])
+def test_conv128_two_step_variant_bit_identical(ops, k2):
+    """The 128-channel ping-pong kernel with two K-steps per barrier pair (rag_conv_k2) keeps
+    every accumulator's MFMA order, so its outputs -- forward with bias+ReLU, with a residual,
+    masked dgrad, and the BN-prologue forward / dgrad with their column statistics -- equal the
+    one-step kernel's bit for bit; the forward also against fp32 PyTorch."""
+    from rocalphago_amd.ops.hipops import _lib
+    dev = "cuda"
+    torch.manual_seed(11)
+    B, C, S = 256, 128, 19
+    x = bfr(torch.randn(B, C, S, S, device=dev)).relu()
+    w = torch.randn(C, C, 3, 3, device=dev) * 0.05
+    b = torch.randn(C, device=dev) * 0.1
+    xp = ops.pack_nchw(x, 1, C)
+    rp = ops.pack_nchw(bfr(torch.randn(B, C, S, S, device=dev)), 1, C)
+    gp = ops.pack_nchw(bfr(torch.randn(B, C, S, S, device=dev)), 1, C)
+    wf, wb = ops.pack_weights(w, C, C, wb=torch.empty(9, C, C, dtype=torch.bfloat16, device=dev))
+    coef = torch.zeros(3, S, device=dev)
+    coef[0] = torch.rand(S, device=dev) + 0.5
+    coef[2] = torch.randn(S, device=dev) * 0.3
+    mean = torch.randn(S, device=dev) * 0.1
+    nblk = ops.conv_bn_stat_blocks(B, S, C)
+
+    def run():
+        outs = []
+        for form in range(5):
+            y = ops.alloc_padded(B, S, 1, C, dev)
+            part = torch.zeros(nblk, 2, S, device=dev)
+            if form == 0:
+                ops.conv_igemm(xp, wf, b, y, B, S, 1, 1, C, C, 3, True)
+            elif form == 1:
+                ops.conv_igemm(xp, wf, None, y, B, S, 1, 1, C, C, 3, False, residual=rp)
+            elif form == 2:
+                ops.conv_igemm(gp, wb, None, y, B, S, 1, 1, C, C, 3, False, mask=xp)
+            elif form == 3:
+                ops.conv_igemm_bn(xp, wf, b, y, B, S, C, C, False, bn_coef=coef, residual=rp,
+                                  stat_part=part)
+            else:
+                ops.conv_igemm_bn(gp, wb, None, y, B, S, C, C, False, mask=xp, mask_coef=coef,
+                                  stat_part=part, stat_mean=mean)
+            outs.append((y.clone(), part.clone()))
+        torch.cuda.synchronize()
+        return outs
+
+    old = _lib().rag_conv_k2(0)
+    try:
+        ref = run()
+        _lib().rag_conv_k2(k2)
+        got = run()
+    finally:
+        _lib().rag_conv_k2(old)
+    for form, ((yr, pr), (yg, pg)) in enumerate(zip(ref, got)):
+        assert torch.equal(yr, yg), form
+        assert torch.equal(pr, pg), form
+    want = F.relu(F.conv2d(x, bfr(w), b, padding=1))
+    got0 = ops.unpack(got[0][0], C, 1)
+    assert (got0 - want).abs().max().item() < 2e-2 * want.abs().max().item()
