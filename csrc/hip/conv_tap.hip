@@ -41,6 +41,10 @@ constexpr int kBL = kBN / 64;         // weight glds per wave
 
 __device__ __forceinline__ int swz4(int row) { return ((row >> 2) & 1) << 1; }
 
+template <int V> struct IntC {
+  static constexpr int value = V;
+};
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -784,8 +788,17 @@ constexpr int kPPSlabRows192x5 = 448;    // 192-pixel blocks, 5x5 taps (<= 424 r
 // NB = 6 tiles (two being read, two landed, two in flight); the next chunk's slab is issued at
 // tap 1 (the super-step holding tap 0 may still read the chunk before, tap 8) and completes --
 // and, with BNP, is transformed over taps 4..7 -- before the super-step that reads its tap 0.
+// RS (register staging): the loop's staging goes through VGPRs instead of LDS-DMA. A
+// global_load_lds piece costs 100-230 issue cycles inside a read phase (segment accounting:
+// group 1's 2-3 weight pieces + wait took 427-519 cycles per step, group 0's slab pieces ~250);
+// a global_load_dwordx4 issues in a few cycles and its ds_write_b128 lands a step later.
+// RS = 1: group 1 loads the weight tile of step s+2 into registers after its fragment reads of
+// step s and writes it to the ring at step s+1; RS = 2: also the next chunk's slab, two pieces
+// per tap loaded after group 0's MFMA issue at taps 0..4 and written (BNP: transformed in
+// registers, no LDS round trip) a tap later. Chunk 0's slab stays LDS-DMA (prologue).
 template <int NB, int DIAG = 0, int ISSUE = 0, int NT = kNT, bool BNP = false, int KS = 3,
-          int MT = kMT, int SPREAD = 0, int WG0 = 0, int PRIO = 0, int PAIR = 0, int K2 = 0>
+          int MT = kMT, int SPREAD = 0, int WG0 = 0, int PRIO = 0, int PAIR = 0, int K2 = 0,
+          int RS = 0>
 __global__ void __launch_bounds__(512, MT == kMT ? 1 : 4)
 conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                    const float* __restrict__ bias, bf16* __restrict__ Y,
@@ -801,6 +814,7 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
   static_assert(WG0 >= 0 && PB1 >= 1 && (WG0 == 0 || (!BNP && !ISSUE)), "WG0 split");
   static_assert(!K2 || (KS == 3 && MT == kMT && NB >= 6 && !DIAG && !ISSUE && !SPREAD && !WG0 &&
                         !PAIR), "two K-steps per barrier pair: the plain 3x3 ping-pong");
+  static_assert(!RS || (!ISSUE && !WG0 && !PAIR && !K2 && !(DIAG & 3)), "register staging");
   constexpr int TAPS = KS * KS;  // 9 (3x3) or 25 (the 5x5 layers: SL input, ResNet unit 0)
   // slab rows: 640 cover any 384-pixel run's 9-tap window (554), 768 its 25-tap one (748)
   // MT = 3: 192-pixel blocks (sub-chip grids, e.g. 128-game self-play passes): <= 298 rows
@@ -887,11 +901,11 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
       }
     }
   };
-  const bf16* bsrc[PPBL];
+  int bofs[PPBL];  // this lane's weight-row element offsets (32-bit: fewer live VGPRs)
 #pragma unroll
   for (int k = 0; k < PPBL; ++k) {
     const int r = (wl + 4 * k) * 16 + lrow;
-    bsrc[k] = Wt + (long)(n0 + r) * CIN + ((lcol ^ swz4(r)) * 8);
+    bofs[k] = (n0 + r) * CIN + ((lcol ^ swz4(r)) * 8);
   }
   auto stage_a = [&](int q, int k0 = 0, int k1 = 1 << 20) {  // chunk q, pieces k0 .. k1-1
     bf16* dst = lds + (q & 1) * SLAB;
@@ -926,7 +940,7 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
     if (PR && q == 1 && vhi && t + 1 < TAPS) off += tap_stride - 16;
 #pragma unroll
     for (int k = 0; k < PPBL; ++k)
-      if (k >= k0 && k < k1) glds16(bsrc[k] + off, dst + (wl + 4 * k) * 16 * kBK);
+      if (k >= k0 && k < k1) glds16(Wt + (bofs[k] + off), dst + (wl + 4 * k) * 16 * kBK);
   };
 
   const int frow = lane & 15;
@@ -1022,7 +1036,7 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
         int q, t;
         decode(sb, q, t);
         bf16* dst = lds + 2 * SLAB + (sb % NB) * BTile;
-        glds16(bsrc[j] + t * tap_stride + q * kBK, dst + (wl + 4 * j) * 16 * kBK);
+        glds16(Wt + (bofs[j] + t * tap_stride + q * kBK), dst + (wl + 4 * j) * 16 * kBK);
       }
     }
     __builtin_amdgcn_s_setprio(0);
@@ -1126,6 +1140,149 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
         wait_vm_rt(yb > 0 ? yb * PB1 : 0);
       }
       mfmas_pair(had1);
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+    }
+  } else if constexpr (RS > 0) {
+    constexpr int SLT = (AL + 1) / 2;  // RS = 2: slab piece pairs, loaded at taps 0 .. SLT-1
+    static_assert(RS < 2 || SLT + 1 < TAPS, "slab pieces land before the chunk's last tap");
+    if (grp == 0) {
+      stage_a(0);
+      wait_vm<0>();
+      bn_slab(0, 0, AL);
+      bf16x8 sreg[2];
+      // pieces 2p, 2p+1 of chunk q's slab -> sreg
+      auto slab_get = [&](int q, int p) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int k = 2 * p + e;
+          if (k >= AL) continue;
+          const int r = (wl + 4 * k) * 16 + lrow;
+          long g = base + r;
+          g = g < total_rows ? g : total_rows - 1;
+          sreg[e] = *reinterpret_cast<const bf16x8*>(X + g * CIN + ((lcol ^ swz4(r)) * 8) +
+                                                      q * kBK);
+        }
+      };
+      // sreg -> the slab buffer of chunk q (BNP: U = ReLU(cx x + cc) of the piece's row). The
+      // piece index is a template constant (a switch on the pair), so pcx / pcc stay registers
+      // (a runtime-indexed form was rewritten by the compiler into scratch accesses).
+      auto put_piece = [&](bf16* dst, auto kc) {
+        constexpr int k = decltype(kc)::value;
+        if constexpr (k < AL) {
+          bf16x8 v = sreg[k & 1];
+          if constexpr (BNP) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = (bf16)fmaxf(fmaf(pcx[k], (float)v[e], pcc[k]), 0.f);
+          }
+          *reinterpret_cast<bf16x8*>(dst + (wl + 4 * k) * 16 * kBK + lane * 8) = v;
+        }
+      };
+      auto slab_put = [&](int q, int p) {
+        bf16* dst = lds + (q & 1) * SLAB;
+        static_assert(AL <= 12, "slab_put covers six piece pairs");
+        switch (p) {
+          case 0: put_piece(dst, IntC<0>{}); put_piece(dst, IntC<1>{}); break;
+          case 1: put_piece(dst, IntC<2>{}); put_piece(dst, IntC<3>{}); break;
+          case 2: put_piece(dst, IntC<4>{}); put_piece(dst, IntC<5>{}); break;
+          case 3: put_piece(dst, IntC<6>{}); put_piece(dst, IntC<7>{}); break;
+          case 4: put_piece(dst, IntC<8>{}); put_piece(dst, IntC<9>{}); break;
+          default: put_piece(dst, IntC<10>{}); put_piece(dst, IntC<11>{}); break;
+        }
+      };
+#pragma unroll 1
+      for (int s = 0; s < nsteps; ++s) {
+        int q, t;
+        decode(s, q, t);
+        const bool more = q + 1 < cchunks;
+        const long long c1 = now();
+        __builtin_amdgcn_s_barrier();  // X_s
+        asm volatile("" ::: "memory");
+        const long long c2 = now();
+        if constexpr (RS == 1) {  // slab by LDS-DMA, as the default loop
+          if constexpr (SPREAD && !BNP) {
+            if (t < TAPS - 1 && more) stage_a(q + 1, t * AL / (TAPS - 1), (t + 1) * AL / (TAPS - 1));
+          } else {
+            if (t == 0 && more) stage_a(q + 1);
+          }
+        }
+        read_frags(s);
+        const long long c3 = now();
+        __builtin_amdgcn_s_barrier();  // Y_s
+        asm volatile("" ::: "memory");
+        const long long c4 = now();
+        mfmas();
+        const long long c5 = now();
+        if constexpr (RS == 1) {
+          if constexpr (BNP) {
+            if (t >= 4 && more) {
+              if (t == 4) wait_vm<0>();
+              bn_slab(q + 1, 2 * (t - 4), 2 * (t - 4) + 2);
+            }
+          } else {
+            if (t == TAPS - 1 && more) wait_vm<0>();
+          }
+        } else if (more) {
+          // behind the MFMA issue: last tap's pieces -> LDS, this tap's pieces -> registers
+          if (t >= 1 && t <= SLT) slab_put(q + 1, t - 1);
+          if (t < SLT) slab_get(q + 1, t);
+        }
+        const long long c6 = now();
+        if constexpr (DIAG & 8) {
+          acc_t[0] += c2 - c1;
+          acc_t[1] += c3 - c2;
+          acc_t[2] += c4 - c3;
+          acc_t[3] += c5 - c4;
+          acc_t[4] += c6 - c5;
+        }
+      }
+    } else {
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+      bf16x8 wreg[PB1];
+      auto w_get = [&](int s) {
+        int q, t;
+        decode(s, q, t);
+        const long off = t * tap_stride + q * kBK;
+#pragma unroll
+        for (int k = 0; k < PB1; ++k) wreg[k] = *reinterpret_cast<const bf16x8*>(Wt + (bofs[k] + off));
+      };
+      auto w_put = [&](int s) {
+        bf16* dst = lds + 2 * SLAB + (s % NB) * BTile;
+#pragma unroll
+        for (int k = 0; k < PB1; ++k)
+          *reinterpret_cast<bf16x8*>(dst + (wl + 4 * k) * 16 * kBK + lane * 8) = wreg[k];
+      };
+      w_get(0);
+      w_put(0);
+      if (nsteps > 1) w_get(1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // B(0) in the ring before X_0
+#pragma unroll 1
+      for (int s = 0; s < nsteps; ++s) {
+        const long long c0 = now();
+        __builtin_amdgcn_s_barrier();  // X_s
+        asm volatile("" ::: "memory");
+        const long long c1 = now();
+        if (s > 0) mfmas();  // step s - 1, beside group 0's reads of step s
+        const long long c2 = now();
+        __builtin_amdgcn_s_barrier();  // Y_s
+        asm volatile("" ::: "memory");
+        const long long c3 = now();
+        read_into(s, xa, wb);  // beside group 0's MFMAs of step s
+        const long long c4 = now();
+        // B(s+1) (loaded a step ago) -> its ring slot (last read at step s+1-NB); B(s+2) -> regs;
+        // the fragment-read retire below also retires the ds_write before X_{s+1}
+        if (s + 1 < nsteps) w_put(s + 1);
+        if (s + 2 < nsteps) w_get(s + 2);
+        lds_reads_done();
+        const long long c5 = now();
+        if constexpr (DIAG & 8) {
+          acc_t[0] += c1 - c0;
+          acc_t[1] += c2 - c1;
+          acc_t[2] += c3 - c2;
+          acc_t[3] += c4 - c3;
+          acc_t[4] += c5 - c4;
+        }
+      }
+      mfmas();
       if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     }
   } else if (grp == 0) {
@@ -1295,6 +1452,14 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
 
 int g_tap_mode = -1;  // -1: read RAG_CONV_TAP on first use (default on)
 int g_conv_k2 = -1;   // -1: read RAG_CONV_K2 on first use (128-channel 3x3 ping-pong variant)
+int g_conv_rs = -1;   // -1: read RAG_CONV_RS on first use (register staging, 3x3 ping-pong)
+int conv_rs() {
+  if (g_conv_rs < 0) {
+    const char* e = getenv("RAG_CONV_RS");
+    g_conv_rs = e ? atoi(e) : 0;
+  }
+  return g_conv_rs;
+}
 int g_ep_lds_override = -1;  // rag_conv_ep_lds(): A/B switch of conv_tap_kernel's epilogue
 
 // Worst-case slab extent of a bm-pixel run (host check of the kernels' slab-row assumptions).
@@ -1315,23 +1480,52 @@ long long* g_stamps = nullptr;
 
 // Diagnostic launches of the ping-pong kernel (results are WRONG for diag 1-3): diag bit 0 = no
 // staging, bit 1 = no fragment reads; every diag launch records per-block (cycles, 100 MHz ticks)
-// of the main loop, read back with rag_conv_diag_stamps. 3x3 forward/dgrad shapes only.
+// of the main loop, read back with rag_conv_diag_stamps; bit 4 = the 128-channel kernel. 3x3
+// forward/dgrad shapes only.
 RAG_API int rag_conv_pp_diag(int diag, const void* X, const void* W, const float* bias, void* Y,
                              const void* mask, int B, int S, int HI, int HO, int CIN, int COUTP,
                              int YC, int relu, int HM, hipStream_t stream) {
   if (!g_stamps && hipMalloc(&g_stamps, 16 * 4096 * sizeof(long long)) != hipSuccess) return -3;
   const int M = B * S * S, WI = S + 2 * HI, WO = S + 2 * HO, shift = HI - 1;
-  const int nconv = ((M + kPPBM - 1) / kPPBM) * (COUTP / kBN);
-  if (nconv > 4096 || COUTP % kBN || CIN % kBK) return -1;
+  const bool n128 = diag & 16;  // the 128-channel kernel (NT = 4, 3-deep ring)
+  const int rsd = (diag >> 5) & 3;  // bits 5-6: register staging (timing builds 4 / 12 only)
+  const int BNW = n128 ? 128 : kBN;
+  const int nconv = ((M + kPPBM - 1) / kPPBM) * (COUTP / BNW);
+  if (nconv > 4096 || COUTP % BNW || CIN % kBK) return -1;
   const long total = (long)B * WI * WI;
   const bf16 *x = (const bf16*)X, *w = (const bf16*)W, *mk = (const bf16*)mask;
   bf16* y = (bf16*)Y;
   WgradRed r{};
 #define RAG_PPD(D)                                                                               \
-  conv_tap_pp_kernel<4, D><<<nconv, 512, 0, stream>>>(x, w, bias, y, mk, nullptr, M, S, WI,      \
-                                                      shift, WO, HO, CIN, COUTP, YC, relu, HM,  \
-                                                      total, nconv, r, nullptr, nullptr, \
-                                                      nullptr, nullptr, g_stamps)
+  if (n128)                                                                                      \
+    conv_tap_pp_kernel<3, D, 0, 4><<<nconv, 512, 0, stream>>>(                                   \
+        x, w, bias, y, mk, nullptr, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total,    \
+        nconv, r, nullptr, nullptr, nullptr, nullptr, g_stamps);                                 \
+  else                                                                                           \
+    conv_tap_pp_kernel<4, D><<<nconv, 512, 0, stream>>>(x, w, bias, y, mk, nullptr, M, S, WI,    \
+                                                        shift, WO, HO, CIN, COUTP, YC, relu, HM, \
+                                                        total, nconv, r, nullptr, nullptr,       \
+                                                        nullptr, nullptr, g_stamps)
+#define RAG_PPDR(D, RSV)                                                                          \
+  if (n128)                                                                                      \
+    conv_tap_pp_kernel<3, D, 0, 4, false, 3, kMT, 0, 0, 0, 0, 0, RSV><<<nconv, 512, 0, stream>>>( \
+        x, w, bias, y, mk, nullptr, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total,    \
+        nconv, r, nullptr, nullptr, nullptr, nullptr, g_stamps);                                 \
+  else                                                                                           \
+    conv_tap_pp_kernel<3, D, 0, kNT, false, 3, kMT, 0, 0, 1, 0, 0, RSV>                          \
+        <<<nconv, 512, 0, stream>>>(x, w, bias, y, mk, nullptr, M, S, WI, shift, WO, HO, CIN,    \
+                                    COUTP, YC, relu, HM, total, nconv, r, nullptr, nullptr,      \
+                                    nullptr, nullptr, g_stamps)
+  if (rsd) {
+    if ((diag & 3) != 0) return -1;
+    if (rsd == 1) {
+      if (diag & 8) { RAG_PPDR(12, 1); } else { RAG_PPDR(4, 1); }
+    } else {
+      if (diag & 8) { RAG_PPDR(12, 2); } else { RAG_PPDR(4, 2); }
+    }
+    return (int)hipGetLastError();
+  }
+#undef RAG_PPDR
   switch (diag & 11) {
     case 0: RAG_PPD(4); break;
     case 1: RAG_PPD(5); break;
@@ -1359,6 +1553,12 @@ RAG_API int rag_conv_diag_segments(long long* host, int nblocks) {
 RAG_API int rag_conv_ep_lds(int on) {
   const int old = g_ep_lds_override;
   g_ep_lds_override = on;
+  return old;
+}
+
+RAG_API int rag_conv_rs(int v) {
+  const int old = g_conv_rs;
+  g_conv_rs = v;
   return old;
 }
 
@@ -1530,20 +1730,26 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
       const char* e = getenv("RAG_CONV_K2");
       g_conv_k2 = e ? atoi(e) : 0;
     }
-    // K2 (two K-steps per barrier pair, rag_conv_k2): 1 = plain, 2 = + static group-1 priority
-#define RAG_PP128(BNPV, PRIOV, K2V, BNC)                                                          \
-  conv_tap_pp_kernel<K2V ? 6 : 3, 0, 0, 4, BNPV, 3, kMT, 0, 0, PRIOV, 0, K2V>                     \
+    // K2 (two K-steps per barrier pair, rag_conv_k2): 1 = plain, 2 = + static group-1 priority;
+    // RS (register staging, rag_conv_rs): 1 = weights, 2 = weights + slab
+#define RAG_PP128(BNPV, PRIOV, K2V, RSV, BNC)                                                     \
+  conv_tap_pp_kernel<K2V ? 6 : 3, 0, 0, 4, BNPV, 3, kMT, 0, 0, PRIOV, 0, K2V, RSV>                \
       <<<nconv + nred, 512, 0, stream>>>(x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN,   \
                                          COUTP, YC, relu, HM, total_rows, nconv, r, BNC, mcoef,  \
                                          spart, smean)
+    const int rs = conv_rs();
     if (bnc) {
-      if (g_conv_k2 == 1) RAG_PP128(true, 0, 1, bnc);
-      else if (g_conv_k2 == 2) RAG_PP128(true, 1, 1, bnc);
-      else RAG_PP128(true, 0, 0, bnc);
+      if (rs == 1) RAG_PP128(true, 0, 0, 1, bnc);
+      else if (rs == 2) RAG_PP128(true, 0, 0, 2, bnc);
+      else if (g_conv_k2 == 1) RAG_PP128(true, 0, 1, 0, bnc);
+      else if (g_conv_k2 == 2) RAG_PP128(true, 1, 1, 0, bnc);
+      else RAG_PP128(true, 0, 0, 0, bnc);
     } else {
-      if (g_conv_k2 == 1) RAG_PP128(false, 0, 1, nullptr);
-      else if (g_conv_k2 == 2) RAG_PP128(false, 1, 1, nullptr);
-      else RAG_PP128(false, 0, 0, nullptr);
+      if (rs == 1) RAG_PP128(false, 0, 0, 1, nullptr);
+      else if (rs == 2) RAG_PP128(false, 0, 0, 2, nullptr);
+      else if (g_conv_k2 == 1) RAG_PP128(false, 0, 1, 0, nullptr);
+      else if (g_conv_k2 == 2) RAG_PP128(false, 1, 1, 0, nullptr);
+      else RAG_PP128(false, 0, 0, 0, nullptr);
     }
 #undef RAG_PP128
     return true;
@@ -1587,6 +1793,14 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
       conv_tap_pp_kernel<3, 0, 0, kNT, false, 3, kMT, 1, 1><<<nconv + nred, 512, 0, stream>>>(
           x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
           nconv, r);
+    else if (g_tap_mode == 12 && conv_rs() == 1)
+      conv_tap_pp_kernel<3, 0, 0, kNT, false, 3, kMT, 1, 0, 1, 0, 0, 1>
+          <<<nconv + nred, 512, 0, stream>>>(x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN,
+                                             COUTP, YC, relu, HM, total_rows, nconv, r);
+    else if (g_tap_mode == 12 && conv_rs() == 2)
+      conv_tap_pp_kernel<3, 0, 0, kNT, false, 3, kMT, 0, 0, 1, 0, 0, 2>
+          <<<nconv + nred, 512, 0, stream>>>(x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN,
+                                             COUTP, YC, relu, HM, total_rows, nconv, r);
     else if (g_tap_mode == 12)
       conv_tap_pp_kernel<3, 0, 0, kNT, false, 3, kMT, 1, 0, 1><<<nconv + nred, 512, 0, stream>>>(
           x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,

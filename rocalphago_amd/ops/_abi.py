@@ -65,6 +65,7 @@ SIGNATURES = {
     "rag_conv_order": [I],
     "rag_conv_tap_mode": [I],
     "rag_conv_k2": [I],
+    "rag_conv_rs": [I],
     "rag_conv_ep_lds": [I],
     "rag_wgrad_slab_nbuf": [I],
     "rag_wgrad_slab_part_bf16": [I],

@@ -53,23 +53,28 @@ for C in (128, 192):
     _lib().rag_conv_tap_mode(6)
     out["c%d_wgrad_us" % C] = round(timeit(lambda: ops.conv_wgrad(
         g, xp, dw, db, B, S, 1, C, C, C, C, 3, work=work, hg=1)), 2)
+    _lib().rag_conv_tap_mode(12)  # the default mode (the RS variants are mode-12 kernels)
+    coef = torch.zeros(3, S, device=dev)
+    coef[0] = 1.0
     if C == 128:  # BN prologue forms (ResnetPolicy)
-        coef = torch.zeros(3, S, device=dev)
-        coef[0] = 1.0
         cases["bn_fwd_res"] = lambda: ops.conv_igemm_bn(
             xp, wf, None, y, B, S, C, C, False, bn_coef=coef, residual=rp)
         cases["bn_dgrad"] = lambda: ops.conv_igemm_bn(
             g, wb, None, y, B, S, C, C, False, mask=xp, mask_coef=coef)
-        for rep in range(2):  # interleaved repeats
-            for k2 in [int(v) for v in os.environ.get("K2", "0,1,2").split(",")]:
-                _lib().rag_conv_k2(k2)
-                for k, fn in cases.items():
-                    key = "c128_%s_k2_%d_us" % (k, k2)
-                    t = round(timeit(fn), 2)
-                    out[key] = min(out.get(key, 1e9), t)
-        _lib().rag_conv_k2(0)
-        out["c128_bn_fwd_res_us"] = out["c128_bn_fwd_res_k2_0_us"]
-        out["c128_bn_dgrad_us"] = out["c128_bn_dgrad_k2_0_us"]
+    # variants (interleaved repeats): "k2_<v>" (rag_conv_k2) / "rs_<v>" (rag_conv_rs)
+    variants = os.environ.get("VARIANTS", "k2_0,k2_1,rs_1,rs_2").split(",")
+    for rep in range(2):
+        for var in variants:
+            knob, v = var.rsplit("_", 1)
+            getattr(_lib(), "rag_conv_" + knob)(int(v))
+            for k, fn in cases.items():
+                key = "c%d_%s_%s_us" % (C, k, var)
+                t = round(timeit(fn), 2)
+                out[key] = min(out.get(key, 1e9), t)
+            getattr(_lib(), "rag_conv_" + knob)(0)
+    if C == 128:
+        out["c128_bn_fwd_res_us"] = out.get("c128_bn_fwd_res_k2_0_us")
+        out["c128_bn_dgrad_us"] = out.get("c128_bn_dgrad_k2_0_us")
         out["c128_bn_wgrad_us"] = round(timeit(lambda: ops.conv_wgrad(
             g, xp, dw, db, B, S, 1, C, C, C, C, 3, work=work, hg=1, xcoef=coef)), 2)
         h = ops.PendingReduction()

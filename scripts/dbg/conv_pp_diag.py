@@ -15,7 +15,10 @@ from rocalphago_amd.ops import hipops as ops  # noqa: E402
 from rocalphago_amd.ops.hipops import _lib  # noqa: E402
 
 dev = torch.device("cuda")
-B, S, C = int(os.environ.get("B", 256)), 19, 192
+B, S, C = int(os.environ.get("B", 256)), 19, int(os.environ.get("C", 192))
+N128 = 16 if C == 128 else 0  # diag bit 4: the 128-channel (NT = 4) kernel
+RS = int(os.environ.get("RS", 0))  # diag bits 5-6: register staging (timing builds only)
+N128 |= RS << 5
 x = torch.randn(B, C, S, S, device=dev).relu()
 w = torch.randn(C, C, 3, 3, device=dev) * 0.05
 xp = ops.pack_nchw(x, 1, C)
@@ -30,7 +33,7 @@ nblk = ((B * S * S + 383) // 384)
 
 
 def run(diag):
-    rc = lib.rag_conv_pp_diag(diag, ops._ptr(xp), ops._ptr(wf), ops._ptr(bias), ops._ptr(y), None,
+    rc = lib.rag_conv_pp_diag(diag | N128, ops._ptr(xp), ops._ptr(wf), ops._ptr(bias), ops._ptr(y), None,
                               B, S, 1, 1, C, C, C, 1, 1, ops._stream())
     assert rc == 0, rc
 
@@ -49,6 +52,8 @@ def timeit(fn, iters=40):
 
 
 names = {0: "full", 1: "no_staging", 2: "no_frag_reads", 3: "mfma_only"}
+if RS:
+    names = {0: "full"}
 res = {n: [] for n in names.values()}
 clk = {}
 for r in range(4):
@@ -79,13 +84,14 @@ seg = np.median(seg.reshape(nblk, 10).astype(np.float64), axis=0)
 segments = {"g0_Xwait": seg[0], "g0_slab_read": seg[1], "g0_Ywait": seg[2],
             "g0_mfma_issue": seg[3], "g0_vmwait": seg[4], "g1_Xwait": seg[5], "g1_mfma_issue": seg[6],
             "g1_Ywait": seg[7], "g1_read": seg[8], "g1_stage_vmwait": seg[9]}
-out = {"B": B, "segments_cycles_per_step": {k: round(v / 54.0, 1) for k, v in segments.items()}}
+out = {"B": B, "C": C, "RS": RS,
+       "segments_cycles_per_step": {k: round(v / (9.0 * C / 32), 1) for k, v in segments.items()}}
 for n, v in res.items():
     out[n + "_us_min"] = round(min(v), 2)
     out[n + "_GHz"] = round(float(np.median(clk[n])), 3)
     out[n + "_loop_us_med"] = round(float(np.median(clk[n + "_loop_us"])), 2)
     pr = clk[n + "_prof"][-1]
     out[n + "_timeline"] = {k: round(v, 2) for k, v in pr.items()}
-flop = 2.0 * B * 361 * 192 * 1728
+flop = 2.0 * B * 361 * C * 9 * C
 out["full_TFLOPs"] = round(flop / out["full_us_min"] / 1e6, 1)
 print(json.dumps(out))

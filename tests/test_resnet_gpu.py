@@ -357,16 +357,20 @@ def test_bn_apply_with_folded_finalize_matches_two_launches(ops, residual):
     assert out[:, 0].abs().max().item() == 0 and out[:, :, -1].abs().max().item() == 0
 
 
-@pytest.mark.parametrize("k2", [1, 2])
-def test_conv128_two_step_variant_bit_identical(ops, k2):
-    """The 128-channel ping-pong kernel with two K-steps per barrier pair (rag_conv_k2) keeps
-    every accumulator's MFMA order, so its outputs -- forward with bias+ReLU, with a residual,
-    masked dgrad, and the BN-prologue forward / dgrad with their column statistics -- equal the
-    one-step kernel's bit for bit; the forward also against fp32 PyTorch."""
+@pytest.mark.parametrize("knob,val,C", [("k2", 1, 128), ("k2", 2, 128), ("rs", 1, 128),
+                                        ("rs", 2, 128), ("rs", 1, 192), ("rs", 2, 192)])
+def test_conv_pp_variants_bit_identical(ops, knob, val, C):
+    """The ping-pong conv variants keep every accumulator's MFMA order, so their outputs equal
+    the default kernel's bit for bit (the BN statistics partials to fp32 atomic-order rounding):
+    two K-steps per barrier pair (rag_conv_k2, 128 channels) and register staging of the weight
+    ring / slab (rag_conv_rs, 128 and 192 channels) -- forward with bias+ReLU, with a residual,
+    masked dgrad, and at 128 channels the BN-prologue forward / dgrad with their column
+    statistics; the forward also against fp32 PyTorch."""
     from rocalphago_amd.ops.hipops import _lib
+    setter = getattr(_lib(), "rag_conv_" + knob)
     dev = "cuda"
     torch.manual_seed(11)
-    B, C, S = 256, 128, 19
+    B, S = 256, 19
     x = bfr(torch.randn(B, C, S, S, device=dev)).relu()
     w = torch.randn(C, C, 3, 3, device=dev) * 0.05
     b = torch.randn(C, device=dev) * 0.1
@@ -378,11 +382,11 @@ def test_conv128_two_step_variant_bit_identical(ops, k2):
     coef[0] = torch.rand(S, device=dev) + 0.5
     coef[2] = torch.randn(S, device=dev) * 0.3
     mean = torch.randn(S, device=dev) * 0.1
-    nblk = ops.conv_bn_stat_blocks(B, S, C)
+    nblk = ops.conv_bn_stat_blocks(B, S, C) if C == 128 else 1
 
     def run():
         outs = []
-        for form in range(5):
+        for form in range(5 if C == 128 else 3):
             y = ops.alloc_padded(B, S, 1, C, dev)
             part = torch.zeros(nblk, 2, S, device=dev)
             if form == 0:
@@ -401,16 +405,17 @@ def test_conv128_two_step_variant_bit_identical(ops, k2):
         torch.cuda.synchronize()
         return outs
 
-    old = _lib().rag_conv_k2(0)
+    old = setter(0)
     try:
         ref = run()
-        _lib().rag_conv_k2(k2)
+        setter(val)
         got = run()
     finally:
-        _lib().rag_conv_k2(old)
+        setter(old)
     for form, ((yr, pr), (yg, pg)) in enumerate(zip(ref, got)):
         assert torch.equal(yr, yg), form
-        assert torch.equal(pr, pg), form
+        # column statistics: LDS atomics in the epilogue, order-dependent in the last bits
+        assert torch.allclose(pr, pg, rtol=1e-5, atol=1e-3), form
     want = F.relu(F.conv2d(x, bfr(w), b, padding=1))
     got0 = ops.unpack(got[0][0], C, 1)
     assert (got0 - want).abs().max().item() < 2e-2 * want.abs().max().item()
