@@ -83,23 +83,25 @@ struct Pos {
   // recursive true-eye rule (go.py:298-327) as an explicit DFS; ancestors = frames below top
   __device__ bool is_eye(int p, int owner) const {
     if (!eyeish(p, owner)) return false;
+    // frame = point | next diagonal << 9 | bad-diagonal count << 12, one int (a private array:
+    // only the few lanes on eye-shaped points ever touch it)
     constexpr int MAXD = 24;
-    int fp[MAXD], fi[MAXD], fb[MAXD];
+    int fr[MAXD];
     int sp = 0;
-    fp[0] = p;
-    fi[0] = 0;
-    fb[0] = 0;
+    fr[0] = p;
     bool ret = true;
     bool have_ret = false;
     while (true) {
-      const int cur = fp[sp];
+      int f = fr[sp];
+      const int cur = f & 511;
+      int fi = (f >> 9) & 7, fb = f >> 12;
       const int allow = nnb(cur) == 4 ? 1 : 0;
       bool done = false;
       if (have_ret) {
         have_ret = false;
         if (!ret) {
-          fb[sp]++;
-          if (fb[sp] > allow) {
+          fb++;
+          if (fb > allow) {
             ret = false;
             done = true;
           }
@@ -107,30 +109,31 @@ struct Pos {
       }
       if (!done) {
         bool pushed = false;
-        while (fi[sp] < 4) {
-          const int d = dg(cur, fi[sp]++);
+        int d = -1;
+        while (fi < 4) {
+          d = dg(cur, fi++);
           if (d < 0) continue;
           if (col[d] == -owner) {
-            if (++fb[sp] > allow) break;
+            if (++fb > allow) break;
           } else if (col[d] == 0) {
             bool anc = false;
-            for (int k = 0; k < sp; ++k) anc |= fp[k] == d;
+            for (int k = 0; k < sp; ++k) anc |= (fr[k] & 511) == d;
             if (anc) continue;
             if (!eyeish(d, owner)) {
-              if (++fb[sp] > allow) break;
+              if (++fb > allow) break;
               continue;
             }
             if (sp + 1 >= MAXD) continue;  // deeper than any real board position
-            ++sp;
-            fp[sp] = d;
-            fi[sp] = 0;
-            fb[sp] = 0;
             pushed = true;
             break;
           }
         }
-        if (pushed) continue;
-        ret = fb[sp] <= allow;
+        fr[sp] = cur | (fi << 9) | (fb << 12);
+        if (pushed) {
+          fr[++sp] = d;
+          continue;
+        }
+        ret = fb <= allow;
       }
       if (sp == 0) return ret;
       --sp;
@@ -139,7 +142,22 @@ struct Pos {
   }
 };
 
-// set helpers over kNW words
+// set helpers over kNW words. Word selection is unrolled (compile-time indices): a runtime index
+// into a register array puts the array in scratch.
+__device__ __forceinline__ void set_bit6(unsigned long long* s, int q) {
+#pragma unroll
+  for (int w = 0; w < kNW; ++w) s[w] |= (w == (q >> 6)) ? (1ull << (q & 63)) : 0ull;
+}
+__device__ __forceinline__ void clear_bit6(unsigned long long* s, int q) {
+#pragma unroll
+  for (int w = 0; w < kNW; ++w) s[w] &= (w == (q >> 6)) ? ~(1ull << (q & 63)) : ~0ull;
+}
+__device__ __forceinline__ bool get_bit6(const unsigned long long* s, int q) {
+  unsigned long long v = 0ull;
+#pragma unroll
+  for (int w = 0; w < kNW; ++w) v = (w == (q >> 6)) ? s[w] : v;
+  return (v >> (q & 63)) & 1ull;
+}
 __device__ __forceinline__ int popc6(const unsigned long long* s) {
   int c = 0;
 #pragma unroll
@@ -147,7 +165,14 @@ __device__ __forceinline__ int popc6(const unsigned long long* s) {
   return c;
 }
 
-__global__ void __launch_bounds__(kPMAX)
+// No scratch and ~171 VGPRs (was 256 + 448 B/lane of scratch: runtime-indexed neighbour lists,
+// bit sets and DFS frames): two waves of a block now fit on a SIMD beside one of the search's
+// resident rollout waves (128 VGPRs); at 256 a block needed SIMDs free of rollout waves, and the
+// 512-leaf feature passes waited behind the 5 ms rollout kernels (413 us per pass,
+// profiles/mcts_kernels_r4.txt). WPE = 4 (RAG_FEATURES_WPE=4): 128 VGPRs, so a wave fits even
+// beside three resident rollout waves (their 3 x 128 VGPRs), at the cost of scratch spills.
+template <int WPE>
+__global__ void __launch_bounds__(kPMAX, WPE)
 features_kernel(const int8_t* __restrict__ colors, const int16_t* __restrict__ ages,
                 const int32_t* __restrict__ meta, const uint8_t* __restrict__ extra_illegal,
                 const uint8_t* __restrict__ ladders, int n_pos, int S, const int* __restrict__ fids,
@@ -206,17 +231,21 @@ features_kernel(const int8_t* __restrict__ colors, const int16_t* __restrict__ a
       atomicAdd(&gsz[l], 1);
       atomicOr(&sh.stonebits[l][p >> 6], bit);
     } else {
-      int seen[4], ns = 0;
+      // each distinct neighbouring group gains this liberty (neighbours unrolled: static indices)
+      int nl[4];
+#pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int q = g.nb(p, i);
-        if (q < 0 || col[q] == 0) continue;
-        const int l = lab[q];
-        bool dup = false;
-        for (int j = 0; j < ns; ++j) dup |= seen[j] == l;
+        nl[i] = (q >= 0 && col[q] != 0) ? (int)lab[q] : -1;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        bool dup = nl[i] < 0;
+#pragma unroll
+        for (int j = 0; j < i; ++j) dup |= nl[j] == nl[i];
         if (dup) continue;
-        seen[ns++] = l;
-        atomicAdd(&lib[l], 1);
-        atomicOr(&sh.libbits[l][p >> 6], bit);
+        atomicAdd(&lib[nl[i]], 1);
+        atomicOr(&sh.libbits[nl[i]][p >> 6], bit);
       }
     }
   }
@@ -226,11 +255,18 @@ features_kernel(const int8_t* __restrict__ colors, const int16_t* __restrict__ a
   // plane offsets of the requested features
   uint8_t* o = out + (size_t)pos * F * P;
   {
-    // ---- legality, captures and the simulated move
-    int own_l[4], cap_l[4], nown = 0, ncap = 0, empty_nb = 0;
+    // ---- legality, captures and the simulated move. Per neighbour i: its group label nlab[i]
+    // and class cls[i] (0 off-board / empty, 1 own, 2 capturable opponent, 3 other opponent);
+    // uniq[i]: the first neighbour of its (class, group). Unrolled, so no array leaves registers.
+    int nlab[4], cls[4];
+    bool uniq[4];
+    int empty_nb = 0, ncap = 0;
     bool own_multi = false;
+#pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int q = g.nb(p, i);
+      cls[i] = 0;
+      nlab[i] = -1;
       if (q < 0) continue;
       const int cq = col[q];
       if (cq == 0) {
@@ -238,22 +274,29 @@ features_kernel(const int8_t* __restrict__ colors, const int16_t* __restrict__ a
         continue;
       }
       const int l = lab[q];
+      nlab[i] = l;
       if (cq == me) {
+        cls[i] = 1;
         if (lib[l] > 1) own_multi = true;
-        bool dup = false;
-        for (int j = 0; j < nown; ++j) dup |= own_l[j] == l;
-        if (!dup) own_l[nown++] = l;
-      } else if (lib[l] == 1) {
-        bool dup = false;
-        for (int j = 0; j < ncap; ++j) dup |= cap_l[j] == l;
-        if (!dup) cap_l[ncap++] = l;
+      } else {
+        cls[i] = lib[l] == 1 ? 2 : 3;
+      }
+    }
+    int cap_size = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bool u = cls[i] == 1 || cls[i] == 2;
+#pragma unroll
+      for (int j = 0; j < i; ++j) u &= !(cls[j] == cls[i] && nlab[j] == nlab[i]);
+      uniq[i] = u;
+      if (u && cls[i] == 2) {
+        ++ncap;
+        cap_size += gsz[nlab[i]];
       }
     }
     const bool suicide = empty_nb == 0 && !own_multi && ncap == 0;
     const bool legal = c == 0 && p != ko && !suicide &&
                        !(extra_illegal && extra_illegal[(size_t)pos * P + p]);
-    int cap_size = 0;
-    for (int j = 0; j < ncap; ++j) cap_size += gsz[cap_l[j]];
     int libs_after = 0, size_after = 1;
     bool need_after = false;
     for (int fi = 0; fi < nf; ++fi)
@@ -262,14 +305,17 @@ features_kernel(const int8_t* __restrict__ colors, const int16_t* __restrict__ a
       unsigned long long ls[kNW];
 #pragma unroll
       for (int w = 0; w < kNW; ++w) ls[w] = 0ull;
+#pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int q = g.nb(p, i);
-        if (q >= 0 && col[q] == 0) ls[q >> 6] |= 1ull << (q & 63);
+        if (q >= 0 && col[q] == 0) set_bit6(ls, q);
       }
-      for (int j = 0; j < nown; ++j) {
-        size_after += gsz[own_l[j]];
 #pragma unroll
-        for (int w = 0; w < kNW; ++w) ls[w] |= sh.libbits[own_l[j]][w];
+      for (int i = 0; i < 4; ++i) {
+        if (!(uniq[i] && cls[i] == 1)) continue;
+        size_after += gsz[nlab[i]];
+#pragma unroll
+        for (int w = 0; w < kNW; ++w) ls[w] |= sh.libbits[nlab[i]][w];
       }
       if (ncap > 0) {
         unsigned long long grp[kNW], cap[kNW];
@@ -278,13 +324,16 @@ features_kernel(const int8_t* __restrict__ colors, const int16_t* __restrict__ a
           grp[w] = 0ull;
           cap[w] = 0ull;
         }
-        grp[p >> 6] |= 1ull << (p & 63);
-        for (int j = 0; j < nown; ++j)
+        set_bit6(grp, p);
 #pragma unroll
-          for (int w = 0; w < kNW; ++w) grp[w] |= sh.stonebits[own_l[j]][w];
-        for (int j = 0; j < ncap; ++j)
+        for (int i = 0; i < 4; ++i) {
+          if (!uniq[i]) continue;
 #pragma unroll
-          for (int w = 0; w < kNW; ++w) cap[w] |= sh.stonebits[cap_l[j]][w];
+          for (int w = 0; w < kNW; ++w) {
+            if (cls[i] == 1) grp[w] |= sh.stonebits[nlab[i]][w];
+            else cap[w] |= sh.stonebits[nlab[i]][w];
+          }
+        }
         // captured stones orthogonally adjacent to the merged group become liberties
 #pragma unroll
         for (int w = 0; w < kNW; ++w) {
@@ -293,15 +342,16 @@ features_kernel(const int8_t* __restrict__ colors, const int16_t* __restrict__ a
             const int s = w * 64 + __builtin_ctzll(m);
             m &= m - 1;
             bool adj = false;
+#pragma unroll
             for (int i = 0; i < 4; ++i) {
               const int q = g.nb(s, i);
-              adj |= q >= 0 && ((grp[q >> 6] >> (q & 63)) & 1ull);
+              adj |= q >= 0 && get_bit6(grp, q);
             }
             if (adj) ls[w] |= 1ull << (s & 63);
           }
         }
       }
-      ls[p >> 6] &= ~(1ull << (p & 63));
+      clear_bit6(ls, p);
       libs_after = popc6(ls);
     }
     // ---- write the planes (the true-eye DFS at most once per point)
@@ -401,8 +451,17 @@ RAG_API int rag_features(const void* colors, const void* ages, const int32_t* me
                          hipStream_t stream) {
   if (S < 2 || S * S > kPMAX || n_pos <= 0) return -1;
   const int threads = (S * S + 63) / 64 * 64;
-  features_kernel<<<dim3(n_pos), threads, 0, stream>>>((const int8_t*)colors, (const int16_t*)ages,
-                                                 meta, extra_illegal, ladders, n_pos, S, fids,
-                                                 nf, F, out, sens);
+  static const int wpe = [] {
+    const char* e = getenv("RAG_FEATURES_WPE");
+    return e && atoi(e) == 4 ? 4 : 2;
+  }();
+  if (wpe == 4)
+    features_kernel<4><<<dim3(n_pos), threads, 0, stream>>>(
+        (const int8_t*)colors, (const int16_t*)ages, meta, extra_illegal, ladders, n_pos, S, fids,
+        nf, F, out, sens);
+  else
+    features_kernel<2><<<dim3(n_pos), threads, 0, stream>>>(
+        (const int8_t*)colors, (const int16_t*)ages, meta, extra_illegal, ladders, n_pos, S, fids,
+        nf, F, out, sens);
   return (int)hipGetLastError();
 }
