@@ -1,4 +1,7 @@
 // pybind11 module `rocalphago_amd._rocgo`: Go engine, feature extraction, LZF codec, search.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -304,6 +307,9 @@ PYBIND11_MODULE(_rocgo, m) {
          py::array_t<uint64_t, py::array::c_style> zw, py::array_t<uint64_t, py::array::c_style> zb,
          int nthreads, int chunk_rows, int lead) -> py::tuple {
         auto zob = make_zobrist(zw, zb);
+        static const bool timing = std::getenv("RAG_CONVERT_TIMING") != nullptr;
+        auto tnow = [] { return std::chrono::steady_clock::now(); };
+        auto t_0 = tnow();
         const int n = (int)texts.size();
         std::vector<std::string> buf(n);
         for (int i = 0; i < n; ++i) buf[i] = texts[i];
@@ -324,6 +330,7 @@ PYBIND11_MODULE(_rocgo, m) {
             rp[i] = (int64_t)(ac[i].size() / 2);
           });
         }
+        auto t_1 = tnow();
         const int F = total_planes(fids), P = bd_size * bd_size;
         const size_t row_bytes = (size_t)F * P;
         std::vector<int64_t> off(n + 1, 0);
@@ -379,10 +386,29 @@ PYBIND11_MODULE(_rocgo, m) {
             extract_row(r, sd + (size_t)k * row_bytes);
           });
         }
-        if (chunk_rows <= 0) return py::make_tuple(status, rows, sa, aa);
+        auto t_2 = tnow();
+        {  // the position boards go on the pool too (12k+ board destructors per batch)
+          py::gil_scoped_release nogil;
+          parallel_for(n, nthreads, [&](int i) { std::vector<Board>().swap(bd[i]); });
+        }
+        auto t_3 = tnow();
+        auto report = [&] {
+          if (!timing) return;
+          auto ms = [](auto a, auto b) {
+            return std::chrono::duration<double, std::milli>(b - a).count();
+          };
+          std::fprintf(stderr, "convert_games n=%d rows=%lld replay %.2f ms planes %.2f ms free %.2f "
+                       "ms wrap %.2f ms\n", n, (long long)total, ms(t_0, t_1), ms(t_1, t_2),
+                       ms(t_2, t_3), ms(t_3, tnow()));
+        };
+        if (chunk_rows <= 0) {
+          report();
+          return py::make_tuple(status, rows, sa, aa);
+        }
         py::list chunks;
         for (int64_t t = 0; t < nfull; ++t)
           chunks.append(py::make_tuple(py::bytes(comp[(size_t)t]), (bool)ok[(size_t)t]));
+        report();
         return py::make_tuple(status, rows, sa, aa, chunks, (py::ssize_t)L);
       },
       py::arg("texts"), py::arg("fids"), py::arg("bd_size"), py::arg("zobrist_white"),
