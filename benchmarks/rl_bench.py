@@ -134,7 +134,8 @@ def main():
         # replay) / native play, and the time waiting on the GPU
         r["selfplay_split_s"] = {k: round(sp[k], 3) for k in ("pack_s", "launch_s", "play_s",
                                                               "host_s", "gpu_wait_s",
-                                                              "gpu_pass_s", "wall_s")
+                                                              "gpu_pass_s", "wall_s", "rec_s",
+                                                              "gather_s")
                                  if k in sp}
         # share of the self-play wall time the GPU spends in ply passes: with the two pipelined
         # groups a busy host overlaps the other group's GPU pass, so this, not the host share,

@@ -275,7 +275,7 @@ class NativeSelfPlay(object):
         groups = [np.nonzero(grp == k)[0].astype(np.int32) for k in range(K)]
         current = [self.learner] * K
         jobs = [None] * K
-        recs = []  # (learner plane rows of a ply, their games, moves)
+        recs = []  # (a learner ply's slot planes, played rows in them, their games, moves)
 
         def start(k):
             idx = self._active(batch, grp, k)
@@ -290,15 +290,22 @@ class NativeSelfPlay(object):
                 idx = jobs[k]["idx"]
                 planes, played, pos = self._finish(batch, jobs[k], size)
                 if current[k] is self.learner:
+                    t_r = time.perf_counter()
                     r = np.nonzero(played >= 0)[0]
                     if len(r):
-                        # copied out now: the slot's planes buffer is refilled by its next ply
-                        rows = torch.from_numpy(pos[r].astype(np.int64)).to(self.device)
-                        recs.append((planes.index_select(0, rows), idx[r], played[r]))
+                        # the slot's planes buffer is refilled by its next ply: copy it out now,
+                        # whole (a device-side clone queued behind the pass; selecting the played
+                        # rows here needed a host->device index copy, which synchronised the
+                        # stream -- i.e. waited for the OTHER group's just-launched pass every
+                        # learner ply); the rows are selected once, in _per_game
+                        recs.append((planes.clone(), pos[r], idx[r], played[r]))
+                    self.stats["rec_s"] = self.stats.get("rec_s", 0.0) + time.perf_counter() - t_r
                 current[k] = self.opponent if current[k] is self.learner else self.learner
                 jobs[k] = start(k)
         self.illegal = batch.illegal
+        t_g = time.perf_counter()
         feats, moves = self._per_game(recs, num_games)
+        self.stats["gather_s"] = self.stats.get("gather_s", 0.0) + time.perf_counter() - t_g
         self.stats["wall_s"] = self.stats.get("wall_s", 0.0) + time.perf_counter() - t_start
         return feats, moves, colors, batch.winners()
 
@@ -306,12 +313,17 @@ class NativeSelfPlay(object):
         if not recs:
             return [[] for _ in range(num_games)], [[] for _ in range(num_games)]
         dev = self.device
-        rows = torch.cat([pl for pl, _, _ in recs])
-        gid = np.concatenate([g for _, g, _ in recs]).astype(np.int64)
-        mv = np.concatenate([m for _, _, m in recs]).astype(np.int64)
+        # recs: (a ply's whole slot planes [n, F, S, S], the played games' rows in it, their
+        # game ids, their moves); one concatenation, one host->device row index, one gather
+        base = np.cumsum([0] + [pl.shape[0] for pl, _, _, _ in recs])[:-1]
+        sel = np.concatenate([b + p for b, (_, p, _, _) in zip(base, recs)]).astype(np.int64)
+        gid = np.concatenate([g for _, _, g, _ in recs]).astype(np.int64)
+        mv = np.concatenate([m for _, _, _, m in recs]).astype(np.int64)
         order = np.argsort(gid, kind="stable")  # plies were recorded in move order
         counts = np.bincount(gid, minlength=num_games)
-        rows = rows[torch.from_numpy(order).to(dev)]
+        allrows = torch.cat([pl for pl, _, _, _ in recs])
+        rows = allrows.index_select(0, torch.from_numpy(sel[order]).to(dev))
+        del allrows
         parts = torch.split(rows, counts.tolist())
         mparts = np.split(mv[order], np.cumsum(counts)[:-1])
         feats = [p if c else [] for p, c in zip(parts, counts)]

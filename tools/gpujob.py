@@ -53,6 +53,9 @@ STEPS = {
                    + PY + " bench.py --model resnet --no-mcts --steps 6 --warmup 2", "tail1"),
     "pmc2-sl": (150, "rocprofv3 --pmc " + PMC_LDS + " --output-format csv -d {dir} -- " +
                 PY + " bench.py --no-mcts --steps 6 --warmup 2", "tail1"),
+    "rl": (300, PY + " benchmarks/rl_bench.py --config 19 --game-batch 256", "json"),
+    "trace-rl": (300, "rocprofv3 --kernel-trace -d {dir} -o rl -- " + PY +
+                 " benchmarks/rl_bench.py --config 19 --game-batch 256", "tail1"),
     "kernels": (600, PY + " -m pytest tests/test_hip_kernels.py tests/test_gpu_models.py "
                 "tests/test_gpu_bench_path.py -m gpu -x -q --timeout 200 "
                 "--timeout-method thread", "tail2"),
