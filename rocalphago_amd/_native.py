@@ -46,7 +46,9 @@ def hip(required=True):
     with _lock:
         if _hip is None:
             from . import _build
-            path = _build.HIP_SO
+            # RAG_HIP_SO: an alternative build of the kernel library (same-box A/B of two
+            # source revisions, tools/ab_build.py)
+            path = os.environ.get("RAG_HIP_SO") or _build.HIP_SO
             if not os.path.exists(path):
                 try:
                     _build.build_hip()
