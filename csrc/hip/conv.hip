@@ -645,6 +645,7 @@ struct PendingRed {
   int valid;
   hipStream_t stream;
   WgradRed r;
+  unsigned* dticket;  // the handle's [2] device claim counters (allocated on first deferral)
 };
 
 RAG_API size_t rag_wgrad_pending_bytes() { return sizeof(PendingRed); }
@@ -974,6 +975,19 @@ static int conv_wgrad_impl(const void* G, const void* X, float* dW, float* db, f
     if (defer && rs == stream) {
       PendingRed* p = static_cast<PendingRed*>(pending);
       p->r = r;
+      // RAG_WGRAD_CLAIM=0: the riding reduce blocks split the reduction statically (A/B)
+      static const bool claim = [] {
+        const char* e = getenv("RAG_WGRAD_CLAIM");
+        return !(e && e[0] == '0');
+      }();
+      if (claim) {
+        if (!p->dticket) {
+          if (hipMalloc(&p->dticket, 2 * sizeof(unsigned)) != hipSuccess) return -3;
+          if (hipMemsetAsync(p->dticket, 0, 2 * sizeof(unsigned), stream) != hipSuccess)
+            return -3;
+        }
+        p->r.ticket = p->dticket;
+      }
       p->stream = stream;
       p->valid = 1;
       return 0;

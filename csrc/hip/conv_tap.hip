@@ -832,8 +832,14 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
   constexpr int D = ISSUE ? NB : NB - 1;
   // + a [2][64] float BN-statistics accumulator past the ring / epilogue image
   __shared__ __attribute__((aligned(16))) bf16 lds[kL + 256];
+  // claimed reductions (red.ticket) ride only in 128-wide launches: the 192-wide kernels keep
+  // the static split and none of the claim code (SL -1 % with it compiled in, same-box A/B)
+  constexpr bool kClaim = NT == 4;
   if ((int)blockIdx.x >= nconv) {
-    wslab_reduce_blocks<kRedU>(red, (int)blockIdx.x - nconv, (int)gridDim.x - nconv);
+    if (kClaim && red.ticket)
+      wslab_reduce_dynamic<kRedU>(red, reinterpret_cast<int*>(lds));
+    else
+      wslab_reduce_blocks<kRedU>(red, (int)blockIdx.x - nconv, (int)gridDim.x - nconv);
     return;
   }
   float* sred = spart ? reinterpret_cast<float*>(lds + kL) : nullptr;
@@ -901,11 +907,11 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
       }
     }
   };
-  int bofs[PPBL];  // this lane's weight-row element offsets (32-bit: fewer live VGPRs)
+  const bf16* bsrc[PPBL];  // (32-bit offsets instead: SL -0.5 %, profiles/conv_phase_experiments_r4.txt)
 #pragma unroll
   for (int k = 0; k < PPBL; ++k) {
     const int r = (wl + 4 * k) * 16 + lrow;
-    bofs[k] = (n0 + r) * CIN + ((lcol ^ swz4(r)) * 8);
+    bsrc[k] = Wt + (long)(n0 + r) * CIN + ((lcol ^ swz4(r)) * 8);
   }
   auto stage_a = [&](int q, int k0 = 0, int k1 = 1 << 20) {  // chunk q, pieces k0 .. k1-1
     bf16* dst = lds + (q & 1) * SLAB;
@@ -940,7 +946,7 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
     if (PR && q == 1 && vhi && t + 1 < TAPS) off += tap_stride - 16;
 #pragma unroll
     for (int k = 0; k < PPBL; ++k)
-      if (k >= k0 && k < k1) glds16(Wt + (bofs[k] + off), dst + (wl + 4 * k) * 16 * kBK);
+      if (k >= k0 && k < k1) glds16(bsrc[k] + off, dst + (wl + 4 * k) * 16 * kBK);
   };
 
   const int frow = lane & 15;
@@ -1036,7 +1042,7 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
         int q, t;
         decode(sb, q, t);
         bf16* dst = lds + 2 * SLAB + (sb % NB) * BTile;
-        glds16(Wt + (bofs[j] + t * tap_stride + q * kBK), dst + (wl + 4 * j) * 16 * kBK);
+        glds16(bsrc[j] + t * tap_stride + q * kBK, dst + (wl + 4 * j) * 16 * kBK);
       }
     }
     __builtin_amdgcn_s_setprio(0);
@@ -1243,7 +1249,7 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
         decode(s, q, t);
         const long off = t * tap_stride + q * kBK;
 #pragma unroll
-        for (int k = 0; k < PB1; ++k) wreg[k] = *reinterpret_cast<const bf16x8*>(Wt + (bofs[k] + off));
+        for (int k = 0; k < PB1; ++k) wreg[k] = *reinterpret_cast<const bf16x8*>(bsrc[k] + off);
       };
       auto w_put = [&](int s) {
         bf16* dst = lds + 2 * SLAB + (s % NB) * BTile;
@@ -1432,6 +1438,10 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
       const int q = threadIdx.x / S, wc = threadIdx.x - q * S;
       spart[((size_t)blockIdx.x * 2 + q) * S + wc] = sred[q * 64 + wc];
     }
+  }
+  // a deferred wgrad reduction riding in this launch: the tile done, help finish it
+  if constexpr (kClaim) {
+    if (red.ticket && gridDim.x > nconv) wslab_reduce_dynamic<kRedU>(red, reinterpret_cast<int*>(lds));
   }
   if constexpr (DIAG & 4) {
     // per block: loop cycles, loop ticks, then absolute ticks at entry / loop start / loop end /
@@ -1650,6 +1660,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
       WgradRed r{};
       if (red) {
         r = *red;
+        r.ticket = nullptr;  // claimed reduction: 128-wide launches only (SL -1.3 %)
         nred = std::max(8, (256 - n192 % 256) % 256);
       }
       if (pair5)
@@ -1667,6 +1678,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
     WgradRed r{};
     if (red) {
       r = *red;
+      if (w192) r.ticket = nullptr;  // claimed reduction: 128-wide launches only
       nred = std::max(8, (256 - nconv % 256) % 256);
     }
     // (the spread / static-priority 3x3 variants measured slower on the 5x5 layer: 52.9-53.7
@@ -1724,6 +1736,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
     WgradRed r{};
     if (red) {
       r = *red;
+      // claimed reduction (r.ticket): CNNPolicy-128 164.9 -> 169.2 k positions/s
       nred = std::max(8, (256 - nconv % 256) % 256);
     }
     if (g_conv_k2 < 0) {
@@ -1767,6 +1780,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
     WgradRed r{};
     if (red) {
       r = *red;
+      r.ticket = nullptr;  // claimed reduction: 128-wide launches only (SL -1.3 %)
       nred = std::max(8, (256 - nconv % 256) % 256);
     }
     if (g_tap_mode == 5)
@@ -1838,6 +1852,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
     WgradRed r{};
     if (red) {
       r = *red;
+      r.ticket = nullptr;  // claimed reduction: 128-wide launches only (SL -1.3 %)
       nred = std::max(8, (256 - n192 % 256) % 256);
     }
     conv_tap_pp_kernel<3, 0, 0, kNT, false, 3, 3><<<n192 + nred, 512, 0, stream>>>(
@@ -1860,6 +1875,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
   WgradRed r{};
   if (red) {
     r = *red;
+    r.ticket = nullptr;  // claimed reduction: 128-wide launches only (SL -1.3 %)
     nred = std::min(64, std::max(8, 2 * 256 - nconv));
   }
   static const int ep_lds = [] {  // RAG_EP_LDS=0: the register epilogue (A/B)

@@ -33,6 +33,9 @@ struct WgradRed {
   int n, waves, blk;   // block channels (192 | 128), waves (n / 16), accumulators per block
   int taps, kgrp;      // KS * KS; blocks per c-tile (5x5: one kernel row each, else 1)
   int pair5;           // 5x5 with <= 48 of 64 channels: pseudo c-tiles 5..7 = c-tile 1, rows 2p, 2p+1
+  // [2] device counters (claim ticket, finished blocks), zero between launches: kernels that
+  // support it claim the reduction in block-sized units (wslab_reduce_dynamic); null = static
+  unsigned* ticket;
 };
 
 __device__ __forceinline__ void wslab_add8(float (&s)[8], const uint4& v, float sc) {
@@ -96,34 +99,75 @@ __device__ __forceinline__ void wslab_store_oct(const WgradRed& r, int q, const 
 
 // Reduce blocks fused into another kernel: block b of nb handles octs b*T + tid, stepping nb*T,
 // each summed over all chunks with U 16-byte loads in flight; block 0 also sums the bias.
+// One oct: its chunk sum (U 16-byte loads in flight) scattered to dW.
+template <int U>
+__device__ __forceinline__ void wslab_reduce_oct(const WgradRed& r, int q) {
+  const size_t st = (size_t)r.ntc * r.blk / 8;  // uint4 stride between chunks
+  float s[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = 0.f;
+  const uint4* p = reinterpret_cast<const uint4*>(r.part) + q;
+  const float* sc = r.scale + (q * 8) / r.blk;  // + chunk * ntc
+  int k = 0;
+  for (; k + U <= r.nchunks; k += U) {
+    uint4 a[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) a[j] = p[(size_t)(k + j) * st];
+#pragma unroll
+    for (int j = 0; j < U; ++j) wslab_add8(s, a[j], sc[(k + j) * r.ntc]);
+  }
+  for (; k < r.nchunks; ++k) wslab_add8(s, p[(size_t)k * st], sc[k * r.ntc]);
+  wslab_store_oct(r, q, s);
+}
+
+__device__ __forceinline__ void wslab_reduce_bias(const WgradRed& r, int tid, int T) {
+  for (int n = tid; n < r.COUT; n += T) {
+    float v = 0.f;
+    for (int k = 0; k < r.nchunks; ++k) v += r.bpart[(size_t)k * r.n + n];
+    r.db[n] = r.accumulate ? r.db[n] + v : v;
+  }
+}
+
 template <int U>
 __device__ __forceinline__ void wslab_reduce_blocks(const WgradRed& r, int b, int nb) {
   const int T = blockDim.x, tid = threadIdx.x;
   const int octs = r.ntc * r.blk / 8;
-  const size_t st = (size_t)r.ntc * r.blk / 8;  // uint4 stride between chunks
-  const uint4* base = reinterpret_cast<const uint4*>(r.part);
-  for (int q = b * T + tid; q < octs; q += nb * T) {
-    float s[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) s[j] = 0.f;
-    const uint4* p = base + q;
-    const float* sc = r.scale + (q * 8) / r.blk;  // + chunk * ntc
-    int k = 0;
-    for (; k + U <= r.nchunks; k += U) {
-      uint4 a[U];
-#pragma unroll
-      for (int j = 0; j < U; ++j) a[j] = p[(size_t)(k + j) * st];
-#pragma unroll
-      for (int j = 0; j < U; ++j) wslab_add8(s, a[j], sc[(k + j) * r.ntc]);
+  for (int q = b * T + tid; q < octs; q += nb * T) wslab_reduce_oct<U>(r, q);
+  if (b == 0 && r.db && r.bpart) wslab_reduce_bias(r, tid, T);
+}
+
+// The reduction claimed in units of blockDim.x octs (the last unit: the bias) through the
+// r.ticket counter, by EVERY block of the launch: the riding reduce blocks from the start (in the
+// CU slots the convolution grid leaves free), the convolution blocks after their epilogue. With
+// a static split the few riding blocks did all of it and were the launch's tail (128-channel
+// dgrad: 50 vs 38 us without a reduction). Each block exits after its first failed claim, then
+// counts itself finished; the last one resets both counters for the next launch (the claim's
+// returned value orders it before the count). smem: one int of LDS, free at the call.
+template <int U>
+__device__ __forceinline__ void wslab_reduce_dynamic(const WgradRed& r, int* smem) {
+  const int T = blockDim.x, tid = threadIdx.x;
+  const int octs = r.ntc * r.blk / 8;
+  const int units = (octs + T - 1) / T;
+  const int nunits = units + ((r.db && r.bpart) ? 1 : 0);
+  __syncthreads();  // smem may still be read by the caller's last LDS phase
+  while (true) {
+    if (tid == 0) smem[0] = (int)atomicAdd(&r.ticket[0], 1u);
+    __syncthreads();
+    const int u = smem[0];
+    __syncthreads();
+    if (u >= nunits) break;
+    if (u < units) {
+      const int q = u * T + tid;
+      if (q < octs) wslab_reduce_oct<U>(r, q);
+    } else {
+      wslab_reduce_bias(r, tid, T);
     }
-    for (; k < r.nchunks; ++k) wslab_add8(s, p[(size_t)k * st], sc[k * r.ntc]);
-    wslab_store_oct(r, q, s);
   }
-  if (b == 0 && r.db && r.bpart) {
-    for (int n = tid; n < r.COUT; n += T) {
-      float v = 0.f;
-      for (int k = 0; k < r.nchunks; ++k) v += r.bpart[(size_t)k * r.n + n];
-      r.db[n] = r.accumulate ? r.db[n] + v : v;
+  if (tid == 0) {
+    const unsigned done = atomicAdd(&r.ticket[1], 1u);
+    if (done == gridDim.x - 1) {
+      atomicExch(&r.ticket[0], 0u);
+      atomicExch(&r.ticket[1], 0u);
     }
   }
 }

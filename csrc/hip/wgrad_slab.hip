@@ -735,7 +735,7 @@ bool rag_wgrad_slab_bf16() {
 WgradRed rag_wgrad_slab_red(const void* part, const float* bpart, float* dW, float* db,
                             int nchunks, int CINP, int COUTP, int COUT, int CIN, int accumulate,
                             int KS, int pair5) {
-  WgradRed r;
+  WgradRed r{};  // ticket null: a static split unless the deferral hands it claim counters
   r.part = (const f16*)part;
   r.bpart = bpart;
   r.dW = dW;

@@ -91,7 +91,9 @@ def parse(spec):
             k, v = item.split("=", 1)
             env[k] = v
     secs, cmd, mode = STEPS[spec]
-    tag = spec + "".join("_%s%s" % (k.replace("RAG_", "").lower(), v) for k, v in env.items())
+    tag = spec + "".join("_%s%s" % (k.replace("RAG_", "").lower(), os.path.basename(v))
+                         for k, v in env.items())
+    tag = "".join(c if c.isalnum() or c in "._-" else "_" for c in tag)
     return tag, secs, cmd, mode, env
 
 
