@@ -268,6 +268,11 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
       }
     }
   }
+  // prio bits 0-1: MFMA priority mode; bit 2 (RAG_WGRAD_LATE): stage s+kNBUF-1 after the first
+  // k-step's MFMAs instead of right after the barrier (the LDS-DMA issues otherwise sit in front
+  // of every wave's first fragment reads of the stage)
+  const int late = (prio >> 2) & 3;  // 0: after the barrier, 1: after k-step 0, 2: after k-step 1
+  prio &= 3;
   if (prio == 2 && w >= kWaves - 4) __builtin_amdgcn_s_setprio(1);  // the last-dispatched waves
   for (int s = 0; s < nsteps; ++s) {
     // retire stage s; up to kNBUF-2 younger stages (2 or 3 glds of this wave each) stay in flight
@@ -279,7 +284,7 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
       wait_young<2>(young);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (s + kNBUF - 1 < nsteps) stage(s + kNBUF - 1, (s + kNBUF - 1) % kNBUF);
+    if (!late && s + kNBUF - 1 < nsteps) stage(s + kNBUF - 1, (s + kNBUF - 1) % kNBUF);
     const bf16* lb = lds + (s % kNBUF) * kStage;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -301,6 +306,7 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
 #pragma unroll
         for (int a = 0; a < NA; ++a) acc[i][a] = mfma16(fa[a], fb[i], acc[i][a]);
       if (prio == 0) __builtin_amdgcn_s_setprio(0);
+      if (late == kk + 1 && s + kNBUF - 1 < nsteps) stage(s + kNBUF - 1, (s + kNBUF - 1) % kNBUF);
     }
     if constexpr (BNX) {
       // stage s+2 landed (s+3 stays in flight): fetch this lane's chunk for step s+1's xstore
@@ -760,6 +766,19 @@ WgradRed rag_wgrad_slab_red(const void* part, const float* bpart, float* dW, flo
   return r;
 }
 
+// Where the slab kernels issue a stage's LDS-DMA (prio bits 2-3; RAG_WGRAD_LATE): 1 (default)
+// after the first k-step's MFMAs -- SL 110.2-110.7k -> 113.5-114.0k positions/s on one box
+// (profiles/wgrad_late_r4.txt) --, 2 after the second, 0 right after the stage barrier (the
+// round-3 placement: every wave's 2-3 issues delayed its first fragment reads of the stage).
+int wslab_late() {
+  static const int v = [] {
+    const char* e = getenv("RAG_WGRAD_LATE");
+    const int m = e ? atoi(e) : 1;
+    return (m >= 0 && m <= 2 ? m : 1) << 2;
+  }();
+  return v;
+}
+
 int rag_launch_wgrad_slab_reduce(const WgradRed& r, hipStream_t stream) {
   const int octs = (int)((size_t)r.ntc * r.blk / 8);
   const int blocks = (octs + 63) / 64 + (r.n + 255) / 256;
@@ -787,10 +806,10 @@ int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpar
     const dim3 g5(nchunks * (pair5 ? 8 : (CINP / kC) * 5));
     if (COUTP == 192)
       wgrad_slab_kernel<3, true, 0, 192, false, 5><<<g5, 768, 0, stream>>>(
-          G, X, part, bpart, R, WP, GC, CIN, spc, CINP, nullptr, 0, pair5);
+          G, X, part, bpart, R, WP, GC, CIN, spc, CINP, nullptr, 0, pair5, wslab_late());
     else if (COUTP == 128)
       wgrad_slab_kernel<3, true, 0, 128, false, 5><<<g5, 512, 0, stream>>>(
-          G, X, part, bpart, R, WP, GC, CIN, spc, CINP, nullptr, 0, pair5);
+          G, X, part, bpart, R, WP, GC, CIN, spc, CINP, nullptr, 0, pair5, wslab_late());
     else
       return -5;
     return (int)hipGetLastError();
@@ -800,7 +819,7 @@ int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpar
     if (CINP != 128 || !bf || S > 64) return -5;
     wgrad_slab_kernel<4, true, 0, 128, true><<<grid, 512, 0, stream>>>(G, X, part, bpart, R, WP,
                                                                        GC, CIN, spc, CINP, xcoef,
-                                                                       S);
+                                                                       S, 0, wslab_late());
     return (int)hipGetLastError();
   }
   if (CINP == kN && bf && wslab_pp()) {
@@ -810,7 +829,8 @@ int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpar
   if (CINP == 128) {  // 8 waves, map 0
     if (bf)
       wgrad_slab_kernel<3, true, 0, 128><<<grid, 512, 0, stream>>>(G, X, part, bpart, R, WP, GC,
-                                                                   CIN, spc, CINP);
+                                                                   CIN, spc, CINP, nullptr, 0, 0,
+                                                                   wslab_late());
     else
       wgrad_slab_kernel<3, false, 0, 128><<<grid, 512, 0, stream>>>(G, X, part, bpart, R, WP, GC,
                                                                     CIN, spc, CINP);
@@ -818,7 +838,7 @@ int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpar
   }
   static const int wprio = [] {  // RAG_WGRAD_PRIO: 0 flips around MFMAs, 1 none, 2 static
     const char* e = getenv("RAG_WGRAD_PRIO");
-    return e ? atoi(e) : 0;
+    return (e ? atoi(e) : 0) | wslab_late();
   }();
 #define RAG_WSLAB2(NB, BF, MP)                                                                 \
   wgrad_slab_kernel<NB, BF, MP><<<grid, 64 * WS<kN>::Waves, 0, stream>>>(                      \
