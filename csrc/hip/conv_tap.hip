@@ -1311,7 +1311,7 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
       const long long c2 = now();
       int slab_now = 0;  // slab pieces this wave issues in this step (younger than B(s+1)'s)
       if constexpr (!(DIAG & 1)) {
-        if constexpr (SPREAD && !BNP) {
+        if constexpr (SPREAD == 1 && !BNP) {
           // pieces [t*AL/(TAPS-1), (t+1)*AL/(TAPS-1)) at taps 0 .. TAPS-2; all retired by the
           // wait after the last tap's MFMAs, as before
           if (t < TAPS - 1 && more) {
@@ -1319,7 +1319,7 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
             stage_a(q + 1, k0, k1);
             slab_now = k1 - k0;
           }
-        } else {
+        } else if constexpr (SPREAD == 0 || BNP) {
           if (t == 0 && more) {
             stage_a(q + 1);
             slab_now = AL;
@@ -1333,6 +1333,11 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
       const long long c4 = now();
       mfmas();
       const long long c5 = now();
+      if constexpr (SPREAD == 2 && !BNP && !(DIAG & 1)) {
+        // SPREAD = 2: the same pieces issued behind this step's MFMA issue instead of in front of
+        // its fragment reads (as the wgrad slab kernel's stage placement, RAG_WGRAD_LATE)
+        if (t < TAPS - 1 && more) stage_a(q + 1, t * AL / (TAPS - 1), (t + 1) * AL / (TAPS - 1));
+      }
       if constexpr (BNP) {
         // slab(q+1) complete at tap 4, transformed over taps 4..8 (this wave's reads of step s+1
         // drain the writes before the next chunk's X barrier)
@@ -1639,7 +1644,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
       const char* v = getenv("RAG_CONV_PP5");
       return !(v && v[0] == '0');
     }();
-    if (!pp5 || bnc || mcoef || spart || g_tap_mode < 5 || g_tap_mode > 15) return false;
+    if (!pp5 || bnc || mcoef || spart || g_tap_mode < 5 || g_tap_mode > 16) return false;
     // <= 48 real input channels in a 64-channel layout (the caller's hint, rag_conv_igemm_cin):
     // chunk 1 steps pair two taps (PAIR; RAG_CONV_PAIR5=0 disables)
     static const bool pair_on = [] {
@@ -1730,7 +1735,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
   }();
   if (w128) {
     const int nconv = ((M + kPPBM - 1) / kPPBM) * (COUTP / 128);
-    if (g_tap_mode < 5 || g_tap_mode > 15 || cached_rows8 > kPPSlabRows || nconv < pp_min)
+    if (g_tap_mode < 5 || g_tap_mode > 16 || cached_rows8 > kPPSlabRows || nconv < pp_min)
       return false;  // small batches: conv_pipe
     int nred = 0;
     WgradRed r{};
@@ -1772,7 +1777,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
     const char* v = getenv("RAG_CONV_PP192");
     return v && v[0] == '2';
   }();
-  if ((g_tap_mode >= 5 && g_tap_mode <= 15) && cached_rows8 <= kPPSlabRows && pp_fills &&
+  if ((g_tap_mode >= 5 && g_tap_mode <= 16) && cached_rows8 <= kPPSlabRows && pp_fills &&
       !pp192_all) {
     // ping-pong kernel: one block per CU; reduce blocks fill the CUs its last round leaves free
     const int nconv = ((M + kPPBM - 1) / kPPBM) * (COUTP / kBN);
@@ -1815,6 +1820,10 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
       conv_tap_pp_kernel<3, 0, 0, kNT, false, 3, kMT, 0, 0, 1, 0, 0, 2>
           <<<nconv + nred, 512, 0, stream>>>(x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN,
                                              COUTP, YC, relu, HM, total_rows, nconv, r);
+    else if (g_tap_mode == 16)
+      conv_tap_pp_kernel<3, 0, 0, kNT, false, 3, kMT, 2, 0, 1><<<nconv + nred, 512, 0, stream>>>(
+          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
+          nconv, r);
     else if (g_tap_mode == 12)
       conv_tap_pp_kernel<3, 0, 0, kNT, false, 3, kMT, 1, 0, 1><<<nconv + nred, 512, 0, stream>>>(
           x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
@@ -1846,7 +1855,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
     return !(v && v[0] == '0');
   }();
   const int n192 = ((M + kBM - 1) / kBM) * (COUTP / kBN);
-  if (pp192 && g_tap_mode >= 5 && g_tap_mode <= 15 && n192 >= pp_min &&
+  if (pp192 && g_tap_mode >= 5 && g_tap_mode <= 16 && n192 >= pp_min &&
       cached_rows <= kPPSlabRows192) {
     int nred = 0;
     WgradRed r{};
@@ -1897,7 +1906,7 @@ bool rag_conv_tap_bn_ok(int M, int S, int WI, int shift, int CIN, int COUTP, int
   const char* e = getenv("RAG_PP_MIN_BLOCKS");
   const int pp_min = e ? atoi(e) : 200;
   const int nconv = ((M + kPPBM - 1) / kPPBM) * (COUTP / 128);
-  return g_tap_mode >= 5 && g_tap_mode <= 15 && KS == 3 && COUTP % kBN != 0 && COUTP % 128 == 0 &&
+  return g_tap_mode >= 5 && g_tap_mode <= 16 && KS == 3 && COUTP % kBN != 0 && COUTP % 128 == 0 &&
          CIN % kBK == 0 && CIN >= kBK && nconv >= pp_min &&
          max_slab_rows(S, WI, shift, kPPBM) <= kPPSlabRows;
 }

@@ -181,16 +181,17 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
     }
     __syncthreads();
   }
-  auto stage = [&](int s, int buf) {
+  auto stage = [&](int s, int buf, int part = 3) {  // part: 1 the G pieces, 2 the X piece
     const int r0 = (sbeg + s) * kRows;
     bf16* lg = lds + buf * kStage;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
+      if (!(part & 1)) break;
       int r = r0 + grow[k];
       r = r < R ? r : R - 1;  // past the end: the last padded row is halo (zero)
       glds16(G + (size_t)r * GC + gcol[k], lg + (2 * w + k) * 512);
     }
-    if (xw) {
+    if (xw && (part & 2)) {
       int r = r0 + xshift + xrow;
       r = r < 0 ? 0 : (r < R ? r : R - 1);  // only ever paired with zero (halo) G rows
       glds16(X + (size_t)r * CIN + xcol, lg + kGElems + w * 512);
@@ -271,7 +272,8 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
   // prio bits 0-1: MFMA priority mode; bit 2 (RAG_WGRAD_LATE): stage s+kNBUF-1 after the first
   // k-step's MFMAs instead of right after the barrier (the LDS-DMA issues otherwise sit in front
   // of every wave's first fragment reads of the stage)
-  const int late = (prio >> 2) & 3;  // 0: after the barrier, 1: after k-step 0, 2: after k-step 1
+  // 0: after the barrier, 1: after k-step 0, 2: after k-step 1, 3: G after k-step 0, X after 1
+  const int late = (prio >> 2) & 3;
   prio &= 3;
   if (prio == 2 && w >= kWaves - 4) __builtin_amdgcn_s_setprio(1);  // the last-dispatched waves
   for (int s = 0; s < nsteps; ++s) {
@@ -306,7 +308,10 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
 #pragma unroll
         for (int a = 0; a < NA; ++a) acc[i][a] = mfma16(fa[a], fb[i], acc[i][a]);
       if (prio == 0) __builtin_amdgcn_s_setprio(0);
-      if (late == kk + 1 && s + kNBUF - 1 < nsteps) stage(s + kNBUF - 1, (s + kNBUF - 1) % kNBUF);
+      if (s + kNBUF - 1 < nsteps) {
+        if (late == kk + 1) stage(s + kNBUF - 1, (s + kNBUF - 1) % kNBUF);
+        if (late == 3) stage(s + kNBUF - 1, (s + kNBUF - 1) % kNBUF, kk == 0 ? 1 : 2);
+      }
     }
     if constexpr (BNX) {
       // stage s+2 landed (s+3 stays in flight): fetch this lane's chunk for step s+1's xstore
@@ -774,7 +779,7 @@ int wslab_late() {
   static const int v = [] {
     const char* e = getenv("RAG_WGRAD_LATE");
     const int m = e ? atoi(e) : 1;
-    return (m >= 0 && m <= 2 ? m : 1) << 2;
+    return (m >= 0 && m <= 3 ? m : 1) << 2;
   }();
   return v;
 }
