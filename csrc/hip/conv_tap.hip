@@ -1379,9 +1379,16 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
       __builtin_amdgcn_s_barrier();  // X_s
       asm volatile("" ::: "memory");
       const long long c1 = now();
-      if constexpr (ISSUE && !(DIAG & 1)) {
+      if constexpr (ISSUE == 1 && !(DIAG & 1)) {
         // step s - 1's MFMAs carry the loads of B(s - 1 + D)
         if (s > 0) mfmas_staged(s - 1 + D < nsteps ? s - 1 + D : -1);
+      } else if constexpr (ISSUE == 2 && !(DIAG & 1)) {
+        // ISSUE = 2: B(s - 1 + D) issued right behind step s - 1's MFMA issue (the placement that
+        // paid in the wgrad slab kernel), not after this group's fragment reads
+        if (s > 0) {
+          mfmas();
+          if (s - 1 + D < nsteps) stage_b(s - 1 + D, 0, PB1);
+        }
       } else {
         if (s > 0) mfmas();          // step s - 1, beside group 0's reads of step s
       }
@@ -1644,7 +1651,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
       const char* v = getenv("RAG_CONV_PP5");
       return !(v && v[0] == '0');
     }();
-    if (!pp5 || bnc || mcoef || spart || g_tap_mode < 5 || g_tap_mode > 16) return false;
+    if (!pp5 || bnc || mcoef || spart || g_tap_mode < 5 || g_tap_mode > 17) return false;
     // <= 48 real input channels in a 64-channel layout (the caller's hint, rag_conv_igemm_cin):
     // chunk 1 steps pair two taps (PAIR; RAG_CONV_PAIR5=0 disables)
     static const bool pair_on = [] {
@@ -1735,7 +1742,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
   }();
   if (w128) {
     const int nconv = ((M + kPPBM - 1) / kPPBM) * (COUTP / 128);
-    if (g_tap_mode < 5 || g_tap_mode > 16 || cached_rows8 > kPPSlabRows || nconv < pp_min)
+    if (g_tap_mode < 5 || g_tap_mode > 17 || cached_rows8 > kPPSlabRows || nconv < pp_min)
       return false;  // small batches: conv_pipe
     int nred = 0;
     WgradRed r{};
@@ -1777,7 +1784,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
     const char* v = getenv("RAG_CONV_PP192");
     return v && v[0] == '2';
   }();
-  if ((g_tap_mode >= 5 && g_tap_mode <= 16) && cached_rows8 <= kPPSlabRows && pp_fills &&
+  if ((g_tap_mode >= 5 && g_tap_mode <= 17) && cached_rows8 <= kPPSlabRows && pp_fills &&
       !pp192_all) {
     // ping-pong kernel: one block per CU; reduce blocks fill the CUs its last round leaves free
     const int nconv = ((M + kPPBM - 1) / kPPBM) * (COUTP / kBN);
@@ -1820,6 +1827,10 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
       conv_tap_pp_kernel<3, 0, 0, kNT, false, 3, kMT, 0, 0, 1, 0, 0, 2>
           <<<nconv + nred, 512, 0, stream>>>(x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN,
                                              COUTP, YC, relu, HM, total_rows, nconv, r);
+    else if (g_tap_mode == 17)
+      conv_tap_pp_kernel<3, 0, 2, kNT, false, 3, kMT, 1, 0, 1><<<nconv + nred, 512, 0, stream>>>(
+          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
+          nconv, r);
     else if (g_tap_mode == 16)
       conv_tap_pp_kernel<3, 0, 0, kNT, false, 3, kMT, 2, 0, 1><<<nconv + nred, 512, 0, stream>>>(
           x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
@@ -1855,7 +1866,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
     return !(v && v[0] == '0');
   }();
   const int n192 = ((M + kBM - 1) / kBM) * (COUTP / kBN);
-  if (pp192 && g_tap_mode >= 5 && g_tap_mode <= 16 && n192 >= pp_min &&
+  if (pp192 && g_tap_mode >= 5 && g_tap_mode <= 17 && n192 >= pp_min &&
       cached_rows <= kPPSlabRows192) {
     int nred = 0;
     WgradRed r{};
@@ -1906,7 +1917,7 @@ bool rag_conv_tap_bn_ok(int M, int S, int WI, int shift, int CIN, int COUTP, int
   const char* e = getenv("RAG_PP_MIN_BLOCKS");
   const int pp_min = e ? atoi(e) : 200;
   const int nconv = ((M + kPPBM - 1) / kPPBM) * (COUTP / 128);
-  return g_tap_mode >= 5 && g_tap_mode <= 16 && KS == 3 && COUTP % kBN != 0 && COUTP % 128 == 0 &&
+  return g_tap_mode >= 5 && g_tap_mode <= 17 && KS == 3 && COUTP % kBN != 0 && COUTP % 128 == 0 &&
          CIN % kBK == 0 && CIN >= kBK && nconv >= pp_min &&
          max_slab_rows(S, WI, shift, kPPBM) <= kPPSlabRows;
 }
