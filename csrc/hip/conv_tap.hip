@@ -829,7 +829,7 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
   constexpr int kL = kLoop > BM * EpRow ? kLoop : BM * EpRow;  // loop ring | epilogue image
   // weight tiles staged ahead of the current step (issued in the MFMA segment, the slot's last
   // reader is one phase further back: NB tiles ahead are safe)
-  constexpr int D = ISSUE ? NB : NB - 1;
+  constexpr int D = (ISSUE == 1 || ISSUE == 2) ? NB : NB - 1;
   // + a [2][64] float BN-statistics accumulator past the ring / epilogue image
   __shared__ __attribute__((aligned(16))) bf16 lds[kL + 256];
   // claimed reductions (red.ticket) ride only in 128-wide launches: the 192-wide kernels keep
@@ -1326,7 +1326,15 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
           }
         }
       }
-      read_frags(s);
+      if constexpr (SPREAD == 3 && !BNP && !(DIAG & 3)) {
+        // SPREAD = 3: the same pieces issued between this step's fragment reads and their retire
+        // (the LDS-DMA issue overlaps the reads' latency instead of delaying them)
+        read_into(s, xa, wb);
+        if (t < TAPS - 1 && more) stage_a(q + 1, t * AL / (TAPS - 1), (t + 1) * AL / (TAPS - 1));
+        lds_reads_done();
+      } else {
+        read_frags(s);
+      }
       const long long c3 = now();
       __builtin_amdgcn_s_barrier();  // Y_s
       asm volatile("" ::: "memory");
@@ -1396,16 +1404,25 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
       __builtin_amdgcn_s_barrier();  // Y_s
       asm volatile("" ::: "memory");
       const long long c3 = now();
-      read_frags(s);                 // beside group 0's MFMAs of step s
+      if constexpr (ISSUE == 3 && !(DIAG & 3)) {
+        // ISSUE = 3: B(s+D) issued between this group's fragment reads and their retire
+        read_into(s, xa, wb);
+        if (s + D < nsteps) stage_b(s + D, 0, PB1);
+        lds_reads_done();
+      } else {
+        read_frags(s);               // beside group 0's MFMAs of step s
+      }
       const long long c4 = now();
       if constexpr (!(DIAG & 1)) {
-        if constexpr (ISSUE) {
+        if constexpr (ISSUE == 1 || ISSUE == 2) {
           // B(s+1) complete before X_{s+1}: issued so far are B(.. min(s-1+D, nsteps-1))
           int last = s - 1 + D < nsteps - 1 ? s - 1 + D : nsteps - 1;
           const int yb = last - (s + 1);
           wait_vm_rt(yb > 0 ? yb * PPBL : 0);
         } else {
-          if (s + D < nsteps) stage_b(s + D, 0, PB1);
+          if constexpr (ISSUE != 3) {
+            if (s + D < nsteps) stage_b(s + D, 0, PB1);
+          }
           // B(s+1) complete before X_{s+1}: younger are B(s+2 .. min(s+D, nsteps-1))
           int yb = nsteps - 2 - s;
           yb = yb < D - 1 ? yb : D - 1;
@@ -1651,7 +1668,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
       const char* v = getenv("RAG_CONV_PP5");
       return !(v && v[0] == '0');
     }();
-    if (!pp5 || bnc || mcoef || spart || g_tap_mode < 5 || g_tap_mode > 17) return false;
+    if (!pp5 || bnc || mcoef || spart || g_tap_mode < 5 || g_tap_mode > 20) return false;
     // <= 48 real input channels in a 64-channel layout (the caller's hint, rag_conv_igemm_cin):
     // chunk 1 steps pair two taps (PAIR; RAG_CONV_PAIR5=0 disables)
     static const bool pair_on = [] {
@@ -1742,7 +1759,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
   }();
   if (w128) {
     const int nconv = ((M + kPPBM - 1) / kPPBM) * (COUTP / 128);
-    if (g_tap_mode < 5 || g_tap_mode > 17 || cached_rows8 > kPPSlabRows || nconv < pp_min)
+    if (g_tap_mode < 5 || g_tap_mode > 20 || cached_rows8 > kPPSlabRows || nconv < pp_min)
       return false;  // small batches: conv_pipe
     int nred = 0;
     WgradRed r{};
@@ -1784,7 +1801,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
     const char* v = getenv("RAG_CONV_PP192");
     return v && v[0] == '2';
   }();
-  if ((g_tap_mode >= 5 && g_tap_mode <= 17) && cached_rows8 <= kPPSlabRows && pp_fills &&
+  if ((g_tap_mode >= 5 && g_tap_mode <= 20) && cached_rows8 <= kPPSlabRows && pp_fills &&
       !pp192_all) {
     // ping-pong kernel: one block per CU; reduce blocks fill the CUs its last round leaves free
     const int nconv = ((M + kPPBM - 1) / kPPBM) * (COUTP / kBN);
@@ -1827,6 +1844,18 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
       conv_tap_pp_kernel<3, 0, 0, kNT, false, 3, kMT, 0, 0, 1, 0, 0, 2>
           <<<nconv + nred, 512, 0, stream>>>(x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN,
                                              COUTP, YC, relu, HM, total_rows, nconv, r);
+    else if (g_tap_mode == 18)
+      conv_tap_pp_kernel<3, 0, 0, kNT, false, 3, kMT, 3, 0, 1><<<nconv + nred, 512, 0, stream>>>(
+          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
+          nconv, r);
+    else if (g_tap_mode == 19)
+      conv_tap_pp_kernel<3, 0, 3, kNT, false, 3, kMT, 1, 0, 1><<<nconv + nred, 512, 0, stream>>>(
+          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
+          nconv, r);
+    else if (g_tap_mode == 20)
+      conv_tap_pp_kernel<3, 0, 3, kNT, false, 3, kMT, 3, 0, 1><<<nconv + nred, 512, 0, stream>>>(
+          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
+          nconv, r);
     else if (g_tap_mode == 17)
       conv_tap_pp_kernel<3, 0, 2, kNT, false, 3, kMT, 1, 0, 1><<<nconv + nred, 512, 0, stream>>>(
           x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
@@ -1866,7 +1895,7 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
     return !(v && v[0] == '0');
   }();
   const int n192 = ((M + kBM - 1) / kBM) * (COUTP / kBN);
-  if (pp192 && g_tap_mode >= 5 && g_tap_mode <= 17 && n192 >= pp_min &&
+  if (pp192 && g_tap_mode >= 5 && g_tap_mode <= 20 && n192 >= pp_min &&
       cached_rows <= kPPSlabRows192) {
     int nred = 0;
     WgradRed r{};
@@ -1917,7 +1946,7 @@ bool rag_conv_tap_bn_ok(int M, int S, int WI, int shift, int CIN, int COUTP, int
   const char* e = getenv("RAG_PP_MIN_BLOCKS");
   const int pp_min = e ? atoi(e) : 200;
   const int nconv = ((M + kPPBM - 1) / kPPBM) * (COUTP / 128);
-  return g_tap_mode >= 5 && g_tap_mode <= 17 && KS == 3 && COUTP % kBN != 0 && COUTP % 128 == 0 &&
+  return g_tap_mode >= 5 && g_tap_mode <= 20 && KS == 3 && COUTP % kBN != 0 && COUTP % 128 == 0 &&
          CIN % kBK == 0 && CIN >= kBK && nconv >= pp_min &&
          max_slab_rows(S, WI, shift, kPPBM) <= kPPSlabRows;
 }

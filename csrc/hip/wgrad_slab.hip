@@ -773,7 +773,7 @@ WgradRed rag_wgrad_slab_red(const void* part, const float* bpart, float* dW, flo
 
 // Where the slab kernels issue a stage's LDS-DMA (prio bits 2-3; RAG_WGRAD_LATE): 1 (default)
 // after the first k-step's MFMAs -- SL 110.2-110.7k -> 113.5-114.0k positions/s on one box
-// (profiles/wgrad_late_r4.txt) --, 2 after the second, 0 right after the stage barrier (the
+// (profiles/dma_placement_r4.txt) --, 2 after the second, 0 right after the stage barrier (the
 // round-3 placement: every wave's 2-3 issues delayed its first fragment reads of the stage).
 int wslab_late() {
   static const int v = [] {
