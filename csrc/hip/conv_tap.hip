@@ -1712,11 +1712,22 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
     }
     // (the spread / static-priority 3x3 variants measured slower on the 5x5 layer: 52.9-53.7
     // vs 49.9 us, profiles/conv_variants_r4b.txt; every mode runs the plain ping-pong here)
-    if (w192 && pair5)
-      conv_tap_pp_kernel<3, 0, 0, 6, false, 5, kMT, 0, 0, 0, 1><<<nconv + nred, 512, 0,
-                                                                   stream>>>(
-          x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
-          nconv, r);
+    // RAG_CONV5_VAR (A/B of the paired 192-filter input layer): 1 static priority, 2 spread
+    // slab + static priority, 3 a 4-deep weight ring
+    static const int v5 = [] {
+      const char* e = getenv("RAG_CONV5_VAR");
+      return e ? atoi(e) : 0;
+    }();
+#define RAG_PP5(NBV, SPV, PRV)                                                                   \
+  conv_tap_pp_kernel<NBV, 0, 0, 6, false, 5, kMT, SPV, 0, PRV, 1><<<nconv + nred, 512, 0, stream>>>( \
+      x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows, nconv, r)
+    if (w192 && pair5) {
+      if (v5 == 1) RAG_PP5(3, 0, 1);
+      else if (v5 == 2) RAG_PP5(3, 1, 1);
+      else if (v5 == 3) RAG_PP5(4, 0, 0);
+      else RAG_PP5(3, 0, 0);
+    }
+#undef RAG_PP5
     else if (w192)
       conv_tap_pp_kernel<3, 0, 0, 6, false, 5><<<nconv + nred, 512, 0, stream>>>(
           x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM, total_rows,
