@@ -58,6 +58,8 @@ STEPS = {
                  " benchmarks/rl_bench.py --config 19 --game-batch 256", "tail1"),
     "trace-cnn128": (300, "rocprofv3 --kernel-trace --stats -d {dir} -o cnn -- " + PY +
                      " bench.py --filters 128 --no-mcts --steps 10 --warmup 3", "tail1"),
+    "trace-value": (300, "rocprofv3 --kernel-trace --stats -d {dir} -o val -- " + PY +
+                    " bench.py --model value --no-mcts --steps 10 --warmup 3", "tail1"),
     "rl512": (300, PY + " benchmarks/rl_bench.py --config 19 --game-batch 512", "json"),
     "valuegen": (300, PY + " benchmarks/value_gen_bench.py", "json"),
     "kernels": (600, PY + " -m pytest tests/test_hip_kernels.py tests/test_gpu_models.py "
