@@ -30,7 +30,31 @@ __global__ void sl_batch_kernel(const int64_t* __restrict__ index,
   lab_out[i] = tf_table[(size_t)t * P + labels[index[i]]];
 }
 
+// The value-net step's batch: tf_out[i] as sl_batch, y_out[i] = values[index[i]] (the outcome
+// is invariant under the board's symmetries).
+__global__ void value_batch_kernel(const int64_t* __restrict__ index,
+                                   const float* __restrict__ values,
+                                   const int* __restrict__ sym, int nsym, uint32_t seed,
+                                   uint32_t step, int* __restrict__ tf_out,
+                                   float* __restrict__ y_out, int B) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  const uint32_t h = mix32(seed ^ mix32(step * 0x9E3779B9u + (uint32_t)i * 0x85EBCA6Bu + 1u));
+  tf_out[i] = sym[h % (uint32_t)nsym];
+  y_out[i] = values[index[i]];
+}
+
 }  // namespace
+
+RAG_API int rag_value_batch(const int64_t* index, const float* values, const int* sym, int nsym,
+                            unsigned seed, unsigned step, int* tf_out, float* y_out, int B,
+                            hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (nsym <= 0) return -1;
+  value_batch_kernel<<<(B + 255) / 256, 256, 0, stream>>>(index, values, sym, nsym, seed, step,
+                                                          tf_out, y_out, B);
+  return (int)hipGetLastError();
+}
 
 RAG_API int rag_sl_batch(const int64_t* index, const int64_t* labels, const int64_t* tf_table,
                          int P, const int* sym, int nsym, unsigned seed, unsigned step,

@@ -38,6 +38,7 @@ SIGNATURES = {
     "rag_value_mlp_workspace": [I, I],
     "rag_value_mlp_bwd": [P] * 16 + [I, I, I, I, P],
     "rag_sl_batch": [P, P, P, I, P, I, C.c_uint, C.c_uint, P, P, I, P],
+    "rag_value_batch": [P, P, P, I, C.c_uint, C.c_uint, P, P, I, P],
     "rag_value_mlp_bwd_workspace": [I, I],
     # optim.hip
     "rag_sgd": [P, P, P, I64, F, F, F, I, P],

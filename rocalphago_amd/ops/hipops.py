@@ -464,6 +464,24 @@ def sl_batch(index, labels, tf_table, sym, seed, step, tf_out=None, lab_out=None
     return tf_out, lab_out
 
 
+def value_batch(index, values, sym, seed, step, tf_out=None, y_out=None):
+    """One launch per value-net step (batch.hip): a random allowed dihedral transform per sampled
+    row (int32 [B]) and its target outcome values[index] (float [B, 1])."""
+    B = index.numel()
+    dev = index.device
+    for t, dt in ((index, torch.int64), (values, torch.float32), (sym, torch.int32)):
+        if t.dtype != dt or not t.is_contiguous():
+            raise ValueError("value_batch: bad dtype / layout")
+    if tf_out is None:
+        tf_out = torch.empty(B, dtype=torch.int32, device=dev)
+    if y_out is None:
+        y_out = torch.empty((B, 1), dtype=torch.float32, device=dev)
+    _check(_lib().rag_value_batch(_ptr(index), _ptr(values), _ptr(sym), sym.numel(),
+                                  ctypes.c_uint(seed & 0xFFFFFFFF), ctypes.c_uint(step & 0xFFFFFFFF),
+                                  _ptr(tf_out), _ptr(y_out), B, _stream()), "value_batch")
+    return tf_out, y_out
+
+
 _mlp_train_ws = {}
 
 

@@ -212,7 +212,8 @@ class ValueTrainer(object):
         self.sym = torch.tensor(transform_ids(symmetries or ["noop"]), dtype=torch.int32,
                                 device=self.dev)
         self.gen = torch.Generator(device=self.dev)
-        self.gen.manual_seed(seed + (dp.rank if dp else 0))
+        self.seed = seed + (dp.rank if dp else 0)
+        self.gen.manual_seed(self.seed)
         self.plan = value_model._plan_for() if self.dev.type == "cuda" else None
         self.bucketer = None
         if self.plan is not None and dp is not None and dp.enabled:
@@ -227,18 +228,22 @@ class ValueTrainer(object):
     def step(self, index):
         n = index.numel()
         model = self.model
-        tf = self.sym[torch.randint(0, self.sym.numel(), (n,), generator=self.gen,
-                                    device=self.dev)]
-        y = self.values[index]
         if self.plan is not None:
+            # one launch for the transforms and the targets (batch.hip), as the SL step does
+            from ..ops import hipops as ops
+            tf, y = ops.value_batch(index.long().contiguous(), self.values.reshape(-1),
+                                    self.sym, self.seed, self.count)
             B = self.plan.prepare(self.states, index=index, transforms=tf)
             hook = self.bucketer.layer_done if self.bucketer else None
             loss = self.plan.fwd_bwd(B, y, None, on_layer_grads=hook)
             if self.bucketer:
                 self.bucketer.finish()
             model.optimizer.apply(model.net)
-            self.loss_sum += loss * n
+            self.loss_sum.add_(loss, alpha=n)
         else:
+            tf = self.sym[torch.randint(0, self.sym.numel(), (n,), generator=self.gen,
+                                        device=self.dev)]
+            y = self.values[index]
             X = self._host_states(index, tf)
             saved = model.grad_allreduce
             if self.dp is not None and self.dp.enabled:
