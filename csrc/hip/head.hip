@@ -38,7 +38,8 @@ policy_head_fwd_kernel(const bf16* __restrict__ H, const float* __restrict__ w, 
                        float* __restrict__ loss, float* __restrict__ dz, float* __restrict__ hit,
                        const float* __restrict__ pass_w, const float* __restrict__ pass_b,
                        float* __restrict__ zout, float* __restrict__ dpass,
-                       float* __restrict__ acc, int S, int KP, int K, int mode, float gscale) {
+                       float* __restrict__ acc, int S, int KP, int K, int mode, float gscale,
+                       float* __restrict__ dzsum = nullptr) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* z = smem;                        // S*S logits (+ the pass logit)
   float* ws = smem + ((S * S + 4) & ~3);  // KP weights
@@ -48,16 +49,28 @@ policy_head_fwd_kernel(const bf16* __restrict__ H, const float* __restrict__ w, 
   for (int k = threadIdx.x; k < KP; k += blockDim.x) ws[k] = k < K ? w[k] : 0.f;
   __syncthreads();
   const float bias0 = b0 ? *b0 : 0.f;
-  for (int p = threadIdx.x; p < S2; p += blockDim.x) {
-    const int i = p / S, j = p - (p / S) * S;
-    const bf16* row = H + ((size_t)(b * WP + i + 1) * WP + j + 1) * KP;
-    float acc = 0.f;
-    for (int c = 0; c < KP; c += 8) {
-      const bf16x8 v = *reinterpret_cast<const bf16x8*>(row + c);
+  // 8 lanes per pixel, each a 16-byte slice of every 128-byte channel segment: a wave's load
+  // instruction reads 8 pixels x 128 contiguous bytes (one lane per pixel read 384-byte rows in
+  // 16-byte steps, one dependent load after another: 18 us for B = 256), then a 3-step
+  // cross-lane sum
+  {
+    const int sub = threadIdx.x & 7;
+    for (int p0 = threadIdx.x >> 3; p0 < ((S2 + 7) & ~7); p0 += blockDim.x >> 3) {
+      const int p = p0 < S2 ? p0 : S2 - 1;
+      const int i = p / S, j = p - (p / S) * S;
+      const bf16* row = H + ((size_t)(b * WP + i + 1) * WP + j + 1) * KP;
+      float acc = 0.f;
+#pragma unroll 4
+      for (int c = sub * 8; c < KP; c += 64) {
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(row + c);
 #pragma unroll
-      for (int t = 0; t < 8; ++t) acc += (float)v[t] * ws[c + t];
+        for (int t = 0; t < 8; ++t) acc += (float)v[t] * ws[c + t];
+      }
+      acc += __shfl_xor(acc, 1);
+      acc += __shfl_xor(acc, 2);
+      acc += __shfl_xor(acc, 4);
+      if (sub == 0 && p0 < S2) z[p] = acc + bias0 + (pbias ? pbias[p] : 0.f);
     }
-    z[p] = acc + bias0 + (pbias ? pbias[p] : 0.f);
   }
   __syncthreads();
   // optional pass logit (PassLogit layer): W . z + b over the position logits, the
@@ -99,13 +112,20 @@ policy_head_fwd_kernel(const bf16* __restrict__ H, const float* __restrict__ w, 
       if (mode && dpass) dpass[b] = dp;
     }
   }
+  float dsum = 0.f;
   for (int p = threadIdx.x; p < S2; p += blockDim.x) {
     const float pr = __expf(z[p] - gmax) * inv;
     probs[(size_t)b * C + p] = pr;
     if (mode && dz) {
       const float y = (p == lab) ? 1.f : 0.f;
-      dz[(size_t)b * S2 + p] = (pr - y) * sw * cls * gscale + (has_pass ? dp * pass_w[p] : 0.f);
+      const float d = (pr - y) * sw * cls * gscale + (has_pass ? dp * pass_w[p] : 0.f);
+      dz[(size_t)b * S2 + p] = d;
+      dsum += d;
     }
+  }
+  if (mode && dz && dzsum) {  // the board's sum of dz (block-uniform branch), for db0
+    dsum = block_reduce(dsum, red, false);
+    if (threadIdx.x == 0) dzsum[b] = dsum;
   }
   if (mode && threadIdx.x == 0 && lab >= 0) {
     float pl = __expf(z[lab] - gmax) * inv;
@@ -213,10 +233,52 @@ head_bwd_kernel(const bf16* __restrict__ H, const float* __restrict__ w,
 __global__ void __launch_bounds__(1024)
 head_bwd_reduce_kernel(const float* __restrict__ dwpart, const float* __restrict__ dz,
                        float* __restrict__ dw, float* __restrict__ db0,
-                       float* __restrict__ dpbias, int nblk, int B, int S2, int KP, int K) {
+                       float* __restrict__ dpbias, int nblk, int B, int S2, int KP, int K,
+                       const float* __restrict__ mloss = nullptr,
+                       const float* __restrict__ mhit = nullptr, float* __restrict__ acc = nullptr,
+                       const float* __restrict__ dzsum = nullptr) {
   __shared__ float red[16][65];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int kt = (K + 63) / 64;
+  if ((int)blockIdx.x == (int)gridDim.x - 1) {
+    // the last block: db0 = sum of all dz (fixed summation order, so the step is bit-for-bit
+    // reproducible -- per-block atomics made it depend on block timing), and the forward's
+    // running metrics acc[0] += sum loss, acc[1] += sum hit (instead of two contended device
+    // atomics per board in the head forward)
+    float d = 0.f, a = 0.f, h = 0.f;
+    if (db0 && dzsum)  // the head forward's per-board sums
+      for (int i = threadIdx.x; i < B; i += blockDim.x) d += dzsum[i];
+    else if (db0)
+      for (size_t i = threadIdx.x; i < (size_t)B * S2; i += blockDim.x) d += dz[i];
+    if (acc)
+      for (int i = threadIdx.x; i < B; i += blockDim.x) {
+        a += mloss[i];
+        h += mhit[i];
+      }
+    d = warp_sum(d);
+    a = warp_sum(a);
+    h = warp_sum(h);
+    if (tx == 0) {
+      red[ty][0] = d;
+      red[ty][1] = a;
+      red[ty][2] = h;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float sd = 0.f, sa = 0.f, sh = 0.f;
+      for (int k = 0; k < (int)(blockDim.x >> 6); ++k) {
+        sd += red[k][0];
+        sa += red[k][1];
+        sh += red[k][2];
+      }
+      if (db0) *db0 = sd;
+      if (acc) {
+        acc[0] += sa;
+        acc[1] += sh;
+      }
+    }
+    return;
+  }
   const bool isw = (int)blockIdx.x < kt;
   const int col = (isw ? (int)blockIdx.x : (int)blockIdx.x - kt) * 64 + tx;
   const int ncol = isw ? K : S2;
@@ -249,12 +311,6 @@ head_bwd_reduce_kernel(const float* __restrict__ dwpart, const float* __restrict
         dpbias[col] = v;
       }
     }
-    if (!isw && db0) {  // one atomic per block: the sum of its dpbias columns
-      v = col < ncol ? v : 0.f;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-      if (tx == 0) atomicAdd(db0, v);
-    }
   }
 }
 
@@ -264,19 +320,28 @@ head_linear_kernel(const bf16* __restrict__ H, const float* __restrict__ w, cons
                    float* __restrict__ z, int B, int S, int KP, int K) {
   const int S2 = S * S, WP = S + 2;
   const int total = B * S2;
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += gridDim.x * blockDim.x) {
+  // 8 lanes per pixel (coalesced 128-byte channel segments, as policy_head_fwd_kernel)
+  const int sub = threadIdx.x & 7;
+  const int lanes = gridDim.x * blockDim.x;
+  for (int t0 = blockIdx.x * blockDim.x + threadIdx.x; t0 < ((total * 8 + lanes - 1) / lanes) *
+       lanes; t0 += lanes) {
+    const int idx0 = t0 >> 3;
+    const int idx = idx0 < total ? idx0 : total - 1;
     const int b = idx / S2, p = idx - (idx / S2) * S2;
     const int i = p / S, j = p - (p / S) * S;
     const bf16* row = H + ((size_t)(b * WP + i + 1) * WP + j + 1) * KP;
     float acc = 0.f;
-    for (int c = 0; c < K; c += 8) {
+#pragma unroll 4
+    for (int c = sub * 8; c < K; c += 64) {
       const bf16x8 v = *reinterpret_cast<const bf16x8*>(row + c);
 #pragma unroll
       for (int t = 0; t < 8; ++t)
         if (c + t < K) acc += (float)v[t] * w[c + t];
     }
-    z[idx] = acc + (b0 ? *b0 : 0.f);
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    acc += __shfl_xor(acc, 4);
+    if (sub == 0 && idx0 < total) z[idx] = acc + (b0 ? *b0 : 0.f);
   }
 }
 
@@ -424,6 +489,21 @@ RAG_API int rag_policy_head_fwd(const void* H, const float* w, const float* b0,
   return (int)hipGetLastError();
 }
 
+// As rag_policy_head_fwd, plus dzsum [B]: each board's sum of dz (the head bias gradient's
+// per-board term, summed in a fixed order by rag_head_bwd_m).
+RAG_API int rag_policy_head_fwd_s(const void* H, const float* w, const float* b0,
+                                  const float* pbias, float* probs, const int64_t* labels,
+                                  const float* sweight, float* loss, float* dz, float* hit,
+                                  float* acc, float* dzsum, int B, int S, int KP, int K, int mode,
+                                  float gscale, hipStream_t stream) {
+  const size_t sm = (size_t)(((S * S + 4) & ~3) + KP) * sizeof(float);
+  policy_head_fwd_kernel<<<B, kHeadFwdThreads, sm, stream>>>((const bf16*)H, w, b0, pbias, probs,
+                                                          labels, sweight, loss, dz, hit, nullptr,
+                                                          nullptr, nullptr, nullptr, acc, S, KP,
+                                                          K, mode, gscale, dzsum);
+  return (int)hipGetLastError();
+}
+
 // With a pass logit (pass_w [S*S], pass_b [1]): probs [B, S*S + 1], labels may be S*S (pass),
 // zout [B, S*S] receives the position logits and dpass [B] dL/d(pass logit) for the PassLogit
 // weight gradients (dW = dpass^T zout, db = sum dpass); dz already carries dpass * pass_w.
@@ -442,9 +522,12 @@ RAG_API int rag_policy_head_pass_fwd(const void* H, const float* w, const float*
   return (int)hipGetLastError();
 }
 
-RAG_API int rag_head_bwd(const void* H, const float* w, const float* dz, void* dH, float* dw,
-                         float* db0, float* dpbias, float* work, int B, int S, int KP, int K,
-                         int relu_mask, hipStream_t stream) {
+// mloss / mhit / acc (optional): the head forward's per-board loss and top-1 hit (written with
+// a null acc), summed into the running metrics acc[0..1] by one extra reduce block.
+RAG_API int rag_head_bwd_m(const void* H, const float* w, const float* dz, void* dH, float* dw,
+                           float* db0, float* dpbias, float* work, int B, int S, int KP, int K,
+                           int relu_mask, const float* mloss, const float* mhit, float* acc,
+                           const float* dzsum, hipStream_t stream) {
   // work: >= rag_head_bwd_workspace(B, S, KP) floats
   const int npix = B * S * S;
   int nblk = (npix + 47) / 48;
@@ -462,9 +545,16 @@ RAG_API int rag_head_bwd(const void* H, const float* w, const float* dz, void* d
   }
 #undef RAG_HB
   const int rblocks = (K + 63) / 64 + (S * S + 63) / 64;
-  head_bwd_reduce_kernel<<<rblocks, 1024, 0, stream>>>(work, dz, dw, db0, dpbias, nblk, B, S * S,
-                                                       KP, K);
+  head_bwd_reduce_kernel<<<rblocks + 1, 1024, 0, stream>>>(
+      work, dz, dw, db0, dpbias, nblk, B, S * S, KP, K, mloss, mhit, acc, dzsum);
   return (int)hipGetLastError();
+}
+
+RAG_API int rag_head_bwd(const void* H, const float* w, const float* dz, void* dH, float* dw,
+                         float* db0, float* dpbias, float* work, int B, int S, int KP, int K,
+                         int relu_mask, hipStream_t stream) {
+  return rag_head_bwd_m(H, w, dz, dH, dw, db0, dpbias, work, B, S, KP, K, relu_mask, nullptr,
+                        nullptr, nullptr, nullptr, stream);
 }
 
 RAG_API size_t rag_head_bwd_workspace(int B, int S, int KP) {
@@ -477,7 +567,7 @@ RAG_API size_t rag_head_bwd_workspace(int B, int S, int KP) {
 RAG_API int rag_head_linear(const void* H, const float* w, const float* b0, float* z, int B,
                             int S, int KP, int K, hipStream_t stream) {
   const int total = B * S * S;
-  const int blocks = (total + kHeadThreads - 1) / kHeadThreads;
+  const int blocks = (int)(((size_t)total * 8 + kHeadThreads - 1) / kHeadThreads);  // 8 lanes / pixel
   head_linear_kernel<<<blocks < 4096 ? blocks : 4096, kHeadThreads, 0, stream>>>(
       (const bf16*)H, w, b0, z, B, S, KP, K);
   return (int)hipGetLastError();

@@ -492,6 +492,7 @@ class PolicyHeadEngine(object):
         self.dz = torch.empty((B, S2), device=dev)
         self.loss = torch.empty((B,), device=dev)
         self.hit = torch.empty((B,), device=dev)
+        self.dzsum = torch.empty((B,), device=dev)
         if self.pass_logit:
             self.zpos = torch.empty((B, S2), device=dev)
             self.dpass = torch.empty((B,), device=dev)
@@ -507,10 +508,15 @@ class PolicyHeadEngine(object):
         if pass_params is not None:
             pk = dict(pass_w=pass_params[0], pass_b=pass_params[1], zout=self.zpos[:B],
                       dpass=self.dpass[:B] if mode else None)
+        # running metrics: summed by the backward's reduce launch from the per-board loss / hit
+        # (acc in the forward kernel meant two contended device atomics per board)
+        self._macc = acc if mode else None
         ops.policy_head_fwd(h, w, b0, pbias, self.probs[:B], self.K, labels=labels,
                             sweight=sweight, loss=self.loss[:B] if mode else None,
                             dz=self.dz[:B] if mode else None, hit=self.hit[:B] if mode else None,
-                            mode=mode, gscale=gscale, acc=acc, **pk)
+                            mode=mode, gscale=gscale, acc=None if mode else acc,
+                            dzsum=self.dzsum[:B] if (mode and not pk) else None, **pk)
+        self._dzsum = bool(mode and not pk)
         return self.probs[:B]
 
     def pass_grads(self, B, dW, db):
@@ -521,8 +527,11 @@ class PolicyHeadEngine(object):
     def backward(self, B, w, dz, dw, db0, dpbias):
         """dz [B, S*S] -> head param grads + trunk top gradient (ReLU-masked) in grad buffer 0."""
         h = self.trunk.output(B)
+        acc, self._macc = getattr(self, "_macc", None), None
         ops.head_bwd(h, w, dz, self.trunk.top_grad(B), dw, db0, dpbias, self.K,
-                     relu_mask=self.trunk.top_relu)
+                     relu_mask=self.trunk.top_relu,
+                     metrics=(self.loss[:B], self.hit[:B], acc) if acc is not None else None,
+                     dzsum=self.dzsum[:B] if getattr(self, "_dzsum", False) else None)
 
 
 class ValueHeadEngine(object):

@@ -32,6 +32,8 @@ SIGNATURES = {
     "rag_policy_head_pass_fwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F,
                                  P],
     "rag_head_bwd": [P, P, P, P, P, P, P, P, I, I, I, I, I, P],
+    "rag_head_bwd_m": [P, P, P, P, P, P, P, P, I, I, I, I, I, P, P, P, P, P],
+    "rag_policy_head_fwd_s": [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, P],
     "rag_head_bwd_workspace": [I, I, I],
     "rag_head_linear": [P, P, P, P, I, I, I, I, P],
     "rag_value_mlp_fwd": [P, P, P, P, P, P, P, P, I, I, I, I, P],

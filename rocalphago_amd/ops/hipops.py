@@ -354,7 +354,7 @@ def pack_nchw(t, H, CP, out=None):
 
 def policy_head_fwd(h, w, b0, pbias, probs, K, labels=None, sweight=None, loss=None, dz=None,
                     hit=None, mode=0, gscale=1.0, pass_w=None, pass_b=None, zout=None,
-                    dpass=None, acc=None):
+                    dpass=None, acc=None, dzsum=None):
     """Fused 1x1 conv + bias + softmax (+ loss / dL/dz). With ``pass_w``/``pass_b`` (PassLogit)
     probs are [B, S*S + 1] (pass last), ``zout`` gets the position logits and ``dpass`` the
     pass-logit gradient for the PassLogit weight gradients. ``acc`` (fp32 [2], optional): the
@@ -369,6 +369,12 @@ def policy_head_fwd(h, w, b0, pbias, probs, K, labels=None, sweight=None, loss=N
             _ptr(labels), _ptr(sweight), _ptr(loss), _ptr(dz), _ptr(hit), _ptr(zout),
             _ptr(dpass), _ptr(acc), B, S, KP, K, mode, float(gscale), _stream()),
             "policy_head_pass_fwd")
+        return
+    if dzsum is not None:  # + each board's sum of dz (head_bwd's fixed-order db0)
+        _check(_lib().rag_policy_head_fwd_s(_ptr(h), _ptr(w), _ptr(b0), _ptr(pbias), _ptr(probs),
+                                            _ptr(labels), _ptr(sweight), _ptr(loss), _ptr(dz),
+                                            _ptr(hit), _ptr(acc), _ptr(dzsum), B, S, KP, K, mode,
+                                            float(gscale), _stream()), "policy_head_fwd")
         return
     _check(_lib().rag_policy_head_fwd(_ptr(h), _ptr(w), _ptr(b0), _ptr(pbias), _ptr(probs),
                                       _ptr(labels), _ptr(sweight), _ptr(loss), _ptr(dz),
@@ -388,8 +394,11 @@ def pass_grads(zout, dpass, dW, db):
 _head_ws = {}
 
 
-def head_bwd(h, w, dz, dh, dw, db0, dpbias, K, relu_mask=True, work=None):
-    """dH (ReLU-masked) + dw / db0 / dpbias (all overwritten, not accumulated)."""
+def head_bwd(h, w, dz, dh, dw, db0, dpbias, K, relu_mask=True, work=None, metrics=None,
+             dzsum=None):
+    """dH (ReLU-masked) + dw / db0 / dpbias (all overwritten, not accumulated). ``metrics``:
+    (loss [B], hit [B], acc fp32 [2]) -- the head forward's per-board values, added to the
+    running sums acc by the reduce launch (policy_head_fwd then runs with acc=None)."""
     B, WP, _, KP = h.shape
     S = WP - 2
     if work is None:
@@ -398,8 +407,17 @@ def head_bwd(h, w, dz, dh, dw, db0, dpbias, K, relu_mask=True, work=None):
         if work is None or work.numel() < need:
             work = torch.empty(need, dtype=torch.float32, device=h.device)
             _head_ws[h.device] = work
-    _check(_lib().rag_head_bwd(_ptr(h), _ptr(w), _ptr(dz), _ptr(dh), _ptr(dw), _ptr(db0),
-                               _ptr(dpbias), _ptr(work), B, S, KP, K, int(relu_mask), _stream()),
+    ml = mh = acc = None
+    if metrics is not None:
+        ml, mh, acc = metrics
+        if acc.dtype != torch.float32 or acc.numel() < 2 or ml.numel() < B or mh.numel() < B:
+            raise ValueError("head_bwd metrics: loss [B], hit [B], fp32 acc [2]")
+    if dzsum is not None and dzsum.numel() < B:
+        raise ValueError("head_bwd dzsum: [B] per-board sums expected")
+    # db0 in a fixed summation order (from dzsum, or from dz itself when the forward gave none)
+    _check(_lib().rag_head_bwd_m(_ptr(h), _ptr(w), _ptr(dz), _ptr(dh), _ptr(dw), _ptr(db0),
+                                 _ptr(dpbias), _ptr(work), B, S, KP, K, int(relu_mask),
+                                 _ptr(ml), _ptr(mh), _ptr(acc), _ptr(dzsum), _stream()),
            "head_bwd")
 
 
