@@ -15,9 +15,10 @@ using namespace rag;
 namespace {
 
 constexpr int kHeadThreads = 256;
-// policy_head_fwd: 384 threads, so a 19x19 board's 361 pixel dot products take one pass (with
-// 256 threads 105 of them took two serial 384-byte row walks: the kernel is latency-bound)
-constexpr int kHeadFwdThreads = 384;
+// policy_head_fwd: 1024 threads, 8 per pixel: a 19x19 board's 361 dot products take three
+// coalesced passes (one lane per pixel and 384 threads: 18.3 us for B = 256, now 13.5 us; the
+// kernel is latency-bound, one block per board)
+constexpr int kHeadFwdThreads = 1024;
 
 __device__ __forceinline__ float block_reduce(float v, float* sh, bool is_max) {
   v = is_max ? warp_max(v) : warp_sum(v);
