@@ -165,8 +165,11 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[NT][MT], int mw, int
 // 192 channels (384 contiguous bytes in the channels-last activation) with 16-byte lane chunks,
 // applying the dgrad ReLU mask from equally coalesced reads. The register epilogue above writes
 // 16 pixels x 32 bytes per store instruction; this one writes whole rows.
+#ifndef RAG_EP_PREFETCH
+#define RAG_EP_PREFETCH 512  // the ping-pong epilogue's mask prefetch (0: the per-chunk loads)
+#endif
 constexpr int kEpRow = kBN + 8;  // bf16 per LDS image row (192 channels; NT = 4: 136)
-template <int BM, int NT = kNT, int MT = kMT>
+template <int BM, int NT = kNT, int MT = kMT, int NTHR = 0>
 __device__ __forceinline__ void epilogue_lds(const f32x4 (&acc)[NT][MT], bf16* __restrict__ img,
                                              int mwl, int nwl, int m0, int n0, int M, int S,
                                              int WO, int HO, int YC, int HM,
@@ -192,14 +195,41 @@ __device__ __forceinline__ void epilogue_lds(const f32x4 (&acc)[NT][MT], bf16* _
       *reinterpret_cast<bf16x4*>(img + (mwl + i * 16 + frow) * EpRow + n) = o;
     }
   }
-  __syncthreads();
   const int S2 = S * S, WMK = S + 2 * HM;
   constexpr int kChunks = 32 * NT / 8;  // 16-byte chunks per pixel row
+  // NTHR (the block size, when the caller fixes it): every mask chunk of this thread is loaded
+  // here, before the barrier, all in flight at once, instead of one dependent load per row
+  // chunk inside the store loop (dgrad: the mask read was that loop's latency chain)
+  constexpr int kIt = NTHR > 0 ? (BM * kChunks + NTHR - 1) / NTHR : 1;
+  bf16x8 mkp[kIt];
+  if constexpr (NTHR > 0) {
+    if (mask) {
+#pragma unroll
+      for (int it = 0; it < kIt; ++it) {
+        const int c = threadIdx.x + it * NTHR;
+        const int row = c / kChunks, k8 = (c - row * kChunks) * 8;
+        const int m = m0 + row;
+        if (c < BM * kChunks && m < M) {
+          const int b = m / S2;
+          const int rem = m - b * S2;
+          const int pi = rem / S, pj = rem - pi * S;
+          mkp[it] = *reinterpret_cast<const bf16x8*>(
+              mask + (size_t)((b * WMK + pi + HM) * WMK + pj + HM) * YC + n0 + k8);
+        }
+      }
+    }
+  }
+  __syncthreads();
   // with statistics (128-channel tiles only): kChunks consecutive threads own one pixel row
   // (kChunks | 64, and BM * kChunks a multiple of the block size, so every thread runs the same
   // iterations)
   if constexpr (64 % kChunks == 0) if (sred) {
-    for (int c = threadIdx.x; c < BM * kChunks; c += blockDim.x) {
+    const int step = NTHR > 0 ? NTHR : (int)blockDim.x;
+    const int nit = NTHR > 0 ? kIt : (BM * kChunks - (int)threadIdx.x + step - 1) / step;
+#pragma unroll
+    for (int it = 0; it < nit; ++it) {
+      const int c = threadIdx.x + it * step;
+      if (NTHR > 0 && c >= BM * kChunks) break;
       const int row = c / kChunks, k8 = (c - row * kChunks) * 8;
       const int m = m0 + row;
       float s0 = 0.f, s1 = 0.f;
@@ -211,8 +241,12 @@ __device__ __forceinline__ void epilogue_lds(const f32x4 (&acc)[NT][MT], bf16* _
         pj = rem - pi * S;
         bf16x8 v = *reinterpret_cast<const bf16x8*>(img + row * EpRow + k8);
         if (mask) {
-          const bf16x8 mk = *reinterpret_cast<const bf16x8*>(
-              mask + (size_t)((b * WMK + pi + HM) * WMK + pj + HM) * YC + n0 + k8);
+          bf16x8 mk;
+          if constexpr (NTHR > 0)
+            mk = mkp[it];
+          else
+            mk = *reinterpret_cast<const bf16x8*>(
+                mask + (size_t)((b * WMK + pi + HM) * WMK + pj + HM) * YC + n0 + k8);
           const float cx = mcoef ? mcoef[pj] : 0.f, cc = mcoef ? mcoef[2 * S + pj] : 0.f;
           const float mu = smean ? smean[pj] : 0.f;
 #pragma unroll
@@ -247,7 +281,12 @@ __device__ __forceinline__ void epilogue_lds(const f32x4 (&acc)[NT][MT], bf16* _
     }
     return;
   }  // if (sred)
-  for (int c = threadIdx.x; c < BM * kChunks; c += blockDim.x) {
+  const int step = NTHR > 0 ? NTHR : (int)blockDim.x;
+  const int nit = NTHR > 0 ? kIt : (BM * kChunks - (int)threadIdx.x + step - 1) / step;
+#pragma unroll
+  for (int it = 0; it < nit; ++it) {
+    const int c = threadIdx.x + it * step;
+    if (NTHR > 0 && c >= BM * kChunks) break;
     const int row = c / kChunks, k8 = (c - row * kChunks) * 8;
     const int m = m0 + row;
     if (m >= M) continue;
@@ -256,8 +295,12 @@ __device__ __forceinline__ void epilogue_lds(const f32x4 (&acc)[NT][MT], bf16* _
     const int pi = rem / S, pj = rem - pi * S;
     bf16x8 v = *reinterpret_cast<const bf16x8*>(img + row * EpRow + k8);
     if (mask) {
-      const bf16x8 mk = *reinterpret_cast<const bf16x8*>(
-          mask + (size_t)((b * WMK + pi + HM) * WMK + pj + HM) * YC + n0 + k8);
+      bf16x8 mk;
+      if constexpr (NTHR > 0)
+        mk = mkp[it];
+      else
+        mk = *reinterpret_cast<const bf16x8*>(
+            mask + (size_t)((b * WMK + pi + HM) * WMK + pj + HM) * YC + n0 + k8);
       if (mcoef) {
         // the layer input U = ReLU(cx[col] * x + cc[col]) was never stored (BN prologue): the
         // mask is recomputed from the BN input x and the column coefficients
@@ -1458,8 +1501,10 @@ conv_tap_pp_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
              relu, mask, Y, frow, fq, sred);
   } else {
     __syncthreads();  // every wave is past its last LDS read: the ring becomes the output image
-    epilogue_lds<BM, NT>(acc, lds, wm * (16 * MT), wn * (16 * NT), m0, n0, M, S, WO, HO, YC, HM,
-                        bias, relu, mask, Y, frow, fq, mcoef, sred, smean);
+    // (the 128-wide kernels keep the per-chunk loads: CNNPolicy-128 162.0 vs 165.9k with them)
+    epilogue_lds<BM, NT, MT, NT == kNT ? RAG_EP_PREFETCH : 0>(acc, lds, wm * (16 * MT), wn * (16 * NT), m0, n0,
+                                              M, S, WO, HO, YC, HM, bias, relu, mask, Y, frow,
+                                              fq, mcoef, sred, smean);
   }
   if (spart) {  // the block's column partials
     __syncthreads();
