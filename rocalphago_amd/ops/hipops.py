@@ -495,8 +495,9 @@ def value_batch(index, values, sym, seed, step, tf_out=None, y_out=None):
     if y_out is None:
         y_out = torch.empty((B, 1), dtype=torch.float32, device=dev)
     _check(_lib().rag_value_batch(_ptr(index), _ptr(values), _ptr(sym), sym.numel(),
-                                  ctypes.c_uint(seed & 0xFFFFFFFF), ctypes.c_uint(step & 0xFFFFFFFF),
-                                  _ptr(tf_out), _ptr(y_out), B, _stream()), "value_batch")
+                                  ctypes.c_uint(seed & 0xFFFFFFFF),
+                                  ctypes.c_uint(step & 0xFFFFFFFF), _ptr(tf_out), _ptr(y_out),
+                                  B, _stream()), "value_batch")
     return tf_out, y_out
 
 
