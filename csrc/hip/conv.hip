@@ -1075,12 +1075,16 @@ __global__ void __launch_bounds__(256) pack_trunk_kernel(const int64_t* __restri
   float* bo = (float*)t[9];
   const int taps = KS * KS;
   const int ntn = (COUTP + 63) / 64, ntc = (CINP + 63) / 64;
-  int tile = blockIdx.x;
-  if (tile >= taps * ntn * ntc) return;
-  const int ct = tile % ntc;
-  tile /= ntc;
-  const int nt = tile % ntn;
-  const int tap = tile / ntn;
+  // XCD-grouped order (the grid width is a multiple of 8, so block x runs on XCD x % 8): the
+  // taps of one 64 x 64 (n, c) tile are blocks x, x + 8, x + 16, ... of one XCD. A tap's OIHW
+  // reads stride 9 (25) floats, so each block pulls the cache lines of all its tile's taps; with
+  // the taps on one XCD they come from its L2 instead of once per XCD.
+  const int x = blockIdx.x, xcd = x & 7, j = x >> 3;
+  const int g = (j / taps) * 8 + xcd;  // (n, c) tile
+  const int tap = j % taps;
+  if (g >= ntn * ntc) return;
+  const int ct = g % ntc;
+  const int nt = g / ntc;
   __shared__ float tl[64][65];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
 #pragma unroll 4
@@ -1100,14 +1104,14 @@ __global__ void __launch_bounds__(256) pack_trunk_kernel(const int64_t* __restri
       if (c < CINP && n < COUTP) Wb[((taps - 1 - tap) * CINP + c) * COUTP + n] = (bf16)tl[tx][cl];
     }
   }
-  if (bo && blockIdx.x == 0)
+  if (bo && g == 0 && tap == 0)
     for (int n = threadIdx.x; n < COUTP; n += blockDim.x) bo[n] = (b && n < COUT) ? b[n] : 0.f;
 }
 }  // namespace
 
 RAG_API int rag_pack_trunk(const int64_t* table, int nlayers, int64_t total, hipStream_t stream) {
-  // total: 64x64 tiles (x taps) of the largest layer = grid width
-  if (nlayers <= 0 || total <= 0) return 0;
+  // total: the grid width, max over layers of 8 * taps * ceil(64x64 tiles / 8) (XCD-grouped order)
+  if (nlayers <= 0 || total <= 0 || total % 8) return -1;
   const dim3 grid((unsigned)total, (unsigned)nlayers);
   pack_trunk_kernel<<<grid, 256, 0, stream>>>(table);
   return (int)hipGetLastError();

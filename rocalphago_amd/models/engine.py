@@ -68,8 +68,10 @@ class _PackedConvs(object):
                              self._wb[l].data_ptr(), self._bias[l].data_ptr(), start])
                 start += s.ks * s.ks * s.coutp * s.cinp + s.coutp
             self._pack_table = torch.tensor(rows, dtype=torch.int64).to(self.device)
-            # grid width: 64x64 tiles of the largest layer
-            self._pack_total = max(s.ks * s.ks * (-(-s.coutp // 64)) * (-(-s.cinp // 64))
+            # grid width (conv.hip pack_trunk_kernel's XCD-grouped order): 8 x taps x
+            # ceil(64x64 tiles / 8) of the widest layer
+            self._pack_total = max(8 * s.ks * s.ks * -(-((-(-s.coutp // 64)) *
+                                                          (-(-s.cinp // 64))) // 8)
                                    for s in self.specs)
             self._pack_key = key
             self._pack_keep = ws  # keep contiguous copies alive while the table points at them
