@@ -33,6 +33,14 @@ class ConvSpec(object):
         self.halo_in = max(1, ks // 2)
 
 
+def pack_grid_width(specs):
+    """Grid width of conv.hip's pack_trunk_kernel (XCD-grouped order: block x runs tap
+    (x / 8) % taps of 64x64 tile ((x / 8) / taps) * 8 + x % 8): 8 x taps x ceil(tiles / 8) of
+    the widest layer, a multiple of 8."""
+    return max(8 * s.ks * s.ks * -(-((-(-s.coutp // 64)) * (-(-s.cinp // 64))) // 8)
+               for s in specs)
+
+
 class _PackedConvs(object):
     """bf16 GEMM layouts (+ padded fp32 biases) of a list of convolutions, repacked from the fp32
     OIHW masters in one launch whenever the model's weight version changes."""
@@ -68,11 +76,7 @@ class _PackedConvs(object):
                              self._wb[l].data_ptr(), self._bias[l].data_ptr(), start])
                 start += s.ks * s.ks * s.coutp * s.cinp + s.coutp
             self._pack_table = torch.tensor(rows, dtype=torch.int64).to(self.device)
-            # grid width (conv.hip pack_trunk_kernel's XCD-grouped order): 8 x taps x
-            # ceil(64x64 tiles / 8) of the widest layer
-            self._pack_total = max(8 * s.ks * s.ks * -(-((-(-s.coutp // 64)) *
-                                                          (-(-s.cinp // 64))) // 8)
-                                   for s in self.specs)
+            self._pack_total = pack_grid_width(self.specs)
             self._pack_key = key
             self._pack_keep = ws  # keep contiguous copies alive while the table points at them
         ops.pack_trunk(self._pack_table, len(self.specs), self._pack_total)
