@@ -650,6 +650,26 @@ struct PendingRed {
 
 RAG_API size_t rag_wgrad_pending_bytes() { return sizeof(PendingRed); }
 
+// The handle's claim counters, allocated (and zeroed) when the handle is created rather than on
+// its first deferral (hipMalloc synchronises the device in the middle of a step), and freed
+// with it (ops.PendingReduction.__del__).
+RAG_API int rag_wgrad_pending_init(void* h) {
+  PendingRed* p = static_cast<PendingRed*>(h);
+  if (!p) return -1;
+  if (!p->dticket) {
+    if (hipMalloc(&p->dticket, 2 * sizeof(unsigned)) != hipSuccess) return -3;
+    if (hipMemset(p->dticket, 0, 2 * sizeof(unsigned)) != hipSuccess) return -3;
+  }
+  return 0;
+}
+RAG_API int rag_wgrad_pending_free(void* h) {
+  PendingRed* p = static_cast<PendingRed*>(h);
+  if (!p || !p->dticket) return 0;
+  const hipError_t e = hipFree(p->dticket);
+  p->dticket = nullptr;
+  return e == hipSuccess ? 0 : -3;
+}
+
 // Take the handle's reduction if there is one: returns false if it was empty.
 static bool take_pending(void* h, WgradRed* r, hipStream_t* st) {
   PendingRed* p = static_cast<PendingRed*>(h);
@@ -728,6 +748,31 @@ RAG_API int rag_conv_igemm_bn(const void* X, const void* W, const float* bias, v
   if ((!bnc && !mcoef && !spart) || (mcoef && resid) || (smean && !mcoef)) return -5;
   return conv_igemm_impl(X, W, bias, Y, mask, resid, B, S, HI, HO, CIN, COUTP, YC, 3, relu, HM,
                          stream, pending, bnc, mcoef, spart, smean);
+}
+
+// Winograd F(2,3) 3x3 convolution (conv_wino.hip): forward or dgrad with the layer's Winograd
+// weights [12][NOUT][KIN] (rag_wino_pack). A deferred wgrad reduction in `pending` rides along
+// the launch (every block claims units of it after its epilogue) when it has claim counters and
+// the grid is one-dimensional; otherwise it goes out on its own first.
+int rag_conv_wino_launch(const void* X, const void* W, const float* bias, void* Y,
+                         const void* mask, int B, int S, int KIN, int NOUT, int HO, int YC,
+                         int relu, int HM, hipStream_t stream, const WgradRed* red);
+RAG_API int rag_conv_wino_p(const void* X, const void* W, const float* bias, void* Y,
+                            const void* mask, int B, int S, int KIN, int NOUT, int HO, int YC,
+                            int relu, int HM, hipStream_t stream, void* pending) {
+  WgradRed pend;
+  hipStream_t pend_stream = nullptr;
+  const WgradRed* red = nullptr;
+  if (take_pending(pending, &pend, &pend_stream)) {
+    if (pend_stream == stream && pend.ticket && NOUT == 192) {
+      red = &pend;
+    } else {
+      const int rc = rag_launch_wgrad_slab_reduce(pend, pend_stream);
+      if (rc) return rc;
+    }
+  }
+  return rag_conv_wino_launch(X, W, bias, Y, mask, B, S, KIN, NOUT, HO, YC, relu, HM, stream,
+                              red);
 }
 
 // Partial rows rag_conv_igemm_bn writes to `spart` (one per convolution block).

@@ -134,6 +134,8 @@ policy_head_fwd_kernel(const bf16* __restrict__ H, const float* __restrict__ w, 
     const float lb = -__logf(pl) * sw * cls;
     if (loss) loss[b] = lb;
     if (acc) atomicAdd(&acc[0], lb);  // running metric sums (training loops read them lazily)
+  } else if (mode && threadIdx.x == 0 && loss) {
+    loss[b] = 0.f;  // unlabelled board: the backward's metric reduce sums loss[:B] as is
   }
   // top-1 hit (ties -> lowest index, like argmax)
   if (mode && hit) {

@@ -507,7 +507,13 @@ class PolicyHeadEngine(object):
     def forward(self, B, w, b0, pbias, labels=None, sweight=None, mode=0, gscale=1.0,
                 pass_params=None, acc=None):
         """pass_params: (W [S*S], b [1]) of a PassLogit layer, or None. acc: fp32 [2] running
-        (loss sum, hit count), added to in the kernel."""
+        (loss sum, hit count). In a training forward (mode > 0) the sums are added by the
+        matching backward() (its reduce launch sums the per-board loss / hit arrays), so every
+        training forward that passes ``acc`` must be followed by backward() before the next
+        one; a second such forward raises instead of silently dropping the first's metrics."""
+        if mode and acc is not None and getattr(self, "_macc", None) is not None:
+            raise RuntimeError("PolicyHeadEngine: training forward with acc= while the previous "
+                               "one's metrics are still pending (backward() not called)")
         self.ensure(B)
         h = self.trunk.output(B)
         pk = {}

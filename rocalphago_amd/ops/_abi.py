@@ -20,8 +20,17 @@ SIGNATURES = {
     "rag_conv_wgrad_deferred_bn": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, P, P, P],
     "rag_wgrad_flush": [P, P],
     "rag_wgrad_pending_bytes": [],
+    "rag_wgrad_pending_init": [P],
+    "rag_wgrad_pending_free": [P],
     "rag_pack_weights": [P, P, P, I, I, I, I, I, P],
     "rag_pack_trunk": [P, I, I64, P],
+    # conv_wino.hip (+ the pending-handle entry in conv.hip)
+    "rag_conv_wino_ok": [I, I, I, I, I],
+    "rag_conv_wino": [P, P, P, P, P, I, I, I, I, I, I, I, I, P],
+    "rag_conv_wino_p": [P, P, P, P, P, I, I, I, I, I, I, I, I, P, P],
+    "rag_wino_pack": [P, I, I, P],
+    "rag_conv_wino_diag": [I, P, P, P, P, P, I, I, I, I, I, I, I, I, P],
+    "rag_conv_wino_stamps": [P, I],
     "rag_pack_input_u8": [P, P, P, P, I, I, I, I, I, I, P],
     "rag_pack_input_f32": [P, P, P, P, I, I, I, I, I, I, P],
     "rag_pack_input_bits": [P, P, P, P, I, I, I, I, I, P],

@@ -76,6 +76,16 @@ class PendingReduction(object):
 
     def __init__(self):
         self.buf = ctypes.create_string_buffer(int(_lib().rag_wgrad_pending_bytes()))
+        # claim counters allocated now (a hipMalloc on first deferral synchronised the device
+        # mid-step) and freed with the handle
+        _check(_lib().rag_wgrad_pending_init(self.ptr), "wgrad_pending_init")
+        self._free = _lib().rag_wgrad_pending_free
+
+    def __del__(self):
+        try:
+            self._free(self.ptr)
+        except Exception:  # interpreter shutdown: the library may be gone already
+            pass
 
     @property
     def ptr(self):
@@ -127,6 +137,52 @@ def conv_igemm(x, wpack, bias, y, B, S, hi, ho, cinp, coutp, ks, relu, mask=None
     _check(_lib().rag_conv_igemm(_ptr(x), _ptr(wpack), _ptr(bias), _ptr(y), _ptr(mask),
                                  _ptr(residual), B, S, hi, ho, cinp, coutp, y.shape[-1], ks,
                                  int(relu), hm, _stream(), _hptr(pending)), "conv_igemm")
+    return y
+
+
+def conv_wino_ok(S, hi, kin, nout, ks):
+    """True if conv_wino (Winograd F(2,3) along the width, csrc/hip/conv_wino.hip) runs this
+    layer: 3x3, input halo 1, input channels a multiple of 32, output channels of 192."""
+    return bool(_lib().rag_conv_wino_ok(S, hi, kin, nout, ks))
+
+
+def wino_pack(table, nlayers, max_tiles):
+    """Winograd weights of 3x3 layers from their fp32 OIHW masters in one launch. ``table``:
+    device int64 [nlayers, 8] = (W, cout, cin, coutp, cinp, Uf, Ub or 0, 0); Uf [12, coutp,
+    cinp] (forward), Ub [12, cinp, coutp] (dgrad); ``max_tiles``: 64x64 (n, c) tiles of the
+    widest layer."""
+    _check(_lib().rag_wino_pack(_ptr(table), nlayers, int(max_tiles), _stream()), "wino_pack")
+
+
+def wino_weights(w, coutp, cinp, dgrad=True):
+    """(Uf, Ub) Winograd weights of one OIHW fp32 3x3 weight tensor (tests, one-off layers)."""
+    cout, cin = w.shape[:2]
+    w = w.contiguous()
+    uf = torch.empty((12, coutp, cinp), dtype=torch.bfloat16, device=w.device)
+    ub = torch.empty((12, cinp, coutp), dtype=torch.bfloat16, device=w.device) if dgrad else None
+    table = torch.tensor([[w.data_ptr(), cout, cin, coutp, cinp, uf.data_ptr(),
+                           0 if ub is None else ub.data_ptr(), 0]], dtype=torch.int64)
+    table = table.to(w.device)
+    wino_pack(table, 1, -(-coutp // 64) * -(-cinp // 64))
+    torch.cuda.current_stream(w.device).synchronize()  # the table is a temporary
+    return uf, ub
+
+
+def conv_wino(x, u, bias, y, B, S, kin, nout, ho, relu, mask=None, mask_halo=None,
+              pending=None):
+    """y[pad ho] = act(conv3x3(x[pad 1]) + bias) through the Winograd kernel with the layer's
+    Winograd weights ``u`` [12, nout, kin] (wino_pack), or the dgrad form with a ReLU mask (the
+    layer input, y's channel count, halo ``mask_halo``). ``pending``: a PendingReduction whose
+    deferred wgrad reduction rides along the launch."""
+    _index_range_ok(x, y, mask)
+    hm = ho if mask_halo is None else mask_halo
+    if x.shape[1] != S + 2 or x.shape[-1] != kin:
+        raise ValueError("conv_wino input must have halo 1 and %d channels" % kin)
+    if mask is not None and (mask.shape[1] != S + 2 * hm or mask.shape[-1] != y.shape[-1]):
+        raise ValueError("mask layout does not match (halo %d, %d channels)" % (hm, y.shape[-1]))
+    _check(_lib().rag_conv_wino_p(_ptr(x), _ptr(u), _ptr(bias), _ptr(y), _ptr(mask), B, S, kin,
+                                  nout, ho, y.shape[-1], int(relu), hm, _stream(),
+                                  _hptr(pending)), "conv_wino")
     return y
 
 

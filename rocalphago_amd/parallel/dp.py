@@ -50,11 +50,21 @@ def _single_rank_env():
 
 
 class DPContext(object):
-    def __init__(self, device=None, backend=None, timeout_s=600):
+    """One rank of a data-parallel job (one process per GPU, torch.distributed; "nccl" is RCCL
+    on ROCm). Enabled when WORLD_SIZE > 1, when RAG_FORCE_PG forces a one-rank group, or, with
+    ``adopt=True``, when the process already joined a group (an embedded gloo group, tests):
+    a group that merely exists is not adopted by default, and an adopted group
+    supplies rank, world AND the local rank (device) together."""
+
+    def __init__(self, device=None, backend=None, timeout_s=600, adopt=False):
         world, rank, local = env_world()
         self.world, self.rank, self.local_rank = world, rank, local
-        self.enabled = world > 1 or force_pg() or (dist.is_available() and dist.is_initialized())
-        if self.enabled and world == 1 and not dist.is_initialized():
+        existing = dist.is_available() and dist.is_initialized()
+        self.enabled = world > 1 or force_pg() or (adopt and existing)
+        if self.enabled and existing and world == 1:
+            # adopted group: the environment says nothing about it
+            self.local_rank = local = dist.get_rank() % max(1, torch.cuda.device_count())
+        if self.enabled and world == 1 and not existing:
             _single_rank_env()
         if device is None:
             device = torch.device("cuda", local % max(1, torch.cuda.device_count())) \

@@ -224,6 +224,7 @@ class ValueTrainer(object):
                                               timer=metrics.comm if metrics else None)
         self.loss_sum = torch.zeros((), device=self.dev)
         self.count = 0
+        self.steps = 0  # steps taken by this trainer (never reset)
 
     def step(self, index):
         n = index.numel()
@@ -232,7 +233,7 @@ class ValueTrainer(object):
             # one launch for the transforms and the targets (batch.hip), as the SL step does
             from ..ops import hipops as ops
             tf, y = ops.value_batch(index.long().contiguous(), self.values.reshape(-1),
-                                    self.sym, self.seed, self.count)
+                                    self.sym, self.seed, self.draw_counter())
             B = self.plan.prepare(self.states, index=index, transforms=tf)
             hook = self.bucketer.layer_done if self.bucketer else None
             loss = self.plan.fwd_bwd(B, y, None, on_layer_grads=hook)
@@ -252,8 +253,18 @@ class ValueTrainer(object):
             model.grad_allreduce = saved
             self.loss_sum += float(loss) * n
         self.count += n
+        self.steps += 1
         if self.metrics is not None:
             self.metrics.step_done()
+
+    def draw_counter(self):
+        """Counter of the hashed per-sample transform draw (batch.hip value_batch): the
+        optimizer's global iteration, which the checkpoint saves, so a resumed run draws the same
+        transforms and no two steps share a draw. (``self.count`` was a per-window sample count
+        that ``pop_loss`` resets: every logging window repeated the previous window's draws.)
+        Models without an iteration counter fall back to this trainer's own step count."""
+        it = getattr(self.model.optimizer, "iterations", None)
+        return int(it) if it is not None else self.steps
 
     def _host_states(self, index, tf=None):
         from .data import apply_transform_np

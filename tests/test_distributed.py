@@ -451,3 +451,31 @@ def test_dp_rl_update_symmetry_and_union(tmp_path):
     assert np.abs(single).max() > 0
     assert np.linalg.norm(dw0 - single) <= 1e-5 * np.linalg.norm(single)
     np.testing.assert_allclose(dl0, -dw0, rtol=1e-3, atol=1e-7 * np.abs(dw0).max())
+
+
+def _adopt_worker(rank, world, port, outdir):
+    import torch.distributed as dist
+    _setup(rank, world, port)
+    dist.init_process_group("gloo")
+    from rocalphago_amd.parallel.dp import DPContext
+    # a group exists but the environment claims a single process: not adopted by default
+    os.environ["WORLD_SIZE"] = "1"
+    os.environ.pop("RAG_FORCE_PG", None)
+    plain = DPContext(device="cpu")
+    adopted = DPContext(device="cpu", adopt=True)
+    res = [int(plain.enabled), plain.world, int(adopted.enabled), adopted.world, adopted.rank,
+           adopted.local_rank]
+    with open(os.path.join(outdir, "r%d.txt" % rank), "w") as f:
+        f.write(" ".join(map(str, res)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dpcontext_adopts_an_existing_group_only_on_request(tmp_path):
+    """DPContext used to switch itself on whenever any process group existed, taking
+    rank/world from the group but the device from the environment."""
+    mp.spawn(_adopt_worker, args=(2, _port(), str(tmp_path)), nprocs=2, join=True)
+    ndev = max(1, torch.cuda.device_count())
+    for r in range(2):
+        got = open(os.path.join(str(tmp_path), "r%d.txt" % r)).read().split()
+        assert got == ["0", "1", "1", "2", str(r), str(r % ndev)], got

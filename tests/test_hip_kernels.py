@@ -512,18 +512,22 @@ def test_width128_pingpong_conv_and_wgrad_slab(ops):
     yr = ops.alloc_padded(B, S, 1, C, dev)
     ops.conv_igemm(xp, wf, None, yr, B, S, 1, 1, C, C, 3, relu=False, residual=rp)
     assert rel_err(ops.unpack(yr, C, 1), F.conv2d(bf(x), bf(w), padding=1) + bf(r)) < 2e-2
-    # wgrad (deferred) + dgrad with the ReLU mask of the layer input
+    # wgrad (deferred) + dgrad with the ReLU mask of the layer input, twice on one handle: the
+    # claimed reduction's counters must be back at zero for the second launch (a
+    # missed reset would skip the whole second reduction and leave dw / db at their NaN fill)
     xr, wr = bf(x).requires_grad_(), bf(w).requires_grad_()
     (F.conv2d(xr, wr, padding=1) * bf(g)).sum().backward()
     h = ops.PendingReduction()
-    dw, db = torch.zeros(C, C, 3, 3, device=dev), torch.zeros(C, device=dev)
-    ops.conv_wgrad(gp, xp, dw, db, B, S, 1, C, C, C, C, 3, hg=1, defer=True, pending=h)
-    dx = ops.alloc_padded(B, S, 1, C, dev)
-    ops.conv_igemm(gp, wb, None, dx, B, S, 1, 1, C, C, 3, relu=False, mask=xp, pending=h)
-    torch.cuda.synchronize()
-    assert rel_err(ops.unpack(dx, C, 1), xr.grad * (x > 0)) < 2e-2
-    assert rel_err(dw, wr.grad) < 1e-2
-    assert rel_err(db, bf(g).sum((0, 2, 3))) < 1e-2
+    for rnd in range(2):
+        dw = torch.full((C, C, 3, 3), float("nan"), device=dev)
+        db = torch.full((C,), float("nan"), device=dev)
+        ops.conv_wgrad(gp, xp, dw, db, B, S, 1, C, C, C, C, 3, hg=1, defer=True, pending=h)
+        dx = ops.alloc_padded(B, S, 1, C, dev)
+        ops.conv_igemm(gp, wb, None, dx, B, S, 1, 1, C, C, 3, relu=False, mask=xp, pending=h)
+        torch.cuda.synchronize()
+        assert rel_err(ops.unpack(dx, C, 1), xr.grad * (x > 0)) < 2e-2
+        assert rel_err(dw, wr.grad) < 1e-2, "round %d" % rnd
+        assert rel_err(db, bf(g).sum((0, 2, 3))) < 1e-2, "round %d" % rnd
 
 
 @pytest.mark.gpu

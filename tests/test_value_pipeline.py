@@ -111,3 +111,28 @@ def test_generate_cli_two_ranks(tmp_path):
         X = f["states"][()]
     # rank 0 holds rows 0-2, rank 1 rows 3-5: per-rank player streams give different games
     assert not np.array_equal(X[:3], X[3:])
+
+
+def test_value_trainer_draw_counter_survives_logging_windows():
+    """The hashed transform draw of the device value step is keyed by the optimizer's global
+    iteration: consecutive steps, also across a pop_loss() logging window, get
+    distinct keys, and a trainer rebuilt on a resumed model continues the sequence."""
+    import torch
+
+    from rocalphago_amd.models import kerasish as K
+    val = CNNValue(VALUE_FEATURES, board=7, filters_per_layer=8, layers=2, device="cpu", seed=2)
+    val.model.compile(loss="mean_squared_error", optimizer=K.SGD(lr=0.001))
+    n = 16
+    states = np.random.RandomState(0).randint(0, 2, (n, 49, 7, 7)).astype(np.uint8)
+    values = np.random.RandomState(1).choice([-1.0, 1.0], n).astype(np.float32)
+    tr = vt.ValueTrainer(val.model, states, values, 4, ["noop", "rot90"], seed=5)
+    keys = []
+    for window in range(3):
+        for _ in range(2):
+            keys.append(tr.draw_counter())
+            tr.step(torch.arange(4) + 4 * (len(keys) % 4))
+        tr.pop_loss()
+    assert len(set(keys)) == len(keys) == 6
+    # a new trainer on the same (resumed) model continues from the saved iteration
+    tr2 = vt.ValueTrainer(val.model, states, values, 4, ["noop", "rot90"], seed=5)
+    assert tr2.draw_counter() == keys[-1] + 1

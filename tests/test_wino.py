@@ -1,0 +1,132 @@
+"""Winograd F(2,3) 3x3 convolution (csrc/hip/conv_wino.hip) against fp32 PyTorch (GPU only).
+
+The kernel computes the reference's 3x3 Convolution2D (policy.py:96-136) as four width-wise
+Winograd GEMMs: the inputs are bf16, the transformed inputs V = d_a +- d_b are rounded to bf16
+once, the weights U = G g once, and everything accumulates in fp32. That adds one rounding per
+operand to the direct kernel's arithmetic: ~0.3 % relative (norm) error against an fp32
+convolution of the same bf16 inputs, against ~0.2 % for the bf16 output rounding alone."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+def rel_max(a, b):
+    return ((a - b).abs().max() / (b.abs().max() + 1e-6)).item()
+
+
+def rel_norm(a, b):
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+@pytest.fixture(scope="module")
+def ops():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from rocalphago_amd.ops import hipops
+    return hipops
+
+
+@pytest.mark.parametrize("B,S,ho", [(1, 19, 1), (3, 19, 2), (256, 19, 1), (3, 13, 1),
+                                    (5, 9, 1), (7, 7, 2)])
+def test_wino_forward_matches_fp32(ops, B, S, ho):
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    C = 192
+    assert ops.conv_wino_ok(S, 1, C, C, 3)
+    x = F.relu(torch.randn(B, C, S, S, device=dev))
+    w = torch.randn(C, C, 3, 3, device=dev) * 0.05
+    b = torch.randn(C, device=dev) * 0.1
+    ref = F.relu(F.conv2d(bf(x), bf(w), b, padding=1))
+    xp = ops.pack_nchw(x, 1, C)
+    uf, _ = ops.wino_weights(w, C, C, dgrad=False)
+    # one extra board past B: the kernel must not touch it
+    y = ops.alloc_padded(B + 1, S, ho, C, dev)
+    ops.conv_wino(xp, uf, b.contiguous(), y[:B], B, S, C, C, ho, True)
+    out = ops.unpack(y[:B], C, ho)
+    assert rel_norm(out, ref) < 6e-3
+    assert rel_max(out, ref) < 2e-2
+    # the output halo and the board past B stay zero
+    assert y[B].abs().max().item() == 0
+    assert y[:, :ho].abs().max().item() == 0 and y[:, :, -ho:].abs().max().item() == 0
+    # and it agrees with the direct implicit-GEMM kernel on the same inputs
+    wf, _ = ops.pack_weights(w, C, C)
+    yd = ops.alloc_padded(B, S, ho, C, dev)
+    ops.conv_igemm(xp, wf, b.contiguous(), yd, B, S, 1, ho, C, C, 3, relu=True)
+    assert rel_norm(out, ops.unpack(yd, C, ho)) < 6e-3
+
+
+@pytest.mark.parametrize("B,S,ho", [(3, 19, 1), (2, 19, 2), (4, 13, 1)])
+def test_wino_dgrad_with_mask_matches_autograd(ops, B, S, ho):
+    """dgrad form: the Winograd weights of the flipped, transposed kernel (Ub) and the ReLU
+    mask of the layer input in the epilogue, output halo 1 or 2 (the SL trunk's layer-1 dgrad
+    writes the 5x5 input layer's halo-2 gradient)."""
+    dev = torch.device("cuda")
+    torch.manual_seed(1)
+    C = 192
+    x = F.relu(torch.randn(B, C, S, S, device=dev))
+    w = torch.randn(C, C, 3, 3, device=dev) * 0.05
+    g = torch.randn(B, C, S, S, device=dev)
+    xr = bf(x).requires_grad_()
+    (F.conv2d(xr, bf(w), padding=1) * bf(g)).sum().backward()
+    ref = xr.grad * (x > 0)
+    gp = ops.pack_nchw(g, 1, C)
+    xm = ops.pack_nchw(x, ho, C)
+    _, ub = ops.wino_weights(w, C, C)
+    dx = ops.alloc_padded(B, S, ho, C, dev)
+    ops.conv_wino(gp, ub, None, dx, B, S, C, C, ho, False, mask=xm, mask_halo=ho)
+    out = ops.unpack(dx, C, ho)
+    assert rel_norm(out, ref) < 6e-3
+    assert rel_max(out, ref) < 2e-2
+
+
+def test_wino_pack_layouts(ops):
+    """Uf[ky*4+q] = G[q] . w[:, :, ky, :] and Ub the same of w[:, :, 2-ky, ::-1] transposed,
+    with zero padding past (cout, cin)."""
+    dev = torch.device("cuda")
+    torch.manual_seed(2)
+    cout, cin, coutp, cinp = 150, 100, 192, 128
+    w = torch.randn(cout, cin, 3, 3, device=dev)
+    uf, ub = ops.wino_weights(w, coutp, cinp)
+    G = torch.tensor([[1, 0, 0], [.5, .5, .5], [.5, -.5, .5], [0, 0, 1]], device=dev)
+    ref = torch.einsum("qk,ncyk->yqnc", G, w).reshape(12, cout, cin)
+    assert torch.equal(uf[:, :cout, :cin].float(), bf(ref))
+    assert uf[:, cout:].abs().max().item() == 0 and uf[:, :, cin:].abs().max().item() == 0
+    wflip = w.flip(2, 3).transpose(0, 1)  # [cin, cout, ky', kx']
+    refb = torch.einsum("qk,cnyk->yqcn", G, wflip).reshape(12, cin, cout)
+    assert torch.equal(ub[:, :cin, :cout].float(), bf(refb))
+
+
+def test_wino_dgrad_carries_deferred_wgrad_reduction_twice(ops):
+    """A deferred wgrad reduction rides in the Winograd dgrad launch (every block claims units
+    of it after its epilogue; the last block resets the claim counters). Two rounds on the same
+    handle: the second launch finds the counters reset and reduces again."""
+    dev = torch.device("cuda")
+    torch.manual_seed(3)
+    B, S, C = 64, 19, 192
+    h = ops.PendingReduction()
+    ref_dw, ref_db = None, None
+    for rnd in range(2):
+        x = F.relu(torch.randn(B, C, S, S, device=dev))
+        g = torch.randn(B, C, S, S, device=dev)
+        xp = ops.pack_nchw(x, 1, C)
+        gp = ops.pack_nchw(g, 1, C)
+        w = torch.randn(C, C, 3, 3, device=dev) * 0.05
+        _, ub = ops.wino_weights(w, C, C)
+        # reference: non-deferred wgrad
+        ref_dw = torch.zeros(C, C, 3, 3, device=dev)
+        ref_db = torch.zeros(C, device=dev)
+        ops.conv_wgrad(gp, xp, ref_dw, ref_db, B, S, 1, C, C, C, C, 3, hg=1)
+        dw = torch.full((C, C, 3, 3), float("nan"), device=dev)
+        db = torch.full((C,), float("nan"), device=dev)
+        ops.conv_wgrad(gp, xp, dw, db, B, S, 1, C, C, C, C, 3, hg=1, defer=True, pending=h)
+        dx = ops.alloc_padded(B, S, 1, C, dev)
+        ops.conv_wino(gp, ub, None, dx, B, S, C, C, 1, False, mask=xp, pending=h)
+        torch.cuda.synchronize()
+        assert torch.isfinite(dw).all() and torch.isfinite(db).all(), "round %d" % rnd
+        assert rel_max(dw, ref_dw) < 1e-5 and rel_max(db, ref_db) < 1e-5
