@@ -8,32 +8,33 @@
 //   M_q = sum_{ky, c} V_q[row i+ky][t][c] * U_{ky,q}[n][c]                 (four GEMMs, K = 3C)
 //   y(2t) = M0 + M1 + M2      y(2t+1) = M1 - M2 - M3
 // 12 GEMM taps (ky, q) per output pair instead of 18 direct taps per two pixels: 2/3 of the MFMA
-// work. The transform mixes only +-1 terms (one bf16 rounding of V, exact U up to the bf16
-// rounding of (g0+-g1+g2)/2); tests/test_wino.py pins it against fp32 F.conv2d.
+// work. The transform mixes only +-1 terms (one bf16 rounding of V, one of U = G g);
+// tests/test_wino.py pins it against fp32 F.conv2d.
 //
-// Accumulators: the loop runs the q = 1 and q = 2 GEMMs first into A and B (M1, M2), turns them
-// into (M1 + M2, M1 - M2) in registers, then accumulates q = 0 into A and q = 3 into B with
-// V3' = d3 - d1 = -V3: A = y(2t), B = y(2t+1). Two accumulator sets per output pair = one per
-// pixel, the same register budget as the direct kernel, so one block still covers a whole board.
+// Accumulators: two sets A, B per wave. Phase 1 runs the q = 1 and q = 2 GEMMs into A and B
+// (M1, M2), a register butterfly makes them (M1 + M2, M1 - M2), phase 2 accumulates q = 0 into A
+// and q = 3 into B with V3' = d3 - d1 = -V3: A = y(2t), B = y(2t+1). Two sets per output pair =
+// one accumulator per pixel, the direct kernel's register budget: one block covers a whole
+// 19x19 board (190 output pairs, padded to 192) x 192 output channels; smaller boards pack
+// several per block (nb, host side).
 //
-// Block: one 19x19 board (190 output pairs, padded to 192 = 4 wave rows x 48) x 192 output
-// channels (2 wave columns x 96), 8 waves in two ping-pong groups of 4 (conv_tap_pp_kernel's
-// structure: per K-step two raw s_barriers X / Y; group 0 reads fragments while group 1 runs its
-// MFMAs and the other way round). Smaller boards pack several per block (nb boards, host side).
-// K-steps: 2 phases x (C/32) chunks x 2 slots x 3 ky = 72 for C = 192, 18 MFMAs (48 x 96 x 32)
-// per wave per step from 3 V fragments + 6 weight fragments.
-//
-// Per 32-channel chunk-phase k (phase = k / chunks, chunk = k % chunks):
-//   * raw slab: the block's padded input rows (board rows x 21 columns, 64 B each), staged by
-//     group 0 with LDS-DMA two chunk-phases ahead (double buffered);
-//   * V slab: V for the two slots of the phase, [vrow = (board row) x 10 + t][32 ch], built from
-//     the raw slab one chunk-phase ahead by every wave (2 or 4 LDS reads, the +- in fp32, one
-//     16-byte store per slot), double buffered. A fragment of 16 consecutive output pairs reads
-//     16 consecutive V rows (no halo columns in between, unlike the pixel slab of the direct
-//     kernel, whose fragments straddle board-row ends): the row-bit-2 swizzle keeps it
-//     conflict-free;
-//   * weights: one [192 n][32 c] tile per step through a 3-deep ring, staged by group 1.
-// LDS: 4 x 14 KB (V) + 2 x 32 KB (raw) + 3 x 12 KB (weights) = 156 KB -> one block per CU.
+// Block: 8 waves, wave (wm, wn) = 96 pairs (6 fragments) x 48 channels (3 fragments) of both
+// sets. K-step (chunk-phase k, ky), 36 per C = 192 layer: per set 6 V fragments from LDS and 3
+// weight fragments from registers, 18 MFMA 16x16x32 -> 36 MFMAs per wave per step.
+//   * weights never touch LDS: they are packed fragment-major (every 16 x 32 MFMA operand one
+//     contiguous 1 KB, rag_wino_pack) and each wave loads its fragments for step s+1 straight
+//     into registers right after its step-s MFMAs have read them (L1 serves the two waves that
+//     share a column). The first version staged them through an LDS ring with LDS-DMA: ~150 -
+//     220 issue cycles per 1 KB piece (s_memtime segments) for 12 KB per 144 MFMAs, more than
+//     the MFMAs themselves;
+//   * V slab per chunk-phase, [2 sets][vrow = (board row) x 10 + t][32 ch] in LDS, double
+//     buffered (56 KB): built one chunk-phase ahead by every thread from raw input rows loaded
+//     straight from L2 into registers (two units per thread, loads one step ahead of their
+//     +- and 16-byte LDS stores). A fragment of 16 consecutive output pairs reads 16
+//     consecutive V rows (no halo columns in between, unlike the direct kernel's pixel slab):
+//     the row-bit-2 swizzle keeps it conflict-free;
+//   * one barrier per chunk-phase (the V buffer flip); no per-step barriers, the two waves of
+//     a SIMD overlap freely.
 #include "common.h"
 #include "wgrad_part.h"
 
@@ -42,70 +43,60 @@ using namespace rag;
 namespace {
 
 constexpr int kWK = 32;                  // channels per chunk (MFMA K)
-constexpr int kWMT = 3, kWNT = 6;        // fragments per wave along pairs / output channels
-constexpr int kWP = 64 * kWMT;           // 192 output pairs per block (4 wave rows)
-constexpr int kWN = 32 * kWNT;           // 192 output channels per block (2 wave columns)
+constexpr int kWMT = 6, kWNT = 3;        // fragments per wave along pairs / output channels
+constexpr int kWP = 32 * kWMT;           // 192 output pairs per block (2 wave rows)
+constexpr int kWN = 64 * kWNT;           // 192 output channels per block (4 wave columns)
 constexpr int kVRows = 224;              // V slab rows (a 19x19 board: 21 x 10 = 210)
-constexpr int kRRows = 512;              // raw slab rows (a 19x19 board: 21 x 21 + 1 = 442)
-constexpr int kWRing = 3;                // weight tiles in flight / being read
+constexpr int kRRows = 512;              // raw rows a block may touch (19x19: 21 x 21 + 1)
 constexpr int kVSlot = kVRows * kWK;
-constexpr int kRSlab = kRRows * kWK;
-constexpr int kWTile = kWN * kWK;
-constexpr int kOffR = 4 * kVSlot;        // V: [2 chunk-phase buffers][2 slots]
-constexpr int kOffW = kOffR + 2 * kRSlab;
-constexpr int kLoopLds = kOffW + kWRing * kWTile;
+constexpr int kLoopLds = 4 * kVSlot;     // [2 chunk-phase buffers][2 sets]
 constexpr int kEpRow = kWN + 8;          // bf16 per row of the epilogue image
 constexpr int kEpImg = 2 * kWP * kEpRow; // one image row per output pixel (pair, column)
 constexpr int kLdsElems = kLoopLds > kEpImg ? kLoopLds : kEpImg;
-constexpr int kRawPieces = kRRows / 64;  // 16-row LDS-DMA pieces per group-0 wave per chunk
-constexpr int kWPieces = kWN / 64;       // weight pieces per group-1 wave per step
 constexpr int kRedU = 14;                // chunk loads in flight per reduce thread
 static_assert(kLdsElems * 2 <= 160 * 1024, "LDS budget");
-static_assert(kRawPieces == 8, "raw pieces are issued two per step over steps 0..3");
 
 __device__ __forceinline__ int swz4w(int row) { return ((row >> 2) & 1) << 1; }
 
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
+template <int V> struct IntC {
+  static constexpr int value = V;
+};
 
-__device__ __forceinline__ bf16x8 vsum(const bf16x8& a, const bf16x8& b) {
-  bf16x8 o;
+// a + s * b of 8 bf16 (s = +-1), rounded once: one 32-bit word (two elements) at a time, so the
+// transform never holds more than a few fp32 temporaries next to the 144 accumulators
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <int SGN>
+__device__ __forceinline__ bf16x8 vaddsub(const bf16x8& a, const bf16x8& b) {
+  const u32x4 ua = __builtin_bit_cast(u32x4, a), ub = __builtin_bit_cast(u32x4, b);
+  u32x4 o;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) o[e] = (bf16)((float)a[e] + (float)b[e]);
-  return o;
+  for (int w = 0; w < 4; ++w) {
+    const float a0 = __uint_as_float(ua[w] << 16), a1 = __uint_as_float(ua[w] & 0xffff0000u);
+    const float b0 = __uint_as_float(ub[w] << 16), b1 = __uint_as_float(ub[w] & 0xffff0000u);
+    const bf16x2 r = {(bf16)(SGN > 0 ? a0 + b0 : a0 - b0), (bf16)(SGN > 0 ? a1 + b1 : a1 - b1)};
+    o[w] = __builtin_bit_cast(uint32_t, r);
+  }
+  return __builtin_bit_cast(bf16x8, o);
 }
-__device__ __forceinline__ bf16x8 vdiff(const bf16x8& a, const bf16x8& b) {
-  bf16x8 o;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) o[e] = (bf16)((float)a[e] - (float)b[e]);
-  return o;
-}
+__device__ __forceinline__ bf16x8 vsum(const bf16x8& a, const bf16x8& b) { return vaddsub<1>(a, b); }
+__device__ __forceinline__ bf16x8 vdiff(const bf16x8& a, const bf16x8& b) { return vaddsub<-1>(a, b); }
 
-// X: padded input [B][S+2][S+2][KIN] (halo 1). U: Winograd weights [12 = (ky, q)][NOUT][KIN].
-// Y: padded output (halo HO, YC channels); mask: the dgrad ReLU mask (halo HM) or null.
+// X: padded input [B][S+2][S+2][KIN] (halo 1). U: Winograd weights, fragment-major
+// [12 = (ky, q)][KIN / 32][NOUT / 16][64 lanes][8] (rag_wino_pack). Y: padded output (halo HO,
+// YC channels); mask: the dgrad ReLU mask (halo HM) or null.
 // Block (x, y): boards [x * nb, x * nb + nb), output channels [192 y, 192 y + 192).
-// DIAG (timing builds, WRONG results): bit 0 no transform in the loop, bit 1 no raw staging,
-// bit 2 no weight staging, bit 3 no MFMAs, bit 4 no fragment reads, bit 5 no epilogue stores;
-// bit 6 (results correct): per-wave s_memtime segment sums of the loop into `stamps`.
-template <int DIAG = 0>
+// SINGLE: one board per block (19x19): the V row of output pair m is m itself (pad pairs 190,
+// 191 read rows < 224 whose outputs are dropped), so no per-fragment row table is kept.
+template <bool SINGLE>
 __global__ void __launch_bounds__(512, 1)
 conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
                  const float* __restrict__ bias, bf16* __restrict__ Y,
                  const bf16* __restrict__ mask, int B, int S, int KIN, int NOUT, int HO, int YC,
-                 int relu, int HM, int nb, WgradRed red, long long* stamps = nullptr) {
+                 int relu, int HM, int nb, WgradRed red) {
   __shared__ __attribute__((aligned(16))) bf16 lds[kLdsElems];
-  long long seg[6] = {0, 0, 0, 0, 0, 0};
-  auto now = [&]() -> long long {
-    if constexpr ((DIAG & 64) != 0) return __builtin_amdgcn_s_memtime();
-    return 0;
-  };
   const int lane = lane_id();
   const int w = wave_id();
-  const int grp = w >> 2;  // waves w and w + 4 share a SIMD
-  const int wl = w & 3;
-  const int wm = grp * 2 + (wl & 1), wn = wl >> 1;
+  const int wm = w & 1, wn = w >> 1;
   const int frow = lane & 15, fq = lane >> 4;
   const int WI = S + 2, TJ = (S + 1) >> 1;
   const int PB = S * TJ;    // output pairs per board
@@ -115,128 +106,101 @@ conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
   const int n0 = blockIdx.y * kWN;
   const long total_rows = (long)B * RPB;
   const int cchunks = KIN / kWK;
-  const int NK = 2 * cchunks;      // chunk-phases
-  const int nsteps = 6 * NK;
+  const int NK = 2 * cchunks;  // chunk-phases
 
-  // ---- per-lane fragment offsets
-  int vb[kWMT];  // V row of this lane's output pair (tap ky adds ky * TJ)
+  // ---- V rows of this lane's output pairs (tap ky adds ky * TJ)
+  int vb[SINGLE ? 1 : kWMT];
 #pragma unroll
-  for (int i = 0; i < kWMT; ++i) {
+  for (int i = 0; i < (SINGLE ? 1 : kWMT); ++i) {
     int m = wm * (16 * kWMT) + i * 16 + frow;
+    if (SINGLE) {
+      vb[i] = m;
+      continue;
+    }
     m = m < nb * PB ? m : nb * PB - 1;  // pad pairs read a valid row, their output is dropped
     const int bl = m / PB, rem = m - bl * PB;
     const int ii = rem / TJ, t = rem - ii * TJ;
     vb[i] = (bl * WI + ii) * TJ + t;
   }
-  // weight fragment j: tile row wn * 96 + 16 j + frow; the swizzle depends on row bit 2 only
-  // (= frow bit 2), so fragment j sits at a constant 16 * 32 * j elements from fragment 0
-  const int boff0 = (wn * (16 * kWNT) + frow) * kWK + ((fq ^ swz4w(frow)) * 8);
-  // ---- transform units of this thread (the same for every chunk-phase): V row, 8-channel group,
-  // raw row of d0
+
+  // ---- global loads are buffer loads: a wave-uniform descriptor (SGPRs), a 32-bit lane offset
+  // and a uniform SGPR offset, one VGPR per address instead of 64-bit pointers (the kernel sat
+  // at 256 VGPRs and its scratch reloads, being VMEM, forced vmcnt(0) waits on every weight
+  // load in flight); the descriptor's range check also replaces the raw rows' clamp.
+  auto rsrc = [](const void* p, long bytes) {
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const int nb = __builtin_amdgcn_readfirstlane((int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL));
+    return __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0, nb, 0x00020000);
+  };
+  // weight fragments: fragment (tap, chunk, nf) is 512 contiguous bf16, lane l's 8 at 8 l
+  const int NF = NOUT / 16;
+  const auto urs = rsrc(U, 12L * NOUT * KIN * 2);
+  const uint32_t uoff = (uint32_t)((((n0 >> 4) + wn * kWNT) * 512 + lane * 8) * 2);
+  auto wfrag = [&](int tap, int c, int j) {
+    const int so = ((tap * cchunks + c) * NF + j) * 1024;
+    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(urs, uoff, so, 0));
+  };
+  // taps: set A q = 1 (phase 1) / 0 (phase 2), set B q = 2 / 3; tap (ky, q) = 4 ky + q
+
+  // ---- transform units of this thread (the same for every chunk-phase): V row, 8-channel
+  // group, raw row of d0 (named scalars: a runtime-indexed array went to scratch)
+  // packed: V row (bits 0-9), 8-channel group (10-11), raw row of d0 (12-30), -1 = no unit
   const int NU = nb * VPB * 4;
-  // (named scalars, not arrays: a runtime-indexed array went to scratch)
-  int tv0, tk0, tr0, tv1, tk1, tr1;
-  auto unit = [&](int it, int& tv, int& tk, int& tr) {
+  auto unit = [&](int it) {
     const int u = threadIdx.x + it * 512;
     const int v = u >> 2;
-    tk = u & 3;
-    tv = u < NU ? v : -1;
     const int bl = v / VPB, rem = v - bl * VPB;
     const int r = rem / TJ, t = rem - r * TJ;
-    tr = (bl * WI + r) * WI + 2 * t;
+    const int rr = (bl * WI + r) * WI + 2 * t;
+    return u < NU ? (v | ((u & 3) << 10) | (rr << 12)) : -1;
   };
-  unit(0, tv0, tk0, tr0);
-  unit(1, tv1, tk1, tr1);
-  // Both of this thread's units of V(kk) from raw(kk) in one pass: all LDS reads first, then
-  // the arithmetic, then the stores (one unit at a time was a dependent read -> add -> write
-  // chain of ~1000 cycles per call).
-  auto transform2 = [&](int kk) {
-    int v0 = tv0, k0 = tk0, r0 = tr0, v1 = tv1, k1 = tk1, r1 = tr1;
-    asm volatile("" : "+v"(v0), "+v"(k0), "+v"(r0), "+v"(v1), "+v"(k1), "+v"(r1));
-    if (v0 < 0) return;         // (boards of S = 2: NU < 512)
-    const bool has1 = v1 >= 0;  // unit 1 may be past the end
-    if (!has1) {
-      v1 = v0;
-      k1 = k0;
-      r1 = r0;
-    }
-    const bf16* raw = lds + kOffR + (kk & 1) * kRSlab;
-    auto ld = [&](int row, int k8) {
-      return *reinterpret_cast<const bf16x8*>(raw + row * kWK + ((k8 ^ swz4w(row)) * 8));
-    };
-    bf16x8 a0, b0v, a1, b1;
-    if (kk < cchunks) {  // phase 1: V1 = d1 + d2, V2 = d2 - d1
-      const bf16x8 p1 = ld(r0 + 1, k0), p2 = ld(r0 + 2, k0);
-      const bf16x8 q1 = ld(r1 + 1, k1), q2 = ld(r1 + 2, k1);
-      a0 = vsum(p1, p2);
-      b0v = vdiff(p2, p1);
-      a1 = vsum(q1, q2);
-      b1 = vdiff(q2, q1);
-    } else {  // phase 2: V0 = d0 - d2, V3' = d3 - d1
-      const bf16x8 p0 = ld(r0, k0), p1 = ld(r0 + 1, k0), p2 = ld(r0 + 2, k0),
-                   p3 = ld(r0 + 3, k0);
-      const bf16x8 q0 = ld(r1, k1), q1 = ld(r1 + 1, k1), q2 = ld(r1 + 2, k1),
-                   q3 = ld(r1 + 3, k1);
-      a0 = vdiff(p0, p2);
-      b0v = vdiff(p3, p1);
-      a1 = vdiff(q0, q2);
-      b1 = vdiff(q3, q1);
-    }
-    bf16* vs = lds + (kk & 1) * 2 * kVSlot;
-    const int o0 = v0 * kWK + ((k0 ^ swz4w(v0)) * 8);
-    const int o1 = v1 * kWK + ((k1 ^ swz4w(v1)) * 8);
-    *reinterpret_cast<bf16x8*>(vs + o0) = a0;
-    *reinterpret_cast<bf16x8*>(vs + kVSlot + o0) = b0v;
-    if (has1) {
-      *reinterpret_cast<bf16x8*>(vs + o1) = a1;
-      *reinterpret_cast<bf16x8*>(vs + kVSlot + o1) = b1;
-    }
+  const int tu0 = unit(0), tu1 = unit(1);
+  // raw rows of this block's boards (out of range, i.e. the last block's +1 row, reads 0)
+  const auto xrs = rsrc(X + (long)b0 * RPB * KIN, (total_rows - (long)b0 * RPB) * KIN * 2);
+  // The transform of V(kk) runs as four "ops" per thread and chunk-phase, two raw-pixel loads
+  // each: op 2u + h of unit u (h = set): phase 1 loads (d1, d2) for both sets (V1 = d1 + d2,
+  // V2 = d2 - d1), phase 2 (d0, d2) for set A (V0 = d0 - d2) and (d3, d1) for set B
+  // (V3' = d3 - d1). An op's loads go out one MFMA block before its +- and store.
+  // Every global load in the loop is issued unconditionally (a missing unit or a chunk-phase
+  // past the end loads a valid dummy row and skips only its LDS store): with loads under
+  // branches hipcc's counter analysis fell back to `s_waitcnt vmcnt(0)`, so each transform
+  // store and each set's first MFMA waited for every load in flight, the next step's weights
+  // included.
+  bf16x8 da, db;
+  auto op_unit = [&](int o, int& v, int& k8, int& rr) {
+    int pk = (o >> 1) ? tu1 : tu0;
+    asm volatile("" : "+v"(pk));
+    v = pk < 0 ? -1 : (pk & 1023);
+    pk = pk < 0 ? 0 : pk;
+    k8 = (pk >> 10) & 3;
+    rr = pk >> 12;
   };
-
-  // ---- staging: raw slab (group 0), weight tiles (group 1)
-  // Every LDS-DMA source is a wave-uniform base (SGPRs) plus this lane's 32-bit byte offset,
-  // so a piece issues as `global_load_lds_dwordx4 v_off, s[base]` with one VALU add: with
-  // per-lane 64-bit addresses (and the raw rows' clamp) each 1 KB piece cost 150-220 cycles of
-  // the issuing wave (s_memtime segments), and hoisted they were 11 live pointers (spills).
-  // Lane (lrow, lcol) of piece p stages row 64 p + 16 wl + lrow, 16-byte chunk lcol ^ swz
-  // (the swizzle depends on row bit 2 only, the same for every piece).
-  const int lrow = lane >> 2, lcol = lane & 3;
-  const int prow0 = wl * 16 + lrow;
-  const uint32_t loff_r = (uint32_t)(prow0 * KIN + ((lcol ^ swz4w(prow0)) * 8)) * 2u;
-  const uint32_t piece_r = (uint32_t)(64 * KIN) * 2u;  // bytes between pieces
-  // the block's raw rows run past the tensor's end only in the last block(s): clamp there only
-  const int rowlim = (int)(total_rows - (long)b0 * RPB) - 1;  // last valid raw row of the block
-  const bool raw_fits = rowlim >= kRRows - 1;
-  auto stage_raw = [&](int kk, int p0, int p1) {  // pieces p0 .. p1-1 of raw(kk)
-    if ((DIAG & 2) && kk >= 2) return;
-    bf16* dst = lds + kOffR + (kk & 1) * kRSlab + wl * 16 * kWK;
-    const int c = kk % cchunks;
-    const char* xb = reinterpret_cast<const char*>(X + ((long)b0 * RPB) * KIN + c * kWK);
-#pragma unroll
-    for (int p = 0; p < kRawPieces; ++p) {
-      if (p < p0 || p >= p1) continue;
-      if (raw_fits) {
-        glds16(xb + (loff_r + p * piece_r), dst + p * 64 * kWK);
-      } else {
-        const int r = prow0 + 64 * p;
-        const int rc = r < rowlim ? r : rowlim;
-        glds16(xb + (uint32_t)(rc * KIN + ((lcol ^ swz4w(r)) * 8)) * 2u, dst + p * 64 * kWK);
-      }
-    }
+  // P1: the V being built belongs to phase 1 (compile time: a runtime phase test put both
+  // arithmetic paths and a join into the loop, and hipcc's counters and registers with them)
+  auto op_load = [&](auto p1c, int kk, int o) {  // kk may be NK (past the end): a dummy
+    constexpr bool P1 = decltype(p1c)::value;
+    int v, k8, rr;
+    op_unit(o, v, k8, rr);
+    const int h = o & 1;
+    const int ra = P1 ? 1 : (h ? 3 : 0), rb = P1 ? 2 : (h ? 1 : 2);
+    const int so = (kk % cchunks) * kWK * 2;
+    const uint32_t o0 = (uint32_t)((rr + ra) * KIN + k8 * 8) * 2u;
+    const uint32_t o1 = (uint32_t)((rr + rb) * KIN + k8 * 8) * 2u;
+    da = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(xrs, o0, so, 0));
+    db = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(xrs, o1, so, 0));
   };
-  const long tap_stride = (long)NOUT * KIN;
-  const uint32_t loff_w = loff_r;  // weight rows: the same lane -> (row, chunk) map
-  // step s -> chunk-phase kk, slot (0: accumulator A, 1: B), ky
-  auto stage_w = [&](int s) {
-    if ((DIAG & 4) && s >= 2) return;
-    const int kk = s / 6, u = s - kk * 6;
-    const int slot = u / 3, ky = u - slot * 3;
-    const int q = kk < cchunks ? 1 + slot : 3 * slot;  // phase 1: q = 1, 2; phase 2: q = 0, 3
-    bf16* dst = lds + kOffW + (s % kWRing) * kWTile + wl * 16 * kWK;
-    const char* ub = reinterpret_cast<const char*>(
-        U + (ky * 4 + q) * tap_stride + (long)n0 * KIN + (kk % cchunks) * kWK);
-#pragma unroll
-    for (int k = 0; k < kWPieces; ++k) glds16(ub + (loff_w + k * piece_r), dst + k * 64 * kWK);
+  auto op_store = [&](auto p1c, int kk, int o) {  // branch-free: no unit -> the last V row
+    constexpr bool P1 = decltype(p1c)::value;
+    int v, k8, rr;
+    op_unit(o, v, k8, rr);
+    v = v < 0 ? kVRows - 1 : v;
+    const int h = o & 1;
+    bf16* vs = lds + (kk & 1) * 2 * kVSlot + h * kVSlot;
+    const bf16x8 val = P1 ? (h ? vdiff(db, da) : vsum(da, db)) : vdiff(da, db);
+    *reinterpret_cast<bf16x8*>(vs + v * kWK + ((k8 ^ swz4w(v)) * 8)) = val;
   };
 
   f32x4 accA[kWNT][kWMT], accB[kWNT][kWMT];
@@ -247,158 +211,129 @@ conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
       accA[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
       accB[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-  bf16x8 xa[kWMT], wb[kWNT];
-  auto read_frags = [&](int s) {
-    if constexpr ((DIAG & 16) != 0) {
-      asm volatile("" : "+v"(xa[0]), "+v"(wb[0]));
-      return;
-    }
-    const int kk = s / 6, u = s - kk * 6;
-    const int slot = u / 3, ky = u - slot * 3;
-    const bf16* vs = lds + ((kk & 1) * 2 + slot) * kVSlot;
-    const bf16* wt = lds + kOffW + (s % kWRing) * kWTile;
+  // V fragments are read in two halves of three (12 registers instead of 24: with all six
+  // live, hipcc spilled the transform's raw loads and waited for them at once)
+  constexpr int kH = kWMT / 2;
+  bf16x8 xa[kH], wA[kWNT], wB[kWNT];
+  auto read_v = [&](int kk, int ky, int set, int h) {
+    const bf16* vs = lds + ((kk & 1) * 2 + set) * kVSlot;
     const int sh = ky * TJ;
+    if constexpr (SINGLE) {
+      int r0 = vb[0];
+      asm volatile("" : "+v"(r0));  // not hoisted: per-(fragment, ky) addresses, 18 registers
+      r0 += sh + h * kH * 16;
+      const int sw0 = (fq ^ swz4w(r0)) * 8;  // rows r0 + 16 i share row bit 2
 #pragma unroll
-    for (int i = 0; i < kWMT; ++i) {
-      // opaque per step: hoisted, the (fragment, ky) addresses were loop-invariant registers
-      asm volatile("" : "+v"(vb[i]));
-      const int r = vb[i] + sh;
-      xa[i] = *reinterpret_cast<const bf16x8*>(vs + r * kWK + ((fq ^ swz4w(r)) * 8));
-    }
-#pragma unroll
-    for (int j = 0; j < kWNT; ++j)
-      wb[j] = *reinterpret_cast<const bf16x8*>(wt + boff0 + j * 16 * kWK);
-    lds_reads_done();  // retire the burst (and any transform writes) before the next barrier
-  };
-  auto mfmas = [&](int u) {  // u = the step's index within its chunk-phase (a constant)
-    if constexpr ((DIAG & 8) != 0) {
-      asm volatile("" : "+v"(xa[0]), "+v"(wb[0]), "+v"(xa[1]), "+v"(wb[1]));
-      return;
-    }
-    if (u < 3) {
-#pragma unroll
-      for (int j = 0; j < kWNT; ++j)
-#pragma unroll
-        for (int i = 0; i < kWMT; ++i) accA[j][i] = mfma16(wb[j], xa[i], accA[j][i]);
+      for (int i = 0; i < kH; ++i)
+        xa[i] = *reinterpret_cast<const bf16x8*>(vs + (r0 + i * 16) * kWK + sw0);
     } else {
 #pragma unroll
-      for (int j = 0; j < kWNT; ++j)
-#pragma unroll
-        for (int i = 0; i < kWMT; ++i) accB[j][i] = mfma16(wb[j], xa[i], accB[j][i]);
+      for (int i = 0; i < kH; ++i) {
+        int v = vb[h * kH + i];
+        asm volatile("" : "+v"(v));
+        const int r = v + sh;
+        xa[i] = *reinterpret_cast<const bf16x8*>(vs + r * kWK + ((fq ^ swz4w(r)) * 8));
+      }
     }
   };
-  auto butterfly = [&]() {  // (M1, M2) -> (M1 + M2, M1 - M2)
-#pragma unroll
-    for (int j = 0; j < kWNT; ++j)
-#pragma unroll
-      for (int i = 0; i < kWMT; ++i) {
-        const f32x4 a = accA[j][i], b = accB[j][i];
-        accA[j][i] = a + b;
-        accB[j][i] = a - b;
-      }
-  };
-  // after this wave's MFMAs of step s: the butterfly at the phase boundary, and the transform
-  // units of V(kk + 1) at steps u = 1 and 3 of chunk-phase kk
-  auto after_mfmas = [&](int kk, int u) {
-    if (u == 5 && kk == NK / 2 - 1) butterfly();
-    if (kk + 1 < NK && !(DIAG & 1) && u == 1) transform2(kk + 1);
-  };
 
-  // ---- prologue: raw(0), raw(1) and V(0) (every wave), B(0), B(1)
-  if (grp == 0) {
-    stage_raw(0, 0, kRawPieces);
-    stage_raw(1, 0, kRawPieces);
-    wait_vm<kRawPieces>();  // raw(0) landed (raw(1)'s pieces are younger)
-  } else {
-    stage_w(0);
-    stage_w(1);
+  // ---- prologue: step (0, 0)'s weights, V(0)
+#pragma unroll
+  for (int j = 0; j < kWNT; ++j) {
+    wA[j] = wfrag(1, 0, j);
+    wB[j] = wfrag(2, 0, j);
   }
-  __builtin_amdgcn_s_barrier();  // raw(0) visible
-  asm volatile("" ::: "memory");
-  transform2(0);
+#pragma unroll
+  for (int o = 0; o < 4; ++o) {  // V(0) (phase 1)
+    op_load(IntC<1>{}, 0, o);
+    op_store(IntC<1>{}, 0, o);
+  }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  if (grp == 0)
-    wait_vm<0>();           // raw(1)
-  else
-    wait_vm<kWPieces>();    // B(0) (B(1) younger)
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 
-  if (grp == 0) {
+  // one chunk-phase: CUR = phase of kk (its taps), NXT = phase of kk + 1 (the V built and the
+  // weights prefetched during kk)
+  auto chunk_phase = [&](int kk, auto curc, auto nxtc) {
+    constexpr bool CUR1 = decltype(curc)::value, NXT1 = decltype(nxtc)::value;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      // next step's weights: (kk, ky + 1) or (kk + 1, 0); past the end: a dummy (the last
+      // step's again)
+      const bool nxt1 = ky < 2 ? CUR1 : NXT1;
+      int nkk = ky < 2 ? kk : kk + 1, nky = ky < 2 ? ky + 1 : 0;
+      if (nkk >= NK) {
+        nkk = NK - 1;
+        nky = 2;
+      }
+      const int nc = nkk % cchunks;
+      const int ntA = nky * 4 + (nxt1 ? 1 : 0), ntB = nky * 4 + (nxt1 ? 2 : 3);
+      // transform ops of V(kk + 1) in the six (ky, set) slots: slot t stores op t-1 and loads
+      // op t (loads in slots 0..3, stores in 1..4; in the last chunk-phase they fill the idle
+      // buffer, read by nobody)
+      if (ky > 0) op_store(nxtc, kk + 1, 2 * ky - 1);
+      __builtin_amdgcn_sched_barrier(0);
+      if (ky < 2) op_load(nxtc, kk + 1, 2 * ky);
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- set A
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        read_v(kk, ky, 0, h);
+#pragma unroll
+        for (int j = 0; j < kWNT; ++j) {
+#pragma unroll
+          for (int i = 0; i < kH; ++i)
+            accA[j][h * kH + i] = mfma16(wA[j], xa[i], accA[j][h * kH + i]);
+          if (h == 1) wA[j] = wfrag(ntA, nc, j);
+        }
+      }
+      // (scheduling fences: hipcc otherwise reads set B's fragments into a second register set
+      // while set A's MFMAs still hold the first, and the kernel spills)
+      __builtin_amdgcn_sched_barrier(0);
+      if (ky < 2) {
+        op_store(nxtc, kk + 1, 2 * ky);
+        __builtin_amdgcn_sched_barrier(0);  // the old op's registers free before the new loads
+        op_load(nxtc, kk + 1, 2 * ky + 1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- set B
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        read_v(kk, ky, 1, h);
+#pragma unroll
+        for (int j = 0; j < kWNT; ++j) {
+#pragma unroll
+          for (int i = 0; i < kH; ++i)
+            accB[j][h * kH + i] = mfma16(wB[j], xa[i], accB[j][h * kH + i]);
+          if (h == 1) wB[j] = wfrag(ntB, nc, j);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // V(kk + 1) complete and V(kk) read by every wave before the buffers flip
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
 #pragma unroll 1
-    for (int kk = 0; kk < NK; ++kk)
+  for (int kk = 0; kk < cchunks - 1; ++kk) chunk_phase(kk, IntC<1>{}, IntC<1>{});
+  chunk_phase(cchunks - 1, IntC<1>{}, IntC<0>{});
+  // (M1, M2) -> (M1 + M2, M1 - M2)
 #pragma unroll
-    for (int u = 0; u < 6; ++u) {  // unrolled: the slot (accumulator) and ky are constants
-      const int s = kk * 6 + u;
-      const long long c0 = now();
-      __builtin_amdgcn_s_barrier();  // X_s
-      asm volatile("" ::: "memory");
-      const long long c1 = now();
-      if (u < 4 && kk + 2 < NK) stage_raw(kk + 2, 2 * u, 2 * u + 2);
-      const long long c2 = now();
-      read_frags(s);
-      const long long c3 = now();
-      __builtin_amdgcn_s_barrier();  // Y_s
-      asm volatile("" ::: "memory");
-      const long long c4 = now();
-      mfmas(u);
-      const long long c5 = now();
-      after_mfmas(kk, u);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // transform writes before X_{s+1}
-      if (u == 5 && kk + 2 < NK) wait_vm<0>();           // raw(kk+2) before chunk-phase kk+1
-      if constexpr ((DIAG & 64) != 0) {  // X wait, staging, reads, Y wait, MFMA issue, post
-        const long long c6 = now();
-        seg[0] += c1 - c0; seg[1] += c2 - c1; seg[2] += c3 - c2;
-        seg[3] += c4 - c3; seg[4] += c5 - c4; seg[5] += c6 - c5;
-      }
+  for (int j = 0; j < kWNT; ++j)
+#pragma unroll
+    for (int i = 0; i < kWMT; ++i) {
+      const f32x4 a = accA[j][i], b = accB[j][i];
+      accA[j][i] = a + b;
+      accB[j][i] = a - b;
     }
-  } else {
-    __builtin_amdgcn_s_setprio(1);  // static priority for the younger half
 #pragma unroll 1
-    for (int kk = 0; kk < NK; ++kk)
-#pragma unroll
-    for (int u = 0; u < 6; ++u) {
-      const int s = kk * 6 + u;
-      const long long c0 = now();
-      __builtin_amdgcn_s_barrier();  // X_s
-      asm volatile("" ::: "memory");
-      const long long c1 = now();
-      long long c2 = c1;
-      if (s > 0) {  // step s - 1, beside group 0's reads of step s
-        mfmas(u == 0 ? 5 : u - 1);
-        c2 = now();
-        after_mfmas(u == 0 ? kk - 1 : kk, u == 0 ? 5 : u - 1);
-      }
-      const long long c3 = now();
-      __builtin_amdgcn_s_barrier();  // Y_s
-      asm volatile("" ::: "memory");
-      const long long c4 = now();
-      read_frags(s);  // beside group 0's MFMAs of step s (also retires the transform writes)
-      const long long c5 = now();
-      if (s + 2 < nsteps) {
-        stage_w(s + 2);
-        wait_vm<kWPieces>();  // B(s+1) complete before X_{s+1}: B(s+2) is younger
-      } else {
-        wait_vm<0>();
-      }
-      if constexpr ((DIAG & 64) != 0) {  // X wait, MFMA issue, transform, Y wait, reads, stage
-        const long long c6 = now();
-        seg[0] += c1 - c0; seg[1] += c2 - c1; seg[2] += c3 - c2;
-        seg[3] += c4 - c3; seg[4] += c5 - c4; seg[5] += c6 - c5;
-      }
-    }
-    mfmas(5);
-    __builtin_amdgcn_s_setprio(0);
-  }
-  if constexpr ((DIAG & 64) != 0) {
-    if (lane == 0 && stamps) {
-      long long* o = stamps + ((size_t)blockIdx.x * 8 + w) * 6;
-#pragma unroll
-      for (int k = 0; k < 6; ++k) o[k] = seg[k];
-    }
-  }
+  for (int kk = cchunks; kk < NK; ++kk) chunk_phase(kk, IntC<0>{}, IntC<0>{});
 
   // ---- epilogue: bias (+ ReLU) -> bf16 image [pair][column][channel] in LDS, then whole
   // 384-byte pixel rows out with the dgrad mask applied
-  __syncthreads();  // every wave is past its last LDS read
+  __syncthreads();
 #pragma unroll
   for (int j = 0; j < kWNT; ++j) {
     const int n = wn * (16 * kWNT) + j * 16 + fq * 4;
@@ -427,8 +362,8 @@ conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
     const int S2 = S * S, WO = S + 2 * HO, WMK = S + 2 * HM;
     constexpr int kChunks = kWN / 8;  // 16-byte chunks per pixel row
     const int total = nbl * S2 * kChunks;
-    for (int c = threadIdx.x; c < total; c += 512) {
-      const int pix = c / kChunks, k8 = (c - pix * kChunks) * 8;
+    for (int e = threadIdx.x; e < total; e += 512) {
+      const int pix = e / kChunks, k8 = (e - pix * kChunks) * 8;
       const int bl = pix / S2, rem = pix - bl * S2;
       const int i = rem / S, j = rem - i * S;
       const int m = bl * PB + i * TJ + (j >> 1);
@@ -438,11 +373,7 @@ conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
         const bf16x8 mk = *reinterpret_cast<const bf16x8*>(
             mask + (size_t)((b * WMK + i + HM) * WMK + j + HM) * YC + n0 + k8);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = ((float)mk[e] > 0.f) ? v[e] : (bf16)0.f;
-      }
-      if constexpr ((DIAG & 32) != 0) {
-        if ((float)v[0] == 12345.f) Y[0] = v[1];
-        continue;
+        for (int q = 0; q < 8; ++q) v[q] = ((float)mk[q] > 0.f) ? v[q] : (bf16)0.f;
       }
       *reinterpret_cast<bf16x8*>(Y + (size_t)((b * WO + i + HO) * WO + j + HO) * YC + n0 + k8) = v;
     }
@@ -451,9 +382,11 @@ conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
   if (red.ticket) wslab_reduce_dynamic<kRedU>(red, reinterpret_cast<int*>(lds));
 }
 
-// Winograd weights of 3x3 layers from the fp32 OIHW masters: forward Uf [12][COUTP][CINP]
-// (tap (ky, q) = ky * 4 + q) and dgrad Ub [12][CINP][COUTP] (the same transform of the flipped,
-// transposed kernel W[n][c][2-ky][2-kx]). Block = one 64 (n) x 64 (c) tile of one kernel row ky
+// Winograd weights of 3x3 layers from the fp32 OIHW masters: forward Uf (N = COUTP, K = CINP)
+// and dgrad Ub (N = CINP, K = COUTP: the same transform of the flipped, transposed kernel
+// W[n][c][2-ky][2-kx]), tap (ky, q) = ky * 4 + q, each stored fragment-major
+// [12][K / 32][N / 16][64][8]: element (n, k) of a tap at lane (n % 16) + 16 ((k % 32) / 8),
+// position k % 8 of fragment (k / 32, n / 16), as a 16x16x32 MFMA A operand reads it. Block = one 64 (n) x 64 (c) tile of one kernel row ky
 // of one layer (blockIdx.y): the row's three taps go through LDS so both layouts are written
 // coalesced (Uf along c, Ub along n).
 constexpr int kWinoPackFields = 8;  // W, COUT, CIN, COUTP, CINP, Uf, Ub (or 0), unused
@@ -470,6 +403,11 @@ __global__ void __launch_bounds__(256) wino_pack_kernel(const int64_t* __restric
   __shared__ float tl[3][64][65];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const long tap_stride = (long)COUTP * CINP;
+  // fragment-major offset of (n, k) in a [N][K] tap
+  auto fm = [](int n, int k, int N) {
+    return ((size_t)((k >> 5) * (N >> 4) + (n >> 4)) * 64 + (n & 15) + 16 * ((k & 31) >> 3)) * 8 +
+           (k & 7);
+  };
 #pragma unroll 4
   for (int i = 0; i < 16; ++i) {
     const int nl = ty + 4 * i;
@@ -485,7 +423,7 @@ __global__ void __launch_bounds__(256) wino_pack_kernel(const int64_t* __restric
     tl[1][nl][tx] = g1;
     tl[2][nl][tx] = g2;
     if (n < COUTP && c < CINP) {
-      const size_t o = (size_t)n * CINP + c;
+      const size_t o = fm(n, c, COUTP);
       Uf[(ky * 4 + 0) * tap_stride + o] = (bf16)g0;
       Uf[(ky * 4 + 1) * tap_stride + o] = (bf16)(0.5f * (g0 + g1 + g2));
       Uf[(ky * 4 + 2) * tap_stride + o] = (bf16)(0.5f * (g0 - g1 + g2));
@@ -501,7 +439,7 @@ __global__ void __launch_bounds__(256) wino_pack_kernel(const int64_t* __restric
     const int c = ct * 64 + cl, n = nt * 64 + tx;
     if (c < CINP && n < COUTP) {
       const float h0 = tl[2][tx][cl], h1 = tl[1][tx][cl], h2 = tl[0][tx][cl];
-      const size_t o = (size_t)c * COUTP + n;
+      const size_t o = fm(c, n, CINP);
       Ub[(kyb * 4 + 0) * tap_stride + o] = (bf16)h0;
       Ub[(kyb * 4 + 1) * tap_stride + o] = (bf16)(0.5f * (h0 + h1 + h2));
       Ub[(kyb * 4 + 2) * tap_stride + o] = (bf16)(0.5f * (h0 - h1 + h2));
@@ -510,13 +448,13 @@ __global__ void __launch_bounds__(256) wino_pack_kernel(const int64_t* __restric
   }
 }
 
-// Boards per block: as many as fit the 192 pair rows, the V slab and the raw slab.
+// Boards per block: as many as fit the 192 pair rows and the V slab.
 int wino_boards_per_block(int S) {
   const int WI = S + 2, TJ = (S + 1) / 2;
   const int PB = S * TJ, VPB = WI * TJ, RPB = WI * WI;
   int nb = kWP / PB;
   if (nb * VPB > kVRows) nb = kVRows / VPB;
-  if (nb * RPB + 1 > kRRows) nb = (kRRows - 1) / RPB;
+  if (nb * RPB + 1 > kRRows) nb = (kRRows - 1) / RPB;  // (32-bit raw offsets stay small)
   return nb;
 }
 
@@ -530,8 +468,8 @@ RAG_API int rag_conv_wino_ok(int S, int HI, int KIN, int NOUT, int KS) {
          wino_boards_per_block(S) >= 1;
 }
 
-// Winograd 3x3 conv (forward or dgrad): X [B][S+2][S+2][KIN] bf16, U [12][NOUT][KIN] bf16
-// (rag_wino_pack), Y padded with halo HO and YC >= NOUT channels, mask (dgrad) with halo HM.
+// Winograd 3x3 conv (forward or dgrad): X [B][S+2][S+2][KIN] bf16, U the layer's fragment-major
+// Winograd weights (rag_wino_pack), Y padded with halo HO and YC >= NOUT channels, mask (dgrad) with halo HM.
 // `pending`: a deferred wgrad reduction handle (conv.hip PendingRed) or null.
 int rag_conv_wino_launch(const void* X, const void* W, const float* bias, void* Y,
                          const void* mask, int B, int S, int KIN, int NOUT, int HO, int YC,
@@ -541,9 +479,14 @@ int rag_conv_wino_launch(const void* X, const void* W, const float* bias, void* 
   WgradRed r{};
   if (red) r = *red;
   const dim3 grid((B + nb - 1) / nb, NOUT / kWN);
-  conv_wino_kernel<0><<<grid, 512, 0, stream>>>((const bf16*)X, (const bf16*)W, bias, (bf16*)Y,
-                                             (const bf16*)mask, B, S, KIN, NOUT, HO, YC, relu,
-                                             HM, nb, r);
+  if (nb == 1)
+    conv_wino_kernel<true><<<grid, 512, 0, stream>>>((const bf16*)X, (const bf16*)W, bias,
+                                                     (bf16*)Y, (const bf16*)mask, B, S, KIN, NOUT,
+                                                     HO, YC, relu, HM, nb, r);
+  else
+    conv_wino_kernel<false><<<grid, 512, 0, stream>>>((const bf16*)X, (const bf16*)W, bias,
+                                                      (bf16*)Y, (const bf16*)mask, B, S, KIN,
+                                                      NOUT, HO, YC, relu, HM, nb, r);
   return (int)hipGetLastError();
 }
 
@@ -552,44 +495,6 @@ RAG_API int rag_conv_wino(const void* X, const void* W, const float* bias, void*
                           int relu, int HM, hipStream_t stream) {
   return rag_conv_wino_launch(X, W, bias, Y, mask, B, S, KIN, NOUT, HO, YC, relu, HM, stream,
                               nullptr);
-}
-
-static long long* g_wino_stamps = nullptr;
-// Per-wave loop segment cycle sums of the last DIAG-64 launch: [block][wave][6] int64.
-RAG_API int rag_conv_wino_stamps(long long* host, int nblocks) {
-  if (!g_wino_stamps) return -1;
-  if (hipDeviceSynchronize() != hipSuccess) return -2;
-  return (int)hipMemcpy(host, g_wino_stamps, (size_t)nblocks * 8 * 6 * sizeof(long long),
-                        hipMemcpyDeviceToHost);
-}
-
-// Timing-diagnostic launches (WRONG results): diag = the kernel's DIAG bits.
-RAG_API int rag_conv_wino_diag(int diag, const void* X, const void* W, const float* bias, void* Y,
-                               const void* mask, int B, int S, int KIN, int NOUT, int HO, int YC,
-                               int relu, int HM, hipStream_t stream) {
-  if (!rag_conv_wino_ok(S, 1, KIN, NOUT, 3) || YC < NOUT || B <= 0) return -1;
-  const int nb = wino_boards_per_block(S);
-  WgradRed r{};
-  const dim3 grid((B + nb - 1) / nb, NOUT / kWN);
-  const bf16 *x = (const bf16*)X, *w = (const bf16*)W, *mk = (const bf16*)mask;
-  bf16* y = (bf16*)Y;
-#define RAG_WD(D)                                                                              \
-  case D:                                                                                      \
-    conv_wino_kernel<D><<<grid, 512, 0, stream>>>(x, w, bias, y, mk, B, S, KIN, NOUT, HO, YC, \
-                                                  relu, HM, nb, r, stamps);                  \
-    break;
-  static long long* stamps = nullptr;
-  if ((diag & 64) && !stamps && hipMalloc(&stamps, 4096 * 8 * 6 * sizeof(long long)) != hipSuccess)
-    return -3;
-  if ((diag & 64) && grid.x > 4096) return -1;
-  g_wino_stamps = stamps;
-  switch (diag) {
-    RAG_WD(1) RAG_WD(2) RAG_WD(4) RAG_WD(8) RAG_WD(16) RAG_WD(32) RAG_WD(3) RAG_WD(7) RAG_WD(24)
-    RAG_WD(63) RAG_WD(64)
-    default: return -1;
-  }
-#undef RAG_WD
-  return (int)hipGetLastError();
 }
 
 // table: kWinoPackFields int64 per layer (W, COUT, CIN, COUTP, CINP, Uf, Ub or 0, 0).

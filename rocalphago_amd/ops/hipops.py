@@ -148,9 +148,10 @@ def conv_wino_ok(S, hi, kin, nout, ks):
 
 def wino_pack(table, nlayers, max_tiles):
     """Winograd weights of 3x3 layers from their fp32 OIHW masters in one launch. ``table``:
-    device int64 [nlayers, 8] = (W, cout, cin, coutp, cinp, Uf, Ub or 0, 0); Uf [12, coutp,
-    cinp] (forward), Ub [12, cinp, coutp] (dgrad); ``max_tiles``: 64x64 (n, c) tiles of the
-    widest layer."""
+    device int64 [nlayers, 8] = (W, cout, cin, coutp, cinp, Uf, Ub or 0, 0); Uf (forward, N =
+    coutp, K = cinp) and Ub (dgrad, N = cinp, K = coutp) each 12 * N * K bf16, stored
+    fragment-major [12][K/32][N/16][64][8] (conv_wino.hip); ``max_tiles``: 64x64 (n, c) tiles of
+    the widest layer."""
     _check(_lib().rag_wino_pack(_ptr(table), nlayers, int(max_tiles), _stream()), "wino_pack")
 
 

@@ -85,14 +85,20 @@ def test_wino_dgrad_with_mask_matches_autograd(ops, B, S, ho):
     assert rel_max(out, ref) < 2e-2
 
 
+def unfrag(u, N, K):
+    """Fragment-major [12][K/32][N/16][64 lanes][8] -> [12][N][K] (lane = n%16 + 16 (k%32)/8)."""
+    return u.reshape(12, K // 32, N // 16, 4, 16, 8).permute(0, 2, 4, 1, 3, 5).reshape(12, N, K)
+
+
 def test_wino_pack_layouts(ops):
     """Uf[ky*4+q] = G[q] . w[:, :, ky, :] and Ub the same of w[:, :, 2-ky, ::-1] transposed,
-    with zero padding past (cout, cin)."""
+    with zero padding past (cout, cin), both stored fragment-major."""
     dev = torch.device("cuda")
     torch.manual_seed(2)
     cout, cin, coutp, cinp = 150, 100, 192, 128
     w = torch.randn(cout, cin, 3, 3, device=dev)
     uf, ub = ops.wino_weights(w, coutp, cinp)
+    uf, ub = unfrag(uf, coutp, cinp), unfrag(ub, cinp, coutp)
     G = torch.tensor([[1, 0, 0], [.5, .5, .5], [.5, -.5, .5], [0, 0, 1]], device=dev)
     ref = torch.einsum("qk,ncyk->yqnc", G, w).reshape(12, cout, cin)
     assert torch.equal(uf[:, :cout, :cin].float(), bf(ref))
