@@ -2,6 +2,7 @@
 (+ ReLU mask), interleaved rounds in one process (guide §5.4 rule 24), on random data.
 
     python benchmarks/wino_bench.py [--batch 256] [--rounds 5] [--iters 40]
+                                    [--wcopies 16] [--xcopies 8]
 
 Prints one JSON line: median / min microseconds per launch of every (kernel, pass), the
 effective dense-equivalent TFLOP/s (2 * B * 361 * 192 * 1728 FLOP per launch, i.e. what the
@@ -22,11 +23,10 @@ def main(argv=None):
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=40)
     ap.add_argument("--size", type=int, default=19)
-    ap.add_argument("--diag", default="", help="comma list of conv_wino DIAG timing variants "
-                    "(wrong results): 1 no transform, 2 no raw staging, 4 no weight staging, "
-                    "8 no MFMAs, 16 no fragment reads, 32 no output stores")
-    ap.add_argument("--segments", action="store_true",
-                    help="s_memtime segment accounting of the Winograd loop (DIAG 64)")
+    ap.add_argument("--wcopies", type=int, default=1,
+                    help="rotate over this many copies of the weights (cold L2, as in the step)")
+    ap.add_argument("--xcopies", type=int, default=1,
+                    help="rotate over this many copies of the inputs (beyond the 256 MB MALL)")
     a = ap.parse_args(argv)
     from rocalphago_amd.ops import hipops as ops
     dev = torch.device("cuda")
@@ -35,27 +35,33 @@ def main(argv=None):
     x = torch.randn(B, C, S, S, device=dev).relu()
     w = torch.randn(C, C, 3, 3, device=dev) * 0.05
     g = torch.randn(B, C, S, S, device=dev)
-    xp = ops.pack_nchw(x, 1, C)
-    gp = ops.pack_nchw(g, 1, C)
+    xps = [ops.pack_nchw(x, 1, C) for _ in range(a.xcopies)]
+    gps = [ops.pack_nchw(g, 1, C) for _ in range(a.xcopies)]
+    xp, gp = xps[0], gps[0]
     wf, wb = ops.pack_weights(w, C, C, wb=torch.empty(9, C, C, dtype=torch.bfloat16, device=dev))
     uf, ub = ops.wino_weights(w, C, C)
+    wfs, wbs = [wf] + [wf.clone() for _ in range(a.wcopies - 1)], \
+        [wb] + [wb.clone() for _ in range(a.wcopies - 1)]
+    ufs, ubs = [uf] + [uf.clone() for _ in range(a.wcopies - 1)], \
+        [ub] + [ub.clone() for _ in range(a.wcopies - 1)]
     bias = torch.randn(C, device=dev) * 0.1
     y = {k: ops.alloc_padded(B, S, 1, C, dev) for k in ("fd", "fw", "dd", "dw")}
+    it = {}
+
+    def nxt(v):
+        i = it[id(v)] = it.get(id(v), -1) + 1
+        return v[i % len(v)]
+
     cases = {
-        "fwd_direct": lambda: ops.conv_igemm(xp, wf, bias, y["fd"], B, S, 1, 1, C, C, 3, True),
-        "fwd_wino": lambda: ops.conv_wino(xp, uf, bias, y["fw"], B, S, C, C, 1, True),
-        "dgrad_direct": lambda: ops.conv_igemm(gp, wb, None, y["dd"], B, S, 1, 1, C, C, 3,
-                                               False, mask=xp),
-        "dgrad_wino": lambda: ops.conv_wino(gp, ub, None, y["dw"], B, S, C, C, 1, False,
-                                            mask=xp),
+        "fwd_direct": lambda: ops.conv_igemm(nxt(xps), nxt(wfs), bias, y["fd"], B, S, 1, 1, C,
+                                             C, 3, True),
+        "fwd_wino": lambda: ops.conv_wino(nxt(xps), nxt(ufs), bias, y["fw"], B, S, C, C, 1,
+                                          True),
+        "dgrad_direct": lambda: ops.conv_igemm(nxt(gps), nxt(wbs), None, y["dd"], B, S, 1, 1, C,
+                                               C, 3, False, mask=xp),
+        "dgrad_wino": lambda: ops.conv_wino(nxt(gps), nxt(ubs), None, y["dw"], B, S, C, C, 1,
+                                            False, mask=xp),
     }
-    lib = ops._lib()
-    for d in [int(v) for v in a.diag.split(",") if v]:
-        yd = ops.alloc_padded(B, S, 1, C, dev)
-        cases["fwd_wino_diag%d" % d] = (
-            lambda d=d, yd=yd: lib.rag_conv_wino_diag(d, xp.data_ptr(), uf.data_ptr(),
-                                                      bias.data_ptr(), yd.data_ptr(), None, B, S,
-                                                      C, C, 1, C, 1, 1, ops._stream()))
     times = {k: [] for k in cases}
     s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for r in range(a.rounds):
@@ -80,22 +86,6 @@ def main(argv=None):
         p, q = ops.unpack(p, C, 1), ops.unpack(q, C, 1)
         return round(((p - q).norm() / q.norm()).item(), 5)
 
-    if a.segments:
-        import numpy as np
-        yd = ops.alloc_padded(B, S, 1, C, dev)
-        for _ in range(3):
-            rc = lib.rag_conv_wino_diag(64, xp.data_ptr(), uf.data_ptr(), bias.data_ptr(),
-                                        yd.data_ptr(), None, B, S, C, C, 1, C, 1, 1, ops._stream())
-            assert rc == 0, rc
-        nblk = B  # one board per block at 19x19
-        st = np.zeros((nblk, 8, 6), np.int64)
-        assert lib.rag_conv_wino_stamps(st.ctypes.data, nblk) == 0
-        steps = 6 * 2 * (C // 32)
-        out["segments_cycles_per_step"] = {
-            "group0 [Xwait, stage, read, Ywait, mfma, post]":
-                [round(float(v), 1) for v in st[:, 0:4].mean((0, 1)) / steps],
-            "group1 [Xwait, mfma, transform, Ywait, read, stage]":
-                [round(float(v), 1) for v in st[:, 4:8].mean((0, 1)) / steps]}
     out["fwd_rel_diff"] = rel(y["fw"], y["fd"])
     out["dgrad_rel_diff"] = rel(y["dw"], y["dd"])
     print(json.dumps(out))

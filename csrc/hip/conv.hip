@@ -1128,6 +1128,11 @@ __global__ void __launch_bounds__(256) pack_trunk_kernel(const int64_t* __restri
   const int g = (j / taps) * 8 + xcd;  // (n, c) tile
   const int tap = j % taps;
   if (g >= ntn * ntc) return;
+  if (!Wf && !Wb) {  // bias-only row (a Winograd layer: its weights come from rag_wino_pack)
+    if (bo && g == 0 && tap == 0)
+      for (int n = threadIdx.x; n < COUTP; n += blockDim.x) bo[n] = (b && n < COUT) ? b[n] : 0.f;
+    return;
+  }
   const int ct = g % ntc;
   const int nt = g / ntc;
   __shared__ float tl[64][65];
@@ -1138,7 +1143,7 @@ __global__ void __launch_bounds__(256) pack_trunk_kernel(const int64_t* __restri
     const int n = nt * 64 + nl, c = ct * 64 + tx;
     const float v = (n < COUT && c < CIN) ? W[(n * CIN + c) * taps + tap] : 0.f;
     tl[nl][tx] = v;
-    if (n < COUTP && c < CINP) Wf[(tap * COUTP + n) * CINP + c] = (bf16)v;
+    if (Wf && n < COUTP && c < CINP) Wf[(tap * COUTP + n) * CINP + c] = (bf16)v;
   }
   if (Wb) {
     __syncthreads();

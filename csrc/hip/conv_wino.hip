@@ -169,7 +169,10 @@ conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
   // branches hipcc's counter analysis fell back to `s_waitcnt vmcnt(0)`, so each transform
   // store and each set's first MFMA waited for every load in flight, the next step's weights
   // included.
-  bf16x8 da, db;
+  // two ops in flight (op o in register pair o & 1): an op's loads go out two MFMA blocks
+  // before its +- and store, ~0.5 us: the raw rows of a layer written by the previous launch
+  // come from HBM / MALL, and one block's distance cost up to 7 us per launch in the step
+  bf16x8 da0, db0, da1, db1;
   auto op_unit = [&](int o, int& v, int& k8, int& rr) {
     int pk = (o >> 1) ? tu1 : tu0;
     asm volatile("" : "+v"(pk));
@@ -180,25 +183,33 @@ conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
   };
   // P1: the V being built belongs to phase 1 (compile time: a runtime phase test put both
   // arithmetic paths and a join into the loop, and hipcc's counters and registers with them)
-  auto op_load = [&](auto p1c, int kk, int o) {  // kk may be NK (past the end): a dummy
+  auto op_load = [&](auto p1c, int kk, auto oc) {  // kk may be NK (past the end): a dummy
     constexpr bool P1 = decltype(p1c)::value;
+    constexpr int o = decltype(oc)::value, h = o & 1;
     int v, k8, rr;
     op_unit(o, v, k8, rr);
-    const int h = o & 1;
     const int ra = P1 ? 1 : (h ? 3 : 0), rb = P1 ? 2 : (h ? 1 : 2);
     const int so = (kk % cchunks) * kWK * 2;
     const uint32_t o0 = (uint32_t)((rr + ra) * KIN + k8 * 8) * 2u;
     const uint32_t o1 = (uint32_t)((rr + rb) * KIN + k8 * 8) * 2u;
-    da = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(xrs, o0, so, 0));
-    db = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(xrs, o1, so, 0));
+    const bf16x8 a = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(xrs, o0, so, 0));
+    const bf16x8 b = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(xrs, o1, so, 0));
+    if constexpr (h) {
+      da1 = a;
+      db1 = b;
+    } else {
+      da0 = a;
+      db0 = b;
+    }
   };
-  auto op_store = [&](auto p1c, int kk, int o) {  // branch-free: no unit -> the last V row
+  auto op_store = [&](auto p1c, int kk, auto oc) {  // branch-free: no unit -> the last V row
     constexpr bool P1 = decltype(p1c)::value;
+    constexpr int o = decltype(oc)::value, h = o & 1;
     int v, k8, rr;
     op_unit(o, v, k8, rr);
     v = v < 0 ? kVRows - 1 : v;
-    const int h = o & 1;
     bf16* vs = lds + (kk & 1) * 2 * kVSlot + h * kVSlot;
+    const bf16x8 da = h ? da1 : da0, db = h ? db1 : db0;
     const bf16x8 val = P1 ? (h ? vdiff(db, da) : vsum(da, db)) : vdiff(da, db);
     *reinterpret_cast<bf16x8*>(vs + v * kWK + ((k8 ^ swz4w(v)) * 8)) = val;
   };
@@ -237,17 +248,36 @@ conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
     }
   };
 
-  // ---- prologue: step (0, 0)'s weights, V(0)
+  // ---- prologue: this XCD's L2 warmed with the layer's weights (block x runs on XCD x % 8:
+  // its blocks each touch one slice; in the step every launch finds its weights cold, and the
+  // in-loop weight loads, one MFMA block ahead, then waited on HBM), step (0, 0)'s weights, V(0)
+  uint32_t warm = 0;
+  {
+    const int lin = blockIdx.y * gridDim.x + blockIdx.x;
+    const int per_xcd = (gridDim.x * gridDim.y + 7) >> 3;
+    const uint32_t slice = (uint32_t)((12L * NOUT * KIN * 2 + per_xcd - 1) / per_xcd);
+    const uint32_t base = (uint32_t)((lin >> 3) % per_xcd) * slice;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t off = (uint32_t)(threadIdx.x + k * 512) * 16u;
+      const uint32_t o = off < slice ? base + off : 0xfffffff0u;  // out of range: reads 0
+      warm ^= (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(urs, o, 0, 0);
+    }
+  }
 #pragma unroll
   for (int j = 0; j < kWNT; ++j) {
     wA[j] = wfrag(1, 0, j);
     wB[j] = wfrag(2, 0, j);
   }
-#pragma unroll
-  for (int o = 0; o < 4; ++o) {  // V(0) (phase 1)
-    op_load(IntC<1>{}, 0, o);
-    op_store(IntC<1>{}, 0, o);
-  }
+  op_load(IntC<1>{}, 0, IntC<0>{});  // V(0) (phase 1)
+  op_store(IntC<1>{}, 0, IntC<0>{});
+  op_load(IntC<1>{}, 0, IntC<1>{});
+  op_store(IntC<1>{}, 0, IntC<1>{});
+  op_load(IntC<1>{}, 0, IntC<2>{});
+  op_store(IntC<1>{}, 0, IntC<2>{});
+  op_load(IntC<1>{}, 0, IntC<3>{});
+  op_store(IntC<1>{}, 0, IntC<3>{});
+  asm volatile("" ::"v"(warm));  // (the warming loads are not dead)
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
@@ -268,12 +298,14 @@ conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
       }
       const int nc = nkk % cchunks;
       const int ntA = nky * 4 + (nxt1 ? 1 : 0), ntB = nky * 4 + (nxt1 ? 2 : 3);
-      // transform ops of V(kk + 1) in the six (ky, set) slots: slot t stores op t-1 and loads
-      // op t (loads in slots 0..3, stores in 1..4; in the last chunk-phase they fill the idle
+      // transform ops of V(kk + 1) in the six (ky, set) slots: slot t stores op t-2 and loads
+      // op t (loads in slots 0..3, stores in 2..5; in the last chunk-phase they fill the idle
       // buffer, read by nobody)
-      if (ky > 0) op_store(nxtc, kk + 1, 2 * ky - 1);
+      if (ky == 1) op_store(nxtc, kk + 1, IntC<0>{});
+      if (ky == 2) op_store(nxtc, kk + 1, IntC<2>{});
       __builtin_amdgcn_sched_barrier(0);
-      if (ky < 2) op_load(nxtc, kk + 1, 2 * ky);
+      if (ky == 0) op_load(nxtc, kk + 1, IntC<0>{});
+      if (ky == 1) op_load(nxtc, kk + 1, IntC<2>{});
       __builtin_amdgcn_sched_barrier(0);
       // ---- set A
 #pragma unroll
@@ -290,11 +322,11 @@ conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
       // (scheduling fences: hipcc otherwise reads set B's fragments into a second register set
       // while set A's MFMAs still hold the first, and the kernel spills)
       __builtin_amdgcn_sched_barrier(0);
-      if (ky < 2) {
-        op_store(nxtc, kk + 1, 2 * ky);
-        __builtin_amdgcn_sched_barrier(0);  // the old op's registers free before the new loads
-        op_load(nxtc, kk + 1, 2 * ky + 1);
-      }
+      if (ky == 1) op_store(nxtc, kk + 1, IntC<1>{});
+      if (ky == 2) op_store(nxtc, kk + 1, IntC<3>{});
+      __builtin_amdgcn_sched_barrier(0);  // the old op's registers free before the new loads
+      if (ky == 0) op_load(nxtc, kk + 1, IntC<1>{});
+      if (ky == 1) op_load(nxtc, kk + 1, IntC<3>{});
       __builtin_amdgcn_sched_barrier(0);
       // ---- set B
 #pragma unroll
@@ -466,6 +498,27 @@ int wino_boards_per_block(int S) {
 RAG_API int rag_conv_wino_ok(int S, int HI, int KIN, int NOUT, int KS) {
   return KS == 3 && HI == 1 && KIN % kWK == 0 && KIN >= kWK && NOUT % kWN == 0 && S >= 2 &&
          wino_boards_per_block(S) >= 1;
+}
+
+// True if conv_wino should take a layer of this batch rather than the direct kernel (given
+// rag_conv_wino_ok): one board per block (multi-board blocks of small boards are not measured
+// faster yet) and a grid of 512-thread blocks, one per CU, whose last wave fills at least 7/8 of
+// the CUs. The Winograd kernel's time is one fixed cost per wave (50.5 us at 19x19, 192 -> 192
+// on MI355X) against the direct kernel's per-pixel cost (57 us per 256 boards), so a ragged
+// last wave gives the gain back.
+RAG_API int rag_conv_wino_prefer(int B, int S, int KIN, int NOUT) {
+  if (!rag_conv_wino_ok(S, 1, KIN, NOUT, 3) || B <= 0 || wino_boards_per_block(S) != 1) return 0;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 0;
+    cus = n;
+  }
+  const long blocks = (long)B * (NOUT / kWN);
+  const long waves = (blocks + cus - 1) / cus;
+  return blocks * 8 >= waves * cus * 7;
 }
 
 // Winograd 3x3 conv (forward or dgrad): X [B][S+2][S+2][KIN] bf16, U the layer's fragment-major

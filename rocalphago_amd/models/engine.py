@@ -3,7 +3,10 @@
 A ``HipTrunk`` executes a sequential stack of 'same' convolutions (+bias, optional ReLU) on
 preallocated padded channels-last bf16 activations (layout: csrc/hip/conv.hip), with
 
-  * forward    : one implicit-GEMM MFMA launch per layer (bias + ReLU fused in the epilogue)
+  * forward    : one implicit-GEMM MFMA launch per layer (bias + ReLU fused in the epilogue);
+                 3x3 192 -> 192 layers at full-chip batches: the Winograd F(2,3) kernel
+                 (conv_wino.hip, 2/3 of the MFMA work) instead (and in dgrad when no deferred
+                 wgrad reduction rides in it)
   * backward   : per layer one wgrad launch (+ slab reduce) and one dgrad launch whose epilogue
                  applies the ReLU derivative of the layer below (so no separate mask pass)
   * weights    : fp32 OIHW master parameters (views of one flat buffer owned by the model) are
@@ -45,11 +48,20 @@ class _PackedConvs(object):
     """bf16 GEMM layouts (+ padded fp32 biases) of a list of convolutions, repacked from the fp32
     OIHW masters in one launch whenever the model's weight version changes."""
 
-    def _init_packing(self, specs, device):
+    def _init_packing(self, specs, device, wino=None):
         self._wf = [None] * len(specs)
         self._wb = [None] * len(specs)
         self._bias = [torch.zeros(s.coutp, device=device) for s in specs]
         self._packed_version = None
+        # Winograd layers (conv_wino.hip): their fragment-major forward Winograd weights are
+        # packed on every weight change, and either their dgrad Winograd weights (wino_dgrad) or
+        # the direct dgrad layout; the direct forward layout only when a batch the Winograd
+        # kernel does not take (conv_wino_prefer) needs it (_direct_layouts)
+        self._wino = list(wino) if wino is not None else [False] * len(specs)
+        self._uf = [None] * len(specs)
+        self._ub = [None] * len(specs)
+        self._direct_version = None
+        self.wino_dgrad = False
 
     def sync_weights(self, weights, biases, version):
         """Repack bf16 GEMM layouts from fp32 OIHW masters when ``version`` changed."""
@@ -62,25 +74,55 @@ class _PackedConvs(object):
                                           device=self.device)
                 self._wb[l] = torch.empty((taps, s.cinp, s.coutp), dtype=torch.bfloat16,
                                           device=self.device)
-        # one launch repacks all layers (GEMM layouts + padded biases); the pointer table is
-        # rebuilt only when a parameter tensor moved
+            if self._wino[l] and self._uf[l] is None:
+                self._uf[l] = torch.empty((12, s.coutp, s.cinp), dtype=torch.bfloat16,
+                                          device=self.device)
+                if self.wino_dgrad:
+                    self._ub[l] = torch.empty((12, s.cinp, s.coutp), dtype=torch.bfloat16,
+                                              device=self.device)
+        # one launch repacks all layers (GEMM layouts + padded biases; Winograd layers: bias
+        # only, their weights in one wino_pack launch); the pointer tables are rebuilt only when
+        # a parameter tensor moved
         ws = [w.contiguous() for w in weights]
         key = tuple(w.data_ptr() for w in ws) + \
             tuple(0 if b is None else b.data_ptr() for b in biases)
         if getattr(self, "_pack_key", None) != key:
-            rows, start = [], 0
+            rows, drows, wrows, start = [], [], [], 0
             for l, s in enumerate(self.specs):
                 b = biases[l]
-                rows.append([ws[l].data_ptr(), 0 if b is None else b.data_ptr(), s.cout, s.cin,
-                             s.ks, s.coutp, s.cinp, self._wf[l].data_ptr(),
-                             self._wb[l].data_ptr(), self._bias[l].data_ptr(), start])
+                row = [ws[l].data_ptr(), 0 if b is None else b.data_ptr(), s.cout, s.cin, s.ks,
+                       s.coutp, s.cinp, self._wf[l].data_ptr(), self._wb[l].data_ptr(),
+                       self._bias[l].data_ptr(), start]
                 start += s.ks * s.ks * s.coutp * s.cinp + s.coutp
+                if self._wino[l]:
+                    drows.append(row)
+                    ub = self._ub[l].data_ptr() if self.wino_dgrad else 0
+                    wrows.append([ws[l].data_ptr(), s.cout, s.cin, s.coutp, s.cinp,
+                                  self._uf[l].data_ptr(), ub, 0])
+                    # the direct dgrad layout unless the dgrad runs Winograd too
+                    row = row[:7] + [0, 0 if self.wino_dgrad else row[8]] + row[9:]
+                rows.append(row)
             self._pack_table = torch.tensor(rows, dtype=torch.int64).to(self.device)
             self._pack_total = pack_grid_width(self.specs)
+            wsp = [s for l, s in enumerate(self.specs) if self._wino[l]]
+            if wsp:
+                self._dpack_table = torch.tensor(drows, dtype=torch.int64).to(self.device)
+                self._dpack_total = pack_grid_width(wsp)
+                self._wpack_table = torch.tensor(wrows, dtype=torch.int64).to(self.device)
+                self._wpack_tiles = max(-(-s.coutp // 64) * -(-s.cinp // 64) for s in wsp)
             self._pack_key = key
             self._pack_keep = ws  # keep contiguous copies alive while the table points at them
         ops.pack_trunk(self._pack_table, len(self.specs), self._pack_total)
+        if any(self._wino):
+            ops.wino_pack(self._wpack_table, sum(self._wino), self._wpack_tiles)
         self._packed_version = version
+
+    def _direct_layouts(self):
+        """Direct GEMM layouts of the Winograd layers, for a batch that runs them on the direct
+        kernel: packed once per weight version, on first use."""
+        if self._direct_version != self._packed_version:
+            ops.pack_trunk(self._dpack_table, sum(self._wino), self._dpack_total)
+            self._direct_version = self._packed_version
 
 
 class HipTrunk(_PackedConvs):
@@ -95,11 +137,23 @@ class HipTrunk(_PackedConvs):
         self._B = 0
         self.acts = []
         self._gbufs = {}
-        self._init_packing(specs, device)
+        # 3x3 192 -> 192 layers run the Winograd F(2,3) kernel (conv_wino.hip) forward at
+        # batches that fill its grid (RAG_WINO=0: direct kernel only)
+        wino_on = device.type == "cuda" and os.environ.get("RAG_WINO", "1") != "0"
+        wino = [wino_on and s.ks == 3 and ops.conv_wino_ok(board, 1, s.cinp, s.coutp, 3)
+                and ops.conv_wino_ok(board, 1, s.coutp, s.cinp, 3) for s in specs]
+        self._init_packing(specs, device, wino)
+        self._wino_plans = {}
         self._work = None
         self._rstream = None
         # wgrad slab reductions ride along the next dgrad launch (RAG_WGRAD_DEFER=0: own kernels)
         self.defer_reduce = os.environ.get("RAG_WGRAD_DEFER", "1") != "0"
+        # The dgrad of a Winograd layer runs the direct kernel while it carries a deferred
+        # reduction: the Winograd grid is exactly one wave of blocks (one per CU), so the
+        # reduction's ~28 MB of partial slabs stream after every block's epilogue (+6-8 us in
+        # the step), while the direct kernel's ragged last wave absorbs them (+1-2 us); without
+        # deferral (own reduce kernels, or the reduce stream) the dgrad runs Winograd as well.
+        self.wino_dgrad = not self.defer_reduce or os.environ.get("RAG_WGRAD_OVERLAP") == "1"
         self._pending = ops.PendingReduction() if device.type == "cuda" else None
 
     # ------------------------------------------------------------------ buffers
@@ -171,12 +225,28 @@ class HipTrunk(_PackedConvs):
         """Where the head writes dL/d(trunk output) (ReLU-masked if top_relu)."""
         return self.grad_buffer(self.L - 1, 0, B)
 
+    def wino_plan(self, B):
+        """Per layer: True if it runs the Winograd kernel at batch B (forward and dgrad)."""
+        plan = self._wino_plans.get(B)
+        if plan is None:
+            plan = [w and ops.conv_wino_prefer(B, self.S, s.cinp, s.coutp)
+                    for w, s in zip(self._wino, self.specs)]
+            self._wino_plans[B] = plan
+        if any(w and not p for w, p in zip(self._wino, plan)):
+            self._direct_layouts()
+        return plan
+
     def forward(self, B, training=False):
         S = self.S
+        wino = self.wino_plan(B)
         for l, s in enumerate(self.specs):
             x, y = self.acts[l][:B], self.acts[l + 1][:B]
-            ops.conv_igemm(x, self._wf[l], self._bias[l], y, B, S, self.halo[l],
-                           self.halo[l + 1], s.cinp, s.coutp, s.ks, s.relu, cin=s.cin)
+            if wino[l]:
+                ops.conv_wino(x, self._uf[l], self._bias[l], y, B, S, s.cinp, s.coutp,
+                              self.halo[l + 1], s.relu)
+            else:
+                ops.conv_igemm(x, self._wf[l], self._bias[l], y, B, S, self.halo[l],
+                               self.halo[l + 1], s.cinp, s.coutp, s.ks, s.relu, cin=s.cin)
         return self.acts[-1][:B]
 
     def backward(self, B, dws, dbs, top_which=0, accumulate=False, on_layer_done=None):
@@ -185,6 +255,7 @@ class HipTrunk(_PackedConvs):
         ``on_layer_done(l)`` fires right after layer l's wgrad is queued (DP bucket overlap)."""
         S = self.S
         which = top_which
+        wino = self.wino_plan(B)
         main = torch.cuda.current_stream(self.device)
         rs = self._rstream
         for i, l in enumerate(range(self.L - 1, -1, -1)):
@@ -210,10 +281,16 @@ class HipTrunk(_PackedConvs):
                 below = self.specs[l - 1]
                 which ^= 1
                 gout = self.grad_buffer(l - 1, which, B)
-                ops.conv_igemm(g, self._wb[l], None, gout, B, S, self.halo[l],
-                               self.halo[l - 1], s.coutp, s.cinp, s.ks, False,
-                               mask=x if below.relu else None, mask_halo=self.halo[l],
-                               pending=self._pending if defer else None)
+                if wino[l] and self.wino_dgrad:
+                    ops.conv_wino(g, self._ub[l], None, gout, B, S, s.coutp, s.cinp,
+                                  self.halo[l - 1], False, mask=x if below.relu else None,
+                                  mask_halo=self.halo[l],
+                                  pending=self._pending if defer else None)
+                else:
+                    ops.conv_igemm(g, self._wb[l], None, gout, B, S, self.halo[l],
+                                   self.halo[l - 1], s.coutp, s.cinp, s.ks, False,
+                                   mask=x if below.relu else None, mask_halo=self.halo[l],
+                                   pending=self._pending if defer else None)
             elif defer:
                 ops.wgrad_flush(self._pending)
             if on_layer_done is not None:

@@ -146,6 +146,12 @@ def conv_wino_ok(S, hi, kin, nout, ks):
     return bool(_lib().rag_conv_wino_ok(S, hi, kin, nout, ks))
 
 
+def conv_wino_prefer(B, S, kin, nout):
+    """True if conv_wino should take this layer at batch B rather than the direct kernel: one
+    board per block and a last wave of blocks that fills at least 7/8 of the CUs."""
+    return bool(_lib().rag_conv_wino_prefer(B, S, kin, nout))
+
+
 def wino_pack(table, nlayers, max_tiles):
     """Winograd weights of 3x3 layers from their fp32 OIHW masters in one launch. ``table``:
     device int64 [nlayers, 8] = (W, cout, cin, coutp, cinp, Uf, Ub or 0, 0); Uf (forward, N =

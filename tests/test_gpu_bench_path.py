@@ -59,16 +59,62 @@ class _Inject(torch.autograd.Function):
         return (_bf(g) if ctx.store_bf16 else g), None, None
 
 
-def _trunk_ref(x, Ws, bs, acts=None, store_bf16=True):
+def _wino_corr(x, w):
+    """3x3 'same' correlation of x [B, C, H, W] with w [N, C, 3, 3] computed the way
+    conv_wino.hip does: Winograd F(2,3) along the width, the transformed inputs
+    V = (d0 - d2, d1 + d2, d2 - d1, d1 - d3) and weights U = (g0, (g0+g1+g2)/2, (g0-g1+g2)/2, g2)
+    each rounded to bf16 once (U from the fp32 masters), then fp32 products and sums."""
+    B, C, H, W = x.shape
+    T = (W + 1) // 2
+    xp = F.pad(x, (1, 2 * T + 1 - W, 1, 1))
+    d = [xp[..., k:k + 2 * T:2] for k in range(4)]
+    V = [_bf(d[0] - d[2]), _bf(d[1] + d[2]), _bf(d[2] - d[1]), _bf(d[1] - d[3])]
+    g0, g1, g2 = w[..., 0], w[..., 1], w[..., 2]
+    U = [_bf(g0), _bf((g0 + g1 + g2) / 2), _bf((g0 - g1 + g2) / 2), _bf(g2)]
+    M = [F.conv2d(V[q], U[q].unsqueeze(-1)) for q in range(4)]
+    y = torch.stack([M[0] + M[1] + M[2], M[1] - M[2] - M[3]], -1)
+    return y.reshape(B, -1, H, 2 * T)[..., :W]
+
+
+class _WinoConv(torch.autograd.Function):
+    """3x3 conv on bf16 weights whose forward (``fwd``) and / or input gradient (``dgrad``: with
+    the flipped, transposed weights) are computed the Winograd way (_wino_corr); weight / bias
+    gradients plain fp32."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, fwd, dgrad):
+        ctx.save_for_backward(x, W)
+        ctx.dgrad = dgrad
+        if fwd:
+            return _wino_corr(x, W) + b.view(1, -1, 1, 1)
+        return F.conv2d(x, _bf(W), b, padding=1)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, W = ctx.saved_tensors
+        if ctx.dgrad:
+            gx = _wino_corr(g, W.flip(2, 3).transpose(0, 1))
+        else:
+            gx = torch.nn.grad.conv2d_input(x.shape, _bf(W), g, padding=1)
+        gw = torch.nn.grad.conv2d_weight(x, W.shape, g, padding=1)
+        return gx, gw, g.sum((0, 2, 3)), None, None
+
+
+def _trunk_ref(x, Ws, bs, acts=None, store_bf16=True, wino=None):
     """fp32 trunk on bf16-rounded weights and layer inputs (autograd through the roundings is
     the identity: straight-through). ``acts``: the kernels' stored activations per layer
     (NCHW fp32), injected as each layer's output — the backward is then fp32 autograd of the
-    exact forward point the kernels differentiated."""
+    exact forward point the kernels differentiated. ``wino``: (forward, dgrad) per-layer flags
+    of the layers the trunk ran through conv_wino.hip, computed the Winograd way here (the
+    forward only without ``acts``)."""
     h = x
     for l, (W, b) in enumerate(zip(Ws, bs)):
         hin = h + (_bf(h) - h).detach()
         Wq = W + (_bf(W) - W).detach()
-        pre = F.conv2d(hin, Wq, b, padding=W.shape[-1] // 2)
+        if wino is not None and (wino[0][l] or wino[1][l]):
+            pre = _WinoConv.apply(hin, W, b, acts is None and wino[0][l], wino[1][l])
+        else:
+            pre = F.conv2d(hin, Wq, b, padding=W.shape[-1] // 2)
         h = F.relu(pre) if acts is None else _Inject.apply(pre, acts[l], store_bf16)
     return h + (_bf(h) - h).detach()
 
@@ -81,25 +127,35 @@ def _gpu_acts(plan, B):
     return out
 
 
-@pytest.mark.parametrize("augment", [False, True])
-def test_north_star_sl_step_matches_fp32(cuda, augment):
+@pytest.mark.parametrize("augment,defer", [(False, True), (True, True), (False, False)])
+def test_north_star_sl_step_matches_fp32(cuda, augment, defer, monkeypatch):
     """Gradients of one bench-path step vs fp32 autograd, two references:
     (a) fp32 autograd at the kernels' own forward point (their stored bf16 activations injected
         as each layer's output, ReLU masks from them, dL/d(pre-activation) rounded to bf16 where
         the kernels store it) — pins the whole backward arithmetic: head, dgrad, fp32
         accumulation, fp16 block-scaled partial slabs reduced inside the next dgrad launch.
-        Every tensor within 2e-2. Without the bf16 storage rounding the top layer's bias
-        gradient (a sum that cancels to a few % of its terms at init) differs by ~5 %.
-    (b) an independent fp32 forward + backward (bf16-rounded weights / layer inputs) — within
-        0.25. Its forward activations differ from the kernels' by 0.2-0.6 % (accumulation order
+        Every tensor within 2e-2; Winograd dgrads (when the trunk runs them) are computed as
+        conv_wino.hip computes them (bf16 V and U, _wino_corr). Without the bf16 storage
+        rounding the top layer's bias gradient (a sum that cancels to a few % of its terms at
+        init) differs by ~5 %, and without the Winograd roundings the top layers' weight
+        gradients by ~3.6 % (same cancellation: ~0.35 % noise in g, amplified ~10x).
+    (b) an independent fp32 forward + backward (bf16-rounded weights / layer inputs) with the
+        Winograd layers' forward (and dgrad) rounded as the kernels round them — within 0.25. Its forward activations differ from the kernels' by 0.2-0.6 % (accumulation order
         changes bf16 roundings, scripts/dbg/bench_path_err.py), and at random init the 12-layer
         trunk's activations are nearly constant over the board, so the gradient
         sum_p x(p) (p(p) - y(p)) cancels to a few % of its terms and amplifies that into ~12 %
         per tensor (3 layers: 1-4 %; identical with fp32 partial slabs and without deferred
         reductions, i.e. not a kernel error).
+    (c) the same with plain direct-convolution arithmetic everywhere — within 0.4: the Winograd
+        roundings (bf16 V and U, ~0.3 % relative per layer against ~0.2 % for the direct kernel)
+        go through the same amplification (0.28 measured on MI355X with Winograd dgrads too).
     ``augment``: the bench's random dihedral augmentation (all 8 transforms, drawn by the
     sl_batch kernel and applied while packing the input) -- the reference applies the same
-    per-sample transforms to the planes and the targets with numpy."""
+    per-sample transforms to the planes and the targets with numpy. ``defer=False``
+    (RAG_WGRAD_DEFER=0): the wgrad reductions run as their own launches and the dgrads of the
+    Winograd layers run Winograd too."""
+    if not defer:
+        monkeypatch.setenv("RAG_WGRAD_DEFER", "0")
     torch.backends.cudnn.allow_tf32 = False
     torch.backends.cuda.matmul.allow_tf32 = False
     pol = CNNPolicy(DEFAULT_FEATURES, board=19, filters_per_layer=192, layers=12, device=cuda,
@@ -135,13 +191,22 @@ def test_north_star_sl_step_matches_fp32(cuda, augment):
         assert len(set(tfs.tolist())) == 8  # every transform drawn in a batch of 256
     x = torch.from_numpy(np.stack([apply_transform_np(xs[b], int(tfs[b]))
                                    for b in range(256)]).astype(np.float32)).to(cuda)
-    cases = (("kernels' forward point, bf16-stored grads", True, True, 2e-2),
-             ("kernels' forward point, fp32 grads", True, False, 0.1),
-             ("independent fp32", False, False, 0.25))
-    for label, inject, store, bound in cases:
+    # the 3x3 192 -> 192 layers run forward (and dgrad, unless it carries a deferred wgrad
+    # reduction) through the Winograd kernel at B = 256; references (a) and (b) compute them the
+    # same way (_wino_corr), the others do not
+    wf = plan.trunk.wino_plan(256)
+    assert wf == [False] + [True] * 11
+    assert plan.trunk.wino_dgrad == (not defer)
+    wino = (wf, [w and plan.trunk.wino_dgrad for w in wf])
+    cases = (("kernels' forward point, bf16-stored grads", True, True, True, 2e-2),
+             ("kernels' forward point, fp32 grads", True, False, False, 0.1),
+             ("independent fp32, Winograd roundings", False, False, True, 0.25),
+             ("independent fp32, direct arithmetic", False, False, False, 0.4))
+    for label, inject, store, wi, bound in cases:
         leaf = {n: [p.clone().requires_grad_(True) for p in ps] for n, ps in params.items()}
         h = _trunk_ref(x, [leaf[n][0] for n in plan.conv_names],
-                       [leaf[n][1] for n in plan.conv_names], acts if inject else None, store)
+                       [leaf[n][1] for n in plan.conv_names], acts if inject else None, store,
+                       wino if wi else None)
         hw, hb = leaf[plan.head_name]
         z = F.conv2d(h, hw, hb).reshape(256, -1) + leaf[plan.bias_name][0]
         loss = F.cross_entropy(z, labels)

@@ -455,6 +455,15 @@ def test_trunk_repack_matches_per_layer_packer(ops):
     ws = [torch.randn(s.cout, s.cin, s.ks, s.ks, device=dev) for s in specs]
     bs = [torch.randn(s.cout, device=dev) for s in specs]
     tr.sync_weights(ws, bs, 1)
+    # the 192 -> 192 layer is a Winograd layer: its fragment-major Winograd weights come with
+    # every repack (and its direct dgrad layout while the dgrad carries deferred reductions),
+    # its direct forward layout on first demand
+    assert tr._wino == [False, True, False, False, False]
+    for l in (1,):
+        uf, ub = ops.wino_weights(ws[l], 192, 192)
+        assert torch.equal(tr._uf[l], uf)
+        assert (tr._ub[l] is None) if not tr.wino_dgrad else torch.equal(tr._ub[l], ub)
+    tr._direct_layouts()
     torch.cuda.synchronize()
     for l, s in enumerate(specs):
         wb = torch.empty(s.ks * s.ks, s.cinp, s.coutp, dtype=torch.bfloat16, device=dev)

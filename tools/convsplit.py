@@ -1,5 +1,6 @@
 """Split a rocprofv3 kernel-trace (.db) of the SL step into 3x3 forward / dgrad / 5x5 conv and
-wgrad launch averages (forward = conv launches before the step's first wgrad launch).
+wgrad launch averages (forward = conv launches before the step's first wgrad launch; direct
+conv_tap_pp and Winograd conv_wino launches alike).
 
     python tools/convsplit.py gpurun_out/<job>/trace-sl/sl_results.db [...]
 """
@@ -21,6 +22,9 @@ def split(path):
             state = 'b'
             wg.append(d)
             continue
+        if 'conv_wino_kernel' in n:
+            (fw if state == 'f' else dg).append(d)
+            continue
         m = re.search(r'conv_tap_pp_kernel<([^>]*)>', n)
         if not m:
             continue
@@ -31,8 +35,10 @@ def split(path):
             continue
         (fw if state == 'f' else dg).append(d)
     mean = lambda v: st.mean(v) if v else float('nan')
-    return ("fwd3x3 %.2f us (n=%d)  dgrad %.2f us (n=%d)  5x5 %.2f us  wgrad %.2f us (n=%d)"
-            % (mean(fw), len(fw), mean(dg), len(dg), mean(f5), mean(wg), len(wg)))
+    med = lambda v: st.median(v) if v else float('nan')
+    return ("fwd3x3 %.2f us (median %.2f, n=%d)  dgrad %.2f us (median %.2f, n=%d)  5x5 %.2f us"
+            "  wgrad %.2f us (n=%d)" % (mean(fw), med(fw), len(fw), mean(dg), med(dg), len(dg),
+                                       mean(f5), mean(wg), len(wg)))
 
 
 if __name__ == "__main__":
