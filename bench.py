@@ -52,7 +52,7 @@ def allreduce_probe(dp, dev, nbytes=15531176, reps=10):
     dt = (time.perf_counter() - t0) / reps
     ok = bool(torch.all(buf == float(dp.world) ** (reps + 2)).item())
     n = dp.world
-    return {"rccl_ranks": n, "comm_backend": dp.backend,
+    return {"comm_ranks": n, "comm_backend": dp.backend,
             "allreduce_bytes": nbytes, "allreduce_us": round(dt * 1e6, 1),
             "allreduce_algbw_GBps": round(nbytes / dt / 1e9, 2),
             "allreduce_busbw_GBps": round(2.0 * (n - 1) / n * nbytes / dt / 1e9, 2),
@@ -326,6 +326,15 @@ def main():
                                         else "1 GPU")
             if dp.is_root and "leaves_per_rank" in r:
                 result["mcts_leaves_per_rank"] = r["leaves_per_rank"]
+            if dp.is_root and dp.world > 1:
+                # rank 0's host split of the N-GPU search (fractions of its wall time) and the
+                # mean round time: the diagnosis of a scale run, not just its rate
+                for k, v in r.items():
+                    if k.startswith("t_") and k.endswith("_frac"):
+                        result["mcts_" + k] = v
+                for k in ("rounds", "round_ms"):
+                    if k in r:
+                        result["mcts_" + k] = r[k]
             if dp.is_root and dp.world > 1:
                 # over-crediting guard: simulations of one tree are all distinct; with N
                 # independent trees (mode shared) the duplicated expansions are measured live

@@ -122,8 +122,12 @@ def measure_distributed(dp, device, playouts=8192, warmup=512, moves=1, filters=
            "mode": "master", "duplication": 1.0, "leaves_per_round": batch * dp.world}
     if lmbda > 0:
         out["rollouts_per_s"] = s["sims"] * rollouts_per_leaf / dt
-    for k in ("t_select", "t_eval", "t_backup"):
+    # rank 0's round split (search/distributed.py DistributedMCTS.search)
+    for k in ("t_select", "t_pack", "t_ship", "t_gather", "t_backup", "t_eval"):
         out[k + "_frac"] = round(s.get(k, 0.0) / dt, 3)
+    if s.get("rounds"):
+        out["rounds"] = int(s["rounds"])
+        out["round_ms"] = round(dt / s["rounds"] * 1e3, 3)
     return out
 
 

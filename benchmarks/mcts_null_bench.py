@@ -6,6 +6,8 @@ board construction, leaf packing, expansion and backup) can sustain. No GPU is u
   python benchmarks/mcts_null_bench.py [--playouts 65536] [--batch 512] [--threads 16]
   python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \
       benchmarks/mcts_null_bench.py --distributed --threads 4
+  python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
+      benchmarks/mcts_null_bench.py --distributed --mode master --batch 128 --threads 2
 
 Single process: one JSON line with sims/s and the per-phase split (select, pack, eval = the
 null evaluator itself, backup). ``--distributed`` (gloo, CPU): the shared-root multi-rank search
@@ -45,6 +47,8 @@ class NullEvaluator(object):
     def _plans(self):
         return None
 
+    delay = 0.0  # seconds per call: a stand-in for the GPU pass of a wave (--eval-ms)
+
     def sensible(self, boards):
         sfid = [self.rg.FEATURE_IDS["sensibleness"]] if hasattr(self.rg, "FEATURE_IDS") else [9]
         return self.rg.batch_features(boards, sfid, self.nthreads).reshape(len(boards), -1)
@@ -54,6 +58,10 @@ class NullEvaluator(object):
         n = len(boards)
         pri = np.broadcast_to(self.prior_row, (n, self.P))
         sens = self.sensible(boards)
+        if self.delay > 0:
+            rest = self.delay - (time.perf_counter() - t)
+            if rest > 0:
+                time.sleep(rest)
         self.t_eval += time.perf_counter() - t
         return np.ascontiguousarray(pri), np.zeros(n, np.float32), sens
 
@@ -150,6 +158,71 @@ def run_distributed(args):
         dp.shutdown()
 
 
+class NullRollout(object):
+    """Rollout policy stand-in: every game a draw (z = 0), returned at once."""
+
+    def rollouts(self, boards, seed=0, limit=500, nthreads=1):
+        return np.zeros(len(boards), np.int32)
+
+
+def run_master(args):
+    """DistributedMCTS master mode (search/distributed.py, the multi-GPU bench's search) with
+    the null evaluator and null rollouts on every rank: ONE tree on rank 0, each round's waves of
+    ``--batch`` leaves scattered to the ranks as records, rebuilt there, "evaluated" and
+    all-gathered back. Rank 0's sims/s is the host ceiling of the N-GPU search; its split
+    (select / pack / ship / gather / backup fractions of its wall time) says what bounds it.
+    ``--eval-ms``: a fixed per-wave evaluation time on every rank (the GPU pass it stands for).
+    gloo on CPU (torchrun, 127.0.0.1)."""
+    import torch
+    from rocalphago_amd.engine.gamestate import GameState
+    from rocalphago_amd.parallel.dp import DPContext
+    from rocalphago_amd.search.distributed import DistributedMCTS
+    dp = DPContext(device="cpu", backend="gloo")
+    # rank 0 owns the tree: on a real node every rank has its own cores, so the master may get
+    # more host threads than the evaluating ranks (--threads-master)
+    nt = args.threads_master if dp.rank == 0 and args.threads_master else args.threads
+    ev = NullEvaluator(nthreads=nt, seed=dp.rank)
+    ev.delay = args.eval_ms * 1e-3
+    mc = DistributedMCTS(None, value=True, evaluator=ev, dp=dp, lmbda=args.lmbda,
+                         batch=args.batch, nthreads=nt,
+                         rollout_delay=args.rollout_delay, force_master=True)
+    mc.leaf_eval.rollout = NullRollout()  # the ranks' rollouts (the tree keeps its policy)
+    st = GameState()
+    mc.n_playout = 4 * args.batch * dp.world
+    mc.get_move(st)  # warm-up (arenas, pools); a fresh tree below
+    mc._search = None
+    mc.stats = {"waves": 0, "sims": 0}
+    mc.rank_leaves = 0
+    mc.n_playout = args.playouts
+    dp.barrier()
+    t0 = time.perf_counter()
+    mc.get_move(st)
+    dt = time.perf_counter() - t0
+    if dp.rank == 0:
+        s = mc.stats
+        out = {"metric": "DistributedMCTS master-mode host ceiling (null evaluator + rollouts, "
+                         "gloo), 19x19",
+               "ranks": dp.world, "threads_rank0": nt, "threads_per_rank": args.threads,
+               "batch_per_rank": args.batch,
+               "lmbda": args.lmbda, "rollout_delay": args.rollout_delay,
+               "eval_ms_per_wave": args.eval_ms, "sims": int(s["sims"]),
+               "seconds": round(dt, 3), "sims_per_s": round(s["sims"] / dt, 1),
+               "rounds": int(s.get("rounds", 0)),
+               "round_ms": round(dt / max(1, s.get("rounds", 0)) * 1e3, 3),
+               "us_per_sim": {k[2:]: round(s.get(k, 0.0) / max(1, s["sims"]) * 1e6, 3)
+                              for k in ("t_select", "t_pack", "t_ship", "t_gather",
+                                        "t_backup")},
+               "frac": {k[2:]: round(s.get(k, 0.0) / dt, 3)
+                        for k in ("t_select", "t_pack", "t_ship", "t_gather", "t_backup")},
+               "leaves_per_rank": [int(c) for c in mc.leaf_counts()]}
+        print(json.dumps(out), flush=True)
+    else:
+        mc.leaf_counts()
+    _ = torch
+    if dp.enabled:
+        dp.shutdown()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--playouts", type=int, default=65536)
@@ -158,7 +231,17 @@ def main():
     ap.add_argument("--lmbda", type=float, default=0.5)
     ap.add_argument("--pack", type=int, default=1, help="also build the GPU input arrays")
     ap.add_argument("--distributed", action="store_true")
+    ap.add_argument("--mode", default="shared", choices=("shared", "master"),
+                    help="--distributed: shared-root trees or the one-tree master search")
+    ap.add_argument("--eval-ms", type=float, default=0.0,
+                    help="master: fixed evaluation time per wave and rank")
+    ap.add_argument("--rollout-delay", type=int, default=6)
+    ap.add_argument("--threads-master", type=int, default=0,
+                    help="master: rank 0's host threads (default --threads)")
     args = ap.parse_args()
+    if args.distributed and args.mode == "master":
+        run_master(args)
+        return
     if args.distributed:
         run_distributed(args)
         return

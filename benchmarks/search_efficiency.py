@@ -3,6 +3,8 @@
 playouts, over many positions. One JSON line per search design.
 
   python benchmarks/search_efficiency.py [--ranks 2 4 8] [--positions 50] [--per-rank 128]
+  python benchmarks/search_efficiency.py --designs DistributedMCTS/shipped --per-rank 512 \
+      --lmbda 0.5 --rollout-delay 6 --truth-mult 16     (the bench's geometry)
 """
 import argparse
 import json
@@ -22,13 +24,21 @@ def main():
     ap.add_argument("--designs", nargs="+",
                     default=["SharedRootMCTS", "DistributedMCTS", "DistributedMCTS/split"])
     ap.add_argument("--out", default="/tmp/rag_search_eff")
+    ap.add_argument("--lmbda", type=float, default=0.0,
+                    help="0.5: rollouts mixed in as the bench's search does")
+    ap.add_argument("--rollout-delay", type=int, default=0)
+    ap.add_argument("--truth-mult", type=int, default=4)
     args = ap.parse_args()
     from rocalphago_amd.search.efficiency import study
     for d in args.designs:
+        # design suffixes: /split (per-rank wave = wave / N), /shipped (the bench's geometry:
+        # efficiency.shipped_waves)
         cls, _, opt = d.partition("/")
         r = study(worlds=tuple(args.ranks), per_rank=args.per_rank, batch=args.wave,
                   n_positions=args.positions, size=args.board, search_cls=cls,
-                  outdir=os.path.join(args.out, d.replace("/", "_")), split_wave=opt == "split")
+                  outdir=os.path.join(args.out, d.replace("/", "_")), split_wave=opt == "split",
+                  shipped=opt == "shipped", lmbda=args.lmbda, rollout_delay=args.rollout_delay,
+                  truth_mult=args.truth_mult)
         r["design"] = d
         print(json.dumps(r), flush=True)
 

@@ -29,6 +29,13 @@ enum RolloutFeature : int {
 };
 constexpr int RP_PATTERNS = 1 << 16;
 
+// Seed of a position-keyed rollout: a function of the stones and the player to move only, so
+// every search that reaches a position plays the same rollout from it (search/efficiency.py
+// compares search designs with such rollouts: the only difference left is the tree's shape).
+inline uint64_t position_key_seed(uint64_t hash, int player) {
+  return hash * 0xD6E8FEB86659FD93ull ^ (uint64_t)(player + 2) * 0xA0761D6478BD642Full;
+}
+
 struct Rng {
   uint64_t s;
   explicit Rng(uint64_t seed) : s(seed * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull) {}

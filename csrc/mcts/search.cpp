@@ -28,6 +28,7 @@ void register_search(py::module_& m) {
       .def_readwrite("rollout_limit", &Search::rollout_limit)
       .def_readwrite("max_depth", &Search::max_depth)
       .def_readwrite("seed", &Search::seed)
+      .def_readwrite("keyed_rollouts", &Search::keyed_rollouts)
       .def_property_readonly("nthreads", &Search::nthreads)
       .def("set_rollout_policy",
            [](Search& s, std::shared_ptr<RolloutPolicy> p) { s.rollout_policy = p; })
@@ -217,7 +218,7 @@ void register_rollout(py::module_& m) {
            py::arg("board"), py::arg("seed") = 1, py::arg("limit") = 500)
       .def("rollouts",
            [](const RolloutPolicy& p, const std::vector<const Board*>& boards, uint64_t seed,
-              int limit, int nthreads) {
+              int limit, int nthreads, bool keyed) {
              const int n = (int)boards.size();
              py::array_t<int8_t> out(n);
              int8_t* o = out.mutable_data();
@@ -226,14 +227,17 @@ void register_rollout(py::module_& m) {
                shared_pool(std::max(1, std::min(nthreads, 64))).run(n, [&](int i) {
                  Board c = *boards[i];
                  c.set_enforce_superko(false);
-                 Rng rng(seed + (uint64_t)i * 7919ull);
+                 Rng rng(keyed ? position_key_seed(c.hash(), c.current_player())
+                               : seed + (uint64_t)i * 7919ull);
                  o[i] = (int8_t)p.rollout(c, rng, limit);
                });
              }
              return out;
            },
            py::arg("boards"), py::arg("seed") = 1, py::arg("limit") = 500,
-           py::arg("nthreads") = 8);
+           py::arg("nthreads") = 8, py::arg("keyed") = false,
+           "Winner of one rollout per board; keyed: seeded by the board's position "
+           "(position_key_seed) instead of seed and index");
   m.attr("ROLLOUT_FEATURES") = py::int_((int)RF_COUNT);
   m.attr("ROLLOUT_PATTERNS") = py::int_((int)RP_PATTERNS);
 }

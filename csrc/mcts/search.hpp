@@ -274,6 +274,7 @@ class Search {
   // expanded node also gets a PASS child with the network's pass prior
   bool pass_prior = false;
   uint64_t seed = 1;
+  bool keyed_rollouts = false;  // CPU rollouts seeded by the leaf position (position_key_seed)
   std::shared_ptr<RolloutPolicy> rollout_policy;
   // waves of at least this many leaves descend (and back up) on the pool; smaller ones run
   // serially and deterministically
@@ -768,7 +769,8 @@ class Search {
         Board b = L.board;
         b.set_enforce_superko(false);
         b.set_light(true);
-        Rng rng(base + (uint64_t)i * 7919ull);
+        Rng rng(keyed_rollouts ? position_key_seed(L.board.hash(), L.board.current_player())
+                               : base + (uint64_t)i * 7919ull);
         const int ptm = L.board.current_player();
         const int win = rollout_policy->rollout(b, rng, rollout_limit);
         L.z = win == 0 ? 0.f : (win == ptm ? 1.f : -1.f);

@@ -7,6 +7,8 @@ whole network (forward, fused softmax/loss, backward, SGD) runs on the hand-writ
 kernels (models/fused.py). Defaults follow the reference (128 filters, 12
 layers); the north-star benchmark model is 48 planes / 192 filters / 12+1 layers.
 """
+import warnings
+
 import numpy as np
 
 from ..engine.gamestate import PASS_MOVE
@@ -19,36 +21,25 @@ from .nn_util import Bias, NeuralNetBase, neuralnet
 class CNNPolicy(NeuralNetBase):
     """Convolutional policy network: state -> distribution over board points."""
 
-    def _select_moves_and_normalize(self, nn_output, moves, size):
-        if len(moves) == 0:
-            return []
-        if len(nn_output) > size * size:  # pass-logit network: pass is a move like any other
-            moves = list(moves) + ([PASS_MOVE] if PASS_MOVE not in moves else [])
-        move_indices = [size * size if m is PASS_MOVE else flatten_idx(m, size) for m in moves]
-        distribution = nn_output[move_indices]
-        distribution = distribution / distribution.sum()
-        return list(zip(moves, distribution))
-
     def batch_eval_state(self, states, moves_lists=None):
-        """Evaluate many states in one network call: [eval_state(s) for s in states]."""
-        n_states = len(states)
-        if n_states == 0:
+        """``[eval_state(s) for s in states]`` through one forward pass (reference
+        policy.py:27-48): every state must have the same board size."""
+        if not states:
             return []
-        state_size = states[0].size
-        if not all([st.size == state_size for st in states]):
-            raise ValueError("all states must have the same size")
-        nn_input = self.preprocessor.states_to_tensor_u8(states)
-        network_output = self.forward(nn_input)
-        moves_lists = moves_lists or [st.get_legal_moves() for st in states]
-        return [self._select_moves_and_normalize(network_output[i], moves_lists[i], state_size)
-                for i in range(n_states)]
+        sizes = {st.size for st in states}
+        if len(sizes) > 1:
+            raise ValueError("batch_eval_state: mixed board sizes %s" % sorted(sizes))
+        probs = self.forward(self.preprocessor.states_to_tensor_u8(states))
+        if moves_lists is None:
+            moves_lists = [st.get_legal_moves() for st in states]
+        return [_move_distribution(p, mv, st.size)
+                for p, mv, st in zip(probs, moves_lists, states)]
 
     def eval_state(self, state, moves=None):
-        """(move, probability) pairs over ``moves`` (default: all legal moves, quirk Q5)."""
-        tensor = self.preprocessor.state_to_tensor(state)
-        network_output = self.forward(tensor)
-        moves = moves or state.get_legal_moves()
-        return self._select_moves_and_normalize(network_output[0], moves, state.size)
+        """(move, probability) pairs over ``moves`` (default: all legal moves, quirk Q5),
+        renormalised over those moves (reference policy.py:50-64)."""
+        probs = self.forward(self.preprocessor.state_to_tensor(state))[0]
+        return _move_distribution(probs, moves or state.get_legal_moves(), state.size)
 
     @staticmethod
     def create_network(**kwargs):
@@ -139,9 +130,9 @@ class ResnetPolicy(CNNPolicy):
         layer = 1
         while layer < params['layers']:
             path, layer = add_resnet_unit(path, layer)
-        if layer > params['layers']:
-            print("Due to skipping, ended with {} layers instead of {}"
-                  .format(layer, params['layers']))
+        if layer > params['layers']:  # an n_skip_K ran past the requested depth
+            warnings.warn("ResnetPolicy: n_skip settings give %d layers (%d requested)"
+                          % (layer, params['layers']))
         path = add(K.Activation('relu'), [path])
         path = add(K.Convolution2D(nb_filter=1, nb_row=1, nb_col=1, init='uniform',
                                    border_mode='same'), [path])
@@ -165,3 +156,18 @@ def policy_probabilities(policy, states):
     """(B, S*S) probabilities for a list of states (fast path for players / search)."""
     x = policy.preprocessor.states_to_tensor_u8(states)
     return np.asarray(policy.forward(x))
+
+
+def _move_distribution(probs, moves, size):
+    """The network's probabilities of ``moves`` (PASS_MOVE maps to the pass logit of a
+    pass-logit network, which also always offers it), renormalised to sum to one."""
+    if not moves:
+        return []
+    moves = list(moves)
+    pass_slot = len(probs) > size * size
+    if pass_slot and PASS_MOVE not in moves:
+        moves.append(PASS_MOVE)
+    idx = np.fromiter((size * size if m is PASS_MOVE else flatten_idx(m, size) for m in moves),
+                      dtype=np.int64, count=len(moves))
+    sel = np.asarray(probs)[idx]
+    return list(zip(moves, sel / sel.sum()))

@@ -32,7 +32,7 @@ DistributedMCTS (``mode="master"``) — one tree on rank 0, leaf evaluation spre
     sensible-move masks of this round's wave and the rollout results of the wave it started
     ``rollout_delay`` rounds earlier (rollouts take longer than a network pass; the native tree
     keeps such a wave's virtual loss until its rollout backup, as in the single-GPU pipeline);
-  * results come back with one all-gather; rank 0 backs them up and selects the next round.
+  * results come back to rank 0 with one gather; it backs them up and selects the next round.
 
 So the tree, the selection and the backups stay on one host (no tree synchronisation), and all
 the per-leaf work that scales — ladder reading, features, both networks, rollouts — is split
@@ -41,6 +41,7 @@ all-reduced only at the end) remains available as ``ParallelMCTS(dp=...)``.
 """
 import math
 import collections
+import os
 import time
 
 import numpy as np
@@ -75,22 +76,18 @@ class LeafCodec(object):
         self.superko = bool(superko)
         self.L = (6 * P + 32 + 7) // 8 * 8 if superko else (3 * P + 32 + 7) // 8 * 8
 
-    def pack(self, search, wid, nthreads):
-        boards = search.leaf_boards(wid)
-        _, meta8 = search.rollout_inputs(wid)
-        superko = boards[0].enforce_superko
-        if superko and not self.superko:
-            raise ValueError("a superko wave needs LeafCodec(S, superko=True)")
-        colors, ages, _, illegal, lad = _rg.gpu_feature_inputs(boards, superko, nthreads)
-        n, P = len(boards), self.P
-        rec = np.zeros((n, self.L), np.uint8)
-        rec[:, :P] = colors.view(np.uint8)
-        rec[:, self.o_age:self.o_meta] = np.ascontiguousarray(ages).view(np.uint8)
-        rec[:, self.o_meta:self.o_ill] = np.ascontiguousarray(meta8).view(np.uint8)
-        if superko:
-            if illegal is not None:
-                rec[:, self.o_ill:self.o_lad] = illegal
-            rec[:, self.o_lad:self.o_lad + 2 * P] = lad.reshape(n, 2 * P)
+    def pack(self, search, wid, nthreads, out=None):
+        """The wave's records, written by the native search straight into the record columns
+        (one parallel pass over the leaves; ``out``: a [>= n, L] uint8 buffer to fill, e.g. a
+        row of the round's scatter buffer). Returns (records [n, L], superko)."""
+        superko = self.superko
+        n, P = search.num_leaves(wid), self.P
+        rec = out[:n] if out is not None else np.empty((n, self.L), np.uint8)
+        search.pack_inputs(wid, colors=rec[:, :P].view(np.int8),
+                           ages=rec[:, self.o_age:self.o_meta].view(np.int16),
+                           meta8=rec[:, self.o_meta:self.o_ill].view(np.int32),
+                           illegal=rec[:, self.o_ill:self.o_lad] if superko else None,
+                           ladders=rec[:, self.o_lad:self.o_lad + 2 * P] if superko else None)
         return rec, superko
 
     def unpack(self, rec):
@@ -117,7 +114,8 @@ class WaveEvaluator(object):
         self.limit = int(rollout_limit)
         self.nthreads = nthreads
         model = net.policy if net.policy is not None else net.value
-        self.device = model.model.net.device
+        inner = getattr(getattr(model, "model", None), "net", None)  # (None: a host evaluator)
+        self.device = inner.device if inner is not None else torch.device("cpu")
         self.gpu = self.device.type == "cuda"
         self._gro = None
         # the networks run on their own stream: the collectives queued on the default stream
@@ -133,12 +131,15 @@ class WaveEvaluator(object):
         pr, v, sens = ev.result()
         return pr, v, sens, pend
 
-    def submit(self, codec, rec, superko, komi, seed):
+    def submit(self, codec, rec, superko, komi, seed, boards=None):
         """Start the wave's evaluation: (handle whose result() is (priors, values, sensible) as
         numpy, rollout handle or None). On the GPU the networks run asynchronously into pinned
-        host buffers, so the caller can take part in collectives meanwhile."""
+        host buffers, so the caller can take part in collectives meanwhile. ``boards``: the
+        leaves' native boards when this rank has them (rank 0's own wave: the tree's leaf
+        boards), instead of rebuilding them from the records."""
         colors, ages, meta8, illegal, lad = codec.unpack(rec)
-        boards = self._boards(colors, ages, meta8, codec.S, komi)
+        if boards is None:
+            boards = self._boards(colors, ages, meta8, codec.S, komi)
         pend = self._rollouts(boards, colors, meta8, codec.S, komi, seed) \
             if self.lmbda > 0 else None
         if self.gpu:
@@ -147,13 +148,17 @@ class WaveEvaluator(object):
         res = self.net(boards)
         return _Done(tuple(res[:3]) if len(res) > 2 else (res[0], res[1], None)), pend
 
-    def _gpu_eval(self, boards, colors, ages, meta8, illegal, lad, superko):
+    def planes(self, boards, colors, ages, meta8, illegal, lad, superko):
+        """(policy planes, value planes, the planes holding the sensibleness plane) of a
+        shipped wave on the device: from the master's superko-aware ladder planes and illegal
+        mask when the boards enforce superko, else the evaluator's HIP feature path on the
+        rebuilt boards (the single-GPU search's own path)."""
         ev = self.net
-        plans = ev._plans()
+        ev._plans()
         n = len(boards)
 
-        def planes(key):
-            if superko:  # the master's superko-aware ladder planes and illegal mask
+        def one(key):
+            if superko:
                 meta4 = np.zeros((n, 4), np.int32)
                 meta4[:, :2] = meta8[:, :2]
                 meta4[:, 2] = 1
@@ -161,12 +166,17 @@ class WaveEvaluator(object):
             return ev.gpu[key](boards)
 
         if ev.shared or ev.value is None:
-            x = planes("p")
-            xp, xv = (x[:, :ev.npol].contiguous() if ev.shared else x), x
-        else:
-            xp = planes("p") if ev.policy is not None else None
-            xv = planes("v")
-            x = xp if xp is not None else xv
+            x = one("p")
+            return (x[:, :ev.npol].contiguous() if ev.shared else x), x, x
+        xp = one("p") if ev.policy is not None else None
+        xv = one("v")
+        return xp, xv, (xp if xp is not None else xv)
+
+    def _gpu_eval(self, boards, colors, ages, meta8, illegal, lad, superko):
+        ev = self.net
+        plans = ev._plans()
+        n = len(boards)
+        xp, xv, x = self.planes(boards, colors, ages, meta8, illegal, lad, superko)
         ppol, pval = plans
         with torch.no_grad():
             sens = x[:, ev._sens_off].reshape(n, -1) if ev._sens_off is not None else None
@@ -224,9 +234,16 @@ class DistributedMCTS(ParallelMCTS):
     Call ``get_move(state)`` on EVERY rank (all ranks return the same move; only rank 0's
     ``state`` is read) and ``update_with_move(move)`` on every rank after playing it."""
 
-    def __init__(self, policy=None, value=None, rollout=None, dp=None, rollout_delay=6, **kw):
+    def __init__(self, policy=None, value=None, rollout=None, dp=None, rollout_delay=6,
+                 force_master=None, **kw):
+        """``force_master`` (default: RAG_FORCE_PG=1): run the round loop — record packing,
+        WaveEvaluator on shipped records, the round pipeline — even with one rank, instead of
+        the single-GPU ParallelMCTS search (the GPU tests of the multi-GPU leaf path)."""
         kw.setdefault("pipeline", 1)
         super(DistributedMCTS, self).__init__(policy, value, rollout, dp=None, **kw)
+        if force_master is None:
+            force_master = os.environ.get("RAG_FORCE_PG") == "1"
+        self.force_master = bool(force_master)
         self.ddp = dp
         self.world = dp.world if dp is not None and dp.enabled else 1
         self.rank = dp.rank if dp is not None and dp.enabled else 0
@@ -256,6 +273,14 @@ class DistributedMCTS(ParallelMCTS):
                 h[HDR:] = torch.tensor(counts, dtype=torch.int64)
         return self._bcast(h).cpu().numpy()
 
+    def _round_records(self, codec):
+        """Rank 0's [world, batch, L] record buffer of a round (reused; a wave's rows past its
+        leaf count are stale and never read)."""
+        buf = getattr(self, "_recbuf", None)
+        if buf is None or buf.shape[2] != codec.L:
+            buf = self._recbuf = np.zeros((self.world, self.batch, codec.L), np.uint8)
+        return buf
+
     def _ship(self, codec, recs, counts, superko, komi):
         """Phase 1 of a round on every rank: receive the waves, start evaluating this rank's."""
         B = self.batch
@@ -265,16 +290,12 @@ class DistributedMCTS(ParallelMCTS):
             return (rnd, 0, None, codec)
         mine = None
         if self.world > 1:
-            # each rank receives only its own wave's records (scatter, not a broadcast of all)
-            buf = torch.zeros((B, codec.L), dtype=torch.uint8, device=self.device)
+            # each rank receives only its own wave's records (scatter, not a broadcast of all);
+            # rank 0's round buffer goes to the device in one copy
+            buf = torch.empty((B, codec.L), dtype=torch.uint8, device=self.device)
             if self.rank == 0:
-                parts = []
-                for r, rec in enumerate(recs):
-                    t = torch.zeros((B, codec.L), dtype=torch.uint8)
-                    if rec is not None and len(rec):
-                        t[:len(rec)] = torch.from_numpy(rec)
-                    parts.append(t.to(self.device, non_blocking=False))
-                dist.scatter(buf, scatter_list=parts, src=0)
+                allr = torch.from_numpy(self._round_records(codec)).to(self.device)
+                dist.scatter(buf, scatter_list=list(allr.unbind(0)), src=0)
             else:
                 dist.scatter(buf, src=0)
             if n:
@@ -283,7 +304,8 @@ class DistributedMCTS(ParallelMCTS):
         if n:
             mine = mine if mine is not None else recs[0]
             seed = (self.seed * 7919 + rnd * 131 + self.rank) & 0x7FFFFFFF
-            handle, pend = self.leaf_eval.submit(codec, mine, superko, komi, seed)
+            own = getattr(self, "_own_boards", None) if self.rank == 0 else None
+            handle, pend = self.leaf_eval.submit(codec, mine, superko, komi, seed, boards=own)
             if pend is not None:
                 self._pending.append((rnd, pend))
             self.rank_leaves += n
@@ -316,10 +338,15 @@ class DistributedMCTS(ParallelMCTS):
             meta[1], meta[2] = zr, len(z)
         flat = np.concatenate([out.reshape(-1), meta])
         if self.world > 1:
+            # to rank 0 only (gather, not all_gather: the other ranks never read the results)
             flat = torch.from_numpy(flat).to(self.device)
-            gathered = [torch.empty_like(flat) for _ in range(self.world)]
-            dist.all_gather(gathered, flat)
-            gathered = [g.cpu().numpy() for g in gathered] if self.rank == 0 else None
+            if self.rank == 0:
+                gathered = [torch.empty_like(flat) for _ in range(self.world)]
+                dist.gather(flat, gather_list=gathered, dst=0)
+                gathered = torch.stack(gathered).cpu().numpy()
+            else:
+                dist.gather(flat, dst=0)
+                gathered = None
         else:
             gathered = [flat]
         if self.rank != 0:
@@ -349,75 +376,100 @@ class DistributedMCTS(ParallelMCTS):
         s = self._sync_root(state)
         codec = LeafCodec(state.size, bool(s.root_board.enforce_superko))
         target = s.root_visits + (n_playout or self.n_playout)
-        waves = {}  # (round, rank) -> wave id still waiting for its rollout results
-        inflight = None  # (shipped, counts, wids) of the round not collected yet
+        # round -> [wave id, leaf counts per rank, {rank: rollout z}] until its rollouts are in
+        waves = {}
+        inflight = None  # (shipped, counts, wid) of the round not collected yet
         stall = 0
-        t_sel = t_rt = t_back = 0.0
+        # rank 0's round split: tree selection, record packing, header + scatter + starting its
+        # own wave, collecting (its own results + the gather), backups
+        tm = dict.fromkeys(("t_select", "t_pack", "t_ship", "t_gather", "t_backup"), 0.0)
+        rounds = 0
         superko = int(s.root_board.enforce_superko)
+        B, W = self.batch, self.world
         while True:
+            # ONE native wave per round (one parallel descent + board build, one record pack,
+            # one value backup, one rollout backup), dealt to the ranks in contiguous chunks of
+            # at most `batch` leaves: leaf i goes to rank i // batch
             t0 = time.perf_counter()
-            recs, counts, wids = [], [], []
             room = target - s.root_visits - (sum(inflight[1]) if inflight else 0)
-            for r in range(self.world):
-                want = min(self.batch, max(room, 0))
-                wid, n = s.select(want) if want > 0 else (-1, 0)
-                if n > 0:
-                    rec, _ = codec.pack(s, wid, self.nthreads)
-                    room -= n
-                else:
-                    rec = None
-                recs.append(rec)
-                counts.append(n)
-                wids.append(wid if n > 0 else -1)
+            want = min(B * W, max(room, 0))
+            wid, n = s.select(want) if want > 0 else (-1, 0)
+            counts = [max(0, min(B, n - r * B)) for r in range(W)]
+            recs = [None] * W
+            ta = time.perf_counter()
+            if n > 0:
+                flat = self._round_records(codec).reshape(W * B, codec.L)
+                codec.pack(s, wid, self.nthreads, out=flat)
+                recs = [flat[r * B:r * B + c] if c else None for r, c in enumerate(counts)]
             t1 = time.perf_counter()
-            if sum(counts) == 0 and inflight is None and not waves:
+            if n == 0 and inflight is None and not waves:
                 stall += 1
                 if stall > 3 or s.root_visits >= target:
                     break
                 continue
             stall = 0
             shipped = None
-            if sum(counts) or not inflight:
+            if n or not inflight:
                 # a new round (possibly empty: it only brings rollout results back)
                 self._header(CMD_ROUND, counts, superko=superko, komi=state.komi, S=state.size,
                              gather=inflight is not None)
+                self._own_boards = s.leaf_boards(wid)[:counts[0]] if counts[0] else None
                 shipped = self._ship(codec, recs, counts, superko, state.komi)
+                self._own_boards = None
                 self._round += 1
             else:
-                self._header(CMD_FLUSH, [0] * self.world, gather=1)
+                self._header(CMD_FLUSH, [0] * W, gather=1)
+            ts = time.perf_counter()
             res = self._collect(inflight[0]) if inflight is not None else None
             t2 = time.perf_counter()
             if res is not None:
                 self._backup(s, res, inflight, waves)
-            inflight = (shipped, counts, wids) if shipped is not None else None
-            t_sel += t1 - t0
-            t_rt += t2 - t1
-            t_back += time.perf_counter() - t2
+            inflight = (shipped, counts, wid) if shipped is not None else None
+            rounds += 1
+            tm["t_select"] += ta - t0
+            tm["t_pack"] += t1 - ta
+            tm["t_ship"] += ts - t1
+            tm["t_gather"] += t2 - ts
+            tm["t_backup"] += time.perf_counter() - t2
             if s.root_visits >= target and not waves and inflight is None:
                 break
             if s.root_visits >= target and not waves and inflight is not None and \
                     sum(inflight[1]) == 0:
-                self._header(CMD_FLUSH, [0] * self.world, gather=1)
+                self._header(CMD_FLUSH, [0] * W, gather=1)
                 self._backup(s, self._collect(inflight[0]), inflight, waves)
                 break
-        self._acc("t_select", t_sel)
-        self._acc("t_eval", t_rt)
-        self._acc("t_backup", t_back)
+        for k, v in tm.items():
+            self._acc(k, v)
+        # (t_eval: everything between selection and backup, the pre-round-5 split)
+        self._acc("t_eval", tm["t_ship"] + tm["t_gather"])
+        self._acc("rounds", rounds)
         return s
 
     def _backup(self, s, res, inflight, waves):
-        shipped, counts, wids = inflight
+        """Back up a collected round: the value backup of its wave (the ranks' results joined
+        in leaf order), and every rollout result that came back with it — a round's rollouts
+        are backed up once all the ranks that evaluated leaves of it have returned theirs."""
+        shipped, counts, wid = inflight
         rnd = shipped[0]
-        for r, (pr, v, sens, zr) in enumerate(res):
-            if counts[r]:
-                s.backup_value(wids[r], pr if self.evaluator.policy is not None else None,
-                               v if self.evaluator.value is not None else None,
-                               sens.astype(np.uint8) if self._has_sens() else None)
-                if self.lmbda > 0:
-                    waves[(rnd, r)] = wids[r]
-            if zr is not None:
-                s.backup_rollout(waves.pop((zr[0], r)), zr[1])
-        self.stats["waves"] += sum(1 for c in counts if c)
+        live = [r for r in range(len(counts)) if counts[r]]
+        if live:
+            cat = (lambda i: res[live[0]][i]) if len(live) == 1 else \
+                (lambda i: np.concatenate([res[r][i] for r in live]))
+            s.backup_value(wid, cat(0) if self.evaluator.policy is not None else None,
+                           cat(1) if self.evaluator.value is not None else None,
+                           cat(2).astype(np.uint8) if self._has_sens() else None)
+            if self.lmbda > 0:
+                waves[rnd] = [wid, list(counts), {}]
+        for r, (_, _, _, zr) in enumerate(res):
+            if zr is None:
+                continue
+            ent = waves[zr[0]]
+            ent[2][r] = zr[1]
+            if len(ent[2]) == sum(1 for c in ent[1] if c):
+                z = np.concatenate([ent[2][q] for q in range(len(ent[1])) if ent[1][q]])
+                s.backup_rollout(ent[0], z)
+                del waves[zr[0]]
+        self.stats["waves"] += len(live)
         self.stats["sims"] += sum(counts)
 
     def _has_sens(self):
@@ -425,7 +477,7 @@ class DistributedMCTS(ParallelMCTS):
         return self.evaluator._sens_off is not None
 
     def get_move(self, state):
-        if self.world == 1:
+        if self.world == 1 and not self.force_master:
             return super(DistributedMCTS, self).get_move(state)
         if self.rank != 0:
             return self.serve()

@@ -66,8 +66,21 @@ def nets(size, seed=3, filters=16, layers=3):
     return pol, val
 
 
-def _search_kw(batch):
-    return dict(lmbda=0.0, batch=batch, nthreads=1, pipeline=1, c_puct=5.0, virtual_loss=3)
+def _search_kw(batch, lmbda=0.0):
+    """Search settings of every tree in the study; lmbda > 0 adds native CPU rollouts (one per
+    leaf, AlphaGo's mixing V = (1 - lmbda) v + lmbda z, as the bench's search)."""
+    return dict(lmbda=lmbda, batch=batch, nthreads=1, pipeline=1, c_puct=5.0, virtual_loss=3,
+                rollout_limit=200)
+
+
+def shipped_waves(per_rank, world, bench_budget=8192, bench_wave=512, bench_min=128):
+    """(single-tree wave, per-rank wave at N = world) of the bench's geometry scaled to a study
+    budget: the bench searches 8192 playouts per GPU per move with 512-leaf waves on one GPU and
+    max(128, 512 / N) leaves per rank and round on N GPUs (benchmarks/mcts_bench.py
+    distributed_wave); the study keeps the same leaves-in-flight to budget ratios."""
+    w1 = max(1, int(round(per_rank * bench_wave / bench_budget)))
+    wmin = max(1, int(round(per_rank * bench_min / bench_budget)))
+    return w1, max(wmin, w1 // world)
 
 
 def root_visits(s, P):
@@ -79,12 +92,12 @@ def root_visits(s, P):
     return v
 
 
-def single_tree(pol, val, states, budget, batch):
+def single_tree(pol, val, states, budget, batch, lmbda=0.0, seed=1):
     """Root visit vectors and expanded-node counts of one tree per state."""
     from .apv import ParallelMCTS
     out, nodes = [], []
     for st in states:
-        mc = ParallelMCTS(pol, val, n_playout=budget, **_search_kw(batch))
+        mc = ParallelMCTS(pol, val, n_playout=budget, seed=seed, **_search_kw(batch, lmbda))
         s = mc.search(st, budget)
         out.append(root_visits(s, st.size * st.size))
         nodes.append(len(s.expanded_keys()))
@@ -105,9 +118,9 @@ def _rank_worker(rank, world, port, outdir, cfg):
     vis, keys, offs = [], [], [0]
     master = cfg["search_cls"] == "DistributedMCTS"
     for st in states:
-        kw = _search_kw(cfg["batch"])
+        kw = _search_kw(cfg["batch"], cfg.get("lmbda", 0.0))
         if master:
-            kw["rollout_delay"] = 0
+            kw["rollout_delay"] = cfg.get("rollout_delay", 0)
         mc = cls(pol, val, dp=dp, n_playout=cfg["total"], **kw)
         P = st.size * st.size
         if master and rank > 0:
@@ -179,19 +192,23 @@ def equivalent_budget(ladder, k):
 
 def study(worlds=(2, 4, 8), per_rank=128, batch=16, n_positions=50, size=9, truth_mult=4,
           search_cls="SharedRootMCTS", outdir="/tmp/rag_eff", pos_seed=0, net_seed=3,
-          ladder_top=None, split_wave=False):
+          ladder_top=None, split_wave=False, lmbda=0.0, rollout_delay=0, shipped=False):
     """The whole comparison; returns a JSON-able dict. ``split_wave``: the N-rank search's
     per-rank wave is batch / N (the job keeps the one-GPU search's leaves in flight per round
-    instead of N times as many)."""
+    instead of N times as many). ``shipped``: the bench's geometry instead (shipped_waves: the
+    single trees' wave and the per-rank waves scaled from the 19x19 bench; ``batch`` ignored),
+    normally with ``lmbda`` 0.5 and ``rollout_delay`` 6 as the bench runs it."""
     os.makedirs(outdir, exist_ok=True)
     pol, val = nets(size, net_seed)
     states = positions(n_positions, size, pos_seed)
+    if shipped:
+        batch = shipped_waves(per_rank, 1)[0]
     top = ladder_top or per_rank * max(worlds)
-    truth, truth_nodes = single_tree(pol, val, states, top * truth_mult, batch)
+    truth, truth_nodes = single_tree(pol, val, states, top * truth_mult, batch, lmbda, seed=99)
     ladder, rows = [], {}
     b = per_rank
     while b <= top:
-        v, nodes = single_tree(pol, val, states, b, batch)
+        v, nodes = single_tree(pol, val, states, b, batch, lmbda)
         k = kl(truth, v)
         ladder.append((b, k))
         rows["single_%d" % b] = {"budget": b, "kl": round(k, 4),
@@ -199,11 +216,15 @@ def study(worlds=(2, 4, 8), per_rank=128, batch=16, n_positions=50, size=9, trut
                                  "nodes": float(nodes.mean())}
         b *= 2
     cfg = {"size": size, "net_seed": net_seed, "pos_seed": pos_seed,
-           "n_positions": n_positions, "batch": batch, "search_cls": search_cls}
+           "n_positions": n_positions, "batch": batch, "search_cls": search_cls,
+           "lmbda": lmbda, "rollout_delay": rollout_delay}
     for w in worlds:
         d = os.path.join(outdir, "%s_w%d" % (search_cls, w))
         os.makedirs(d, exist_ok=True)
-        wcfg = dict(cfg, batch=max(1, batch // w)) if split_wave else cfg
+        if shipped:
+            wcfg = dict(cfg, batch=shipped_waves(per_rank, w)[1])
+        else:
+            wcfg = dict(cfg, batch=max(1, batch // w)) if split_wave else cfg
         vis, dup = multi_rank(w, per_rank * w, wcfg, d)
         k = kl(truth, vis)
         teq = equivalent_budget(ladder, k)
@@ -215,4 +236,5 @@ def study(worlds=(2, 4, 8), per_rank=128, batch=16, n_positions=50, size=9, trut
             "efficiency": round(teq / (per_rank * w), 3)}
     return {"positions": n_positions, "board": size, "per_rank_playouts": per_rank,
             "wave": batch, "truth_budget": top * truth_mult, "search": search_cls,
+            "lmbda": lmbda, "rollout_delay": rollout_delay, "shipped_geometry": bool(shipped),
             "truth_nodes": float(truth_nodes.mean()), "rows": rows}

@@ -111,29 +111,95 @@ def test_one_search_two_ranks_pass_logit(tmp_path):
     assert -1 in set(np.load(tmp_path / "rootmoves.npy").tolist())
 
 
+def _played(size, n, seed, superko):
+    st = go.GameState(size=size, enforce_superko=superko)
+    rng = np.random.RandomState(seed)
+    for _ in range(n):
+        legal = st.get_legal_moves(include_eyes=False)
+        if not legal:
+            break
+        st.do_move(legal[rng.randint(len(legal))])
+    return st
+
+
 @__import__("pytest").mark.gpu
-def test_distributed_search_gpu_single_rank(cuda):
-    """The GPU leaf path of the multi-GPU search (rebuilt boards, host ladders, HIP features,
-    fused networks, GPU rollouts) on one rank: a full search plays a legal move and every
-    simulation's rollout is backed up."""
-    from rocalphago_amd.engine.gamestate import GameState
+@__import__("pytest").mark.parametrize("superko", [False, True])
+def test_distributed_leaf_path_gpu(cuda, superko):
+    """The multi-GPU search's leaf path on one GPU at the bench geometry (19x19, 192 filters,
+    12 layers): a wave of tree leaves packed as records (LeafCodec), rebuilt on the receiving
+    side, gives bit-exactly the feature planes of the single-GPU path on the tree's own boards
+    (with superko: from the master's illegal mask and ladder planes), and the shipped wave's
+    priors / values match the direct evaluation. Then a full search whose round loop runs
+    (force_master) under a one-rank RCCL group plays legal moves with every rollout backed up."""
+    import os
+    import socket
+    import torch
+    import torch.distributed as dist
     from rocalphago_amd.models.policy import CNNPolicy
     from rocalphago_amd.models.value import CNNValue
-    from rocalphago_amd.search.distributed import DistributedMCTS
+    from rocalphago_amd.parallel.dp import DPContext
+    from rocalphago_amd.search.distributed import DistributedMCTS, LeafCodec
     dev = cuda
-    pol = CNNPolicy(DEFAULT_FEATURES, board=19, filters_per_layer=64, layers=4, device=dev,
+    pol = CNNPolicy(DEFAULT_FEATURES, board=19, filters_per_layer=192, layers=12, device=dev,
                     seed=1)
-    val = CNNValue(list(DEFAULT_FEATURES) + ["color"], board=19, filters_per_layer=64, layers=4,
-                   device=dev, seed=2)
-    mc = DistributedMCTS(pol, val, dp=None, lmbda=0.5, n_playout=1024, batch=128, nthreads=8)
-    st = GameState()
-    for _ in range(2):
-        mv = mc.get_move(st)
-        assert mv is None or st.is_legal(mv)
-        st.do_move(mv)
-        mc.update_with_move(mv)
-    assert mc.stats["sims"] >= 2 * 1024 - 2
-    assert mc._search.rollouts == mc._search.sims
+    val = CNNValue(list(DEFAULT_FEATURES) + ["color"], board=19, filters_per_layer=192,
+                   layers=12, device=dev, seed=2)
+    st = _played(19, 40, 5, superko)
+    mc = DistributedMCTS(pol, val, dp=None, lmbda=0.5, n_playout=1024, batch=128, nthreads=8,
+                         force_master=True)
+    # ---- one wave, shipped vs direct
+    s = mc._sync_root(st)
+    w0, n0 = s.select(1)  # the root itself: expand it first (then a wave of its children)
+    assert n0 == 1
+    pri0, v0, sens0 = mc.evaluator(s.leaf_boards(w0))[:3]
+    s.backup_value(w0, pri0, v0, sens0.astype(np.uint8) if sens0 is not None else None)
+    wid, n = s.select(64)
+    assert n > 8
+    codec = LeafCodec(19, superko)
+    rec, sk = codec.pack(s, wid, 8)
+    assert sk == superko
+    tree = s.leaf_boards(wid)
+    colors, ages, meta8, illegal, lad = codec.unpack(rec)
+    rebuilt = mc.leaf_eval._boards(colors, ages, meta8, 19, st.komi)
+    ev = mc.evaluator
+    ev._plans()
+    xp, xv, _ = mc.leaf_eval.planes(rebuilt, colors, ages, meta8, illegal, lad, superko)
+    if ev.shared:  # one extraction feeds both networks (policy planes = the first npol)
+        xd = ev.gpu["p"](tree)
+        assert torch.equal(xv, xd) and torch.equal(xp, xd[:, :ev.npol])
+    else:
+        assert torch.equal(xp, ev.gpu["p"](tree)) and torch.equal(xv, ev.gpu["v"](tree))
+    if superko:
+        assert lad is not None and illegal is not None
+    handle, pend = mc.leaf_eval.submit(codec, rec, superko, st.komi, seed=3)
+    pr, v, sens = handle.result()
+    pr_d, v_d, sens_d = ev(tree)[:3]
+    assert np.abs(pr - pr_d).max() <= 2e-2 * max(1e-6, float(np.abs(pr_d).max()))
+    assert np.abs(v - v_d).max() <= 2e-2
+    assert np.array_equal(np.asarray(sens) > 0.5, np.asarray(sens_d) > 0.5)
+    assert pend is not None and len(pend.result()) == n
+    # ---- the round loop under a one-rank RCCL group
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0,
+                            world_size=1)
+    try:
+        dp = DPContext(device=dev, adopt=True)
+        mc = DistributedMCTS(pol, val, dp=dp, lmbda=0.5, n_playout=1024, batch=128,
+                             nthreads=8, force_master=True)
+        assert os.environ.get("RAG_FORCE_PG") == "1" or mc.force_master
+        for _ in range(2):
+            mv = mc.get_move(st)
+            assert mv is None or st.is_legal(mv)
+            st.do_move(mv)
+            mc.update_with_move(mv)
+        assert mc._round > 0 and mc.stats.get("rounds", 0) > 0  # the master round loop ran
+        assert mc.stats["sims"] >= 2 * 1024 - 2
+        assert mc._search.rollouts == mc._search.sims
+    finally:
+        dist.destroy_process_group()
 
 
 def test_root_deltas_and_external_stats_steer_root_selection():
