@@ -614,10 +614,6 @@ bool rag_conv_pipe_launch(const bf16* x, const bf16* w, const float* bias, bf16*
                           const bf16* mk, const bf16* res, int M, int S, int WI, int shift,
                           int WO, int HO, int CIN, int COUTP, int YC, int KS, int relu, int HM,
                           hipStream_t stream);  // conv_fwd.hip
-bool rag_conv_slab_launch(const bf16* x, const bf16* w, const float* bias, bf16* y,
-                          const bf16* mk, const bf16* res, int B, int S, int HI, int WO, int HO,
-                          int CIN, int COUTP, int YC, int KS, int relu, int HM,
-                          hipStream_t stream);  // conv_slab.hip
 bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* y,
                          const bf16* mk, const bf16* res, int M, int S, int WI, int shift, int WO,
                          int HO, int CIN, int COUTP, int YC, int KS, int relu, int HM,
@@ -795,10 +791,6 @@ static int conv_igemm_impl(const void* X, const void* W, const float* bias, void
   bf16* y = (bf16*)Y;
   const bf16* mk = (const bf16*)mask;
   const bf16* res = (const bf16*)resid;
-  static const bool use_pipe = [] {
-    const char* e = getenv("RAG_CONV_PIPE");
-    return !(e && e[0] == '0');
-  }();
   WgradRed pend;
   hipStream_t pend_stream = nullptr;
   const WgradRed* red = nullptr;
@@ -817,12 +809,7 @@ static int conv_igemm_impl(const void* X, const void* W, const float* bias, void
     if (red) rag_launch_wgrad_slab_reduce(*red, stream);
     return -5;
   }
-  if (rag_conv_slab_launch(x, w, bias, y, mk, res, B, S, HI, WO, HO, CIN, COUTP, YC, KS, relu,
-                           HM, stream)) {
-    const int rc = red ? rag_launch_wgrad_slab_reduce(*red, stream) : 0;  // opt-in slab conv
-    return rc ? rc : (int)hipGetLastError();
-  }
-  if (use_pipe && rag_conv_tap_launch(x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN,
+  if (rag_conv_tap_launch(x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN,
                                       COUTP, YC, KS, relu, HM, (long)B * WI * WI, stream, red,
                                       nullptr, nullptr, nullptr, nullptr))
     return (int)hipGetLastError();
@@ -830,7 +817,7 @@ static int conv_igemm_impl(const void* X, const void* W, const float* bias, void
     const int rc = rag_launch_wgrad_slab_reduce(*red, stream);
     if (rc) return rc;
   }
-  if (use_pipe && rag_conv_pipe_launch(x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN,
+  if (rag_conv_pipe_launch(x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN,
                                        COUTP, YC, KS, relu, HM, stream))
     return (int)hipGetLastError();
   switch (KS) {
@@ -959,12 +946,8 @@ static int conv_wgrad_impl(const void* G, const void* X, float* dW, float* db, f
   const bool slab = rag_wgrad_slab_ok(S, HI, HG, GC, COUTP, CINP, KS);
   if (xcoef && !(slab && KS == 3 && rag_wgrad_slab_bf16() && CINP == 128)) return -5;
   // 5x5 with <= 48 real of 64 input channels (the SL input layer): c-tile 1's blocks pair two
-  // kernel rows instead of computing a zero c-fragment (RAG_WGRAD_PAIR5=0 disables)
-  static const bool pair_on = [] {
-    const char* e = getenv("RAG_WGRAD_PAIR5");
-    return !(e && e[0] == '0');
-  }();
-  const int pair5 = pair_on && KS == 5 && CINP == 64 && CIN <= 48 && !xcoef ? 1 : 0;
+  // kernel rows instead of computing a zero c-fragment
+  const int pair5 = KS == 5 && CINP == 64 && CIN <= 48 && !xcoef ? 1 : 0;
   if (slab) {
     bf16_part = rag_wgrad_slab_bf16();
     const int WP = S + 2 * HI;
@@ -1020,19 +1003,13 @@ static int conv_wgrad_impl(const void* G, const void* X, float* dW, float* db, f
     if (defer && rs == stream) {
       PendingRed* p = static_cast<PendingRed*>(pending);
       p->r = r;
-      // RAG_WGRAD_CLAIM=0: the riding reduce blocks split the reduction statically (A/B)
-      static const bool claim = [] {
-        const char* e = getenv("RAG_WGRAD_CLAIM");
-        return !(e && e[0] == '0');
-      }();
-      if (claim) {
-        if (!p->dticket) {
-          if (hipMalloc(&p->dticket, 2 * sizeof(unsigned)) != hipSuccess) return -3;
-          if (hipMemsetAsync(p->dticket, 0, 2 * sizeof(unsigned), stream) != hipSuccess)
-            return -3;
-        }
-        p->r.ticket = p->dticket;
+      // the riding reduce blocks claim units dynamically (launches that keep the static split
+      // clear the ticket); the counters come with the handle (rag_wgrad_pending_init)
+      if (!p->dticket) {
+        if (hipMalloc(&p->dticket, 2 * sizeof(unsigned)) != hipSuccess) return -3;
+        if (hipMemsetAsync(p->dticket, 0, 2 * sizeof(unsigned), stream) != hipSuccess) return -3;
       }
+      p->r.ticket = p->dticket;
       p->stream = stream;
       p->valid = 1;
       return 0;
@@ -1040,21 +1017,9 @@ static int conv_wgrad_impl(const void* G, const void* X, float* dW, float* db, f
     return rag_launch_wgrad_slab_reduce(r, rs);
   }
   const int total = taps * COUTP * CINP / 4 + COUTP;
-  static int unroll = -1;  // RAG_WRED_UNROLL (4 | 8 | 16): chunk loads in flight per thread
-  if (unroll < 0) {
-    const char* e = getenv("RAG_WRED_UNROLL");
-    unroll = e ? atoi(e) : 4;
-  }
-  const int blocks = (total + 255) / 256;
-  if (unroll >= 16)
-    wgrad_reduce_kernel<16><<<blocks, 256, 0, rs>>>(part, bpart, dW, db, nchunks, taps, COUT, CIN,
-                                                    COUTP, CINP, KS, accumulate);
-  else if (unroll >= 8)
-    wgrad_reduce_kernel<8><<<blocks, 256, 0, rs>>>(part, bpart, dW, db, nchunks, taps, COUT, CIN,
-                                                   COUTP, CINP, KS, accumulate);
-  else
-    wgrad_reduce_kernel<4><<<blocks, 256, 0, rs>>>(part, bpart, dW, db, nchunks, taps, COUT, CIN,
-                                                   COUTP, CINP, KS, accumulate);
+  const int blocks = (total + 255) / 256;  // 4 chunk loads in flight per thread (8 / 16: same)
+  wgrad_reduce_kernel<4><<<blocks, 256, 0, rs>>>(part, bpart, dW, db, nchunks, taps, COUT, CIN,
+                                                 COUTP, CINP, KS, accumulate);
   return (int)hipGetLastError();
 }
 

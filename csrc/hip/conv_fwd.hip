@@ -23,13 +23,11 @@ namespace {
 
 constexpr int kBK = 32;
 constexpr int kNBUF = 3;
-// K-loop order: 0 = tap outer / channel chunk inner, 1 (default: 3-8 % faster, measured with
-// scripts/dbg/conv_ab.py) = channel chunk outer / tap inner
-int g_conv_order = -1;
-// fragment double-buffering (see the K loop): needs ~48 more VGPRs and spills at 2 blocks/CU
-// with the 192x192 tile, so it is off
+// K-loop order: 0 = tap outer / channel chunk inner (A/B, rag_conv_order), 1 (default: 3-8 %
+// faster) = channel chunk outer / tap inner
+int g_conv_order = 1;
 
-template <int KS, int NT, int MT, bool kFragPrefetch>
+template <int KS, int NT, int MT>
 __global__ void __launch_bounds__(256, 2)
 conv_pipe_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                  const float* __restrict__ bias, bf16* __restrict__ Y,
@@ -123,7 +121,6 @@ conv_pipe_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
 
   stage(0, 0);
   if (nsteps > 1) stage(1, 1);
-  if (kFragPrefetch && nsteps > 2) stage(2, 2);
 
   const int frow = lane & 15;
   const int fq = lane >> 4;
@@ -140,58 +137,6 @@ conv_pipe_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
     boffs[j] = kBM * kBK + row * kBK + ((fq ^ swz64(row)) * 8);
   }
 
-  if constexpr (kFragPrefetch) {
-    // Fragment double-buffering: the ds_reads of step s+1 are issued before the MFMAs of step
-    // s, so LDS latency hides behind the MFMA burst. Ring of 3 LDS stages: at step s the
-    // stage s+1 is read, s+2 is landing and s+3 is issued into the buffer of stage s (whose
-    // fragments every wave already holds in registers when it passes the barrier).
-    bf16x8 xa0[MT], wb0[NT], xa1[MT], wb1[NT];
-    auto read_frags = [&](int b, bf16x8 (&xa)[MT], bf16x8 (&wb)[NT]) {
-      const bf16* lb = lds + b * STAGE;
-#pragma unroll
-      for (int i = 0; i < MT; ++i) xa[i] = *reinterpret_cast<const bf16x8*>(lb + aoffs[i]);
-#pragma unroll
-      for (int j = 0; j < NT; ++j) wb[j] = *reinterpret_cast<const bf16x8*>(lb + boffs[j]);
-    };
-    auto mfmas = [&](bf16x8 (&xa)[MT], bf16x8 (&wb)[NT]) {
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int j = 0; j < NT; ++j)
-#pragma unroll
-        for (int i = 0; i < MT; ++i) acc[j][i] = mfma16(wb[j], xa[i], acc[j][i]);
-      __builtin_amdgcn_s_setprio(0);
-    };
-    int bcur = 0;  // LDS buffer of stage s
-    auto step = [&](int s, bf16x8 (&xc)[MT], bf16x8 (&wc)[NT], bf16x8 (&xn)[MT],
-                    bf16x8 (&wn2)[NT]) {
-      const int bnext = bcur + 1 == kNBUF ? 0 : bcur + 1;
-      if (s + 1 < nsteps) {
-        if (s + 2 < nsteps)
-          asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PER_STAGE) : "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        if (s + 3 < nsteps) stage(bcur, s + 3);
-        read_frags(bnext, xn, wn2);
-      }
-      mfmas(xc, wc);
-      bcur = bnext;
-    };
-    if (nsteps > 2)
-      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * PER_STAGE) : "memory");
-    else if (nsteps == 2)
-      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PER_STAGE) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    read_frags(0, xa0, wb0);
-    for (int s = 0; s < nsteps; s += 2) {
-      step(s, xa0, wb0, xa1, wb1);
-      if (s + 1 < nsteps) step(s + 1, xa1, wb1, xa0, wb0);
-    }
-  } else {
   int buf = 0;
   for (int s = 0; s < nsteps; ++s) {
     if (s + 1 < nsteps)
@@ -218,7 +163,6 @@ conv_pipe_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
       for (int i = 0; i < MT; ++i) acc[j][i] = mfma16(wb[j], xa[i], acc[j][i]);
     __builtin_amdgcn_s_setprio(0);
     buf = buf + 1 == kNBUF ? 0 : buf + 1;
-  }
   }
 
   // epilogue: lane owns channels n..n+3 of pixel m for every (j, i) tile
@@ -269,19 +213,18 @@ conv_pipe_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
 }
 
 template <int KS>
-bool launch_ks(int nt, int mt, bool pf, dim3 grid, hipStream_t st, const bf16* X, const bf16* W,
+bool launch_ks(int nt, int mt, dim3 grid, hipStream_t st, const bf16* X, const bf16* W,
                const float* bias, bf16* Y, const bf16* mask, const bf16* res, int M, int S,
                int WI, int shift, int WO, int HO, int CIN, int WROWS, int YC, int relu, int HM) {
-#define RAG_PIPE(N, T, PF)                                                                    \
-  if (nt == N && mt == T && pf == PF) {                                                       \
-    conv_pipe_kernel<KS, N, T, PF><<<grid, 256, 0, st>>>(X, W, bias, Y, mask, res, M, S, WI,    \
+#define RAG_PIPE(N, T)                                                                        \
+  if (nt == N && mt == T) {                                                                   \
+    conv_pipe_kernel<KS, N, T><<<grid, 256, 0, st>>>(X, W, bias, Y, mask, res, M, S, WI,    \
                                                          shift, WO, HO, CIN, WROWS, YC, relu,  \
                                                          HM, g_conv_order);                    \
     return true;                                                                              \
   }
-  RAG_PIPE(2, 4, false) RAG_PIPE(2, 6, false) RAG_PIPE(2, 8, false) RAG_PIPE(4, 4, false)
-  RAG_PIPE(4, 6, false) RAG_PIPE(4, 8, false) RAG_PIPE(6, 4, false) RAG_PIPE(6, 6, false)
-  RAG_PIPE(6, 4, true) RAG_PIPE(4, 4, true) RAG_PIPE(4, 6, true)
+  RAG_PIPE(2, 4) RAG_PIPE(2, 6) RAG_PIPE(2, 8) RAG_PIPE(4, 4)
+  RAG_PIPE(4, 6) RAG_PIPE(4, 8) RAG_PIPE(6, 4) RAG_PIPE(6, 6)
 #undef RAG_PIPE
   return false;
 }
@@ -320,27 +263,15 @@ bool rag_conv_pipe_launch(const bf16* x, const bf16* w, const float* bias, bf16*
   const int nt = COUTP % 192 == 0 ? 6 : (COUTP % 128 == 0 ? 4 : (COUTP % 64 == 0 ? 2 : 0));
   if (!nt) return false;
   const int ntn = COUTP / (32 * nt);
-  static const int force_mt = [] {
-    const char* e = getenv("RAG_CONV_MT");
-    return e ? atoi(e) : 0;
-  }();
-  const int mt = force_mt ? force_mt : pick_mt(M, nt, ntn);
-  if (g_conv_order < 0) {
-    const char* e = getenv("RAG_CONV_ORDER");
-    g_conv_order = e ? atoi(e) : 1;
-  }
-  static const bool pf = [] {  // experimental: fragment double-buffering (RAG_CONV_PF=1)
-    const char* e = getenv("RAG_CONV_PF");
-    return e && e[0] == '1';
-  }();
+  const int mt = pick_mt(M, nt, ntn);
   const int bm = 32 * mt;
   const int nblk_m = (M + bm - 1) / bm;
   dim3 grid(nblk_m * ntn);
   switch (KS) {
-    case 1: return launch_ks<1>(nt, mt, pf, grid, stream, x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM);
-    case 3: return launch_ks<3>(nt, mt, pf, grid, stream, x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM);
-    case 5: return launch_ks<5>(nt, mt, pf, grid, stream, x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM);
-    case 7: return launch_ks<7>(nt, mt, pf, grid, stream, x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM);
+    case 1: return launch_ks<1>(nt, mt, grid, stream, x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM);
+    case 3: return launch_ks<3>(nt, mt, grid, stream, x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM);
+    case 5: return launch_ks<5>(nt, mt, grid, stream, x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM);
+    case 7: return launch_ks<7>(nt, mt, grid, stream, x, w, bias, y, mk, res, M, S, WI, shift, WO, HO, CIN, COUTP, YC, relu, HM);
     default: return false;
   }
 }

@@ -210,26 +210,14 @@ wgrad_taps_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
   if (do_bias && (int)threadIdx.x < 64) bpart[(size_t)chunk * COUTP + n0 + threadIdx.x] = bsum;
 }
 
-// LDS ring depth: 2 stages (prefetch distance 1, two blocks per CU) or 3 (distance 2, one
-// block per CU, half as many partial slabs). RAG_WGRAD_NBUF overrides the default.
-int nbuf() {
-  static const int n = [] {
-    const char* e = getenv("RAG_WGRAD_NBUF");
-    return (e && e[0] == '3') ? 3 : 2;
-  }();
-  return n;
-}
-
+// LDS ring depth 2 (prefetch distance 1, two blocks per CU; 3 stages at one block per CU
+// measured no faster, deleted round 5).
 template <int KS, int RG>
 void launch(const bf16* G, const bf16* X, float* part, float* bpart, int R, int WP, int GC,
             int CIN, int spc, int COUTP, int CINP, int nchunks, hipStream_t st) {
   dim3 grid(nchunks * (KS / RG) * (COUTP / 64) * (CINP / 64));
-  if (nbuf() == 3)
-    wgrad_taps_kernel<KS, RG, 3><<<grid, 256, 0, st>>>(G, X, part, bpart, R, WP, GC, CIN, spc,
-                                                       COUTP, CINP);
-  else
-    wgrad_taps_kernel<KS, RG, 2><<<grid, 256, 0, st>>>(G, X, part, bpart, R, WP, GC, CIN, spc,
-                                                       COUTP, CINP);
+  wgrad_taps_kernel<KS, RG, 2><<<grid, 256, 0, st>>>(G, X, part, bpart, R, WP, GC, CIN, spc,
+                                                     COUTP, CINP);
 }
 
 }  // namespace
@@ -240,7 +228,7 @@ bool rag_wgrad_taps_fits(int WP, int KS, int RG) {
 }
 
 // Concurrent blocks the taps kernel is sized for (2 per CU with 2 LDS buffers).
-int rag_wgrad_taps_target_blocks() { return nbuf() == 2 ? 512 : 256; }
+int rag_wgrad_taps_target_blocks() { return 512; }
 
 int rag_launch_wgrad_taps(const bf16* G, const bf16* X, float* part, float* bpart, int R, int WP,
                           int GC, int CIN, int spc, int COUTP, int CINP, int KS, int RG,

@@ -60,12 +60,7 @@ __device__ __forceinline__ void wslab_store_oct(const WgradRed& r, int q, const 
   const int wv = (loc >> 8) % r.waves;
   const int slot = (loc >> 8) / r.waves;  // i * NA + a
   int nb, cb, t;
-  if (r.map == 2) {  // wgrad_pp_kernel: wave (g, wl) = c-frag g, n-frags 3 wl + a, all 9 taps
-    const int a = slot % 3, i = slot / 3;
-    t = i;
-    nb = ((wv & 3) * 3 + a) * 16;
-    cb = ctile * kWsC + (wv >> 2) * 16;
-  } else if (r.map) {
+  if (r.map) {
     const int a = slot % 6, i = slot / 6;
     t = (wv >> 2) * 3 + i;
     nb = ((wv & 1) * 6 + a) * 16;

@@ -392,221 +392,6 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Ping-pong wgrad (192 channels, fp16 partials; RAG_WGRAD_PP=1, opt-in): the same block tile
-// (192 n x one 32-channel c-tile x 9 taps over a chunk of 64-row stages, 3-stage ring) run by 8
-// waves in two groups that alternate roles at every barrier, as conv_tap_pp_kernel does for the
-// forward: per MFMA k-step t (two per stage)
-//
-//   X(t): group 0 reads step t's fragments        group 1 runs the MFMAs of step t-1
-//   ---- s_barrier ----
-//   Y(t): group 0 runs the MFMAs of step t         group 1 reads step t's fragments
-//   ---- s_barrier ----
-//
-// so the two waves of a SIMD (w, w+4) never want the matrix pipe at the same time and no wave
-// needs a second fragment register set. Wave (g, wl): c-fragment g, n-fragments 3 wl .. 3 wl + 2,
-// all 9 taps (27 MFMAs per k-step from 3 + 9 transposed fragment reads). Every wave stages three
-// of the 24 G glds of a stage and waves 0-6 one X glds each; stage s+2 is issued at X(2s) and a
-// wave retires its stage s+1 loads (counted vmcnt, stage s+2 stays in flight) before the barrier
-// into X(2s+2), the first read of stage s+1. Group 1 also sums the bias columns of each stage in
-// its MFMA phase. Partials: the kBF layout of wgrad_slab_kernel with NA = 3, NT = 9, 8 waves
-// (WgradRed.map = 2). Measured SLOWER than the 12-wave slab kernel (B = 256: 97 vs 83 us alone,
-// 148 vs 135 us with the deferred dgrad; SL 99.6k vs 107.2k positions/s,
-// profiles/wgrad_pp_ab_r3.txt): three waves per SIMD already overlap one wave's fragment reads
-// with the others' MFMAs, and four barriers per stage instead of one cost more than the
-// ping-pong saves. Kept opt-in, with its test, as the measured alternative.
-constexpr int kPPWaves = 8;
-template <int NB>
-__global__ void __launch_bounds__(512)
-wgrad_pp_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X, float* __restrict__ part,
-                float* __restrict__ bpart, int R, int WP, int GC, int CIN, int spc, int CINP) {
-  using L = WS<kN>;
-  constexpr int kStage = L::Stage, kGElems = L::GElems, kGChunks = L::GChunks;
-  constexpr int kBlk = L::Blk;
-  constexpr int NA = 3, NT = 9, kGrp = 1;
-  static_assert(kRows * kGChunks == kPPWaves * 3 * 64, "three G glds per wave");
-  static_assert(NA * NT * kPPWaves == 9 * (kN / 16) * (kC / 16), "the waves cover the tile");
-  __shared__ __attribute__((aligned(16))) bf16 lds[NB * kStage];
-
-  const int lane = lane_id();
-  const int w = wave_id();
-  const int grp = w >> 2, wl = w & 3;  // waves w and w + 4 share a SIMD
-  const int tid = threadIdx.x;
-  const int ntc = CINP / kC;
-  const int wid = xcd_remap(blockIdx.x, gridDim.x);  // the c-tiles of a chunk share one XCD
-  const int chunk = wid / (ntc * kGrp);
-  const int pct = wid - chunk * ntc * kGrp;  // pseudo c-tile: c-tile * kGrp + ky
-  const int ctile = pct / kGrp, ky = pct - ctile * kGrp;
-  const int c0 = ctile * kC;
-  const int steps = (R + kRows - 1) / kRows;
-  const int sbeg = chunk * spc;
-  int nsteps = steps - sbeg;
-  nsteps = nsteps < spc ? nsteps : spc;
-  nsteps = nsteps > 0 ? nsteps : 0;
-  const int xshift = -(WP + 1);
-
-  int grow[3], gcol[3];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const int slot = (3 * w + k) * 64 + lane;
-    const int row = slot / kGChunks;
-    const int pc = slot - row * kGChunks;
-    grow[k] = row;
-    gcol[k] = (pc ^ L::swz_g(row)) * 8;
-  }
-  const bool xw = w < kXWaves;
-  const int xrow = w * 16 + (lane >> 2);
-  const int xcol = c0 + (((lane & 3) ^ swz_x(xrow)) * 8);
-  const int nl = xw ? 4 : 3;  // this wave's loads per stage
-  auto stage = [&](int s) {
-    const int r0 = (sbeg + s) * kRows;
-    bf16* lg = lds + (s % NB) * kStage;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      int r = r0 + grow[k];
-      r = r < R ? r : R - 1;
-      glds16(G + (size_t)r * GC + gcol[k], lg + (3 * w + k) * 512);
-    }
-    if (xw) {
-      int r = r0 + xshift + xrow;
-      r = r < 0 ? 0 : (r < R ? r : R - 1);
-      glds16(X + (size_t)r * CIN + xcol, lg + kGElems + w * 512);
-    }
-  };
-  auto wait_stage = [&](int young) {  // own loads: `young` younger stages stay in flight
-    if (young <= 0) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else if (nl == 4) {
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-    }
-  };
-
-  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  const int kr = krow(g, q);
-  int goff[NA];
-#pragma unroll
-  for (int a = 0; a < NA; ++a)
-    goff[a] = kr * kN + ((((wl * NA + a) * 2 + (p >> 1)) ^ L::swz_g(kr)) * 8) + 4 * (p & 1);
-  int xoff[NT];
-#pragma unroll
-  for (int i = 0; i < NT; ++i) {
-    const int xr = kr + (i / 3) * WP + (i % 3);
-    xoff[i] = kGElems + xr * kC + (((grp * 2 + (p >> 1)) ^ swz_x(xr)) * 8) + 4 * (p & 1);
-  }
-  f32x4 acc[NT][NA];
-#pragma unroll
-  for (int i = 0; i < NT; ++i)
-#pragma unroll
-    for (int a = 0; a < NA; ++a) acc[i][a] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 fa[NA], fb[NT];
-  auto read_frags = [&](int t) {
-    const bf16* lb = lds + ((t >> 1) % NB) * kStage;
-    const int ro = (t & 1) * 32;
-#pragma unroll
-    for (int a = 0; a < NA; ++a)
-      fa[a] = tr_frag(lb + goff[a] + ro * kN, lb + goff[a] + (ro + 16) * kN);
-#pragma unroll
-    for (int i = 0; i < NT; ++i)
-      fb[i] = tr_frag(lb + xoff[i] + ro * kC, lb + xoff[i] + (ro + 16) * kC);
-    lds_reads_done();
-  };
-  auto mfmas = [&]() {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < NT; ++i)
-#pragma unroll
-      for (int a = 0; a < NA; ++a) acc[i][a] = mfma16(fa[a], fb[i], acc[i][a]);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  const bool do_bias = bpart != nullptr;
-  const int bt = tid - 256;  // group 1's threads sum the bias columns
-  const int bcol = ctile * 32 + (bt & 31);
-  float bsum = 0.f;
-
-  const int T = 2 * nsteps;
-  if (nsteps > 0) stage(0);
-  if (nsteps > 1) stage(1);
-  if (nsteps > 0) wait_stage(nsteps > 1 ? 1 : 0);
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  if (grp == 0) {
-#pragma unroll 1
-    for (int t = 0; t < T; ++t) {
-      const int s = t >> 1;
-      if (!(t & 1) && s + 2 < nsteps) stage(s + 2);
-      read_frags(t);
-      __builtin_amdgcn_s_barrier();  // X -> Y
-      asm volatile("" ::: "memory");
-      mfmas();
-      if ((t & 1) && s + 1 < nsteps) wait_stage(s + 2 < nsteps ? 1 : 0);
-      __builtin_amdgcn_s_barrier();  // Y -> X(t+1)
-      asm volatile("" ::: "memory");
-    }
-  } else {
-#pragma unroll 1
-    for (int t = 0; t < T; ++t) {
-      const int s = t >> 1;
-      if (!(t & 1) && s + 2 < nsteps) stage(s + 2);
-      if (t > 0) mfmas();  // step t-1, beside group 0's reads of step t
-      if (!(t & 1) && do_bias && bcol < kN) {
-        const bf16* lb = lds + (s % NB) * kStage;
-#pragma unroll
-        for (int r = bt >> 5; r < kRows; r += 8)
-          bsum += (float)lb[r * kN + (((bcol >> 3) ^ L::swz_g(r)) << 3) + (bcol & 7)];
-      }
-      __builtin_amdgcn_s_barrier();  // X -> Y
-      asm volatile("" ::: "memory");
-      read_frags(t);                 // beside group 0's MFMAs of step t
-      if ((t & 1) && s + 1 < nsteps) wait_stage(s + 2 < nsteps ? 1 : 0);
-      __builtin_amdgcn_s_barrier();  // Y -> X(t+1)
-      asm volatile("" ::: "memory");
-    }
-    if (T > 0) mfmas();
-  }
-
-  // scaled fp16 partials in the MFMA C layout: [chunk][ctile][i * NA + a][wave][lane][4]
-  float mx = 0.f;
-#pragma unroll
-  for (int i = 0; i < NT; ++i)
-#pragma unroll
-    for (int a = 0; a < NA; ++a)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) mx = fmaxf(mx, fabsf(acc[i][a][r]));
-  mx = warp_max(mx);
-  float* red = reinterpret_cast<float*>(lds);
-  __syncthreads();  // every wave is done with the staging ring
-  if (lane == 0) red[w] = mx;
-  __syncthreads();
-  mx = red[0];
-#pragma unroll
-  for (int k = 1; k < kPPWaves; ++k) mx = fmaxf(mx, red[k]);
-  const int e = mx > 0.f ? max(ilogbf(mx), -100) : 0;
-  const float up = ldexpf(1.f, 14 - e);
-  if (tid == 0) part_scale(part, gridDim.x, kBlk)[wid] = ldexpf(1.f, e - 14);
-  f16* dst = reinterpret_cast<f16*>(part) + (size_t)wid * kBlk + (w * 64 + lane) * 4;
-#pragma unroll
-  for (int i = 0; i < NT; ++i)
-#pragma unroll
-    for (int a = 0; a < NA; ++a) {
-      f16x4 o;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = (f16)(acc[i][a][r] * up);
-      *reinterpret_cast<f16x4*>(dst + (i * NA + a) * (kPPWaves * 256)) = o;
-    }
-  if (do_bias) {
-    float* bred = reinterpret_cast<float*>(lds) + 64;
-    if (tid >= 256) bred[bt] = bsum;
-    __syncthreads();
-    if (tid < 32 && ctile * 32 + tid < kN) {
-      float v = 0.f;
-      for (int k = 0; k < 8; ++k) v += bred[k * 32 + tid];
-      bpart[(size_t)chunk * kN + ctile * 32 + tid] = v;
-    }
-  }
-}
-
 // Sums the fp16 partial slabs of wgrad_slab_kernel<.., true> over chunks in fp32 and scatters
 // to OIHW dW [COUT][CIN][3][3] (+ the fp32 bias partials). A 256-thread block owns 64 "octs"
 // (8 consecutive partial elements = two lanes' 4-value C fragments); its 4 waves split the chunks
@@ -673,16 +458,12 @@ bool rag_wgrad_slab_ok(int S, int H, int HG, int GC, int COUTP, int CINP, int KS
     const char* e = getenv("RAG_WGRAD_SLAB");
     return !(e && e[0] == '0');
   }();
-  static const bool on5 = [] {  // RAG_WGRAD_SLAB5=0: the 5x5 layers keep wgrad_taps
-    const char* e = getenv("RAG_WGRAD_SLAB5");
-    return !(e && e[0] == '0');
-  }();
   const int WP = S + 2 * H;
   if (!on || (COUTP != 192 && COUTP != 128) || GC % 8 || GC < COUTP || CINP % kC) return false;
   if (KS == 3)
     return H == 1 && HG == 1 && CINP == COUTP && kRows + 2 * WP + 2 <= kXRows;
   // 5x5: per-row blocks; the 5 * CINP / 32 pseudo c-tiles must cover the COUTP bias columns
-  return KS == 5 && on5 && rag_wgrad_slab_bf16() && H == 2 && HG == 2 &&
+  return KS == 5 && rag_wgrad_slab_bf16() && H == 2 && HG == 2 &&
          5 * CINP >= COUTP && kRows + 4 <= kXRows;
 }
 
@@ -697,21 +478,6 @@ int rag_wgrad_slab_nchunks(int R, int CINP, int* spc, int KS, int pair5) {
   return (steps + s - 1) / s;
 }
 
-// ping-pong 192-channel kernel (RAG_WGRAD_PP=1, opt-in: measured slower, see wgrad_pp_kernel)
-static int g_wslab_pp = -1;
-static bool wslab_pp() {
-  if (g_wslab_pp < 0) {
-    const char* e = getenv("RAG_WGRAD_PP");
-    g_wslab_pp = e ? (atoi(e) != 0) : 0;
-  }
-  return g_wslab_pp != 0;
-}
-RAG_API int rag_wgrad_slab_pp(int on) {
-  const int old = g_wslab_pp;
-  g_wslab_pp = on;
-  return old;
-}
-static int g_wslab_nbuf = -1;  // RAG_WGRAD_NBUF (3..5), read on first use
 static int g_wslab_bf = -1;    // block-scaled fp16 partial slabs unless RAG_WGRAD_PART=fp32
 static int g_wslab_map = -1;   // wave -> tile map (WMap), RAG_WGRAD_MAP
 
@@ -764,25 +530,14 @@ WgradRed rag_wgrad_slab_red(const void* part, const float* bpart, float* dW, flo
   r.blk = KS == 5 ? 5 * COUTP * kC : ws_blk(COUTP);
   r.scale = part_scale((float*)part, nchunks * r.ntc, r.blk);
   r.map = (COUTP == kN && KS == 3) ? wslab_map() : 0;
-  if (COUTP == kN && KS == 3 && wslab_pp()) {  // wgrad_pp_kernel's layout
-    r.map = 2;
-    r.waves = kPPWaves;
-  }
   return r;
 }
 
-// Where the slab kernels issue a stage's LDS-DMA (prio bits 2-3; RAG_WGRAD_LATE): 1 (default)
-// after the first k-step's MFMAs -- SL 110.2-110.7k -> 113.5-114.0k positions/s on one box
-// (profiles/dma_placement_r4.txt) --, 2 after the second, 0 right after the stage barrier (the
-// round-3 placement: every wave's 2-3 issues delayed its first fragment reads of the stage).
-int wslab_late() {
-  static const int v = [] {
-    const char* e = getenv("RAG_WGRAD_LATE");
-    const int m = e ? atoi(e) : 1;
-    return (m >= 0 && m <= 3 ? m : 1) << 2;
-  }();
-  return v;
-}
+// Where the slab kernels issue a stage's LDS-DMA (prio bits 2-3): after the first k-step's MFMAs
+// -- SL 110.2-110.7k -> 113.5-114.0k positions/s on one box against right after the stage
+// barrier (profiles/dma_placement_r4.txt; "after the second" measured no better) -- and the
+// per-segment priority flips around the MFMAs (prio bits 0-1 = 0; none / static: no faster).
+constexpr int kWslabPrio = 1 << 2;
 
 int rag_launch_wgrad_slab_reduce(const WgradRed& r, hipStream_t stream) {
   const int octs = (int)((size_t)r.ntc * r.blk / 8);
@@ -791,19 +546,9 @@ int rag_launch_wgrad_slab_reduce(const WgradRed& r, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
-RAG_API int rag_wgrad_slab_nbuf(int n) {
-  const int old = g_wslab_nbuf;
-  g_wslab_nbuf = n;
-  return old;
-}
-
 int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpart, int R, int WP,
                           int GC, int CIN, int spc, int CINP, int nchunks, hipStream_t stream,
                           const float* xcoef, int S, int KS, int COUTP, int pair5) {
-  if (g_wslab_nbuf < 0) {
-    const char* e = getenv("RAG_WGRAD_NBUF");
-    g_wslab_nbuf = e ? atoi(e) : 3;
-  }
   const bool bf = rag_wgrad_slab_bf16();
   if (KS == 5) {  // per-row blocks, fp16 partials, map 0
     if (!bf || xcoef) return -5;
@@ -811,10 +556,10 @@ int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpar
     const dim3 g5(nchunks * (pair5 ? 8 : (CINP / kC) * 5));
     if (COUTP == 192)
       wgrad_slab_kernel<3, true, 0, 192, false, 5><<<g5, 768, 0, stream>>>(
-          G, X, part, bpart, R, WP, GC, CIN, spc, CINP, nullptr, 0, pair5, wslab_late());
+          G, X, part, bpart, R, WP, GC, CIN, spc, CINP, nullptr, 0, pair5, kWslabPrio);
     else if (COUTP == 128)
       wgrad_slab_kernel<3, true, 0, 128, false, 5><<<g5, 512, 0, stream>>>(
-          G, X, part, bpart, R, WP, GC, CIN, spc, CINP, nullptr, 0, pair5, wslab_late());
+          G, X, part, bpart, R, WP, GC, CIN, spc, CINP, nullptr, 0, pair5, kWslabPrio);
     else
       return -5;
     return (int)hipGetLastError();
@@ -824,44 +569,29 @@ int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpar
     if (CINP != 128 || !bf || S > 64) return -5;
     wgrad_slab_kernel<4, true, 0, 128, true><<<grid, 512, 0, stream>>>(G, X, part, bpart, R, WP,
                                                                        GC, CIN, spc, CINP, xcoef,
-                                                                       S, 0, wslab_late());
-    return (int)hipGetLastError();
-  }
-  if (CINP == kN && bf && wslab_pp()) {
-    wgrad_pp_kernel<3><<<grid, 512, 0, stream>>>(G, X, part, bpart, R, WP, GC, CIN, spc, CINP);
+                                                                       S, 0, kWslabPrio);
     return (int)hipGetLastError();
   }
   if (CINP == 128) {  // 8 waves, map 0
     if (bf)
       wgrad_slab_kernel<3, true, 0, 128><<<grid, 512, 0, stream>>>(G, X, part, bpart, R, WP, GC,
                                                                    CIN, spc, CINP, nullptr, 0, 0,
-                                                                   wslab_late());
+                                                                   kWslabPrio);
     else
       wgrad_slab_kernel<3, false, 0, 128><<<grid, 512, 0, stream>>>(G, X, part, bpart, R, WP, GC,
                                                                     CIN, spc, CINP);
     return (int)hipGetLastError();
   }
-  static const int wprio = [] {  // RAG_WGRAD_PRIO: 0 flips around MFMAs, 1 none, 2 static
-    const char* e = getenv("RAG_WGRAD_PRIO");
-    return (e ? atoi(e) : 0) | wslab_late();
-  }();
-#define RAG_WSLAB2(NB, BF, MP)                                                                 \
-  wgrad_slab_kernel<NB, BF, MP><<<grid, 64 * WS<kN>::Waves, 0, stream>>>(                      \
-      G, X, part, bpart, R, WP, GC, CIN, spc, CINP, nullptr, 0, 0, wprio)
-#define RAG_WSLAB(NB, BF) \
-  if (mp) RAG_WSLAB2(NB, BF, 1); else RAG_WSLAB2(NB, BF, 0)
+  // 192 channels: a 3-stage ring (4 / 5 measured no faster, deleted round 5); A/B axes: the
+  // fp32 partial slabs (RAG_WGRAD_PART=fp32) and the wave -> tile map (RAG_WGRAD_MAP=0)
+#define RAG_WSLAB(BF, MP)                                                                       \
+  wgrad_slab_kernel<3, BF, MP><<<grid, 64 * WS<kN>::Waves, 0, stream>>>(                       \
+      G, X, part, bpart, R, WP, GC, CIN, spc, CINP, nullptr, 0, 0, kWslabPrio)
   const int mp = wslab_map();
-  switch (g_wslab_nbuf) {
-    case 4:
-      if (bf) RAG_WSLAB(4, true); else RAG_WSLAB(4, false);
-      break;
-    case 5:
-      if (bf) RAG_WSLAB(5, true); else RAG_WSLAB(5, false);
-      break;
-    default:
-      if (bf) RAG_WSLAB(3, true); else RAG_WSLAB(3, false);
-  }
+  if (bf && mp) RAG_WSLAB(true, 1);
+  else if (bf) RAG_WSLAB(true, 0);
+  else if (mp) RAG_WSLAB(false, 1);
+  else RAG_WSLAB(false, 0);
 #undef RAG_WSLAB
-#undef RAG_WSLAB2
   return (int)hipGetLastError();
 }

@@ -71,17 +71,10 @@ SIGNATURES = {
     # ladder.hip
     "rag_ladder_workspace": [I, I],
     "rag_ladders": [P, P, I, I, P, P, P],
-    # conv_slab.hip
-    "rag_conv_slab_mode": [I],
     "rag_conv_order": [I],
     "rag_conv_tap_mode": [I],
-    "rag_conv_k2": [I],
-    "rag_conv_rs": [I],
-    "rag_conv_ep_lds": [I],
-    "rag_wgrad_slab_nbuf": [I],
     "rag_wgrad_slab_part_bf16": [I],
     "rag_wgrad_slab_map": [I],
-    "rag_wgrad_slab_pp": [I],
 }
 
 RESTYPES = {"rag_conv_wgrad_workspace": SZ, "rag_head_bwd_workspace": SZ,

@@ -85,9 +85,11 @@ def test_conv_backward(ops, B, cin, cout, ks, hi, hg, S):
     assert rel_err(db, bf(g).sum((0, 2, 3))) < 2e-2
 
 
-def test_conv_slab_residual(ops):
-    """The one-board-per-block slab kernel (conv_slab.hip, opt-in) vs fp32 PyTorch: residual
-    sum-merge epilogue, output halo 2 (stays zero), boards past B untouched, and dgrad."""
+def test_conv_residual_halo2_ragged_batch(ops):
+    """The default 3x3 dispatch at a ragged batch (B = 131: the 192-pixel kernels) vs fp32
+    PyTorch: residual sum-merge epilogue, output halo 2 (stays zero), boards past B untouched,
+    and dgrad. (The opt-in one-board-per-block slab kernel it used to force was deleted in
+    round 5.)"""
     dev = torch.device("cuda")
     torch.manual_seed(3)
     B, C, S = 131, 192, 19
@@ -102,22 +104,17 @@ def test_conv_slab_residual(ops):
     y[B:] = 7.0
     rp = ops.alloc_padded(B, S, 2, C, dev)
     rp[:, 2:-2, 2:-2] = ops.pack_nchw(r, 2, C)[:, 2:-2, 2:-2]
-    lib = ops._lib()
-    prev = lib.rag_conv_slab_mode(1)  # opt-in kernel (conv_slab.hip): force it for this test
-    try:
-        ops.conv_igemm(xp, wf, b, y[:B], B, S, 1, 2, C, C, 3, relu=True, residual=rp)
-        # dgrad form (ReLU mask of the layer input) through the slab kernel as well
-        wf2, wb2 = ops.pack_weights(w, C, C, wb=torch.empty(9, C, C, dtype=torch.bfloat16,
-                                                              device=dev))
-        g = torch.randn(B, C, S, S, device=dev)
-        xr = bf(F.relu(x)).requires_grad_()
-        F.conv2d(xr, bf(w), padding=1).mul(bf(g)).sum().backward()
-        xm = ops.pack_nchw(F.relu(x), 1, C)
-        dx = ops.alloc_padded(B, S, 1, C, dev)
-        ops.conv_igemm(ops.pack_nchw(g, 1, C), wb2, None, dx, B, S, 1, 1, C, C, 3, relu=False,
-                       mask=xm)
-    finally:
-        lib.rag_conv_slab_mode(prev)
+    ops.conv_igemm(xp, wf, b, y[:B], B, S, 1, 2, C, C, 3, relu=True, residual=rp)
+    # dgrad form (ReLU mask of the layer input)
+    wf2, wb2 = ops.pack_weights(w, C, C, wb=torch.empty(9, C, C, dtype=torch.bfloat16,
+                                                          device=dev))
+    g = torch.randn(B, C, S, S, device=dev)
+    xr = bf(F.relu(x)).requires_grad_()
+    F.conv2d(xr, bf(w), padding=1).mul(bf(g)).sum().backward()
+    xm = ops.pack_nchw(F.relu(x), 1, C)
+    dx = ops.alloc_padded(B, S, 1, C, dev)
+    ops.conv_igemm(ops.pack_nchw(g, 1, C), wb2, None, dx, B, S, 1, 1, C, C, 3, relu=False,
+                   mask=xm)
     assert rel_err(ops.unpack(dx, C, 1), xr.grad * (x > 0)) < 2e-2
     assert rel_err(ops.unpack(y[:B], C, 2), ref) < 2e-2
     assert y[:B, :2].abs().max().item() == 0 and y[:B, :, -2:].abs().max().item() == 0
@@ -537,44 +534,6 @@ def test_width128_pingpong_conv_and_wgrad_slab(ops):
         assert rel_err(ops.unpack(dx, C, 1), xr.grad * (x > 0)) < 2e-2
         assert rel_err(dw, wr.grad) < 1e-2, "round %d" % rnd
         assert rel_err(db, bf(g).sum((0, 2, 3))) < 1e-2, "round %d" % rnd
-
-
-@pytest.mark.gpu
-def test_wgrad_pingpong_matches_slab_kernel(ops):
-    """The ping-pong 192-channel wgrad (two wave groups alternating MFMA / fragment-read phases,
-    partial layout map 2) against the 12-wave slab kernel and fp32 PyTorch, deferred into a dgrad
-    and standalone, accumulating, at the bench shape (B = 256)."""
-    dev = torch.device("cuda")
-    torch.manual_seed(13)
-    B, C, S = 256, 192, 19
-    x = F.relu(torch.randn(B, C, S, S, device=dev))
-    g = torch.randn(B, C, S, S, device=dev)
-    w = torch.randn(C, C, 3, 3, device=dev) * 0.05
-    ref = torch.nn.grad.conv2d_weight(bf(x), (C, C, 3, 3), bf(g), padding=1)
-    xp, gp = ops.pack_nchw(x, 1, C), ops.pack_nchw(g, 1, C)
-    _, wb = ops.pack_weights(w, C, C, wb=torch.empty(9, C, C, dtype=torch.bfloat16, device=dev))
-    lib = ops._lib()
-    out = {}
-    for pp in (1, 0):
-        prev = lib.rag_wgrad_slab_pp(pp)
-        try:
-            dw = torch.full((C, C, 3, 3), 0.5, device=dev)
-            db = torch.full((C,), 0.5, device=dev)
-            ops.conv_wgrad(gp, xp, dw, db, B, S, 1, C, C, C, C, 3, accumulate=True, hg=1)
-            h = ops.PendingReduction()
-            ops.conv_wgrad(gp, xp, dw, db, B, S, 1, C, C, C, C, 3, accumulate=True, hg=1,
-                           defer=True, pending=h)
-            dx = ops.alloc_padded(B, S, 1, C, dev)
-            ops.conv_igemm(gp, wb, None, dx, B, S, 1, 1, C, C, 3, False, mask=xp, pending=h)
-            torch.cuda.synchronize()
-            out[pp] = (dw - 0.5, db - 0.5)
-        finally:
-            lib.rag_wgrad_slab_pp(prev)
-    for pp in (1, 0):
-        assert rel_err(out[pp][0], 2 * ref) < 1e-2
-        assert rel_err(out[pp][1], 2 * bf(g).sum((0, 2, 3))) < 1e-2
-    assert rel_err(out[1][0], out[0][0]) < 1e-3
-    assert rel_err(out[1][1], out[0][1]) < 1e-5
 
 
 @pytest.mark.gpu

@@ -29,7 +29,7 @@ def split(path):
         if not m:
             continue
         a = [x.strip() for x in m.group(1).split(',')]
-        if a[5] == '5':
+        if a[3] == '5':  # <NB, NT, BNP, KS, ...> (round 5 template)
             f5.append(d)
             state = 'f'
             continue
