@@ -4,8 +4,9 @@ The reference accumulates every playout into one root of one tree
 (/root/reference/AlphaGo/mcts.py:191-206) and leaves ``ParallelMCTS`` a stub (:219-220). An
 N-rank search with a total budget of T playouts is only worth N GPUs if it finds what one tree
 with T playouts finds. This module measures that, on the CPU with a deterministic evaluator
-(fixed random-init policy and value networks, value-only leaves, serial descents), so that the
-only difference between two searches is how the work is split:
+(fixed random-init policy and value networks, value-only leaves or — lmbda > 0 — rollouts
+seeded by the leaf position, so every design plays the same rollout from a given leaf), so that
+the only difference between two searches is how the work is split:
 
 * ``truth``: one tree with ``truth_mult`` x the largest budget;
 * the single-tree ladder: one tree with t, 2t, 4t, ... playouts (t = one rank's share);
@@ -98,6 +99,7 @@ def single_tree(pol, val, states, budget, batch, lmbda=0.0, seed=1):
     out, nodes = [], []
     for st in states:
         mc = ParallelMCTS(pol, val, n_playout=budget, seed=seed, **_search_kw(batch, lmbda))
+        mc.keyed_rollouts = True
         s = mc.search(st, budget)
         out.append(root_visits(s, st.size * st.size))
         nodes.append(len(s.expanded_keys()))
@@ -122,6 +124,9 @@ def _rank_worker(rank, world, port, outdir, cfg):
         if master:
             kw["rollout_delay"] = cfg.get("rollout_delay", 0)
         mc = cls(pol, val, dp=dp, n_playout=cfg["total"], **kw)
+        mc.keyed_rollouts = True
+        if hasattr(mc, "leaf_eval"):
+            mc.leaf_eval.keyed = True
         P = st.size * st.size
         if master and rank > 0:
             mc.serve()  # evaluates rank 0's waves until it stops
@@ -204,11 +209,25 @@ def study(worlds=(2, 4, 8), per_rank=128, batch=16, n_positions=50, size=9, trut
     if shipped:
         batch = shipped_waves(per_rank, 1)[0]
     top = ladder_top or per_rank * max(worlds)
-    truth, truth_nodes = single_tree(pol, val, states, top * truth_mult, batch, lmbda, seed=99)
+    # the single trees (truth and ladder) depend only on these: cached across studies that vary
+    # the N-rank search alone (e.g. its rollout delay)
+    ck = os.path.join(outdir, "single_%d_%d_%d_%d_%d_%g_%d_%d.npz" % (
+        n_positions, size, pos_seed, net_seed, batch, lmbda, top * truth_mult, per_rank))
+    cache = dict(np.load(ck)) if os.path.exists(ck) else {}
+
+    def single(budget, seed=1):
+        key = "b%d" % budget
+        if key not in cache:
+            v, nodes = single_tree(pol, val, states, budget, batch, lmbda, seed=seed)
+            cache[key], cache[key + "_n"] = v, nodes
+            np.savez(ck, **cache)
+        return cache[key], cache[key + "_n"]
+
+    truth, truth_nodes = single(top * truth_mult, seed=99)
     ladder, rows = [], {}
     b = per_rank
     while b <= top:
-        v, nodes = single_tree(pol, val, states, b, batch, lmbda)
+        v, nodes = single(b)
         k = kl(truth, v)
         ladder.append((b, k))
         rows["single_%d" % b] = {"budget": b, "kl": round(k, 4),

@@ -43,9 +43,12 @@ def _player_kind(player):
 class NativeSelfPlay(object):
     """Lock-step games of ``learner`` vs ``opponent`` (policy players on HIP models)."""
 
-    def __init__(self, learner, opponent, nthreads=16, pipeline=2):
+    def __init__(self, learner, opponent, nthreads=16, pipeline=None):
+        import os
         self.learner, self.opponent = learner, opponent
         self.nthreads = nthreads
+        if pipeline is None:
+            pipeline = int(os.environ.get("RAG_SELFPLAY_PIPELINE", "2"))
         self.pipeline = max(1, int(pipeline))
         self.device = learner.policy.model.device
         self._gf = {}
