@@ -23,6 +23,7 @@ def main(argv=None):
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=40)
     ap.add_argument("--size", type=int, default=19)
+    ap.add_argument("--channels", type=int, default=192, help="192 or 128 (the 128-wide tile)")
     ap.add_argument("--wcopies", type=int, default=1,
                     help="rotate over this many copies of the weights (cold L2, as in the step)")
     ap.add_argument("--xcopies", type=int, default=1,
@@ -31,7 +32,7 @@ def main(argv=None):
     from rocalphago_amd.ops import hipops as ops
     dev = torch.device("cuda")
     torch.manual_seed(0)
-    B, S, C = a.batch, a.size, 192
+    B, S, C = a.batch, a.size, a.channels
     x = torch.randn(B, C, S, S, device=dev).relu()
     w = torch.randn(C, C, 3, 3, device=dev) * 0.05
     g = torch.randn(B, C, S, S, device=dev)

@@ -760,7 +760,7 @@ RAG_API int rag_conv_wino_p(const void* X, const void* W, const float* bias, voi
   hipStream_t pend_stream = nullptr;
   const WgradRed* red = nullptr;
   if (take_pending(pending, &pend, &pend_stream)) {
-    if (pend_stream == stream && pend.ticket && NOUT == 192) {
+    if (pend_stream == stream && pend.ticket && (NOUT == 192 || NOUT == 128)) {  // 1-D grids
       red = &pend;
     } else {
       const int rc = rag_launch_wgrad_slab_reduce(pend, pend_stream);

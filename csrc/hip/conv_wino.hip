@@ -43,18 +43,35 @@ using namespace rag;
 namespace {
 
 constexpr int kWK = 32;                  // channels per chunk (MFMA K)
-constexpr int kWMT = 6, kWNT = 3;        // fragments per wave along pairs / output channels
-constexpr int kWP = 32 * kWMT;           // 192 output pairs per block (2 wave rows)
-constexpr int kWN = 64 * kWNT;           // 192 output channels per block (4 wave columns)
+constexpr int kWP = 192;                 // output pairs per block (a 19x19 board: 190)
 constexpr int kVRows = 224;              // V slab rows (a 19x19 board: 21 x 10 = 210)
 constexpr int kRRows = 512;              // raw rows a block may touch (19x19: 21 x 21 + 1)
 constexpr int kVSlot = kVRows * kWK;
 constexpr int kLoopLds = 4 * kVSlot;     // [2 chunk-phase buffers][2 sets]
-constexpr int kEpRow = kWN + 8;          // bf16 per row of the epilogue image
-constexpr int kEpImg = 2 * kWP * kEpRow; // one image row per output pixel (pair, column)
-constexpr int kLdsElems = kLoopLds > kEpImg ? kLoopLds : kEpImg;
 constexpr int kRedU = 14;                // chunk loads in flight per reduce thread
-static_assert(kLdsElems * 2 <= 160 * 1024, "LDS budget");
+
+// Output-tile geometry per block width WN (output channels per block): 8 waves = MW wave rows
+// along the 192 pairs x (8 / MW) wave columns along WN; per wave MT pair fragments x NT channel
+// fragments of both accumulator sets, its V fragments read in RG groups.
+//   WN = 192 (the north-star trunk): 2 x 4 waves of 96 pairs x 48 channels (18 MFMAs per 6 V
+//            fragment reads per set and step, 144 accumulator registers);
+//   WN = 128 (CNNPolicy's default width): 4 x 2 waves of 48 pairs x 64 channels (12 MFMAs per
+//            3 V reads: the 96 x 32 tile of the 192 layout would read twice as much LDS per MFMA).
+template <int WN> struct WinoGeo;
+template <> struct WinoGeo<192> {
+  static constexpr int MW = 2, MT = 6, NT = 3, RG = 2;
+};
+template <> struct WinoGeo<128> {
+  static constexpr int MW = 4, MT = 3, NT = 4, RG = 1;
+};
+template <int WN> struct WinoTile : WinoGeo<WN> {
+  using G = WinoGeo<WN>;
+  static_assert(G::MW * 16 * G::MT == kWP && (8 / G::MW) * 16 * G::NT == WN, "wave tiling");
+  static constexpr int EpRow = WN + 8;          // bf16 per row of the epilogue image
+  static constexpr int EpImg = 2 * kWP * EpRow;  // one image row per output pixel (pair, column)
+  static constexpr int Lds = kLoopLds > EpImg ? kLoopLds : EpImg;
+  static_assert(Lds * 2 <= 160 * 1024, "LDS budget");
+};
 
 __device__ __forceinline__ int swz4w(int row) { return ((row >> 2) & 1) << 1; }
 
@@ -87,16 +104,18 @@ __device__ __forceinline__ bf16x8 vdiff(const bf16x8& a, const bf16x8& b) { retu
 // Block (x, y): boards [x * nb, x * nb + nb), output channels [192 y, 192 y + 192).
 // SINGLE: one board per block (19x19): the V row of output pair m is m itself (pad pairs 190,
 // 191 read rows < 224 whose outputs are dropped), so no per-fragment row table is kept.
-template <bool SINGLE>
+template <int WN, bool SINGLE>
 __global__ void __launch_bounds__(512, 1)
 conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
                  const float* __restrict__ bias, bf16* __restrict__ Y,
                  const bf16* __restrict__ mask, int B, int S, int KIN, int NOUT, int HO, int YC,
                  int relu, int HM, int nb, WgradRed red) {
-  __shared__ __attribute__((aligned(16))) bf16 lds[kLdsElems];
+  using T = WinoTile<WN>;
+  constexpr int kWMT = T::MT, kWNT = T::NT, kWN = WN, kEpRow = T::EpRow;
+  __shared__ __attribute__((aligned(16))) bf16 lds[T::Lds];
   const int lane = lane_id();
   const int w = wave_id();
-  const int wm = w & 1, wn = w >> 1;
+  const int wm = w % T::MW, wn = w / T::MW;
   const int frow = lane & 15, fq = lane >> 4;
   const int WI = S + 2, TJ = (S + 1) >> 1;
   const int PB = S * TJ;    // output pairs per board
@@ -224,7 +243,7 @@ conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
     }
   // V fragments are read in two halves of three (12 registers instead of 24: with all six
   // live, hipcc spilled the transform's raw loads and waited for them at once)
-  constexpr int kH = kWMT / 2;
+  constexpr int kH = kWMT / T::RG;  // V fragments per read group
   bf16x8 xa[kH], wA[kWNT], wB[kWNT];
   auto read_v = [&](int kk, int ky, int set, int h) {
     const bf16* vs = lds + ((kk & 1) * 2 + set) * kVSlot;
@@ -309,14 +328,14 @@ conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
       __builtin_amdgcn_sched_barrier(0);
       // ---- set A
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
+      for (int h = 0; h < T::RG; ++h) {
         read_v(kk, ky, 0, h);
 #pragma unroll
         for (int j = 0; j < kWNT; ++j) {
 #pragma unroll
           for (int i = 0; i < kH; ++i)
             accA[j][h * kH + i] = mfma16(wA[j], xa[i], accA[j][h * kH + i]);
-          if (h == 1) wA[j] = wfrag(ntA, nc, j);
+          if (h == T::RG - 1) wA[j] = wfrag(ntA, nc, j);
         }
       }
       // (scheduling fences: hipcc otherwise reads set B's fragments into a second register set
@@ -330,14 +349,14 @@ conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
       __builtin_amdgcn_sched_barrier(0);
       // ---- set B
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
+      for (int h = 0; h < T::RG; ++h) {
         read_v(kk, ky, 1, h);
 #pragma unroll
         for (int j = 0; j < kWNT; ++j) {
 #pragma unroll
           for (int i = 0; i < kH; ++i)
             accB[j][h * kH + i] = mfma16(wB[j], xa[i], accB[j][h * kH + i]);
-          if (h == 1) wB[j] = wfrag(ntB, nc, j);
+          if (h == T::RG - 1) wB[j] = wfrag(ntB, nc, j);
         }
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -490,14 +509,22 @@ int wino_boards_per_block(int S) {
   return nb;
 }
 
+// Output channels per block for a layer of NOUT channels: 192-multiples take 192-wide tiles,
+// exactly 128 the 128-wide one (one board per block only), else 0 (no Winograd kernel).
+int wino_tile(int NOUT, int S) {
+  if (NOUT % 192 == 0) return 192;
+  if (NOUT == 128 && wino_boards_per_block(S) == 1) return 128;
+  return 0;
+}
+
 }  // namespace
 
 // True if conv_wino can run this layer: 3x3, input halo 1, input channels a multiple of 32 (at
-// most 12 chunks: nothing indexes past them), output channels a multiple of 192, a board that
-// fits the block's slabs.
+// most 12 chunks: nothing indexes past them), output channels a multiple of 192 or exactly 128,
+// a board that fits the block's slabs.
 RAG_API int rag_conv_wino_ok(int S, int HI, int KIN, int NOUT, int KS) {
-  return KS == 3 && HI == 1 && KIN % kWK == 0 && KIN >= kWK && NOUT % kWN == 0 && S >= 2 &&
-         wino_boards_per_block(S) >= 1;
+  return KS == 3 && HI == 1 && KIN % kWK == 0 && KIN >= kWK && S >= 2 &&
+         wino_boards_per_block(S) >= 1 && wino_tile(NOUT, S) > 0;
 }
 
 // True if conv_wino should take a layer of this batch rather than the direct kernel (given
@@ -516,7 +543,7 @@ RAG_API int rag_conv_wino_prefer(int B, int S, int KIN, int NOUT) {
       return 0;
     cus = n;
   }
-  const long blocks = (long)B * (NOUT / kWN);
+  const long blocks = (long)B * (NOUT / wino_tile(NOUT, S));
   const long waves = (blocks + cus - 1) / cus;
   return blocks * 8 >= waves * cus * 7;
 }
@@ -531,15 +558,20 @@ int rag_conv_wino_launch(const void* X, const void* W, const float* bias, void* 
   const int nb = wino_boards_per_block(S);
   WgradRed r{};
   if (red) r = *red;
-  const dim3 grid((B + nb - 1) / nb, NOUT / kWN);
-  if (nb == 1)
-    conv_wino_kernel<true><<<grid, 512, 0, stream>>>((const bf16*)X, (const bf16*)W, bias,
-                                                     (bf16*)Y, (const bf16*)mask, B, S, KIN, NOUT,
-                                                     HO, YC, relu, HM, nb, r);
+  const int wt = wino_tile(NOUT, S);
+  const dim3 grid((B + nb - 1) / nb, NOUT / wt);
+  if (wt == 128)
+    conv_wino_kernel<128, true><<<grid, 512, 0, stream>>>((const bf16*)X, (const bf16*)W, bias,
+                                                          (bf16*)Y, (const bf16*)mask, B, S, KIN,
+                                                          NOUT, HO, YC, relu, HM, nb, r);
+  else if (nb == 1)
+    conv_wino_kernel<192, true><<<grid, 512, 0, stream>>>((const bf16*)X, (const bf16*)W, bias,
+                                                          (bf16*)Y, (const bf16*)mask, B, S, KIN,
+                                                          NOUT, HO, YC, relu, HM, nb, r);
   else
-    conv_wino_kernel<false><<<grid, 512, 0, stream>>>((const bf16*)X, (const bf16*)W, bias,
-                                                      (bf16*)Y, (const bf16*)mask, B, S, KIN,
-                                                      NOUT, HO, YC, relu, HM, nb, r);
+    conv_wino_kernel<192, false><<<grid, 512, 0, stream>>>((const bf16*)X, (const bf16*)W, bias,
+                                                           (bf16*)Y, (const bf16*)mask, B, S, KIN,
+                                                           NOUT, HO, YC, relu, HM, nb, r);
   return (int)hipGetLastError();
 }
 

@@ -32,12 +32,14 @@ def ops():
     return hipops
 
 
-@pytest.mark.parametrize("B,S,ho", [(1, 19, 1), (3, 19, 2), (256, 19, 1), (3, 13, 1),
-                                    (5, 9, 1), (7, 7, 2)])
-def test_wino_forward_matches_fp32(ops, B, S, ho):
+@pytest.mark.parametrize("B,S,ho,C", [(1, 19, 1, 192), (3, 19, 2, 192), (256, 19, 1, 192),
+                                      (3, 13, 1, 192), (5, 9, 1, 192), (7, 7, 2, 192),
+                                      (3, 19, 1, 128), (256, 19, 2, 128)])
+def test_wino_forward_matches_fp32(ops, B, S, ho, C):
+    """192-wide tiles (one or several boards per block) and the 128-wide tile (CNNPolicy's
+    default width: 48 pairs x 64 channels per wave)."""
     dev = torch.device("cuda")
     torch.manual_seed(0)
-    C = 192
     assert ops.conv_wino_ok(S, 1, C, C, 3)
     x = F.relu(torch.randn(B, C, S, S, device=dev))
     w = torch.randn(C, C, 3, 3, device=dev) * 0.05
@@ -61,14 +63,14 @@ def test_wino_forward_matches_fp32(ops, B, S, ho):
     assert rel_norm(out, ops.unpack(yd, C, ho)) < 6e-3
 
 
-@pytest.mark.parametrize("B,S,ho", [(3, 19, 1), (2, 19, 2), (4, 13, 1)])
-def test_wino_dgrad_with_mask_matches_autograd(ops, B, S, ho):
+@pytest.mark.parametrize("B,S,ho,C", [(3, 19, 1, 192), (2, 19, 2, 192), (4, 13, 1, 192),
+                                      (3, 19, 1, 128)])
+def test_wino_dgrad_with_mask_matches_autograd(ops, B, S, ho, C):
     """dgrad form: the Winograd weights of the flipped, transposed kernel (Ub) and the ReLU
     mask of the layer input in the epilogue, output halo 1 or 2 (the SL trunk's layer-1 dgrad
     writes the 5x5 input layer's halo-2 gradient)."""
     dev = torch.device("cuda")
     torch.manual_seed(1)
-    C = 192
     x = F.relu(torch.randn(B, C, S, S, device=dev))
     w = torch.randn(C, C, 3, 3, device=dev) * 0.05
     g = torch.randn(B, C, S, S, device=dev)
