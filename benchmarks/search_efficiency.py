@@ -32,12 +32,13 @@ def main():
     from rocalphago_amd.search.efficiency import study
     for d in args.designs:
         # design suffixes: /split (per-rank wave = wave / N), /shipped (the bench's geometry:
-        # efficiency.shipped_waves)
+        # efficiency.shipped_waves), /capped (the same with the round capped at one GPU's wave)
         cls, _, opt = d.partition("/")
         r = study(worlds=tuple(args.ranks), per_rank=args.per_rank, batch=args.wave,
                   n_positions=args.positions, size=args.board, search_cls=cls,
                   outdir=os.path.join(args.out, d.replace("/", "_")), split_wave=opt == "split",
-                  shipped=opt == "shipped", lmbda=args.lmbda, rollout_delay=args.rollout_delay,
+                  shipped=opt in ("shipped", "capped"), capped=opt == "capped",
+                  lmbda=args.lmbda, rollout_delay=args.rollout_delay,
                   truth_mult=args.truth_mult)
         r["design"] = d
         print(json.dumps(r), flush=True)

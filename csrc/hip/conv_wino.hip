@@ -57,21 +57,28 @@ constexpr int kRedU = 14;                // chunk loads in flight per reduce thr
 //            fragment reads per set and step, 144 accumulator registers);
 //   WN = 128 (CNNPolicy's default width): 4 x 2 waves of 48 pairs x 64 channels (12 MFMAs per
 //            3 V reads: the 96 x 32 tile of the 192 layout would read twice as much LDS per MFMA).
-template <int WN> struct WinoGeo;
-template <> struct WinoGeo<192> {
+//   PAIRS = 96 (half a 19x19 board per block, WN = 192): 2 x 4 waves of 48 pairs x 48 channels
+//            -- batches of ~128 boards, whose one-board blocks would leave half the chip idle,
+//            run two blocks per board (V rows of the half plus two halo rows built by each).
+template <int WN, int PAIRS> struct WinoGeo;
+template <> struct WinoGeo<192, 192> {
   static constexpr int MW = 2, MT = 6, NT = 3, RG = 2;
 };
-template <> struct WinoGeo<128> {
+template <> struct WinoGeo<128, 192> {
   static constexpr int MW = 4, MT = 3, NT = 4, RG = 1;
 };
-template <int WN> struct WinoTile : WinoGeo<WN> {
-  using G = WinoGeo<WN>;
-  static_assert(G::MW * 16 * G::MT == kWP && (8 / G::MW) * 16 * G::NT == WN, "wave tiling");
-  static constexpr int EpRow = WN + 8;          // bf16 per row of the epilogue image
-  static constexpr int EpImg = 2 * kWP * EpRow;  // one image row per output pixel (pair, column)
+template <> struct WinoGeo<192, 96> {
+  static constexpr int MW = 2, MT = 3, NT = 3, RG = 1;
+};
+template <int WN, int PAIRS> struct WinoTile : WinoGeo<WN, PAIRS> {
+  using G = WinoGeo<WN, PAIRS>;
+  static_assert(G::MW * 16 * G::MT == PAIRS && (8 / G::MW) * 16 * G::NT == WN, "wave tiling");
+  static constexpr int EpRow = WN + 8;            // bf16 per row of the epilogue image
+  static constexpr int EpImg = 2 * PAIRS * EpRow;  // one image row per output pixel (pair, col)
   static constexpr int Lds = kLoopLds > EpImg ? kLoopLds : EpImg;
   static_assert(Lds * 2 <= 160 * 1024, "LDS budget");
 };
+constexpr int kHalfPairs = 96;
 
 __device__ __forceinline__ int swz4w(int row) { return ((row >> 2) & 1) << 1; }
 
@@ -104,14 +111,16 @@ __device__ __forceinline__ bf16x8 vdiff(const bf16x8& a, const bf16x8& b) { retu
 // Block (x, y): boards [x * nb, x * nb + nb), output channels [192 y, 192 y + 192).
 // SINGLE: one board per block (19x19): the V row of output pair m is m itself (pad pairs 190,
 // 191 read rows < 224 whose outputs are dropped), so no per-fragment row table is kept.
-template <int WN, bool SINGLE>
+template <int WN, bool SINGLE, int PAIRS = kWP>
 __global__ void __launch_bounds__(512, 1)
 conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
                  const float* __restrict__ bias, bf16* __restrict__ Y,
                  const bf16* __restrict__ mask, int B, int S, int KIN, int NOUT, int HO, int YC,
                  int relu, int HM, int nb, WgradRed red) {
-  using T = WinoTile<WN>;
+  using T = WinoTile<WN, PAIRS>;
   constexpr int kWMT = T::MT, kWNT = T::NT, kWN = WN, kEpRow = T::EpRow;
+  constexpr bool HALF = PAIRS == kHalfPairs;  // two blocks per board (SINGLE geometry)
+  static_assert(!HALF || SINGLE, "half-board blocks: one board");
   __shared__ __attribute__((aligned(16))) bf16 lds[T::Lds];
   const int lane = lane_id();
   const int w = wave_id();
@@ -121,8 +130,13 @@ conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
   const int PB = S * TJ;    // output pairs per board
   const int VPB = WI * TJ;  // V rows per board
   const int RPB = WI * WI;  // raw rows per board
-  const int b0 = blockIdx.x * nb;
+  const int b0 = HALF ? (int)(blockIdx.x >> 1) : (int)blockIdx.x * nb;
   const int n0 = blockIdx.y * kWN;
+  // HALF: this block's output pairs are [p0, p0 + 96) of the board; its V rows start at padded
+  // row i0 (V row of pair p at ky: p - i0 TJ + ky TJ)
+  const int p0 = HALF ? (int)(blockIdx.x & 1) * kHalfPairs : 0;
+  const int i0 = HALF ? p0 / TJ : 0;
+  const int voff = p0 - i0 * TJ;
   const long total_rows = (long)B * RPB;
   const int cchunks = KIN / kWK;
   const int NK = 2 * cchunks;  // chunk-phases
@@ -133,7 +147,7 @@ conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
   for (int i = 0; i < (SINGLE ? 1 : kWMT); ++i) {
     int m = wm * (16 * kWMT) + i * 16 + frow;
     if (SINGLE) {
-      vb[i] = m;
+      vb[i] = m + voff;
       continue;
     }
     m = m < nb * PB ? m : nb * PB - 1;  // pad pairs read a valid row, their output is dropped
@@ -167,13 +181,14 @@ conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
   // ---- transform units of this thread (the same for every chunk-phase): V row, 8-channel
   // group, raw row of d0 (named scalars: a runtime-indexed array went to scratch)
   // packed: V row (bits 0-9), 8-channel group (10-11), raw row of d0 (12-30), -1 = no unit
-  const int NU = nb * VPB * 4;
+  // (HALF: the V rows of padded rows i0 .. (last pair's row) + 2 only)
+  const int NU = HALF ? ((p0 + kHalfPairs - 1) / TJ - i0 + 3) * TJ * 4 : nb * VPB * 4;
   auto unit = [&](int it) {
     const int u = threadIdx.x + it * 512;
     const int v = u >> 2;
     const int bl = v / VPB, rem = v - bl * VPB;
     const int r = rem / TJ, t = rem - r * TJ;
-    const int rr = (bl * WI + r) * WI + 2 * t;
+    const int rr = (bl * WI + r + i0) * WI + 2 * t;
     return u < NU ? (v | ((u & 3) << 10) | (rr << 12)) : -1;
   };
   const int tu0 = unit(0), tu1 = unit(1);
@@ -412,12 +427,16 @@ conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
     const int nbl = B - b0 < nb ? B - b0 : nb;
     const int S2 = S * S, WO = S + 2 * HO, WMK = S + 2 * HM;
     constexpr int kChunks = kWN / 8;  // 16-byte chunks per pixel row
-    const int total = nbl * S2 * kChunks;
+    // HALF: the pixels of pairs [p0, min(p0 + 96, PB)) (2 per pair, the last column odd S)
+    const int pe = p0 + kHalfPairs < PB ? p0 + kHalfPairs : PB;
+    const int pixb = HALF ? (p0 / TJ) * S + 2 * (p0 % TJ) : 0;
+    const int pixe = HALF ? (pe / TJ) * S + 2 * (pe % TJ) : 0;
+    const int total = HALF ? ((pixe < S2 ? pixe : S2) - pixb) * kChunks : nbl * S2 * kChunks;
     for (int e = threadIdx.x; e < total; e += 512) {
-      const int pix = e / kChunks, k8 = (e - pix * kChunks) * 8;
-      const int bl = pix / S2, rem = pix - bl * S2;
+      const int pix = e / kChunks + pixb, k8 = (e - (e / kChunks) * kChunks) * 8;
+      const int bl = HALF ? 0 : pix / S2, rem = pix - bl * S2;
       const int i = rem / S, j = rem - i * S;
-      const int m = bl * PB + i * TJ + (j >> 1);
+      const int m = bl * PB + i * TJ + (j >> 1) - p0;
       bf16x8 v = *reinterpret_cast<const bf16x8*>(lds + (2 * m + (j & 1)) * kEpRow + k8);
       const int b = b0 + bl;
       if (mask) {
@@ -533,8 +552,12 @@ RAG_API int rag_conv_wino_ok(int S, int HI, int KIN, int NOUT, int KS) {
 // the CUs. The Winograd kernel's time is one fixed cost per wave (50.5 us at 19x19, 192 -> 192
 // on MI355X) against the direct kernel's per-pixel cost (57 us per 256 boards), so a ragged
 // last wave gives the gain back.
-RAG_API int rag_conv_wino_prefer(int B, int S, int KIN, int NOUT) {
-  if (!rag_conv_wino_ok(S, 1, KIN, NOUT, 3) || B <= 0 || wino_boards_per_block(S) != 1) return 0;
+// Half-board blocks (96 pairs, 192-wide tiles): boards of more than 96 and at most 192 pairs.
+static bool wino_half_ok(int S, int NOUT) {
+  const int TJ = (S + 1) / 2;
+  return NOUT % 192 == 0 && wino_boards_per_block(S) == 1 && S * TJ > kHalfPairs;
+}
+static int wino_cus() {
   static int cus = 0;
   if (!cus) {
     int dev = 0, n = 0;
@@ -543,9 +566,28 @@ RAG_API int rag_conv_wino_prefer(int B, int S, int KIN, int NOUT) {
       return 0;
     cus = n;
   }
-  const long blocks = (long)B * (NOUT / wino_tile(NOUT, S));
-  const long waves = (blocks + cus - 1) / cus;
-  return blocks * 8 >= waves * cus * 7;
+  return cus;
+}
+// 1: one-board blocks, 2: half-board blocks (a batch whose one-board grid would leave a ragged
+// last wave, e.g. the 128-board self-play plies, but whose half-board grid fills), 0: neither.
+static int wino_mode(int B, int S, int KIN, int NOUT) {
+  if (!rag_conv_wino_ok(S, 1, KIN, NOUT, 3) || B <= 0 || wino_boards_per_block(S) != 1) return 0;
+  const int cus = wino_cus();
+  if (!cus) return 0;
+  auto fills = [&](long blocks) {
+    const long waves = (blocks + cus - 1) / cus;
+    return blocks * 8 >= waves * cus * 7;
+  };
+  const long full = (long)B * (NOUT / wino_tile(NOUT, S));
+  if (fills(full)) return 1;
+  if (wino_half_ok(S, NOUT) && fills(2 * full)) return 2;
+  return 0;
+}
+RAG_API int rag_conv_wino_prefer(int B, int S, int KIN, int NOUT) {
+  return wino_mode(B, S, KIN, NOUT) != 0;
+}
+RAG_API int rag_conv_wino_mode(int B, int S, int KIN, int NOUT) {
+  return wino_mode(B, S, KIN, NOUT);
 }
 
 // Winograd 3x3 conv (forward or dgrad): X [B][S+2][S+2][KIN] bf16, U the layer's fragment-major
@@ -560,7 +602,11 @@ int rag_conv_wino_launch(const void* X, const void* W, const float* bias, void* 
   if (red) r = *red;
   const int wt = wino_tile(NOUT, S);
   const dim3 grid((B + nb - 1) / nb, NOUT / wt);
-  if (wt == 128)
+  if (wt == 192 && wino_mode(B, S, KIN, NOUT) == 2)  // two blocks per board
+    conv_wino_kernel<192, true, kHalfPairs><<<dim3(2 * B, NOUT / wt), 512, 0, stream>>>(
+        (const bf16*)X, (const bf16*)W, bias, (bf16*)Y, (const bf16*)mask, B, S, KIN, NOUT, HO,
+        YC, relu, HM, 1, r);
+  else if (wt == 128)
     conv_wino_kernel<128, true><<<grid, 512, 0, stream>>>((const bf16*)X, (const bf16*)W, bias,
                                                           (bf16*)Y, (const bf16*)mask, B, S, KIN,
                                                           NOUT, HO, YC, relu, HM, nb, r);

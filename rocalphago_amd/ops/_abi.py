@@ -30,6 +30,7 @@ SIGNATURES = {
     "rag_conv_wino_p": [P, P, P, P, P, I, I, I, I, I, I, I, I, P, P],
     "rag_wino_pack": [P, I, I, P],
     "rag_conv_wino_prefer": [I, I, I, I],
+    "rag_conv_wino_mode": [I, I, I, I],
     "rag_pack_input_u8": [P, P, P, P, I, I, I, I, I, I, P],
     "rag_pack_input_f32": [P, P, P, P, I, I, I, I, I, I, P],
     "rag_pack_input_bits": [P, P, P, P, I, I, I, I, I, P],

@@ -152,6 +152,12 @@ def conv_wino_prefer(B, S, kin, nout):
     return bool(_lib().rag_conv_wino_prefer(B, S, kin, nout))
 
 
+def conv_wino_mode(B, S, kin, nout):
+    """How conv_wino runs batch B: 1 one-board blocks, 2 half-board blocks (two per board:
+    batches whose one-board grid would leave the chip half idle), 0 not preferred."""
+    return int(_lib().rag_conv_wino_mode(B, S, kin, nout))
+
+
 def wino_pack(table, nlayers, max_tiles):
     """Winograd weights of 3x3 layers from their fp32 OIHW masters in one launch. ``table``:
     device int64 [nlayers, 8] = (W, cout, cin, coutp, cinp, Uf, Ub or 0, 0); Uf (forward, N =

@@ -526,6 +526,9 @@ class ParallelMCTS(object):
         s.pass_prior = has_pass_logit(getattr(self.evaluator, "policy", None))
         s.c_puct = self.c_puct
         s.lmbda = self.lmbda
+        # CPU rollouts seeded by the leaf position instead of (seed, wave, index): every search
+        # that reaches a position plays the same rollout from it (search/efficiency.py)
+        s.keyed_rollouts = bool(getattr(self, "keyed_rollouts", False))
         s.n_vl = self.virtual_loss
         s.rollout_limit = self.rollout_limit
         s.max_depth = self.playout_depth

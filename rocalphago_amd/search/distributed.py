@@ -30,8 +30,9 @@ DistributedMCTS (``mode="master"``) — one tree on rank 0, leaf evaluation spre
     planes with the HIP feature kernel, runs the policy and value networks and starts the wave's
     fast rollouts on its rollout streams (WaveEvaluator). It returns the priors, values and
     sensible-move masks of this round's wave and the rollout results of the wave it started
-    ``rollout_delay`` rounds earlier (rollouts take longer than a network pass; the native tree
-    keeps such a wave's virtual loss until its rollout backup, as in the single-GPU pipeline);
+    ``rollout_delay`` rounds earlier at the latest -- as soon as they are done, usually the next
+    round or two (rollouts take longer than a network pass; the native tree keeps such a wave's
+    virtual loss until its rollout backup, as in the single-GPU pipeline);
   * results come back to rank 0 with one gather; it backs them up and selects the next round.
 
 So the tree, the selection and the backups stay on one host (no tree synchronisation), and all
@@ -113,6 +114,7 @@ class WaveEvaluator(object):
         self.R = int(rollouts_per_leaf)
         self.limit = int(rollout_limit)
         self.nthreads = nthreads
+        self.keyed = False  # CPU rollouts seeded by the leaf position (search/efficiency.py)
         model = net.policy if net.policy is not None else net.value
         inner = getattr(getattr(model, "model", None), "net", None)  # (None: a host evaluator)
         self.device = inner.device if inner is not None else torch.device("cpu")
@@ -203,7 +205,8 @@ class WaveEvaluator(object):
             ev, _, _, _, host = self._gro._launch(colors, meta8, S, komi, self.R, self.limit,
                                                   seed)
             return _Pending(ev, host, colors.shape[0], self.R)
-        win = self.rollout.rollouts(boards, seed=seed, limit=self.limit, nthreads=self.nthreads)
+        win = self.rollout.rollouts(boards, seed=seed, limit=self.limit, nthreads=self.nthreads,
+                                    keyed=self.keyed)
         z = np.where(win == go.BLACK, 1.0, np.where(win == go.WHITE, -1.0, 0.0))
         return _Done(z.astype(np.float32))
 
@@ -331,7 +334,13 @@ class DistributedMCTS(ParallelMCTS):
             if v is not None:
                 out[:n, PW + P] = v
         meta[0] = n
-        if self._pending and (self._pending[0][0] <= rnd - self.delay or n == 0):
+        # the oldest pending rollout wave comes back as soon as it is done (its leaves keep
+        # their virtual loss until then), and at the latest `rollout_delay` rounds after it was
+        # shipped (then this collect waits for it)
+        # (never a wave shipped after the collected round: rank 0 backs its values up first)
+        if self._pending and self._pending[0][0] <= rnd and (
+                self._pending[0][0] <= rnd - self.delay or n == 0 or
+                getattr(self._pending[0][1], "done", lambda: True)()):
             zr, pend = self._pending.popleft()
             z = pend.result()
             out[:len(z), PW + P + 1] = z

@@ -74,13 +74,15 @@ def _search_kw(batch, lmbda=0.0):
                 rollout_limit=200)
 
 
-def shipped_waves(per_rank, world, bench_budget=8192, bench_wave=512, bench_min=128):
+def shipped_waves(per_rank, world, bench_budget=8192, bench_wave=512, bench_min=128, cap=False):
     """(single-tree wave, per-rank wave at N = world) of the bench's geometry scaled to a study
     budget: the bench searches 8192 playouts per GPU per move with 512-leaf waves on one GPU and
     max(128, 512 / N) leaves per rank and round on N GPUs (benchmarks/mcts_bench.py
     distributed_wave); the study keeps the same leaves-in-flight to budget ratios."""
     w1 = max(1, int(round(per_rank * bench_wave / bench_budget)))
     wmin = max(1, int(round(per_rank * bench_min / bench_budget)))
+    if cap:  # the round's leaves capped at the one-GPU wave (no per-GPU minimum)
+        return w1, max(1, w1 // world)
     return w1, max(wmin, w1 // world)
 
 
@@ -197,7 +199,8 @@ def equivalent_budget(ladder, k):
 
 def study(worlds=(2, 4, 8), per_rank=128, batch=16, n_positions=50, size=9, truth_mult=4,
           search_cls="SharedRootMCTS", outdir="/tmp/rag_eff", pos_seed=0, net_seed=3,
-          ladder_top=None, split_wave=False, lmbda=0.0, rollout_delay=0, shipped=False):
+          ladder_top=None, split_wave=False, lmbda=0.0, rollout_delay=0, shipped=False,
+          capped=False):
     """The whole comparison; returns a JSON-able dict. ``split_wave``: the N-rank search's
     per-rank wave is batch / N (the job keeps the one-GPU search's leaves in flight per round
     instead of N times as many). ``shipped``: the bench's geometry instead (shipped_waves: the
@@ -241,7 +244,7 @@ def study(worlds=(2, 4, 8), per_rank=128, batch=16, n_positions=50, size=9, trut
         d = os.path.join(outdir, "%s_w%d" % (search_cls, w))
         os.makedirs(d, exist_ok=True)
         if shipped:
-            wcfg = dict(cfg, batch=shipped_waves(per_rank, w)[1])
+            wcfg = dict(cfg, batch=shipped_waves(per_rank, w, cap=capped)[1])
         else:
             wcfg = dict(cfg, batch=max(1, batch // w)) if split_wave else cfg
         vis, dup = multi_rank(w, per_rank * w, wcfg, d)
@@ -256,4 +259,5 @@ def study(worlds=(2, 4, 8), per_rank=128, batch=16, n_positions=50, size=9, trut
     return {"positions": n_positions, "board": size, "per_rank_playouts": per_rank,
             "wave": batch, "truth_budget": top * truth_mult, "search": search_cls,
             "lmbda": lmbda, "rollout_delay": rollout_delay, "shipped_geometry": bool(shipped),
+            "capped": bool(capped),
             "truth_nodes": float(truth_nodes.mean()), "rows": rows}

@@ -34,10 +34,12 @@ def ops():
 
 @pytest.mark.parametrize("B,S,ho,C", [(1, 19, 1, 192), (3, 19, 2, 192), (256, 19, 1, 192),
                                       (3, 13, 1, 192), (5, 9, 1, 192), (7, 7, 2, 192),
-                                      (3, 19, 1, 128), (256, 19, 2, 128)])
+                                      (3, 19, 1, 128), (256, 19, 2, 128), (128, 19, 1, 192),
+                                      (120, 19, 2, 192)])
 def test_wino_forward_matches_fp32(ops, B, S, ho, C):
-    """192-wide tiles (one or several boards per block) and the 128-wide tile (CNNPolicy's
-    default width: 48 pairs x 64 channels per wave)."""
+    """192-wide tiles (one or several boards per block), the 128-wide tile (CNNPolicy's
+    default width: 48 pairs x 64 channels per wave) and half-board blocks (B = 120, 128 on 256
+    CUs: two 96-pair blocks per board)."""
     dev = torch.device("cuda")
     torch.manual_seed(0)
     assert ops.conv_wino_ok(S, 1, C, C, 3)
@@ -45,6 +47,8 @@ def test_wino_forward_matches_fp32(ops, B, S, ho, C):
     w = torch.randn(C, C, 3, 3, device=dev) * 0.05
     b = torch.randn(C, device=dev) * 0.1
     ref = F.relu(F.conv2d(bf(x), bf(w), b, padding=1))
+    if B in (120, 128) and ops.conv_wino_mode(B, S, C, C) != 2:
+        pytest.skip("half-board blocks are chosen for B = %d on 256 CUs only" % B)
     xp = ops.pack_nchw(x, 1, C)
     uf, _ = ops.wino_weights(w, C, C, dgrad=False)
     # one extra board past B: the kernel must not touch it
@@ -64,7 +68,7 @@ def test_wino_forward_matches_fp32(ops, B, S, ho, C):
 
 
 @pytest.mark.parametrize("B,S,ho,C", [(3, 19, 1, 192), (2, 19, 2, 192), (4, 13, 1, 192),
-                                      (3, 19, 1, 128)])
+                                      (3, 19, 1, 128), (128, 19, 2, 192)])
 def test_wino_dgrad_with_mask_matches_autograd(ops, B, S, ho, C):
     """dgrad form: the Winograd weights of the flipped, transposed kernel (Ub) and the ReLU
     mask of the layer input in the epilogue, output halo 1 or 2 (the SL trunk's layer-1 dgrad
