@@ -63,14 +63,17 @@ def measure(device, playouts=8192, warmup=512, moves=1, **kw):
 
 
 def distributed_wave(world, mode="master"):
-    """Leaves per rank and round of the N-GPU search. master: the round (N waves) keeps about
-    the one-GPU search's leaves in flight (512-leaf waves) -- N x 512 per round would search
-    like one tree with N-times-wider waves (budget efficiency 0.24 at N = 8 in
-    search/efficiency.py's study, 1.0 with the split) -- but at least 128 leaves per GPU pass.
-    shared: every rank runs the one-GPU search."""
+    """Leaves per rank and round of the N-GPU search. master: the round (N waves) keeps the
+    one-GPU search's 512 leaves in flight -- N x 512 per round would search like one tree with
+    N-times-wider waves (budget efficiency 0.24 at N = 8 in search/efficiency.py's study) --
+    down to 64 leaves per GPU pass. With at least 128 per GPU (round 4) N = 8 ran 1024 leaves per
+    round and measured 0.63 at the bench's geometry (lambda 0.5, rollouts); capped at 512 it
+    measures 0.81 (profiles/search_efficiency_r5.json), and rank 0's tree work per simulation,
+    which bounds the N = 8 rate, is the same either way. shared: every rank runs the one-GPU
+    search."""
     if mode != "master" or world <= 1:
         return 512
-    return max(128, 512 // world)
+    return max(64, 512 // world)
 
 
 def measure_distributed(dp, device, playouts=8192, warmup=512, moves=1, filters=192,

@@ -301,3 +301,18 @@ def test_search_budget_efficiency_two_ranks(tmp_path):
                    search_cls="SharedRootMCTS", outdir=str(tmp_path / "s"))
     sr = shared["rows"]["SharedRootMCTS_2"]
     assert sr["duplication"] > 1.5 and sr["efficiency"] <= 0.75, shared["rows"]
+
+
+def test_search_budget_efficiency_shipped_geometry_two_ranks(tmp_path):
+    """the one-tree 2-rank search at the geometry the bench ships (lambda 0.5
+    with rollouts seeded by the leaf position, rollout results returned as soon as done with
+    rollout_delay 6 as the cap, per-rank waves scaled from the 19x19 bench) is worth two ranks:
+    budget efficiency >= 0.85 against a truth of 8x the largest budget (deterministic; the full
+    48-position study is profiles/search_efficiency_r5.json: 0.95 / 0.86 / 0.81 at N = 2 / 4 / 8)."""
+    from rocalphago_amd.search.efficiency import study
+    r = study(worlds=(2,), per_rank=256, n_positions=16, truth_mult=8,
+              search_cls="DistributedMCTS", outdir=str(tmp_path), lmbda=0.5, rollout_delay=6,
+              shipped=True)
+    row = r["rows"]["DistributedMCTS_2"]
+    assert row["duplication"] == 1.0
+    assert row["efficiency"] >= 0.85, r["rows"]
