@@ -308,7 +308,8 @@ def test_search_budget_efficiency_shipped_geometry_two_ranks(tmp_path):
     with rollouts seeded by the leaf position, rollout results returned as soon as done with
     rollout_delay 6 as the cap, per-rank waves scaled from the 19x19 bench) is worth two ranks:
     budget efficiency >= 0.85 against a truth of 8x the largest budget (deterministic; the full
-    48-position study is profiles/search_efficiency_r5.json: 0.95 / 0.86 / 0.81 at N = 2 / 4 / 8)."""
+    48-position study is profiles/search_efficiency_r5.json: 0.95 / 0.86 / 0.81 at N = 2 / 4 /
+    8)."""
     from rocalphago_amd.search.efficiency import study
     r = study(worlds=(2,), per_rank=256, n_positions=16, truth_mult=8,
               search_cls="DistributedMCTS", outdir=str(tmp_path), lmbda=0.5, rollout_delay=6,

@@ -140,7 +140,8 @@ def test_north_star_sl_step_matches_fp32(cuda, augment, defer, monkeypatch):
         init) differs by ~5 %, and without the Winograd roundings the top layers' weight
         gradients by ~3.6 % (same cancellation: ~0.35 % noise in g, amplified ~10x).
     (b) an independent fp32 forward + backward (bf16-rounded weights / layer inputs) with the
-        Winograd layers' forward (and dgrad) rounded as the kernels round them — within 0.25. Its forward activations differ from the kernels' by 0.2-0.6 % (accumulation order
+        Winograd layers' forward (and dgrad) rounded as the kernels round them — within 0.25.
+        Its forward activations differ from the kernels' by 0.2-0.6 % (accumulation order
         changes bf16 roundings, scripts/dbg/bench_path_err.py), and at random init the 12-layer
         trunk's activations are nearly constant over the board, so the gradient
         sum_p x(p) (p(p) - y(p)) cancels to a few % of its terms and amplifies that into ~12 %
