@@ -1,7 +1,7 @@
 """Direct (conv_tap_pp) vs Winograd F(2,3) (conv_wino) 3x3 192->192 kernels, forward and dgrad
 (+ ReLU mask), interleaved rounds in one process (guide §5.4 rule 24), on random data.
 
-    python benchmarks/wino_bench.py [--batch 256] [--rounds 5] [--iters 40]
+    python benchmarks/wino_bench.py [--batch 256 [128 64 ...]] [--rounds 5] [--iters 40]
                                     [--wcopies 16] [--xcopies 8]
 
 Prints one JSON line: median / min microseconds per launch of every (kernel, pass), the
@@ -19,7 +19,8 @@ import torch  # noqa: E402
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--batch", type=int, nargs="+", default=[256],
+                    help="one JSON line per batch (small batches: the self-play tail)")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=40)
     ap.add_argument("--size", type=int, default=19)
@@ -29,10 +30,15 @@ def main(argv=None):
     ap.add_argument("--xcopies", type=int, default=1,
                     help="rotate over this many copies of the inputs (beyond the 256 MB MALL)")
     a = ap.parse_args(argv)
+    for B in a.batch:
+        run(a, B)
+
+
+def run(a, B):
     from rocalphago_amd.ops import hipops as ops
     dev = torch.device("cuda")
     torch.manual_seed(0)
-    B, S, C = a.batch, a.size, a.channels
+    S, C = a.size, a.channels
     x = torch.randn(B, C, S, S, device=dev).relu()
     w = torch.randn(C, C, 3, 3, device=dev) * 0.05
     g = torch.randn(B, C, S, S, device=dev)
@@ -46,7 +52,7 @@ def main(argv=None):
     ufs, ubs = [uf] + [uf.clone() for _ in range(a.wcopies - 1)], \
         [ub] + [ub.clone() for _ in range(a.wcopies - 1)]
     bias = torch.randn(C, device=dev) * 0.1
-    y = {k: ops.alloc_padded(B, S, 1, C, dev) for k in ("fd", "fw", "dd", "dw")}
+    y = {k: ops.alloc_padded(B, S, 1, C, dev) for k in ("fd", "fw", "fh", "dd", "dw")}
     it = {}
 
     def nxt(v):
@@ -58,6 +64,9 @@ def main(argv=None):
                                              C, 3, True),
         "fwd_wino": lambda: ops.conv_wino(nxt(xps), nxt(ufs), bias, y["fw"], B, S, C, C, 1,
                                           True),
+        # half-board blocks (two per board) at any batch (192-wide tiles)
+        "fwd_wino_half": lambda: ops.conv_wino(nxt(xps), nxt(ufs), bias, y["fh"], B, S, C, C, 1,
+                                               True, half=True),
         "dgrad_direct": lambda: ops.conv_igemm(nxt(gps), nxt(wbs), None, y["dd"], B, S, 1, 1, C,
                                                C, 3, False, mask=xp),
         "dgrad_wino": lambda: ops.conv_wino(nxt(gps), nxt(ubs), None, y["dw"], B, S, C, C, 1,
@@ -88,6 +97,7 @@ def main(argv=None):
         return round(((p - q).norm() / q.norm()).item(), 5)
 
     out["fwd_rel_diff"] = rel(y["fw"], y["fd"])
+    out["fwd_half_rel_diff"] = rel(y["fh"], y["fd"])
     out["dgrad_rel_diff"] = rel(y["dw"], y["dd"])
     print(json.dumps(out))
 

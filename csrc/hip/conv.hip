@@ -752,23 +752,56 @@ RAG_API int rag_conv_igemm_bn(const void* X, const void* W, const float* bias, v
 // the grid is one-dimensional; otherwise it goes out on its own first.
 int rag_conv_wino_launch(const void* X, const void* W, const float* bias, void* Y,
                          const void* mask, int B, int S, int KIN, int NOUT, int HO, int YC,
-                         int relu, int HM, hipStream_t stream, const WgradRed* red);
+                         int relu, int HM, hipStream_t stream, const WgradRed* red, int half);
+// The pending reduction of `pending` for a Winograd launch of NOUT channels on `stream`: it rides
+// (returned in *pend, *red = pend) when it has claim counters and the grid is one-dimensional,
+// else it goes out on its own now. Returns that launch's error code (0).
+static int wino_pending(void* pending, hipStream_t stream, int NOUT, WgradRed* pend,
+                        const WgradRed** red) {
+  hipStream_t pend_stream = nullptr;
+  *red = nullptr;
+  if (!take_pending(pending, pend, &pend_stream)) return 0;
+  if (pend_stream == stream && pend->ticket && (NOUT == 192 || NOUT == 128)) {  // 1-D grids
+    *red = pend;
+    return 0;
+  }
+  return rag_launch_wgrad_slab_reduce(*pend, pend_stream);
+}
+
 RAG_API int rag_conv_wino_p(const void* X, const void* W, const float* bias, void* Y,
                             const void* mask, int B, int S, int KIN, int NOUT, int HO, int YC,
-                            int relu, int HM, hipStream_t stream, void* pending) {
+                            int relu, int HM, hipStream_t stream, void* pending, int half) {
   WgradRed pend;
-  hipStream_t pend_stream = nullptr;
   const WgradRed* red = nullptr;
-  if (take_pending(pending, &pend, &pend_stream)) {
-    if (pend_stream == stream && pend.ticket && (NOUT == 192 || NOUT == 128)) {  // 1-D grids
-      red = &pend;
-    } else {
-      const int rc = rag_launch_wgrad_slab_reduce(pend, pend_stream);
-      if (rc) return rc;
-    }
-  }
+  if (const int rc = wino_pending(pending, stream, NOUT, &pend, &red)) return rc;
   return rag_conv_wino_launch(X, W, bias, Y, mask, B, S, KIN, NOUT, HO, YC, relu, HM, stream,
-                              red);
+                              red, half);
+}
+
+// Winograd 3x3 conv with the fused BatchNorm of the residual trunk (conv_wino.hip WinoBN):
+// forward with `coef` (X = the BN input, U = ReLU(coef[0][col] x + coef[2][col]) built in the
+// transform; `resid` optional) or dgrad with `mcoef` (mask = x); `spart` [B][2][S] per-board
+// column statistics (forward: sum y, sum y^2; dgrad with smean: sum dU, sum dU (x - mean)).
+// -5 when rag_conv_wino_bn_ok is false for the shape or the argument set has no kernel.
+int rag_conv_wino_bn_launch(const void* X, const void* W, const float* bias, void* Y,
+                            const void* mask, const void* res, int B, int S, int KIN, int NOUT,
+                            int HO, int YC, int relu, int HM, hipStream_t stream,
+                            const WgradRed* red, const float* coef, const float* mcoef,
+                            float* spart, const float* smean);
+RAG_API int rag_conv_wino_bn_ok(int B, int S, int KIN, int NOUT);
+RAG_API int rag_conv_wino_bn(const void* X, const void* W, const float* bias, void* Y,
+                             const void* mask, const void* resid, int B, int S, int KIN, int NOUT,
+                             int HO, int YC, int relu, int HM, hipStream_t stream, void* pending,
+                             const float* coef, const float* mcoef, float* spart,
+                             const float* smean) {
+  if (!rag_conv_wino_bn_ok(B, S, KIN, NOUT) || YC < NOUT || (coef != nullptr) == (mcoef != nullptr) ||
+      (mcoef && (!mask || resid)) || (smean && !mcoef))
+    return -5;  // (checked before the pending reduction is taken)
+  WgradRed pend;
+  const WgradRed* red = nullptr;
+  if (const int rc = wino_pending(pending, stream, NOUT, &pend, &red)) return rc;
+  return rag_conv_wino_bn_launch(X, W, bias, Y, mask, resid, B, S, KIN, NOUT, HO, YC, relu, HM,
+                                 stream, red, coef, mcoef, spart, smean);
 }
 
 // Partial rows rag_conv_igemm_bn writes to `spart` (one per convolution block).

@@ -104,6 +104,40 @@ __device__ __forceinline__ bf16x8 vaddsub(const bf16x8& a, const bf16x8& b) {
 }
 __device__ __forceinline__ bf16x8 vsum(const bf16x8& a, const bf16x8& b) { return vaddsub<1>(a, b); }
 __device__ __forceinline__ bf16x8 vdiff(const bf16x8& a, const bf16x8& b) { return vaddsub<-1>(a, b); }
+// The same with the BN prologue (ResnetPolicy): the raw values are BN inputs x and
+// the transform runs on U = ReLU(cx x + cc) of each column (cx = cc = 0 on halo pixels: U = 0),
+// kept in fp32 up to the one rounding of V
+template <int SGN>
+__device__ __forceinline__ bf16x8 vaddsub_bn(const bf16x8& a, const bf16x8& b, float cxa,
+                                             float cca, float cxb, float ccb) {
+  const u32x4 ua = __builtin_bit_cast(u32x4, a), ub = __builtin_bit_cast(u32x4, b);
+  u32x4 o;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const float a0 = fmaxf(fmaf(cxa, __uint_as_float(ua[w] << 16), cca), 0.f);
+    const float a1 = fmaxf(fmaf(cxa, __uint_as_float(ua[w] & 0xffff0000u), cca), 0.f);
+    const float b0 = fmaxf(fmaf(cxb, __uint_as_float(ub[w] << 16), ccb), 0.f);
+    const float b1 = fmaxf(fmaf(cxb, __uint_as_float(ub[w] & 0xffff0000u), ccb), 0.f);
+    const bf16x2 r = {(bf16)(SGN > 0 ? a0 + b0 : a0 - b0), (bf16)(SGN > 0 ? a1 + b1 : a1 - b1)};
+    o[w] = __builtin_bit_cast(uint32_t, r);
+  }
+  return __builtin_bit_cast(bf16x8, o);
+}
+
+// Fused BatchNorm of the 128-channel residual trunk (BNM template argument of conv_wino_kernel):
+//   BNM 1 (forward): X is the BN input x, the layer input U = ReLU(coef[0][col] x + coef[2][col])
+//          is built in the transform (never stored); `res` (or null) is added to the output; with
+//          spart, the block's (sum y, sum y^2) per board column of the stored output;
+//   BNM 2 (dgrad): the ReLU mask of U is recomputed from mask = x and coef; with spart,
+//          (sum dU, sum dU (x - smean)) per column of the masked output.
+// spart: [gridDim.x][2][S] fp32 partials (one row pair per block = per board) for bn.hip's
+// finalize, as conv_tap_pp_kernel's BNP / mcoef / spart forms on the direct kernel.
+struct WinoBN {
+  const float* coef;
+  const bf16* res;
+  float* spart;
+  const float* smean;
+};
 
 // X: padded input [B][S+2][S+2][KIN] (halo 1). U: Winograd weights, fragment-major
 // [12 = (ky, q)][KIN / 32][NOUT / 16][64 lanes][8] (rag_wino_pack). Y: padded output (halo HO,
@@ -111,17 +145,23 @@ __device__ __forceinline__ bf16x8 vdiff(const bf16x8& a, const bf16x8& b) { retu
 // Block (x, y): boards [x * nb, x * nb + nb), output channels [192 y, 192 y + 192).
 // SINGLE: one board per block (19x19): the V row of output pair m is m itself (pad pairs 190,
 // 191 read rows < 224 whose outputs are dropped), so no per-fragment row table is kept.
-template <int WN, bool SINGLE, int PAIRS = kWP>
+template <int WN, bool SINGLE, int PAIRS = kWP, int BNM = 0>
 __global__ void __launch_bounds__(512, 1)
 conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
                  const float* __restrict__ bias, bf16* __restrict__ Y,
                  const bf16* __restrict__ mask, int B, int S, int KIN, int NOUT, int HO, int YC,
-                 int relu, int HM, int nb, WgradRed red) {
+                 int relu, int HM, int nb, WgradRed red, WinoBN bn = WinoBN{}) {
   using T = WinoTile<WN, PAIRS>;
   constexpr int kWMT = T::MT, kWNT = T::NT, kWN = WN, kEpRow = T::EpRow;
   constexpr bool HALF = PAIRS == kHalfPairs;  // two blocks per board (SINGLE geometry)
   static_assert(!HALF || SINGLE, "half-board blocks: one board");
-  __shared__ __attribute__((aligned(16))) bf16 lds[T::Lds];
+  static_assert(BNM == 0 || (SINGLE && !HALF && WN == 128), "fused BN: the 128-wide one-board tile");
+  // + a [2][64] float column-statistics accumulator past the loop ring / epilogue image
+  __shared__ __attribute__((aligned(16))) bf16 lds[T::Lds + (BNM ? 256 : 0)];
+  float* sred = reinterpret_cast<float*>(lds + T::Lds);
+  if constexpr (BNM != 0) {
+    if (bn.spart && threadIdx.x < 128) sred[threadIdx.x] = 0.f;  // published by the first barrier
+  }
   const int lane = lane_id();
   const int w = wave_id();
   const int wm = w % T::MW, wn = w / T::MW;
@@ -192,6 +232,25 @@ conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
     return u < NU ? (v | ((u & 3) << 10) | (rr << 12)) : -1;
   };
   const int tu0 = unit(0), tu1 = unit(1);
+  // BNM 1: per transform unit, the BN coefficients of its four raw columns d0..d3 (zero on halo
+  // pixels and for a missing unit, so U = 0 there)
+  float bcx[2][4], bcc[2][4];
+  if constexpr (BNM == 1) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int pk = q ? tu1 : tu0;
+      const int v = pk < 0 ? 0 : (pk & 1023);
+      const int r = v / TJ, t = v - r * TJ;  // padded row r, pair column t (one board)
+      const bool rin = pk >= 0 && r >= 1 && r <= S;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int pc = 2 * t + s;  // padded column of d_s
+        const bool in = rin && pc >= 1 && pc <= S;
+        bcx[q][s] = in ? bn.coef[pc - 1] : 0.f;
+        bcc[q][s] = in ? bn.coef[2 * S + pc - 1] : 0.f;
+      }
+    }
+  }
   // raw rows of this block's boards (out of range, i.e. the last block's +1 row, reads 0)
   const auto xrs = rsrc(X + (long)b0 * RPB * KIN, (total_rows - (long)b0 * RPB) * KIN * 2);
   // The transform of V(kk) runs as four "ops" per thread and chunk-phase, two raw-pixel loads
@@ -244,7 +303,16 @@ conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
     v = v < 0 ? kVRows - 1 : v;
     bf16* vs = lds + (kk & 1) * 2 * kVSlot + h * kVSlot;
     const bf16x8 da = h ? da1 : da0, db = h ? db1 : db0;
-    const bf16x8 val = P1 ? (h ? vdiff(db, da) : vsum(da, db)) : vdiff(da, db);
+    bf16x8 val;
+    if constexpr (BNM == 1) {
+      constexpr int q = o >> 1, ra = P1 ? 1 : (h ? 3 : 0), rb = P1 ? 2 : (h ? 1 : 2);
+      if constexpr (P1 && h)
+        val = vaddsub_bn<-1>(db, da, bcx[q][rb], bcc[q][rb], bcx[q][ra], bcc[q][ra]);
+      else
+        val = vaddsub_bn<P1 ? 1 : -1>(da, db, bcx[q][ra], bcc[q][ra], bcx[q][rb], bcc[q][rb]);
+    } else {
+      val = P1 ? (h ? vdiff(db, da) : vsum(da, db)) : vdiff(da, db);
+    }
     *reinterpret_cast<bf16x8*>(vs + v * kWK + ((k8 ^ swz4w(v)) * 8)) = val;
   };
 
@@ -423,7 +491,71 @@ conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
     }
   }
   __syncthreads();
-  {
+  if constexpr (BNM != 0) {
+    // one board: 16 consecutive threads own one pixel row of 128 channels (512 = 32 rows per
+    // pass, every thread runs the same passes so the row reductions' shuffles see whole waves)
+    const int S2 = S * S, WO = S + 2 * HO, WMK = S + 2 * HM;
+    constexpr int kChunks = kWN / 8;
+    const int total = S2 * kChunks, nit = (total + 511) / 512;
+    const bool st = bn.spart != nullptr;
+    for (int it = 0; it < nit; ++it) {
+      const int e = threadIdx.x + it * 512;
+      const bool valid = e < total;
+      const int pix = valid ? e / kChunks : 0, k8 = (e % kChunks) * 8;
+      const int i = pix / S, j = pix - (pix / S) * S;
+      float s0 = 0.f, s1 = 0.f;
+      if (valid) {
+        const int m = i * TJ + (j >> 1);
+        bf16x8 v = *reinterpret_cast<const bf16x8*>(lds + (2 * m + (j & 1)) * kEpRow + k8);
+        const size_t yo = (size_t)((b0 * WO + i + HO) * WO + j + HO) * YC + n0 + k8;
+        if constexpr (BNM == 1) {
+          if (bn.res) {  // the residual unit's skip (bias (+ ReLU) already in the image)
+            const bf16x8 r = *reinterpret_cast<const bf16x8*>(bn.res + yo);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = (bf16)((float)v[q] + (float)r[q]);
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const float f = (float)v[q];
+            s0 += f;
+            s1 = fmaf(f, f, s1);
+          }
+        } else {
+          const bf16x8 mk = *reinterpret_cast<const bf16x8*>(
+              mask + (size_t)((b0 * WMK + i + HM) * WMK + j + HM) * YC + n0 + k8);
+          const float cx = bn.coef[j], cc = bn.coef[2 * S + j];
+          const float mu = bn.smean ? bn.smean[j] : 0.f;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const float xm = (float)mk[q];
+            v[q] = fmaf(cx, xm, cc) > 0.f ? v[q] : (bf16)0.f;
+            const float d = (float)v[q];
+            s0 += d;
+            s1 = fmaf(d, xm - mu, s1);  // backward: sum dU (x - mean)
+          }
+        }
+        *reinterpret_cast<bf16x8*>(Y + yo) = v;
+      }
+      if (st) {
+#pragma unroll
+        for (int o = kChunks / 2; o > 0; o >>= 1) {
+          s0 += __shfl_xor(s0, o, 64);
+          s1 += __shfl_xor(s1, o, 64);
+        }
+        if ((threadIdx.x & (kChunks - 1)) == 0 && valid) {
+          atomicAdd(sred + j, s0);
+          atomicAdd(sred + 64 + j, s1);
+        }
+      }
+    }
+    if (st) {
+      __syncthreads();
+      if ((int)threadIdx.x < 2 * S) {
+        const int q = threadIdx.x / S, c = threadIdx.x - q * S;
+        bn.spart[((size_t)blockIdx.x * 2 + q) * S + c] = sred[q * 64 + c];
+      }
+    }
+  } else {
     const int nbl = B - b0 < nb ? B - b0 : nb;
     const int S2 = S * S, WO = S + 2 * HO, WMK = S + 2 * HM;
     constexpr int kChunks = kWN / 8;  // 16-byte chunks per pixel row
@@ -459,13 +591,17 @@ conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
 // position k % 8 of fragment (k / 32, n / 16), as a 16x16x32 MFMA A operand reads it. Block = one 64 (n) x 64 (c) tile of one kernel row ky
 // of one layer (blockIdx.y): the row's three taps go through LDS so both layouts are written
 // coalesced (Uf along c, Ub along n).
-constexpr int kWinoPackFields = 8;  // W, COUT, CIN, COUTP, CINP, Uf, Ub (or 0), unused
+// Wd (or 0): the direct dgrad layout [tap'][CINP][COUTP] (tap' = 8 - (3 ky + kx), conv.hip
+// pack_trunk_kernel's Wb) from the same LDS tile, for layers whose dgrad runs the direct kernel:
+// the fp32 weights are read once per step instead of once more by pack_trunk.
+constexpr int kWinoPackFields = 8;  // W, COUT, CIN, COUTP, CINP, Uf, Ub (or 0), Wd (or 0)
 __global__ void __launch_bounds__(256) wino_pack_kernel(const int64_t* __restrict__ table) {
   const int64_t* t = table + (size_t)blockIdx.y * kWinoPackFields;
   const float* W = (const float*)t[0];
   const int COUT = (int)t[1], CIN = (int)t[2], COUTP = (int)t[3], CINP = (int)t[4];
   bf16* Uf = (bf16*)t[5];
   bf16* Ub = (bf16*)t[6];
+  bf16* Wd = (bf16*)t[7];
   const int ntn = (COUTP + 63) / 64, ntc = (CINP + 63) / 64;
   const int g = blockIdx.x / 3, ky = blockIdx.x - g * 3;
   if (g >= ntn * ntc) return;
@@ -500,14 +636,19 @@ __global__ void __launch_bounds__(256) wino_pack_kernel(const int64_t* __restric
       Uf[(ky * 4 + 3) * tap_stride + o] = (bf16)g2;
     }
   }
-  if (!Ub) return;
+  if (!Ub && !Wd) return;
   __syncthreads();
   const int kyb = 2 - ky;  // dgrad kernel row; its kx is flipped: (h0, h1, h2) = (g2, g1, g0)
 #pragma unroll 4
   for (int i = 0; i < 16; ++i) {
     const int cl = ty + 4 * i;
     const int c = ct * 64 + cl, n = nt * 64 + tx;
-    if (c < CINP && n < COUTP) {
+    if (Wd && c < CINP && n < COUTP) {
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx)
+        Wd[((size_t)(8 - (3 * ky + kx)) * CINP + c) * COUTP + n] = (bf16)tl[kx][tx][cl];
+    }
+    if (Ub && c < CINP && n < COUTP) {
       const float h0 = tl[2][tx][cl], h1 = tl[1][tx][cl], h2 = tl[0][tx][cl];
       const size_t o = fm(c, n, CINP);
       Ub[(kyb * 4 + 0) * tap_stride + o] = (bf16)h0;
@@ -593,16 +734,20 @@ RAG_API int rag_conv_wino_mode(int B, int S, int KIN, int NOUT) {
 // Winograd 3x3 conv (forward or dgrad): X [B][S+2][S+2][KIN] bf16, U the layer's fragment-major
 // Winograd weights (rag_wino_pack), Y padded with halo HO and YC >= NOUT channels, mask (dgrad) with halo HM.
 // `pending`: a deferred wgrad reduction handle (conv.hip PendingRed) or null.
+// half (192-wide tiles only): run half-board blocks whenever the shape has them (wino_half_ok),
+// not only when the one-board grid would leave a ragged wave -- for launches that share the chip
+// with long resident kernels (the search's GPU rollouts hold a 128-VGPR wave on most CUs: a
+// one-board block needs 2 x 244 VGPRs on every SIMD, a half-board block 2 x 165).
 int rag_conv_wino_launch(const void* X, const void* W, const float* bias, void* Y,
                          const void* mask, int B, int S, int KIN, int NOUT, int HO, int YC,
-                         int relu, int HM, hipStream_t stream, const WgradRed* red) {
+                         int relu, int HM, hipStream_t stream, const WgradRed* red, int half) {
   if (!rag_conv_wino_ok(S, 1, KIN, NOUT, 3) || YC < NOUT || B <= 0) return -1;
   const int nb = wino_boards_per_block(S);
   WgradRed r{};
   if (red) r = *red;
   const int wt = wino_tile(NOUT, S);
   const dim3 grid((B + nb - 1) / nb, NOUT / wt);
-  if (wt == 192 && wino_mode(B, S, KIN, NOUT) == 2)  // two blocks per board
+  if (wt == 192 && ((half && wino_half_ok(S, NOUT)) || wino_mode(B, S, KIN, NOUT) == 2))
     conv_wino_kernel<192, true, kHalfPairs><<<dim3(2 * B, NOUT / wt), 512, 0, stream>>>(
         (const bf16*)X, (const bf16*)W, bias, (bf16*)Y, (const bf16*)mask, B, S, KIN, NOUT, HO,
         YC, relu, HM, 1, r);
@@ -621,14 +766,48 @@ int rag_conv_wino_launch(const void* X, const void* W, const float* bias, void* 
   return (int)hipGetLastError();
 }
 
+// The fused-BN forms (WinoBN, ResnetPolicy's 128-channel trunk): the 128-wide one-board tile at
+// batches whose grid fills the chip.
+static bool wino_bn_ok(int B, int S, int KIN, int NOUT) {
+  return NOUT == 128 && KIN == 128 && S <= 64 && wino_tile(NOUT, S) == 128 &&
+         wino_mode(B, S, KIN, NOUT) == 1;
+}
+RAG_API int rag_conv_wino_bn_ok(int B, int S, int KIN, int NOUT) {
+  return wino_bn_ok(B, S, KIN, NOUT);
+}
+
+// Forward (coef: BN prologue on X, res optional) or dgrad (mcoef: mask = the BN input x) form;
+// spart [B][2][S] optional, smean with mcoef only. -5 if the shape or the argument set has no
+// kernel.
+int rag_conv_wino_bn_launch(const void* X, const void* W, const float* bias, void* Y,
+                            const void* mask, const void* res, int B, int S, int KIN, int NOUT,
+                            int HO, int YC, int relu, int HM, hipStream_t stream,
+                            const WgradRed* red, const float* coef, const float* mcoef,
+                            float* spart, const float* smean) {
+  if (!wino_bn_ok(B, S, KIN, NOUT) || YC < NOUT || (coef != nullptr) == (mcoef != nullptr) ||
+      (mcoef && (!mask || res)) || (smean && !mcoef))
+    return -5;
+  WgradRed r{};
+  if (red) r = *red;
+  if (coef)
+    conv_wino_kernel<128, true, kWP, 1><<<B, 512, 0, stream>>>(
+        (const bf16*)X, (const bf16*)W, bias, (bf16*)Y, nullptr, B, S, KIN, NOUT, HO, YC, relu,
+        HM, 1, r, WinoBN{coef, (const bf16*)res, spart, nullptr});
+  else
+    conv_wino_kernel<128, true, kWP, 2><<<B, 512, 0, stream>>>(
+        (const bf16*)X, (const bf16*)W, bias, (bf16*)Y, (const bf16*)mask, B, S, KIN, NOUT, HO,
+        YC, relu, HM, 1, r, WinoBN{mcoef, nullptr, spart, smean});
+  return (int)hipGetLastError();
+}
+
 RAG_API int rag_conv_wino(const void* X, const void* W, const float* bias, void* Y,
                           const void* mask, int B, int S, int KIN, int NOUT, int HO, int YC,
                           int relu, int HM, hipStream_t stream) {
   return rag_conv_wino_launch(X, W, bias, Y, mask, B, S, KIN, NOUT, HO, YC, relu, HM, stream,
-                              nullptr);
+                              nullptr, 0);
 }
 
-// table: kWinoPackFields int64 per layer (W, COUT, CIN, COUTP, CINP, Uf, Ub or 0, 0).
+// table: kWinoPackFields int64 per layer (W, COUT, CIN, COUTP, CINP, Uf, Ub or 0, Wd or 0).
 RAG_API int rag_wino_pack(const int64_t* table, int nlayers, int max_tiles, hipStream_t stream) {
   if (nlayers <= 0 || max_tiles <= 0) return -1;
   const dim3 grid((unsigned)(3 * max_tiles), (unsigned)nlayers);

@@ -97,10 +97,12 @@ class _PackedConvs(object):
                 if self._wino[l]:
                     drows.append(row)
                     ub = self._ub[l].data_ptr() if self.wino_dgrad else 0
+                    # the direct dgrad layout (unless the dgrad runs Winograd too) comes out of
+                    # wino_pack's tiles: the pack_trunk row keeps only the bias
+                    wd = 0 if self.wino_dgrad else self._wb[l].data_ptr()
                     wrows.append([ws[l].data_ptr(), s.cout, s.cin, s.coutp, s.cinp,
-                                  self._uf[l].data_ptr(), ub, 0])
-                    # the direct dgrad layout unless the dgrad runs Winograd too
-                    row = row[:7] + [0, 0 if self.wino_dgrad else row[8]] + row[9:]
+                                  self._uf[l].data_ptr(), ub, wd])
+                    row = row[:7] + [0, 0] + row[9:]
                 rows.append(row)
             self._pack_table = torch.tensor(rows, dtype=torch.int64).to(self.device)
             self._pack_total = pack_grid_width(self.specs)
@@ -144,6 +146,9 @@ class HipTrunk(_PackedConvs):
                 and ops.conv_wino_ok(board, 1, s.coutp, s.cinp, 3) for s in specs]
         self._init_packing(specs, device, wino)
         self._wino_plans = {}
+        # half-board Winograd blocks at every batch (set by a search whose GPU rollouts share the
+        # chip: RAG_WINO_HALF=1 forces it for experiments)
+        self.wino_half = os.environ.get("RAG_WINO_HALF") == "1"
         self._work = None
         self._rstream = None
         # wgrad slab reductions ride along the next dgrad launch (RAG_WGRAD_DEFER=0: own kernels)
@@ -243,7 +248,7 @@ class HipTrunk(_PackedConvs):
             x, y = self.acts[l][:B], self.acts[l + 1][:B]
             if wino[l]:
                 ops.conv_wino(x, self._uf[l], self._bias[l], y, B, S, s.cinp, s.coutp,
-                              self.halo[l + 1], s.relu)
+                              self.halo[l + 1], s.relu, half=self.wino_half)
             else:
                 ops.conv_igemm(x, self._wf[l], self._bias[l], y, B, S, self.halo[l],
                                self.halo[l + 1], s.cinp, s.coutp, s.ks, s.relu, cin=s.cin)
@@ -350,7 +355,15 @@ class ResTrunk(_PackedConvs):
             assert s.cin == K and s.cout == K, "residual trunk needs constant width"
         self.K, self.KP = K, specs[0].coutp
         self._B = 0
-        self._init_packing(specs, device)
+        # 3x3 128 -> 128 layers whose input BN is fused (_prologue_ok) run the Winograd kernel
+        # with the BN built into its input transform (conv_wino.hip WinoBN) at batches that fill
+        # its grid; RAG_RES_WINO: 0 off, 1 forward only, 2 (default) forward and dgrad
+        mode = os.environ.get("RAG_RES_WINO", "2") if device.type == "cuda" else "0"
+        wino = [mode != "0" and l > 0 and s.ks == 3 and s.cinp == s.coutp == 128
+                and ops.conv_wino_ok(board, 1, s.cinp, s.coutp, 3) for l, s in enumerate(specs)]
+        self._init_packing(specs, device, wino)
+        self.wino_dgrad = mode == "2"
+        self._wino_plans = {}
         self.hin = [max(1, s.ks // 2) for s in specs]
         self.halo = [self.hin[0]]
         # last conv of each unit, and the gradient halo each unit's output gradient needs
@@ -398,7 +411,8 @@ class ResTrunk(_PackedConvs):
         self.bcoef = torch.zeros((3, S), dtype=torch.float32, device=dev)
         # BN column-statistics partials written by the fused conv epilogues (forward: one per
         # BN, whose input that conv produced; backward: one, reused layer by layer)
-        nblk = ops.conv_bn_stat_blocks(B, S, KP) if KP % 128 == 0 and KP % 192 else 1
+        # (the Winograd kernel writes one partial per board)
+        nblk = max(ops.conv_bn_stat_blocks(B, S, KP), B) if KP % 128 == 0 and KP % 192 else 1
         self.spart = torch.zeros((nb, nblk, 2, S), dtype=torch.float32, device=dev)
         self.bpart = torch.zeros((nblk, 2, S), dtype=torch.float32, device=dev)
         need = max(ops._lib().rag_conv_wgrad_workspace(B, S, s.coutp, s.cinp, s.ks, None)
@@ -431,6 +445,25 @@ class ResTrunk(_PackedConvs):
         return (self.bn_prologue and sp.ks == 3 and self.hin[j + 1] == 1 and self.K == self.KP
                 and ops.conv_bn_fusable(B, self.S, 1, sp.cinp, sp.coutp, sp.ks))
 
+    def _plan(self, B):
+        """(fused, wino) at batch B: per BN j, fused into conv j+1's prologue; per conv l, runs
+        the Winograd BN kernel (its input BN fused, a grid that fills the chip)."""
+        plan = self._wino_plans.get(B)
+        if plan is None:
+            fused = [self._prologue_ok(j, B) for j in range(len(self.bns))]
+            wino = [w and l > 0 and fused[l - 1] and ops.conv_wino_bn_ok(B, self.S, self.KP,
+                                                                         self.KP)
+                    for l, w in enumerate(self._wino)]
+            plan = self._wino_plans[B] = (fused, wino)
+        if any(w and not p for w, p in zip(self._wino, plan[1])):
+            self._direct_layouts()
+        return plan
+
+    def _stat_blocks(self, l, B, dgrad=False):
+        """Partial rows of the BN statistics conv l's forward (or dgrad) epilogue writes."""
+        wino = self._plan(B)[1][l] and (self.wino_dgrad or not dgrad)
+        return B if wino else ops.conv_bn_stat_blocks(B, self.S, self.KP)
+
     # ------------------------------------------------------------------ compute
     def forward(self, B, training=False):
         S, K = self.S, self.K
@@ -439,14 +472,15 @@ class ResTrunk(_PackedConvs):
                        self.hin[0], 1, s0.cinp, s0.coutp, s0.ks, False, cin=s0.cin)
         j = 0
         nb = len(self.bns)
-        self._fused = [self._prologue_ok(jj, B) for jj in range(nb)]
-        nblk = ops.conv_bn_stat_blocks(B, S, self.KP) if any(self._fused) else 0
+        fused, wino = self._plan(B)
+        self._fused = list(fused)
         stat_ready = [False] * nb  # BN j's input statistics came out of the conv producing it
         for u, n in enumerate(self.units):
             for i in range(n):
                 bn, x, U = self.bns[j], self._bn_input(j, u, B), self.U[j][:B]
                 if training and stat_ready[j]:
-                    ops.bn_finalize_fwd(self.spart[j], nblk, B, S, K, bn.gamma, bn.beta,
+                    ops.bn_finalize_fwd(self.spart[j], self._stat_blocks(j, B), B, S, K,
+                                        bn.gamma, bn.beta,
                                         bn.rmean, bn.rvar, bn.eps, bn.momentum, self.stats[j],
                                         self.coef[j])
                 elif training:
@@ -462,9 +496,14 @@ class ResTrunk(_PackedConvs):
                 if self._fused[j]:
                     # this conv's output is BN l's input: its epilogue also sums BN l's stats
                     sp_out = self.spart[l] if training and l < nb else None
-                    ops.conv_igemm_bn(x, self._wf[l], self._bias[l], y, B, S, sp.cinp, sp.coutp,
-                                      False, bn_coef=self.coef[j], residual=res,
-                                      stat_part=sp_out)
+                    if wino[l]:
+                        ops.conv_wino_bn(x, self._uf[l], self._bias[l], y, B, S, sp.cinp,
+                                         sp.coutp, False, bn_coef=self.coef[j], residual=res,
+                                         stat_part=sp_out)
+                    else:
+                        ops.conv_igemm_bn(x, self._wf[l], self._bias[l], y, B, S, sp.cinp,
+                                          sp.coutp, False, bn_coef=self.coef[j], residual=res,
+                                          stat_part=sp_out)
                     if sp_out is not None:
                         stat_ready[l] = True
                 else:
@@ -482,6 +521,7 @@ class ResTrunk(_PackedConvs):
         (BN j's grads, which sit between conv j and conv j+1 in the flat buffer, are complete
         by then)."""
         S, K = self.S, self.K
+        wino = self._plan(B)[1]
         cur, hcur = self.G[1][:B], 1  # dL/dA_{u+1}
         for u in range(len(self.units) - 1, -1, -1):
             n, jend = self.units[u], self._unit_last[u]
@@ -503,10 +543,16 @@ class ResTrunk(_PackedConvs):
                                    defer=defer, pending=self._pending if defer else None,
                                    xcoef=self.coef[j])
                     # its epilogue also sums BN j's backward statistics (dU, dU (x - mean))
-                    ops.conv_igemm_bn(gx, self._wb[l], None, dU, B, S, sp.coutp, sp.cinp, False,
-                                      mask=x, mask_coef=self.coef[j],
-                                      pending=self._pending if defer else None,
-                                      stat_part=self.bpart, stat_mean=self.stats[j])
+                    if wino[l] and self.wino_dgrad:
+                        ops.conv_wino_bn(gx, self._ub[l], None, dU, B, S, sp.coutp, sp.cinp,
+                                         False, mask=x, mask_coef=self.coef[j],
+                                         pending=self._pending if defer else None,
+                                         stat_part=self.bpart, stat_mean=self.stats[j])
+                    else:
+                        ops.conv_igemm_bn(gx, self._wb[l], None, dU, B, S, sp.coutp, sp.cinp,
+                                          False, mask=x, mask_coef=self.coef[j],
+                                          pending=self._pending if defer else None,
+                                          stat_part=self.bpart, stat_mean=self.stats[j])
                 else:
                     ops.conv_wgrad(gx, U, dws[l], dbs[l], B, S, self.hin[l], sp.cout, sp.coutp,
                                    sp.cin, sp.cinp, sp.ks, accumulate=accumulate,
@@ -528,12 +574,12 @@ class ResTrunk(_PackedConvs):
                     out, res = self.G[hn][:B], cur
                 if fused and self.fold_bwd_finalize:
                     # the finalize folded into the apply (each block sums the dgrad's partials)
-                    ops.bn_apply_bwd_part(self.bpart, ops.conv_bn_stat_blocks(B, S, self.KP), x,
+                    ops.bn_apply_bwd_part(self.bpart, self._stat_blocks(l, B, True), x,
                                           out, B, S, K, bn.gamma, self.stats[j], bn.dgamma,
                                           bn.dbeta, dU, residual=res)
                 else:
                     if fused:
-                        ops.bn_finalize_bwd(self.bpart, ops.conv_bn_stat_blocks(B, S, self.KP),
+                        ops.bn_finalize_bwd(self.bpart, self._stat_blocks(l, B, True),
                                             B, S, K, bn.gamma, self.stats[j], bn.dgamma,
                                             bn.dbeta, self.bcoef)
                     else:

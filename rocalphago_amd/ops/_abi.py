@@ -27,10 +27,12 @@ SIGNATURES = {
     # conv_wino.hip (+ the pending-handle entry in conv.hip)
     "rag_conv_wino_ok": [I, I, I, I, I],
     "rag_conv_wino": [P, P, P, P, P, I, I, I, I, I, I, I, I, P],
-    "rag_conv_wino_p": [P, P, P, P, P, I, I, I, I, I, I, I, I, P, P],
+    "rag_conv_wino_p": [P, P, P, P, P, I, I, I, I, I, I, I, I, P, P, I],
     "rag_wino_pack": [P, I, I, P],
     "rag_conv_wino_prefer": [I, I, I, I],
     "rag_conv_wino_mode": [I, I, I, I],
+    "rag_conv_wino_bn_ok": [I, I, I, I],
+    "rag_conv_wino_bn": [P] * 6 + [I] * 8 + [P] * 6,
     "rag_pack_input_u8": [P, P, P, P, I, I, I, I, I, I, P],
     "rag_pack_input_f32": [P, P, P, P, I, I, I, I, I, I, P],
     "rag_pack_input_bits": [P, P, P, P, I, I, I, I, I, P],

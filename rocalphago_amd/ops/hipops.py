@@ -160,10 +160,10 @@ def conv_wino_mode(B, S, kin, nout):
 
 def wino_pack(table, nlayers, max_tiles):
     """Winograd weights of 3x3 layers from their fp32 OIHW masters in one launch. ``table``:
-    device int64 [nlayers, 8] = (W, cout, cin, coutp, cinp, Uf, Ub or 0, 0); Uf (forward, N =
-    coutp, K = cinp) and Ub (dgrad, N = cinp, K = coutp) each 12 * N * K bf16, stored
-    fragment-major [12][K/32][N/16][64][8] (conv_wino.hip); ``max_tiles``: 64x64 (n, c) tiles of
-    the widest layer."""
+    device int64 [nlayers, 8] = (W, cout, cin, coutp, cinp, Uf, Ub or 0, Wd or 0); Uf (forward,
+    N = coutp, K = cinp) and Ub (dgrad, N = cinp, K = coutp) each 12 * N * K bf16, stored
+    fragment-major [12][K/32][N/16][64][8] (conv_wino.hip); Wd: the direct dgrad layout
+    [9, cinp, coutp] (pack_trunk's); ``max_tiles``: 64x64 (n, c) tiles of the widest layer."""
     _check(_lib().rag_wino_pack(_ptr(table), nlayers, int(max_tiles), _stream()), "wino_pack")
 
 
@@ -182,11 +182,12 @@ def wino_weights(w, coutp, cinp, dgrad=True):
 
 
 def conv_wino(x, u, bias, y, B, S, kin, nout, ho, relu, mask=None, mask_halo=None,
-              pending=None):
+              pending=None, half=False):
     """y[pad ho] = act(conv3x3(x[pad 1]) + bias) through the Winograd kernel with the layer's
     Winograd weights ``u`` [12, nout, kin] (wino_pack), or the dgrad form with a ReLU mask (the
     layer input, y's channel count, halo ``mask_halo``). ``pending``: a PendingReduction whose
-    deferred wgrad reduction rides along the launch."""
+    deferred wgrad reduction rides along the launch. ``half``: half-board blocks whenever the
+    shape has them (launches sharing the chip with resident kernels, e.g. GPU rollouts)."""
     _index_range_ok(x, y, mask)
     hm = ho if mask_halo is None else mask_halo
     if x.shape[1] != S + 2 or x.shape[-1] != kin:
@@ -195,7 +196,38 @@ def conv_wino(x, u, bias, y, B, S, kin, nout, ho, relu, mask=None, mask_halo=Non
         raise ValueError("mask layout does not match (halo %d, %d channels)" % (hm, y.shape[-1]))
     _check(_lib().rag_conv_wino_p(_ptr(x), _ptr(u), _ptr(bias), _ptr(y), _ptr(mask), B, S, kin,
                                   nout, ho, y.shape[-1], int(relu), hm, _stream(),
-                                  _hptr(pending)), "conv_wino")
+                                  _hptr(pending), int(bool(half))), "conv_wino")
+    return y
+
+
+def conv_wino_bn_ok(B, S, kin, nout):
+    """True if conv_wino_bn (the Winograd kernel with the residual trunk's fused BatchNorm) runs
+    a batch of B: 128 -> 128 channels, one board per block, a grid that fills the chip."""
+    return bool(_lib().rag_conv_wino_bn_ok(B, S, kin, nout))
+
+
+def conv_wino_bn(x, u, bias, y, B, S, kin, nout, relu, bn_coef=None, mask=None, mask_coef=None,
+                 residual=None, pending=None, stat_part=None, stat_mean=None):
+    """conv_igemm_bn's two forms on the Winograd kernel (conv_wino.hip WinoBN) with the layer's
+    Winograd weights ``u``: forward (``bn_coef``: x is the BN input, U = ReLU(bn_coef[0][col] x +
+    bn_coef[2][col]) is built in the input transform; optional ``residual``) or dgrad
+    (``mask`` = x and ``mask_coef``). ``stat_part`` [B, 2, S]: one partial row pair per board
+    (bn_finalize_fwd / bn_finalize_bwd with nblk = B). Needs conv_wino_bn_ok(B, ...)."""
+    _index_range_ok(x, y, mask, residual)
+    if x.shape[1] != S + 2 or x.shape[-1] != kin or y.shape[1] != S + 2:
+        raise ValueError("conv_wino_bn input and output have halo 1 (%d input channels)" % kin)
+    if residual is not None and residual.shape[1:] != y.shape[1:]:
+        raise ValueError("residual layout does not match the output")
+    if mask is not None and (mask.shape[1] != S + 2 or mask.shape[-1] != y.shape[-1]):
+        raise ValueError("mask layout does not match (halo 1, %d channels)" % y.shape[-1])
+    if (mask is None) != (mask_coef is None) or (bn_coef is None) == (mask_coef is None):
+        raise ValueError("conv_wino_bn: bn_coef (forward) or mask + mask_coef (dgrad)")
+    if stat_part is not None and stat_part.shape[0] < B:
+        raise ValueError("stat_part needs one row pair per board")
+    _check(_lib().rag_conv_wino_bn(_ptr(x), _ptr(u), _ptr(bias), _ptr(y), _ptr(mask),
+                                   _ptr(residual), B, S, kin, nout, 1, y.shape[-1], int(relu), 1,
+                                   _stream(), _hptr(pending), _ptr(bn_coef), _ptr(mask_coef),
+                                   _ptr(stat_part), _ptr(stat_mean)), "conv_wino_bn")
     return y
 
 
