@@ -709,8 +709,12 @@ static int wino_cus() {
   }
   return cus;
 }
-// 1: one-board blocks, 2: half-board blocks (a batch whose one-board grid would leave a ragged
-// last wave, e.g. the 128-board self-play plies, but whose half-board grid fills), 0: neither.
+// 1: one-board blocks, 2: half-board blocks, 0: neither (the direct kernel).
+// A grid of at most one wave of blocks (one per CU) costs one block's time whatever its size, and
+// that beats the direct kernel at every batch: 192 -> 192 at 19x19 (benchmarks/wino_bench.py
+// --batch sweep, one box) one-board blocks 41-45 us for B = 32..200 against 45-55 us direct,
+// half-board blocks 29-35 us for B <= 128 (their 2B blocks still one wave). Several waves: a
+// ragged last wave gives the gain back, so the Winograd grid must fill 7/8 of its last wave.
 static int wino_mode(int B, int S, int KIN, int NOUT) {
   if (!rag_conv_wino_ok(S, 1, KIN, NOUT, 3) || B <= 0 || wino_boards_per_block(S) != 1) return 0;
   const int cus = wino_cus();
@@ -720,8 +724,10 @@ static int wino_mode(int B, int S, int KIN, int NOUT) {
     return blocks * 8 >= waves * cus * 7;
   };
   const long full = (long)B * (NOUT / wino_tile(NOUT, S));
+  const bool half = wino_half_ok(S, NOUT);
+  if (full <= cus) return half && 2 * full <= cus ? 2 : 1;
   if (fills(full)) return 1;
-  if (wino_half_ok(S, NOUT) && fills(2 * full)) return 2;
+  if (half && fills(2 * full)) return 2;
   return 0;
 }
 RAG_API int rag_conv_wino_prefer(int B, int S, int KIN, int NOUT) {

@@ -357,8 +357,11 @@ class ResTrunk(_PackedConvs):
         self._B = 0
         # 3x3 128 -> 128 layers whose input BN is fused (_prologue_ok) run the Winograd kernel
         # with the BN built into its input transform (conv_wino.hip WinoBN) at batches that fill
-        # its grid; RAG_RES_WINO: 0 off, 1 forward only, 2 (default) forward and dgrad
-        mode = os.environ.get("RAG_RES_WINO", "2") if device.type == "cuda" else "0"
+        # its grid; RAG_RES_WINO: 0 off, 1 (default) forward only, 2 forward and dgrad (the
+        # dgrad carries the deferred wgrad reduction: one wave of Winograd blocks pays for it in
+        # full, 51.6 vs 48.6 us on the direct kernel; ResNet 71.6 k (1) / 70.9 k (2) / 68.0 k (0)
+        # positions/s on one box)
+        mode = os.environ.get("RAG_RES_WINO", "1") if device.type == "cuda" else "0"
         wino = [mode != "0" and l > 0 and s.ks == 3 and s.cinp == s.coutp == 128
                 and ops.conv_wino_ok(board, 1, s.cinp, s.coutp, 3) for l, s in enumerate(specs)]
         self._init_packing(specs, device, wino)

@@ -160,10 +160,27 @@ class NativeSelfPlay(object):
                  "seed": ((1,), torch.int64)}
         if host_lad:
             specs["ladders"] = ((n, 2, P), torch.uint8)
-        h = {k: torch.zeros(shp, dtype=dt, pin_memory=True) for k, (shp, dt) in specs.items()}
+        # every input field lives in ONE pinned buffer (16-byte aligned views) mirrored by one
+        # device buffer: a ply's inputs go up in one copy instead of one per field (each small
+        # copy held the stream ~5 us; 7.5 copies per ply were 4 % of the RL trace)
+        offs, total = {}, 0
+        for k, (shp, dt) in specs.items():
+            offs[k] = total
+            nbytes = int(np.prod(shp)) * torch.empty((), dtype=dt).element_size()
+            total += (nbytes + 15) // 16 * 16
+        hraw = torch.zeros((total,), dtype=torch.uint8, pin_memory=True)
+        draw = torch.zeros((total,), dtype=torch.uint8, device=self.device)
+
+        def view(raw, k):
+            shp, dt = specs[k]
+            nb = int(np.prod(shp)) * torch.empty((), dtype=dt).element_size()
+            return raw[offs[k]:offs[k] + nb].view(dt).view(shp)
+
+        h = {k: view(hraw, k) for k in specs}
         h["moves"] = torch.zeros((n,), dtype=torch.int32, pin_memory=True)
-        d = {k: torch.zeros(shp, dtype=dt, device=self.device) for k, (shp, dt) in specs.items()}
+        d = {k: view(draw, k) for k in specs}
         b = {"n": n, "h": h, "d": d, "hv": {k: v.numpy() for k, v in h.items()},
+             "hraw": hraw, "draw": draw,
              "planes": torch.empty((n, gf.F, S, S), dtype=torch.uint8, device=self.device),
              "sens": torch.empty((n, P), dtype=torch.uint8, device=self.device),
              "mv": torch.empty((n,), dtype=torch.int32, device=self.device), "graphs": {}}
@@ -173,8 +190,7 @@ class NativeSelfPlay(object):
     def _gpu_pass(self, b, policy, gf, n, S, P, beta):
         from ..ops import hipops as ops
         h, d = b["h"], b["d"]
-        for k in d:
-            d[k][:n].copy_(h[k][:n], non_blocking=True)
+        b["draw"].copy_(b["hraw"], non_blocking=True)
         planes = gf.run(d["colors"][:n], d["ages"][:n], d["meta4"][:n], None,
                         d["ladders"][:n] if "ladders" in d else None, n, S,
                         out=b["planes"][:n], sens_out=b["sens"][:n])

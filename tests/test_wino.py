@@ -35,11 +35,11 @@ def ops():
 @pytest.mark.parametrize("B,S,ho,C", [(1, 19, 1, 192), (3, 19, 2, 192), (256, 19, 1, 192),
                                       (3, 13, 1, 192), (5, 9, 1, 192), (7, 7, 2, 192),
                                       (3, 19, 1, 128), (256, 19, 2, 128), (128, 19, 1, 192),
-                                      (120, 19, 2, 192)])
+                                      (120, 19, 2, 192), (200, 19, 1, 192)])
 def test_wino_forward_matches_fp32(ops, B, S, ho, C):
     """192-wide tiles (one or several boards per block), the 128-wide tile (CNNPolicy's
-    default width: 48 pairs x 64 channels per wave) and half-board blocks (B = 120, 128 on 256
-    CUs: two 96-pair blocks per board)."""
+    default width: 48 pairs x 64 channels per wave) and half-board blocks (B <= 128 at 19x19 on
+    256 CUs: two 96-pair blocks per board; B = 200: one wave of one-board blocks)."""
     dev = torch.device("cuda")
     torch.manual_seed(0)
     assert ops.conv_wino_ok(S, 1, C, C, 3)
