@@ -622,10 +622,6 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
                          const float* smean);  // conv_tap.hip
 bool rag_conv_tap_bn_ok(int M, int S, int WI, int shift, int CIN, int COUTP, int KS);
 bool rag_wgrad_slab_ok(int S, int H, int HG, int GC, int COUTP, int CINP, int KS);
-bool rag_wgrad_wino_ok(int S, int H, int HG, int GC, int COUTP, int CINP, int KS);  // wgrad_wino.hip
-int rag_wgrad_wino_nchunks(int B, int S, int* spc);
-int rag_launch_wgrad_wino(const bf16* G, const bf16* X, float* part, float* bpart, int B, int S,
-                          int GC, int CIN, int spc, int nchunks, hipStream_t stream);
 
 // Conv forward / dgrad.  X: padded input (halo HI, CIN channels, CIN % 32 == 0).  W: packed
 // bf16 weights [taps][WROWS][CIN].  Y: padded output (halo HO, YC channels, COUTP % 32 == 0,
@@ -939,10 +935,6 @@ RAG_API size_t rag_conv_wgrad_workspace(int B, int S, int COUTP, int CINP, int K
       }
     }
   }
-  if (rag_wgrad_wino_ok(S, 1, 1, COUTP, COUTP, CINP, KS)) {
-    const int wn = rag_wgrad_wino_nchunks(B, S, nullptr);
-    if (wn > nc) nc = wn;
-  }
   if (nchunks) *nchunks = nc;
   return (size_t)nc * taps * COUTP * CINP + (size_t)nc * COUTP;
 }
@@ -989,17 +981,7 @@ static int conv_wgrad_impl(const void* G, const void* X, float* dW, float* db, f
   // 5x5 with <= 48 real of 64 input channels (the SL input layer): c-tile 1's blocks pair two
   // kernel rows instead of computing a zero c-fragment
   const int pair5 = KS == 5 && CINP == 64 && CIN <= 48 && !xcoef ? 1 : 0;
-  // 3x3 192 -> 192: the Winograd F(2,3) wgrad (wgrad_wino.hip, same partial layout, map 0)
-  const bool wino = slab && !xcoef && rag_wgrad_slab_bf16() &&
-                    rag_wgrad_wino_ok(S, HI, HG, GC, COUTP, CINP, KS);
-  if (wino) {
-    bf16_part = true;
-    int spc = 1;
-    nchunks = rag_wgrad_wino_nchunks(B, S, &spc);
-    bpart = db ? work + (size_t)nchunks * taps * COUTP * CINP : nullptr;
-    const int rc = rag_launch_wgrad_wino(g, x, part, bpart, B, S, GC, CINP, spc, nchunks, stream);
-    if (rc) return rc;
-  } else if (slab) {
+  if (slab) {
     bf16_part = rag_wgrad_slab_bf16();
     const int WP = S + 2 * HI;
     const int R = B * WP * WP;
@@ -1049,9 +1031,8 @@ static int conv_wgrad_impl(const void* G, const void* X, float* dW, float* db, f
     rs = reduce_stream;
   }
   if (bf16_part) {
-    WgradRed r = rag_wgrad_slab_red(part, bpart, dW, db, nchunks, CINP, COUTP, COUT, CIN,
-                                    accumulate, KS, slab ? pair5 : 0);
-    if (wino) r.map = 0;
+    const WgradRed r = rag_wgrad_slab_red(part, bpart, dW, db, nchunks, CINP, COUTP, COUT, CIN,
+                                          accumulate, KS, slab ? pair5 : 0);
     if (defer && rs == stream) {
       PendingRed* p = static_cast<PendingRed*>(pending);
       p->r = r;

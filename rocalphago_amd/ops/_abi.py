@@ -78,7 +78,6 @@ SIGNATURES = {
     "rag_conv_tap_mode": [I],
     "rag_wgrad_slab_part_bf16": [I],
     "rag_wgrad_slab_map": [I],
-    "rag_wgrad_wino_mode": [I],
 }
 
 RESTYPES = {"rag_conv_wgrad_workspace": SZ, "rag_head_bwd_workspace": SZ,
