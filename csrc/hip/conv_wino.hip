@@ -628,7 +628,7 @@ __global__ void __launch_bounds__(256) wino_pack_kernel(const int64_t* __restric
     tl[0][nl][tx] = g0;
     tl[1][nl][tx] = g1;
     tl[2][nl][tx] = g2;
-    if (n < COUTP && c < CINP) {
+    if (Uf && n < COUTP && c < CINP) {
       const size_t o = fm(n, c, COUTP);
       Uf[(ky * 4 + 0) * tap_stride + o] = (bf16)g0;
       Uf[(ky * 4 + 1) * tap_stride + o] = (bf16)(0.5f * (g0 + g1 + g2));
@@ -813,7 +813,7 @@ RAG_API int rag_conv_wino(const void* X, const void* W, const float* bias, void*
                               nullptr, 0);
 }
 
-// table: kWinoPackFields int64 per layer (W, COUT, CIN, COUTP, CINP, Uf, Ub or 0, Wd or 0).
+// table: kWinoPackFields int64 per layer (W, COUT, CIN, COUTP, CINP, Uf or 0, Ub or 0, Wd or 0).
 RAG_API int rag_wino_pack(const int64_t* table, int nlayers, int max_tiles, hipStream_t stream) {
   if (nlayers <= 0 || max_tiles <= 0) return -1;
   const dim3 grid((unsigned)(3 * max_tiles), (unsigned)nlayers);

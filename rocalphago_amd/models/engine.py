@@ -61,6 +61,7 @@ class _PackedConvs(object):
         self._uf = [None] * len(specs)
         self._ub = [None] * len(specs)
         self._direct_version = None
+        self._ub_version = None
         self.wino_dgrad = False
 
     def sync_weights(self, weights, biases, version):
@@ -119,6 +120,27 @@ class _PackedConvs(object):
             ops.wino_pack(self._wpack_table, sum(self._wino), self._wpack_tiles)
         self._packed_version = version
 
+    def _dgrad_wino_layouts(self):
+        """Winograd dgrad weights of the Winograd layers when the dgrad normally runs the direct
+        kernel (a large batch takes Winograd, see HipTrunk.backward): packed once per weight
+        version, on first use."""
+        if self.wino_dgrad or self._ub_version == self._packed_version:
+            return
+        if getattr(self, "_ubpack_table", None) is None or self._ubpack_key != self._pack_key:
+            rows = []
+            for l, s in enumerate(self.specs):
+                if not self._wino[l]:
+                    continue
+                if self._ub[l] is None:
+                    self._ub[l] = torch.empty((12, s.cinp, s.coutp), dtype=torch.bfloat16,
+                                              device=self.device)
+                rows.append([self._pack_keep[l].data_ptr(), s.cout, s.cin, s.coutp, s.cinp, 0,
+                             self._ub[l].data_ptr(), 0])
+            self._ubpack_table = torch.tensor(rows, dtype=torch.int64).to(self.device)
+            self._ubpack_key = self._pack_key
+        ops.wino_pack(self._ubpack_table, sum(self._wino), self._wpack_tiles)
+        self._ub_version = self._packed_version
+
     def _direct_layouts(self):
         """Direct GEMM layouts of the Winograd layers, for a batch that runs them on the direct
         kernel: packed once per weight version, on first use."""
@@ -159,6 +181,7 @@ class HipTrunk(_PackedConvs):
         # the step), while the direct kernel's ragged last wave absorbs them (+1-2 us); without
         # deferral (own reduce kernels, or the reduce stream) the dgrad runs Winograd as well.
         self.wino_dgrad = not self.defer_reduce or os.environ.get("RAG_WGRAD_OVERLAP") == "1"
+        self.wino_dgrad_min_batch = 512
         self._pending = ops.PendingReduction() if device.type == "cuda" else None
 
     # ------------------------------------------------------------------ buffers
@@ -286,7 +309,12 @@ class HipTrunk(_PackedConvs):
                 below = self.specs[l - 1]
                 which ^= 1
                 gout = self.grad_buffer(l - 1, which, B)
-                if wino[l] and self.wino_dgrad:
+                # batches of two or more block waves (the RL learner's 8192-position chunks) run
+                # the dgrad on Winograd too: a riding reduction costs a few us there, not a wave
+                big = wino[l] and not self.wino_dgrad and B >= self.wino_dgrad_min_batch
+                if big:
+                    self._dgrad_wino_layouts()
+                if wino[l] and (self.wino_dgrad or big):
                     ops.conv_wino(g, self._ub[l], None, gout, B, S, s.coutp, s.cinp,
                                   self.halo[l - 1], False, mask=x if below.relu else None,
                                   mask_halo=self.halo[l],
@@ -357,10 +385,11 @@ class ResTrunk(_PackedConvs):
         self._B = 0
         # 3x3 128 -> 128 layers whose input BN is fused (_prologue_ok) run the Winograd kernel
         # with the BN built into its input transform (conv_wino.hip WinoBN) at batches that fill
-        # its grid; RAG_RES_WINO: 0 off, 1 (default) forward only, 2 forward and dgrad (the
-        # dgrad carries the deferred wgrad reduction: one wave of Winograd blocks pays for it in
-        # full, 51.6 vs 48.6 us on the direct kernel; ResNet 71.6 k (1) / 70.9 k (2) / 68.0 k (0)
-        # positions/s on one box)
+        # its grid; RAG_RES_WINO: 0 off, 1 (default) forward only, 2 forward and dgrad. The dgrad
+        # carries the deferred wgrad reduction: one wave of Winograd blocks pays for it in full
+        # (51.6 vs 48.6 us on the direct kernel; standalone it is 37.4 us + a 16.6 us reduction,
+        # and riding in the BN backward apply made that pass 47.9 instead of 18.5 us). ResNet
+        # 71.6 k (1) / 70.9 k (2) / 69.7 k (2, no deferral) / 68.0 k (0) positions/s on one box.
         mode = os.environ.get("RAG_RES_WINO", "1") if device.type == "cuda" else "0"
         wino = [mode != "0" and l > 0 and s.ks == 3 and s.cinp == s.coutp == 128
                 and ops.conv_wino_ok(board, 1, s.cinp, s.coutp, 3) for l, s in enumerate(specs)]
@@ -566,8 +595,6 @@ class ResTrunk(_PackedConvs):
                     ops.conv_igemm(gx, self._wb[l], None, dU, B, S, self.hin[l], 1, sp.coutp,
                                    sp.cinp, sp.ks, False, mask=U, mask_halo=self.hin[l],
                                    pending=self._pending if defer else None)
-                if on_layer_done is not None:
-                    on_layer_done(l)
                 # i > 0: gradient of the inner conv output Xin[j] = conv j's gx; i == 0:
                 # dL/dA_u = BN'(dU) + skip gradient (in place when halos agree)
                 if i > 0:
@@ -590,6 +617,8 @@ class ResTrunk(_PackedConvs):
                                         bn.dbeta, self.bcoef)
                     ops.bn_apply(x, out, B, S, K, coef=self.bcoef, relu=False, dy=dU,
                                  residual=res)
+                if on_layer_done is not None:  # dW[l] final (its reduction ran by now)
+                    on_layer_done(l)
                 if i > 0:
                     gx = out
                 else:

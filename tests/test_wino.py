@@ -142,3 +142,33 @@ def test_wino_dgrad_carries_deferred_wgrad_reduction_twice(ops):
         torch.cuda.synchronize()
         assert torch.isfinite(dw).all() and torch.isfinite(db).all(), "round %d" % rnd
         assert rel_max(dw, ref_dw) < 1e-5 and rel_max(db, ref_db) < 1e-5
+
+
+def test_trunk_large_batch_dgrad_on_winograd(ops):
+    """HipTrunk runs the dgrad of its Winograd layers on the Winograd kernel at batches of two or
+    more block waves (wino_dgrad_min_batch; the deferred wgrad reduction then costs a few us in
+    its last wave) with the Winograd dgrad weights packed on first use: the same gradients as the
+    direct dgrad."""
+    import numpy as np
+    from rocalphago_amd.features.preprocessing import DEFAULT_FEATURES
+    from rocalphago_amd.models import kerasish as KZ
+    from rocalphago_amd.models.policy import CNNPolicy
+    B = 600
+    rs = np.random.RandomState(2)
+    X = (rs.rand(B, 48, 19, 19) > 0.6).astype(np.uint8)
+    Y = np.zeros((B, 361), np.float32)
+    Y[np.arange(B), rs.randint(0, 361, B)] = 1
+    grads = []
+    for min_batch in (512, 10 ** 9):
+        pol = CNNPolicy(DEFAULT_FEATURES, board=19, filters_per_layer=192, layers=4,
+                        device="cuda", seed=5)
+        trunk = pol.model._plan_for().trunk
+        trunk.wino_dgrad_min_batch = min_batch
+        pol.model.compile(loss="categorical_crossentropy", optimizer=KZ.SGD(lr=0.0))
+        pol.model.train_on_batch(X, Y)
+        torch.cuda.synchronize()
+        assert (trunk._ub_version is not None) == (min_batch == 512)
+        grads.append(torch.cat([g.detach().reshape(-1).float() for g in pol.model.net._gviews]))
+    a, b = grads
+    cos = torch.dot(a, b).item() / (a.norm().item() * b.norm().item())
+    assert cos > 0.999, cos
