@@ -180,7 +180,8 @@ class HipTrunk(_PackedConvs):
         # reduction's ~28 MB of partial slabs stream after every block's epilogue (+6-8 us in
         # the step), while the direct kernel's ragged last wave absorbs them (+1-2 us); without
         # deferral (own reduce kernels, or the reduce stream) the dgrad runs Winograd as well.
-        self.wino_dgrad = not self.defer_reduce or os.environ.get("RAG_WGRAD_OVERLAP") == "1"
+        self.wino_dgrad = (not self.defer_reduce or os.environ.get("RAG_WGRAD_OVERLAP") == "1"
+                           or os.environ.get("RAG_WINO_DGRAD") == "1")
         self.wino_dgrad_min_batch = 512
         self._pending = ops.PendingReduction() if device.type == "cuda" else None
 
