@@ -38,8 +38,10 @@ struct FShared {
   unsigned long long stonebits[kPMAX][kNW];
   int lib[kPMAX];
   int gsz[kPMAX];
+  int16_t dgt[kPMAX][4];  // diagonal neighbours in the reference order (-1 off the board)
   int16_t lab[kPMAX];
   int8_t col[kPMAX];
+  uint8_t ey[kPMAX];       // bit 0: eyeish for the player to move, bit 1: four neighbours
 };
 
 struct Pos {
@@ -80,66 +82,6 @@ struct Pos {
     }
     return true;
   }
-  // recursive true-eye rule (go.py:298-327) as an explicit DFS; ancestors = frames below top
-  __device__ bool is_eye(int p, int owner) const {
-    if (!eyeish(p, owner)) return false;
-    // frame = point | next diagonal << 9 | bad-diagonal count << 12, one int (a private array:
-    // only the few lanes on eye-shaped points ever touch it)
-    constexpr int MAXD = 24;
-    int fr[MAXD];
-    int sp = 0;
-    fr[0] = p;
-    bool ret = true;
-    bool have_ret = false;
-    while (true) {
-      int f = fr[sp];
-      const int cur = f & 511;
-      int fi = (f >> 9) & 7, fb = f >> 12;
-      const int allow = nnb(cur) == 4 ? 1 : 0;
-      bool done = false;
-      if (have_ret) {
-        have_ret = false;
-        if (!ret) {
-          fb++;
-          if (fb > allow) {
-            ret = false;
-            done = true;
-          }
-        }
-      }
-      if (!done) {
-        bool pushed = false;
-        int d = -1;
-        while (fi < 4) {
-          d = dg(cur, fi++);
-          if (d < 0) continue;
-          if (col[d] == -owner) {
-            if (++fb > allow) break;
-          } else if (col[d] == 0) {
-            bool anc = false;
-            for (int k = 0; k < sp; ++k) anc |= (fr[k] & 511) == d;
-            if (anc) continue;
-            if (!eyeish(d, owner)) {
-              if (++fb > allow) break;
-              continue;
-            }
-            if (sp + 1 >= MAXD) continue;  // deeper than any real board position
-            pushed = true;
-            break;
-          }
-        }
-        fr[sp] = cur | (fi << 9) | (fb << 12);
-        if (pushed) {
-          fr[++sp] = d;
-          continue;
-        }
-        ret = fb <= allow;
-      }
-      if (sp == 0) return ret;
-      --sp;
-      have_ret = true;
-    }
-  }
 };
 
 // set helpers over kNW words. Word selection is unrolled (compile-time indices): a runtime index
@@ -163,6 +105,76 @@ __device__ __forceinline__ int popc6(const unsigned long long* s) {
 #pragma unroll
   for (int k = 0; k < kNW; ++k) c += __popcll(s[k]);
   return c;
+}
+
+// Recursive true-eye rule (go.py:298-327) of point p for the player to move, as an explicit DFS
+// over the diagonal neighbours: frame = point | next diagonal << 9 | bad-diagonal count << 12,
+// the ancestors of the top frame as a 361-bit set in registers (membership in a few
+// instructions instead of a scan of the frames), diagonals / eyeish / four-neighbour flags from
+// the block's LDS tables (no divisions by S per step). The DFS explores every simple path through
+// a diagonal cluster of eyeish points (exponential on checkerboard interiors of late random
+// games): its per-step cost is what the late-game planes pay (380 -> see docs/KERNELS.md).
+__device__ bool is_eye_dfs(int p, int owner, const int8_t* col, const int16_t (*dgt)[4],
+                           const uint8_t* ey) {
+  if (!(ey[p] & 1)) return false;
+  constexpr int MAXD = 24;
+  int fr[MAXD];
+  unsigned long long anc[kNW];
+#pragma unroll
+  for (int w = 0; w < kNW; ++w) anc[w] = 0ull;
+  int sp = 0;
+  fr[0] = p;
+  bool ret = true;
+  bool have_ret = false;
+  while (true) {
+    const int f = fr[sp];
+    const int cur = f & 511;
+    int fi = (f >> 9) & 7, fb = f >> 12;
+    const int allow = (ey[cur] >> 1) & 1;
+    bool done = false;
+    if (have_ret) {
+      have_ret = false;
+      if (!ret) {
+        fb++;
+        if (fb > allow) {
+          ret = false;
+          done = true;
+        }
+      }
+    }
+    if (!done) {
+      bool pushed = false;
+      int d = -1;
+      while (fi < 4) {
+        d = dgt[cur][fi++];
+        if (d < 0) continue;
+        const int cd = col[d];
+        if (cd == -owner) {
+          if (++fb > allow) break;
+        } else if (cd == 0) {
+          if (get_bit6(anc, d)) continue;  // an ancestor on the current path
+          if (!(ey[d] & 1)) {
+            if (++fb > allow) break;
+            continue;
+          }
+          if (sp + 1 >= MAXD) continue;  // deeper than any real board position
+          pushed = true;
+          break;
+        }
+      }
+      fr[sp] = cur | (fi << 9) | (fb << 12);
+      if (pushed) {
+        set_bit6(anc, cur);
+        fr[++sp] = d;
+        continue;
+      }
+      ret = fb <= allow;
+    }
+    if (sp == 0) return ret;
+    --sp;
+    clear_bit6(anc, fr[sp] & 511);  // the new top is no longer its own ancestor
+    have_ret = true;
+  }
 }
 
 // No scratch and ~171 VGPRs (was 256 + 448 B/lane of scratch: runtime-indexed neighbour lists,
@@ -204,6 +216,11 @@ features_kernel(const int8_t* __restrict__ colors, const int16_t* __restrict__ a
     }
   }
   __syncthreads();
+  if (on) {  // the true-eye DFS tables (col[] of every point is in LDS now)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sh.dgt[p][k] = (int16_t)g.dg(p, k);
+    sh.ey[p] = (uint8_t)((g.eyeish(p, me) ? 1 : 0) | (g.nnb(p) == 4 ? 2 : 0));
+  }
   // labels: min stone index of the group. Lanes of other waves may read a neighbour's label
   // while it is lowered; every value read is the index of a stone of the same group and labels
   // only decrease, so the race is benign, and an iteration in which no lane changed anything saw
@@ -357,7 +374,7 @@ features_kernel(const int8_t* __restrict__ colors, const int16_t* __restrict__ a
     // ---- write the planes (the true-eye DFS at most once per point)
     int sensible = -1;
     auto get_sensible = [&]() {
-      if (sensible < 0) sensible = legal && !g.is_eye(p, me);
+      if (sensible < 0) sensible = legal && !is_eye_dfs(p, me, col, sh.dgt, sh.ey);
       return sensible;
     };
     if (sens) sens[(size_t)pos * P + p] = (uint8_t)get_sensible();
