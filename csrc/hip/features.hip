@@ -27,6 +27,7 @@ namespace {
 // walking 6 points per lane (164 -> ~30 us per 128-position ply, profiles/rl_bench_r3.txt).
 constexpr int kNW = 6;    // 64-bit words of a 361-point set
 constexpr int kPMAX = 384;
+constexpr int kEye = 192;  // compact eyeish indices (3 x 64-bit ancestor words)
 
 // feature ids (csrc/engine/go_engine.hpp FeatureId)
 enum { F_BOARD = 0, F_ONES, F_TURNS_SINCE, F_LIBERTIES, F_CAPTURE_SIZE, F_SELF_ATARI_SIZE,
@@ -38,10 +39,17 @@ struct FShared {
   unsigned long long stonebits[kPMAX][kNW];
   int lib[kPMAX];
   int gsz[kPMAX];
-  int16_t dgt[kPMAX][4];  // diagonal neighbours in the reference order (-1 off the board)
+  // true-eye DFS of the player to move, over the eyeish points only (<= 181 on 19x19: no two
+  // are orthogonally adjacent), numbered compactly: per eyeish point its four diagonals in the
+  // reference order as 10-bit entries (target index | class << 8; class 0 off the board / own
+  // stone, 1 bad: an opponent stone or a non-eyeish empty point, 2 an eyeish point), bit 40 =
+  // four neighbours (one bad diagonal allowed)
+  unsigned long long einfo[kEye];
+  int16_t eid[kPMAX];      // compact index of an eyeish point, -1 otherwise
+  int ewave[8];            // eyeish points per wave (the prefix of the numbering)
+  int16_t frs[24][kPMAX];  // the DFS frame stack of each lane (level-major)
   int16_t lab[kPMAX];
   int8_t col[kPMAX];
-  uint8_t ey[kPMAX];       // bit 0: eyeish for the player to move, bit 1: four neighbours
 };
 
 struct Pos {
@@ -107,73 +115,65 @@ __device__ __forceinline__ int popc6(const unsigned long long* s) {
   return c;
 }
 
-// Recursive true-eye rule (go.py:298-327) of point p for the player to move, as an explicit DFS
-// over the diagonal neighbours: frame = point | next diagonal << 9 | bad-diagonal count << 12,
-// the ancestors of the top frame as a 361-bit set in registers (membership in a few
-// instructions instead of a scan of the frames), diagonals / eyeish / four-neighbour flags from
-// the block's LDS tables (no divisions by S per step). The DFS explores every simple path through
-// a diagonal cluster of eyeish points (exponential on checkerboard interiors of late random
-// games): its per-step cost is what the late-game planes pay (380 -> see docs/KERNELS.md).
-__device__ bool is_eye_dfs(int p, int owner, const int8_t* col, const int16_t (*dgt)[4],
-                           const uint8_t* ey) {
-  if (!(ey[p] & 1)) return false;
+// Recursive true-eye rule (go.py:298-327) for the player to move, as an explicit DFS over the
+// compactly numbered eyeish points: the ancestors of the top frame as a 192-bit set in registers,
+// a point's four classified diagonals from one 8-byte LDS entry, the frames below the top in this
+// lane's LDS column. The body is kept small because the lanes of a wave run it in lock-step: the
+// first forms (a private frame array indexed by the per-lane depth, divisions by S, a scan of the
+// frames, then a 361-bit set) cost up to ~3.7k cycles per DFS step, 350 of the 380 us of a
+// late-game 128-board pass (benchmarks/features_bench.py --moves 250 450).
+__device__ __forceinline__ bool anc_has(const unsigned long long (&a)[3], int i) {
+  const unsigned long long w = i < 64 ? a[0] : (i < 128 ? a[1] : a[2]);
+  return (w >> (i & 63)) & 1ull;
+}
+__device__ __forceinline__ void anc_flip(unsigned long long (&a)[3], int i) {
+  const unsigned long long b = 1ull << (i & 63);
+  a[0] ^= i < 64 ? b : 0ull;
+  a[1] ^= (i >= 64 && i < 128) ? b : 0ull;
+  a[2] ^= i >= 128 ? b : 0ull;
+}
+__device__ bool is_eye_dfs(int ci, const unsigned long long* einfo, int16_t* stk) {
   constexpr int MAXD = 24;
-  int fr[MAXD];
-  unsigned long long anc[kNW];
-#pragma unroll
-  for (int w = 0; w < kNW; ++w) anc[w] = 0ull;
-  int sp = 0;
-  fr[0] = p;
-  bool ret = true;
-  bool have_ret = false;
+  unsigned long long anc[3] = {0ull, 0ull, 0ull};
+  int sp = 0, cur = ci, fi = 0, fb = 0;
+  unsigned long long inf = einfo[cur];
   while (true) {
-    const int f = fr[sp];
-    const int cur = f & 511;
-    int fi = (f >> 9) & 7, fb = f >> 12;
-    const int allow = (ey[cur] >> 1) & 1;
-    bool done = false;
-    if (have_ret) {
-      have_ret = false;
-      if (!ret) {
-        fb++;
-        if (fb > allow) {
-          ret = false;
-          done = true;
-        }
+    int allow = (int)((inf >> 40) & 1);
+    int t = 0;
+    bool pushed = false;
+    while (fi < 4) {  // the remaining diagonals of the top frame
+      const int e = (int)((inf >> (10 * fi++)) & 1023);
+      t = e & 255;
+      const int cls = e >> 8;
+      if (cls == 1) {
+        if (++fb > allow) break;
+      } else if (cls == 2 && !anc_has(anc, t) && sp + 1 < MAXD) {  // (deeper: as the reference
+        pushed = true;                                                 // positions never reach)
+        break;
       }
     }
-    if (!done) {
-      bool pushed = false;
-      int d = -1;
-      while (fi < 4) {
-        d = dgt[cur][fi++];
-        if (d < 0) continue;
-        const int cd = col[d];
-        if (cd == -owner) {
-          if (++fb > allow) break;
-        } else if (cd == 0) {
-          if (get_bit6(anc, d)) continue;  // an ancestor on the current path
-          if (!(ey[d] & 1)) {
-            if (++fb > allow) break;
-            continue;
-          }
-          if (sp + 1 >= MAXD) continue;  // deeper than any real board position
-          pushed = true;
-          break;
-        }
-      }
-      fr[sp] = cur | (fi << 9) | (fb << 12);
-      if (pushed) {
-        set_bit6(anc, cur);
-        fr[++sp] = d;
-        continue;
-      }
-      ret = fb <= allow;
+    if (pushed) {
+      stk[sp++ * kPMAX] = (int16_t)(cur | (fi << 8) | (fb << 11));
+      anc_flip(anc, cur);
+      cur = t;
+      inf = einfo[t];
+      fi = 0;
+      fb = 0;
+      continue;
     }
-    if (sp == 0) return ret;
-    --sp;
-    clear_bit6(anc, fr[sp] & 511);  // the new top is no longer its own ancestor
-    have_ret = true;
+    bool r = fb <= allow;
+    while (true) {  // hand r to the parents: a false one is a bad diagonal of the parent
+      if (sp == 0) return r;
+      const int f = stk[--sp * kPMAX];
+      cur = f & 255;
+      fi = (f >> 8) & 7;
+      fb = f >> 11;
+      anc_flip(anc, cur);
+      inf = einfo[cur];
+      allow = (int)((inf >> 40) & 1);
+      if (!r && ++fb > allow) continue;  // the parent fails too
+      break;                              // the parent resumes its diagonals
+    }
   }
 }
 
@@ -216,10 +216,34 @@ features_kernel(const int8_t* __restrict__ colors, const int16_t* __restrict__ a
     }
   }
   __syncthreads();
-  if (on) {  // the true-eye DFS tables (col[] of every point is in LDS now)
+  // the true-eye DFS tables (col[] of every point is in LDS now): eyeish points numbered by a
+  // ballot prefix over the waves, then each one's classified diagonals
+  const bool eyish = on && g.eyeish(p, me);
+  {
+    const unsigned long long bm = __ballot(eyish);
+    if ((p & 63) == 0) sh.ewave[p >> 6] = __popcll(bm);
+    __syncthreads();
+    int base = 0;
+    for (int k = 0; k < (p >> 6); ++k) base += sh.ewave[k];
+    const int rank = __popcll(bm & ((1ull << (p & 63)) - 1ull));
+    if (on) sh.eid[p] = eyish ? (int16_t)(base + rank) : (int16_t)-1;
+    __syncthreads();
+  }
+  if (eyish) {
+    unsigned long long inf = 0ull;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) sh.dgt[p][k] = (int16_t)g.dg(p, k);
-    sh.ey[p] = (uint8_t)((g.eyeish(p, me) ? 1 : 0) | (g.nnb(p) == 4 ? 2 : 0));
+    for (int k = 0; k < 4; ++k) {
+      const int d = g.dg(p, k);
+      int e = 0;
+      if (d >= 0) {
+        const int cd = col[d];
+        if (cd == -me) e = 1 << 8;
+        else if (cd == 0) e = sh.eid[d] >= 0 ? (2 << 8) | sh.eid[d] : (1 << 8);
+      }
+      inf |= (unsigned long long)e << (10 * k);
+    }
+    if (g.nnb(p) == 4) inf |= 1ull << 40;
+    sh.einfo[sh.eid[p]] = inf;
   }
   // labels: min stone index of the group. Lanes of other waves may read a neighbour's label
   // while it is lowered; every value read is the index of a stone of the same group and labels
@@ -374,7 +398,8 @@ features_kernel(const int8_t* __restrict__ colors, const int16_t* __restrict__ a
     // ---- write the planes (the true-eye DFS at most once per point)
     int sensible = -1;
     auto get_sensible = [&]() {
-      if (sensible < 0) sensible = legal && !is_eye_dfs(p, me, col, sh.dgt, sh.ey);
+      if (sensible < 0)
+        sensible = legal && !(sh.eid[p] >= 0 && is_eye_dfs(sh.eid[p], sh.einfo, &sh.frs[0][p]));
       return sensible;
     };
     if (sens) sens[(size_t)pos * P + p] = (uint8_t)get_sensible();
