@@ -118,10 +118,10 @@ __device__ __forceinline__ int popc6(const unsigned long long* s) {
 // Recursive true-eye rule (go.py:298-327) for the player to move, as an explicit DFS over the
 // compactly numbered eyeish points: the ancestors of the top frame as a 192-bit set in registers,
 // a point's four classified diagonals from one 8-byte LDS entry, the frames below the top in this
-// lane's LDS column. The body is kept small because the lanes of a wave run it in lock-step: the
-// first forms (a private frame array indexed by the per-lane depth, divisions by S, a scan of the
-// frames, then a 361-bit set) cost up to ~3.7k cycles per DFS step, 350 of the 380 us of a
-// late-game 128-board pass (benchmarks/features_bench.py --moves 250 450).
+// lane's LDS column. The lanes of a wave run it in lock-step, so each iteration does one small
+// action: the first forms (a private frame array indexed by the per-lane depth, divisions by S, a
+// scan of the frames, nested scan / unwind loops) cost up to ~3.7k cycles per DFS step, 350 of
+// the 380 us of a late-game 128-board pass (benchmarks/features_bench.py --moves 250 450).
 __device__ __forceinline__ bool anc_has(const unsigned long long (&a)[3], int i) {
   const unsigned long long w = i < 64 ? a[0] : (i < 128 ? a[1] : a[2]);
   return (w >> (i & 63)) & 1ull;
@@ -137,32 +137,13 @@ __device__ bool is_eye_dfs(int ci, const unsigned long long* einfo, int16_t* stk
   unsigned long long anc[3] = {0ull, 0ull, 0ull};
   int sp = 0, cur = ci, fi = 0, fb = 0;
   unsigned long long inf = einfo[cur];
+  int allow = (int)((inf >> 40) & 1);
+  bool ret = false, r = true;
+  // one action per iteration (scan one diagonal, push, or hand a result to the parent): the lanes
+  // of a wave stay in step, so a wave pays the longest lane's action count, not its scan steps
+  // plus its deepest unwinding in every round (nested scan / unwind loops: ~3k cycles a round)
   while (true) {
-    int allow = (int)((inf >> 40) & 1);
-    int t = 0;
-    bool pushed = false;
-    while (fi < 4) {  // the remaining diagonals of the top frame
-      const int e = (int)((inf >> (10 * fi++)) & 1023);
-      t = e & 255;
-      const int cls = e >> 8;
-      if (cls == 1) {
-        if (++fb > allow) break;
-      } else if (cls == 2 && !anc_has(anc, t) && sp + 1 < MAXD) {  // (deeper: as the reference
-        pushed = true;                                                 // positions never reach)
-        break;
-      }
-    }
-    if (pushed) {
-      stk[sp++ * kPMAX] = (int16_t)(cur | (fi << 8) | (fb << 11));
-      anc_flip(anc, cur);
-      cur = t;
-      inf = einfo[t];
-      fi = 0;
-      fb = 0;
-      continue;
-    }
-    bool r = fb <= allow;
-    while (true) {  // hand r to the parents: a false one is a bad diagonal of the parent
+    if (ret) {
       if (sp == 0) return r;
       const int f = stk[--sp * kPMAX];
       cur = f & 255;
@@ -171,8 +152,30 @@ __device__ bool is_eye_dfs(int ci, const unsigned long long* einfo, int16_t* stk
       anc_flip(anc, cur);
       inf = einfo[cur];
       allow = (int)((inf >> 40) & 1);
-      if (!r && ++fb > allow) continue;  // the parent fails too
-      break;                              // the parent resumes its diagonals
+      if (!r && ++fb > allow) continue;  // the parent fails too (r stays false)
+      ret = false;                        // the parent resumes its diagonals
+      continue;
+    }
+    if (fi == 4) {  // every diagonal seen
+      r = fb <= allow;
+      ret = true;
+      continue;
+    }
+    const int e = (int)((inf >> (10 * fi++)) & 1023);
+    const int t = e & 255, cls = e >> 8;
+    if (cls == 1) {
+      if (++fb > allow) {
+        r = false;
+        ret = true;
+      }
+    } else if (cls == 2 && !anc_has(anc, t) && sp + 1 < MAXD) {  // (deeper: treated as the
+      stk[sp++ * kPMAX] = (int16_t)(cur | (fi << 8) | (fb << 11));  // reference never reaches)
+      anc_flip(anc, cur);
+      cur = t;
+      inf = einfo[t];
+      allow = (int)((inf >> 40) & 1);
+      fi = 0;
+      fb = 0;
     }
   }
 }
