@@ -61,7 +61,8 @@ def main(argv=None):
             e_ev.record()
             torch.cuda.synchronize()
             ts.append(s_ev.elapsed_time(e_ev) / a.iters * 1e3)
-        print(json.dumps({"batch": B, "moves": a.moves, "median_us": round(statistics.median(ts), 2),
+        print(json.dumps({"batch": B, "moves": a.moves,
+                          "median_us": round(statistics.median(ts), 2),
                           "min_us": round(min(ts), 2)}), flush=True)
 
 
