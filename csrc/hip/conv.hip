@@ -878,7 +878,8 @@ WgradRed rag_wgrad_slab_red(const void* part, const float* bpart, float* dW, flo
 int rag_launch_wgrad_slab_reduce(const WgradRed& r, hipStream_t stream);        // wgrad_slab.hip
 int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpart, int R, int WP,
                           int GC, int CIN, int spc, int CINP, int nchunks, hipStream_t stream,
-                          const float* xcoef, int S, int KS, int COUTP, int pair5);
+                          const float* xcoef, int S, int KS, int COUTP, int pair5,
+                          unsigned* ticket_reset);
 
 namespace {
 // all-taps variant applicability and plan (see wgrad.hip)
@@ -988,8 +989,16 @@ static int conv_wgrad_impl(const void* G, const void* X, float* dW, float* db, f
     int spc = 1;
     nchunks = rag_wgrad_slab_nchunks(R, CINP, &spc, KS, pair5);
     bpart = db ? work + (size_t)nchunks * taps * COUTP * CINP : nullptr;
+    // a reduction deferred on this stream gets claim counters, zeroed by this launch (so a
+    // claiming launch that ended early cannot leave the next one a stale ticket)
+    unsigned* ticket_reset = nullptr;
+    if (defer && bf16_part && !(reduce_stream && reduce_stream != stream)) {
+      PendingRed* p = static_cast<PendingRed*>(pending);
+      if (!p->dticket && hipMalloc(&p->dticket, 2 * sizeof(unsigned)) != hipSuccess) return -3;
+      ticket_reset = p->dticket;
+    }
     const int rc = rag_launch_wgrad_slab(g, x, part, bpart, R, WP, GC, CINP, spc, CINP, nchunks,
-                                         stream, xcoef, S, KS, COUTP, pair5);
+                                         stream, xcoef, S, KS, COUTP, pair5, ticket_reset);
     if (rc) return rc;
   } else if (tp.ok) {
     nchunks = tp.nchunks;
@@ -1037,11 +1046,7 @@ static int conv_wgrad_impl(const void* G, const void* X, float* dW, float* db, f
       PendingRed* p = static_cast<PendingRed*>(pending);
       p->r = r;
       // the riding reduce blocks claim units dynamically (launches that keep the static split
-      // clear the ticket); the counters come with the handle (rag_wgrad_pending_init)
-      if (!p->dticket) {
-        if (hipMalloc(&p->dticket, 2 * sizeof(unsigned)) != hipSuccess) return -3;
-        if (hipMemsetAsync(p->dticket, 0, 2 * sizeof(unsigned), stream) != hipSuccess) return -3;
-      }
+      // clear the ticket) through the handle's counters, which the slab launch above zeroed
       p->r.ticket = p->dticket;
       p->stream = stream;
       p->valid = 1;

@@ -136,8 +136,10 @@ __device__ __forceinline__ void wslab_reduce_blocks(const WgradRed& r, int b, in
 // CU slots the convolution grid leaves free), the convolution blocks after their epilogue. With
 // a static split the few riding blocks did all of it and were the launch's tail (128-channel
 // dgrad: 50 vs 38 us without a reduction). Each block exits after its first failed claim, then
-// counts itself finished; the last one resets both counters for the next launch (the claim's
-// returned value orders it before the count). smem: one int of LDS, free at the call.
+// counts itself finished; the last one resets both counters (the claim's returned value orders
+// it before the count). The slab launch that writes the partials zeroes them as well, so a
+// claiming launch in which some block never got here cannot leave the next reduction a stale
+// ticket (which would skip it). smem: one int of LDS, free at the call.
 template <int U>
 __device__ __forceinline__ void wslab_reduce_dynamic(const WgradRed& r, int* smem) {
   const int T = blockDim.x, tid = threadIdx.x;

@@ -120,7 +120,8 @@ __global__ void __launch_bounds__(64 * WS<N>::Waves)
 wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
                   float* __restrict__ part, float* __restrict__ bpart, int R, int WP, int GC,
                   int CIN, int spc, int CINP, const float* __restrict__ xcoef = nullptr,
-                  int S = 0, int pair5 = 0, int prio = 0) {
+                  int S = 0, int pair5 = 0, int prio = 0,
+                  unsigned* __restrict__ ticket_reset = nullptr) {
   using L = WS<N>;
   static_assert(KS == 3 || (KS == 5 && kBF && kMAP == 0 && !BNX), "5x5: fp16 map-0 partials");
   constexpr int kGrp = KS == 3 ? 1 : KS;  // blocks per (chunk, c-tile): kernel rows
@@ -141,6 +142,9 @@ wgrad_slab_kernel(const bf16* __restrict__ G, const bf16* __restrict__ X,
   // blocks take TWO kernel rows -- waves of c-fragment group 1 compute c-fragment 0 of row ky+1
   // (its X window lies WP rows further down the same 112-row slab): 5 + 3 blocks per chunk
   // instead of 10
+  // a deferred reduction of these partials claims its units through the handle's counters in a
+  // later launch of this stream: zero them here, whatever the previous claiming launch left
+  if (ticket_reset && blockIdx.x == 0 && tid < 2) ticket_reset[tid] = 0u;
   const bool pr = KS == 5 && pair5;
   const int ptc = pr ? 8 : ntc * kGrp;  // (pseudo) c-tiles per chunk
   const int wid = xcd_remap(blockIdx.x, gridDim.x);  // the c-tiles of a chunk share one XCD
@@ -548,18 +552,22 @@ int rag_launch_wgrad_slab_reduce(const WgradRed& r, hipStream_t stream) {
 
 int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpart, int R, int WP,
                           int GC, int CIN, int spc, int CINP, int nchunks, hipStream_t stream,
-                          const float* xcoef, int S, int KS, int COUTP, int pair5) {
+                          const float* xcoef, int S, int KS, int COUTP, int pair5,
+                          unsigned* ticket_reset) {
   const bool bf = rag_wgrad_slab_bf16();
+  if (!bf) ticket_reset = nullptr;  // fp32 partials are never deferred
   if (KS == 5) {  // per-row blocks, fp16 partials, map 0
     if (!bf || xcoef) return -5;
     if (pair5 && CINP != 2 * kC) return -5;
     const dim3 g5(nchunks * (pair5 ? 8 : (CINP / kC) * 5));
     if (COUTP == 192)
       wgrad_slab_kernel<3, true, 0, 192, false, 5><<<g5, 768, 0, stream>>>(
-          G, X, part, bpart, R, WP, GC, CIN, spc, CINP, nullptr, 0, pair5, kWslabPrio);
+          G, X, part, bpart, R, WP, GC, CIN, spc, CINP, nullptr, 0, pair5, kWslabPrio,
+          ticket_reset);
     else if (COUTP == 128)
       wgrad_slab_kernel<3, true, 0, 128, false, 5><<<g5, 512, 0, stream>>>(
-          G, X, part, bpart, R, WP, GC, CIN, spc, CINP, nullptr, 0, pair5, kWslabPrio);
+          G, X, part, bpart, R, WP, GC, CIN, spc, CINP, nullptr, 0, pair5, kWslabPrio,
+          ticket_reset);
     else
       return -5;
     return (int)hipGetLastError();
@@ -569,14 +577,15 @@ int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpar
     if (CINP != 128 || !bf || S > 64) return -5;
     wgrad_slab_kernel<4, true, 0, 128, true><<<grid, 512, 0, stream>>>(G, X, part, bpart, R, WP,
                                                                        GC, CIN, spc, CINP, xcoef,
-                                                                       S, 0, kWslabPrio);
+                                                                       S, 0, kWslabPrio,
+                                                                       ticket_reset);
     return (int)hipGetLastError();
   }
   if (CINP == 128) {  // 8 waves, map 0
     if (bf)
       wgrad_slab_kernel<3, true, 0, 128><<<grid, 512, 0, stream>>>(G, X, part, bpart, R, WP, GC,
                                                                    CIN, spc, CINP, nullptr, 0, 0,
-                                                                   kWslabPrio);
+                                                                   kWslabPrio, ticket_reset);
     else
       wgrad_slab_kernel<3, false, 0, 128><<<grid, 512, 0, stream>>>(G, X, part, bpart, R, WP, GC,
                                                                     CIN, spc, CINP);
@@ -586,7 +595,7 @@ int rag_launch_wgrad_slab(const bf16* G, const bf16* X, float* part, float* bpar
   // fp32 partial slabs (RAG_WGRAD_PART=fp32) and the wave -> tile map (RAG_WGRAD_MAP=0)
 #define RAG_WSLAB(BF, MP)                                                                       \
   wgrad_slab_kernel<3, BF, MP><<<grid, 64 * WS<kN>::Waves, 0, stream>>>(                       \
-      G, X, part, bpart, R, WP, GC, CIN, spc, CINP, nullptr, 0, 0, kWslabPrio)
+      G, X, part, bpart, R, WP, GC, CIN, spc, CINP, nullptr, 0, 0, kWslabPrio, ticket_reset)
   const int mp = wslab_map();
   if (bf && mp) RAG_WSLAB(true, 1);
   else if (bf) RAG_WSLAB(true, 0);
