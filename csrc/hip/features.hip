@@ -43,7 +43,8 @@ struct FShared {
   // are orthogonally adjacent), numbered compactly: per eyeish point its four diagonals in the
   // reference order as 10-bit entries (target index | class << 8; class 0 off the board / own
   // stone, 1 bad: an opponent stone or a non-eyeish empty point, 2 an eyeish point), bit 40 =
-  // four neighbours (one bad diagonal allowed)
+  // four neighbours (one bad diagonal allowed), bits 41-43 the class-1 count, bits 44-47 the
+  // class-2 entries
   unsigned long long einfo[kEye];
   int16_t eid[kPMAX];      // compact index of an eyeish point, -1 otherwise
   int ewave[8];            // eyeish points per wave (the prefix of the numbering)
@@ -135,48 +136,43 @@ __device__ __forceinline__ void anc_flip(unsigned long long (&a)[3], int i) {
 __device__ bool is_eye_dfs(int ci, const unsigned long long* einfo, int16_t* stk) {
   constexpr int MAXD = 24;
   unsigned long long anc[3] = {0ull, 0ull, 0ull};
-  int sp = 0, cur = ci, fi = 0, fb = 0;
+  int sp = 0, cur = ci, fi = 0;
   unsigned long long inf = einfo[cur];
-  int allow = (int)((inf >> 40) & 1);
+  int fb = (int)((inf >> 41) & 7);  // the opponent-stone / non-eyeish diagonals, counted up front
   bool ret = false, r = true;
-  // one action per iteration (scan one diagonal, push, or hand a result to the parent): the lanes
-  // of a wave stay in step, so a wave pays the longest lane's action count, not its scan steps
-  // plus its deepest unwinding in every round (nested scan / unwind loops: ~3k cycles a round)
+  // one action per iteration (push one eyeish diagonal, or hand a result to the parent): the lanes
+  // of a wave stay in step, so a wave pays the longest lane's action count. The rule's result does
+  // not depend on the order of the diagonals (the recursion has no side effects: the stack is
+  // restored), so a frame fails as soon as its bad count exceeds the allowance and succeeds as
+  // soon as its remaining eyeish diagonals could not push it over (no recursion for those)
   while (true) {
     if (ret) {
       if (sp == 0) return r;
       const int f = stk[--sp * kPMAX];
       cur = f & 255;
       fi = (f >> 8) & 7;
-      fb = f >> 11;
+      fb = (f >> 11) + (r ? 0 : 1);
       anc_flip(anc, cur);
       inf = einfo[cur];
-      allow = (int)((inf >> 40) & 1);
-      if (!r && ++fb > allow) continue;  // the parent fails too (r stays false)
-      ret = false;                        // the parent resumes its diagonals
-      continue;
+      ret = false;
     }
-    if (fi == 4) {  // every diagonal seen
+    const int allow = (int)((inf >> 40) & 1);
+    const unsigned m = ((unsigned)(inf >> 44) & 15u) >> fi;  // eyeish diagonals not yet visited
+    if (fb > allow || fb + __popc(m) <= allow) {
       r = fb <= allow;
       ret = true;
       continue;
     }
-    const int e = (int)((inf >> (10 * fi++)) & 1023);
-    const int t = e & 255, cls = e >> 8;
-    if (cls == 1) {
-      if (++fb > allow) {
-        r = false;
-        ret = true;
-      }
-    } else if (cls == 2 && !anc_has(anc, t) && sp + 1 < MAXD) {  // (deeper: treated as the
-      stk[sp++ * kPMAX] = (int16_t)(cur | (fi << 8) | (fb << 11));  // reference never reaches)
-      anc_flip(anc, cur);
-      cur = t;
-      inf = einfo[t];
-      allow = (int)((inf >> 40) & 1);
-      fi = 0;
-      fb = 0;
-    }
+    fi += __builtin_ctz(m);  // m != 0 here
+    const int t = (int)((inf >> (10 * fi)) & 255);
+    ++fi;
+    if (anc_has(anc, t) || sp + 1 >= MAXD) continue;  // on the stack (or deeper than the
+    stk[sp++ * kPMAX] = (int16_t)(cur | (fi << 8) | (fb << 11));  // reference ever reaches)
+    anc_flip(anc, cur);
+    cur = t;
+    inf = einfo[t];
+    fi = 0;
+    fb = (int)((inf >> 41) & 7);
   }
 }
 
@@ -234,6 +230,7 @@ features_kernel(const int8_t* __restrict__ colors, const int16_t* __restrict__ a
   }
   if (eyish) {
     unsigned long long inf = 0ull;
+    int n1 = 0, m2 = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int d = g.dg(p, k);
@@ -244,8 +241,11 @@ features_kernel(const int8_t* __restrict__ colors, const int16_t* __restrict__ a
         else if (cd == 0) e = sh.eid[d] >= 0 ? (2 << 8) | sh.eid[d] : (1 << 8);
       }
       inf |= (unsigned long long)e << (10 * k);
+      n1 += (e >> 8) == 1;
+      m2 |= ((e >> 8) == 2) << k;
     }
     if (g.nnb(p) == 4) inf |= 1ull << 40;
+    inf |= (unsigned long long)n1 << 41 | (unsigned long long)m2 << 44;
     sh.einfo[sh.eid[p]] = inf;
   }
   // labels: min stone index of the group. Lanes of other waves may read a neighbour's label

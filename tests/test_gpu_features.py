@@ -61,3 +61,26 @@ def test_gpu_features_superko_and_subsets(dev):
         got = gf([s.native for s in states]).cpu().numpy()
         want = rg.batch_features([s.native for s in states], Preprocess(feats).feature_ids, 4)
         assert np.array_equal(got, want), feats
+
+
+def test_gpu_sensibleness_late_game(dev):
+    """The true-eye DFS (pruned frames: a frame fails once its bad diagonals exceed the allowance
+    and succeeds once its remaining eyeish diagonals cannot) on late-game 19x19 positions, where
+    large eyeish regions make the recursion deep: the same planes as the native extractor."""
+    from rocalphago_amd.ops.features import GpuFeatures
+    rs = np.random.RandomState(11)
+    rp = rg.RolloutPolicy()
+    states = []
+    for _ in range(96):
+        st = GameState()
+        for _ in range(int(rs.randint(250, 450))):
+            mv = rp.sample(st.native, int(rs.randint(1 << 30)))
+            st.do_move(None if mv < 0 else divmod(mv, 19))
+            if st.is_end_of_game:
+                break
+        states.append(st)
+    feats = ["sensibleness", "legal", "board"]
+    gf = GpuFeatures(feats, dev, ladders="host")
+    got = gf([s.native for s in states]).cpu().numpy()
+    want = rg.batch_features([s.native for s in states], Preprocess(feats).feature_ids, 4)
+    assert np.array_equal(got, want), int((got != want).sum())
