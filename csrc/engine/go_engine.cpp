@@ -374,19 +374,28 @@ bool Board::is_eyeish(int p, int owner) const {
   return true;
 }
 
+// The rule's result does not depend on the order of the diagonals (the recursion restores its
+// stack), so the opponent stones are counted first, and a point stops recursing as soon as its
+// bad count exceeds the allowance or its remaining empty diagonals could not push it over.
 bool Board::is_eye_stack(int p, int owner, std::vector<int>& stack) const {
   if (!is_eyeish(p, owner)) return false;
-  int num_bad = 0;
-  int allow = (g_->nnbr[p] == 4) ? 1 : 0;
+  const int allow = (g_->nnbr[p] == 4) ? 1 : 0;
+  int num_bad = 0, rem = 0;
+  int cand[4];
   for (int i = 0; i < g_->ndiag[p]; ++i) {
-    int d = g_->diag[p][i];
+    const int d = g_->diag[p][i];
     if (color_[d] == -owner) {
       num_bad++;
     } else if (color_[d] == EMPTY && std::find(stack.begin(), stack.end(), d) == stack.end()) {
-      stack.push_back(p);
-      if (!is_eye_stack(d, owner, stack)) num_bad++;
-      stack.pop_back();
+      cand[rem++] = d;
     }
+  }
+  if (num_bad > allow) return false;
+  for (int i = 0; i < rem; ++i) {
+    if (num_bad + (rem - i) <= allow) return true;
+    stack.push_back(p);
+    if (!is_eye_stack(cand[i], owner, stack)) num_bad++;
+    stack.pop_back();
     if (num_bad > allow) return false;
   }
   return true;
