@@ -1112,7 +1112,19 @@ constexpr int kPackFields = 11;
 // coalesced: the forward layout [tap][n][c] along c, the dgrad layout [tap'][c][n] along n. The
 // element-per-thread version wrote the dgrad layout 2 bytes per 384-byte stride (29 us/step); one
 // block per all-tap 32x32 tile (contiguous OIHW runs through LDS) measured 29-47 us: kept this.
-__global__ void __launch_bounds__(256) pack_trunk_kernel(const int64_t* __restrict__ table) {
+__global__ void __launch_bounds__(256) pack_trunk_kernel(const int64_t* __restrict__ table,
+                                                         int nrows, int nfull) {
+  if ((int)blockIdx.y == nfull) {  // the bias-only rows (after the nfull packed ones): one block each
+    for (int r = nfull + blockIdx.x; r < nrows; r += gridDim.x) {
+      const int64_t* t = table + (size_t)r * kPackFields;
+      const float* b = (const float*)t[1];
+      const int COUT = (int)t[2], COUTP = (int)t[5];
+      float* bo = (float*)t[9];
+      if (bo)
+        for (int n = threadIdx.x; n < COUTP; n += blockDim.x) bo[n] = (b && n < COUT) ? b[n] : 0.f;
+    }
+    return;
+  }
   const int64_t* t = table + (size_t)blockIdx.y * kPackFields;
   const float* W = (const float*)t[0];
   const float* b = (const float*)t[1];
@@ -1162,11 +1174,15 @@ __global__ void __launch_bounds__(256) pack_trunk_kernel(const int64_t* __restri
 }
 }  // namespace
 
-RAG_API int rag_pack_trunk(const int64_t* table, int nlayers, int64_t total, hipStream_t stream) {
-  // total: the grid width, max over layers of 8 * taps * ceil(64x64 tiles / 8) (XCD-grouped order)
-  if (nlayers <= 0 || total <= 0 || total % 8) return -1;
-  const dim3 grid((unsigned)total, (unsigned)nlayers);
-  pack_trunk_kernel<<<grid, 256, 0, stream>>>(table);
+RAG_API int rag_pack_trunk(const int64_t* table, int nrows, int nfull, int64_t total,
+                           hipStream_t stream) {
+  // total: the grid width, max over layers of 8 * taps * ceil(64x64 tiles / 8) (XCD-grouped order).
+  // Rows [0, nfull) pack weights (one grid row each); rows [nfull, nrows) only pad their bias
+  // (Winograd layers: rag_wino_pack packs the weights) and share one grid row: the 11 bias-only
+  // rows of the SL trunk were 11 x 200 blocks that exited at once.
+  if (nrows <= 0 || nfull < 0 || nfull > nrows || total <= 0 || total % 8) return -1;
+  const dim3 grid((unsigned)total, (unsigned)(nfull + (nrows > nfull ? 1 : 0)));
+  pack_trunk_kernel<<<grid, 256, 0, stream>>>(table, nrows, nfull);
   return (int)hipGetLastError();
 }
 

@@ -105,8 +105,12 @@ class _PackedConvs(object):
                                   self._uf[l].data_ptr(), ub, wd])
                     row = row[:7] + [0, 0] + row[9:]
                 rows.append(row)
+            # the rows that pack weights first; the bias-only rows share one grid row
+            full = [l for l, r in enumerate(rows) if r[7] or r[8]]
+            rows = [rows[l] for l in full] + [r for r in rows if not (r[7] or r[8])]
+            self._pack_nfull = len(full)
             self._pack_table = torch.tensor(rows, dtype=torch.int64).to(self.device)
-            self._pack_total = pack_grid_width(self.specs)
+            self._pack_total = pack_grid_width([self.specs[l] for l in full]) if full else 8
             wsp = [s for l, s in enumerate(self.specs) if self._wino[l]]
             if wsp:
                 self._dpack_table = torch.tensor(drows, dtype=torch.int64).to(self.device)
@@ -115,7 +119,7 @@ class _PackedConvs(object):
                 self._wpack_tiles = max(-(-s.coutp // 64) * -(-s.cinp // 64) for s in wsp)
             self._pack_key = key
             self._pack_keep = ws  # keep contiguous copies alive while the table points at them
-        ops.pack_trunk(self._pack_table, len(self.specs), self._pack_total)
+        ops.pack_trunk(self._pack_table, len(self.specs), self._pack_total, self._pack_nfull)
         if any(self._wino):
             ops.wino_pack(self._wpack_table, sum(self._wino), self._wpack_tiles)
         self._packed_version = version

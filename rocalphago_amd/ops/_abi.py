@@ -23,7 +23,7 @@ SIGNATURES = {
     "rag_wgrad_pending_init": [P],
     "rag_wgrad_pending_free": [P],
     "rag_pack_weights": [P, P, P, I, I, I, I, I, P],
-    "rag_pack_trunk": [P, I, I64, P],
+    "rag_pack_trunk": [P, I, I, I64, P],
     # conv_wino.hip (+ the pending-handle entry in conv.hip)
     "rag_conv_wino_ok": [I, I, I, I, I],
     "rag_conv_wino": [P, P, P, P, P, I, I, I, I, I, I, I, I, P],

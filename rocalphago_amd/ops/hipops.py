@@ -62,10 +62,13 @@ def pack_weights(w, coutp, cinp, wf=None, wb=None):
     return wf, wb
 
 
-def pack_trunk(table, nlayers, total):
-    """Repack every layer of a trunk in one launch (table: device int64 [nlayers, 11], see
-    rag_pack_trunk in csrc/hip/conv.hip; ``total`` = 64x64 tap tiles of the largest layer)."""
-    _check(_lib().rag_pack_trunk(_ptr(table), nlayers, int(total), _stream()), "pack_trunk")
+def pack_trunk(table, nrows, total, nfull=None):
+    """Repack every layer of a trunk in one launch (table: device int64 [nrows, 11], see
+    rag_pack_trunk in csrc/hip/conv.hip; ``total`` = 64x64 tap tiles of the largest layer). Rows
+    past the first ``nfull`` (default: all) only pad their bias."""
+    nfull = nrows if nfull is None else nfull
+    _check(_lib().rag_pack_trunk(_ptr(table), nrows, nfull, int(total), _stream()),
+           "pack_trunk")
 
 
 class PendingReduction(object):
