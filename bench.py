@@ -77,9 +77,9 @@ def main():
                     help="skip the APV-MCTS sims/s measurement (run after the timed SL steps)")
     ap.add_argument("--mcts-playouts", type=int, default=8192)
     ap.add_argument("--mcts-mode", default="master", choices=["master", "shared"],
-                    help="N>1 search: one tree on rank 0 with leaf waves on every GPU (master), "
-                         "or N trees with shared root statistics (shared; measured 1/N budget "
-                         "efficiency, kept for comparison)")
+                    help="N>1 search: one tree on rank 0 whose leaf waves every GPU serves "
+                         "(master), or N trees with shared root statistics (shared; measured "
+                         "1/N budget efficiency, kept for comparison)")
     ap.add_argument("--mcts-guard-s", type=int, default=180,
                     help="N>1: wall-clock limit of the multi-GPU search measurement")
     ap.add_argument("--trace", default=None,
@@ -286,10 +286,10 @@ def main():
             guard.start()
         try:
             if dp.world > 1:
-                # ONE tree (rank 0) whose rounds keep the one-GPU search's leaves in flight,
-                # evaluated on all N GPUs: every simulation is a distinct node of one search
-                # (search/efficiency.py: budget efficiency 1.0 at N = 2, 4, 8, where N trees with
-                # shared root statistics measured 1/N; profiles/search_efficiency_r4.json)
+                # ONE tree (rank 0, native master loop) whose leaf waves every GPU serves through
+                # a shared-memory channel (search/distributed.py); its budget efficiency against
+                # one tree of the same budget is measured separately by search/efficiency.py
+                # (profiles/search_efficiency_r6.json) and not folded into this rate
                 from benchmarks.mcts_bench import distributed_wave, measure_distributed
                 r = measure_distributed(dp, dev, playouts=args.mcts_playouts * dp.world,
                                         mode=args.mcts_mode,
@@ -327,12 +327,12 @@ def main():
             if dp.is_root and "leaves_per_rank" in r:
                 result["mcts_leaves_per_rank"] = r["leaves_per_rank"]
             if dp.is_root and dp.world > 1:
-                # rank 0's host split of the N-GPU search (fractions of its wall time) and the
-                # mean round time: the diagnosis of a scale run, not just its rate
+                # rank 0's host split of the N-GPU search (fractions of its wall time): the
+                # diagnosis of a scale run, not just its rate
                 for k, v in r.items():
                     if k.startswith("t_") and k.endswith("_frac"):
                         result["mcts_" + k] = v
-                for k in ("rounds", "round_ms"):
+                for k in ("waves", "max_leaves_in_flight", "master_share"):
                     if k in r:
                         result["mcts_" + k] = r[k]
             if dp.is_root and dp.world > 1:

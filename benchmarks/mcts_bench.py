@@ -62,27 +62,27 @@ def measure(device, playouts=8192, warmup=512, moves=1, **kw):
     return out
 
 
+# The N-GPU search's geometry (leaves per GPU wave, waves per GPU awaiting values, rank 0's share
+# of a wave), chosen by effective throughput = sims/s x budget efficiency
+# (benchmarks/search_efficiency.py --effective, profiles/search_efficiency_r6.json).
+DIST_GEOMETRY = {"batch": 512, "depth": 2, "master_share": 1.0}
+
+
 def distributed_wave(world, mode="master"):
-    """Leaves per rank and round of the N-GPU search. master: the round (N waves) keeps the
-    one-GPU search's 512 leaves in flight -- N x 512 per round would search like one tree with
-    N-times-wider waves (budget efficiency 0.24 at N = 8 in search/efficiency.py's study) --
-    down to 64 leaves per GPU pass. With at least 128 per GPU (round 4) N = 8 ran 1024 leaves per
-    round and measured 0.63 at the bench's geometry (lambda 0.5, rollouts); capped at 512 it
-    measures 0.81 (profiles/search_efficiency_r5.json), and rank 0's tree work per simulation,
-    which bounds the N = 8 rate, is the same either way. shared: every rank runs the one-GPU
-    search."""
+    """Leaves per GPU wave of the N-GPU search (mode "shared": every rank runs the one-GPU
+    search, 512)."""
     if mode != "master" or world <= 1:
         return 512
-    return max(64, 512 // world)
+    return DIST_GEOMETRY["batch"]
 
 
 def measure_distributed(dp, device, playouts=8192, warmup=512, moves=1, filters=192,
                         layers=12, batch=512, rollouts_per_leaf=1, lmbda=0.5, nthreads=16,
-                        seed=1, rollout_delay=6, mode="master"):
+                        seed=1, mode="master", depth=None, master_share=None):
     """Search over all ranks (search/distributed.py). mode "master" (default): one tree on rank 0
-    with leaf waves dealt to all ranks (DistributedMCTS); "shared": every rank runs the pipelined
-    single-GPU search with shared root statistics (SharedRootMCTS; its duplicated expansions
-    are measured and reported).
+    with leaf waves served by every rank through the shared-memory channel (DistributedMCTS);
+    "shared": every rank runs the pipelined single-GPU search with shared root statistics
+    (SharedRootMCTS; its duplicated expansions are measured and reported).
     Collective: every rank calls it; rank 0's dict has the job's sims/s, the others None."""
     if mode == "shared":
         return _measure_shared(dp, device, playouts, warmup, moves, filters, layers, batch,
@@ -93,44 +93,45 @@ def measure_distributed(dp, device, playouts=8192, warmup=512, moves=1, filters=
     from rocalphago_amd.models.policy import CNNPolicy
     from rocalphago_amd.models.value import CNNValue
     from rocalphago_amd.search.distributed import DistributedMCTS
+    depth = DIST_GEOMETRY["depth"] if depth is None else depth
+    share = DIST_GEOMETRY["master_share"] if master_share is None else master_share
     pol = CNNPolicy(DEFAULT_FEATURES, board=19, filters_per_layer=filters, layers=layers,
                     device=device, seed=seed)
     val = CNNValue(DEFAULT_FEATURES + ["color"], board=19, filters_per_layer=filters,
                    layers=layers, device=device, seed=seed + 1)
     mc = DistributedMCTS(pol, val, dp=dp, lmbda=lmbda, batch=batch, nthreads=nthreads,
-                         rollouts_per_leaf=rollouts_per_leaf, seed=seed,
-                         rollout_delay=rollout_delay)
+                         rollouts_per_leaf=rollouts_per_leaf, seed=seed, depth=depth,
+                         master_share=share, force_master=True)
     st = GameState()
     mc.n_playout = warmup
     mv = mc.get_move(st)  # compiles / allocates; the tree is discarded below
     mc._search = None
     mc.n_playout = playouts
     mc.stats = {"waves": 0, "sims": 0}
+    mc.leaves_per_rank[:] = 0
     torch.cuda.synchronize()
+    dp.barrier()
     t0 = time.perf_counter()
     for _ in range(moves):
         mv = mc.get_move(st)
-        if dp.rank == 0:
-            st.do_move(mv)
+        st.do_move(mv)
         mc.update_with_move(mv)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    counts = mc.leaf_counts()
     if dp.rank != 0:
         return None
     s = mc.stats
+    m = mc.master_stats
     out = {"sims_per_s": s["sims"] / dt, "sims": s["sims"], "seconds": dt, "waves": s["waves"],
-           "batch": batch, "rollouts_per_leaf": rollouts_per_leaf, "rollout_device": "gpu",
-           "gpus": dp.world, "leaves_per_rank": [int(c) for c in counts],
-           "mode": "master", "duplication": 1.0, "leaves_per_round": batch * dp.world}
+           "batch": batch, "depth": depth, "master_share": share, "nslots": mc.nslots,
+           "rollouts_per_leaf": rollouts_per_leaf, "rollout_device": "gpu", "gpus": dp.world,
+           "leaves_per_rank": [int(c) for c in mc.leaf_counts()], "mode": "master",
+           "duplication": 1.0, "max_leaves_in_flight": int(m.get("max_inflight", 0))}
     if lmbda > 0:
         out["rollouts_per_s"] = s["sims"] * rollouts_per_leaf / dt
-    # rank 0's round split (search/distributed.py DistributedMCTS.search)
-    for k in ("t_select", "t_pack", "t_ship", "t_gather", "t_backup", "t_eval"):
+    # rank 0's master-loop split (csrc/mcts/master.hpp run_master)
+    for k in ("t_select", "t_ship", "t_value", "t_rollout", "t_idle"):
         out[k + "_frac"] = round(s.get(k, 0.0) / dt, 3)
-    if s.get("rounds"):
-        out["rounds"] = int(s["rounds"])
-        out["round_ms"] = round(dt / s["rounds"] * 1e3, 3)
     return out
 
 
@@ -222,8 +223,10 @@ def main():
     ap.add_argument("--max-inflight", type=int, default=8, help="rollout waves in flight")
     ap.add_argument("--rollout-group", type=int, default=6, help="waves per rollout launch")
     ap.add_argument("--moves", type=int, default=1)
-    ap.add_argument("--rollout-delay", type=int, default=6,
-                    help="--distributed: rounds a wave's rollouts may stay in flight")
+    ap.add_argument("--depth", type=int, default=None,
+                    help="--distributed: waves per GPU awaiting values (default DIST_GEOMETRY)")
+    ap.add_argument("--master-share", type=float, default=None,
+                    help="--distributed: rank 0's wave relative to the others'")
     ap.add_argument("--distributed", action="store_true",
                     help="one search over all torchrun ranks (search/distributed.py)")
     ap.add_argument("--mode", default="master", choices=["shared", "master"],
@@ -238,7 +241,8 @@ def main():
                                 if args.batch == 512 else args.batch,
                                 moves=args.moves, rollouts_per_leaf=args.rollouts_per_leaf,
                                 lmbda=args.lmbda, filters=args.filters, nthreads=args.threads,
-                                rollout_delay=args.rollout_delay, mode=args.mode)
+                                mode=args.mode, depth=args.depth,
+                                master_share=args.master_share)
         if r is not None:
             r.update({"metric": "MCTS simulations/s (19x19 APV-MCTS, one search over %d GPUs)"
                       % dp.world, "lmbda": args.lmbda})

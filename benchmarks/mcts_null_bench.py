@@ -7,7 +7,8 @@ board construction, leaf packing, expansion and backup) can sustain. No GPU is u
   python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \
       benchmarks/mcts_null_bench.py --distributed --threads 4
   python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
-      benchmarks/mcts_null_bench.py --distributed --mode master --batch 128 --threads 2
+      benchmarks/mcts_null_bench.py --distributed --mode master --batch 512 --threads 2
+  python benchmarks/mcts_null_bench.py --distributed --mode master    (one process: N = 1)
 
 Single process: one JSON line with sims/s and the per-phase split (select, pack, eval = the
 null evaluator itself, backup). ``--distributed`` (gloo, CPU): the shared-root multi-rank search
@@ -158,22 +159,15 @@ def run_distributed(args):
         dp.shutdown()
 
 
-class NullRollout(object):
-    """Rollout policy stand-in: every game a draw (z = 0), returned at once."""
-
-    def rollouts(self, boards, seed=0, limit=500, nthreads=1):
-        return np.zeros(len(boards), np.int32)
-
-
 def run_master(args):
-    """DistributedMCTS master mode (search/distributed.py, the multi-GPU bench's search) with
-    the null evaluator and null rollouts on every rank: ONE tree on rank 0, each round's waves of
-    ``--batch`` leaves scattered to the ranks as records, rebuilt there, "evaluated" and
-    all-gathered back. Rank 0's sims/s is the host ceiling of the N-GPU search; its split
-    (select / pack / ship / gather / backup fractions of its wall time) says what bounds it.
-    ``--eval-ms``: a fixed per-wave evaluation time on every rank (the GPU pass it stands for).
-    gloo on CPU (torchrun, 127.0.0.1)."""
-    import torch
+    """DistributedMCTS (search/distributed.py, the multi-GPU bench's search) with the null
+    evaluator and null rollouts on every rank: ONE tree on rank 0 whose native master loop
+    (csrc/mcts/master.hpp) ships waves of ``--batch`` leaves per rank as move paths through the
+    shared-memory channel; every rank (rank 0 on a second thread, ``--master-share``) replays
+    them, "evaluates" them and answers. Rank 0's sims/s is the host ceiling of the N-GPU search,
+    its split (select / ship / value backup / rollout backup / idle, fractions of its wall time)
+    says what bounds it. ``--eval-ms``: a fixed evaluation time per wave on every rank (the GPU
+    pass it stands for). gloo only for the set-up (torchrun, 127.0.0.1)."""
     from rocalphago_amd.engine.gamestate import GameState
     from rocalphago_amd.parallel.dp import DPContext
     from rocalphago_amd.search.distributed import DistributedMCTS
@@ -181,44 +175,43 @@ def run_master(args):
     # rank 0 owns the tree: on a real node every rank has its own cores, so the master may get
     # more host threads than the evaluating ranks (--threads-master)
     nt = args.threads_master if dp.rank == 0 and args.threads_master else args.threads
-    ev = NullEvaluator(nthreads=nt, seed=dp.rank)
+    ev = NullEvaluator(nthreads=args.threads, seed=dp.rank)
     ev.delay = args.eval_ms * 1e-3
     mc = DistributedMCTS(None, value=True, evaluator=ev, dp=dp, lmbda=args.lmbda,
-                         batch=args.batch, nthreads=nt,
-                         rollout_delay=args.rollout_delay, force_master=True)
-    mc.leaf_eval.rollout = NullRollout()  # the ranks' rollouts (the tree keeps its policy)
+                         batch=args.batch, nthreads=nt, depth=args.depth,
+                         rollout_slots=args.rollout_slots, master_share=args.master_share,
+                         board=19, force_master=True, worker_threads=args.threads)
+    mc.worker_rollouts = "null"
     st = GameState()
     mc.n_playout = 4 * args.batch * dp.world
     mc.get_move(st)  # warm-up (arenas, pools); a fresh tree below
     mc._search = None
     mc.stats = {"waves": 0, "sims": 0}
-    mc.rank_leaves = 0
+    mc.leaves_per_rank[:] = 0
     mc.n_playout = args.playouts
     dp.barrier()
     t0 = time.perf_counter()
-    mc.get_move(st)
-    dt = time.perf_counter() - t0
     if dp.rank == 0:
-        s = mc.stats
-        out = {"metric": "DistributedMCTS master-mode host ceiling (null evaluator + rollouts, "
-                         "gloo), 19x19",
-               "ranks": dp.world, "threads_rank0": nt, "threads_per_rank": args.threads,
-               "batch_per_rank": args.batch,
-               "lmbda": args.lmbda, "rollout_delay": args.rollout_delay,
-               "eval_ms_per_wave": args.eval_ms, "sims": int(s["sims"]),
-               "seconds": round(dt, 3), "sims_per_s": round(s["sims"] / dt, 1),
-               "rounds": int(s.get("rounds", 0)),
-               "round_ms": round(dt / max(1, s.get("rounds", 0)) * 1e3, 3),
-               "us_per_sim": {k[2:]: round(s.get(k, 0.0) / max(1, s["sims"]) * 1e6, 3)
-                              for k in ("t_select", "t_pack", "t_ship", "t_gather",
-                                        "t_backup")},
-               "frac": {k[2:]: round(s.get(k, 0.0) / dt, 3)
-                        for k in ("t_select", "t_pack", "t_ship", "t_gather", "t_backup")},
-               "leaves_per_rank": [int(c) for c in mc.leaf_counts()]}
+        s = mc.search(st)
+        dt = time.perf_counter() - t0
+        mc.stop()
+        m = mc.master_stats
+        keys = ("t_select", "t_ship", "t_value", "t_rollout", "t_idle")
+        out = {"metric": "DistributedMCTS host ceiling (native master loop + shared-memory "
+                         "channel; null evaluator + null rollouts), 19x19",
+               "ranks": dp.world, "threads_master": nt, "threads_per_rank": args.threads,
+               "batch_per_rank": args.batch, "master_share": args.master_share,
+               "depth": args.depth, "nslots": mc.nslots, "lmbda": args.lmbda,
+               "eval_ms_per_wave": args.eval_ms, "sims": int(m["sims"]),
+               "seconds": round(dt, 3), "sims_per_s": round(m["sims"] / dt, 1),
+               "waves": int(m["waves"]), "max_leaves_in_flight": int(m["max_inflight"]),
+               "us_per_sim": {k[2:]: round(m[k] / max(1, m["sims"]) * 1e6, 3) for k in keys},
+               "frac": {k[2:]: round(m[k] / dt, 3) for k in keys},
+               "tree_timers_s": [round(x, 4) for x in s.timers],
+               "leaves_per_rank": [int(c) for c in m["leaves"]]}
         print(json.dumps(out), flush=True)
     else:
-        mc.leaf_counts()
-    _ = torch
+        mc.serve()
     if dp.enabled:
         dp.shutdown()
 
@@ -235,9 +228,13 @@ def main():
                     help="--distributed: shared-root trees or the one-tree master search")
     ap.add_argument("--eval-ms", type=float, default=0.0,
                     help="master: fixed evaluation time per wave and rank")
-    ap.add_argument("--rollout-delay", type=int, default=6)
+    ap.add_argument("--depth", type=int, default=2, help="master: waves per rank awaiting values")
+    ap.add_argument("--rollout-slots", type=int, default=6,
+                    help="master: further waves per rank holding virtual loss until rollouts")
+    ap.add_argument("--master-share", type=float, default=1.0,
+                    help="master: rank 0's wave relative to the other ranks' (0: none)")
     ap.add_argument("--threads-master", type=int, default=0,
-                    help="master: rank 0's host threads (default --threads)")
+                    help="master: rank 0's tree threads (default --threads)")
     args = ap.parse_args()
     if args.distributed and args.mode == "master":
         run_master(args)

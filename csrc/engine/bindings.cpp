@@ -25,6 +25,7 @@ int replay_sgf_positions(const char* text, size_t len, int bd_size,
                          const std::shared_ptr<const Zobrist>& zob, std::vector<Board>& boards,
                          std::vector<uint8_t>& actions);
 void register_rollout(py::module_& m);
+void register_master(py::module_& m);
 void register_gamebatch(py::module_& m);
 
 std::shared_ptr<const Zobrist> make_zobrist(py::array_t<uint64_t, py::array::c_style> w,
@@ -496,4 +497,5 @@ PYBIND11_MODULE(_rocgo, m) {
   register_search(m);
   register_gamebatch(m);
   register_rollout(m);
+  register_master(m);
 }

@@ -921,12 +921,12 @@ bool rag_conv_tap_launch(const bf16* x, const bf16* w, const float* bias, bf16* 
     // chunk 1 steps pair two taps
     const bool pair5 = CIN == 64 && g_conv_cin_real > 0 && g_conv_cin_real <= 48;
     if (nconv < kPPMinBlocks) {
-      // sub-chip grids (128-game self-play passes): 192-pixel blocks, as the 3x3 layers; also
-      // any grid of at most one wave of them (a block's time is the launch's: the self-play
-      // tail's plies of < 107 games ran conv_pipe at 45.6 us against 32.5 us for this kernel
-      // at 128 games, profiles/rl_selfplay_r5.txt)
+      // sub-chip grids (128-game self-play passes): 192-pixel blocks, as the 3x3 layers, at
+      // every such batch (a block's time is the launch's: the self-play tail's plies of < 107
+      // games ran conv_pipe at 45.6 us against 32.5 us for this kernel at 128 games,
+      // profiles/rl_selfplay_r5.txt)
       const int n192 = ((M + kBM - 1) / kBM) * (COUTP / kBN);
-      if (!w192 || (n192 < kPPMinBlocks && n192 > 256) || rows5b > kPPSlabRows192x5) return false;
+      if (!w192 || rows5b > kPPSlabRows192x5) return false;
       const int nred = reduce_slots(n192, red, r, false);
       if (pair5)
         conv_tap_pp_kernel<3, 6, false, 5, 3, 0, 0, 1><<<n192 + nred, 512, 0, stream>>>(

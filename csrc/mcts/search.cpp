@@ -32,8 +32,39 @@ void register_search(py::module_& m) {
       .def_property_readonly("nthreads", &Search::nthreads)
       .def("set_rollout_policy",
            [](Search& s, std::shared_ptr<RolloutPolicy> p) { s.rollout_policy = p; })
-      .def("select", &Search::select, py::arg("batch"),
-           py::call_guard<py::gil_scoped_release>())
+      .def("select", &Search::select, py::arg("batch"), py::arg("build") = true,
+           py::call_guard<py::gil_scoped_release>(),
+           "(wave id, leaves); build=False: no leaf boards (the leaves ship as move paths)")
+      .def("write_paths",
+           [](Search& s, int id, int stride) {
+             const int n = s.num_leaves(id);
+             py::array_t<int16_t> a({n, stride});
+             s.write_paths(id, 0, n, a.mutable_data(), stride);
+             return a;
+           },
+           py::arg("wave"), py::arg("stride") = 64,
+           "[n, stride] int16 path records (depth, moves from the root) of a wave's leaves")
+      .def("load_paths",
+           [](Search& s, py::array_t<int16_t, py::array::c_style | py::array::forcecast> recs) {
+             if (recs.ndim() != 2) throw std::invalid_argument("path records must be [n, stride]");
+             const int n = (int)recs.shape(0), stride = (int)recs.shape(1);
+             const int16_t* p = recs.data();
+             py::gil_scoped_release nogil;
+             return s.load_paths(p, n, stride);
+           },
+           "A wave of leaf boards rebuilt from path records (root board + moves); returns its id")
+      .def("rollout_black_z",
+           [](Search& s, int id) {
+             py::array_t<float> a(s.num_leaves(id));
+             float* o = a.mutable_data();
+             {
+               py::gil_scoped_release nogil;
+               s.rollout_black_z(id, o);
+             }
+             return a;
+           },
+           "CPU rollout results of a wave (start_rollouts) from BLACK's point of view")
+      .def("drop_wave", &Search::drop_wave, py::call_guard<py::gil_scoped_release>())
       .def_readwrite("parallel_select_min", &Search::parallel_select_min)
       .def_readwrite("pass_prior", &Search::pass_prior)
       .def("leaf_nodes",

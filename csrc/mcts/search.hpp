@@ -219,14 +219,16 @@ class Arena {
 };
 
 struct Leaf {
-  Board board;
+  Board board;                // built unless the wave was selected for shipping (paths only)
   std::vector<int32_t> path;  // root .. leaf
   float z = 0.f;
+  int8_t ptm = 0;             // player to move at the leaf
 };
 
 struct Wave {
   std::vector<Leaf> leaves;
   bool value_done = false;
+  bool built = true;   // leaf boards exist (false: select(B, false), the multi-GPU master)
   std::thread worker;  // CPU rollouts
   bool rolling = false;
 };
@@ -454,7 +456,11 @@ class Search {
   // moves) are built in parallel on the pool; (3) descents that ended on a terminal position are
   // scored on their board and backed up at once (their virtual loss, taken in phase 1 so that
   // later walks of the same wave avoid them, is dropped again).
-  std::pair<int, int> select(int B) {
+  //
+  // build = false (the multi-GPU master, csrc/mcts/master.hpp): the leaf boards are not built —
+  // the evaluating rank rebuilds them from the root and the shipped move paths (write_paths /
+  // load_paths) — only terminal descents get a board, to be scored.
+  std::pair<int, int> select(int B, bool build = true) {
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
     collisions_ = 0;
@@ -490,23 +496,34 @@ class Search {
     // terminal descents get a scratch board
     std::unique_ptr<Wave> wave = take_wave();
     wave->leaves.resize(nleaf);
+    wave->built = build;
     std::vector<int> slot(nd);
     int nt = 0, nl = 0;
     for (int i = 0; i < nd; ++i) slot[i] = term[i] ? nt++ : nl++;
     std::vector<Board> tboards(nt);
     const bool light = !rb.enforce_superko();
-    pool_.run(nd, [&](int i) {
-      Board& b = term[i] ? tboards[slot[i]] : wave->leaves[slot[i]].board;
-      b = rb;
-      b.set_light(light);
+    const int rptm = rb.current_player();
+    auto leaf_job = [&](int i) {
       const std::vector<int32_t>& path = paths[i];
-      for (size_t d = 1; d < path.size(); ++d) b.play_unchecked((*nodes_)[path[d]].move);
+      if (build || term[i]) {
+        Board& b = term[i] ? tboards[slot[i]] : wave->leaves[slot[i]].board;
+        b = rb;
+        b.set_light(light);
+        for (size_t d = 1; d < path.size(); ++d) b.play_unchecked((*nodes_)[path[d]].move);
+      }
       if (!term[i]) {
         Leaf& L = wave->leaves[slot[i]];
+        // every move, a pass included, hands the turn over
+        L.ptm = (int8_t)((path.size() - 1) & 1 ? -rptm : rptm);
         L.path.swap(paths[i]);
         L.z = 0.f;
       }
-    });
+    };
+    if (build || nt > 0) {
+      pool_.run(nd, leaf_job);
+    } else {
+      for (int i = 0; i < nd; ++i) leaf_job(i);  // path swaps only: no pool wake-up
+    }
     for (int i = 0; i < nd; ++i) {
       if (!term[i]) continue;
       const Board& b = tboards[slot[i]];
@@ -622,8 +639,10 @@ class Search {
   }
   int num_leaves(int id) { return (int)wave(id).leaves.size(); }
   std::vector<const Board*> leaf_boards(int id) {
+    Wave& wv = wave(id);
+    if (!wv.built) throw std::invalid_argument("leaf_boards of a shipped wave (no leaf boards)");
     std::vector<const Board*> v;
-    for (auto& L : wave(id).leaves) v.push_back(&L.board);
+    for (auto& L : wv.leaves) v.push_back(&L.board);
     return v;
   }
 
@@ -633,8 +652,70 @@ class Search {
   // host-read ladder planes / superko-illegal masks.
   void pack_inputs(int id, const PackOut& o) {
     Wave& wv = wave(id);
+    if (!wv.built) throw std::invalid_argument("pack_inputs of a shipped wave (no leaf boards)");
     pool_.run((int)wv.leaves.size(), [&](int i) { pack_board(wv.leaves[i].board, i, o); });
   }
+
+  // ------------------------------------------------------------------ shipped waves
+  // The multi-GPU search (csrc/mcts/master.hpp) ships a leaf as its move path from the root:
+  // record [depth, move_1 .. move_depth] (int16, PASS = -1) of `stride` entries. The evaluating
+  // rank holds the same root board and replays the path (load_paths), so the master builds no
+  // leaf boards and a record is a few dozen bytes instead of a board.
+  // Writes leaves [lo, hi) of wave `id`; returns the deepest path written.
+  int write_paths(int id, int lo, int hi, int16_t* out, int stride) {
+    Wave& wv = wave(id);
+    int deepest = 0;
+    for (int i = lo; i < hi; ++i) {
+      const std::vector<int32_t>& path = wv.leaves[i].path;
+      const int d = (int)path.size() - 1;
+      if (d + 1 > stride) throw std::runtime_error("leaf path longer than the record stride");
+      int16_t* r = out + (size_t)(i - lo) * stride;
+      r[0] = (int16_t)d;
+      for (int k = 1; k <= d; ++k) r[k] = (int16_t)(*nodes_)[path[k]].move;
+      deepest = std::max(deepest, d);
+    }
+    return deepest;
+  }
+
+  // A wave of n leaves rebuilt from shipped path records (an evaluating rank's search object:
+  // its tree is never used). Boards are the root board + the path's moves, with the root's
+  // history (superko) when the root enforces it — exactly the boards select() builds.
+  int load_paths(const int16_t* recs, int n, int stride) {
+    std::unique_ptr<Wave> wave = take_wave();
+    wave->leaves.resize(n);
+    wave->built = true;
+    const Board& rb = root_board_;
+    const bool light = !rb.enforce_superko();
+    pool_.run(n, [&](int i) {
+      const int16_t* r = recs + (size_t)i * stride;
+      const int d = r[0];
+      Leaf& L = wave->leaves[i];
+      L.board = rb;
+      L.board.set_light(light);
+      for (int k = 1; k <= d && k < stride; ++k) L.board.play_unchecked(r[k]);
+      L.path.clear();
+      L.z = 0.f;
+      L.ptm = (int8_t)L.board.current_player();
+    });
+    std::lock_guard<std::mutex> g(wmu_);
+    const int id = next_wave_++;
+    waves_[id] = std::move(wave);
+    return id;
+  }
+
+  // Mean CPU rollout result per leaf from BLACK's point of view (joins start_rollouts()).
+  void rollout_black_z(int id, float* out) {
+    Wave& wv = wave(id);
+    if (wv.rolling) {
+      wv.worker.join();
+      wv.rolling = false;
+    }
+    for (size_t i = 0; i < wv.leaves.size(); ++i)
+      out[i] = wv.leaves[i].ptm == BLACK ? wv.leaves[i].z : -wv.leaves[i].z;
+  }
+
+  // Forget a wave without backing anything up (load_paths() waves once evaluated).
+  void drop_wave(int id) { finish(id); }
 
   // ------------------------------------------------------------------ value backup
   // priors: [n][stride] network move probabilities (nullptr => uniform); values: [n] (nullptr
@@ -648,6 +729,8 @@ class Search {
     const auto t0 = clk::now();
     Wave& wv = wave(id);
     if (wv.value_done) throw std::runtime_error("value backup twice");
+    if (!wv.built && !sensible)
+      throw std::invalid_argument("a shipped wave (no leaf boards) needs the sensible masks");
     const int n = (int)wv.leaves.size();
     const int P = root_board_.npoints();
     const bool par = n >= parallel_select_min && pool_.size() > 1;
@@ -743,7 +826,7 @@ class Search {
     auto body = [&](int i) {
       Leaf& L = wv.leaves[i];
       float z = L.z;
-      if (black_z) z = L.board.current_player() == BLACK ? black_z[i] : -black_z[i];
+      if (black_z) z = L.ptm == BLACK ? black_z[i] : -black_z[i];
       backup_rollout_path(L.path, z, true);
     };
     if (n >= parallel_select_min && pool_.size() > 1) {
@@ -759,6 +842,7 @@ class Search {
   void start_rollouts(int id) {
     Wave& wv = wave(id);
     if (wv.rolling) return;
+    if (!wv.built) throw std::invalid_argument("rollouts of a shipped wave (no leaf boards)");
     wv.rolling = true;
     const uint64_t base = seed * 0x100000001B3ull + (uint64_t)id * 0x9E3779B9ull;
     Wave* w = &wv;

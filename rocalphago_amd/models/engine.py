@@ -123,6 +123,11 @@ class _PackedConvs(object):
         if any(self._wino):
             ops.wino_pack(self._wpack_table, sum(self._wino), self._wpack_tiles)
         self._packed_version = version
+        # once any batch has run a Winograd layer on the direct kernel, its direct layout stays
+        # fresh on every weight change: a captured graph replayed after sync_weights() never
+        # re-enters wino_plan() (the Python forward that would repack it lazily)
+        if self._direct_version is not None:
+            self._direct_layouts()
 
     def _dgrad_wino_layouts(self):
         """Winograd dgrad weights of the Winograd layers when the dgrad normally runs the direct
@@ -682,14 +687,21 @@ class PolicyHeadEngine(object):
                       dpass=self.dpass[:B] if mode else None)
         # running metrics: summed by the backward's reduce launch from the per-board loss / hit
         # (acc in the forward kernel meant two contended device atomics per board)
-        self._macc = acc if mode else None
+        # (set only once the launch succeeded: a failed forward leaves nothing pending)
+        self._macc = None
         ops.policy_head_fwd(h, w, b0, pbias, self.probs[:B], self.K, labels=labels,
                             sweight=sweight, loss=self.loss[:B] if mode else None,
                             dz=self.dz[:B] if mode else None, hit=self.hit[:B] if mode else None,
                             mode=mode, gscale=gscale, acc=None if mode else acc,
                             dzsum=self.dzsum[:B] if (mode and not pk) else None, **pk)
+        self._macc = acc if mode else None
         self._dzsum = bool(mode and not pk)
         return self.probs[:B]
+
+    def reset_metrics(self):
+        """Drop a training forward's pending metrics (a caller that recovers from an error
+        raised between forward() and backward())."""
+        self._macc = None
 
     def pass_grads(self, B, dW, db):
         """PassLogit weight gradients after a training forward: dW = dpass^T z, db = sum dpass

@@ -182,12 +182,16 @@ class PolicyPlan(_TrunkPlan):
         pb = self.net.params_of(self.bias_name)[0]
         self.head.forward(B, w, b0, pb, labels=labels, sweight=sw, mode=mode, gscale=gscale,
                           pass_params=self._pass_params(), acc=metrics)
-        if self.pass_name:
-            dW, db = self.net.grads_of(self.pass_name)
-            self.head.pass_grads(B, dW, db)
-        dw, db0 = self.head_grads()
-        dpb = self.net.grads_of(self.bias_name)[0]
-        self.head.backward(B, w, self.head.dz[:B], dw, db0, dpb)
+        try:
+            if self.pass_name:
+                dW, db = self.net.grads_of(self.pass_name)
+                self.head.pass_grads(B, dW, db)
+            dw, db0 = self.head_grads()
+            dpb = self.net.grads_of(self.bias_name)[0]
+            self.head.backward(B, w, self.head.dz[:B], dw, db0, dpb)
+        except BaseException:
+            self.head.reset_metrics()  # a retrying caller's next forward must not raise
+            raise
         dWs, dbs = self._grads()
         self.trunk.backward(B, dWs, dbs, on_layer_done=on_layer_grads)
 

@@ -27,6 +27,9 @@ import socket
 import numpy as np
 
 FEATS = ["board", "ones", "turns_since", "liberties", "capture_size", "sensibleness"]
+NET_ARCH = {"filters": 16, "layers": 3, "features": FEATS}
+# bump when a change to the search / rollouts changes the single trees (cached truth + ladder)
+CACHE_VERSION = 2
 
 
 def _port():
@@ -55,7 +58,7 @@ def positions(n, size=9, seed=0, min_moves=4, max_moves=30):
     return out
 
 
-def nets(size, seed=3, filters=16, layers=3):
+def nets(size, seed=3, filters=NET_ARCH["filters"], layers=NET_ARCH["layers"]):
     import torch
     from ..models.policy import CNNPolicy
     from ..models.value import CNNValue
@@ -126,10 +129,14 @@ def _rank_worker(rank, world, port, outdir, cfg):
         kw = _search_kw(cfg["batch"], cfg.get("lmbda", 0.0))
         if master:
             kw["rollout_delay"] = cfg.get("rollout_delay", 0)
+            kw["depth"] = cfg.get("depth", 1)
+            kw["force_master"] = True
         mc = cls(pol, val, dp=dp, n_playout=cfg["total"], **kw)
         mc.keyed_rollouts = True
-        if hasattr(mc, "leaf_eval"):
-            mc.leaf_eval.keyed = True
+        if master:
+            # the GPU pipeline's leaves in flight, deterministically (DistributedMCTS doc)
+            mc.emulate_latency = True
+            mc.idle_us = 20000
         P = st.size * st.size
         if master and rank > 0:
             mc.serve()  # evaluates rank 0's waves until it stops
@@ -201,7 +208,7 @@ def equivalent_budget(ladder, k):
 def study(worlds=(2, 4, 8), per_rank=128, batch=16, n_positions=50, size=9, truth_mult=4,
           search_cls="SharedRootMCTS", outdir="/tmp/rag_eff", pos_seed=0, net_seed=3,
           ladder_top=None, split_wave=False, lmbda=0.0, rollout_delay=0, shipped=False,
-          capped=False):
+          capped=False, depth=1, wave=None):
     """The whole comparison; returns a JSON-able dict. ``split_wave``: the N-rank search's
     per-rank wave is batch / N (the job keeps the one-GPU search's leaves in flight per round
     instead of N times as many). ``shipped``: the bench's geometry instead (shipped_waves: the
@@ -215,8 +222,15 @@ def study(worlds=(2, 4, 8), per_rank=128, batch=16, n_positions=50, size=9, trut
     top = ladder_top or per_rank * max(worlds)
     # the single trees (truth and ladder) depend only on these: cached across studies that vary
     # the N-rank search alone (e.g. its rollout delay)
-    ck = os.path.join(outdir, "single_%d_%d_%d_%d_%d_%g_%d_%d.npz" % (
-        n_positions, size, pos_seed, net_seed, batch, lmbda, top * truth_mult, per_rank))
+    # (keyed by every setting of those trees — search parameters, networks, positions — and a
+    # version tag bumped whenever the search or rollout code changes what a tree finds)
+    import hashlib
+    import json
+    key = json.dumps({"v": CACHE_VERSION, "search": _search_kw(batch, lmbda), "nets": NET_ARCH,
+                      "n": n_positions, "size": size, "pos_seed": pos_seed,
+                      "net_seed": net_seed, "truth": top * truth_mult, "per_rank": per_rank},
+                     sort_keys=True)
+    ck = os.path.join(outdir, "single_%s.npz" % hashlib.sha1(key.encode()).hexdigest()[:16])
     cache = dict(np.load(ck)) if os.path.exists(ck) else {}
 
     def single(budget, seed=1):
@@ -240,11 +254,13 @@ def study(worlds=(2, 4, 8), per_rank=128, batch=16, n_positions=50, size=9, trut
         b *= 2
     cfg = {"size": size, "net_seed": net_seed, "pos_seed": pos_seed,
            "n_positions": n_positions, "batch": batch, "search_cls": search_cls,
-           "lmbda": lmbda, "rollout_delay": rollout_delay}
+           "lmbda": lmbda, "rollout_delay": rollout_delay, "depth": depth}
     for w in worlds:
         d = os.path.join(outdir, "%s_w%d" % (search_cls, w))
         os.makedirs(d, exist_ok=True)
-        if shipped:
+        if wave is not None:  # an explicit per-rank wave (the effective-throughput sweep)
+            wcfg = dict(cfg, batch=int(wave))
+        elif shipped:
             wcfg = dict(cfg, batch=shipped_waves(per_rank, w, cap=capped)[1])
         else:
             wcfg = dict(cfg, batch=max(1, batch // w)) if split_wave else cfg
@@ -253,7 +269,7 @@ def study(worlds=(2, 4, 8), per_rank=128, batch=16, n_positions=50, size=9, trut
         teq = equivalent_budget(ladder, k)
         rows["%s_%d" % (search_cls, w)] = {
             "ranks": w, "budget": per_rank * w, "kl": round(k, 4),
-            "wave_per_rank": wcfg["batch"],
+            "wave_per_rank": wcfg["batch"], "depth": depth, "rollout_delay": rollout_delay,
             "agree": round(agreement(truth, vis), 3), "duplication": round(float(dup.mean()), 3),
             "equivalent_single_tree_budget": round(teq, 1),
             "efficiency": round(teq / (per_rank * w), 3)}

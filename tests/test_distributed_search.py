@@ -1,6 +1,7 @@
-"""Multi-GPU single-tree search plumbing (search/distributed.py): leaves shipped as arrays are
-rebuilt into boards that give exactly the original planes; a 2-rank gloo run of one search
-splits the leaf evaluations over the ranks and plays the same move on every rank."""
+"""Multi-GPU single-tree search plumbing (search/distributed.py, csrc/mcts/master.hpp): leaves
+shipped as move paths are replayed into boards that give exactly the tree's planes; a 2-rank run
+of one search (shared-memory channel, gloo only for the set-up) splits the leaf evaluations over
+the ranks and plays the same move on every rank."""
 import numpy as np
 
 from rocalphago_amd._native import engine
@@ -126,19 +127,17 @@ def _played(size, n, seed, superko):
 @__import__("pytest").mark.parametrize("superko", [False, True])
 def test_distributed_leaf_path_gpu(cuda, superko):
     """The multi-GPU search's leaf path on one GPU at the bench geometry (19x19, 192 filters,
-    12 layers): a wave of tree leaves packed as records (LeafCodec), rebuilt on the receiving
-    side, gives bit-exactly the feature planes of the single-GPU path on the tree's own boards
-    (with superko: from the master's illegal mask and ladder planes), and the shipped wave's
-    priors / values match the direct evaluation. Then a full search whose round loop runs
-    (force_master) under a one-rank RCCL group plays legal moves with every rollout backed up."""
-    import os
-    import socket
+    12 layers): a wave of tree leaves shipped as move paths (Search.write_paths) and replayed on
+    the evaluating side's copy of the root (Search.load_paths) gives bit-exactly the feature
+    planes of the tree's own leaf boards (superko history included), and its packed-wave GPU
+    pass gives the direct evaluation's priors / values / sensible masks. Then a full search
+    through the shared-memory channel (native master loop + serving thread, force_master at one
+    rank) plays legal moves with every rollout backed up."""
     import torch
-    import torch.distributed as dist
     from rocalphago_amd.models.policy import CNNPolicy
     from rocalphago_amd.models.value import CNNValue
-    from rocalphago_amd.parallel.dp import DPContext
-    from rocalphago_amd.search.distributed import DistributedMCTS, LeafCodec
+    from rocalphago_amd.search.apv import _Slots
+    from rocalphago_amd.search.distributed import DistributedMCTS
     dev = cuda
     pol = CNNPolicy(DEFAULT_FEATURES, board=19, filters_per_layer=192, layers=12, device=dev,
                     seed=1)
@@ -147,6 +146,7 @@ def test_distributed_leaf_path_gpu(cuda, superko):
     st = _played(19, 40, 5, superko)
     mc = DistributedMCTS(pol, val, dp=None, lmbda=0.5, n_playout=1024, batch=128, nthreads=8,
                          force_master=True)
+    assert mc.chan is not None and mc.gpu is not None
     # ---- one wave, shipped vs direct
     s = mc._sync_root(st)
     w0, n0 = s.select(1)  # the root itself: expand it first (then a wave of its children)
@@ -155,51 +155,38 @@ def test_distributed_leaf_path_gpu(cuda, superko):
     s.backup_value(w0, pri0, v0, sens0.astype(np.uint8) if sens0 is not None else None)
     wid, n = s.select(64)
     assert n > 8
-    codec = LeafCodec(19, superko)
-    rec, sk = codec.pack(s, wid, 8)
-    assert sk == superko
     tree = s.leaf_boards(wid)
-    colors, ages, meta8, illegal, lad = codec.unpack(rec)
-    rebuilt = mc.leaf_eval._boards(colors, ages, meta8, 19, st.komi)
+    recs = s.write_paths(wid, 128)
+    ws = mc._worker_search(st.native)
+    wid2 = ws.load_paths(recs)
+    rebuilt = ws.leaf_boards(wid2)
+    assert [b.hash for b in rebuilt] == [b.hash for b in tree]
     ev = mc.evaluator
     ev._plans()
-    xp, xv, _ = mc.leaf_eval.planes(rebuilt, colors, ages, meta8, illegal, lad, superko)
     if ev.shared:  # one extraction feeds both networks (policy planes = the first npol)
-        xd = ev.gpu["p"](tree)
-        assert torch.equal(xv, xd) and torch.equal(xp, xd[:, :ev.npol])
+        assert torch.equal(ev.gpu["p"](rebuilt), ev.gpu["p"](tree))
     else:
-        assert torch.equal(xp, ev.gpu["p"](tree)) and torch.equal(xv, ev.gpu["v"](tree))
-    if superko:
-        assert lad is not None and illegal is not None
-    handle, pend = mc.leaf_eval.submit(codec, rec, superko, st.komi, seed=3)
-    pr, v, sens = handle.result()
+        assert torch.equal(ev.gpu["p"](rebuilt), ev.gpu["p"](tree))
+        assert torch.equal(ev.gpu["v"](rebuilt), ev.gpu["v"](tree))
+    assert ev.wave_capable(19)
+    h = ev.submit_wave(ws, wid2, n, _Slots(dev, 2), 128)
+    pr, v, sens = (np.array(x) for x in h.result())
     pr_d, v_d, sens_d = ev(tree)[:3]
     assert np.abs(pr - pr_d).max() <= 2e-2 * max(1e-6, float(np.abs(pr_d).max()))
     assert np.abs(v - v_d).max() <= 2e-2
     assert np.array_equal(np.asarray(sens) > 0.5, np.asarray(sens_d) > 0.5)
-    assert pend is not None and len(pend.result()) == n
-    # ---- the round loop under a one-rank RCCL group
-    sock = socket.socket()
-    sock.bind(("127.0.0.1", 0))
-    port = sock.getsockname()[1]
-    sock.close()
-    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0,
-                            world_size=1)
-    try:
-        dp = DPContext(device=dev, adopt=True)
-        mc = DistributedMCTS(pol, val, dp=dp, lmbda=0.5, n_playout=1024, batch=128,
-                             nthreads=8, force_master=True)
-        assert os.environ.get("RAG_FORCE_PG") == "1" or mc.force_master
-        for _ in range(2):
-            mv = mc.get_move(st)
-            assert mv is None or st.is_legal(mv)
-            st.do_move(mv)
-            mc.update_with_move(mv)
-        assert mc._round > 0 and mc.stats.get("rounds", 0) > 0  # the master round loop ran
-        assert mc.stats["sims"] >= 2 * 1024 - 2
-        assert mc._search.rollouts == mc._search.sims
-    finally:
-        dist.destroy_process_group()
+    ws.drop_wave(wid2)
+    # ---- full searches through the channel
+    for _ in range(2):
+        mv = mc.get_move(st)
+        assert mv is None or st.is_legal(mv)
+        st.do_move(mv)
+        mc.update_with_move(mv)
+    m = mc.master_stats
+    assert m["waves"] > 0 and m["sims"] >= 1024 - 2
+    assert mc.stats["sims"] >= 2 * 1024 - 2
+    assert mc._search.rollouts == mc._search.sims
+    mc.stop()
 
 
 def test_root_deltas_and_external_stats_steer_root_selection():
@@ -317,3 +304,72 @@ def test_search_budget_efficiency_shipped_geometry_two_ranks(tmp_path):
     row = r["rows"]["DistributedMCTS_2"]
     assert row["duplication"] == 1.0
     assert row["efficiency"] >= 0.85, r["rows"]
+
+
+@__import__("pytest").mark.parametrize("superko", [False, True])
+def test_path_records_replay_leaf_boards(superko):
+    """A leaf shipped as its move path from the root (Search.write_paths) and replayed on a
+    second search object of the same root (Search.load_paths) is the tree's leaf board: same
+    hash, player, ko and bit-identical feature planes (superko history included). A wave
+    selected without boards (the master's select(B, False)) ships the same paths."""
+    import pytest
+    st = _played(9, 24, 3, superko)
+    P = 81
+    s = rg.Search(st.native, 2)
+    s.lmbda = 0.0
+    pri = np.full((64, P), 1.0 / P, np.float32)
+    for _ in range(6):  # grow the tree a few plies deep
+        w, n = s.select(16)
+        s.backup_value(w, pri[:n], np.zeros(n, np.float32))
+    w, n = s.select(16)
+    assert n > 4
+    recs = s.write_paths(w, 64)
+    assert recs[:, 0].max() >= 2  # paths of several moves
+    ws = rg.Search(st.native, 2)
+    w2 = ws.load_paths(recs)
+    tree, rebuilt = s.leaf_boards(w), ws.leaf_boards(w2)
+    assert [b.hash for b in rebuilt] == [b.hash for b in tree]
+    assert [b.current_player for b in rebuilt] == [b.current_player for b in tree]
+    assert [b.ko for b in rebuilt] == [b.ko for b in tree]
+    fids = Preprocess(list(DEFAULT_FEATURES) + ["color"]).feature_ids
+    assert np.array_equal(rg.batch_features(rebuilt, fids, 2), rg.batch_features(tree, fids, 2))
+    s.backup_value(w, pri[:n], np.zeros(n, np.float32))
+    ws.drop_wave(w2)
+    # path-only waves: no boards, same records, and value backups need the sensible masks
+    w3, n3 = s.select(8, False)
+    assert n3 > 0
+    with pytest.raises(Exception):
+        s.leaf_boards(w3)
+    with pytest.raises(Exception):
+        s.backup_value(w3, pri[:n3], np.zeros(n3, np.float32))
+    w4 = ws.load_paths(s.write_paths(w3, 64))
+    sens = rg.batch_features(ws.leaf_boards(w4), [Preprocess(["sensibleness"]).feature_ids[0]],
+                             2).reshape(n3, -1)
+    s.backup_value(w3, pri[:n3], np.zeros(n3, np.float32), sens)
+
+
+def test_channel_master_loop_one_process():
+    """The native master loop and a serving thread over the shared-memory channel in one
+    process (force_master): legal moves, every simulation backed up once, the rollouts too, and
+    the slot ring continues across searches."""
+    import torch
+    torch.set_num_threads(1)
+    from rocalphago_amd.models.policy import CNNPolicy
+    from rocalphago_amd.models.value import CNNValue
+    from rocalphago_amd.search.distributed import DistributedMCTS
+    feats = ["board", "ones", "turns_since", "liberties", "sensibleness"]
+    pol = CNNPolicy(feats, board=7, filters_per_layer=8, layers=2, device="cpu", seed=3)
+    val = CNNValue(feats + ["color"], board=7, filters_per_layer=8, layers=2, device="cpu",
+                   seed=4)
+    mc = DistributedMCTS(pol, val, dp=None, lmbda=0.5, n_playout=96, batch=12,
+                         rollout_limit=80, nthreads=1, rollout_delay=1, force_master=True)
+    st = go.GameState(size=7)
+    for _ in range(4):
+        mv = mc.get_move(st)
+        assert mv is None or st.is_legal(mv)
+        st.do_move(mv)
+        mc.update_with_move(mv)
+        assert mc.master_stats["sims"] >= 96 - 2
+    assert mc._search.rollouts == mc._search.sims
+    assert mc.leaf_counts()[0] == mc.stats["sims"]
+    mc.stop()
