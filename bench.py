@@ -167,7 +167,7 @@ def main():
         # heartbeat 2k: step k started; 2k+1: its gradients reached the all-reduce
         k = counter[0]
         counter[0] += 1
-        inject_stall(dp.rank, k)  # RAG_STALL_RANK / RAG_STALL_STEP rehearsal of a hung rank
+        inject_stall(dp.rank, k)  # RAG_STALL=rank:step rehearsal of a hung rank
         if wd is not None:
             wd.beat(2 * k)
         if order["pos"] + args.batch > N:

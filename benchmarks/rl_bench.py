@@ -120,7 +120,8 @@ def main():
     ap.add_argument("--game-batch", type=int, default=None)
     ap.add_argument("--selfplay", default="native", choices=["native", "python"])
     args = ap.parse_args()
-    os.environ["RAG_NATIVE_SELFPLAY"] = "1" if args.selfplay == "native" else "0"
+    from rocalphago_amd.training import reinforcement
+    reinforcement.NATIVE_SELFPLAY = args.selfplay == "native"
     r = bench_ref7(args) if args.config == "ref7" else bench_19(args)
     sp = r.pop("self_play")
     r["selfplay"] = args.selfplay

@@ -66,6 +66,8 @@ void register_search(py::module_& m) {
            "CPU rollout results of a wave (start_rollouts) from BLACK's point of view")
       .def("drop_wave", &Search::drop_wave, py::call_guard<py::gil_scoped_release>())
       .def_readwrite("parallel_select_min", &Search::parallel_select_min)
+      .def_readwrite("batched_select", &Search::batched_select,
+                     "waves of >= parallel_select_min leaves deal their descents top-down")
       .def_readwrite("pass_prior", &Search::pass_prior)
       .def("leaf_nodes",
            [](Search& s, int id) {
@@ -188,6 +190,7 @@ void register_search(py::module_& m) {
            "Other ranks' cumulative root-child statistics [4, P+1], mixed into root selection")
       .def("clear_root_external", &Search::clear_root_external)
       .def_property_readonly("timers", &Search::timers)
+
       .def_property_readonly("root_visits", &Search::root_visits)
       .def_property_readonly("root_board", &Search::root_board,
                              py::return_value_policy::reference_internal);

@@ -281,6 +281,8 @@ class Search {
   // waves of at least this many leaves descend (and back up) on the pool; smaller ones run
   // serially and deterministically
   int parallel_select_min = 64;
+  // such waves deal their descents top-down (descend_batched) instead of walking them one by one
+  bool batched_select = true;
   static constexpr int kSorted = 32;
 
   explicit Search(const Board& root, int nthreads = 8)
@@ -470,7 +472,9 @@ class Search {
     std::vector<uint8_t> term;
     paths.reserve(B);
     term.reserve(B);
-    if (B >= parallel_select_min && pool_.size() > 1) {
+    if (B >= parallel_select_min && batched_select && !has_ext_) {
+      descend_batched(B, paths, term);
+    } else if (B >= parallel_select_min && pool_.size() > 1) {
       descend_parallel(B, paths, term);
     } else {
       int attempts = 0, claimed = 0;
@@ -586,6 +590,180 @@ class Search {
       }
     });
     collisions_ = coll.load();
+  }
+
+  // Batched wave descent: the B descents of a wave dealt top-down instead of walked one by one
+  // (the wave-level form of virtual-loss selection). A node that k descents reach scores its
+  // children ONCE and deals the k descents one at a time to the PUCT argmax, adding each dealt
+  // descent's virtual loss to that child's score before the next deal (a max-heap: one child
+  // changes per deal); the node's sqrt(N) counts all k of the wave's visits. A fresh leaf takes
+  // one descent (its claim), a leaf awaiting its evaluation none, a terminal node any number
+  // (each is scored). Every reached node is scored once per wave and takes its virtual loss in
+  // one atomic add — instead of once per descent through it: B x depth scans of the root's ~360
+  // edges, and every thread's atomics on the root's cache line, were the host ceiling of a
+  // multi-GPU search (profiles/mcts_master_null_r6.txt) — and no descent collides with a leaf
+  // another one claimed. The children of a node that >= kSplit descents reached form the next
+  // level of tasks (dealt in parallel), those of smaller ones are walked depth-first by the
+  // thread that dealt them.
+  static constexpr int kSplit = 16;
+  struct DTask {
+    int node, k, depth, ptm, l1, l2, nm;
+    bool end;
+    std::vector<int32_t> path;  // root .. node
+  };
+
+  void descend_batched(int B, std::vector<std::vector<int32_t>>& paths,
+                       std::vector<uint8_t>& term) {
+    std::atomic<int> coll{0};
+    const Board& rb = root_board_;
+    // level-synchronous: the tasks of one level are handed out by an atomic counter (no queue
+    // lock per task: that lock's waits were 2/3 of a 16-thread wave's descent time); a task
+    // walks its subtree depth-first unless its node took >= kSplit descents, whose children
+    // form the next level
+    struct Scratch {
+      std::vector<std::vector<int32_t>> out;
+      std::vector<uint8_t> oterm;
+      std::vector<DTask> local, next;
+      std::vector<float> sc;
+      std::vector<int> dealt;
+      std::vector<int8_t> cap;
+      std::vector<std::pair<float, int>> heap;
+    };
+    const int nw = std::max(1, pool_.size());
+    std::vector<Scratch> scr(nw);
+    std::vector<DTask> frontier;
+    frontier.push_back(DTask{root_, B, 0, rb.current_player(), rb.last1(), rb.last2(),
+                             rb.nmoves(), rb.end_of_game(), {root_}});
+    while (!frontier.empty()) {
+      std::atomic<int> next{0};
+      const int nf = (int)frontier.size();
+      auto slot = [&](int w) {
+        Scratch& S = scr[w];
+        for (int i = next.fetch_add(1); i < nf; i = next.fetch_add(1)) {
+          S.local.push_back(std::move(frontier[i]));
+          while (!S.local.empty()) {
+            DTask u = std::move(S.local.back());
+            S.local.pop_back();
+            deal(u, S.local, S.next, S.out, S.oterm, coll, S.sc, S.dealt, S.cap, S.heap);
+          }
+        }
+      };
+      if (nf < 4 || nw == 1)
+        slot(0);  // the root level: no pool wake-up
+      else
+        pool_.run(nw, slot);
+      frontier.clear();
+      for (Scratch& S : scr) {
+        for (DTask& t : S.next) frontier.push_back(std::move(t));
+        S.next.clear();
+      }
+    }
+    for (Scratch& S : scr)
+      for (size_t k = 0; k < S.out.size(); ++k) {
+        paths.push_back(std::move(S.out[k]));
+        term.push_back(S.oterm[k]);
+      }
+    collisions_ = coll.load();
+  }
+
+  void deal(DTask& u, std::vector<DTask>& local, std::vector<DTask>& shared,
+            std::vector<std::vector<int32_t>>& out, std::vector<uint8_t>& oterm,
+            std::atomic<int>& coll, std::vector<float>& sc, std::vector<int>& dealt,
+            std::vector<int8_t>& cap, std::vector<std::pair<float, int>>& heap) {
+    NodeArena& N = *nodes_;
+    Node& nd = N[u.node];
+    __atomic_fetch_add(&nd.vl, u.k, __ATOMIC_RELAXED);
+    const uint8_t st = state_of(nd);
+    const bool terminal = u.end || u.depth >= max_depth || (st == N_EXPANDED && nd.nedge == 0);
+    auto give_back = [&](int extra) {
+      for (int id : u.path) __atomic_fetch_sub(&N[id].vl, extra, __ATOMIC_RELAXED);
+      coll.fetch_add(extra, std::memory_order_relaxed);
+    };
+    if (terminal) {  // every descent is scored (and backed up) on its own
+      for (int i = 0; i < u.k; ++i) {
+        out.push_back(u.path);
+        oterm.push_back(1);
+      }
+      return;
+    }
+    if (st != N_EXPANDED) {  // a leaf: one descent claims it, the others collide
+      uint8_t expect = N_NEW;
+      const bool claimed = __atomic_compare_exchange_n(&nd.state, &expect, (uint8_t)N_PENDING,
+                                                       false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE);
+      const int extra = claimed ? u.k - 1 : u.k;
+      if (extra > 0) give_back(extra);
+      if (claimed) {
+        out.push_back(std::move(u.path));
+        oterm.push_back(0);
+      }
+      return;
+    }
+    const int ne = nd.nedge;
+    const Edge* E = &(*edges_)[nd.edges];
+    // candidates: within the sorted-prior prefix the unvisited edges score in prior order and
+    // take one descent each, so k descents reach at most edges [0, hwm + k); else all edges
+    const int h = ld(nd.hwm);
+    const int lim = h + u.k <= std::min(ne, (int)kSorted) ? h + u.k : ne;
+    const float np = (float)(ld(nd.n) + ld(nd.vl) * n_vl);  // the wave's k visits included
+    const float sq = std::sqrt(std::max(np, 1.f));
+    const int cptm = -u.ptm, cnm = u.nm + 1;
+    sc.resize(lim);
+    dealt.assign(lim, 0);
+    cap.resize(lim);
+    heap.clear();
+    auto edge_score = [&](int e) {
+      const int32_t c = __atomic_load_n(&E[e].child, __ATOMIC_ACQUIRE);
+      if (c < 0) return c_puct * E[e].prior * sq;
+      const Node& cn = N[c];
+      return score((float)ld(cn.n), ld(cn.w), (float)ld(cn.nr), ld(cn.wr), ld(cn.vl) + dealt[e],
+                   E[e].prior, sq);
+    };
+    for (int e = 0; e < lim; ++e) {
+      const int m = E[e].move;
+      const bool cend = cnm > 1 && m == PASS && u.l1 == PASS && cptm == WHITE;
+      const int32_t c = __atomic_load_n(&E[e].child, __ATOMIC_ACQUIRE);
+      int8_t cp = 1;  // a fresh leaf: one descent
+      if (cend || u.depth + 1 >= max_depth) {
+        cp = -1;  // terminal: any number
+      } else if (c >= 0) {
+        const uint8_t cs = state_of(N[c]);
+        cp = cs == N_PENDING ? 0 : (cs == N_EXPANDED ? -1 : 1);
+      }
+      cap[e] = cp;
+      if (cp != 0) heap.emplace_back(edge_score(e), -e);
+    }
+    // max-heap on (score, -edge): ties go to the lower edge, as select_edge's first maximum
+    auto less = [](const std::pair<float, int>& a, const std::pair<float, int>& b) {
+      return a.first < b.first || (a.first == b.first && a.second < b.second);
+    };
+    std::make_heap(heap.begin(), heap.end(), less);
+    int left = u.k;
+    while (left > 0 && !heap.empty()) {
+      std::pop_heap(heap.begin(), heap.end(), less);
+      const int e = -heap.back().second;
+      heap.pop_back();
+      ++dealt[e];
+      --left;
+      if (cap[e] < 0) {
+        heap.emplace_back(edge_score(e), -e);
+        std::push_heap(heap.begin(), heap.end(), less);
+      }
+    }
+    if (left > 0) give_back(left);  // every child is awaiting its evaluation
+    for (int e = 0; e < lim; ++e) {
+      if (!dealt[e]) continue;
+      const int child = child_of(u.node, e);
+      const int m = E[e].move;
+      const bool cend = cnm > 1 && m == PASS && u.l1 == PASS && cptm == WHITE;
+      DTask t{child, dealt[e], u.depth + 1, cptm, m, u.l1, cnm, cend, u.path};
+      t.path.push_back(child);
+      // the children of a node many descents reached go to the next level (the root's ~200
+      // small subtrees would otherwise all be walked by the thread that dealt them)
+      if (u.k >= kSplit)
+        shared.push_back(std::move(t));
+      else
+        local.push_back(std::move(t));
+    }
   }
 
   // One walk from the root with virtual loss (atomic adds as the walk passes each node, so
@@ -734,66 +912,54 @@ class Search {
     const int n = (int)wv.leaves.size();
     const int P = root_board_.npoints();
     const bool par = n >= parallel_select_min && pool_.size() > 1;
-    // pass 1 (parallel): children per leaf still to expand — the sensible-move mask's count, or
-    // natively generated moves; then one contiguous edge block for all of them (the leaves of
-    // one wave are distinct nodes: select() skips pending ones, so the blocks never overlap)
-    std::vector<int32_t> cnt(n, -1);
-    std::vector<std::vector<int>> moves(sensible ? 0 : n);
-    pool_.run(n, [&](int i) {
-      const Leaf& L = wv.leaves[i];
-      if (state_of((*nodes_)[L.path.back()]) == N_EXPANDED) return;
-      int c = 0;
-      if (sensible) {
-        const uint8_t* m = sensible + (size_t)i * P;
-        for (int p = 0; p < P; ++p) c += m[p] != 0;
-      } else {
-        std::vector<int> eyes;
-        L.board.legal_moves(moves[i], eyes);
-        c = (int)moves[i].size();
-      }
-      cnt[i] = c;
-    });
     const bool with_pass = pass_prior && priors != nullptr && stride > P;
-    std::vector<int64_t> first(n, -1);
-    size_t total = 0;
-    for (int i = 0; i < n; ++i) {
-      if (cnt[i] < 0) continue;
-      first[i] = (int64_t)total;
-      total += nchildren(cnt[i], with_pass);
-    }
-    if (!edges_->room(total))
+    // one pass per leaf (parallel): its children — the sensible-move mask's moves, or natively
+    // generated ones — get an edge block of their own from the arena's atomic bump pointer (the
+    // leaves of one wave are distinct nodes: select() skips pending ones); then the expansion is
+    // published. The path backups follow on this thread.
+    if (!edges_->room((size_t)n * (P + 1)))
       throw std::runtime_error("search tree full (edge arena); advance() or reset()");
-    const size_t base = edges_->alloc(total);
-    // pass 2: write the edges, publish the expansion, back the value up the path
     auto body = [&](int i) {
       Leaf& L = wv.leaves[i];
-      if (first[i] >= 0) {
-        const float* pri = priors ? priors + (size_t)i * stride : nullptr;
-        const size_t e0 = base + (size_t)first[i];
-        if (sensible) {
-          const uint8_t* m = sensible + (size_t)i * P;
-          int k = 0;
-          fill_edges(e0, cnt[i], with_pass, pri, P, [&]() {
-            while (!m[k]) ++k;
-            return k++;
-          });
-        } else {
-          size_t k = 0;
-          fill_edges(e0, cnt[i], with_pass, pri, P, [&]() { return moves[i][k++]; });
-        }
-        Node& nd = (*nodes_)[L.path.back()];
-        nd.edges = (int32_t)e0;
-        nd.nedge = (int16_t)nchildren(cnt[i], with_pass);
-        nd.hwm = 0;
-        __atomic_store_n(&nd.state, (uint8_t)N_EXPANDED, __ATOMIC_RELEASE);
+      Node& nd = (*nodes_)[L.path.back()];
+      if (state_of(nd) == N_EXPANDED) return;
+      const float* pri = priors ? priors + (size_t)i * stride : nullptr;
+      int nc;
+      size_t e0;
+      if (sensible) {
+        const uint8_t* m = sensible + (size_t)i * P;
+        int c = 0;
+        for (int p = 0; p < P; ++p) c += m[p] != 0;
+        nc = nchildren(c, with_pass);
+        e0 = edges_->alloc(nc);
+        int k = 0;
+        fill_edges(e0, c, with_pass, pri, P, [&]() {
+          while (!m[k]) ++k;
+          return k++;
+        });
+      } else {
+        std::vector<int> mv, eyes;
+        L.board.legal_moves(mv, eyes);
+        nc = nchildren((int)mv.size(), with_pass);
+        e0 = edges_->alloc(nc);
+        size_t k = 0;
+        fill_edges(e0, (int)mv.size(), with_pass, pri, P, [&]() { return mv[k++]; });
       }
-      backup_value_path(L.path, values ? values[i] : 0.f, lambda <= 0.f);
+      nd.edges = (int32_t)e0;
+      nd.nedge = (int16_t)nc;
+      nd.hwm = 0;
+      __atomic_store_n(&nd.state, (uint8_t)N_EXPANDED, __ATOMIC_RELEASE);
     };
     if (par) {
       pool_.run(n, body);
     } else {
       for (int i = 0; i < n; ++i) body(i);
     }
+    // the path backups on this thread: every leaf's path ends at the root, so on the pool they
+    // were all threads' compare-and-swap loops on the same few cache lines; here no other thread
+    // touches the statistics (descents run only inside select()), so plain loads and stores
+    for (int i = 0; i < n; ++i)
+      backup_path_serial(wv.leaves[i].path, values ? values[i] : 0.f, lambda <= 0.f, false);
     wv.value_done = true;
     sims_ += n;
     t_backup_ += std::chrono::duration<double>(clk::now() - t0).count();
@@ -823,16 +989,12 @@ class Search {
       wv.rolling = false;
     }
     const int n = (int)wv.leaves.size();
-    auto body = [&](int i) {
+    // on this thread (see backup_value)
+    for (int i = 0; i < n; ++i) {
       Leaf& L = wv.leaves[i];
       float z = L.z;
       if (black_z) z = L.ptm == BLACK ? black_z[i] : -black_z[i];
-      backup_rollout_path(L.path, z, true);
-    };
-    if (n >= parallel_select_min && pool_.size() > 1) {
-      pool_.run(n, body);
-    } else {
-      for (int i = 0; i < n; ++i) body(i);
+      backup_path_serial(L.path, z, true, true);
     }
     rollouts_ += (long)n;
     release(id);
@@ -1089,6 +1251,24 @@ class Search {
       mcts_detail::atomic_addf(&nd.w, ((D - d) & 1) ? v : -v);
     }
   }
+  // The same on the search's orchestrating thread while no descent runs: relaxed loads and
+  // stores instead of read-modify-writes (rollout = the rollout statistics).
+  void backup_path_serial(const std::vector<int32_t>& path, float v, bool drop_vl,
+                          bool rollout) {
+    const int D = (int)path.size() - 1;
+    for (int d = D; d >= 0; --d) {
+      Node& nd = (*nodes_)[path[d]];
+      int32_t* cnt = rollout ? &nd.nr : &nd.n;
+      float* sum = rollout ? &nd.wr : &nd.w;
+      __atomic_store_n(cnt, __atomic_load_n(cnt, __ATOMIC_RELAXED) + 1, __ATOMIC_RELAXED);
+      if (drop_vl)
+        __atomic_store_n(&nd.vl, __atomic_load_n(&nd.vl, __ATOMIC_RELAXED) - 1, __ATOMIC_RELAXED);
+      float f;
+      __atomic_load(sum, &f, __ATOMIC_RELAXED);
+      f += ((D - d) & 1) ? v : -v;
+      __atomic_store(sum, &f, __ATOMIC_RELAXED);
+    }
+  }
   void backup_rollout_path(const std::vector<int32_t>& path, float z, bool drop_vl) {
     const int D = (int)path.size() - 1;
     for (int d = D; d >= 0; --d) {
@@ -1209,6 +1389,7 @@ class Search {
   long sims_ = 0, rollouts_ = 0, terminal_ = 0;
   int collisions_ = 0;
   double t_descend_ = 0, t_build_ = 0, t_backup_ = 0;
+
   // external root statistics [4][P+1] (other ranks), this rank's last reported root totals
   std::vector<float> ext_, snap_;
   float ext_total_n_ = 0.f;

@@ -211,13 +211,13 @@ class GameConverter(object):
         return done, fused
 
     def sgfs_to_hdf5(self, sgf_files, hdf5_file, bd_size=19, ignore_errors=True, verbose=False,
-                     batch=32, nthreads=8):
+                     batch=32, nthreads=8, fused=True):
         tmp = os.path.join(os.path.dirname(hdf5_file), ".tmp." + os.path.basename(hdf5_file))
         sink = _Sink(tmp, self.feature_processor.feature_list, self.n_features, bd_size)
         if verbose:
             print("created HDF5 dataset in {}".format(tmp))
         sink.states.nthreads = max(1, nthreads)
-        fuse = os.environ.get("RAG_CONVERT_FUSED", "1") != "0"
+        fuse = bool(fused)
         t0, ngames = time.time(), 0
         files = iter(sgf_files)
         # the next batch converts on a helper thread (the native converter releases the GIL)

@@ -159,6 +159,10 @@ class _PackedConvs(object):
 
 
 class HipTrunk(_PackedConvs):
+    # wgrad slab reductions ride along the next dgrad launch (False: their own reduce kernels,
+    # and the dgrads of the Winograd layers run Winograd too)
+    DEFER_REDUCE = True
+
     def __init__(self, specs, board, device):
         assert specs, "empty trunk"
         self.specs = specs
@@ -177,20 +181,19 @@ class HipTrunk(_PackedConvs):
                 and ops.conv_wino_ok(board, 1, s.coutp, s.cinp, 3) for s in specs]
         self._init_packing(specs, device, wino)
         self._wino_plans = {}
-        # half-board Winograd blocks at every batch (set by a search whose GPU rollouts share the
-        # chip: RAG_WINO_HALF=1 forces it for experiments)
-        self.wino_half = os.environ.get("RAG_WINO_HALF") == "1"
+        # half-board Winograd blocks at every batch (a search whose GPU rollouts share the chip
+        # may set it)
+        self.wino_half = False
         self._work = None
-        self._rstream = None
-        # wgrad slab reductions ride along the next dgrad launch (RAG_WGRAD_DEFER=0: own kernels)
-        self.defer_reduce = os.environ.get("RAG_WGRAD_DEFER", "1") != "0"
+        self.defer_reduce = self.DEFER_REDUCE
         # The dgrad of a Winograd layer runs the direct kernel while it carries a deferred
         # reduction: the Winograd grid is exactly one wave of blocks (one per CU), so the
         # reduction's ~28 MB of partial slabs stream after every block's epilogue (+6-8 us in
         # the step), while the direct kernel's ragged last wave absorbs them (+1-2 us); without
-        # deferral (own reduce kernels, or the reduce stream) the dgrad runs Winograd as well.
-        self.wino_dgrad = (not self.defer_reduce or os.environ.get("RAG_WGRAD_OVERLAP") == "1"
-                           or os.environ.get("RAG_WINO_DGRAD") == "1")
+        # deferral (own reduce kernels) the dgrad runs Winograd as well. (Overlapping the
+        # reductions with the dgrad on a second stream measured slower, 78.1k vs 80.8k
+        # positions/s, and was deleted in round 6: docs/KERNELS.md.)
+        self.wino_dgrad = not self.defer_reduce
         self.wino_dgrad_min_batch = 512
         self._pending = ops.PendingReduction() if device.type == "cuda" else None
 
@@ -231,16 +234,7 @@ class HipTrunk(_PackedConvs):
         for s in self.specs:
             need = max(need, ops._lib().rag_conv_wgrad_workspace(B, S, s.coutp, s.cinp, s.ks,
                                                                  None))
-        # two slab workspaces: layer l's reduction (on the reduce stream) may still read one
-        # while layer l-1's wgrad writes the other
-        self._work = [torch.empty(need + 1024, dtype=torch.float32, device=self.device)
-                      for _ in range(2)]
-        self._wevt = [None, None]
-        # Overlapping the reductions with dgrad on a second stream measured slower on MI355X
-        # (78.1k vs 80.8k positions/s: the two contend for CUs and L2); opt-in only.
-        if self._rstream is None and self.device.type == "cuda" and \
-                os.environ.get("RAG_WGRAD_OVERLAP") == "1":
-            self._rstream = torch.cuda.Stream(self.device)
+        self._work = torch.empty(need + 1024, dtype=torch.float32, device=self.device)
 
     def input_buffer(self, B):
         self.ensure_batch(B)
@@ -294,27 +288,18 @@ class HipTrunk(_PackedConvs):
         S = self.S
         which = top_which
         wino = self.wino_plan(B)
-        main = torch.cuda.current_stream(self.device)
-        rs = self._rstream
-        for i, l in enumerate(range(self.L - 1, -1, -1)):
+        for l in range(self.L - 1, -1, -1):
             s = self.specs[l]
             g = self.grad_buffer(l, which, B)
             x = self.acts[l][:B]
-            slot = i & 1 if rs is not None else 0
-            if rs is not None and self._wevt[slot] is not None:
-                main.wait_event(self._wevt[slot])  # the reduction that last read this slab
-            # without a reduce stream, layer l's slab reduction is deferred into the free block
-            # slots of its own dgrad launch (this trunk's PendingReduction handle, passed to that
-            # launch explicitly); dW[l] is final after that
-            defer = rs is None and self.defer_reduce
+            # layer l's slab reduction is deferred into the free block slots of its own dgrad
+            # launch (this trunk's PendingReduction handle, passed to that launch explicitly);
+            # dW[l] is final after that
+            defer = self.defer_reduce
             ops.conv_wgrad(g, x, dws[l], dbs[l], B, S, self.halo[l], s.cout, s.coutp, s.cin,
-                           s.cinp, s.ks, accumulate=accumulate, work=self._work[slot],
-                           hg=self.halo[l], reduce_stream=rs, defer=defer,
+                           s.cinp, s.ks, accumulate=accumulate, work=self._work,
+                           hg=self.halo[l], defer=defer,
                            pending=self._pending if defer else None)
-            if rs is not None:
-                ev = torch.cuda.Event()
-                ev.record(rs)
-                self._wevt[slot] = ev
             if l > 0:
                 below = self.specs[l - 1]
                 which ^= 1
@@ -337,15 +322,8 @@ class HipTrunk(_PackedConvs):
             elif defer:
                 ops.wgrad_flush(self._pending)
             if on_layer_done is not None:
-                if rs is not None:
-                    with torch.cuda.stream(rs):  # the bucket all-reduce follows the reduction
-                        on_layer_done(l)
-                else:
-                    on_layer_done(l)
-        # weight / bias gradients complete before anything on the main stream reads them
-        if rs is not None:
-            main.wait_stream(rs)
-        elif self.defer_reduce:
+                on_layer_done(l)
+        if self.defer_reduce:
             ops.wgrad_flush(self._pending)
 
 
@@ -360,6 +338,11 @@ class BNSpec(object):
 
 
 class ResTrunk(_PackedConvs):
+    # 3x3 128 -> 128 layers whose input BN is fused run the Winograd BN kernel: "0" off, "1"
+    # forward only (default), "2" forward and dgrad (see __init__)
+    WINO_MODE = "1"
+    DEFER_REDUCE = True
+
     """Residual trunk of ResnetPolicy (reference policy.py:196-244) on the HIP engine:
 
         A_0 = conv0(x)                                       (linear, 5x5 by default)
@@ -395,12 +378,12 @@ class ResTrunk(_PackedConvs):
         self._B = 0
         # 3x3 128 -> 128 layers whose input BN is fused (_prologue_ok) run the Winograd kernel
         # with the BN built into its input transform (conv_wino.hip WinoBN) at batches that fill
-        # its grid; RAG_RES_WINO: 0 off, 1 (default) forward only, 2 forward and dgrad. The dgrad
+        # its grid; WINO_MODE: 0 off, 1 (default) forward only, 2 forward and dgrad. The dgrad
         # carries the deferred wgrad reduction: one wave of Winograd blocks pays for it in full
         # (51.6 vs 48.6 us on the direct kernel; standalone it is 37.4 us + a 16.6 us reduction,
         # and riding in the BN backward apply made that pass 47.9 instead of 18.5 us). ResNet
         # 71.6 k (1) / 70.9 k (2) / 69.7 k (2, no deferral) / 68.0 k (0) positions/s on one box.
-        mode = os.environ.get("RAG_RES_WINO", "1") if device.type == "cuda" else "0"
+        mode = str(self.WINO_MODE) if device.type == "cuda" else "0"
         wino = [mode != "0" and l > 0 and s.ks == 3 and s.cinp == s.coutp == 128
                 and ops.conv_wino_ok(board, 1, s.cinp, s.coutp, 3) for l, s in enumerate(specs)]
         self._init_packing(specs, device, wino)
@@ -416,11 +399,11 @@ class ResTrunk(_PackedConvs):
         self._unit_last = ends
         self._work = None
         # 3x3 wgrad slab reductions ride along the dgrad launch that follows them (as HipTrunk)
-        self.defer_reduce = os.environ.get("RAG_WGRAD_DEFER", "1") != "0"
+        self.defer_reduce = self.DEFER_REDUCE
         self._pending = ops.PendingReduction() if device.type == "cuda" else None
-        self.bn_prologue = os.environ.get("RAG_BN_PROLOGUE", "1") != "0"
-        # fused BNs: the backward finalize folded into the apply (RAG_BN_FOLD=0: two launches)
-        self.fold_bwd_finalize = os.environ.get("RAG_BN_FOLD", "1") != "0" and self.S <= 32
+        self.bn_prologue = True
+        # fused BNs: the backward finalize folded into the apply (False: two launches)
+        self.fold_bwd_finalize = self.S <= 32
         self._fused = []  # per BN: fused into the next conv on the last forward
 
     # ------------------------------------------------------------------ buffers
@@ -482,7 +465,7 @@ class ResTrunk(_PackedConvs):
         input x and applies U = ReLU(cx[col] x + cc[col]) while staging, its wgrad does the same,
         and its dgrad recomputes the ReLU mask from x; U is never materialised. Needs the
         128-channel ping-pong / slab kernels (3x3, unpadded width, a grid that fills the chip);
-        other layers keep the bn_apply pass. RAG_BN_PROLOGUE=0 disables it."""
+        other layers keep the bn_apply pass. bn_prologue = False disables it."""
         sp = self.specs[j + 1]
         return (self.bn_prologue and sp.ks == 3 and self.hin[j + 1] == 1 and self.K == self.KP
                 and ops.conv_bn_fusable(B, self.S, 1, sp.cinp, sp.coutp, sp.ks))

@@ -152,11 +152,12 @@ class RankWatchdog(object):
 
 def inject_stall(rank, step):
     """Fault injection for the failure-detection tests and rehearsals: when the environment
-    names this rank and step (RAG_STALL_RANK / RAG_STALL_STEP), stop here (sleep) as a rank
-    whose peer collective never arrives would."""
-    r = os.environ.get("RAG_STALL_RANK")
-    if r is None or int(r) != int(rank):
+    names this rank and step (RAG_STALL="rank:step[:seconds]"), stop here (sleep, default an
+    hour) as a rank whose peer collective never arrives would."""
+    spec = os.environ.get("RAG_STALL")
+    if not spec:
         return
-    if int(os.environ.get("RAG_STALL_STEP", "0")) != int(step):
+    parts = spec.split(":")
+    if int(parts[0]) != int(rank) or int(parts[1] if len(parts) > 1 else 0) != int(step):
         return
-    time.sleep(float(os.environ.get("RAG_STALL_SECONDS", "3600")))
+    time.sleep(float(parts[2]) if len(parts) > 2 else 3600.0)

@@ -17,8 +17,6 @@ full search, built for a GPU evaluator:
 (``get_move(state)``, ``update_with_move(move)``); ``ParallelMCTSPlayer`` mirrors MCTSPlayer.
 """
 import collections
-import os
-import concurrent.futures
 import time
 
 import numpy as np
@@ -75,16 +73,6 @@ class _Ready(object):
     def result(self):
         r = self.res
         return (r[0], r[1], r[2] if len(r) > 2 else None)
-
-
-class _Async(object):
-    """Evaluation submitted from the worker thread: result() joins it, then its _Pending."""
-
-    def __init__(self, future):
-        self.future = future
-
-    def result(self):
-        return self.future.result().result()
 
 
 class _Pending(object):
@@ -155,12 +143,16 @@ class _SlotResult(object):
 class NetworkEvaluator(object):
     """Batched leaf evaluation: native boards -> (move priors [n, S*S], values [n])."""
 
-    def __init__(self, policy=None, value=None, nthreads=8):
+    def __init__(self, policy=None, value=None, nthreads=8, two_streams=True, graph=False):
         self.policy = policy
         self.value = value
-        # policy and value trunks of a wave on two streams (default; RAG_EVAL_STREAMS=1: one):
-        # 95.4k vs 92.8k sims/s, profiles/mcts_eval_streams_r2.txt
-        self.two_streams = os.environ.get("RAG_EVAL_STREAMS", "2") == "2"
+        # policy and value trunks of a wave on two streams (two_streams=False: one): 95.4k vs
+        # 92.8k sims/s, profiles/mcts_eval_streams_r2.txt
+        self.two_streams = bool(two_streams)
+        # graph=True: a wave size seen before replays a captured HIP graph of its whole pass
+        # (measured slower inside the search, 66.4k vs 70k sims/s: the search is GPU-bound and
+        # the replay costs GPU time; kept for host-bound callers)
+        self.graph = bool(graph)
 
         self.nthreads = nthreads
         self.pfids = policy.preprocessor.feature_ids if policy is not None else None
@@ -243,7 +235,7 @@ class NetworkEvaluator(object):
         """Evaluate wave ``wid`` of the native search through a pinned slot (see _Slot): the
         leaves are packed natively into pinned memory (host ladder reads on the search pool),
         then copies in, feature kernel, both networks and copies out are queued on the current
-        stream (a captured HIP graph for full waves, RAG_EVAL_GRAPH=1). Returns a handle whose
+        stream (a captured HIP graph for full waves with graph=True). Returns a handle whose
         result() gives numpy (priors, values, sensible)."""
         S = search.root_board.size
         gf = self.gpu["p"]
@@ -258,8 +250,7 @@ class NetworkEvaluator(object):
             superko = False
         ppol, pval = self._plans()
         key = (n, S, superko, host_lad)
-        if (os.environ.get("RAG_EVAL_GRAPH", "0") == "1" and n == slot.B and
-                self._graph_ok(slot, key)):
+        if self.graph and n == slot.B and self._graph_ok(slot, key):
             for plan in (ppol, pval):
                 if plan is not None:
                     plan.sync_weights()
@@ -377,8 +368,8 @@ class NetworkEvaluator(object):
         of ~30 kernel launches through Python (0.37 -> 0.02 ms of host time per wave, measured).
         The packed bf16 weights are refreshed outside the graph when the fp32 masters changed.
         Measured slower inside the search (66.4k vs 70k sims/s: the search is GPU-bound there and
-        the replay costs GPU time), so it is opt-in: RAG_EVAL_GRAPH=1."""
-        if os.environ.get("RAG_EVAL_GRAPH", "0") != "1":
+        the replay costs GPU time), so it is opt-in: graph=True."""
+        if not self.graph:
             return self._run_nets(xs, ppol, pval)
         graphs = self.__dict__.setdefault("_graphs", {})
         key = (n, xs[0].shape[-1], id(ppol), id(pval))
@@ -403,8 +394,8 @@ class NetworkEvaluator(object):
             side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(side):
                 self._run_nets(xs, ppol, pval)  # buffers sized before capture
-                # thread-local capture: rollout launches of other threads (RAG_ASYNC_EVAL) may
-                # run while this thread captures
+                # thread-local capture: rollout launches of other threads (the multi-GPU search's
+                # serving thread beside rank 0's master) may run while this thread captures
                 with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
                     out = self._run_nets(xs, ppol, pval)
             torch.cuda.current_stream().wait_stream(side)
@@ -511,12 +502,9 @@ class ParallelMCTS(object):
         # GPU rollouts of `rollout_group` consecutive waves go out as one launch
         # (gpu_rollout.RolloutBatcher); up to `max_inflight` waves' rollouts are in flight
         self.rollout_group = int(rollout_group)
-        # RAG_ASYNC_EVAL=1: feature extraction + network launch of a wave run on a worker thread
-        # (the native feature code releases the GIL) while the host selects the next wave.
-        # Measured slower (52-55k vs 59k sims/s): the host ladder reads are the bound and the
-        # concurrent select only competes with them for the CPU share, so it is off by default.
-        self.async_eval = os.environ.get("RAG_ASYNC_EVAL", "0") == "1"
-        self._pool = None
+        # leaves packed natively into pinned slots and evaluated in one GPU pass per wave when
+        # the evaluator supports it (NetworkEvaluator.wave_capable); False: board objects
+        self.packed_waves = True
         self.pipeline = int(pipeline)
         self.stats = {"waves": 0, "sims": 0}
 
@@ -657,8 +645,7 @@ class ParallelMCTS(object):
         # Python board objects), one graph-capturable GPU pass per wave
         slots = None
         cap = getattr(self.evaluator, "wave_capable", None)
-        if cap is not None and os.environ.get("RAG_PACKED_WAVES", "1") == "1" and \
-                cap(s.root_board.size):
+        if cap is not None and self.packed_waves and cap(s.root_board.size):
             slots = self.__dict__.get("_slots")
             if slots is None or slots.depth != self.pipeline:
                 slots = self._slots = _Slots(self.evaluator.gpu["p"].device, self.pipeline)
@@ -678,10 +665,6 @@ class ParallelMCTS(object):
                     t1 = time.perf_counter()
                     if slots is not None:
                         handle = self.evaluator.submit_wave(s, wid, n, slots, self.batch)
-                    elif self.async_eval:
-                        if self._pool is None:
-                            self._pool = concurrent.futures.ThreadPoolExecutor(1)
-                        handle = _Async(self._pool.submit(submit, boards))
                     else:
                         handle = submit(boards)
                     queue.append((wid, n, handle, pending))

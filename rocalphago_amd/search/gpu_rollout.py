@@ -6,7 +6,6 @@ A playout is ~430 strictly sequential moves, so one launch lasts as long as its 
 small ring of streams (separate hardware queues) and run concurrently; on one stream they would
 serialise and cap the search at one wave of rollouts per playout latency."""
 import ctypes
-import os
 
 import numpy as np
 import torch
@@ -107,12 +106,10 @@ class RolloutBatcher(object):
 
 
 class GpuRollouts(object):
-    def __init__(self, policy, device=None, nstreams=None, priority=None):
+    def __init__(self, policy, device=None, nstreams=6, priority=0):
+        """nstreams: ring of rollout streams (hardware queues); priority: torch stream priority
+        (larger = lower; 0 = default)."""
         self.device = torch.device(device or "cuda")
-        if nstreams is None:
-            nstreams = int(os.environ.get("RAG_ROLLOUT_STREAMS", "6"))
-        if priority is None:  # torch: larger number = lower priority; 0 = default
-            priority = int(os.environ.get("RAG_ROLLOUT_PRIORITY", "0"))
         self.streams = [torch.cuda.Stream(self.device, priority=priority)
                         for _ in range(max(1, nstreams))]
         self._next = 0

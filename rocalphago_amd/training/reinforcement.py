@@ -33,6 +33,10 @@ from ..players.ai import ProbabilisticPolicyPlayer
 from ..utils.go_util import flatten_idx
 
 
+# games kept native (training/selfplay.py) whenever both players support it; False: the
+# Python lock-step loop (benchmarks/rl_bench.py --selfplay python)
+NATIVE_SELFPLAY = True
+
 def _make_training_pair(st, mv, preprocessor):
     st_tensor = preprocessor.state_to_tensor(st)
     mv_tensor = np.zeros((1, st.size * st.size))
@@ -111,8 +115,7 @@ def run_n_games(optimizer, learner, opponent, num_games, mock_states=[], mode="p
     board_size = learner.policy.model.input_shape[-1]
     model = learner.policy.model
     from .selfplay import NativeSelfPlay
-    if not mock_states and os.environ.get("RAG_NATIVE_SELFPLAY", "1") == "1" and \
-            NativeSelfPlay.supported(learner, opponent):
+    if not mock_states and NATIVE_SELFPLAY and NativeSelfPlay.supported(learner, opponent):
         # games kept native, one GPU pass + one native call per ply (training/selfplay.py)
         sp = NativeSelfPlay(learner, opponent)
         feats, moves, learner_color, winners = sp.play(num_games, board_size)

@@ -43,13 +43,12 @@ def _player_kind(player):
 class NativeSelfPlay(object):
     """Lock-step games of ``learner`` vs ``opponent`` (policy players on HIP models)."""
 
-    def __init__(self, learner, opponent, nthreads=16, pipeline=None):
-        import os
+    def __init__(self, learner, opponent, nthreads=16, pipeline=2, graphs=True):
         self.learner, self.opponent = learner, opponent
         self.nthreads = nthreads
-        if pipeline is None:
-            pipeline = int(os.environ.get("RAG_SELFPLAY_PIPELINE", "2"))
         self.pipeline = max(1, int(pipeline))
+        # graphs=False: eager launches of the active games only (the graph-replay A/B)
+        self.graphs = bool(graphs)
         self.device = learner.policy.model.device
         self._gf = {}
         self._pinned = {}
@@ -96,11 +95,10 @@ class NativeSelfPlay(object):
         replays as a captured HIP graph after its first eager run -- one host call instead of ~25
         Python kernel launches (the launch sequence was the self-play's host bound,
         profiles/selfplay_host_r3.txt). Finished games ride along; their moves are ignored.
-        RAG_SELFPLAY_GRAPH=0: eager launches of the active games only."""
-        import os
+        graphs=False: eager launches of the active games only."""
         import time
         t0 = time.perf_counter()
-        if group is None or os.environ.get("RAG_SELFPLAY_GRAPH", "1") == "0":
+        if group is None or not self.graphs:
             group = None
             packed = idx
             pos = np.arange(len(idx))

@@ -1,6 +1,6 @@
 """A minimal data-parallel loop with the same failure detection as bench.py (gloo, CPU): every
 rank heart-beats per step into the rank watchdog and all-reduces a gradient-sized buffer;
-RAG_STALL_RANK / RAG_STALL_STEP make one rank hang before its all-reduce. Launched by
+RAG_STALL=rank:step makes one rank hang before its all-reduce. Launched by
 tests/test_watchdog.py under torch.distributed.run."""
 import os
 import sys

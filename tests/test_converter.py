@@ -102,9 +102,9 @@ def test_fused_chunk_compression_writes_the_same_file(tmp_path, ref_data, monkey
             files.append(dst)
     out = {}
     for fused in ("1", "0"):
-        monkeypatch.setenv("RAG_CONVERT_FUSED", fused)
         path = str(tmp_path / ("o%s.h5" % fused))
-        GameConverter(list(DEFAULT_FEATURES)).sgfs_to_hdf5(files, path, nthreads=3, batch=4)
+        GameConverter(list(DEFAULT_FEATURES)).sgfs_to_hdf5(files, path, nthreads=3, batch=4,
+                                                           fused=fused == "1")
         with h5lite.File(path) as f:
             out[fused] = (f["states"][()], f["actions"][()],
                           {k: f["file_offsets"][k][()].tolist() for k in f["file_offsets"]})

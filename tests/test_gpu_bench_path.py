@@ -153,10 +153,11 @@ def test_north_star_sl_step_matches_fp32(cuda, augment, defer, monkeypatch):
     ``augment``: the bench's random dihedral augmentation (all 8 transforms, drawn by the
     sl_batch kernel and applied while packing the input) -- the reference applies the same
     per-sample transforms to the planes and the targets with numpy. ``defer=False``
-    (RAG_WGRAD_DEFER=0): the wgrad reductions run as their own launches and the dgrads of the
-    Winograd layers run Winograd too."""
+    (HipTrunk.DEFER_REDUCE False): the wgrad reductions run as their own launches and the
+    dgrads of the Winograd layers run Winograd too."""
     if not defer:
-        monkeypatch.setenv("RAG_WGRAD_DEFER", "0")
+        from rocalphago_amd.models.engine import HipTrunk
+        monkeypatch.setattr(HipTrunk, "DEFER_REDUCE", False)
     torch.backends.cudnn.allow_tf32 = False
     torch.backends.cuda.matmul.allow_tf32 = False
     pol = CNNPolicy(DEFAULT_FEATURES, board=19, filters_per_layer=192, layers=12, device=cuda,

@@ -222,10 +222,9 @@ def test_native_selfplay_graph_replay_matches_eager(cuda, monkeypatch):
     b = CNNPolicy(feats, board=9, layers=2, filters_per_layer=32, device=cuda, seed=32)
     out = {}
     for mode in ("1", "0"):
-        monkeypatch.setenv("RAG_SELFPLAY_GRAPH", mode)
         la = ProbabilisticPolicyPlayer(a, move_limit=50, rng=np.random.RandomState(7))
         lb = ProbabilisticPolicyPlayer(b, move_limit=50, rng=np.random.RandomState(8))
-        sp = NativeSelfPlay(la, lb)
+        sp = NativeSelfPlay(la, lb, graphs=mode == "1")
         out[mode] = sp.play(130, 9)
         if mode == "1":
             assert any(len(v["graphs"]) for k, v in sp._pinned.items() if k[0] != "eager")

@@ -149,11 +149,9 @@ def test_graph_replayed_evaluation_matches_eager(monkeypatch):
                    device=dev, seed=4)
     boards = [s.native for s in _random_positions(40, 19, 7)]
     other = [s.native for s in _random_positions(40, 19, 8)]
-    monkeypatch.setenv("RAG_EVAL_GRAPH", "0")
     eager = NetworkEvaluator(pol, val)
     ref = [eager.submit(b).result() for b in (boards, other)]
-    monkeypatch.setenv("RAG_EVAL_GRAPH", "1")
-    ev = NetworkEvaluator(pol, val)
+    ev = NetworkEvaluator(pol, val, graph=True)
     for rep in range(3):  # eager, capture + replay, replay
         for b, r in zip((boards, other), ref):
             got = ev.submit(b).result()
@@ -162,10 +160,8 @@ def test_graph_replayed_evaluation_matches_eager(monkeypatch):
     assert len(ev._graphs) == 1
     # a larger wave reallocates the activations: graphs of the smaller size must be re-captured
     small = boards[:20]
-    monkeypatch.setenv("RAG_EVAL_GRAPH", "0")
     ref_small = NetworkEvaluator(pol, val).submit(small).result()
-    monkeypatch.setenv("RAG_EVAL_GRAPH", "1")
-    ev2 = NetworkEvaluator(pol, val)
+    ev2 = NetworkEvaluator(pol, val, graph=True)
     for b in (small, small, small, boards + other, small, small):
         got = ev2.submit(b).result()
         if len(b) == 20:
@@ -175,9 +171,7 @@ def test_graph_replayed_evaluation_matches_eager(monkeypatch):
     w = pol.model.get_weights()
     w[0] = w[0] * 0.5
     pol.model.set_weights(w)
-    monkeypatch.setenv("RAG_EVAL_GRAPH", "0")
     ref2 = NetworkEvaluator(pol, val).submit(boards).result()
-    monkeypatch.setenv("RAG_EVAL_GRAPH", "1")
     got2 = ev.submit(boards).result()
     assert not np.array_equal(ref2[0], ref[0][0])
     for g, e in zip(got2, ref2):
@@ -185,7 +179,7 @@ def test_graph_replayed_evaluation_matches_eager(monkeypatch):
 
 
 def test_two_stream_evaluation_matches_one_stream(monkeypatch):
-    """RAG_EVAL_STREAMS=2 runs the value trunk on a second stream; priors / values /
+    """two_streams=True runs the value trunk on a second stream; priors / values /
     sensibleness equal the single-stream pass for repeated waves of two sizes."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -199,11 +193,8 @@ def test_two_stream_evaluation_matches_one_stream(monkeypatch):
     val = CNNValue(DEFAULT_FEATURES + ["color"], board=19, filters_per_layer=192, layers=4,
                    device=dev, seed=4)
     waves = [[s.native for s in _random_positions(n, 19, 11 + n)] for n in (64, 33)]
-    monkeypatch.setenv("RAG_EVAL_GRAPH", "0")
-    monkeypatch.setenv("RAG_EVAL_STREAMS", "1")
-    one = NetworkEvaluator(pol, val)
+    one = NetworkEvaluator(pol, val, two_streams=False)
     ref = [one.submit(b).result() for b in waves]
-    monkeypatch.setenv("RAG_EVAL_STREAMS", "2")
     two = NetworkEvaluator(pol, val)
     assert two.two_streams
     for rep in range(3):
@@ -233,8 +224,7 @@ def test_packed_wave_matches_board_path(monkeypatch, superko, graph):
     root = GameState(size=19, enforce_superko=superko)
     for mv in st.history:
         root.do_move(mv)
-    monkeypatch.setenv("RAG_EVAL_GRAPH", graph)
-    ev = NetworkEvaluator(pol, val)
+    ev = NetworkEvaluator(pol, val, graph=graph == "1")
     assert ev.wave_capable(19)
     slots = _Slots(dev, 2)
     s = rg.Search(root.native, 4)

@@ -2,6 +2,8 @@
 against plain PyTorch fp32 references: the kernels one by one, then the whole fused plan against
 the generic executor (reference policy.py:141-271; Keras-1 BN axis=-1 on 'th' tensors)."""
 import numpy as np
+
+from rocalphago_amd.models.engine import ResTrunk
 import pytest
 import torch
 import torch.nn.functional as F
@@ -357,11 +359,11 @@ def test_wino_bn_kernels_match_torch(ops):
 @pytest.mark.parametrize("wino", ["0", "2"])
 def test_resnet_bn_prologue_train_step_matches_unfused(ops, monkeypatch, wino):
     """A 128-filter ResnetPolicy train step at B = 256 with BN+ReLU fused into the conv
-    prologues gives the same loss and gradients as the bn_apply path (RAG_BN_PROLOGUE=0): on the
-    direct kernels (RAG_RES_WINO=0), and with the fused layers on the Winograd kernel (forward and
-    dgrad, RAG_RES_WINO=2; its transform roundings put the gradients' cosine at 0.997-0.999)."""
+    prologues gives the same loss and gradients as the bn_apply path (bn_prologue = False): on the
+    direct kernels (WINO_MODE 0), and with the fused layers on the Winograd kernel (forward and
+    dgrad, WINO_MODE 2; its transform roundings put the gradients' cosine at 0.997-0.999)."""
     from rocalphago_amd.models import kerasish as KZ
-    monkeypatch.setenv("RAG_RES_WINO", wino)
+    monkeypatch.setattr(ResTrunk, "WINO_MODE", wino)
     _, fused = _pair(128, 5, 19, {})
     _, plain = _pair(128, 5, 19, {})
     plain.model._plan_for().trunk.bn_prologue = False
@@ -414,10 +416,10 @@ def test_resnet_wino_train_step_vs_fp32(ops, monkeypatch):
     forward + dgrad vs on the ping-pong kernels), weight-gradient cosines against the CPU fp32
     step per tensor and over the whole gradient."""
     from rocalphago_amd.models import kerasish as KZ
-    monkeypatch.setenv("RAG_RES_WINO", "0")
+    monkeypatch.setattr(ResTrunk, "WINO_MODE", "0")
     cpu, direct = _pair(128, 5, 19, {})
-    direct.model._plan_for()  # (the trunk reads RAG_RES_WINO when the plan is built)
-    monkeypatch.setenv("RAG_RES_WINO", "2")
+    direct.model._plan_for()  # (the trunk reads WINO_MODE when the plan is built)
+    monkeypatch.setattr(ResTrunk, "WINO_MODE", "2")
     _, wino = _pair(128, 5, 19, {})
     wino.model._plan_for()
     B = 256

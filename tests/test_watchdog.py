@@ -39,7 +39,7 @@ def test_healthy_two_rank_job_finishes():
 
 
 def test_stalled_rank_is_named_and_job_exits_nonzero():
-    rc, out, dt = _launch({"RAG_STALL_RANK": "1", "RAG_STALL_STEP": "5"}, 120)
+    rc, out, dt = _launch({"RAG_STALL": "1:5"}, 120)
     assert rc != 0, out[-2000:]
     assert dt < 60, "the stall must end the job within the watchdog limit (took %.0fs)" % dt
     # whichever rank's watchdog fires first (the stalled rank's own thread, or a rank blocked in

@@ -11,7 +11,7 @@ it printed) are echoed so gpurun's tail shows the result.
 
 Examples:
     python tools/gpujob.py r4a tests smoke bench
-    python tools/gpujob.py ab sl sl@RAG_WGRAD_DEFER=0 sl
+    python tools/gpujob.py ab sl sl@RAG_WINO=0 sl
     python tools/gpujob.py tr trace-sl pmc-sl
     python tools/gpujob.py x 'conv:300:VARIANTS=7 python scripts/dbg/conv_ab.py'
 """
