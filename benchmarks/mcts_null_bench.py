@@ -197,6 +197,7 @@ def run_master(args):
         mc.stop()
         m = mc.master_stats
         keys = ("t_select", "t_ship", "t_value", "t_rollout", "t_idle")
+        busy = sum(m[k] for k in keys[:4])
         out = {"metric": "DistributedMCTS host ceiling (native master loop + shared-memory "
                          "channel; null evaluator + null rollouts), 19x19",
                "ranks": dp.world, "threads_master": nt, "threads_per_rank": args.threads,
@@ -206,6 +207,10 @@ def run_master(args):
                "seconds": round(dt, 3), "sims_per_s": round(m["sims"] / dt, 1),
                "waves": int(m["waves"]), "max_leaves_in_flight": int(m["max_inflight"]),
                "us_per_sim": {k[2:]: round(m[k] / max(1, m["sims"]) * 1e6, 3) for k in keys},
+               # rank 0's own tree work per simulation (everything but waiting for the ranks)
+               # and the rate it alone would sustain
+               "master_busy_us_per_sim": round(busy / max(1, m["sims"]) * 1e6, 3),
+               "master_ceiling_sims_per_s": round(m["sims"] / max(busy, 1e-9), 1),
                "frac": {k[2:]: round(m[k] / dt, 3) for k in keys},
                "tree_timers_s": [round(x, 4) for x in s.timers],
                "leaves_per_rank": [int(c) for c in m["leaves"]]}

@@ -5,6 +5,13 @@ playouts, over many positions. One JSON line per search design.
   python benchmarks/search_efficiency.py [--ranks 2 4 8] [--positions 50] [--per-rank 128]
   python benchmarks/search_efficiency.py --designs DistributedMCTS/shipped --per-rank 512 \
       --lmbda 0.5 --rollout-delay 6 --truth-mult 16     (the bench's geometry)
+  python benchmarks/search_efficiency.py --effective --per-rank 512 --lmbda 0.5 \
+      --rollout-delay 6 --truth-mult 16 --gpu-waves 64 128 256 512 --depths 1 2 \
+      --ranks 1 2 4 8 --gpu-rates profiles/mcts_wave_rates_r6.json \
+      --master-ceiling 900000 > profiles/search_efficiency_r6.json
+      (every per-GPU wave / depth of the one-tree search at N = 1, 2, 4, 8;
+       efficiency x the modelled rate min(N x one GPU's rate at that wave, the master's
+       ceiling) = effective simulations/s; the argmax per N is the shipped geometry)
 """
 import argparse
 import json
@@ -28,7 +35,20 @@ def main():
                     help="0.5: rollouts mixed in as the bench's search does")
     ap.add_argument("--rollout-delay", type=int, default=0)
     ap.add_argument("--truth-mult", type=int, default=4)
+    ap.add_argument("--effective", action="store_true",
+                    help="sweep the one-tree search's per-GPU wave and depth (module doc)")
+    ap.add_argument("--gpu-waves", type=int, nargs="+", default=[64, 128, 256, 512],
+                    help="--effective: per-GPU waves of the 19x19 bench (8192 playouts per GPU "
+                         "per move), scaled to the study's budget")
+    ap.add_argument("--depths", type=int, nargs="+", default=[1, 2])
+    ap.add_argument("--gpu-rates", default=None,
+                    help="--effective: JSON {wave: one GPU's sims/s} measured on MI355X")
+    ap.add_argument("--master-ceiling", type=float, default=None,
+                    help="--effective: rank 0's host ceiling, sims/s (mcts_null_bench)")
     args = ap.parse_args()
+    if args.effective:
+        effective(args)
+        return
     from rocalphago_amd.search.efficiency import study
     for d in args.designs:
         # design suffixes: /split (per-rank wave = wave / N), /shipped (the bench's geometry:
@@ -42,6 +62,50 @@ def main():
                   truth_mult=args.truth_mult)
         r["design"] = d
         print(json.dumps(r), flush=True)
+
+
+def effective(args):
+    """Efficiency of every (per-GPU wave, depth) at every N, then effective simulations/s =
+    efficiency x min(N x one GPU's rate at that wave, the master's ceiling)."""
+    from rocalphago_amd.search.efficiency import study
+    rates = None
+    if args.gpu_rates:
+        with open(args.gpu_rates) as f:
+            rates = {int(k): float(v) for k, v in json.load(f)["sims_per_s_by_wave"].items()}
+    rows = []
+    for w in args.gpu_waves:
+        sw = max(1, int(round(w * args.per_rank / 8192.0)))  # the study's wave
+        for d in args.depths:
+            r = study(worlds=tuple(args.ranks), per_rank=args.per_rank,
+                      n_positions=args.positions, size=args.board, search_cls="DistributedMCTS",
+                      outdir=os.path.join(args.out, "eff"), lmbda=args.lmbda,
+                      rollout_delay=args.rollout_delay, truth_mult=args.truth_mult,
+                      shipped=True, depth=d, wave=sw)
+            for n in args.ranks:
+                row = dict(r["rows"]["DistributedMCTS_%d" % n])
+                row.update(gpu_wave=w, study_wave=sw)
+                if rates is not None and w in rates:
+                    rate = n * rates[w]
+                    if args.master_ceiling:
+                        rate = min(rate, args.master_ceiling)
+                    row["modelled_sims_per_s"] = round(rate, 1)
+                    row["effective_sims_per_s"] = round(rate * row["efficiency"], 1)
+                rows.append(row)
+                print(json.dumps(row), file=sys.stderr, flush=True)
+    best = {}
+    for row in rows:
+        k = row["ranks"]
+        if "effective_sims_per_s" in row and (k not in best or row["effective_sims_per_s"] >
+                                               best[k]["effective_sims_per_s"]):
+            best[k] = row
+    print(json.dumps({"what": "one-tree multi-GPU search (DistributedMCTS): budget efficiency "
+                              "per (per-GPU wave, waves per GPU awaiting values) at N ranks, "
+                              "and effective sims/s = efficiency x modelled sims/s",
+                      "per_rank_playouts": args.per_rank, "board": args.board,
+                      "positions": args.positions, "lmbda": args.lmbda,
+                      "rollout_delay": args.rollout_delay, "truth_mult": args.truth_mult,
+                      "gpu_rates": rates, "master_ceiling": args.master_ceiling,
+                      "rows": rows, "best_by_ranks": best}, indent=1), flush=True)
 
 
 if __name__ == "__main__":

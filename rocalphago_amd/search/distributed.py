@@ -41,6 +41,7 @@ import math
 import os
 import socket
 import threading
+import time
 import uuid
 
 import numpy as np
@@ -168,6 +169,8 @@ class DistributedMCTS(ParallelMCTS):
         # GPU pipeline's leaves in flight, deterministically, with instant CPU evaluations
         self.emulate_latency = False
         self.idle_us = 20
+        # no request for this long: launch a partial GPU rollout group (the search is ending)
+        self.flush_s = 0.002
         self.chan = None
         if self.world > 1 or self.force_master:
             self.chan = open_channel(dp, self.nslots, max(self.batches), self.S, self.PW,
@@ -335,6 +338,7 @@ class DistributedMCTS(ParallelMCTS):
         zq = collections.deque()   # [slot, wave, rollout handle, index of the wave]
         recv = 0
         ws = None
+        last_req = None
         while True:
             busy = bool(evq or zq)
             got = 0
@@ -362,8 +366,12 @@ class DistributedMCTS(ParallelMCTS):
                         return None
             # values: the oldest wave once its pass is done (blocking only with `depth` waves
             # on the GPU); emulating the GPU's latency (the CPU study), only with `depth` waves
-            # received or nothing more coming
-            idle = got == 0 and len(evq) < self.depth
+            # received or nothing more coming for idle_us
+            now = time.perf_counter()
+            if got == 1 or last_req is None:
+                last_req = now
+            quiet = got == 0 and now - last_req > self.flush_s
+            idle = self.emulate_latency and got == 0 and len(evq) < self.depth
             while evq and (len(evq) >= self.depth or idle or
                            (not self.emulate_latency and _done(evq[0][3]))):
                 k, wid, n, h, roll = evq.popleft()
@@ -372,12 +380,16 @@ class DistributedMCTS(ParallelMCTS):
                     ws.drop_wave(wid)
                 else:
                     zq.append([k, wid, roll, recv])
-            # rollout results, in slot order; nothing else to do: launch a partial rollout group
-            # and stop holding results back (the master may be waiting for the slots)
+            # rollout results, in slot order. A partial rollout group is launched when the master
+            # cannot send more (every slot of this rank holds a wave) or has sent nothing for
+            # flush_s (the end of a search); emulating, results are held back `rollout_delay`
+            # waves unless nothing more comes
             idle = got == 0 and not evq
-            if idle and zq and self._batcher is not None and self._batcher.cur is not None:
+            if zq and self._batcher is not None and self._batcher.cur is not None and \
+                    (len(evq) + len(zq) >= self.nslots or (quiet and not evq)):
                 self._batcher.flush()
-            while zq and zq[0][2].done() and (recv - zq[0][3] >= self.rollout_delay or idle):
+            hold = self.rollout_delay if self.emulate_latency else 0
+            while zq and zq[0][2].done() and (recv - zq[0][3] >= hold or idle):
                 k, wid, roll, _ = zq.popleft()
                 z = roll.result()
                 views[k]["z"][:len(z)] = z
