@@ -41,6 +41,11 @@ def main():
                     help="--effective: per-GPU waves of the 19x19 bench (8192 playouts per GPU "
                          "per move), scaled to the study's budget")
     ap.add_argument("--depths", type=int, nargs="+", default=[1, 2])
+    ap.add_argument("--metric", default="js", choices=["js", "kl"],
+                    help="--effective: distance to the truth behind the equivalent budget")
+    ap.add_argument("--ladder-depth", type=int, default=3,
+                    help="--effective: the one-GPU yardstick's waves awaiting values (the "
+                         "single-GPU bench's pipeline)")
     ap.add_argument("--gpu-rates", default=None,
                     help="--effective: JSON {wave: one GPU's sims/s} measured on MI355X")
     ap.add_argument("--master-ceiling", type=float, default=None,
@@ -80,7 +85,9 @@ def effective(args):
                       n_positions=args.positions, size=args.board, search_cls="DistributedMCTS",
                       outdir=os.path.join(args.out, "eff"), lmbda=args.lmbda,
                       rollout_delay=args.rollout_delay, truth_mult=args.truth_mult,
-                      shipped=True, depth=d, wave=sw)
+                      shipped=True, depth=d, wave=sw, metric=args.metric,
+                      ladder={"depth": args.ladder_depth,
+                              "rollout_delay": args.rollout_delay})
             for n in args.ranks:
                 row = dict(r["rows"]["DistributedMCTS_%d" % n])
                 row.update(gpu_wave=w, study_wave=sw)
@@ -99,8 +106,11 @@ def effective(args):
                                                best[k]["effective_sims_per_s"]):
             best[k] = row
     print(json.dumps({"what": "one-tree multi-GPU search (DistributedMCTS): budget efficiency "
-                              "per (per-GPU wave, waves per GPU awaiting values) at N ranks, "
-                              "and effective sims/s = efficiency x modelled sims/s",
+                              "per (per-GPU wave, waves per GPU awaiting values) at N ranks "
+                              "against ONE GPU at the single-GPU bench geometry searching N "
+                              "times as long (the ladder), and effective sims/s = efficiency x "
+                              "modelled sims/s",
+                      "metric": args.metric, "ladder_depth": args.ladder_depth,
                       "per_rank_playouts": args.per_rank, "board": args.board,
                       "positions": args.positions, "lmbda": args.lmbda,
                       "rollout_delay": args.rollout_delay, "truth_mult": args.truth_mult,

@@ -103,17 +103,19 @@ class ShmChannel {
     if (create) {
       L_ = layout(cap, P, PW, stride);
       const size_t total = align64(sizeof(ChanHead)) + (size_t)nranks * nslots * L_.bytes;
-      int fd = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
-      if (fd < 0) throw std::runtime_error("shm_open(create) failed: " + name);
-      if (ftruncate(fd, (off_t)total) != 0) {
+      int fd = open_fd(name, O_CREAT | O_EXCL | O_RDWR);
+      if (fd < 0) throw std::runtime_error("cannot create the search channel " + name);
+      // the pages are reserved now: a full /dev/shm fails here, not as SIGBUS on a later store
+      if (ftruncate(fd, (off_t)total) != 0 || posix_fallocate(fd, 0, (off_t)total) != 0) {
         close(fd);
-        shm_unlink(name.c_str());
-        throw std::runtime_error("ftruncate of the search channel failed");
+        unlink_name(name);
+        throw std::runtime_error("no room for the search channel " + name + " (" +
+                                 std::to_string(total >> 20) + " MB)");
       }
       base_ = (char*)mmap(nullptr, total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
       close(fd);
       if (base_ == MAP_FAILED) {
-        shm_unlink(name.c_str());
+        unlink_name(name);
         throw std::runtime_error("mmap of the search channel failed");
       }
       bytes_ = total;
@@ -137,8 +139,8 @@ class ShmChannel {
       std::atomic_thread_fence(std::memory_order_seq_cst);
       __atomic_store_n(&h->magic, kChanMagic, __ATOMIC_RELEASE);
     } else {
-      int fd = shm_open(name.c_str(), O_RDWR, 0600);
-      if (fd < 0) throw std::runtime_error("shm_open(attach) failed: " + name);
+      int fd = open_fd(name, O_RDWR);
+      if (fd < 0) throw std::runtime_error("cannot attach the search channel " + name);
       struct stat st;
       if (fstat(fd, &st) != 0 || (size_t)st.st_size < sizeof(ChanHead)) {
         close(fd);
@@ -157,7 +159,20 @@ class ShmChannel {
   }
   ~ShmChannel() {
     if (base_ && base_ != MAP_FAILED) munmap(base_, bytes_);
-    if (owner_) shm_unlink(name_.c_str());
+    if (owner_) unlink_name(name_);
+  }
+  // "/name": a POSIX shared-memory object (/dev/shm); any other name: a file path (a node whose
+  // /dev/shm is too small for the channel maps a file instead, search/distributed.py)
+  static int open_fd(const std::string& name, int flags) {
+    if (!name.empty() && name[0] == '/' && name.find('/', 1) == std::string::npos)
+      return shm_open(name.c_str(), flags, 0600);
+    return ::open(name.c_str(), flags, 0600);
+  }
+  static void unlink_name(const std::string& name) {
+    if (!name.empty() && name[0] == '/' && name.find('/', 1) == std::string::npos)
+      shm_unlink(name.c_str());
+    else
+      ::unlink(name.c_str());
   }
   ShmChannel(const ShmChannel&) = delete;
   ShmChannel& operator=(const ShmChannel&) = delete;
@@ -171,7 +186,7 @@ class ShmChannel {
   uint32_t stride() const { return head()->stride; }
   const std::string& name() const { return name_; }
   void unlink() {
-    if (owner_) shm_unlink(name_.c_str());
+    if (owner_) unlink_name(name_);
     owner_ = false;
   }
 

@@ -70,8 +70,15 @@ def open_channel(dp, nslots, cap, S, PW, stride):
     ch = None
     name = None
     if rank == 0:
-        name = "/rag_mcts_%d_%s" % (os.getpid(), uuid.uuid4().hex[:12])
-        ch = _rg.SearchChannel(name, True, world, nslots, cap, S * S, PW, stride)
+        tag = "rag_mcts_%d_%s" % (os.getpid(), uuid.uuid4().hex[:12])
+        try:
+            name = "/" + tag
+            ch = _rg.SearchChannel(name, True, world, nslots, cap, S * S, PW, stride)
+        except RuntimeError:
+            # /dev/shm too small (containers often give it 64 MB): a mapped file instead
+            import tempfile
+            name = os.path.join(tempfile.gettempdir(), tag)
+            ch = _rg.SearchChannel(name, True, world, nslots, cap, S * S, PW, stride)
     if world > 1:
         obj = [name]
         dist.broadcast_object_list(obj, 0)

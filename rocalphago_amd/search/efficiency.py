@@ -184,6 +184,20 @@ def kl(truth, x):
     return float(np.mean(out))
 
 
+def js(truth, x):
+    """Mean over positions of the Jensen-Shannon divergence between root-visit distributions
+    (+0.5 smoothing on either's children). Symmetric: unlike KL(truth || x) it does not reward a
+    search for spreading visits thinly (virtual loss flattens the visits of wide searches)."""
+    out = []
+    for t, v in zip(truth, x):
+        legal = (t > 0) | (v > 0)
+        p = (t[legal] + 0.5) / (t[legal] + 0.5).sum()
+        q = (v[legal] + 0.5) / (v[legal] + 0.5).sum()
+        m = 0.5 * (p + q)
+        out.append(float(0.5 * (p * np.log(p / m)).sum() + 0.5 * (q * np.log(q / m)).sum()))
+    return float(np.mean(out))
+
+
 def agreement(truth, x):
     return float(np.mean([np.argmax(t) == np.argmax(v) for t, v in zip(truth, x)]))
 
@@ -208,12 +222,18 @@ def equivalent_budget(ladder, k):
 def study(worlds=(2, 4, 8), per_rank=128, batch=16, n_positions=50, size=9, truth_mult=4,
           search_cls="SharedRootMCTS", outdir="/tmp/rag_eff", pos_seed=0, net_seed=3,
           ladder_top=None, split_wave=False, lmbda=0.0, rollout_delay=0, shipped=False,
-          capped=False, depth=1, wave=None):
+          capped=False, depth=1, wave=None, metric="kl", ladder=None):
     """The whole comparison; returns a JSON-able dict. ``split_wave``: the N-rank search's
     per-rank wave is batch / N (the job keeps the one-GPU search's leaves in flight per round
     instead of N times as many). ``shipped``: the bench's geometry instead (shipped_waves: the
     single trees' wave and the per-rank waves scaled from the 19x19 bench; ``batch`` ignored),
-    normally with ``lmbda`` 0.5 and ``rollout_delay`` 6 as the bench runs it."""
+    normally with ``lmbda`` 0.5 and ``rollout_delay`` 6 as the bench runs it.
+    ``metric``: "kl" (KL(truth || visits)) or "js" (Jensen-Shannon, symmetric) for the
+    equivalent-budget interpolation (both are reported). ``ladder``: None (single trees, one
+    wave in flight) or {"depth": d, "rollout_delay": r}: the ladder is the one-tree search on ONE
+    rank at the single-GPU geometry (wave, d waves awaiting values, rollouts returned r waves
+    later), so the efficiency compares N GPUs with one GPU searching N times as long."""
+    dist_fn = js if metric == "js" else kl
     os.makedirs(outdir, exist_ok=True)
     pol, val = nets(size, net_seed)
     states = positions(n_positions, size, pos_seed)
@@ -242,19 +262,33 @@ def study(worlds=(2, 4, 8), per_rank=128, batch=16, n_positions=50, size=9, trut
         return cache[key], cache[key + "_n"]
 
     truth, truth_nodes = single(top * truth_mult, seed=99)
-    ladder, rows = [], {}
-    b = per_rank
-    while b <= top:
-        v, nodes = single(b)
-        k = kl(truth, v)
-        ladder.append((b, k))
-        rows["single_%d" % b] = {"budget": b, "kl": round(k, 4),
-                                 "agree": round(agreement(truth, v), 3),
-                                 "nodes": float(nodes.mean())}
-        b *= 2
     cfg = {"size": size, "net_seed": net_seed, "pos_seed": pos_seed,
            "n_positions": n_positions, "batch": batch, "search_cls": search_cls,
            "lmbda": lmbda, "rollout_delay": rollout_delay, "depth": depth}
+
+    def one_gpu(budget):  # the ladder on one rank at the single-GPU geometry (cached)
+        key = "g%d_d%d_r%d" % (budget, ladder["depth"], ladder["rollout_delay"])
+        if key not in cache:
+            d = os.path.join(outdir, "ladder_%s" % key)
+            os.makedirs(d, exist_ok=True)
+            lcfg = dict(cfg, search_cls="DistributedMCTS", depth=ladder["depth"],
+                        rollout_delay=ladder["rollout_delay"])
+            v, _ = multi_rank(1, budget, lcfg, d)
+            cache[key], cache[key + "_n"] = v, np.full(len(v), float(budget))
+            np.savez(ck, **cache)
+        return cache[key], cache[key + "_n"]
+
+    ladder_pts, rows = [], {}
+    b = per_rank
+    while b <= top:
+        v, nodes = single(b) if ladder is None else one_gpu(b)
+        k = dist_fn(truth, v)
+        ladder_pts.append((b, k))
+        rows["single_%d" % b] = {"budget": b, "kl": round(kl(truth, v), 4),
+                                 "js": round(js(truth, v), 5),
+                                 "agree": round(agreement(truth, v), 3),
+                                 "nodes": float(nodes.mean())}
+        b *= 2
     for w in worlds:
         d = os.path.join(outdir, "%s_w%d" % (search_cls, w))
         os.makedirs(d, exist_ok=True)
@@ -265,10 +299,10 @@ def study(worlds=(2, 4, 8), per_rank=128, batch=16, n_positions=50, size=9, trut
         else:
             wcfg = dict(cfg, batch=max(1, batch // w)) if split_wave else cfg
         vis, dup = multi_rank(w, per_rank * w, wcfg, d)
-        k = kl(truth, vis)
-        teq = equivalent_budget(ladder, k)
+        teq = equivalent_budget(ladder_pts, dist_fn(truth, vis))
         rows["%s_%d" % (search_cls, w)] = {
-            "ranks": w, "budget": per_rank * w, "kl": round(k, 4),
+            "ranks": w, "budget": per_rank * w, "kl": round(kl(truth, vis), 4),
+            "js": round(js(truth, vis), 5),
             "wave_per_rank": wcfg["batch"], "depth": depth, "rollout_delay": rollout_delay,
             "agree": round(agreement(truth, vis), 3), "duplication": round(float(dup.mean()), 3),
             "equivalent_single_tree_budget": round(teq, 1),
@@ -276,5 +310,5 @@ def study(worlds=(2, 4, 8), per_rank=128, batch=16, n_positions=50, size=9, trut
     return {"positions": n_positions, "board": size, "per_rank_playouts": per_rank,
             "wave": batch, "truth_budget": top * truth_mult, "search": search_cls,
             "lmbda": lmbda, "rollout_delay": rollout_delay, "shipped_geometry": bool(shipped),
-            "capped": bool(capped),
+            "capped": bool(capped), "metric": metric, "ladder": ladder or "single trees",
             "truth_nodes": float(truth_nodes.mean()), "rows": rows}

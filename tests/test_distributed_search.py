@@ -373,3 +373,25 @@ def test_channel_master_loop_one_process():
     assert mc._search.rollouts == mc._search.sims
     assert mc.leaf_counts()[0] == mc.stats["sims"]
     mc.stop()
+
+
+@__import__("pytest").mark.parametrize("kind", ["shm", "file"])
+def test_search_channel_slots_and_attach(tmp_path, kind):
+    """The leaf channel (csrc/mcts/master.hpp): a POSIX shared-memory object or, when /dev/shm
+    is too small, a mapped file; a second mapping (another rank) sees the master's request and
+    the rank's answers through the slot sequence numbers."""
+    import os
+    name = ("/rag_test_%d" % os.getpid()) if kind == "shm" else str(tmp_path / "chan")
+    a = rg.SearchChannel(name, True, 2, 3, 16, 49, 50, 8)
+    b = rg.SearchChannel(name, False)
+    a.unlink()
+    assert (b.nranks, b.nslots, b.cap, b.P, b.PW, b.stride) == (2, 3, 16, 49, 50, 8)
+    assert b.wait_request(1, 2, 0, b.cmd()[0], 0) == 0  # nothing posted yet
+    a.view(1, 2, "paths")[:2] = np.arange(16, dtype=np.int16).reshape(2, 8)
+    b.view(1, 2, "priors")[3, 49] = 0.25
+    assert a.view(1, 2, "priors")[3, 49] == 0.25
+    assert np.array_equal(b.view(1, 2, "paths")[1], np.arange(8, 16))
+    a.post_cmd(rg.CHAN_CMD_STOP, 7)
+    assert b.wait_request(1, 2, 0, 0, 1000) == 2 and b.cmd()[1:] == (rg.CHAN_CMD_STOP, 7)
+    b.abort("test")
+    assert a.aborted and "test" in a.why
