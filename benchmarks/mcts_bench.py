@@ -223,6 +223,13 @@ def main():
     ap.add_argument("--max-inflight", type=int, default=8, help="rollout waves in flight")
     ap.add_argument("--rollout-group", type=int, default=6, help="waves per rollout launch")
     ap.add_argument("--moves", type=int, default=1)
+    ap.add_argument("--eval-priority", type=int, default=None,
+                    help="stream priority of the wave passes (e.g. -1: above the rollouts)")
+    ap.add_argument("--rollout-priority", type=int, default=None,
+                    help="stream priority of the GPU rollouts")
+    ap.add_argument("--rollout-slice", type=int, default=None,
+                    help="moves per GPU rollout launch (0: one launch per playout; default "
+                         "search/gpu_rollout.DEFAULT_SLICE)")
     ap.add_argument("--depth", type=int, default=None,
                     help="--distributed: waves per GPU awaiting values (default DIST_GEOMETRY)")
     ap.add_argument("--master-share", type=float, default=None,
@@ -233,6 +240,13 @@ def main():
                     help="--distributed: one tree on rank 0 (default) or shared root statistics")
     args = ap.parse_args()
     import torch
+    from rocalphago_amd.search import apv, gpu_rollout
+    if args.rollout_slice is not None:
+        gpu_rollout.DEFAULT_SLICE = args.rollout_slice
+    if args.eval_priority is not None:
+        apv.ParallelMCTS.eval_priority = args.eval_priority
+    if args.rollout_priority is not None:
+        gpu_rollout.DEFAULT_PRIORITY = args.rollout_priority
     if args.distributed:
         from rocalphago_amd.parallel.dp import DPContext
         dp = DPContext()

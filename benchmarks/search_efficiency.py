@@ -43,6 +43,9 @@ def main():
     ap.add_argument("--depths", type=int, nargs="+", default=[1, 2])
     ap.add_argument("--metric", default="js", choices=["js", "kl"],
                     help="--effective: distance to the truth behind the equivalent budget")
+    ap.add_argument("--ladder-top", type=int, default=None,
+                    help="--effective: the ladder's largest budget (default the largest N-rank "
+                         "budget; larger lets efficiencies above 1 show instead of clamping)")
     ap.add_argument("--ladder-depth", type=int, default=3,
                     help="--effective: the one-GPU yardstick's waves awaiting values (the "
                          "single-GPU bench's pipeline)")
@@ -87,7 +90,8 @@ def effective(args):
                       rollout_delay=args.rollout_delay, truth_mult=args.truth_mult,
                       shipped=True, depth=d, wave=sw, metric=args.metric,
                       ladder={"depth": args.ladder_depth,
-                              "rollout_delay": args.rollout_delay})
+                              "rollout_delay": args.rollout_delay},
+                      ladder_top=args.ladder_top)
             for n in args.ranks:
                 row = dict(r["rows"]["DistributedMCTS_%d" % n])
                 row.update(gpu_wave=w, study_wave=sw)

@@ -97,4 +97,21 @@ __device__ __forceinline__ float warp_max(float v) {
   return v;
 }
 
+// SGD folded into the weight packing (conv.hip pack_trunk_kernel, conv_wino.hip wino_pack_kernel):
+// a packing kernel that reads fp32 master w also reads its gradient g = w[goff] (the model's
+// flat gradient buffer mirrors the parameter buffer), writes back w - lr (g + wd w) and packs
+// the updated value; on = 0: plain packing.
+struct SgdFold {
+  long goff;
+  float lr, wd;
+  int on;
+  __device__ __forceinline__ float step(float* w) const {
+    const float v = *w;
+    if (!on) return v;
+    const float u = v - lr * (w[goff] + wd * v);
+    *w = u;
+    return u;
+  }
+};
+
 }  // namespace rag

@@ -1113,21 +1113,24 @@ constexpr int kPackFields = 11;
 // element-per-thread version wrote the dgrad layout 2 bytes per 384-byte stride (29 us/step); one
 // block per all-tap 32x32 tile (contiguous OIHW runs through LDS) measured 29-47 us: kept this.
 __global__ void __launch_bounds__(256) pack_trunk_kernel(const int64_t* __restrict__ table,
-                                                         int nrows, int nfull) {
+                                                         int nrows, int nfull, SgdFold sgd) {
+  // the padded bias of a layer (its fp32 master stepped first with sgd.on)
+  auto pack_bias = [&](float* b, int COUT, int COUTP, float* bo) {
+    for (int n = threadIdx.x; n < COUTP; n += blockDim.x) {
+      const float v = (b && n < COUT) ? sgd.step(b + n) : 0.f;
+      if (bo) bo[n] = v;
+    }
+  };
   if ((int)blockIdx.y == nfull) {  // the bias-only rows (after the nfull packed ones): one block each
     for (int r = nfull + blockIdx.x; r < nrows; r += gridDim.x) {
       const int64_t* t = table + (size_t)r * kPackFields;
-      const float* b = (const float*)t[1];
-      const int COUT = (int)t[2], COUTP = (int)t[5];
-      float* bo = (float*)t[9];
-      if (bo)
-        for (int n = threadIdx.x; n < COUTP; n += blockDim.x) bo[n] = (b && n < COUT) ? b[n] : 0.f;
+      pack_bias((float*)t[1], (int)t[2], (int)t[5], (float*)t[9]);
     }
     return;
   }
   const int64_t* t = table + (size_t)blockIdx.y * kPackFields;
-  const float* W = (const float*)t[0];
-  const float* b = (const float*)t[1];
+  float* W = (float*)t[0];
+  float* b = (float*)t[1];
   const int COUT = (int)t[2], CIN = (int)t[3], KS = (int)t[4], COUTP = (int)t[5],
             CINP = (int)t[6];
   bf16* Wf = (bf16*)t[7];
@@ -1144,8 +1147,7 @@ __global__ void __launch_bounds__(256) pack_trunk_kernel(const int64_t* __restri
   const int tap = j % taps;
   if (g >= ntn * ntc) return;
   if (!Wf && !Wb) {  // bias-only row (a Winograd layer: its weights come from rag_wino_pack)
-    if (bo && g == 0 && tap == 0)
-      for (int n = threadIdx.x; n < COUTP; n += blockDim.x) bo[n] = (b && n < COUT) ? b[n] : 0.f;
+    if (g == 0 && tap == 0) pack_bias(b, COUT, COUTP, bo);
     return;
   }
   const int ct = g % ntc;
@@ -1156,7 +1158,7 @@ __global__ void __launch_bounds__(256) pack_trunk_kernel(const int64_t* __restri
   for (int i = 0; i < 16; ++i) {
     const int nl = ty + 4 * i;
     const int n = nt * 64 + nl, c = ct * 64 + tx;
-    const float v = (n < COUT && c < CIN) ? W[(n * CIN + c) * taps + tap] : 0.f;
+    const float v = (n < COUT && c < CIN) ? sgd.step(W + (n * CIN + c) * taps + tap) : 0.f;
     tl[nl][tx] = v;
     if (Wf && n < COUTP && c < CINP) Wf[(tap * COUTP + n) * CINP + c] = (bf16)v;
   }
@@ -1169,20 +1171,22 @@ __global__ void __launch_bounds__(256) pack_trunk_kernel(const int64_t* __restri
       if (c < CINP && n < COUTP) Wb[((taps - 1 - tap) * CINP + c) * COUTP + n] = (bf16)tl[tx][cl];
     }
   }
-  if (bo && g == 0 && tap == 0)
-    for (int n = threadIdx.x; n < COUTP; n += blockDim.x) bo[n] = (b && n < COUT) ? b[n] : 0.f;
+  if (g == 0 && tap == 0) pack_bias(b, COUT, COUTP, bo);
 }
 }  // namespace
 
+// lr, wd, goff (elements from a master weight to its gradient), sgd_on: the optimizer step
+// folded into the packing (each master element is stepped by exactly one thread)
 RAG_API int rag_pack_trunk(const int64_t* table, int nrows, int nfull, int64_t total,
-                           hipStream_t stream) {
+                           hipStream_t stream, int64_t goff, float lr, float wd, int sgd_on) {
   // total: the grid width, max over layers of 8 * taps * ceil(64x64 tiles / 8) (XCD-grouped order).
   // Rows [0, nfull) pack weights (one grid row each); rows [nfull, nrows) only pad their bias
   // (Winograd layers: rag_wino_pack packs the weights) and share one grid row: the 11 bias-only
   // rows of the SL trunk were 11 x 200 blocks that exited at once.
   if (nrows <= 0 || nfull < 0 || nfull > nrows || total <= 0 || total % 8) return -1;
   const dim3 grid((unsigned)total, (unsigned)(nfull + (nrows > nfull ? 1 : 0)));
-  pack_trunk_kernel<<<grid, 256, 0, stream>>>(table, nrows, nfull);
+  pack_trunk_kernel<<<grid, 256, 0, stream>>>(table, nrows, nfull,
+                                              SgdFold{(long)goff, lr, wd, sgd_on});
   return (int)hipGetLastError();
 }
 

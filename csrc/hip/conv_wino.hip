@@ -595,9 +595,10 @@ conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
 // pack_trunk_kernel's Wb) from the same LDS tile, for layers whose dgrad runs the direct kernel:
 // the fp32 weights are read once per step instead of once more by pack_trunk.
 constexpr int kWinoPackFields = 8;  // W, COUT, CIN, COUTP, CINP, Uf, Ub (or 0), Wd (or 0)
-__global__ void __launch_bounds__(256) wino_pack_kernel(const int64_t* __restrict__ table) {
+__global__ void __launch_bounds__(256) wino_pack_kernel(const int64_t* __restrict__ table,
+                                                        SgdFold sgd) {
   const int64_t* t = table + (size_t)blockIdx.y * kWinoPackFields;
-  const float* W = (const float*)t[0];
+  float* W = (float*)t[0];
   const int COUT = (int)t[1], CIN = (int)t[2], COUTP = (int)t[3], CINP = (int)t[4];
   bf16* Uf = (bf16*)t[5];
   bf16* Ub = (bf16*)t[6];
@@ -620,10 +621,10 @@ __global__ void __launch_bounds__(256) wino_pack_kernel(const int64_t* __restric
     const int n = nt * 64 + nl, c = ct * 64 + tx;
     float g0 = 0.f, g1 = 0.f, g2 = 0.f;
     if (n < COUT && c < CIN) {
-      const float* p = W + ((size_t)(n * CIN + c) * 3 + ky) * 3;
-      g0 = p[0];
-      g1 = p[1];
-      g2 = p[2];
+      float* p = W + ((size_t)(n * CIN + c) * 3 + ky) * 3;
+      g0 = sgd.step(p);
+      g1 = sgd.step(p + 1);
+      g2 = sgd.step(p + 2);
     }
     tl[0][nl][tx] = g0;
     tl[1][nl][tx] = g1;
@@ -814,9 +815,11 @@ RAG_API int rag_conv_wino(const void* X, const void* W, const float* bias, void*
 }
 
 // table: kWinoPackFields int64 per layer (W, COUT, CIN, COUTP, CINP, Uf or 0, Ub or 0, Wd or 0).
-RAG_API int rag_wino_pack(const int64_t* table, int nlayers, int max_tiles, hipStream_t stream) {
+// goff / lr / wd / sgd_on: the optimizer step folded in (rag_pack_trunk)
+RAG_API int rag_wino_pack(const int64_t* table, int nlayers, int max_tiles, hipStream_t stream,
+                          int64_t goff, float lr, float wd, int sgd_on) {
   if (nlayers <= 0 || max_tiles <= 0) return -1;
   const dim3 grid((unsigned)(3 * max_tiles), (unsigned)nlayers);
-  wino_pack_kernel<<<grid, 256, 0, stream>>>(table);
+  wino_pack_kernel<<<grid, 256, 0, stream>>>(table, SgdFold{(long)goff, lr, wd, sgd_on});
   return (int)hipGetLastError();
 }

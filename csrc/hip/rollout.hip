@@ -39,7 +39,7 @@ namespace {
 constexpr uint8_t kOff = 3;  // colour code of an off-board neighbour
 
 template <int PM>
-struct GameLds {
+struct alignas(16) GameLds {
   float base[2][PM];  // cached logit w/o last-move terms; [0] black to move, [1] white
   int lib[PM];
   int16_t lab[PM];
@@ -374,13 +374,29 @@ struct Game {
   }
 };
 
+// Sliced playouts (rag_rollouts_sliced): a game's whole state — its LDS image, the scalars and
+// every lane's generator — is parked in HBM between launches of at most `slice` moves, so no
+// launch keeps a CU's LDS for a whole ~5 ms playout (conv blocks of the search's networks, which
+// need ~150 KB of a CU's LDS, could not start on any CU holding a rollout wave: their launches
+// overlapping a resident rollout kernel took 1.1 ms instead of 0.1, profiles/
+// mcts_rollout_interference_r5.txt). The moves played are the unsliced kernel's bit for bit.
+template <int PM>
+struct ParkedGame {
+  GameLds<PM> lds;
+  int32_t sc[16];    // cur, ko, l1, l2, pb, pw, nm, end, moves, done
+  uint32_t rng[64];  // per lane
+};
+
 // meta: [cur, ko, last1, last2, passes_b, passes_w, nmoves, end]
+// park: null (one launch plays the whole game) or the game's parked state; first: initialise
+// from colors / meta (else resume from park); slice: moves this launch may play
 template <int SC, int NPL, int PM, int GPB>
 __device__ __forceinline__ void rollout_body(
     BlockLds<PM, GPB>& sh, const int8_t* __restrict__ colors, const int32_t* __restrict__ meta,
     int n_pos, int R, int S_rt, float komi, int limit, const float* __restrict__ w,
     const float* __restrict__ pattern, uint32_t seed, int8_t* __restrict__ winner,
-    int16_t* __restrict__ length, float* __restrict__ dbg_logits) {
+    int16_t* __restrict__ length, float* __restrict__ dbg_logits,
+    ParkedGame<PM>* __restrict__ park = nullptr, int first = 1, int slice = 1 << 30) {
   const int S = SC > 0 ? SC : S_rt;
   const int P = S * S;
   const int wv = threadIdx.x >> 6;
@@ -388,6 +404,8 @@ __device__ __forceinline__ void rollout_body(
   const int game = blockIdx.x * GPB + wv;
   if (game >= n_pos * R) return;  // whole wave exits together
   const int pos = game / R;
+  ParkedGame<PM>* pk = park ? park + game : nullptr;
+  if (pk && !first && pk->sc[9]) return;  // finished in an earlier slice
   GameLds<PM>& L = sh.g[wv];
   Game<SC, NPL, PM> g{S_rt, &L, lane};
   float wl[7];
@@ -399,29 +417,62 @@ __device__ __forceinline__ void rollout_body(
     const int p = lane + 64 * k;
     px[k] = p / S;
     py[k] = p - px[k] * S;
-    if (p < P) {
-      const int c = colors[(size_t)pos * P + p];
-      L.cell[p] = (uint8_t)(c > 0 ? 1 : (c < 0 ? 2 : 0));
-      L.chg[p] = 0;
-      L.dirty[p] = 0;
-    }
   }
-  wave_sync();
-  g.init_labels();
-  g.recount_libs();
+  int cur, ko, l1, l2, pb, pw, nm, moves = 0;
+  bool end;
+  LaneRng rng;
+  if (pk && !first) {
+    // resume: the LDS image back in 16-byte pieces, the scalars, this lane's generator
+    constexpr int kPieces = (int)(sizeof(GameLds<PM>) / 16);
+    static_assert(sizeof(GameLds<PM>) % 16 == 0, "parked LDS image in 16-byte pieces");
+    const uint4* src = reinterpret_cast<const uint4*>(&pk->lds);
+    uint4* dst = reinterpret_cast<uint4*>(&L);
+    for (int i = lane; i < kPieces; i += 64) dst[i] = src[i];
+    cur = pk->sc[0];
+    ko = pk->sc[1];
+    l1 = pk->sc[2];
+    l2 = pk->sc[3];
+    pb = pk->sc[4];
+    pw = pk->sc[5];
+    nm = pk->sc[6];
+    end = pk->sc[7] != 0;
+    moves = pk->sc[8];
+    rng.s = pk->rng[lane];
+    wave_sync();
+  } else {
 #pragma unroll
-  for (int k = 0; k < NPL; ++k) {
-    const int p = lane + 64 * k;
-    if (p < P) {
-      g.compute_base(p, wl, pattern);
-      L.chg[p] = 0;
+    for (int k = 0; k < NPL; ++k) {
+      const int p = lane + 64 * k;
+      if (p < P) {
+        const int c = colors[(size_t)pos * P + p];
+        L.cell[p] = (uint8_t)(c > 0 ? 1 : (c < 0 ? 2 : 0));
+        L.chg[p] = 0;
+        L.dirty[p] = 0;
+      }
     }
+    wave_sync();
+    g.init_labels();
+    g.recount_libs();
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      const int p = lane + 64 * k;
+      if (p < P) {
+        g.compute_base(p, wl, pattern);
+        L.chg[p] = 0;
+      }
+    }
+    wave_sync();
+    const int32_t* m = meta + pos * 8;
+    cur = m[0];
+    ko = m[1];
+    l1 = m[2];
+    l2 = m[3];
+    pb = m[4];
+    pw = m[5];
+    nm = m[6];
+    end = m[7] != 0;
+    rng.s = hash32(seed ^ hash32(game * 0x9E3779B9u + lane * 0x85EBCA6Bu + 1u));
   }
-  wave_sync();
-  const int32_t* m = meta + pos * 8;
-  int cur = m[0], ko = m[1], l1 = m[2], l2 = m[3], pb = m[4], pw = m[5], nm = m[6];
-  bool end = m[7] != 0;
-  LaneRng rng{hash32(seed ^ hash32(game * 0x9E3779B9u + lane * 0x85EBCA6Bu + 1u))};
 
   // logit of lane point k = cached base + last-move terms
   // (branch-free: selects instead of early returns; adding 0 to a finite logit and anything to
@@ -447,8 +498,8 @@ __device__ __forceinline__ void rollout_body(
     return;
   }
 
-  int moves = 0;
-  while (!end && moves < limit) {
+  const int stop = moves + slice < limit ? moves + slice : limit;
+  while (!end && moves < stop) {
     const int own = cur > 0 ? 1 : 2;
     const int l1x = l1 >= 0 ? l1 / S : -100, l1y = l1 >= 0 ? l1 - (l1 / S) * S : -100;
     const int l2x = l2 >= 0 ? l2 / S : -100, l2y = l2 >= 0 ? l2 - (l2 / S) * S : -100;
@@ -550,6 +601,21 @@ __device__ __forceinline__ void rollout_body(
     if (nm > 1 && l1 == -1 && l2 == -1 && cur == -1) end = true;
     ++moves;
   }
+  if (pk && !end && moves < limit) {  // park the game until the next slice
+    constexpr int kPieces = (int)(sizeof(GameLds<PM>) / 16);
+    wave_sync();
+    const uint4* src = reinterpret_cast<const uint4*>(&L);
+    uint4* dst = reinterpret_cast<uint4*>(&pk->lds);
+    for (int i = lane; i < kPieces; i += 64) dst[i] = src[i];
+    pk->rng[lane] = rng.s;
+    if (lane == 0) {
+      const int32_t v[10] = {cur, ko, l1, l2, pb, pw, nm, (int32_t)end, moves, 0};
+#pragma unroll
+      for (int i = 0; i < 10; ++i) pk->sc[i] = v[i];
+    }
+    return;
+  }
+  if (pk && lane == 0) pk->sc[9] = 1;
   // area score: stones + single-point eyeish empties
   int sb = 0, sw = 0;
 #pragma unroll
@@ -587,8 +653,10 @@ __device__ __forceinline__ void rollout_body(
   const int8_t *__restrict__ colors, const int32_t *__restrict__ meta, int n_pos, int R, int S_rt, \
       float komi, int limit, const float *__restrict__ w, const float *__restrict__ pattern,       \
       uint32_t seed, int8_t *__restrict__ winner, int16_t *__restrict__ length,                    \
-      float *__restrict__ dbg_logits
-#define RAG_RO_FWD colors, meta, n_pos, R, S_rt, komi, limit, w, pattern, seed, winner, length, dbg_logits
+      float *__restrict__ dbg_logits, void *__restrict__ park, int first, int slice
+#define RAG_RO_FWD                                                                              \
+  colors, meta, n_pos, R, S_rt, komi, limit, w, pattern, seed, winner, length, dbg_logits,        \
+      reinterpret_cast<ParkedGame<PM>*>(park), first, slice
 
 // The same playout body at two register budgets: the compiler's choice (146 VGPRs for 19x19,
 // 3 waves per SIMD) and a cap at 128 VGPRs (4 waves per SIMD, a few spills outside the move
@@ -625,28 +693,34 @@ int rollout_gpb() {
 template <int SC, int NPL, int PM, int GPB>
 void launch_gpb(hipStream_t st, const int8_t* c, const int32_t* meta, int n_pos, int R, int S,
                 float komi, int limit, const float* w, const float* pattern, unsigned seed,
-                void* winner, void* length, float* dbg) {
+                void* winner, void* length, float* dbg, void* park, int slice) {
   const dim3 grid((n_pos * R + GPB - 1) / GPB);
-  if (rollout_wpe() == 4)
-    rollout_kernel_w4<SC, NPL, PM, GPB><<<grid, 64 * GPB, 0, st>>>(
-        c, meta, n_pos, R, S, komi, limit, w, pattern, seed, (int8_t*)winner, (int16_t*)length,
-        dbg);
-  else
-    rollout_kernel<SC, NPL, PM, GPB><<<grid, 64 * GPB, 0, st>>>(
-        c, meta, n_pos, R, S, komi, limit, w, pattern, seed, (int8_t*)winner, (int16_t*)length,
-        dbg);
+  // unsliced: one launch; sliced: ceil(limit / slice) launches on the same stream, the first
+  // initialising from the inputs, every later one resuming the parked games
+  const int nl = park ? (limit + slice - 1) / slice : 1;
+  for (int l = 0; l < nl; ++l) {
+    const int first = l == 0, sl = park ? slice : (1 << 30);
+    if (rollout_wpe() == 4)
+      rollout_kernel_w4<SC, NPL, PM, GPB><<<grid, 64 * GPB, 0, st>>>(
+          c, meta, n_pos, R, S, komi, limit, w, pattern, seed, (int8_t*)winner,
+          (int16_t*)length, dbg, park, first, sl);
+    else
+      rollout_kernel<SC, NPL, PM, GPB><<<grid, 64 * GPB, 0, st>>>(
+          c, meta, n_pos, R, S, komi, limit, w, pattern, seed, (int8_t*)winner,
+          (int16_t*)length, dbg, park, first, sl);
+  }
 }
 
 template <int SC, int NPL, int PM>
 void launch(hipStream_t st, const int8_t* c, const int32_t* meta, int n_pos, int R, int S,
             float komi, int limit, const float* w, const float* pattern, unsigned seed,
-            void* winner, void* length, float* dbg) {
+            void* winner, void* length, float* dbg, void* park, int slice) {
   if (rollout_gpb() == 4)
     launch_gpb<SC, NPL, PM, 4>(st, c, meta, n_pos, R, S, komi, limit, w, pattern, seed, winner,
-                               length, dbg);
+                               length, dbg, park, slice);
   else
     launch_gpb<SC, NPL, PM, 1>(st, c, meta, n_pos, R, S, komi, limit, w, pattern, seed, winner,
-                               length, dbg);
+                               length, dbg, park, slice);
 }
 
 }  // namespace
@@ -654,15 +728,25 @@ void launch(hipStream_t st, const int8_t* c, const int32_t* meta, int n_pos, int
 // colors [n_pos][S*S] int8, meta [n_pos][8] int32, weights [7], pattern [65536] (or null);
 // winner [n_pos*R] int8 (+1 black, -1 white, 0 draw), length [n_pos*R] int16 (optional).
 // dbg_logits (optional, [n_pos*R][S*S]) switches to "initial logits only" mode.
+// park: null (one launch per playout) or rag_rollout_park_bytes(S) x n_pos x R bytes of device
+// memory (sliced: launches of at most `slice` moves, identical results)
+RAG_API long rag_rollout_park_bytes(int S) {
+  if (S == 19) return (long)sizeof(ParkedGame<384>);
+  if (S == 13) return (long)sizeof(ParkedGame<192>);
+  if (S == 9) return (long)sizeof(ParkedGame<128>);
+  return S * S <= 384 ? (long)sizeof(ParkedGame<384>) : (long)sizeof(ParkedGame<640>);
+}
+
 RAG_API int rag_rollouts(const void* colors, const int32_t* meta, int n_pos, int R, int S,
                          float komi, int limit, const float* w, const float* pattern,
                          unsigned seed, void* winner, void* length, float* dbg_logits,
-                         hipStream_t stream) {
+                         hipStream_t stream, void* park, int slice) {
   if (S < 2 || S > 25 || n_pos <= 0 || R <= 0) return -1;
+  if (park && (slice <= 0 || dbg_logits)) return -1;
   const int8_t* c = (const int8_t*)colors;
 #define RAG_RO(SC, NPL, PM)                                                                     \
   launch<SC, NPL, PM>(stream, c, meta, n_pos, R, S, komi, limit, w, pattern, seed, winner, length, \
-                      dbg_logits)
+                      dbg_logits, park, slice)
   if (S == 19) RAG_RO(19, 6, 384);
   else if (S == 13) RAG_RO(13, 3, 192);
   else if (S == 9) RAG_RO(9, 2, 128);

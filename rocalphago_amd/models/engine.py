@@ -129,6 +129,40 @@ class _PackedConvs(object):
         if self._direct_version is not None:
             self._direct_layouts()
 
+    def sgd_pack(self, weights, biases, flat, flat_grad, lr, version):
+        """The optimizer step of this trunk's parameters folded into their repacking (round 6:
+        pack_trunk + wino_pack re-read the fp32 masters right after sgd_kernel had): wino_pack
+        and pack_trunk read each master and its gradient once, write back w - lr g and pack
+        that. Returns the [start, end) element ranges of ``flat`` it stepped (the caller steps
+        the rest), or None when the packing tables do not point into ``flat`` (then nothing was
+        done)."""
+        if self._packed_version is None or getattr(self, "_pack_key", None) is None:
+            return None
+        ws = [w.contiguous() for w in weights]
+        key = tuple(w.data_ptr() for w in ws) + \
+            tuple(0 if b is None else b.data_ptr() for b in biases)
+        if key != self._pack_key:
+            return None
+        base, esz = flat.data_ptr(), flat.element_size()
+        end = base + flat.numel() * esz
+        ranges = []
+        for t in list(weights) + [b for b in biases if b is not None]:
+            p = t.data_ptr()
+            if not t.is_contiguous() or p < base or p + t.numel() * esz > end:
+                return None
+            ranges.append(((p - base) // esz, (p - base) // esz + t.numel()))
+        if flat_grad.numel() != flat.numel():
+            return None
+        sgd = ((flat_grad.data_ptr() - base) // esz, lr, 0.0)
+        if any(self._wino):
+            ops.wino_pack(self._wpack_table, sum(self._wino), self._wpack_tiles, sgd=sgd)
+        ops.pack_trunk(self._pack_table, len(self.specs), self._pack_total, self._pack_nfull,
+                       sgd=sgd)
+        self._packed_version = version
+        if self._direct_version is not None:
+            self._direct_layouts()
+        return ranges
+
     def _dgrad_wino_layouts(self):
         """Winograd dgrad weights of the Winograd layers when the dgrad normally runs the direct
         kernel (a large batch takes Winograd, see HipTrunk.backward): packed once per weight

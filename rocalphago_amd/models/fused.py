@@ -75,6 +75,25 @@ class _TrunkPlan(object):
         self.conv_names = [ld.name for ld in convs]
         self.head_name = head_conv.name
         self.K = specs[-1].cout
+        net._sgd_fold = self.sgd_fold  # the optimizer's step folded into the weight repack
+
+    def sgd_fold(self, lr):
+        """SGD step of the whole flat buffer with the trunk's part folded into its repack
+        (engine._PackedConvs.sgd_pack) and the rest by the plain kernel. False: not possible
+        (e.g. the packing tables are not built yet), nothing done."""
+        Ws, bs = self._params()
+        net = self.net
+        ver = (net.version + 1, net.flat._version)  # after the optimizer's bump()
+        ranges = self.trunk.sgd_pack(Ws, bs, net.flat, net.flat_grad, lr, ver)
+        if ranges is None:
+            return False
+        pos = 0
+        for a, b in sorted(ranges) + [(net.flat.numel(), net.flat.numel())]:
+            if a > pos:
+                ops.sgd_(net.flat[pos:a], net.flat_grad[pos:a], lr)
+            pos = max(pos, b)
+        self.folded_steps = getattr(self, "folded_steps", 0) + 1
+        return True
 
     def sync_weights(self):
         """Repack the bf16 trunk weights if the fp32 masters changed (a replayed graph reads the
@@ -330,6 +349,7 @@ class ResnetPlan(PolicyPlan):
         self.conv_names = [ld.name for ld in convs]
         self.head_name = head_conv.name
         self.K = specs[-1].cout
+        net._sgd_fold = self.sgd_fold  # the optimizer's step folded into the weight repack
         self.bias_name = bias_layer.name
         self.pass_name = pass_layer.name if pass_layer is not None else None
         self.head = PolicyHeadEngine(self.trunk, self.K, pass_logit=pass_layer is not None)

@@ -505,7 +505,10 @@ class SGD(object):
         lr = self.current_lr()
         if self.momentum and self._velocity is None:
             self._velocity = torch.zeros_like(net.flat)
-        if net.flat.is_cuda:
+        fold = getattr(net, "_sgd_fold", None)
+        if net.flat.is_cuda and not self.momentum and fold is not None and fold(lr):
+            pass  # the trunk's step rode in its weight repack (fused.sgd_fold)
+        elif net.flat.is_cuda:
             from ..ops import hipops as ops
             ops.sgd_(net.flat, net.flat_grad, lr, self.momentum, self._velocity, 0.0,
                      self.nesterov)

@@ -23,12 +23,12 @@ SIGNATURES = {
     "rag_wgrad_pending_init": [P],
     "rag_wgrad_pending_free": [P],
     "rag_pack_weights": [P, P, P, I, I, I, I, I, P],
-    "rag_pack_trunk": [P, I, I, I64, P],
+    "rag_pack_trunk": [P, I, I, I64, P, I64, F, F, I],
     # conv_wino.hip (+ the pending-handle entry in conv.hip)
     "rag_conv_wino_ok": [I, I, I, I, I],
     "rag_conv_wino": [P, P, P, P, P, I, I, I, I, I, I, I, I, P],
     "rag_conv_wino_p": [P, P, P, P, P, I, I, I, I, I, I, I, I, P, P, I],
-    "rag_wino_pack": [P, I, I, P],
+    "rag_wino_pack": [P, I, I, P, I64, F, F, I],
     "rag_conv_wino_prefer": [I, I, I, I],
     "rag_conv_wino_mode": [I, I, I, I],
     "rag_conv_wino_bn_ok": [I, I, I, I],
@@ -56,7 +56,8 @@ SIGNATURES = {
     # optim.hip
     "rag_sgd": [P, P, P, I64, F, F, F, I, P],
     # rollout.hip
-    "rag_rollouts": [P, P, I, I, I, F, I, P, P, C.c_uint, P, P, P, P],
+    "rag_rollouts": [P, P, I, I, I, F, I, P, P, C.c_uint, P, P, P, P, P, I],
+    "rag_rollout_park_bytes": [I],
     # bn.hip
     "rag_bn_workspace": [I, I],
     "rag_bn_train_fwd": [P, I, I, I, I, I, P, P, P, P, F, F, P, P, P, P],
@@ -82,7 +83,8 @@ SIGNATURES = {
 
 RESTYPES = {"rag_conv_wgrad_workspace": SZ, "rag_head_bwd_workspace": SZ,
             "rag_ladder_workspace": SZ, "rag_wgrad_pending_bytes": SZ,
-            "rag_value_mlp_workspace": SZ, "rag_value_mlp_bwd_workspace": SZ}
+            "rag_value_mlp_workspace": SZ, "rag_value_mlp_bwd_workspace": SZ,
+            "rag_rollout_park_bytes": C.c_long}
 
 
 def declare(lib):

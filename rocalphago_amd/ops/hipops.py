@@ -62,12 +62,15 @@ def pack_weights(w, coutp, cinp, wf=None, wb=None):
     return wf, wb
 
 
-def pack_trunk(table, nrows, total, nfull=None):
+def pack_trunk(table, nrows, total, nfull=None, sgd=None):
     """Repack every layer of a trunk in one launch (table: device int64 [nrows, 11], see
     rag_pack_trunk in csrc/hip/conv.hip; ``total`` = 64x64 tap tiles of the largest layer). Rows
-    past the first ``nfull`` (default: all) only pad their bias."""
+    past the first ``nfull`` (default: all) only pad their bias. ``sgd`` = (goff, lr, wd): step
+    every fp32 master by SGD first (its gradient ``goff`` elements further), in the same pass."""
     nfull = nrows if nfull is None else nfull
-    _check(_lib().rag_pack_trunk(_ptr(table), nrows, nfull, int(total), _stream()),
+    goff, lr, wd = sgd if sgd is not None else (0, 0.0, 0.0)
+    _check(_lib().rag_pack_trunk(_ptr(table), nrows, nfull, int(total), _stream(), int(goff),
+                                 float(lr), float(wd), 1 if sgd is not None else 0),
            "pack_trunk")
 
 
@@ -161,13 +164,16 @@ def conv_wino_mode(B, S, kin, nout):
     return int(_lib().rag_conv_wino_mode(B, S, kin, nout))
 
 
-def wino_pack(table, nlayers, max_tiles):
+def wino_pack(table, nlayers, max_tiles, sgd=None):
     """Winograd weights of 3x3 layers from their fp32 OIHW masters in one launch. ``table``:
     device int64 [nlayers, 8] = (W, cout, cin, coutp, cinp, Uf, Ub or 0, Wd or 0); Uf (forward,
     N = coutp, K = cinp) and Ub (dgrad, N = cinp, K = coutp) each 12 * N * K bf16, stored
     fragment-major [12][K/32][N/16][64][8] (conv_wino.hip); Wd: the direct dgrad layout
-    [9, cinp, coutp] (pack_trunk's); ``max_tiles``: 64x64 (n, c) tiles of the widest layer."""
-    _check(_lib().rag_wino_pack(_ptr(table), nlayers, int(max_tiles), _stream()), "wino_pack")
+    [9, cinp, coutp] (pack_trunk's); ``max_tiles``: 64x64 (n, c) tiles of the widest layer.
+    ``sgd`` = (goff, lr, wd): the optimizer step folded in (pack_trunk)."""
+    goff, lr, wd = sgd if sgd is not None else (0, 0.0, 0.0)
+    _check(_lib().rag_wino_pack(_ptr(table), nlayers, int(max_tiles), _stream(), int(goff),
+                                float(lr), float(wd), 1 if sgd is not None else 0), "wino_pack")
 
 
 def wino_weights(w, coutp, cinp, dgrad=True):

@@ -149,6 +149,9 @@ class NetworkEvaluator(object):
         # policy and value trunks of a wave on two streams (two_streams=False: one): 95.4k vs
         # 92.8k sims/s, profiles/mcts_eval_streams_r2.txt
         self.two_streams = bool(two_streams)
+        # stream priority of the wave passes (torch: lower = higher priority; the search runs
+        # them on a stream of this priority, above its GPU rollouts' streams)
+        self.priority = 0
         # graph=True: a wave size seen before replays a captured HIP graph of its whole pass
         # (measured slower inside the search, 66.4k vs 70k sims/s: the search is GPU-bound and
         # the replay costs GPU time; kept for host-bound callers)
@@ -285,7 +288,7 @@ class NetworkEvaluator(object):
                 # policy conv and vice versa (separate plans, separate buffers)
                 side = self.__dict__.get("_vstream")
                 if side is None:
-                    side = self._vstream = torch.cuda.Stream(x.device)
+                    side = self._vstream = torch.cuda.Stream(x.device, priority=self.priority)
                 side.wait_stream(torch.cuda.current_stream())
             if ppol is not None:
                 pr = ppol.forward(x, clone=False)
@@ -350,7 +353,7 @@ class NetworkEvaluator(object):
             main = torch.cuda.current_stream()
             side = self.__dict__.get("_vstream")
             if side is None:
-                side = self._vstream = torch.cuda.Stream(xp.device)
+                side = self._vstream = torch.cuda.Stream(xp.device, priority=self.priority)
             side.wait_stream(main)
             pr = ppol.forward(xp)
             with torch.cuda.stream(side):
@@ -664,7 +667,8 @@ class ParallelMCTS(object):
                             s.start_rollouts(wid)
                     t1 = time.perf_counter()
                     if slots is not None:
-                        handle = self.evaluator.submit_wave(s, wid, n, slots, self.batch)
+                        with self._eval_stream():
+                            handle = self.evaluator.submit_wave(s, wid, n, slots, self.batch)
                     else:
                         handle = submit(boards)
                     queue.append((wid, n, handle, pending))
@@ -701,6 +705,19 @@ class ParallelMCTS(object):
             self._acc("t_rollout_wait", t4 - t3)
             if tick is not None:
                 tick(s)  # e.g. the distributed search's root-statistics exchange
+
+    def _eval_stream(self):
+        """Context of the wave passes: a high-priority stream when ``eval_priority`` is set (the
+        hardware queue scheduler then prefers the networks' blocks over the rollouts')."""
+        pr = getattr(self, "eval_priority", None)
+        if pr is None or not torch.cuda.is_available():
+            return _nullctx()
+        st = self.__dict__.get("_hp_stream")
+        if st is None:
+            st = self._hp_stream = torch.cuda.Stream(priority=pr)
+            st.wait_stream(torch.cuda.current_stream())
+            self.evaluator.priority = pr
+        return torch.cuda.stream(st)
 
     def get_move(self, state):
         s = self.search(state)

@@ -240,6 +240,7 @@ def study(worlds=(2, 4, 8), per_rank=128, batch=16, n_positions=50, size=9, trut
     if shipped:
         batch = shipped_waves(per_rank, 1)[0]
     top = ladder_top or per_rank * max(worlds)
+    truth_budget = per_rank * max(worlds) * truth_mult  # (not scaled by a longer ladder)
     # the single trees (truth and ladder) depend only on these: cached across studies that vary
     # the N-rank search alone (e.g. its rollout delay)
     # (keyed by every setting of those trees — search parameters, networks, positions — and a
@@ -248,7 +249,7 @@ def study(worlds=(2, 4, 8), per_rank=128, batch=16, n_positions=50, size=9, trut
     import json
     key = json.dumps({"v": CACHE_VERSION, "search": _search_kw(batch, lmbda), "nets": NET_ARCH,
                       "n": n_positions, "size": size, "pos_seed": pos_seed,
-                      "net_seed": net_seed, "truth": top * truth_mult, "per_rank": per_rank},
+                      "net_seed": net_seed, "truth": truth_budget, "per_rank": per_rank},
                      sort_keys=True)
     ck = os.path.join(outdir, "single_%s.npz" % hashlib.sha1(key.encode()).hexdigest()[:16])
     cache = dict(np.load(ck)) if os.path.exists(ck) else {}
@@ -261,7 +262,7 @@ def study(worlds=(2, 4, 8), per_rank=128, batch=16, n_positions=50, size=9, trut
             np.savez(ck, **cache)
         return cache[key], cache[key + "_n"]
 
-    truth, truth_nodes = single(top * truth_mult, seed=99)
+    truth, truth_nodes = single(truth_budget, seed=99)
     cfg = {"size": size, "net_seed": net_seed, "pos_seed": pos_seed,
            "n_positions": n_positions, "batch": batch, "search_cls": search_cls,
            "lmbda": lmbda, "rollout_delay": rollout_delay, "depth": depth}
@@ -308,7 +309,7 @@ def study(worlds=(2, 4, 8), per_rank=128, batch=16, n_positions=50, size=9, trut
             "equivalent_single_tree_budget": round(teq, 1),
             "efficiency": round(teq / (per_rank * w), 3)}
     return {"positions": n_positions, "board": size, "per_rank_playouts": per_rank,
-            "wave": batch, "truth_budget": top * truth_mult, "search": search_cls,
+            "wave": batch, "truth_budget": truth_budget, "search": search_cls,
             "lmbda": lmbda, "rollout_delay": rollout_delay, "shipped_geometry": bool(shipped),
             "capped": bool(capped), "metric": metric, "ladder": ladder or "single trees",
             "truth_nodes": float(truth_nodes.mean()), "rows": rows}

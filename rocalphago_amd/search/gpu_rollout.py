@@ -105,11 +105,22 @@ class RolloutBatcher(object):
         g.pending = _Pending(ev, host, colors.shape[0], R)
 
 
+# moves per rollout launch (rag_rollouts' sliced mode: the games are parked in HBM between
+# launches, so no launch holds a CU for a whole playout); 0 = one launch per playout
+DEFAULT_SLICE = 64
+# torch stream priority of the rollout streams (larger = lower; 0 = default)
+DEFAULT_PRIORITY = 0
+
+
 class GpuRollouts(object):
-    def __init__(self, policy, device=None, nstreams=6, priority=0):
+    def __init__(self, policy, device=None, nstreams=6, priority=None, slice_moves=None):
         """nstreams: ring of rollout streams (hardware queues); priority: torch stream priority
-        (larger = lower; 0 = default)."""
+        (larger = lower; 0 = default); slice_moves: moves per launch (None: DEFAULT_SLICE, 0:
+        one launch per playout)."""
         self.device = torch.device(device or "cuda")
+        self.slice = DEFAULT_SLICE if slice_moves is None else int(slice_moves)
+        if priority is None:
+            priority = DEFAULT_PRIORITY
         self.streams = [torch.cuda.Stream(self.device, priority=priority)
                         for _ in range(max(1, nstreams))]
         self._next = 0
@@ -140,11 +151,17 @@ class GpuRollouts(object):
                 .to(self.device, non_blocking=True)
             m = torch.from_numpy(np.ascontiguousarray(meta, np.int32)).pin_memory() \
                 .to(self.device, non_blocking=True)
+            park, sl = None, 0
+            if self.slice > 0 and not dbg and limit > self.slice:
+                # the parked games (allocated on this stream: reused only after the launches)
+                park = torch.empty(games * int(_lib().rag_rollout_park_bytes(S)),
+                                   dtype=torch.uint8, device=self.device)
+                sl = self.slice
             _check(_lib().rag_rollouts(_ptr(c), _ptr(m), n, R, S, float(komi), int(limit),
                                        _ptr(self.w), _ptr(self.pattern),
                                        ctypes.c_uint(seed & 0xFFFFFFFF), _ptr(winners),
                                        _ptr(lengths), _ptr(logits),
-                                       ctypes.c_void_p(stream.cuda_stream)),
+                                       ctypes.c_void_p(stream.cuda_stream), _ptr(park), sl),
                    "rollouts")
             host = torch.empty(games, dtype=torch.int8, pin_memory=True)
             host.copy_(winners, non_blocking=True)

@@ -395,3 +395,57 @@ def test_search_channel_slots_and_attach(tmp_path, kind):
     assert b.wait_request(1, 2, 0, 0, 1000) == 2 and b.cmd()[1:] == (rg.CHAN_CMD_STOP, 7)
     b.abort("test")
     assert a.aborted and "test" in a.why
+
+
+def _gpu_dist_worker(rank, world, port, outdir):
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), RAG_DIST_BACKEND="gloo")
+    import torch
+    from rocalphago_amd.engine.gamestate import GameState
+    from rocalphago_amd.models.policy import CNNPolicy
+    from rocalphago_amd.models.value import CNNValue
+    from rocalphago_amd.parallel.dp import DPContext
+    from rocalphago_amd.search.distributed import DistributedMCTS
+    dev = torch.device("cuda", 0)  # both ranks on the box's one GPU
+    dp = DPContext(device=dev)
+    pol = CNNPolicy(DEFAULT_FEATURES, board=19, filters_per_layer=64, layers=4, device=dev,
+                    seed=1)
+    val = CNNValue(list(DEFAULT_FEATURES) + ["color"], board=19, filters_per_layer=64,
+                   layers=4, device=dev, seed=2)
+    mc = DistributedMCTS(pol, val, dp=dp, lmbda=0.5, n_playout=2048, batch=128, nthreads=4,
+                         depth=2, master_share=0.5)
+    st = GameState()
+    moves = []
+    for _ in range(2):
+        mv = mc.get_move(st)
+        moves.append(-1 if mv is None else mv[0] * 19 + mv[1])
+        st.do_move(mv)
+        mc.update_with_move(mv)
+    np.save(os.path.join(outdir, "gmv%d.npy" % rank), np.array(moves))
+    if rank == 0:
+        np.save(os.path.join(outdir, "gcnt.npy"), mc.leaf_counts())
+        np.save(os.path.join(outdir, "gsims.npy"), np.array([mc.stats["sims"],
+                                                              mc._search.rollouts]))
+    dp.shutdown()
+
+
+@__import__("pytest").mark.gpu
+def test_distributed_search_two_ranks_gpu(tmp_path):
+    """The multi-GPU search with two processes on the GPU box (both ranks on its one GPU, gloo
+    for the set-up): rank 0's native master loop and both ranks' serving loops (GPU features,
+    both networks, GPU rollouts) over the shared-memory channel; the ranks play the same moves,
+    both evaluate leaves, every simulation's rollout is backed up."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.spawn(_gpu_dist_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    assert np.array_equal(np.load(tmp_path / "gmv0.npy"), np.load(tmp_path / "gmv1.npy"))
+    c = np.load(tmp_path / "gcnt.npy")
+    sims, rollouts = np.load(tmp_path / "gsims.npy")
+    assert c[0] > 0 and c[1] > 0, c
+    assert c.sum() == sims >= 2 * 2048 - 2
+    assert rollouts == sims

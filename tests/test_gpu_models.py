@@ -317,3 +317,51 @@ def test_value_batch_kernel_and_trainer_step(cuda):
         losses.append(tr.pop_loss())
         assert float((val.model.net.flat - w0).abs().max()) > 0
     assert np.isfinite(losses[0]) and losses[0] == losses[1]
+
+
+@pytest.mark.parametrize("arch", ["policy", "resnet"])
+def test_sgd_folded_into_weight_repack_is_bit_exact(cuda, arch):
+    """The optimizer step folded into the trunk's weight repack (pack_trunk / wino_pack read
+    each fp32 master and its gradient once, write back w - lr g and pack it; the rest of the
+    flat buffer by the plain SGD kernel) gives bit for bit the weights of sgd_kernel + a separate
+    repack, over several steps, and the next forward uses the stepped weights (ResNet: to the
+    run-to-run reproducibility of its BN statistics' atomics)."""
+    import torch
+    from rocalphago_amd.features.preprocessing import DEFAULT_FEATURES
+    from rocalphago_amd.models import kerasish as KZ
+    from rocalphago_amd.models.policy import ResnetPolicy
+    rs = np.random.RandomState(4)
+    B = 256
+    X = (rs.rand(B, 48, 19, 19) > 0.6).astype(np.uint8)
+    Y = np.zeros((B, 361), np.float32)
+    Y[np.arange(B), rs.randint(0, 361, B)] = 1
+    out = []
+    for fold in (True, False):
+        if arch == "policy":
+            pol = CNNPolicy(DEFAULT_FEATURES, board=19, filters_per_layer=192, layers=4,
+                            device=cuda, seed=9)
+        else:
+            pol = ResnetPolicy(DEFAULT_FEATURES, board=19, filters_per_layer=128, layers=5,
+                               device=cuda, seed=9)
+        m = pol.model
+        m.compile(loss="categorical_crossentropy", optimizer=KZ.SGD(lr=0.05))
+        plan = m._plan_for()
+        assert plan is not None
+        if not fold:
+            m.net._sgd_fold = None
+        steps = 3 if arch == "policy" else 1
+        losses = [m.train_on_batch(X, Y) for _ in range(steps)]
+        torch.cuda.synchronize()
+        assert getattr(plan, "folded_steps", 0) == (steps if fold else 0)
+        out.append((m.net.flat.clone(), losses, pol.forward(X[:8])))
+    (fa, la, pa), (fb, lb, pb) = out
+    if arch == "policy":
+        assert torch.equal(fa, fb)
+        assert la == lb
+        assert np.array_equal(pa, pb)
+    else:  # the BN statistics' atomics make ResNet steps not bit-reproducible run to run
+        # (two plain runs differ by up to ~5e-8 after one step: scripts/dbg/sgd_fold_dbg.py)
+        assert (fa - fb).abs().max().item() < 1e-6
+        assert np.allclose(la, lb, rtol=1e-5)
+        # (a ~5e-8 weight difference may flip a bf16 rounding of a packed weight)
+        assert np.allclose(pa, pb, rtol=1e-2, atol=1e-6)

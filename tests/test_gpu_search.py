@@ -94,6 +94,23 @@ def test_rollouts_bit_exact_vs_recorded_run():
     assert np.array_equal(ref["lg"], lg)
 
 
+@pytest.mark.parametrize("size,slice_moves", [(19, 64), (19, 7), (9, 16)])
+def test_sliced_rollouts_equal_one_launch(size, slice_moves):
+    """Sliced playouts (the games parked in HBM between launches of at most ``slice_moves``
+    moves) play exactly the games of one launch per playout: same winners, same lengths."""
+    from rocalphago_amd.search.gpu_rollout import GpuRollouts
+    rp = rg.RolloutPolicy()
+    rp.pattern = np.random.RandomState(2).randn(rg.ROLLOUT_PATTERNS).astype(np.float32) * 0.3
+    sts = _random_positions(40, size, 5 + size)
+    one = GpuRollouts(rp, torch.device("cuda"), slice_moves=0)
+    sl = GpuRollouts(rp, torch.device("cuda"), slice_moves=slice_moves)
+    w0, l0 = one.run(sts, R=3, limit=500, seed=77)
+    w1, l1 = sl.run(sts, R=3, limit=500, seed=77)
+    assert np.array_equal(w0, w1)
+    assert np.array_equal(l0, l1)
+    assert l0.max() > slice_moves  # the games did span several launches
+
+
 def test_gpu_rollouts_in_search_find_capture(gro):
     from rocalphago_amd.search.apv import ParallelMCTS
     import sys

@@ -147,8 +147,8 @@ def test_wino_dgrad_carries_deferred_wgrad_reduction_twice(ops):
 def test_trunk_large_batch_dgrad_on_winograd(ops):
     """HipTrunk runs the dgrad of its Winograd layers on the Winograd kernel at batches of two or
     more block waves (wino_dgrad_min_batch; the deferred wgrad reduction then costs a few us in
-    its last wave) with the Winograd dgrad weights packed on first use: the same gradients as the
-    direct dgrad."""
+    its last wave) with the Winograd dgrad weights packed on first use: its gradients match an
+    fp32 CPU train step of the same network and batch (and so does the direct dgrad's)."""
     import numpy as np
     from rocalphago_amd.features.preprocessing import DEFAULT_FEATURES
     from rocalphago_amd.models import kerasish as KZ
@@ -169,6 +169,17 @@ def test_trunk_large_batch_dgrad_on_winograd(ops):
         torch.cuda.synchronize()
         assert (trunk._ub_version is not None) == (min_batch == 512)
         grads.append(torch.cat([g.detach().reshape(-1).float() for g in pol.model.net._gviews]))
-    a, b = grads
-    cos = torch.dot(a, b).item() / (a.norm().item() * b.norm().item())
-    assert cos > 0.999, cos
+    ref = CNNPolicy(DEFAULT_FEATURES, board=19, filters_per_layer=192, layers=4, device="cpu",
+                    seed=5)
+    ref.model.compile(loss="categorical_crossentropy", optimizer=KZ.SGD(lr=0.0))
+    ref.model.train_on_batch(X, Y)
+    r = torch.cat([g.detach().reshape(-1).float() for g in ref.model.net._gviews])
+    cos = []
+    for g in grads:  # Winograd dgrad, direct dgrad
+        g = g.cpu()
+        cos.append(torch.dot(g, r).item() / (g.norm().item() * r.norm().item()))
+        assert abs(g.norm().item() / r.norm().item() - 1) < 2e-2
+    # bf16 operands through four layers put either at a cosine of ~0.996 to fp32; the Winograd
+    # roundings must not make it measurably worse than the direct kernel's
+    assert cos[0] > 0.99 and cos[1] > 0.99, cos
+    assert cos[0] >= cos[1] - 1e-3, cos
