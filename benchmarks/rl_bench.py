@@ -119,9 +119,13 @@ def main():
     ap.add_argument("--iterations", type=int, default=None)
     ap.add_argument("--game-batch", type=int, default=None)
     ap.add_argument("--selfplay", default="native", choices=["native", "python"])
+    ap.add_argument("--pipeline", type=int, default=None,
+                    help="native self-play: pipelined game groups (default 2)")
     args = ap.parse_args()
     from rocalphago_amd.training import reinforcement
     reinforcement.NATIVE_SELFPLAY = args.selfplay == "native"
+    if args.pipeline is not None:
+        reinforcement.SELFPLAY_PIPELINE = args.pipeline
     r = bench_ref7(args) if args.config == "ref7" else bench_19(args)
     sp = r.pop("self_play")
     r["selfplay"] = args.selfplay

@@ -76,10 +76,15 @@ def effective(args):
     """Efficiency of every (per-GPU wave, depth) at every N, then effective simulations/s =
     efficiency x min(N x one GPU's rate at that wave, the master's ceiling)."""
     from rocalphago_amd.search.efficiency import study
-    rates = None
+    rates = serving = None
     if args.gpu_rates:
         with open(args.gpu_rates) as f:
-            rates = {int(k): float(v) for k, v in json.load(f)["sims_per_s_by_wave"].items()}
+            js = json.load(f)
+        rates = {int(k): float(v) for k, v in js["sims_per_s_by_wave"].items()}
+        # one GPU serving the multi-GPU search at (wave, depth), where measured
+        serving = {(int(w), int(d)): float(v) for w, dv in js.get("serving_sims_per_s",
+                                                                  {}).items()
+                   for d, v in dv.items()}
     rows = []
     for w in args.gpu_waves:
         sw = max(1, int(round(w * args.per_rank / 8192.0)))  # the study's wave
@@ -95,8 +100,10 @@ def effective(args):
             for n in args.ranks:
                 row = dict(r["rows"]["DistributedMCTS_%d" % n])
                 row.update(gpu_wave=w, study_wave=sw)
-                if rates is not None and w in rates:
-                    rate = n * rates[w]
+                per_gpu = (serving or {}).get((w, d), (rates or {}).get(w))
+                if per_gpu is not None:
+                    row["per_gpu_sims_per_s"] = per_gpu
+                    rate = n * per_gpu
                     if args.master_ceiling:
                         rate = min(rate, args.master_ceiling)
                     row["modelled_sims_per_s"] = round(rate, 1)
@@ -118,7 +125,10 @@ def effective(args):
                       "per_rank_playouts": args.per_rank, "board": args.board,
                       "positions": args.positions, "lmbda": args.lmbda,
                       "rollout_delay": args.rollout_delay, "truth_mult": args.truth_mult,
-                      "gpu_rates": rates, "master_ceiling": args.master_ceiling,
+                      "gpu_rates": rates,
+                      "serving_rates": {"%d/%d" % k: v for k, v in (serving or {}).items()},
+                      "one_gpu_effective_sims_per_s": (rates or {}).get(512),
+                      "master_ceiling": args.master_ceiling,
                       "rows": rows, "best_by_ranks": best}, indent=1), flush=True)
 
 

@@ -36,6 +36,8 @@ from ..utils.go_util import flatten_idx
 # games kept native (training/selfplay.py) whenever both players support it; False: the
 # Python lock-step loop (benchmarks/rl_bench.py --selfplay python)
 NATIVE_SELFPLAY = True
+# pipelined game groups of the native self-play (training/selfplay.py NativeSelfPlay)
+SELFPLAY_PIPELINE = 2
 
 def _make_training_pair(st, mv, preprocessor):
     st_tensor = preprocessor.state_to_tensor(st)
@@ -117,7 +119,7 @@ def run_n_games(optimizer, learner, opponent, num_games, mock_states=[], mode="p
     from .selfplay import NativeSelfPlay
     if not mock_states and NATIVE_SELFPLAY and NativeSelfPlay.supported(learner, opponent):
         # games kept native, one GPU pass + one native call per ply (training/selfplay.py)
-        sp = NativeSelfPlay(learner, opponent)
+        sp = NativeSelfPlay(learner, opponent, pipeline=SELFPLAY_PIPELINE)
         feats, moves, learner_color, winners = sp.play(num_games, board_size)
         won = [int(w) == c for w, c in zip(winners, learner_color)]
         run_n_games.last_stats = sp.stats
