@@ -63,9 +63,12 @@ def measure(device, playouts=8192, warmup=512, moves=1, **kw):
 
 
 # The N-GPU search's geometry (leaves per GPU wave, waves per GPU awaiting values, rank 0's share
-# of a wave), chosen by effective throughput = sims/s x budget efficiency
-# (benchmarks/search_efficiency.py --effective, profiles/search_efficiency_r6.json).
-DIST_GEOMETRY = {"batch": 512, "depth": 2, "master_share": 1.0}
+# of a wave), chosen by effective throughput = one GPU's serving rate x N (capped by rank 0's
+# host ceiling) x budget efficiency (benchmarks/search_efficiency.py --effective,
+# profiles/search_efficiency_r6.json). The leaves in flight grow with N x wave, so the wave
+# shrinks as N grows: 512 / N leaves per GPU, at least 128 (argmax at N = 4 and 8, within 2 % of
+# it at N = 2 where 256 keeps efficiency 0.98 against 0.85 at 512).
+DIST_GEOMETRY = {"batch": 512, "min_batch": 128, "depth": 2, "master_share": 1.0}
 
 
 def distributed_wave(world, mode="master"):
@@ -73,7 +76,7 @@ def distributed_wave(world, mode="master"):
     search, 512)."""
     if mode != "master" or world <= 1:
         return 512
-    return DIST_GEOMETRY["batch"]
+    return max(DIST_GEOMETRY["min_batch"], DIST_GEOMETRY["batch"] // world)
 
 
 def measure_distributed(dp, device, playouts=8192, warmup=512, moves=1, filters=192,

@@ -15,7 +15,7 @@ from rocalphago_amd.search.gpu_rollout import GpuRollouts
 
 def run(games, R, no_pattern=False):
     rg = engine()
-    g = GpuRollouts(rg.RolloutPolicy(), torch.device("cuda"))
+    g = GpuRollouts(rg.RolloutPolicy(), torch.device("cuda"), slice_moves=0)  # alone on the GPU
     if no_pattern:
         g.pattern = None
     st = [GameState() for _ in range(games // R)]

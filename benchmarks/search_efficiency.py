@@ -53,6 +53,12 @@ def main():
                     help="--effective: JSON {wave: one GPU's sims/s} measured on MI355X")
     ap.add_argument("--master-ceiling", type=float, default=None,
                     help="--effective: rank 0's host ceiling, sims/s (mcts_null_bench)")
+    ap.add_argument("--master-ceilings", default=None,
+                    help="--effective: per-wave ceilings 'WAVE:SIMS_PER_S,...' (override "
+                         "--master-ceiling for those waves)")
+    ap.add_argument("--from-rows", default=None,
+                    help="--effective: take the efficiency rows from this earlier output and "
+                         "only recompute the modelled / effective rates")
     args = ap.parse_args()
     if args.effective:
         effective(args)
@@ -85,8 +91,34 @@ def effective(args):
         serving = {(int(w), int(d)): float(v) for w, dv in js.get("serving_sims_per_s",
                                                                   {}).items()
                    for d, v in dv.items()}
+    ceilings = {}
+    for item in (args.master_ceilings or "").split(","):
+        if item:
+            w, v = item.split(":")
+            ceilings[int(w)] = float(v)
+
+    def model(row):
+        w, d, n = row["gpu_wave"], row["depth"], row["ranks"]
+        per_gpu = (serving or {}).get((w, d), (rates or {}).get(w))
+        if per_gpu is None:
+            return row
+        row["per_gpu_sims_per_s"] = per_gpu
+        rate = n * per_gpu
+        cap = ceilings.get(w, args.master_ceiling)
+        if cap:
+            row["master_ceiling"] = cap
+            rate = min(rate, cap)
+        row["modelled_sims_per_s"] = round(rate, 1)
+        row["effective_sims_per_s"] = round(rate * row["efficiency"], 1)
+        return row
+
     rows = []
-    for w in args.gpu_waves:
+    if args.from_rows:
+        with open(args.from_rows) as f:
+            txt = f.read()
+        prev = json.loads(txt[txt.index("{\n"):] if "{\n" in txt else txt)
+        rows = [model(dict(r)) for r in prev["rows"]]
+    for w in ([] if args.from_rows else args.gpu_waves):
         sw = max(1, int(round(w * args.per_rank / 8192.0)))  # the study's wave
         for d in args.depths:
             r = study(worlds=tuple(args.ranks), per_rank=args.per_rank,
@@ -100,15 +132,7 @@ def effective(args):
             for n in args.ranks:
                 row = dict(r["rows"]["DistributedMCTS_%d" % n])
                 row.update(gpu_wave=w, study_wave=sw)
-                per_gpu = (serving or {}).get((w, d), (rates or {}).get(w))
-                if per_gpu is not None:
-                    row["per_gpu_sims_per_s"] = per_gpu
-                    rate = n * per_gpu
-                    if args.master_ceiling:
-                        rate = min(rate, args.master_ceiling)
-                    row["modelled_sims_per_s"] = round(rate, 1)
-                    row["effective_sims_per_s"] = round(rate * row["efficiency"], 1)
-                rows.append(row)
+                rows.append(model(row))
                 print(json.dumps(row), file=sys.stderr, flush=True)
     best = {}
     for row in rows:
@@ -129,6 +153,7 @@ def effective(args):
                       "serving_rates": {"%d/%d" % k: v for k, v in (serving or {}).items()},
                       "one_gpu_effective_sims_per_s": (rates or {}).get(512),
                       "master_ceiling": args.master_ceiling,
+                      "master_ceilings_by_wave": ceilings,
                       "rows": rows, "best_by_ranks": best}, indent=1), flush=True)
 
 

@@ -77,12 +77,12 @@ def _search_kw(batch, lmbda=0.0):
                 rollout_limit=200)
 
 
-def shipped_waves(per_rank, world, bench_budget=8192, bench_wave=512, bench_min=64, cap=False):
+def shipped_waves(per_rank, world, bench_budget=8192, bench_wave=512, bench_min=128, cap=False):
     """(single-tree wave, per-rank wave at N = world) of the bench's geometry scaled to a study
     budget: the bench searches 8192 playouts per GPU per move with 512-leaf waves on one GPU and
-    max(128, 512 / N) leaves per rank and round on N GPUs (benchmarks/mcts_bench.py
-    distributed_wave: max(64, 512 / N) since round 5, 128 before); the study keeps the same
-    leaves-in-flight to budget ratios."""
+    max(128, 512 / N) leaves per GPU wave on N GPUs (benchmarks/mcts_bench.py distributed_wave,
+    round 6; max(64, 512 / N) in round 5); the study keeps the same leaves-in-flight to budget
+    ratios."""
     w1 = max(1, int(round(per_rank * bench_wave / bench_budget)))
     wmin = max(1, int(round(per_rank * bench_min / bench_budget)))
     if cap:  # the round's leaves capped at the one-GPU wave (no per-GPU minimum)

@@ -291,17 +291,20 @@ def test_search_budget_efficiency_two_ranks(tmp_path):
 
 
 def test_search_budget_efficiency_shipped_geometry_two_ranks(tmp_path):
-    """the one-tree 2-rank search at the geometry the bench ships (lambda 0.5
-    with rollouts seeded by the leaf position, rollout results returned as soon as done with
-    rollout_delay 6 as the cap, per-rank waves scaled from the 19x19 bench) is worth two ranks:
-    budget efficiency >= 0.85 against a truth of 8x the largest budget (deterministic; the full
-    48-position study is profiles/search_efficiency_r5.json: 0.95 / 0.86 / 0.81 at N = 2 / 4 /
-    8)."""
-    from rocalphago_amd.search.efficiency import study
+    """the one-tree 2-rank search at the geometry the bench ships at N = 2
+    (benchmarks/mcts_bench.py DIST_GEOMETRY: 256-leaf waves per GPU, 2 waves per GPU awaiting
+    values; lambda 0.5 with rollouts seeded by the leaf position, returned within 6 waves; waves
+    scaled from the 19x19 bench to the study's budget) is worth two GPUs: budget efficiency
+    >= 0.85 against ONE GPU at the single-GPU bench geometry (512-leaf waves, 3 awaiting values)
+    searching twice as long, Jensen-Shannon distance to a truth of 8x the budget (deterministic;
+    the 48-position sweep over waves and N is profiles/search_efficiency_r6.json: 0.98 here)."""
+    from rocalphago_amd.search.efficiency import shipped_waves, study
     r = study(worlds=(2,), per_rank=256, n_positions=16, truth_mult=8,
               search_cls="DistributedMCTS", outdir=str(tmp_path), lmbda=0.5, rollout_delay=6,
-              shipped=True)
+              shipped=True, depth=2, wave=shipped_waves(256, 2)[1], metric="js",
+              ladder={"depth": 3, "rollout_delay": 6})
     row = r["rows"]["DistributedMCTS_2"]
+    assert row["wave_per_rank"] == 8  # 256 of the bench's 8192 playouts per GPU, scaled
     assert row["duplication"] == 1.0
     assert row["efficiency"] >= 0.85, r["rows"]
 
