@@ -105,10 +105,12 @@ struct SgdFold {
   long goff;
   float lr, wd;
   int on;
+  // the update itself (sgd_kernel's arithmetic, so a fold is bit-exact against it)
+  __device__ __forceinline__ float update(float v, float g) const { return v - lr * (g + wd * v); }
   __device__ __forceinline__ float step(float* w) const {
     const float v = *w;
     if (!on) return v;
-    const float u = v - lr * (w[goff] + wd * v);
+    const float u = update(v, w[goff]);
     *w = u;
     return u;
   }

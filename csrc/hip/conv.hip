@@ -1154,11 +1154,32 @@ __global__ void __launch_bounds__(256) pack_trunk_kernel(const int64_t* __restri
   const int nt = g / ntc;
   __shared__ float tl[64][65];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-#pragma unroll 4
+  // all loads of the 16 rows before any store (a per-row load-step-store waits on the stores)
+  float wv[16], wg[16];
+  const float* Wc = W;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int n = nt * 64 + ty + 4 * i, c = ct * 64 + tx;
+    const bool in = n < COUT && c < CIN;
+    const size_t o = in ? (size_t)(n * CIN + c) * taps + tap : 0;
+    wv[i] = in ? Wc[o] : 0.f;
+    wg[i] = (in && sgd.on) ? Wc[o + sgd.goff] : 0.f;
+  }
+  if (sgd.on) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int n = nt * 64 + ty + 4 * i, c = ct * 64 + tx;
+      if (n < COUT && c < CIN) {
+        wv[i] = sgd.update(wv[i], wg[i]);
+        W[(size_t)(n * CIN + c) * taps + tap] = wv[i];
+      }
+    }
+  }
+#pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int nl = ty + 4 * i;
     const int n = nt * 64 + nl, c = ct * 64 + tx;
-    const float v = (n < COUT && c < CIN) ? sgd.step(W + (n * CIN + c) * taps + tap) : 0.f;
+    const float v = wv[i];
     tl[nl][tx] = v;
     if (Wf && n < COUTP && c < CINP) Wf[(tap * COUTP + n) * CINP + c] = (bf16)v;
   }

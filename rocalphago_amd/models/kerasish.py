@@ -479,7 +479,10 @@ class KerasNet(torch.nn.Module):
 
 class SGD(object):
     """Keras-1 SGD: lr_t = lr / (1 + decay * iterations); momentum / nesterov optional.
-    ``lr`` is a plain float attribute and may be reassigned (the RL trainer flips its sign)."""
+    ``lr`` is a plain float attribute and may be reassigned (the RL trainer flips its sign).
+    FOLD: on the GPU without momentum, step the fused trunk's weights inside their repack
+    (fused.sgd_fold) instead of in a separate pass (False: the A/B, scripts/dbg/fold_ab.py)."""
+    FOLD = True
 
     def __init__(self, lr=0.01, momentum=0.0, decay=0.0, nesterov=False, **kw):
         self.lr = lr
@@ -506,7 +509,8 @@ class SGD(object):
         if self.momentum and self._velocity is None:
             self._velocity = torch.zeros_like(net.flat)
         fold = getattr(net, "_sgd_fold", None)
-        if net.flat.is_cuda and not self.momentum and fold is not None and fold(lr):
+        if net.flat.is_cuda and not self.momentum and self.FOLD and fold is not None and \
+                fold(lr):
             pass  # the trunk's step rode in its weight repack (fused.sgd_fold)
         elif net.flat.is_cuda:
             from ..ops import hipops as ops
