@@ -1107,11 +1107,15 @@ RAG_API int rag_pack_weights(const float* W, void* Wf, void* Wb, int COUT, int C
 // bias_out (or 0), first element index; elements of a layer = taps*COUTP*CINP + COUTP.
 namespace {
 constexpr int kPackFields = 11;
-// Block = one 64 (n) x 64 (c) tile of one tap of one layer (blockIdx.y = layer; blocks past a
-// layer's tile count exit). The tile goes through LDS so that both bf16 layouts are written
-// coalesced: the forward layout [tap][n][c] along c, the dgrad layout [tap'][c][n] along n. The
-// element-per-thread version wrote the dgrad layout 2 bytes per 384-byte stride (29 us/step); one
-// block per all-tap 32x32 tile (contiguous OIHW runs through LDS) measured 29-47 us: kept this.
+// Block = 16 (n) x 16 (c) tiles of one layer (blockIdx.y = layer), all its taps, grid-strided
+// over the layer's tiles. A tile's OIHW masters are 16 runs of 16 * taps contiguous floats, read
+// (and with the SGD fold stepped and written back) coalesced, every load before any store; they
+// go through LDS so that both bf16 layouts are written along their contiguous dimension: the
+// forward layout [tap][n][c] along c, the dgrad layout [tap'][c][n] along n. (Until round 6: one
+// block per tap of a 64 x 64 tile, whose lanes read 1 of every taps floats: 15-17 us per SL step
+// for the 5x5 layer alone, and scattered 4-byte master writes from 25 blocks per cache line
+// with the fold.)
+constexpr int kPT = 16, kPTaps = 25;  // tile edge; taps of the largest kernel (5x5)
 __global__ void __launch_bounds__(256) pack_trunk_kernel(const int64_t* __restrict__ table,
                                                          int nrows, int nfull, SgdFold sgd) {
   // the padded bias of a layer (its fp32 master stepped first with sgd.on)
@@ -1136,63 +1140,61 @@ __global__ void __launch_bounds__(256) pack_trunk_kernel(const int64_t* __restri
   bf16* Wf = (bf16*)t[7];
   bf16* Wb = (bf16*)t[8];
   float* bo = (float*)t[9];
+  if (blockIdx.x == 0) pack_bias(b, COUT, COUTP, bo);
+  if (!Wf && !Wb) return;  // bias-only row (a Winograd layer: rag_wino_pack packs its weights)
   const int taps = KS * KS;
-  const int ntn = (COUTP + 63) / 64, ntc = (CINP + 63) / 64;
-  // XCD-grouped order (the grid width is a multiple of 8, so block x runs on XCD x % 8): the
-  // taps of one 64 x 64 (n, c) tile are blocks x, x + 8, x + 16, ... of one XCD. A tap's OIHW
-  // reads stride 9 (25) floats, so each block pulls the cache lines of all its tile's taps; with
-  // the taps on one XCD they come from its L2 instead of once per XCD.
-  const int x = blockIdx.x, xcd = x & 7, j = x >> 3;
-  const int g = (j / taps) * 8 + xcd;  // (n, c) tile
-  const int tap = j % taps;
-  if (g >= ntn * ntc) return;
-  if (!Wf && !Wb) {  // bias-only row (a Winograd layer: its weights come from rag_wino_pack)
-    if (g == 0 && tap == 0) pack_bias(b, COUT, COUTP, bo);
-    return;
-  }
-  const int ct = g % ntc;
-  const int nt = g / ntc;
-  __shared__ float tl[64][65];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  // all loads of the 16 rows before any store (a per-row load-step-store waits on the stores)
-  float wv[16], wg[16];
-  const float* Wc = W;
+  if (taps > kPTaps) return;  // (the host never builds such a row)
+  const int ntc = (CINP + kPT - 1) / kPT, ntiles = ((COUTP + kPT - 1) / kPT) * ntc;
+  const int row = kPT * taps;  // contiguous masters per output channel of a tile
+  __shared__ float tl[kPTaps * kPT * (kPT + 1)];  // [tap][n][c]
+  const int tid = threadIdx.x;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int n0 = (tile / ntc) * kPT, c0 = (tile % ntc) * kPT;
+    float v[kPTaps], gr[kPTaps];  // element tid + 256 i of the tile: i < taps
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int n = nt * 64 + ty + 4 * i, c = ct * 64 + tx;
-    const bool in = n < COUT && c < CIN;
-    const size_t o = in ? (size_t)(n * CIN + c) * taps + tap : 0;
-    wv[i] = in ? Wc[o] : 0.f;
-    wg[i] = (in && sgd.on) ? Wc[o + sgd.goff] : 0.f;
-  }
-  if (sgd.on) {
+    for (int i = 0; i < kPTaps; ++i) {
+      const int idx = tid + 256 * i, r = idx / row, e = idx - r * row;
+      const int n = n0 + r, c = c0 + e / taps;
+      const bool in = i < taps && n < COUT && c < CIN;
+      const size_t o = in ? (size_t)(n * CIN + c0) * taps + e : 0;
+      v[i] = in ? W[o] : 0.f;
+      gr[i] = (in && sgd.on) ? W[o + sgd.goff] : 0.f;
+    }
+    if (sgd.on) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int n = nt * 64 + ty + 4 * i, c = ct * 64 + tx;
-      if (n < COUT && c < CIN) {
-        wv[i] = sgd.update(wv[i], wg[i]);
-        W[(size_t)(n * CIN + c) * taps + tap] = wv[i];
+      for (int i = 0; i < kPTaps; ++i) {
+        const int idx = tid + 256 * i, r = idx / row, e = idx - r * row;
+        const int n = n0 + r, c = c0 + e / taps;
+        if (i < taps && n < COUT && c < CIN) {
+          v[i] = sgd.update(v[i], gr[i]);
+          W[(size_t)(n * CIN + c0) * taps + e] = v[i];
+        }
       }
     }
-  }
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int nl = ty + 4 * i;
-    const int n = nt * 64 + nl, c = ct * 64 + tx;
-    const float v = wv[i];
-    tl[nl][tx] = v;
-    if (Wf && n < COUTP && c < CINP) Wf[(tap * COUTP + n) * CINP + c] = (bf16)v;
-  }
-  if (Wb) {
-    __syncthreads();
-#pragma unroll 4
-    for (int i = 0; i < 16; ++i) {
-      const int cl = ty + 4 * i;
-      const int c = ct * 64 + cl, n = nt * 64 + tx;
-      if (c < CINP && n < COUTP) Wb[((taps - 1 - tap) * CINP + c) * COUTP + n] = (bf16)tl[tx][cl];
+    for (int i = 0; i < kPTaps; ++i) {
+      if (i >= taps) break;
+      const int idx = tid + 256 * i, r = idx / row, e = idx - r * row;
+      const int cl = e / taps, tap = e - cl * taps;
+      tl[(tap * kPT + r) * (kPT + 1) + cl] = v[i];
     }
+    __syncthreads();
+    for (int it = tid; it < taps * kPT * kPT; it += 256) {
+      const int tap = it / (kPT * kPT), q = it - tap * kPT * kPT;
+      if (Wf) {  // c fastest
+        const int cl = q % kPT, r = q / kPT, n = n0 + r, c = c0 + cl;
+        if (n < COUTP && c < CINP)
+          Wf[((size_t)tap * COUTP + n) * CINP + c] = (bf16)tl[(tap * kPT + r) * (kPT + 1) + cl];
+      }
+      if (Wb) {  // n fastest
+        const int r = q % kPT, cl = q / kPT, n = n0 + r, c = c0 + cl;
+        if (n < COUTP && c < CINP)
+          Wb[((size_t)(taps - 1 - tap) * CINP + c) * COUTP + n] =
+              (bf16)tl[(tap * kPT + r) * (kPT + 1) + cl];
+      }
+    }
+    __syncthreads();  // tl is reused by the next tile
   }
-  if (g == 0 && tap == 0) pack_bias(b, COUT, COUTP, bo);
 }
 }  // namespace
 
@@ -1200,7 +1202,7 @@ __global__ void __launch_bounds__(256) pack_trunk_kernel(const int64_t* __restri
 // folded into the packing (each master element is stepped by exactly one thread)
 RAG_API int rag_pack_trunk(const int64_t* table, int nrows, int nfull, int64_t total,
                            hipStream_t stream, int64_t goff, float lr, float wd, int sgd_on) {
-  // total: the grid width, max over layers of 8 * taps * ceil(64x64 tiles / 8) (XCD-grouped order).
+  // total: the grid width (blocks per layer row; each grid-strides over its layer's 16x16 tiles).
   // Rows [0, nfull) pack weights (one grid row each); rows [nfull, nrows) only pad their bias
   // (Winograd layers: rag_wino_pack packs the weights) and share one grid row: the 11 bias-only
   // rows of the SL trunk were 11 x 200 blocks that exited at once.

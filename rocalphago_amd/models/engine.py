@@ -37,11 +37,9 @@ class ConvSpec(object):
 
 
 def pack_grid_width(specs):
-    """Grid width of conv.hip's pack_trunk_kernel (XCD-grouped order: block x runs tap
-    (x / 8) % taps of 64x64 tile ((x / 8) / taps) * 8 + x % 8): 8 x taps x ceil(tiles / 8) of
-    the widest layer, a multiple of 8."""
-    return max(8 * s.ks * s.ks * -(-((-(-s.coutp // 64)) * (-(-s.cinp // 64))) // 8)
-               for s in specs)
+    """Grid width of conv.hip's pack_trunk_kernel: the 16x16 (n, c) all-tap tiles of the widest
+    layer, rounded up to a multiple of 8 (each block grid-strides over its layer's tiles)."""
+    return max(8 * -(-((-(-s.coutp // 16)) * (-(-s.cinp // 16))) // 8) for s in specs)
 
 
 class _PackedConvs(object):

@@ -441,7 +441,7 @@ def test_deferred_reductions_of_two_trunks_interleave_on_one_stream(ops):
 
 @pytest.mark.gpu
 def test_trunk_repack_matches_per_layer_packer(ops):
-    """pack_trunk (one launch, 64x64 tap tiles through LDS) equals pack_weights per layer for
+    """pack_trunk (one launch, 16x16 all-tap tiles through LDS) equals pack_weights per layer for
     both bf16 GEMM layouts and the padded biases: a 5x5 48->192 layer, odd widths, 3x3 layers."""
     from rocalphago_amd.models.engine import ConvSpec, HipTrunk
     dev = torch.device("cuda")
