@@ -18,7 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def build_search(device, filters=192, layers=12, batch=512, rollout_device="gpu",
                  rollouts_per_leaf=1, lmbda=0.5, nthreads=16, seed=1, pipeline=3,
-                 max_inflight=8, rollout_group=6):
+                 max_inflight=8, rollout_group=8):
     from rocalphago_amd.features.preprocessing import DEFAULT_FEATURES
     from rocalphago_amd.models.policy import CNNPolicy
     from rocalphago_amd.models.value import CNNValue
@@ -224,7 +224,7 @@ def main():
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--pipeline", type=int, default=3, help="waves in flight (1 = serial)")
     ap.add_argument("--max-inflight", type=int, default=8, help="rollout waves in flight")
-    ap.add_argument("--rollout-group", type=int, default=6, help="waves per rollout launch")
+    ap.add_argument("--rollout-group", type=int, default=8, help="waves per rollout launch")
     ap.add_argument("--moves", type=int, default=1)
     ap.add_argument("--eval-priority", type=int, default=None,
                     help="stream priority of the wave passes (e.g. -1: above the rollouts)")

@@ -474,7 +474,7 @@ class ParallelMCTS(object):
                  n_playout=1600, batch=512, virtual_loss=3, rollout_limit=500,
                  playout_depth=722, nthreads=8, rollout_device="cpu", rollouts_per_leaf=1,
                  seed=1, evaluator=None, max_inflight=8, pipeline=3, dp=None,
-                 rollout_group=6):
+                 rollout_group=8):
         # dp (parallel/dp.DPContext, world > 1): root parallelism over ranks — every rank
         # searches the same position with its own seed on its own GPU, and get_move() sums the
         # root visit counts over ranks (one all-reduce of S*S+1 counts), so all
@@ -503,7 +503,11 @@ class ParallelMCTS(object):
         self._inflight = []
         self.max_inflight = max_inflight
         # GPU rollouts of `rollout_group` consecutive waves go out as one launch
-        # (gpu_rollout.RolloutBatcher); up to `max_inflight` waves' rollouts are in flight
+        # (gpu_rollout.RolloutBatcher); up to `max_inflight` waves' rollouts are in flight.
+        # 8 / 8: a group's results come back when the next group's first wave is selected (at
+        # most 8 waves, 4.5 on average, later); 6 / 8 returned them 3-8 waves later and left the
+        # host waiting on a group launched 3 waves earlier: 128.5-130.3k against 137.1-138.9k
+        # sims/s on one box (profiles/mcts_rollout_group_r6.txt)
         self.rollout_group = int(rollout_group)
         # leaves packed natively into pinned slots and evaluated in one GPU pass per wave when
         # the evaluator supports it (NetworkEvaluator.wave_capable); False: board objects

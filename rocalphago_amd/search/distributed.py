@@ -139,6 +139,10 @@ class DistributedMCTS(ParallelMCTS):
                  rollout_slots=None, master_share=1.0, rollout_delay=0, max_path=127,
                  board=None, stall_s=120.0, force_master=False, worker_threads=None, **kw):
         kw.setdefault("pipeline", 3)
+        # GPU rollout launches of 6 waves per serving GPU: the geometry its serving rates and the
+        # effective-throughput table were measured at (profiles/mcts_wave_rates_r6.json); the
+        # single-GPU search launches 8 (ParallelMCTS)
+        kw.setdefault("rollout_group", 6)
         super(DistributedMCTS, self).__init__(policy, value, rollout, dp=None, **kw)
         self.ddp = dp
         # host threads of this rank's leaf builder (path replay, input packing, ladder reads);
