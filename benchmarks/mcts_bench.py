@@ -81,7 +81,8 @@ def distributed_wave(world, mode="master"):
 
 def measure_distributed(dp, device, playouts=8192, warmup=512, moves=1, filters=192,
                         layers=12, batch=512, rollouts_per_leaf=1, lmbda=0.5, nthreads=16,
-                        seed=1, mode="master", depth=None, master_share=None):
+                        seed=1, mode="master", depth=None, master_share=None,
+                        rollout_group=None):
     """Search over all ranks (search/distributed.py). mode "master" (default): one tree on rank 0
     with leaf waves served by every rank through the shared-memory channel (DistributedMCTS);
     "shared": every rank runs the pipelined single-GPU search with shared root statistics
@@ -102,9 +103,10 @@ def measure_distributed(dp, device, playouts=8192, warmup=512, moves=1, filters=
                     device=device, seed=seed)
     val = CNNValue(DEFAULT_FEATURES + ["color"], board=19, filters_per_layer=filters,
                    layers=layers, device=device, seed=seed + 1)
+    kw = {} if rollout_group is None else {"rollout_group": int(rollout_group)}
     mc = DistributedMCTS(pol, val, dp=dp, lmbda=lmbda, batch=batch, nthreads=nthreads,
                          rollouts_per_leaf=rollouts_per_leaf, seed=seed, depth=depth,
-                         master_share=share, force_master=True)
+                         master_share=share, force_master=True, **kw)
     st = GameState()
     mc.n_playout = warmup
     mv = mc.get_move(st)  # compiles / allocates; the tree is discarded below
@@ -225,6 +227,9 @@ def main():
     ap.add_argument("--pipeline", type=int, default=3, help="waves in flight (1 = serial)")
     ap.add_argument("--max-inflight", type=int, default=8, help="rollout waves in flight")
     ap.add_argument("--rollout-group", type=int, default=8, help="waves per rollout launch")
+    ap.add_argument("--dist-rollout-group", type=int, default=None,
+                    help="--distributed: waves per rollout launch on each serving GPU "
+                         "(default DistributedMCTS's)")
     ap.add_argument("--moves", type=int, default=1)
     ap.add_argument("--eval-priority", type=int, default=None,
                     help="stream priority of the wave passes (e.g. -1: above the rollouts)")
@@ -259,7 +264,8 @@ def main():
                                 moves=args.moves, rollouts_per_leaf=args.rollouts_per_leaf,
                                 lmbda=args.lmbda, filters=args.filters, nthreads=args.threads,
                                 mode=args.mode, depth=args.depth,
-                                master_share=args.master_share)
+                                master_share=args.master_share,
+                                rollout_group=args.dist_rollout_group)
         if r is not None:
             r.update({"metric": "MCTS simulations/s (19x19 APV-MCTS, one search over %d GPUs)"
                       % dp.world, "lmbda": args.lmbda})
