@@ -215,9 +215,10 @@ def measure_sims_per_s(device, **kw):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--playouts", type=int, default=8192)
-    ap.add_argument("--batch", type=int, default=512,
-                    help="leaves per wave (512 with pipeline 3 measured best: "
-                         "profiles/mcts_sweep_r2.txt)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="leaves per wave (default: 512 on one GPU -- with pipeline 3 measured "
+                         "best, profiles/mcts_sweep_r2.txt -- and distributed_wave(N) per GPU "
+                         "with --distributed)")
     ap.add_argument("--rollout-device", default="gpu", choices=["gpu", "cpu"])
     ap.add_argument("--rollouts-per-leaf", type=int, default=1,
                     help="playouts per leaf (1 = AlphaGo's APV-MCTS: one rollout per simulation)")
@@ -260,7 +261,7 @@ def main():
         dp = DPContext()
         r = measure_distributed(dp, dp.device, playouts=args.playouts,
                                 batch=distributed_wave(dp.world, args.mode)
-                                if args.batch == 512 else args.batch,
+                                if args.batch is None else args.batch,
                                 moves=args.moves, rollouts_per_leaf=args.rollouts_per_leaf,
                                 lmbda=args.lmbda, filters=args.filters, nthreads=args.threads,
                                 mode=args.mode, depth=args.depth,
@@ -274,7 +275,7 @@ def main():
         dp.shutdown()
         return
     dev = torch.device("cuda")
-    r = measure(dev, playouts=args.playouts, batch=args.batch, moves=args.moves,
+    r = measure(dev, playouts=args.playouts, batch=args.batch or 512, moves=args.moves,
                 rollout_device=args.rollout_device, rollouts_per_leaf=args.rollouts_per_leaf,
                 lmbda=args.lmbda, filters=args.filters, nthreads=args.threads,
                 pipeline=args.pipeline, max_inflight=args.max_inflight,
