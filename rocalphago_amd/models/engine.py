@@ -36,6 +36,16 @@ class ConvSpec(object):
         self.halo_in = max(1, ks // 2)
 
 
+def complement(ranges, n):
+    """The [start, end) ranges of [0, n) that none of ``ranges`` covers, in order."""
+    out, pos = [], 0
+    for a, b in sorted(ranges) + [(n, n)]:
+        if a > pos:
+            out.append((pos, a))
+        pos = max(pos, b)
+    return out
+
+
 def pack_grid_width(specs):
     """Grid width of conv.hip's pack_trunk_kernel: the 16x16 (n, c) all-tap tiles of the widest
     layer, rounded up to a multiple of 8 (each block grid-strides over its layer's tiles)."""
@@ -127,13 +137,13 @@ class _PackedConvs(object):
         if self._direct_version is not None:
             self._direct_layouts()
 
-    def sgd_pack(self, weights, biases, flat, flat_grad, lr, version):
+    def sgd_pack(self, weights, biases, flat, flat_grad, lr, version, max_gaps=None):
         """The optimizer step of this trunk's parameters folded into their repacking (round 6:
         pack_trunk + wino_pack re-read the fp32 masters right after sgd_kernel had): wino_pack
         and pack_trunk read each master and its gradient once, write back w - lr g and pack
         that. Returns the [start, end) element ranges of ``flat`` it stepped (the caller steps
-        the rest), or None when the packing tables do not point into ``flat`` (then nothing was
-        done)."""
+        the rest), or None when the packing tables do not point into ``flat`` or the rest of
+        ``flat`` would take more than ``max_gaps`` separate ranges (then nothing was done)."""
         if self._packed_version is None or getattr(self, "_pack_key", None) is None:
             return None
         ws = [w.contiguous() for w in weights]
@@ -150,6 +160,8 @@ class _PackedConvs(object):
                 return None
             ranges.append(((p - base) // esz, (p - base) // esz + t.numel()))
         if flat_grad.numel() != flat.numel():
+            return None
+        if max_gaps is not None and len(complement(ranges, flat.numel())) > max_gaps:
             return None
         sgd = ((flat_grad.data_ptr() - base) // esz, lr, 0.0)
         if any(self._wino):

@@ -77,21 +77,27 @@ class _TrunkPlan(object):
         self.K = specs[-1].cout
         net._sgd_fold = self.sgd_fold  # the optimizer's step folded into the weight repack
 
+    # the fold pays only while the rest of the flat buffer is one or two plain SGD launches: the
+    # ResNet's BN parameters sit between its conv layers, and stepping them range by range took
+    # 20 launches (90 us per step) against one 11 us pass over the whole buffer
+    # (profiles/sgd_fold_r6.txt)
+    SGD_FOLD_MAX_GAPS = 2
+
     def sgd_fold(self, lr):
         """SGD step of the whole flat buffer with the trunk's part folded into its repack
         (engine._PackedConvs.sgd_pack) and the rest by the plain kernel. False: not possible
-        (e.g. the packing tables are not built yet), nothing done."""
+        (e.g. the packing tables are not built yet, or the rest is too fragmented), nothing
+        done."""
+        from .engine import complement
         Ws, bs = self._params()
         net = self.net
         ver = (net.version + 1, net.flat._version)  # after the optimizer's bump()
-        ranges = self.trunk.sgd_pack(Ws, bs, net.flat, net.flat_grad, lr, ver)
+        ranges = self.trunk.sgd_pack(Ws, bs, net.flat, net.flat_grad, lr, ver,
+                                     max_gaps=self.SGD_FOLD_MAX_GAPS)
         if ranges is None:
             return False
-        pos = 0
-        for a, b in sorted(ranges) + [(net.flat.numel(), net.flat.numel())]:
-            if a > pos:
-                ops.sgd_(net.flat[pos:a], net.flat_grad[pos:a], lr)
-            pos = max(pos, b)
+        for a, b in complement(ranges, net.flat.numel()):
+            ops.sgd_(net.flat[a:b], net.flat_grad[a:b], lr)
         self.folded_steps = getattr(self, "folded_steps", 0) + 1
         return True
 

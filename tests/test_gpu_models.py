@@ -349,10 +349,16 @@ def test_sgd_folded_into_weight_repack_is_bit_exact(cuda, arch):
         assert plan is not None
         if not fold:
             m.net._sgd_fold = None
-        steps = 3 if arch == "policy" else 1
-        losses = [m.train_on_batch(X, Y) for _ in range(steps)]
+        if arch == "policy":
+            losses = [m.train_on_batch(X, Y) for _ in range(3)]
+            folded = 3
+        else:
+            # by default the ResNet does not fold (below); exercise the folded path anyway
+            plan.SGD_FOLD_MAX_GAPS = None
+            losses = [m.train_on_batch(X, Y)]
+            folded = 1
         torch.cuda.synchronize()
-        assert getattr(plan, "folded_steps", 0) == (steps if fold else 0)
+        assert getattr(plan, "folded_steps", 0) == (folded if fold else 0)
         out.append((m.net.flat.clone(), losses, pol.forward(X[:8])))
     (fa, la, pa), (fb, lb, pb) = out
     if arch == "policy":
@@ -365,3 +371,10 @@ def test_sgd_folded_into_weight_repack_is_bit_exact(cuda, arch):
         assert np.allclose(la, lb, rtol=1e-5)
         # (a ~5e-8 weight difference may flip a bf16 rounding of a packed weight)
         assert np.allclose(pa, pb, rtol=1e-2, atol=1e-6)
+        # by default the ResNet does not fold: its BN parameters between the conv layers leave
+        # the rest of the flat buffer in many pieces (fused._TrunkPlan.SGD_FOLD_MAX_GAPS)
+        pol = ResnetPolicy(DEFAULT_FEATURES, board=19, filters_per_layer=128, layers=5,
+                           device=cuda, seed=9)
+        pol.model.compile(loss="categorical_crossentropy", optimizer=KZ.SGD(lr=0.05))
+        pol.model.train_on_batch(X, Y)
+        assert getattr(pol.model._plan_for(), "folded_steps", 0) == 0
