@@ -67,6 +67,36 @@ def test_wino_forward_matches_fp32(ops, B, S, ho, C):
     assert rel_norm(out, ops.unpack(yd, C, ho)) < 6e-3
 
 
+@pytest.mark.parametrize("B", [1, 64, 128])
+def test_wino_half_board_blocks_match_fp32(ops, B):
+    """Small one-wave batches (the self-play plies, the search's partial waves) run half-board
+    blocks (two 96-pair blocks per board, all 192 output channels): forward with bias + ReLU
+    and dgrad with the ReLU mask against fp32 F.conv2d."""
+    dev = torch.device("cuda")
+    torch.manual_seed(1)
+    S, C = 19, 192
+    if ops.conv_wino_mode(B, S, C, C) != 2:
+        pytest.skip("half-board blocks are chosen for B <= 128 on 256 CUs only")
+    x = F.relu(torch.randn(B, C, S, S, device=dev))
+    w = torch.randn(C, C, 3, 3, device=dev) * 0.05
+    b = torch.randn(C, device=dev) * 0.1
+    xp = ops.pack_nchw(x, 1, C)
+    uf, ub = ops.wino_weights(w, C, C)
+    y = ops.alloc_padded(B, S, 1, C, dev)
+    ops.conv_wino(xp, uf, b.contiguous(), y, B, S, C, C, 1, True)
+    ref = F.relu(F.conv2d(bf(x), bf(w), b, padding=1))
+    out = ops.unpack(y, C, 1)
+    assert rel_norm(out, ref) < 6e-3 and rel_max(out, ref) < 2e-2
+    g = torch.randn(B, C, S, S, device=dev)
+    dx = ops.alloc_padded(B, S, 1, C, dev)
+    ops.conv_wino(ops.pack_nchw(g, 1, C), ub, None, dx, B, S, C, C, 1, False, mask=xp)
+    xr = bf(x).requires_grad_()
+    F.conv2d(xr, bf(w), None, padding=1).backward(bf(g))
+    ref_dx = xr.grad * (bf(x) > 0)
+    assert rel_norm(ops.unpack(dx, C, 1), ref_dx) < 6e-3
+    assert dx[:, :1].abs().max().item() == 0 and dx[:, :, -1:].abs().max().item() == 0
+
+
 @pytest.mark.parametrize("B,S,ho,C", [(3, 19, 1, 192), (2, 19, 2, 192), (4, 13, 1, 192),
                                       (3, 19, 1, 128), (128, 19, 2, 192)])
 def test_wino_dgrad_with_mask_matches_autograd(ops, B, S, ho, C):
