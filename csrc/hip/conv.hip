@@ -1115,7 +1115,7 @@ constexpr int kPackFields = 11;
 // block per tap of a 64 x 64 tile, whose lanes read 1 of every taps floats: 15-17 us per SL step
 // for the 5x5 layer alone, and scattered 4-byte master writes from 25 blocks per cache line
 // with the fold.)
-constexpr int kPT = 16, kPTaps = 25;  // tile edge; taps of the largest kernel (5x5)
+constexpr int kPT = 16, kPTaps = 49;  // tile edge; taps of the largest kernel packed (7x7)
 __global__ void __launch_bounds__(256) pack_trunk_kernel(const int64_t* __restrict__ table,
                                                          int nrows, int nfull, SgdFold sgd) {
   // the padded bias of a layer (its fp32 master stepped first with sgd.on)
@@ -1143,40 +1143,37 @@ __global__ void __launch_bounds__(256) pack_trunk_kernel(const int64_t* __restri
   if (blockIdx.x == 0) pack_bias(b, COUT, COUTP, bo);
   if (!Wf && !Wb) return;  // bias-only row (a Winograd layer: rag_wino_pack packs its weights)
   const int taps = KS * KS;
-  if (taps > kPTaps) return;  // (the host never builds such a row)
+  if (taps > kPTaps) return;  // (engine._PackedConvs never builds such a row: ks <= 7)
   const int ntc = (CINP + kPT - 1) / kPT, ntiles = ((COUTP + kPT - 1) / kPT) * ntc;
   const int row = kPT * taps;  // contiguous masters per output channel of a tile
   __shared__ float tl[kPTaps * kPT * (kPT + 1)];  // [tap][n][c]
   const int tid = threadIdx.x;
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int n0 = (tile / ntc) * kPT, c0 = (tile % ntc) * kPT;
-    float v[kPTaps], gr[kPTaps];  // element tid + 256 i of the tile: i < taps
+    // element tid + 256 i of the tile (i < taps), in chunks of 16 per thread: each chunk's
+    // loads all go out before its stores
+    for (int i0 = 0; i0 < taps; i0 += 16) {
+      float v[16], gr[16];
 #pragma unroll
-    for (int i = 0; i < kPTaps; ++i) {
-      const int idx = tid + 256 * i, r = idx / row, e = idx - r * row;
-      const int n = n0 + r, c = c0 + e / taps;
-      const bool in = i < taps && n < COUT && c < CIN;
-      const size_t o = in ? (size_t)(n * CIN + c0) * taps + e : 0;
-      v[i] = in ? W[o] : 0.f;
-      gr[i] = (in && sgd.on) ? W[o + sgd.goff] : 0.f;
-    }
-    if (sgd.on) {
-#pragma unroll
-      for (int i = 0; i < kPTaps; ++i) {
-        const int idx = tid + 256 * i, r = idx / row, e = idx - r * row;
+      for (int k = 0; k < 16; ++k) {
+        const int i = i0 + k, idx = tid + 256 * i, r = idx / row, e = idx - r * row;
         const int n = n0 + r, c = c0 + e / taps;
-        if (i < taps && n < COUT && c < CIN) {
-          v[i] = sgd.update(v[i], gr[i]);
-          W[(size_t)(n * CIN + c0) * taps + e] = v[i];
-        }
+        const bool in = i < taps && n < COUT && c < CIN;
+        const size_t o = in ? (size_t)(n * CIN + c0) * taps + e : 0;
+        v[k] = in ? W[o] : 0.f;
+        gr[k] = (in && sgd.on) ? W[o + sgd.goff] : 0.f;
       }
-    }
 #pragma unroll
-    for (int i = 0; i < kPTaps; ++i) {
-      if (i >= taps) break;
-      const int idx = tid + 256 * i, r = idx / row, e = idx - r * row;
-      const int cl = e / taps, tap = e - cl * taps;
-      tl[(tap * kPT + r) * (kPT + 1) + cl] = v[i];
+      for (int k = 0; k < 16; ++k) {
+        const int i = i0 + k, idx = tid + 256 * i, r = idx / row, e = idx - r * row;
+        if (i >= taps) break;
+        const int n = n0 + r, cl = e / taps, tap = e - cl * taps;
+        if (sgd.on && n < COUT && c0 + cl < CIN) {
+          v[k] = sgd.update(v[k], gr[k]);
+          W[(size_t)(n * CIN + c0) * taps + e] = v[k];
+        }
+        tl[(tap * kPT + r) * (kPT + 1) + cl] = v[k];
+      }
     }
     __syncthreads();
     for (int it = tid; it < taps * kPT * kPT; it += 256) {

@@ -57,6 +57,10 @@ class _PackedConvs(object):
     OIHW masters in one launch whenever the model's weight version changes."""
 
     def _init_packing(self, specs, device, wino=None):
+        # conv.hip pack_trunk_kernel stages a 16x16 tile of all taps in LDS: kernels up to 7x7
+        if any(s.ks > 7 for s in specs):
+            raise ValueError("fused HIP trunks take kernels up to 7x7, got %s"
+                             % sorted({s.ks for s in specs}))
         self._wf = [None] * len(specs)
         self._wb = [None] * len(specs)
         self._bias = [torch.zeros(s.coutp, device=device) for s in specs]

@@ -442,11 +442,13 @@ def test_deferred_reductions_of_two_trunks_interleave_on_one_stream(ops):
 @pytest.mark.gpu
 def test_trunk_repack_matches_per_layer_packer(ops):
     """pack_trunk (one launch, 16x16 all-tap tiles through LDS) equals pack_weights per layer for
-    both bf16 GEMM layouts and the padded biases: a 5x5 48->192 layer, odd widths, 3x3 layers."""
+    both bf16 GEMM layouts and the padded biases: a 7x7 and a 5x5 input layer, odd widths, 3x3
+    layers, a 1x1 head."""
     from rocalphago_amd.models.engine import ConvSpec, HipTrunk
     dev = torch.device("cuda")
     torch.manual_seed(4)
-    specs = [ConvSpec(5, 48, 192, True), ConvSpec(3, 192, 192, True), ConvSpec(3, 192, 40, True),
+    specs = [ConvSpec(7, 48, 48, True), ConvSpec(5, 48, 192, True),
+             ConvSpec(3, 192, 192, True), ConvSpec(3, 192, 40, True),
              ConvSpec(3, 40, 64, True), ConvSpec(1, 64, 1, False)]
     tr = HipTrunk(specs, 19, dev)
     ws = [torch.randn(s.cout, s.cin, s.ks, s.ks, device=dev) for s in specs]
@@ -455,8 +457,8 @@ def test_trunk_repack_matches_per_layer_packer(ops):
     # the 192 -> 192 layer is a Winograd layer: its fragment-major Winograd weights come with
     # every repack (and its direct dgrad layout while the dgrad carries deferred reductions),
     # its direct forward layout on first demand
-    assert tr._wino == [False, True, False, False, False]
-    for l in (1,):
+    assert tr._wino == [False, False, True, False, False, False]
+    for l in (2,):
         uf, ub = ops.wino_weights(ws[l], 192, 192)
         assert torch.equal(tr._uf[l], uf)
         assert (tr._ub[l] is None) if not tr.wino_dgrad else torch.equal(tr._ub[l], ub)
