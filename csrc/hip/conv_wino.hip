@@ -588,9 +588,7 @@ conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
 // and dgrad Ub (N = CINP, K = COUTP: the same transform of the flipped, transposed kernel
 // W[n][c][2-ky][2-kx]), tap (ky, q) = ky * 4 + q, each stored fragment-major
 // [12][K / 32][N / 16][64][8]: element (n, k) of a tap at lane (n % 16) + 16 ((k % 32) / 8),
-// position k % 8 of fragment (k / 32, n / 16), as a 16x16x32 MFMA A operand reads it. Block = one 64 (n) x 64 (c) tile of one kernel row ky
-// of one layer (blockIdx.y): the row's three taps go through LDS so both layouts are written
-// coalesced (Uf along c, Ub along n).
+// position k % 8 of fragment (k / 32, n / 16), as a 16x16x32 MFMA A operand reads it.
 // Wd (or 0): the direct dgrad layout [tap'][CINP][COUTP] (tap' = 8 - (3 ky + kx), conv.hip
 // pack_trunk_kernel's Wb) from the same LDS tile, for layers whose dgrad runs the direct kernel:
 // the fp32 weights are read once per step instead of once more by pack_trunk.

@@ -68,3 +68,11 @@ def test_trunk_rejects_kernels_above_7x7():
     from rocalphago_amd.models.engine import HipTrunk
     with pytest.raises(ValueError, match="7x7"):
         HipTrunk([ConvSpec(9, 48, 64, True)], 19, torch.device("cpu"))
+
+
+def test_wino_pack_grid_covers_every_tile():
+    """conv_wino.hip wino_pack_kernel: one block per 32 (n) x 16 (c) tile; rag_wino_pack
+    launches 8 blocks per 64 x 64 tile of the widest layer, which covers every layer's tiles."""
+    for coutp, cinp in [(192, 192), (128, 128), (192, 64), (384, 192), (64, 32), (256, 96)]:
+        max_tiles = -(-coutp // 64) * -(-cinp // 64)
+        assert -(-coutp // 32) * -(-cinp // 16) <= 8 * max_tiles
