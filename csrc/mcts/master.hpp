@@ -51,11 +51,11 @@ struct alignas(64) ChanHead {
   int32_t cmd, arg;
   alignas(64) std::atomic<uint32_t> abort;
   char why[120];
+  alignas(64) uint32_t ring[256];  // per rank: the master's next slot (kept across searches)
   // the search's root as its game record (written by the master before the search's first
   // request): [moves, handicaps, size, superko, 2 x komi, hash, player to move, -] and the
   // handicap stones followed by the moves (PASS = -1); an evaluating rank that did not get the
   // position replays it (search/distributed.py)
-  alignas(64) uint32_t ring[256];  // per rank: the master's next slot (kept across searches)
   alignas(64) int64_t root_meta[8];
   int16_t root_moves[4096];
 };
