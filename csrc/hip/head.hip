@@ -317,34 +317,59 @@ head_bwd_reduce_kernel(const float* __restrict__ dwpart, const float* __restrict
   }
 }
 
-// z[b,p] = sum_k w[k]*h[b,p,k] + b0 (value-head 1x1 conv, no softmax)
+// z[b,p] = sum_k w[k]*h[b,p,k] + b0 (value-head 1x1 conv, no softmax). 8 lanes per pixel
+// (coalesced 128-byte channel segments, as policy_head_fwd_kernel), each lane's NM x 8 weights
+// in registers for the whole grid-stride loop: the first version loaded w[c + t] per element
+// and pixel (24 loads per lane per pixel for K = 192), 23 us for a B = 256 batch against the
+// ~8 us its 35 MB of reads need. NM = 0: any K (weights read per pixel).
+template <int NM>
 __global__ void __launch_bounds__(kHeadThreads)
 head_linear_kernel(const bf16* __restrict__ H, const float* __restrict__ w, const float* b0,
                    float* __restrict__ z, int B, int S, int KP, int K) {
   const int S2 = S * S, WP = S + 2;
   const int total = B * S2;
-  // 8 lanes per pixel (coalesced 128-byte channel segments, as policy_head_fwd_kernel)
   const int sub = threadIdx.x & 7;
-  const int lanes = gridDim.x * blockDim.x;
-  for (int t0 = blockIdx.x * blockDim.x + threadIdx.x; t0 < ((total * 8 + lanes - 1) / lanes) *
-       lanes; t0 += lanes) {
-    const int idx0 = t0 >> 3;
-    const int idx = idx0 < total ? idx0 : total - 1;
-    const int b = idx / S2, p = idx - (idx / S2) * S2;
-    const int i = p / S, j = p - (p / S) * S;
+  float wr[NM > 0 ? NM : 1][8];
+  if constexpr (NM > 0) {
+#pragma unroll
+    for (int m = 0; m < NM; ++m)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int c = m * 64 + sub * 8 + t;
+        wr[m][t] = c < K ? w[c] : 0.f;
+      }
+  }
+  const float bias = b0 ? *b0 : 0.f;
+  const int groups = (int)((gridDim.x * blockDim.x) >> 3);
+  // every lane of an 8-lane group runs the same iterations (the shuffles stay inside it)
+  for (int idx = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 3); idx < total;
+       idx += groups) {
+    const int b = idx / S2, p = idx - b * S2;
+    const int i = p / S, j = p - i * S;
     const bf16* row = H + ((size_t)(b * WP + i + 1) * WP + j + 1) * KP;
     float acc = 0.f;
-#pragma unroll 4
-    for (int c = sub * 8; c < K; c += 64) {
-      const bf16x8 v = *reinterpret_cast<const bf16x8*>(row + c);
+    if constexpr (NM > 0) {
 #pragma unroll
-      for (int t = 0; t < 8; ++t)
-        if (c + t < K) acc += (float)v[t] * w[c + t];
+      for (int m = 0; m < NM; ++m) {
+        const int c = m * 64 + sub * 8;
+        if (c < K) {  // (K a multiple of 8: a lane's 8 channels are all in or all out)
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(row + c);
+#pragma unroll
+          for (int t = 0; t < 8; ++t) acc = fmaf((float)v[t], wr[m][t], acc);
+        }
+      }
+    } else {
+      for (int c = sub * 8; c < K; c += 64) {
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(row + c);
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+          if (c + t < K) acc += (float)v[t] * w[c + t];
+      }
     }
     acc += __shfl_xor(acc, 1);
     acc += __shfl_xor(acc, 2);
     acc += __shfl_xor(acc, 4);
-    if (sub == 0 && idx0 < total) z[idx] = acc + (b0 ? *b0 : 0.f);
+    if (sub == 0) z[idx] = acc + bias;
   }
 }
 
@@ -570,9 +595,17 @@ RAG_API size_t rag_head_bwd_workspace(int B, int S, int KP) {
 RAG_API int rag_head_linear(const void* H, const float* w, const float* b0, float* z, int B,
                             int S, int KP, int K, hipStream_t stream) {
   const int total = B * S * S;
-  const int blocks = (int)(((size_t)total * 8 + kHeadThreads - 1) / kHeadThreads);  // 8 lanes / pixel
-  head_linear_kernel<<<blocks < 4096 ? blocks : 4096, kHeadThreads, 0, stream>>>(
-      (const bf16*)H, w, b0, z, B, S, KP, K);
+  int blocks = (int)(((size_t)total * 8 + kHeadThreads - 1) / kHeadThreads);  // 8 lanes / pixel
+  blocks = blocks < 8192 ? blocks : 8192;
+  const int nm = K % 8 == 0 ? (K + 63) / 64 : 0;
+#define RAG_HL(NM) \
+  head_linear_kernel<NM><<<blocks, kHeadThreads, 0, stream>>>((const bf16*)H, w, b0, z, B, S, KP, K)
+  if (nm == 1) RAG_HL(1);
+  else if (nm == 2) RAG_HL(2);
+  else if (nm == 3) RAG_HL(3);
+  else if (nm == 4) RAG_HL(4);
+  else RAG_HL(0);
+#undef RAG_HL
   return (int)hipGetLastError();
 }
 

@@ -628,3 +628,26 @@ def test_pingpong_conv_192px_blocks_residual_and_dgrad(ops):
     xr = bf(x).requires_grad_()
     (F.conv2d(xr, bf(w), padding=1) * bf(g)).sum().backward()
     assert rel_err(ops.unpack(dx, C, 1), xr.grad * (x > 0)) < 2e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K,KP,B", [(192, 192, 256), (128, 128, 64), (256, 256, 3), (40, 40, 7),
+                                    (36, 40, 5)])
+def test_head_linear_matches_fp32(ops, K, KP, B):
+    """The value head's 1x1 convolution (head.hip head_linear_kernel: weights held in registers
+    for K a multiple of 8 up to 256, the generic loop otherwise) against fp32 PyTorch on the
+    same bf16-rounded inputs, including the padded channels past K."""
+    dev = torch.device("cuda")
+    torch.manual_seed(21)
+    S = 19
+    h = F.relu(torch.randn(B, K, S, S, device=dev))
+    hp = ops.pack_nchw(h, 1, KP)
+    if KP > K:  # garbage in the padded channels must not leak into z
+        hp[..., K:] = 1.0
+    w = torch.randn(K, device=dev)
+    b0 = torch.randn(1, device=dev)
+    z = torch.empty(B, S * S, device=dev)
+    ops.head_linear(hp, w, b0, z, K)
+    hb = h.to(torch.bfloat16).float()
+    ref = (hb * w.view(1, K, 1, 1)).sum(1).reshape(B, S * S) + b0
+    assert torch.allclose(z, ref, rtol=1e-4, atol=1e-3), (z - ref).abs().max().item()
