@@ -100,15 +100,29 @@ class _Slot(object):
         def pin(shape, dt):
             return torch.empty(shape, dtype=dt, pin_memory=True)
 
-        def dev(t):
-            return torch.empty(t.shape, dtype=t.dtype, device=device)
-
         self.B, self.S, self.P = B, S, P
-        self.h = {"colors": pin((B, P), torch.int8), "ages": pin((B, P), torch.int16),
-                  "meta4": pin((B, 4), torch.int32)}
+        # every input field is a view of ONE pinned buffer mirrored by one device buffer: a wave's
+        # inputs go up in one copy instead of one per field (each copy is a blit launch of
+        # ~5-9 us on the GPU; the self-play plies do the same, training/selfplay.py)
+        specs = {"colors": ((B, P), torch.int8), "ages": ((B, P), torch.int16),
+                 "meta4": ((B, 4), torch.int32)}
         if host_ladders:
-            self.h["ladders"] = pin((B, 2, P), torch.uint8)
-        self.d = {k: dev(v) for k, v in self.h.items()}
+            specs["ladders"] = ((B, 2, P), torch.uint8)
+        offs, total = {}, 0
+        for k, (shp, dt) in specs.items():
+            offs[k] = total
+            nbytes = int(np.prod(shp)) * torch.empty((), dtype=dt).element_size()
+            total += (nbytes + 15) // 16 * 16
+        self.hraw = pin((total,), torch.uint8)
+        self.draw = torch.empty((total,), dtype=torch.uint8, device=device)
+
+        def view(raw, k):
+            shp, dt = specs[k]
+            nb = int(np.prod(shp)) * torch.empty((), dtype=dt).element_size()
+            return raw[offs[k]:offs[k] + nb].view(dt).view(shp)
+
+        self.h = {k: view(self.hraw, k) for k in specs}
+        self.d = {k: view(self.draw, k) for k in specs}
         self.n = {k: v.numpy() for k, v in self.h.items()}
         self.h_ill = self.d_ill = None
         self.planes = torch.empty((B, F, S, S), dtype=torch.uint8, device=device)
@@ -269,10 +283,9 @@ class NetworkEvaluator(object):
 
     def _slot_pass(self, slot, n, S, superko, host_lad, ppol, pval):
         gf = self.gpu["p"]
-        d, h = slot.d, slot.h
+        d = slot.d
         with torch.no_grad():
-            for k in d:
-                d[k][:n].copy_(h[k][:n], non_blocking=True)
+            slot.draw.copy_(slot.hraw, non_blocking=True)  # all input fields, one copy
             il = None
             if superko:
                 slot.d_ill[:n].copy_(slot.h_ill[:n], non_blocking=True)
