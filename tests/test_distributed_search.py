@@ -296,8 +296,10 @@ def test_search_budget_efficiency_shipped_geometry_two_ranks(tmp_path):
     values; lambda 0.5 with rollouts seeded by the leaf position, returned within 6 waves; waves
     scaled from the 19x19 bench to the study's budget) is worth two GPUs: budget efficiency
     >= 0.85 against ONE GPU at the single-GPU bench geometry (512-leaf waves, 3 awaiting values)
-    searching twice as long, Jensen-Shannon distance to a truth of 8x the budget (deterministic;
-    the 48-position sweep over waves and N is profiles/search_efficiency_r6.json: 0.98 here)."""
+    searching twice as long, Jensen-Shannon distance to a truth of 8x the budget (deterministic
+    evaluator and rollouts; the emulated GPU latency makes the backup order timing-dependent, a
+    few thousandths of spread in the distance: 0.994-1.0 over repeated runs; the 48-position
+    sweep over waves and N is profiles/search_efficiency_r6.json: 0.92-0.98 here)."""
     from rocalphago_amd.search.efficiency import shipped_waves, study
     r = study(worlds=(2,), per_rank=256, n_positions=16, truth_mult=8,
               search_cls="DistributedMCTS", outdir=str(tmp_path), lmbda=0.5, rollout_delay=6,
