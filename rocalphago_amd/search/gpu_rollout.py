@@ -106,11 +106,12 @@ class RolloutBatcher(object):
 
 
 # moves per rollout launch (rag_rollouts' sliced mode: the games are parked in HBM between
-# launches, so no launch holds a CU for a whole playout); 0 = one launch per playout. In the
-# search 16 measured 128.1-128.8k sims/s against 125.5-128.0k for 0 and 125.8-128.3k for 64
-# (three alternating runs each on one box), with the conv launches that overlap a rollout at
-# 3.6x the median instead of 9.6x (profiles/mcts_rollout_interference_r6.txt)
-DEFAULT_SLICE = 16
+# launches, so no launch holds a CU for a whole playout); 0 = one launch per playout. With
+# 8-wave rollout groups, 4 / 8 / 16 moves measured 138.6-140.2k / 140.7-141.7k / 139.1-142.6k
+# sims/s (three alternating runs each, one box): the same within the spread. The conv launches
+# that overlap a rollout slice ran 1.55x / 2.7x / ~4x the median, against 9.6x for one launch per
+# playout (profiles/mcts_rollout_interference_r6.txt)
+DEFAULT_SLICE = 4
 # torch stream priority of the rollout streams (larger = lower; 0 = default)
 DEFAULT_PRIORITY = 0
 
