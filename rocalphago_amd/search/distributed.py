@@ -135,6 +135,12 @@ class DistributedMCTS(ParallelMCTS):
     tree); rollout_delay: CPU rollouts are returned only this many waves later (the search
     efficiency study's stand-in for the GPU's rollout latency)."""
 
+    # moves per GPU rollout launch on a serving GPU: its rollout groups are small (6 waves of
+    # 128-256 leaves), and 4- or 16-move slices cost it 8-15 % of its serving rate against 64
+    # (wave 128: 74.3-74.6k / 69.6-74.1k / 80.9-82.7k sims/s, profiles/mcts_wave_rates_r6.json);
+    # the single-GPU search's 8-wave groups of 512 take gpu_rollout.DEFAULT_SLICE (4)
+    ROLLOUT_SLICE = 64
+
     def __init__(self, policy=None, value=None, rollout=None, dp=None, depth=2,
                  rollout_slots=None, master_share=1.0, rollout_delay=0, max_path=127,
                  board=None, stall_s=120.0, force_master=False, worker_threads=None, **kw):
@@ -425,8 +431,9 @@ class DistributedMCTS(ParallelMCTS):
             elif mode == "gpu":
                 if self._batcher is None:
                     from .gpu_rollout import GpuRollouts, RolloutBatcher
-                    self._batcher = RolloutBatcher(GpuRollouts(self.rollout, self.gpu),
-                                                   self.rollout_group)
+                    self._batcher = RolloutBatcher(
+                        GpuRollouts(self.rollout, self.gpu, slice_moves=self.ROLLOUT_SLICE),
+                        self.rollout_group)
                 roll = self._batcher.add(ws, wid, self.rollouts_per_leaf, self.rollout_limit,
                                          seed=int(seed) & 0x7FFFFFFF)
             else:
