@@ -20,6 +20,7 @@
 #include <mutex>
 
 #include "common.h"
+#include "pack.h"
 #include "wgrad_part.h"
 
 using namespace rag;
@@ -1102,96 +1103,15 @@ RAG_API int rag_pack_weights(const float* W, void* Wf, void* Wb, int COUT, int C
 }
 
 // One launch that repacks every layer of a trunk after an optimizer step: for each layer the
-// bf16 forward / dgrad GEMM layouts of its OIHW fp32 weights and the padded fp32 bias. `table`
-// holds kPackFields int64 per layer: W, b (or 0), COUT, CIN, KS, COUTP, CINP, Wf, Wb (or 0),
-// bias_out (or 0), first element index; elements of a layer = taps*COUTP*CINP + COUTP.
+// bf16 forward / dgrad GEMM layouts of its OIHW fp32 weights and the padded fp32 bias (pack.h
+// pack_trunk_block: table layout, tiling). The whole SL-style step's repack (with the Winograd
+// layers and the rest of the optimizer step) is one launch instead: conv_wino.hip rag_pack_step.
 namespace {
-constexpr int kPackFields = 11;
-// Block = 16 (n) x 16 (c) tiles of one layer (blockIdx.y = layer), all its taps, grid-strided
-// over the layer's tiles. A tile's OIHW masters are 16 runs of 16 * taps contiguous floats, read
-// (and with the SGD fold stepped and written back) coalesced, every load before any store; they
-// go through LDS so that both bf16 layouts are written along their contiguous dimension: the
-// forward layout [tap][n][c] along c, the dgrad layout [tap'][c][n] along n. (Until round 6: one
-// block per tap of a 64 x 64 tile, whose lanes read 1 of every taps floats: 15-17 us per SL step
-// for the 5x5 layer alone, and scattered 4-byte master writes from 25 blocks per cache line
-// with the fold.)
-constexpr int kPT = 16, kPTaps = 49;  // tile edge; taps of the largest kernel packed (7x7)
 __global__ void __launch_bounds__(256) pack_trunk_kernel(const int64_t* __restrict__ table,
                                                          int nrows, int nfull, SgdFold sgd) {
-  // the padded bias of a layer (its fp32 master stepped first with sgd.on)
-  auto pack_bias = [&](float* b, int COUT, int COUTP, float* bo) {
-    for (int n = threadIdx.x; n < COUTP; n += blockDim.x) {
-      const float v = (b && n < COUT) ? sgd.step(b + n) : 0.f;
-      if (bo) bo[n] = v;
-    }
-  };
-  if ((int)blockIdx.y == nfull) {  // the bias-only rows (after the nfull packed ones): one block each
-    for (int r = nfull + blockIdx.x; r < nrows; r += gridDim.x) {
-      const int64_t* t = table + (size_t)r * kPackFields;
-      pack_bias((float*)t[1], (int)t[2], (int)t[5], (float*)t[9]);
-    }
-    return;
-  }
-  const int64_t* t = table + (size_t)blockIdx.y * kPackFields;
-  float* W = (float*)t[0];
-  float* b = (float*)t[1];
-  const int COUT = (int)t[2], CIN = (int)t[3], KS = (int)t[4], COUTP = (int)t[5],
-            CINP = (int)t[6];
-  bf16* Wf = (bf16*)t[7];
-  bf16* Wb = (bf16*)t[8];
-  float* bo = (float*)t[9];
-  if (blockIdx.x == 0) pack_bias(b, COUT, COUTP, bo);
-  if (!Wf && !Wb) return;  // bias-only row (a Winograd layer: rag_wino_pack packs its weights)
-  const int taps = KS * KS;
-  if (taps > kPTaps) return;  // (engine._PackedConvs never builds such a row: ks <= 7)
-  const int ntc = (CINP + kPT - 1) / kPT, ntiles = ((COUTP + kPT - 1) / kPT) * ntc;
-  const int row = kPT * taps;  // contiguous masters per output channel of a tile
-  __shared__ float tl[kPTaps * kPT * (kPT + 1)];  // [tap][n][c]
-  const int tid = threadIdx.x;
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int n0 = (tile / ntc) * kPT, c0 = (tile % ntc) * kPT;
-    // element tid + 256 i of the tile (i < taps), in chunks of 16 per thread: each chunk's
-    // loads all go out before its stores
-    for (int i0 = 0; i0 < taps; i0 += 16) {
-      float v[16], gr[16];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int i = i0 + k, idx = tid + 256 * i, r = idx / row, e = idx - r * row;
-        const int n = n0 + r, c = c0 + e / taps;
-        const bool in = i < taps && n < COUT && c < CIN;
-        const size_t o = in ? (size_t)(n * CIN + c0) * taps + e : 0;
-        v[k] = in ? W[o] : 0.f;
-        gr[k] = (in && sgd.on) ? W[o + sgd.goff] : 0.f;
-      }
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int i = i0 + k, idx = tid + 256 * i, r = idx / row, e = idx - r * row;
-        if (i >= taps) break;
-        const int n = n0 + r, cl = e / taps, tap = e - cl * taps;
-        if (sgd.on && n < COUT && c0 + cl < CIN) {
-          v[k] = sgd.update(v[k], gr[k]);
-          W[(size_t)(n * CIN + c0) * taps + e] = v[k];
-        }
-        tl[(tap * kPT + r) * (kPT + 1) + cl] = v[k];
-      }
-    }
-    __syncthreads();
-    for (int it = tid; it < taps * kPT * kPT; it += 256) {
-      const int tap = it / (kPT * kPT), q = it - tap * kPT * kPT;
-      if (Wf) {  // c fastest
-        const int cl = q % kPT, r = q / kPT, n = n0 + r, c = c0 + cl;
-        if (n < COUTP && c < CINP)
-          Wf[((size_t)tap * COUTP + n) * CINP + c] = (bf16)tl[(tap * kPT + r) * (kPT + 1) + cl];
-      }
-      if (Wb) {  // n fastest
-        const int r = q % kPT, cl = q / kPT, n = n0 + r, c = c0 + cl;
-        if (n < COUTP && c < CINP)
-          Wb[((size_t)(taps - 1 - tap) * CINP + c) * COUTP + n] =
-              (bf16)tl[(tap * kPT + r) * (kPT + 1) + cl];
-      }
-    }
-    __syncthreads();  // tl is reused by the next tile
-  }
+  __shared__ float tl[pack_trunk_lds(kPTaps)];  // [tap][n][c]
+  pack_trunk_block(table, (int)blockIdx.y, nrows, nfull, sgd, (int)blockIdx.x, (int)gridDim.x,
+                   kPTaps, tl);
 }
 }  // namespace
 

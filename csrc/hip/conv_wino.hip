@@ -36,6 +36,7 @@
 //   * one barrier per chunk-phase (the V buffer flip); no per-step barriers, the two waves of
 //     a SIMD overlap freely.
 #include "common.h"
+#include "pack.h"
 #include "wgrad_part.h"
 
 using namespace rag;
@@ -584,106 +585,53 @@ conv_wino_kernel(const bf16* __restrict__ X, const bf16* __restrict__ U,
   if (red.ticket) wslab_reduce_dynamic<kRedU>(red, reinterpret_cast<int*>(lds));
 }
 
-// Winograd weights of 3x3 layers from the fp32 OIHW masters: forward Uf (N = COUTP, K = CINP)
-// and dgrad Ub (N = CINP, K = COUTP: the same transform of the flipped, transposed kernel
-// W[n][c][2-ky][2-kx]), tap (ky, q) = ky * 4 + q, each stored fragment-major
-// [12][K / 32][N / 16][64][8]: element (n, k) of a tap at lane (n % 16) + 16 ((k % 32) / 8),
-// position k % 8 of fragment (k / 32, n / 16), as a 16x16x32 MFMA A operand reads it.
-// Wd (or 0): the direct dgrad layout [tap'][CINP][COUTP] (tap' = 8 - (3 ky + kx), conv.hip
-// pack_trunk_kernel's Wb) from the same LDS tile, for layers whose dgrad runs the direct kernel:
-// the fp32 weights are read once per step instead of once more by pack_trunk.
-constexpr int kWinoPackFields = 8;  // W, COUT, CIN, COUTP, CINP, Uf, Ub (or 0), Wd (or 0)
-// One block per 32 (n) x 16 (c) tile of a layer, all 9 taps: the tile's OIHW masters are 32 rows
-// of 16 x 9 = 144 contiguous floats, read (and with the SGD fold stepped and written back) with
-// coalesced accesses, staged transposed in LDS, then written out as the forward / dgrad
-// Winograd fragments and the direct dgrad layout. (The first version gave each block one kernel
-// row of a 64 x 64 tile: 3 of every 9 floats per lane. With the fold its scattered 4-byte master
-// writes, three blocks per cache line, took 41-43 us per SL step against 11.5 us unfolded.)
-constexpr int kPackN = 32, kPackC = 16, kPackRow = kPackC * 9;
-__global__ void __launch_bounds__(256) wino_pack_kernel(const int64_t* __restrict__ table,
-                                                        SgdFold sgd) {
-  const int64_t* t = table + (size_t)blockIdx.y * kWinoPackFields;
-  float* W = (float*)t[0];
-  const int COUT = (int)t[1], CIN = (int)t[2], COUTP = (int)t[3], CINP = (int)t[4];
-  bf16* Uf = (bf16*)t[5];
-  bf16* Ub = (bf16*)t[6];
-  bf16* Wd = (bf16*)t[7];
-  const int ntc = (CINP + kPackC - 1) / kPackC, ntn = (COUTP + kPackN - 1) / kPackN;
-  if ((int)blockIdx.x >= ntn * ntc) return;
-  const int n0 = (blockIdx.x / ntc) * kPackN, c0 = (blockIdx.x % ntc) * kPackC;
-  __shared__ float tl[9][kPackN][kPackC + 1];
-  const int tid = threadIdx.x;
-  constexpr int kPer = kPackN * kPackRow / 256;  // 18 floats per thread
-  // ---- masters (and gradients): every load before any store
-  float v[kPer], gr[kPer];
-#pragma unroll
-  for (int i = 0; i < kPer; ++i) {
-    const int idx = tid + 256 * i, r = idx / kPackRow, e = idx - r * kPackRow;
-    const int n = n0 + r, c = c0 + e / 9;
-    const bool in = n < COUT && c < CIN;
-    const size_t o = in ? (size_t)(n * CIN + c0) * 9 + e : 0;
-    v[i] = in ? W[o] : 0.f;
-    gr[i] = (in && sgd.on) ? W[o + sgd.goff] : 0.f;
+// Winograd weights of 3x3 layers from the fp32 OIHW masters (pack.h wino_pack_block: table
+// layout, fragment order, tiling).
+// (at most 128 VGPRs, pack.h pack_rsrc: four blocks per CU, the SL trunk's 792 in one round)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+wino_pack_kernel(const int64_t* __restrict__ table, SgdFold sgd) {
+  __shared__ float tl[kWinoPackLds];
+  wino_pack_block(table, (int)blockIdx.y, (int)blockIdx.x, sgd, tl);
+}
+
+// The rest of a flat parameter buffer after a folded repack: plain SGD over up to two element
+// ranges [a0, a0 + n0), [a1, a1 + n1) of p (gradients sgd.goff elements further).
+struct SgdRest {
+  float* p;
+  long a0, n0, a1, n1;
+};
+
+// The whole weight update of a fused trunk step in ONE launch (round 6: rag_wino_pack +
+// rag_pack_trunk + sgd_kernel were three launches, 38 us per SL step, each mostly its own
+// latency chain): grid rows [0, trows) are the pack_trunk rows (nfull + 1 bias row), the next
+// row (when rest.n0 + rest.n1 > 0) steps the rest of the flat buffer, the last nwino rows are
+// wino_pack rows. The pack_trunk rows come first: blocks dispatch in grid order, and a 5x5
+// layer's tile is the longest chain of the launch (two load rounds of 16 taps); behind 792
+// wino_pack blocks (232 VGPRs: two blocks per CU) it started only in their second round.
+// Dynamic LDS: the larger of the two tiles (pack_trunk sized for the trunk's largest kernel).
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+pack_step_kernel(const int64_t* __restrict__ wtable, int nwino,
+                 const int64_t* __restrict__ ttable, int nrows, int nfull, int max_taps,
+                 SgdFold sgd, SgdRest rest) {
+  extern __shared__ float lds_dyn[];
+  int y = (int)blockIdx.y;
+  const int bx = (int)blockIdx.x, gx = (int)gridDim.x;
+  const int trows = nfull + (nrows > nfull ? 1 : 0);
+  if (y < trows) {
+    pack_trunk_block(ttable, y, nrows, nfull, sgd, bx, gx, max_taps, lds_dyn);
+    return;
   }
-  if (sgd.on) {
-#pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      const int idx = tid + 256 * i, r = idx / kPackRow, e = idx - r * kPackRow;
-      const int n = n0 + r, c = c0 + e / 9;
-      if (n < COUT && c < CIN) {
-        v[i] = sgd.update(v[i], gr[i]);
-        W[(size_t)(n * CIN + c0) * 9 + e] = v[i];
-      }
+  y -= trows;
+  const long n = rest.n0 + rest.n1;
+  if (n > 0 && y == 0) {
+    for (long i = (long)bx * 256 + threadIdx.x; i < n; i += (long)gx * 256) {
+      float* w = rest.p + (i < rest.n0 ? rest.a0 + i : rest.a1 + (i - rest.n0));
+      *w = sgd.update(*w, w[sgd.goff]);
     }
+    return;
   }
-#pragma unroll
-  for (int i = 0; i < kPer; ++i) {
-    const int idx = tid + 256 * i, r = idx / kPackRow, e = idx - r * kPackRow;
-    const int cl = e / 9, tap = e - cl * 9;
-    tl[tap][r][cl] = v[i];
-  }
-  __syncthreads();
-  const long tap_stride = (long)COUTP * CINP;
-  // fragment-major offset of (n, k) in a [N][K] tap
-  auto fm = [](int n, int k, int N) {
-    return ((size_t)((k >> 5) * (N >> 4) + (n >> 4)) * 64 + (n & 15) + 16 * ((k & 31) >> 3)) * 8 +
-           (k & 7);
-  };
-  // ---- forward Winograd weights: U_q of (n, c) at kernel row ky (c fastest across lanes)
-  if (Uf) {
-    for (int it = tid; it < 3 * kPackN * kPackC; it += 256) {
-      const int cl = it % kPackC, r = (it / kPackC) % kPackN, ky = it / (kPackC * kPackN);
-      const int n = n0 + r, c = c0 + cl;
-      if (n >= COUTP || c >= CINP) continue;
-      const float g0 = tl[3 * ky][r][cl], g1 = tl[3 * ky + 1][r][cl], g2 = tl[3 * ky + 2][r][cl];
-      const size_t o = fm(n, c, COUTP);
-      Uf[(ky * 4 + 0) * tap_stride + o] = (bf16)g0;
-      Uf[(ky * 4 + 1) * tap_stride + o] = (bf16)(0.5f * (g0 + g1 + g2));
-      Uf[(ky * 4 + 2) * tap_stride + o] = (bf16)(0.5f * (g0 - g1 + g2));
-      Uf[(ky * 4 + 3) * tap_stride + o] = (bf16)g2;
-    }
-  }
-  // ---- dgrad: N = cin, K = cout (n fastest across lanes); dgrad kernel row 2 - ky with its kx
-  // flipped: (h0, h1, h2) = (g2, g1, g0)
-  for (int it = tid; it < 3 * kPackN * kPackC; it += 256) {
-    const int r = it % kPackN, cl = (it / kPackN) % kPackC, ky = it / (kPackC * kPackN);
-    const int n = n0 + r, c = c0 + cl;
-    if (n >= COUTP || c >= CINP) continue;
-    const float h0 = tl[3 * ky + 2][r][cl], h1 = tl[3 * ky + 1][r][cl], h2 = tl[3 * ky][r][cl];
-    if (Wd) {
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx)
-        Wd[((size_t)(8 - (3 * ky + kx)) * CINP + c) * COUTP + n] = (bf16)tl[3 * ky + kx][r][cl];
-    }
-    if (Ub) {
-      const int kyb = 2 - ky;
-      const size_t o = fm(c, n, CINP);
-      Ub[(kyb * 4 + 0) * tap_stride + o] = (bf16)h0;
-      Ub[(kyb * 4 + 1) * tap_stride + o] = (bf16)(0.5f * (h0 + h1 + h2));
-      Ub[(kyb * 4 + 2) * tap_stride + o] = (bf16)(0.5f * (h0 - h1 + h2));
-      Ub[(kyb * 4 + 3) * tap_stride + o] = (bf16)h2;
-    }
-  }
+  y -= n > 0 ? 1 : 0;
+  if (y < nwino) wino_pack_block(wtable, y, bx, sgd, lds_dyn);
 }
 
 // Boards per block: as many as fit the 192 pair rows and the V slab.
@@ -848,5 +796,31 @@ RAG_API int rag_wino_pack(const int64_t* table, int nlayers, int max_tiles, hipS
   // 32 x 16 tiles: at most 8 per 64 x 64 tile of the widest layer (wino_pack_kernel)
   const dim3 grid((unsigned)(8 * max_tiles), (unsigned)nlayers);
   wino_pack_kernel<<<grid, 256, 0, stream>>>(table, SgdFold{(long)goff, lr, wd, sgd_on});
+  return (int)hipGetLastError();
+}
+
+// One launch for a fused trunk's whole weight update (pack_step_kernel): the pack_trunk rows of
+// `ttable` (nrows, nfull: rag_pack_trunk's table and split; kernels up to max_taps taps, at most
+// 49), the Winograd rows of `wtable` (nwino, rag_wino_pack's table; 0 = none), on a grid `width`
+// blocks wide (at least 8 per 64 x 64 tile of the widest Winograd layer, and the widest
+// pack_trunk layer's 16 x 16 tiles), and -- with the fold -- plain SGD over up to two ranges
+// [a0, a0 + n0), [a1, a1 + n1) of the flat buffer `flat`.
+RAG_API int rag_pack_step(const int64_t* wtable, int nwino, const int64_t* ttable, int nrows,
+                          int nfull, int max_taps, int width, hipStream_t stream, int64_t goff,
+                          float lr, float wd, int sgd_on, float* flat, int64_t a0, int64_t n0,
+                          int64_t a1, int64_t n1) {
+  if (nwino < 0 || nrows < 0 || nfull < 0 || nfull > nrows || width <= 0 || max_taps < 1 ||
+      max_taps > kPTaps || n0 < 0 || n1 < 0 || (nwino > 0 && !wtable) || (nrows > 0 && !ttable))
+    return -1;
+  const bool rest = sgd_on && n0 + n1 > 0;
+  if (rest && !flat) return -1;
+  const int trows = nfull + (nrows > nfull ? 1 : 0);
+  const int rows = nwino + trows + (rest ? 1 : 0);
+  if (rows == 0) return 0;
+  const int l1 = kWinoPackLds, l2 = pack_trunk_lds(max_taps);
+  const size_t lds = (size_t)(nfull > 0 && l2 > l1 ? l2 : l1) * sizeof(float);
+  const SgdRest r{flat, (long)a0, rest ? (long)n0 : 0L, (long)a1, rest ? (long)n1 : 0L};
+  pack_step_kernel<<<dim3((unsigned)width, (unsigned)rows), 256, lds, stream>>>(
+      wtable, nwino, ttable, nrows, nfull, max_taps, SgdFold{(long)goff, lr, wd, sgd_on}, r);
   return (int)hipGetLastError();
 }

@@ -85,17 +85,19 @@ class _PackedConvs(object):
             if self._wf[l] is None:
                 self._wf[l] = torch.empty((taps, s.coutp, s.cinp), dtype=torch.bfloat16,
                                           device=self.device)
-                self._wb[l] = torch.empty((taps, s.cinp, s.coutp), dtype=torch.bfloat16,
-                                          device=self.device)
+                # the trunk input takes no gradient: layer 0 has no dgrad layout
+                if l > 0:
+                    self._wb[l] = torch.empty((taps, s.cinp, s.coutp), dtype=torch.bfloat16,
+                                              device=self.device)
             if self._wino[l] and self._uf[l] is None:
                 self._uf[l] = torch.empty((12, s.coutp, s.cinp), dtype=torch.bfloat16,
                                           device=self.device)
                 if self.wino_dgrad:
                     self._ub[l] = torch.empty((12, s.cinp, s.coutp), dtype=torch.bfloat16,
                                               device=self.device)
-        # one launch repacks all layers (GEMM layouts + padded biases; Winograd layers: bias
-        # only, their weights in one wino_pack launch); the pointer tables are rebuilt only when
-        # a parameter tensor moved
+        # one launch repacks all layers (GEMM layouts + padded biases; Winograd layers: their
+        # Winograd weights, bias in the pack_trunk rows); the pointer tables are rebuilt only
+        # when a parameter tensor moved
         ws = [w.contiguous() for w in weights]
         key = tuple(w.data_ptr() for w in ws) + \
             tuple(0 if b is None else b.data_ptr() for b in biases)
@@ -103,8 +105,9 @@ class _PackedConvs(object):
             rows, drows, wrows, start = [], [], [], 0
             for l, s in enumerate(self.specs):
                 b = biases[l]
+                wbp = 0 if self._wb[l] is None else self._wb[l].data_ptr()
                 row = [ws[l].data_ptr(), 0 if b is None else b.data_ptr(), s.cout, s.cin, s.ks,
-                       s.coutp, s.cinp, self._wf[l].data_ptr(), self._wb[l].data_ptr(),
+                       s.coutp, s.cinp, self._wf[l].data_ptr(), wbp,
                        self._bias[l].data_ptr(), start]
                 start += s.ks * s.ks * s.coutp * s.cinp + s.coutp
                 if self._wino[l]:
@@ -112,7 +115,7 @@ class _PackedConvs(object):
                     ub = self._ub[l].data_ptr() if self.wino_dgrad else 0
                     # the direct dgrad layout (unless the dgrad runs Winograd too) comes out of
                     # wino_pack's tiles: the pack_trunk row keeps only the bias
-                    wd = 0 if self.wino_dgrad else self._wb[l].data_ptr()
+                    wd = 0 if self.wino_dgrad else wbp
                     wrows.append([ws[l].data_ptr(), s.cout, s.cin, s.coutp, s.cinp,
                                   self._uf[l].data_ptr(), ub, wd])
                     row = row[:7] + [0, 0] + row[9:]
@@ -123,6 +126,7 @@ class _PackedConvs(object):
             self._pack_nfull = len(full)
             self._pack_table = torch.tensor(rows, dtype=torch.int64).to(self.device)
             self._pack_total = pack_grid_width([self.specs[l] for l in full]) if full else 8
+            self._pack_taps = max([self.specs[l].ks ** 2 for l in full] or [1])
             wsp = [s for l, s in enumerate(self.specs) if self._wino[l]]
             if wsp:
                 self._dpack_table = torch.tensor(drows, dtype=torch.int64).to(self.device)
@@ -131,9 +135,7 @@ class _PackedConvs(object):
                 self._wpack_tiles = max(-(-s.coutp // 64) * -(-s.cinp // 64) for s in wsp)
             self._pack_key = key
             self._pack_keep = ws  # keep contiguous copies alive while the table points at them
-        ops.pack_trunk(self._pack_table, len(self.specs), self._pack_total, self._pack_nfull)
-        if any(self._wino):
-            ops.wino_pack(self._wpack_table, sum(self._wino), self._wpack_tiles)
+        self._launch_pack()
         self._packed_version = version
         # once any batch has run a Winograd layer on the direct kernel, its direct layout stays
         # fresh on every weight change: a captured graph replayed after sync_weights() never
@@ -141,13 +143,35 @@ class _PackedConvs(object):
         if self._direct_version is not None:
             self._direct_layouts()
 
-    def sgd_pack(self, weights, biases, flat, flat_grad, lr, version, max_gaps=None):
+    # ONE_LAUNCH: the repack (+ folded optimizer step) of all layers in one pack_step launch;
+    # False: the separate wino_pack + pack_trunk (+ sgd_kernel) launches (the A/B)
+    ONE_LAUNCH = True
+
+    def _launch_pack(self, sgd=None, flat=None, rest=()):
+        """Repack every layer from its fp32 master (with ``sgd``: stepped first, and the
+        ``rest`` ranges of ``flat`` stepped by plain SGD in the same launch; ONE_LAUNCH only)."""
+        wino = sum(self._wino)
+        if self.ONE_LAUNCH:
+            width = max(8 * self._wpack_tiles, self._pack_total) if wino else self._pack_total
+            ops.pack_step(self._wpack_table if wino else None, wino, self._pack_table,
+                          len(self.specs), self._pack_nfull, self._pack_taps, width, sgd=sgd,
+                          flat=flat, rest=rest)
+            return
+        if wino:
+            ops.wino_pack(self._wpack_table, wino, self._wpack_tiles, sgd=sgd)
+        ops.pack_trunk(self._pack_table, len(self.specs), self._pack_total, self._pack_nfull,
+                       sgd=sgd)
+
+    def sgd_pack(self, weights, biases, flat, flat_grad, lr, version, max_gaps=None,
+                 step_rest=False):
         """The optimizer step of this trunk's parameters folded into their repacking (round 6:
         pack_trunk + wino_pack re-read the fp32 masters right after sgd_kernel had): wino_pack
         and pack_trunk read each master and its gradient once, write back w - lr g and pack
         that. Returns the [start, end) element ranges of ``flat`` it stepped (the caller steps
         the rest), or None when the packing tables do not point into ``flat`` or the rest of
-        ``flat`` would take more than ``max_gaps`` separate ranges (then nothing was done)."""
+        ``flat`` would take more than ``max_gaps`` separate ranges (then nothing was done).
+        ``step_rest``: the rest too, in the same launch, when it is at most two ranges (the
+        returned ranges then cover all of ``flat``)."""
         if self._packed_version is None or getattr(self, "_pack_key", None) is None:
             return None
         ws = [w.contiguous() for w in weights]
@@ -168,10 +192,11 @@ class _PackedConvs(object):
         if max_gaps is not None and len(complement(ranges, flat.numel())) > max_gaps:
             return None
         sgd = ((flat_grad.data_ptr() - base) // esz, lr, 0.0)
-        if any(self._wino):
-            ops.wino_pack(self._wpack_table, sum(self._wino), self._wpack_tiles, sgd=sgd)
-        ops.pack_trunk(self._pack_table, len(self.specs), self._pack_total, self._pack_nfull,
-                       sgd=sgd)
+        rest = complement(ranges, flat.numel()) if step_rest and self.ONE_LAUNCH else []
+        if len(rest) > 2:
+            rest = []
+        self._launch_pack(sgd=sgd, flat=flat, rest=rest)
+        ranges = ranges + rest
         self._packed_version = version
         if self._direct_version is not None:
             self._direct_layouts()

@@ -93,7 +93,7 @@ class _TrunkPlan(object):
         net = self.net
         ver = (net.version + 1, net.flat._version)  # after the optimizer's bump()
         ranges = self.trunk.sgd_pack(Ws, bs, net.flat, net.flat_grad, lr, ver,
-                                     max_gaps=self.SGD_FOLD_MAX_GAPS)
+                                     max_gaps=self.SGD_FOLD_MAX_GAPS, step_rest=True)
         if ranges is None:
             return False
         for a, b in complement(ranges, net.flat.numel()):

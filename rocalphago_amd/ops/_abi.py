@@ -29,6 +29,7 @@ SIGNATURES = {
     "rag_conv_wino": [P, P, P, P, P, I, I, I, I, I, I, I, I, P],
     "rag_conv_wino_p": [P, P, P, P, P, I, I, I, I, I, I, I, I, P, P, I],
     "rag_wino_pack": [P, I, I, P, I64, F, F, I],
+    "rag_pack_step": [P, I, P, I, I, I, I, P, I64, F, F, I, P, I64, I64, I64, I64],
     "rag_conv_wino_prefer": [I, I, I, I],
     "rag_conv_wino_mode": [I, I, I, I],
     "rag_conv_wino_bn_ok": [I, I, I, I],

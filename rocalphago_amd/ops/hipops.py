@@ -74,6 +74,18 @@ def pack_trunk(table, nrows, total, nfull=None, sgd=None):
            "pack_trunk")
 
 
+# (free function, handle buffer) of PendingReduction handles dropped during a stream capture
+_DEFERRED_FREE = []
+
+
+def _free_deferred():
+    """Frees the handles whose owners died during a stream capture (called where a handle is
+    created: never inside a capture, which a hipMalloc would invalidate as well)."""
+    while _DEFERRED_FREE:
+        free, buf = _DEFERRED_FREE.pop()
+        free(ctypes.cast(buf, ctypes.c_void_p))
+
+
 class PendingReduction(object):
     """Caller-owned handle of a deferred wgrad partial-slab reduction (conv.hip PendingRed):
     ``conv_wgrad(defer=True, pending=h)`` leaves the reduction in ``h``; the next
@@ -81,6 +93,7 @@ class PendingReduction(object):
     ``wgrad_flush(h)`` launches it on its own. Launches without the handle never touch it."""
 
     def __init__(self):
+        _free_deferred()
         self.buf = ctypes.create_string_buffer(int(_lib().rag_wgrad_pending_bytes()))
         # claim counters allocated now (a hipMalloc on first deferral synchronised the device
         # mid-step) and freed with the handle
@@ -89,6 +102,12 @@ class PendingReduction(object):
 
     def __del__(self):
         try:
+            # the cyclic garbage collector can drop a dead trunk's handle in the middle of a HIP
+            # graph capture on this thread (torch.cuda.graph does not collect first), and a
+            # hipFree there invalidates the capture: keep it for the next safe point instead
+            if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+                _DEFERRED_FREE.append((self._free, self.buf))
+                return
             self._free(self.ptr)
         except Exception:  # interpreter shutdown: the library may be gone already
             pass
@@ -174,6 +193,23 @@ def wino_pack(table, nlayers, max_tiles, sgd=None):
     goff, lr, wd = sgd if sgd is not None else (0, 0.0, 0.0)
     _check(_lib().rag_wino_pack(_ptr(table), nlayers, int(max_tiles), _stream(), int(goff),
                                 float(lr), float(wd), 1 if sgd is not None else 0), "wino_pack")
+
+
+def pack_step(wtable, nwino, ttable, nrows, nfull, max_taps, width, sgd=None, flat=None,
+              rest=()):
+    """A fused trunk's whole weight update in one launch (rag_pack_step, csrc/hip/conv_wino.hip):
+    the ``nwino`` Winograd rows of ``wtable`` (wino_pack's table), the pack_trunk rows of
+    ``ttable`` (``nrows``, ``nfull``: pack_trunk's; kernels up to ``max_taps`` taps) on a grid
+    ``width`` blocks wide, and with ``sgd`` = (goff, lr, wd) the optimizer step folded in plus
+    plain SGD over the (at most two) [start, end) element ranges ``rest`` of ``flat``."""
+    if len(rest) > 2:
+        raise ValueError("pack_step steps at most two rest ranges, got %d" % len(rest))
+    goff, lr, wd = sgd if sgd is not None else (0, 0.0, 0.0)
+    rr = [(a, b - a) for a, b in rest] + [(0, 0)] * (2 - len(rest))
+    _check(_lib().rag_pack_step(_ptr(wtable), int(nwino), _ptr(ttable), int(nrows), int(nfull),
+                                int(max_taps), int(width), _stream(), int(goff), float(lr),
+                                float(wd), 1 if sgd is not None else 0, _ptr(flat),
+                                rr[0][0], rr[0][1], rr[1][0], rr[1][1]), "pack_step")
 
 
 def wino_weights(w, coutp, cinp, dgrad=True):

@@ -468,10 +468,73 @@ def test_trunk_repack_matches_per_layer_packer(ops):
         wb = torch.empty(s.ks * s.ks, s.cinp, s.coutp, dtype=torch.bfloat16, device=dev)
         wf, wb = ops.pack_weights(ws[l], s.coutp, s.cinp, wb=wb)
         assert torch.equal(tr._wf[l], wf), l
-        assert torch.equal(tr._wb[l], wb), l
+        # the trunk input takes no gradient: no dgrad layout for layer 0
+        assert (tr._wb[l] is None) if l == 0 else torch.equal(tr._wb[l], wb), l
         ref_b = torch.zeros(s.coutp, device=dev)
         ref_b[:s.cout] = bs[l]
         assert torch.equal(tr._bias[l], ref_b), l
+
+
+@pytest.mark.gpu
+def test_one_launch_repack_matches_separate_launches(ops):
+    """pack_step (conv_wino.hip: the Winograd rows, the pack_trunk rows and the rest of the flat
+    buffer's SGD in one launch) writes bit for bit what wino_pack + pack_trunk + sgd_kernel write:
+    the packed layouts and biases, and the stepped fp32 masters, with and without the fold."""
+    from rocalphago_amd.models.engine import ConvSpec, HipTrunk, complement
+    dev = torch.device("cuda")
+    specs = [ConvSpec(5, 48, 192, True), ConvSpec(3, 192, 192, True), ConvSpec(3, 192, 192, True),
+             ConvSpec(3, 192, 40, True), ConvSpec(1, 40, 4, False)]
+    sizes = [s.cout * s.cin * s.ks * s.ks for s in specs]
+
+    def packed(tr):
+        # what a repack writes: the direct layouts of the non-Winograd layers (a Winograd layer's
+        # direct forward layout is packed on first demand only), the Winograd weights, the direct
+        # dgrad layouts of layers 1.. (the Winograd layers' out of their wino_pack rows), biases
+        d = {}
+        for l in range(len(specs)):
+            if not tr._wino[l]:
+                d["wf%d" % l] = tr._wf[l].clone()
+            else:
+                d["uf%d" % l] = tr._uf[l].clone()
+            if l > 0:
+                d["wb%d" % l] = tr._wb[l].clone()
+            d["b%d" % l] = tr._bias[l].clone()
+        return d
+
+    out = []
+    for one in (True, False):
+        torch.manual_seed(5)
+        # flat buffer: a head-like block in front, the trunk's weights and biases, a tail block
+        # (every range 16-byte aligned: sgd_kernel's float4 accesses)
+        n = 780 + sum(sizes) + sum(s.cout for s in specs) + 332
+        flat = torch.randn(n, device=dev)
+        grad = torch.randn(n, device=dev)
+        ws, bs, p = [], [], 780
+        for s, k in zip(specs, sizes):
+            ws.append(flat[p:p + k].view(s.cout, s.cin, s.ks, s.ks))
+            p += k
+            bs.append(flat[p:p + s.cout])
+            p += s.cout
+        tr = HipTrunk(specs, 19, dev)
+        tr.ONE_LAUNCH = one
+        assert tr._wino == [False, True, True, False, False]
+        tr.sync_weights(ws, bs, 1)
+        torch.cuda.synchronize()
+        p1 = packed(tr)
+        ranges = tr.sgd_pack(ws, bs, flat, grad, 0.05, 2, step_rest=True)
+        rest = complement(ranges, n)
+        assert rest == ([] if one else [(0, 780), (n - 332, n)])
+        for a, b in rest:  # what fused.sgd_fold does with the rest
+            ops.sgd_(flat[a:b], grad[a:b], 0.05)
+        torch.cuda.synchronize()
+        assert tr._wb[0] is None
+        out.append((p1, flat.clone(), packed(tr)))
+    (pa, fa, qa), (pb, fb, qb) = out
+    for k in pa:
+        assert torch.equal(pa[k], pb[k]), k
+    assert torch.equal(fa, fb)
+    for k in qa:
+        assert torch.equal(qa[k], qb[k]), k
 
 
 @pytest.mark.gpu
@@ -651,3 +714,28 @@ def test_head_linear_matches_fp32(ops, K, KP, B):
     hb = h.to(torch.bfloat16).float()
     ref = (hb * w.view(1, K, 1, 1)).sum(1).reshape(B, S * S) + b0
     assert torch.allclose(z, ref, rtol=1e-4, atol=1e-3), (z - ref).abs().max().item()
+
+
+@pytest.mark.gpu
+def test_pending_handle_dropped_inside_capture_keeps_the_capture_valid(ops):
+    """A PendingReduction whose owner dies during a HIP graph capture (the cyclic GC dropping a
+    dead trunk mid-capture) defers its hipFree: the capture stays valid, and the next handle
+    created frees it."""
+    from rocalphago_amd.ops import hipops
+    h = ops.PendingReduction()
+    x = torch.zeros(4, device="cuda")
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
+            x.add_(1)
+            del h
+            x.add_(1)
+    assert len(hipops._DEFERRED_FREE) == 1
+    g.replay()
+    torch.cuda.synchronize()
+    assert x.tolist() == [2.0] * 4
+    ops.PendingReduction()
+    assert not hipops._DEFERRED_FREE
+
