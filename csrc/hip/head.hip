@@ -249,10 +249,31 @@ head_bwd_reduce_kernel(const float* __restrict__ dwpart, const float* __restrict
     // running metrics acc[0] += sum loss, acc[1] += sum hit (instead of two contended device
     // atomics per board in the head forward)
     float d = 0.f, a = 0.f, h = 0.f;
-    if (db0 && dzsum)  // the head forward's per-board sums
+    if (db0 && dzsum) {  // the head forward's per-board sums
       for (int i = threadIdx.x; i < B; i += blockDim.x) d += dzsum[i];
-    else if (db0)
-      for (size_t i = threadIdx.x; i < (size_t)B * S2; i += blockDim.x) d += dz[i];
+    } else if (db0) {
+      // all of dz (the value head: no per-board sums): 16-byte loads, four in flight per
+      // thread on independent sums (one dependent 4-byte load at a time took 24 us for
+      // 256 x 361 values -- the whole value-net step's longest small kernel)
+      const size_t n = (size_t)B * S2, n4 = (reinterpret_cast<uintptr_t>(dz) & 15) ? 0 : n / 4;
+      const float4* d4 = reinterpret_cast<const float4*>(dz);
+      const size_t bt = blockDim.x;
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+      size_t i = threadIdx.x;
+      for (; i + 3 * bt < n4; i += 4 * bt) {
+        const float4 a = d4[i], b = d4[i + bt], c = d4[i + 2 * bt], e = d4[i + 3 * bt];
+        s0 += (a.x + a.y) + (a.z + a.w);
+        s1 += (b.x + b.y) + (b.z + b.w);
+        s2 += (c.x + c.y) + (c.z + c.w);
+        s3 += (e.x + e.y) + (e.z + e.w);
+      }
+      for (; i < n4; i += bt) {
+        const float4 a = d4[i];
+        s0 += (a.x + a.y) + (a.z + a.w);
+      }
+      for (size_t j = n4 * 4 + threadIdx.x; j < n; j += bt) s1 += dz[j];
+      d = (s0 + s1) + (s2 + s3);
+    }
     if (acc)
       for (int i = threadIdx.x; i < B; i += blockDim.x) {
         a += mloss[i];

@@ -175,6 +175,27 @@ def test_policy_head_and_backward(ops):
     assert rel_err(dpb, pbr.grad) < 2e-2
 
 
+@pytest.mark.parametrize("B", [256, 7])
+def test_head_bwd_bias_gradient_sums_all_of_dz(ops, B):
+    """Without per-board sums (the value head) head_bwd's db0 is the sum of all B x 361 dz values
+    (16-byte loads, four sums per thread; B = 7: 2527 values, not a multiple of 4)."""
+    dev = torch.device("cuda")
+    torch.manual_seed(3)
+    K, S = 192, 19
+    h = F.relu(torch.randn(B, K, S, S, device=dev))
+    hp = ops.pack_nchw(h, 1, K)
+    w = torch.randn(K, device=dev) * 0.1
+    dz = torch.randn(B, S * S, device=dev)
+    dh = ops.alloc_padded(B, S, 1, K, dev)
+    dw = torch.zeros(K, device=dev)
+    db0 = torch.zeros(1, device=dev)
+    ops.head_bwd(hp, w, dz, dh, dw, db0, None, K, relu_mask=True)
+    ref = dz.double().sum().item()
+    assert abs(db0.item() - ref) < 1e-5 * dz.abs().sum().item()
+    ref_dw = (bf(h) * dz.view(B, 1, S, S)).sum((0, 2, 3))
+    assert rel_err(dw, ref_dw) < 1e-2
+
+
 def test_sgd(ops):
     dev = torch.device("cuda")
     p = torch.randn(1001, device=dev)
