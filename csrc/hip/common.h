@@ -97,7 +97,7 @@ __device__ __forceinline__ float warp_max(float v) {
   return v;
 }
 
-// SGD folded into the weight packing (conv.hip pack_trunk_kernel, conv_wino.hip wino_pack_kernel):
+// SGD folded into the weight packing (pack.h pack_trunk_block / wino_pack_block):
 // a packing kernel that reads fp32 master w also reads its gradient g = w[goff] (the model's
 // flat gradient buffer mirrors the parameter buffer), writes back w - lr (g + wd w) and packs
 // the updated value; on = 0: plain packing.

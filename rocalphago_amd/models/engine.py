@@ -47,7 +47,7 @@ def complement(ranges, n):
 
 
 def pack_grid_width(specs):
-    """Grid width of conv.hip's pack_trunk_kernel: the 16x16 (n, c) all-tap tiles of the widest
+    """Grid width of the pack_trunk rows (csrc/hip/pack.h pack_trunk_block): the 16x16 (n, c) all-tap tiles of the widest
     layer, rounded up to a multiple of 8 (each block grid-strides over its layer's tiles)."""
     return max(8 * -(-((-(-s.coutp // 16)) * (-(-s.cinp // 16))) // 8) for s in specs)
 
@@ -57,7 +57,7 @@ class _PackedConvs(object):
     OIHW masters in one launch whenever the model's weight version changes."""
 
     def _init_packing(self, specs, device, wino=None):
-        # conv.hip pack_trunk_kernel stages a 16x16 tile of all taps in LDS: kernels up to 7x7
+        # pack.h pack_trunk_block stages a 16x16 tile of all taps in LDS: kernels up to 7x7
         if any(s.ks > 7 for s in specs):
             raise ValueError("fused HIP trunks take kernels up to 7x7, got %s"
                              % sorted({s.ks for s in specs}))

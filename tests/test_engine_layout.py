@@ -5,12 +5,12 @@ import pytest
 
 from rocalphago_amd.models.engine import ConvSpec, pack_grid_width
 
-_PT = 16  # conv.hip pack_trunk_kernel: 16 (n) x 16 (c) all-tap tiles
+_PT = 16  # pack.h pack_trunk_block: 16 (n) x 16 (c) all-tap tiles
 
 
 def _pack_tiles(spec, width):
-    """Tiles the blocks x < width of conv.hip pack_trunk_kernel visit for one layer (each block
-    grid-strides over the layer's tiles: the kernel's own loop, restated)."""
+    """Tiles the blocks x < width of a pack_trunk launch (pack.h pack_trunk_block) visit for one
+    layer (each block grid-strides over the layer's tiles: the kernel's own loop, restated)."""
     ntiles = -(-spec.coutp // _PT) * -(-spec.cinp // _PT)
     seen = []
     for x in range(width):
@@ -71,7 +71,7 @@ def test_trunk_rejects_kernels_above_7x7():
 
 
 def test_wino_pack_grid_covers_every_tile():
-    """conv_wino.hip wino_pack_kernel: one block per 32 (n) x 16 (c) tile; rag_wino_pack
+    """pack.h wino_pack_block: one block per 32 (n) x 16 (c) tile; rag_wino_pack
     launches 8 blocks per 64 x 64 tile of the widest layer, which covers every layer's tiles."""
     for coutp, cinp in [(192, 192), (128, 128), (192, 64), (384, 192), (64, 32), (256, 96)]:
         max_tiles = -(-coutp // 64) * -(-cinp // 64)
