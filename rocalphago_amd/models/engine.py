@@ -47,8 +47,9 @@ def complement(ranges, n):
 
 
 def pack_grid_width(specs):
-    """Grid width of the pack_trunk rows (csrc/hip/pack.h pack_trunk_block): the 16x16 (n, c) all-tap tiles of the widest
-    layer, rounded up to a multiple of 8 (each block grid-strides over its layer's tiles)."""
+    """Grid width of the pack_trunk rows (csrc/hip/pack.h pack_trunk_block): the 16x16 (n, c)
+    all-tap tiles of the widest layer, rounded up to a multiple of 8 (each block grid-strides over
+    its layer's tiles)."""
     return max(8 * -(-((-(-s.coutp // 16)) * (-(-s.cinp // 16))) // 8) for s in specs)
 
 
